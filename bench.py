@@ -1,0 +1,202 @@
+#!/usr/bin/env python3
+"""Throughput of the MI355X ByteTrack update() (BASELINE.json headline metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--streams S] [--n 1024]
+
+A step = one `tracker.update()` frame for every one of the S independent streams on each GPU
+(each stream: 1024 tracks x 1024 detections per frame, SURVEY.md §8(d) synthetic generator).
+All frames are staged in HBM before the timed region; the engine's device-buffer entry point
+runs the whole update on the GPU (outputs stay in HBM).  N > 1: one process per GPU
+(torch.distributed.run), streams sharded per rank, no data-path collective, barrier + max over
+ranks around the timed region (scaling "weak": per-GPU work is fixed).
+
+Rank 0 prints one JSON line with `roofline` (dominant kernel, HIP events on the engine stream)
+and `cpu_baseline` (the oracle's CPU restatement on this host, 1 core, bounded sample).
+"""
+import argparse
+import ctypes
+import json
+import os
+import subprocess
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+PHASES = ["begin", "predict", "edges1", "lap1", "stage1", "prep23", "edges2", "lap2", "edges3",
+          "lap3", "stage23", "finish", "dedup", "output"]
+HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+# Canonical algorithmic bytes per update: ByteTrack 1024 x 1024
+BYTES_PER_UPDATE_1024 = 19_259_392
+
+
+def algorithmic_bytes(n, m):
+    """B = 4*S*N + 56*M + 16*N*M + 64*N with S = 576 (ByteTrack)."""
+    return 4 * 576 * n + 56 * m + 16 * n * m + 64 * n
+
+
+def kernel_bytes(phase, n, m, streams):
+    """Algorithmic bytes one launch of `phase` moves for `streams` streams of n tracks x m dets
+    (DESIGN.md §Kernels): the KF kernels read+write the 352-B packed state per track; the cost /
+    edge kernel reads every track box and detection box+score once (the N x M cost itself is
+    never materialised: only c < cost_limit candidates are written)."""
+    per = {
+        "predict": 2 * 352 * n + 32 * n,
+        "stage1": 2 * 352 * n + 48 * n,
+        "edges1": 32 * n + 40 * m + 16 * n,
+        "lap1": 16 * n + 8 * (n + m),
+        "finish": 352 * m,
+    }.get(phase, 0)
+    return per * streams
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=30)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--streams", type=int, default=64, help="streams per GPU")
+    p.add_argument("--n", type=int, default=1024, help="tracks = detections per frame")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-frames", type=int, default=40)
+    p.add_argument("--seed", type=int, default=1000)
+    return p.parse_args()
+
+
+def gen_stream_frames(n, frames, seed):
+    from yolo_tracking_amd.synth import make_frames
+    return [d for d, _ in make_frames(n, frames, seed)]
+
+
+def cpu_baseline(n, frames, seed):
+    """Time the oracle (CPU restatement: NumPy ByteTrack + C lapjv) on one stream, 1 thread."""
+    env = dict(os.environ, OMP_NUM_THREADS="1", OPENBLAS_NUM_THREADS="1", MKL_NUM_THREADS="1")
+    code = (
+        "import sys,time,json; sys.path.insert(0,%r)\n"
+        "from oracle.bytetrack import ByteTrackOracle\n"
+        "from yolo_tracking_amd.synth import make_frames\n"
+        "fr=[d for d,_ in make_frames(%d,%d,%d)]\n"
+        "t=ByteTrackOracle(0.5,0.8,30,30); t.update(fr[0])\n"
+        "t0=time.perf_counter()\n"
+        "for d in fr[1:]: t.update(d)\n"
+        "dt=time.perf_counter()-t0\n"
+        "print(json.dumps({'frames':len(fr)-1,'seconds':dt}))\n" % (REPO, n, frames, seed))
+    try:
+        r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
+                           timeout=900)
+        res = json.loads(r.stdout.strip().splitlines()[-1])
+    except Exception as exc:  # report, never fail the bench on the baseline leg
+        return {"value": None, "unit": "calls/s", "cores": 1, "kind": "port",
+                "sample": f"failed: {exc}"}
+    return {"value": res["frames"] / res["seconds"], "unit": "calls/s", "cores": 1, "kind": "port",
+            "sample": f"oracle ByteTrack (NumPy + C lapjv), 1 stream {n}x{n}, frames 2..{frames} "
+                      f"of seed {seed}, {res['seconds']:.1f} s, 1 thread"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    torch.cuda.set_device(local_rank)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    from yolo_tracking_amd import ByteTrackEngine, _lib
+    S, N = args.streams, args.n
+    F = args.warmup + args.steps
+    # synthetic frames for this rank's streams, staged in HBM: [F][S*N][6] + offsets
+    t_gen = time.time()
+    per_stream = [gen_stream_frames(N, F, args.seed + rank * S + s) for s in range(S)]
+    host = np.stack([np.concatenate([per_stream[s][f] for s in range(S)]) for f in range(F)])
+    off = np.array([[sum(len(per_stream[q][f]) for q in range(s)) for s in range(S + 1)]
+                    for f in range(F)], dtype=np.int32)
+    d_dets = torch.from_numpy(host).to("cuda")
+    d_off = torch.from_numpy(off).to("cuda")
+    gen_s = time.time() - t_gen
+
+    eng = ByteTrackEngine(S, track_thresh=0.5, match_thresh=0.8, track_buffer=30, frame_rate=30,
+                          device=local_rank, track_capacity=2 * N, max_dets=N)
+    cap, _ = eng.capacity()
+    d_out = torch.empty((S * cap, 8), dtype=torch.float64, device="cuda")
+    d_cnt = torch.zeros(S, dtype=torch.int32, device="cuda")
+    lib = eng.lib
+    h = eng.handle
+    row_bytes = N * 6 * 8 * S
+
+    def step(f):
+        _lib.check(lib.yta_bytetrack_update_device(
+            h, ctypes.c_void_p(d_dets.data_ptr() + f * row_bytes),
+            ctypes.c_void_p(d_off.data_ptr() + f * (S + 1) * 4),
+            ctypes.c_void_p(d_out.data_ptr()), ctypes.c_void_p(d_cnt.data_ptr())))
+
+    torch.cuda.synchronize()
+    for f in range(args.warmup):
+        step(f)
+    _lib.check(lib.yta_bytetrack_sync(h))
+    _lib.check(lib.yta_bytetrack_profile(h, 1))
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for f in range(args.warmup, F):
+        step(f)
+    _lib.check(lib.yta_bytetrack_sync(h))
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    ms = (ctypes.c_double * len(PHASES))()
+    nfr = ctypes.c_int()
+    _lib.check(lib.yta_bytetrack_profile_collect(h, ms, ctypes.byref(nfr)))
+    phase_ms = {PHASES[k]: ms[k] / max(nfr.value, 1) for k in range(len(PHASES))}
+
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    calls = world * S * args.steps
+    value = calls / elapsed
+    ms_per_step = 1000.0 * elapsed / args.steps
+
+    if rank == 0:
+        dom = max((p for p in phase_ms if kernel_bytes(p, N, N, S)), key=lambda p: phase_ms[p])
+        dom_ms = phase_ms[dom]
+        b = kernel_bytes(dom, N, N, S)
+        achieved = b / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
+        busiest = max(phase_ms, key=lambda p: phase_ms[p])
+        cpu = None if args.no_cpu_baseline else cpu_baseline(N, args.cpu_frames, args.seed)
+        line = {
+            "metric": "tracker.update() calls/sec @ 1024 tracks×1024 dets; 1/2/4/8 MI355X",
+            "value": value, "unit": "calls/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+            "config": {"workload": f"bytetrack {N}x{N}, {S} streams/GPU, inputs resident in HBM",
+                       "tracker": "bytetrack", "tracks": N, "dets": N, "streams_per_gpu": S,
+                       "parallelism": f"stream-sharded x{world}"},
+            "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved,
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "algorithmic_bytes_per_launch": b, "avg_launch_ms": dom_ms},
+            "cpu_baseline": cpu,
+            "per_kernel_ms": phase_ms,
+            "busiest_kernel": busiest,
+            "single_stream_equiv_ms": ms_per_step,
+            "algorithmic_bytes_per_update": algorithmic_bytes(N, N),
+            "stage_seconds": round(gen_s, 1),
+        }
+        print(json.dumps(line))
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

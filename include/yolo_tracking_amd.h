@@ -1,0 +1,123 @@
+/*
+ * yolo_tracking_amd — C ABI of the MI355X tracker.update() hot path.
+ *
+ * Every entry point returns an int status (YTA_OK = 0, negative = error; the message is available
+ * from yta_last_error(), thread-local).  No torch / HIP types cross this boundary: plain pointers,
+ * sizes and opaque handles only.  Host buffers are caller-owned; device buffers are owned by the
+ * library (except in the *_device entry points, which take caller-owned device pointers).
+ *
+ * What each entry point replaces in the reference (BoxMOT 10.0.51, /root/reference):
+ *   yta_bytetrack_*          boxmot/trackers/bytetrack/byte_tracker.py:114-281  BYTETracker.__init__/update
+ *                            (created by boxmot/tracker_zoo.py:56-64 create_tracker('bytetrack', ...))
+ *   yta_box_affinity         boxmot/utils/iou.py:6-188  iou/giou/diou/ciou/centroid_batch
+ *   yta_iou_distance         boxmot/utils/matching.py:94-119 iou_distance (+ fuse_score :213-221)
+ *   yta_kf_xyah_initiate     boxmot/motion/kalman_filters/bytetrack_kf.py:55-86
+ *   yta_kf_xyah_predict      boxmot/motion/kalman_filters/bytetrack_kf.py:155-192 (multi_predict)
+ *   yta_kf_xyah_update       boxmot/motion/kalman_filters/bytetrack_kf.py:194-226 (+ project :126-153)
+ *   yta_lap_limited          boxmot/utils/matching.py:56-71 linear_assignment -> lap.lapjv(cost,
+ *                            extend_cost=True, cost_limit=thresh)
+ */
+#ifndef YOLO_TRACKING_AMD_H
+#define YOLO_TRACKING_AMD_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define YTA_OK 0
+#define YTA_ERR_INVALID (-1)   /* bad argument (shape, null pointer, unknown kind)        */
+#define YTA_ERR_HIP (-2)       /* HIP runtime failure (no device, launch or copy failure)  */
+#define YTA_ERR_CAPACITY (-3)  /* track / detection / output capacity exceeded            */
+#define YTA_ERR_NOMEM (-4)     /* host or device allocation failed                        */
+
+/* ---- library ---------------------------------------------------------------------------- */
+int yta_version(void);                       /* returns the ABI version (positive) */
+const char *yta_last_error(void);            /* message of the last failing call on this thread */
+int yta_device_count(int *count);
+
+/* ---- association primitives (parity / KAT entry points; synchronous, host buffers) ---------
+ * Boxes are [x1, y1, x2, y2] float64 rows. */
+#define YTA_AFF_IOU 0
+#define YTA_AFF_GIOU 1
+#define YTA_AFF_DIOU 2
+#define YTA_AFF_CIOU 3
+#define YTA_AFF_CENTROID 4
+/* out[i*nb + j] = affinity(a_i, b_j), exactly iou.py's *_batch(a, b) (centroid uses img_w/img_h) */
+int yta_box_affinity(int device, int kind, const double *a, int na, const double *b, int nb,
+                     double img_w, double img_h, double *out);
+/* out = 1 - iou_batch(a, b); if scores != NULL, then fuse_score: 1 - (1 - out) * scores[j] */
+int yta_iou_distance(int device, const double *a, int na, const double *b, int nb,
+                     const double *scores, double *out);
+
+/* ---- ByteTrack Kalman filter, xyah state (parity / KAT entry points) -----------------------
+ * mean: n x 8, cov: n x 8 x 8 (row-major, full matrices), meas / z: n x 4 [xc, yc, a, h]. */
+int yta_kf_xyah_initiate(int device, int n, const double *meas, double *mean, double *cov);
+/* in place; the caller applies the reference's `mean[7] = 0` for non-tracked tracks beforehand */
+int yta_kf_xyah_predict(int device, int n, double *mean, double *cov);
+int yta_kf_xyah_update(int device, int n, double *mean, double *cov, const double *z);
+
+/* ---- linear assignment with lapx cost_limit semantics -------------------------------------
+ * Minimises sum(matched cost) + cost_limit/2 * (#unmatched rows + #unmatched cols); x[r] = col or
+ * -1, y[c] = row or -1 (lap.lapjv(cost, extend_cost=True, cost_limit=cost_limit)). */
+int yta_lap_limited(int device, int nr, int nc, const double *cost, double cost_limit, int *x,
+                    int *y);
+
+/* ---- ByteTrack engine: S independent streams, state resident in HBM -----------------------
+ * One engine = S trackers with identical parameters (BYTETracker(track_thresh, match_thresh,
+ * track_buffer, frame_rate)).  Stream s keeps its own tracks and its own ID counter. */
+typedef struct yta_bytetrack yta_bytetrack;
+typedef struct {
+    double track_thresh;   /* bytetrack.yaml:1   (ctor default 0.45) */
+    double match_thresh;   /* bytetrack.yaml:3   (ctor default 0.8)  */
+    int track_buffer;      /* bytetrack.yaml:2   (ctor default 25)   */
+    int frame_rate;        /* bytetrack.yaml:4   (ctor default 30)   */
+} yta_bytetrack_params;
+
+/* track_capacity: live (tracked + lost) tracks per stream; max_dets: detections per stream per
+ * frame.  The host-buffer update grows both on demand; the device-buffer update treats them as
+ * hard limits (YTA_ERR_CAPACITY from yta_bytetrack_sync). */
+int yta_bytetrack_create(int device, int n_streams, int track_capacity, int max_dets,
+                         const yta_bytetrack_params *params, yta_bytetrack **engine);
+int yta_bytetrack_destroy(yta_bytetrack *engine);
+int yta_bytetrack_reset(yta_bytetrack *engine);
+
+/* Grow the per-stream track capacity / max detections (never shrinks), keeping every stream's
+ * state.  yta_bytetrack_update() calls this itself when a frame would not fit. */
+int yta_bytetrack_reserve(yta_bytetrack *engine, int track_capacity, int max_dets);
+int yta_bytetrack_capacity(yta_bytetrack *engine, int *track_capacity, int *max_dets);
+
+/* Host-buffer update of all S streams (one frame each).  dets: packed rows of
+ * [x1, y1, x2, y2, conf, cls] float64 for stream 0, then stream 1, ...; det_offsets: S+1
+ * prefix offsets (rows).  next_id: S counters (in: the last issued ID per stream, i.e. the
+ * reference's BaseTrack._count; out: updated), may be NULL to use the engine's own counters.
+ * out: caller buffer of out_capacity rows x 8 float64 [x1,y1,x2,y2,id,conf,cls,det_ind];
+ * out_offsets: S+1 prefix offsets written by the call.  Synchronous. */
+int yta_bytetrack_update(yta_bytetrack *engine, const double *dets, const int *det_offsets,
+                         long long *next_id, double *out, int out_capacity, int *out_offsets);
+
+/* Device-resident update for throughput runs: d_dets / d_det_offsets are device pointers laid out
+ * as above; results stay on the device: d_out holds S * track_capacity rows x 8, stream s at row
+ * s * track_capacity, d_out_counts[s] rows.  Asynchronous on the engine's HIP stream. */
+int yta_bytetrack_update_device(yta_bytetrack *engine, const double *d_dets,
+                                const int *d_det_offsets, double *d_out, int *d_out_counts);
+int yta_bytetrack_sync(yta_bytetrack *engine);      /* waits; reports device-side errors */
+
+/* Parity introspection: copy stream s's live tracks, tracked list first then lost list, in list
+ * order.  Per track: list (0 tracked / 1 lost), id, state (0 New 1 Tracked 2 Lost 3 Removed),
+ * activated, frame_id, start_frame, tracklet_len (ints: 7 x int64 per track), mean (8 f64), cov
+ * (64 f64).  *n_tracks receives the count; buffers must hold track_capacity entries. */
+int yta_bytetrack_get_state(yta_bytetrack *engine, int stream, int *n_tracks, long long *ints,
+                            double *mean, double *cov);
+/* Measurement: when enabled, HIP events are recorded around each of the 14 launches of a frame on
+ * the engine's stream; collect returns per-launch milliseconds summed over the covered frames in
+ * launch order (begin, predict, edges1, lap1, stage1, prep23, edges2, lap2, edges3, lap3,
+ * stage23, finish, dedup, output). */
+int yta_bytetrack_profile(yta_bytetrack *engine, int enable);
+int yta_bytetrack_profile_collect(yta_bytetrack *engine, double *ms, int *frames);
+/* Throughput helper: the engine's HIP stream (hipStream_t as void*) */
+int yta_bytetrack_hip_stream(yta_bytetrack *engine, void **stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,103 @@
+"""CPU: the oracle (CPU restatement) reproduces the reference's golden vectors.
+
+Goldens were produced by importing the reference itself (tests/golden/make_goldens.py).
+"""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import mot_frames
+from oracle import geometry, kalman_xyah
+from oracle.bytetrack import ByteTrackOracle
+from oracle.lap import lapjv
+
+
+def test_iou_family_bit_exact(golden_dir):
+    g = np.load(os.path.join(golden_dir, "kat_iou.npz"))
+    a, b = g["a"], g["b"]
+    assert np.array_equal(geometry.iou_batch(a, b), g["iou"])
+    assert np.array_equal(geometry.giou_batch(a, b), g["giou"])
+    assert np.array_equal(geometry.diou_batch(a, b), g["diou"])
+    assert np.array_equal(geometry.ciou_batch(a, b), g["ciou"])
+    assert np.array_equal(geometry.centroid_batch(a, b, 640, 480), g["centroid"])
+    d = geometry.iou_distance(a, b)
+    assert np.array_equal(d, g["iou_distance"])
+    assert np.array_equal(geometry.fuse_score(d, g["det_scores"]), g["fuse_score"])
+
+
+def test_kf_xyah(golden_dir):
+    g = np.load(os.path.join(golden_dir, "kat_kf_xyah.npz"))
+    for i, z in enumerate(g["meas"]):
+        m, c = kalman_xyah.initiate(z)
+        assert np.array_equal(m, g["init_mean"][i]) and np.array_equal(c, g["init_cov"][i])
+    pm, pc = kalman_xyah.multi_predict(g["pred_in_mean"], g["pred_in_cov"])
+    assert np.array_equal(pm, g["pred_mean"])
+    np.testing.assert_allclose(pc, g["pred_cov"], rtol=1e-12, atol=0)
+    for i in range(len(pm)):
+        um, uc = kalman_xyah.update(g["pred_mean"][i], g["pred_cov"][i], g["z"][i])
+        np.testing.assert_allclose(um, g["upd_mean"][i], rtol=1e-10, atol=1e-9)
+        np.testing.assert_allclose(uc, g["upd_cov"][i], rtol=1e-8, atol=1e-9)
+
+
+def test_lapjv_kat(golden_dir):
+    g = np.load(os.path.join(golden_dir, "kat_lap.npz"))
+    for k in range(int(g["n_cases"])):
+        cost, lim = g[f"c{k}__cost"], float(g[f"c{k}__limit"])
+        opt, x, y = lapjv(cost, extend_cost=True, cost_limit=lim)
+        assert np.array_equal(x, g[f"c{k}__x"]), k
+        assert np.array_equal(y, g[f"c{k}__y"]), k
+        assert np.isclose(opt, float(g[f"c{k}__opt"])), k
+
+
+@pytest.mark.parametrize("case", ["n64_s11", "n256_s12", "n1024_s13"])
+def test_bytetrack_synthetic(golden_dir, case):
+    g = np.load(os.path.join(golden_dir, "bytetrack_synth.npz"))
+    dets, dc = g[f"{case}__dets"], g[f"{case}__det_counts"]
+    oc, out = g[f"{case}__out_counts"], g[f"{case}__out"]
+    t = ByteTrackOracle(track_thresh=0.5, match_thresh=0.8, track_buffer=30, frame_rate=30)
+    o0 = r0 = 0
+    for f, n in enumerate(dc):
+        got = t.update(dets[o0:o0 + n]).reshape(-1, 8)
+        exp = out[r0:r0 + oc[f]]
+        o0 += n
+        r0 += oc[f]
+        assert got.shape == exp.shape, f
+        assert np.array_equal(got[:, 4:], exp[:, 4:]), f
+        np.testing.assert_allclose(got[:, :4], exp[:, :4], rtol=1e-9, atol=1e-9)
+    # final Kalman state of every live track, list order
+    recs = t.state_snapshot()
+    assert len(recs) == len(g[f"{case}__st_id"])
+    for k, (lst, tr) in enumerate(recs):
+        assert lst == g[f"{case}__st_list"][k] and tr.track_id == g[f"{case}__st_id"][k]
+        np.testing.assert_allclose(tr.mean, g[f"{case}__st_mean"][k], rtol=1e-9, atol=1e-8)
+        np.testing.assert_allclose(tr.cov, g[f"{case}__st_cov"][k], rtol=1e-7, atol=1e-8)
+
+
+@pytest.mark.parametrize("seq", ["MOT17-02-FRCNN", "MOT17-05-FRCNN", "MOT17-09-FRCNN",
+                                 "MOT17-13-FRCNN"])
+def test_bytetrack_mot17(golden_dir, seq):
+    g = np.load(os.path.join(golden_dir, "bytetrack_mot17.npz"))
+    key = seq.replace("-", "_")
+    oc, box, ints, sc = (g[f"{key}__out_counts"], g[f"{key}__out_box"], g[f"{key}__out_int"],
+                         g[f"{key}__out_score"])
+    t = ByteTrackOracle(track_thresh=0.5, match_thresh=0.8, track_buffer=30, frame_rate=30)
+    r0 = 0
+    for f, dets in enumerate(mot_frames(g, key)):
+        got = t.update(dets).reshape(-1, 8)
+        n = oc[f]
+        assert len(got) == n, f
+        assert np.array_equal(got[:, [4, 6, 7]].astype(np.int64), ints[r0:r0 + n]), f
+        assert np.array_equal(got[:, 5], sc[r0:r0 + n]), f
+        np.testing.assert_allclose(got[:, :4], box[r0:r0 + n], rtol=1e-9, atol=1e-9)
+        r0 += n
+
+
+def test_reference_kat_bytetrack_output():
+    """tests/test_python.py:165-185 of the reference: two dets -> (2, 8) on every frame."""
+    det = np.array([[144, 212, 578, 480, 0.82, 0], [425, 281, 576, 472, 0.86, 65]])
+    t = ByteTrackOracle(track_thresh=0.5, match_thresh=0.8, track_buffer=30, frame_rate=30)
+    for _ in range(3):
+        out = t.update(det)
+        assert out.shape == (2, 8)
+    np.testing.assert_allclose(det, np.delete(out, [4, 7], axis=1), atol=1, rtol=7e-3)

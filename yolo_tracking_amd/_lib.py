@@ -1,0 +1,179 @@
+"""ctypes binding of the gfx950 C-ABI library (include/yolo_tracking_amd.h -> libyta.so).
+
+There is no CPU fallback: if the library is missing, or no HIP device is present, every tracker
+call raises `YTAError`.  `build()` in __graft_entry__.py (or `make -C yolo_tracking_amd/csrc`)
+produces the library in-tree.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libyta.so")
+
+YTA_OK = 0
+YTA_ERR_INVALID = -1
+YTA_ERR_HIP = -2
+YTA_ERR_CAPACITY = -3
+YTA_ERR_NOMEM = -4
+
+AFF_KINDS = {"iou": 0, "giou": 1, "diou": 2, "ciou": 3, "centroid": 4}
+
+
+class YTAError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"yolo_tracking_amd error {code}: {msg}")
+        self.code = code
+
+
+class CapacityError(YTAError):
+    pass
+
+
+class BtParams(ctypes.Structure):
+    _fields_ = [("track_thresh", ctypes.c_double), ("match_thresh", ctypes.c_double),
+                ("track_buffer", ctypes.c_int), ("frame_rate", ctypes.c_int)]
+
+
+_lib = None
+
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+_D = ctypes.c_double
+
+_SIGS = {
+    "yta_version": ([], _I),
+    "yta_last_error": ([], ctypes.c_char_p),
+    "yta_device_count": ([_P], _I),
+    "yta_box_affinity": ([_I, _I, _P, _I, _P, _I, _D, _D, _P], _I),
+    "yta_iou_distance": ([_I, _P, _I, _P, _I, _P, _P], _I),
+    "yta_kf_xyah_initiate": ([_I, _I, _P, _P, _P], _I),
+    "yta_kf_xyah_predict": ([_I, _I, _P, _P], _I),
+    "yta_kf_xyah_update": ([_I, _I, _P, _P, _P], _I),
+    "yta_lap_limited": ([_I, _I, _I, _P, _D, _P, _P], _I),
+    "yta_bytetrack_create": ([_I, _I, _I, _I, _P, _P], _I),
+    "yta_bytetrack_destroy": ([_P], _I),
+    "yta_bytetrack_reset": ([_P], _I),
+    "yta_bytetrack_reserve": ([_P, _I, _I], _I),
+    "yta_bytetrack_capacity": ([_P, _P, _P], _I),
+    "yta_bytetrack_update": ([_P, _P, _P, _P, _P, _I, _P], _I),
+    "yta_bytetrack_update_device": ([_P, _P, _P, _P, _P], _I),
+    "yta_bytetrack_sync": ([_P], _I),
+    "yta_bytetrack_get_state": ([_P, _I, _P, _P, _P, _P], _I),
+    "yta_bytetrack_profile": ([_P, _I], _I),
+    "yta_bytetrack_profile_collect": ([_P, _P, _P], _I),
+    "yta_bytetrack_hip_stream": ([_P, _P], _I),
+}
+
+EXPORTED_SYMBOLS = tuple(_SIGS)
+
+
+def load_library(path=None):
+    """Load (once) and return the ctypes handle; raises if the library is absent."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise YTAError(YTA_ERR_HIP, f"HIP library not built: {p} (run __graft_entry__.build() "
+                                    "or `make -C yolo_tracking_amd/csrc`)")
+    lib = ctypes.CDLL(p)
+    for name, (args, res) in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = res
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def check(rc):
+    if rc != YTA_OK:
+        msg = load_library().yta_last_error()
+        msg = msg.decode() if msg else ""
+        cls = CapacityError if rc == YTA_ERR_CAPACITY else YTAError
+        raise cls(rc, msg)
+
+
+def device_count():
+    n = ctypes.c_int(0)
+    check(load_library().yta_device_count(ctypes.byref(n)))
+    return n.value
+
+
+def ptr(a):
+    return a.ctypes.data if a is not None else None
+
+
+def parse_device(device):
+    """Map the reference's `device` argument ('cpu', '0', 'cuda:1', 1, torch.device) to a HIP
+    ordinal.  The tracker arithmetic always runs on an MI355X; 'cpu' (which in the reference only
+    places the ReID model) selects device 0."""
+    if device is None:
+        return 0
+    if isinstance(device, int):
+        return device
+    s = str(device).strip().lower()
+    if s in ("", "cpu", "cuda", "gpu"):
+        return 0
+    if ":" in s:
+        s = s.split(":", 1)[1]
+    s = s.split(",")[0]
+    try:
+        return int(s)
+    except ValueError:
+        return 0
+
+
+# ------------------------------------------------------------------------- primitive wrappers
+def box_affinity(a, b, kind="iou", img_w=0.0, img_h=0.0, device=0):
+    a = np.ascontiguousarray(a, dtype=np.float64).reshape(-1, 4)
+    b = np.ascontiguousarray(b, dtype=np.float64).reshape(-1, 4)
+    out = np.empty((len(a), len(b)), dtype=np.float64)
+    check(load_library().yta_box_affinity(device, AFF_KINDS[kind], ptr(a), len(a), ptr(b), len(b),
+                                          float(img_w), float(img_h), ptr(out)))
+    return out
+
+
+def iou_distance(a, b, scores=None, device=0):
+    a = np.ascontiguousarray(a, dtype=np.float64).reshape(-1, 4)
+    b = np.ascontiguousarray(b, dtype=np.float64).reshape(-1, 4)
+    s = None if scores is None else np.ascontiguousarray(scores, dtype=np.float64)
+    out = np.empty((len(a), len(b)), dtype=np.float64)
+    check(load_library().yta_iou_distance(device, ptr(a), len(a), ptr(b), len(b), ptr(s), ptr(out)))
+    return out
+
+
+def kf_xyah_initiate(meas, device=0):
+    meas = np.ascontiguousarray(meas, dtype=np.float64).reshape(-1, 4)
+    n = len(meas)
+    mean = np.empty((n, 8))
+    cov = np.empty((n, 8, 8))
+    check(load_library().yta_kf_xyah_initiate(device, n, ptr(meas), ptr(mean), ptr(cov)))
+    return mean, cov
+
+
+def kf_xyah_predict(mean, cov, device=0):
+    mean = np.array(mean, dtype=np.float64, order="C").reshape(-1, 8)
+    cov = np.array(cov, dtype=np.float64, order="C").reshape(-1, 8, 8)
+    check(load_library().yta_kf_xyah_predict(device, len(mean), ptr(mean), ptr(cov)))
+    return mean, cov
+
+
+def kf_xyah_update(mean, cov, z, device=0):
+    mean = np.array(mean, dtype=np.float64, order="C").reshape(-1, 8)
+    cov = np.array(cov, dtype=np.float64, order="C").reshape(-1, 8, 8)
+    z = np.ascontiguousarray(z, dtype=np.float64).reshape(-1, 4)
+    check(load_library().yta_kf_xyah_update(device, len(mean), ptr(mean), ptr(cov), ptr(z)))
+    return mean, cov
+
+
+def lap_limited(cost, cost_limit, device=0):
+    """lap.lapjv(cost, extend_cost=True, cost_limit=cost_limit) -> (x, y)."""
+    c = np.ascontiguousarray(cost, dtype=np.float64)
+    nr, nc = c.shape
+    x = np.empty(nr, dtype=np.int32)
+    y = np.empty(nc, dtype=np.int32)
+    check(load_library().yta_lap_limited(device, nr, nc, ptr(c), float(cost_limit), ptr(x), ptr(y)))
+    return x, y

@@ -1,0 +1,1016 @@
+// ByteTrack update() for S independent streams on gfx950, all state resident in HBM.
+//
+// Follows boxmot/trackers/bytetrack/byte_tracker.py:132-325.  Per frame (every launch covers all
+// S streams; "block/stream" kernels do the order-preserving list algebra with block-wide scans):
+//   k_begin     [block/stream]  frame_id++, confidence split (:149-158), STrack box conversions
+//                               (:14-25), tracked -> activated / unconfirmed, pool = act ++ lost
+//   k_predict   [grid]          STrack.multi_predict over the pool (:35-48) + pool / unconfirmed boxes
+//   stage 1     edges + lap     iou_distance + fuse_score, lapjv cost_limit=match_thresh (:181-186)
+//   k_stage1    [grid]          Kalman update / re_activate of matched pool rows (:188-196)
+//   k_prep23    [block/stream]  leftovers = unmatched Tracked rows (:205-209); rest = unmatched dets (:229)
+//   stage 2 & 3 edges + lap     leftovers x low dets, IoU, 0.5 (:210-211); unconfirmed x rest, fused, 0.7 (:230-233)
+//   k_stage23   [grid]          stage-2/3 updates, mark lost (:222-226) / removed (:237-240)
+//   k_finish    [block/stream]  births (:242-248), lost expiry (:250-253), joint/sub list algebra
+//                               incl. the removed_stracks quirk (:257-265)
+//   k_dedup     [grid]          remove_duplicate_stracks pairs at IoU distance < 0.15 (:312-325)
+//   k_output    [block/stream]  final lists, output rows (:270-281), free-slot list
+#include <algorithm>
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "bytetrack.hpp"
+
+namespace yta {
+namespace {
+
+constexpr int BLK = 1024;   // block/stream kernels
+constexpr int GRID_T = 256; // grid kernels
+
+__device__ __forceinline__ void load_kf(const double *kf, long long slot, KfState &s) {
+    const double2 *src = reinterpret_cast<const double2 *>(kf + slot * KF_REC);
+#pragma unroll
+    for (int k = 0; k < 22; ++k) {
+        double2 v = src[k];
+        double *dst = k < 4 ? s.m + 2 * k : s.p + 2 * (k - 4);
+        dst[0] = v.x;
+        dst[1] = v.y;
+    }
+}
+
+__device__ __forceinline__ void store_kf(double *kf, long long slot, const KfState &s) {
+    double2 *dst = reinterpret_cast<double2 *>(kf + slot * KF_REC);
+#pragma unroll
+    for (int k = 0; k < 22; ++k) {
+        const double *src = k < 4 ? s.m + 2 * k : s.p + 2 * (k - 4);
+        dst[k] = make_double2(src[0], src[1]);
+    }
+}
+
+__device__ __forceinline__ Box kf_box(const double *kf, long long slot) {
+    const double *m = kf + slot * KF_REC;
+    return xyah_mean_to_box(m[0], m[1], m[2], m[3]);
+}
+
+__device__ __forceinline__ int st_of(int flags) { return flags & FL_STATE; }
+
+// ------------------------------------------------------------------------------------ k_begin
+__global__ __launch_bounds__(BLK) void k_begin(BtArgs a) {
+    __shared__ int wsum[32];
+    const int s = blockIdx.x, t = threadIdx.x;
+    BtCounters *c = a.cnt + s;
+    const long long db = (long long)s * a.MAXD, tb = (long long)s * a.CAP;
+    int nd = a.det_off[s + 1] - a.det_off[s];
+    if (nd > a.MAXD || nd < 0) {
+        if (t == 0) atomicOr(&c->err, ERR_DET_CAPACITY);
+        nd = nd < 0 ? 0 : a.MAXD;
+    }
+    const double *din = a.det_in + (long long)a.det_off[s] * 6;
+    for (int i = t; i < nd; i += BLK) {
+        const double *d = din + (long long)i * 6;
+        double xywh[4];
+        det_xyxy_to_xywh(d, xywh);                    // STrack.__init__ (:16-18)
+        a.det_box[db + i] = xywh_to_box(xywh);        // STrack.xyxy with mean None (:105-106)
+        xywh_to_xyah(xywh, a.det_xyah + (db + i) * 4);
+        a.det_conf[db + i] = d[4];
+        a.det_cls[db + i] = d[5];
+    }
+    __syncthreads();
+    const double thr = a.track_thresh;
+    const double *conf = a.det_conf + db;
+    int n_high = block_compact(nd, wsum, [&](int i) { return conf[i] > thr; },
+                               [&](int i, int pos) {
+                                   a.high[db + pos] = i;
+                                   a.high_box[db + pos] = a.det_box[db + i];
+                                   a.high_score[db + pos] = conf[i];
+                               });
+    int n_second = block_compact(nd, wsum,
+                                 [&](int i) { return conf[i] > 0.1 && conf[i] < thr; },
+                                 [&](int i, int pos) {
+                                     a.second[db + pos] = i;
+                                     a.second_box[db + pos] = a.det_box[db + i];
+                                 });
+    const int n_tracked = c->n_tracked, n_lost = c->n_lost;
+    const int *tracked = a.tracked + tb;
+    int n_act = block_compact(n_tracked, wsum,
+                              [&](int i) { return (a.meta[tb + tracked[i]].flags & FL_ACTIVATED) != 0; },
+                              [&](int i, int pos) { a.pool[tb + pos] = tracked[i]; });
+    int n_unc = block_compact(n_tracked, wsum,
+                              [&](int i) { return (a.meta[tb + tracked[i]].flags & FL_ACTIVATED) == 0; },
+                              [&](int i, int pos) { a.unc[tb + pos] = tracked[i]; });
+    for (int i = t; i < n_lost; i += BLK) a.pool[tb + n_act + i] = a.lost[tb + i];
+    if (t == 0) {
+        c->frame_id += 1;
+        c->n_dets = nd;
+        c->n_high = n_high;
+        c->n_second = n_second;
+        c->n_act = n_act;
+        c->n_unc = n_unc;
+        c->n_pool = n_act + n_lost;
+        c->n_left = 0;
+        c->n_rest = 0;
+        c->n_births = 0;
+        c->n_edges[0] = c->n_edges[1] = c->n_edges[2] = 0;
+    }
+}
+
+// ------------------------------------------------------------------------------------ k_predict
+__global__ __launch_bounds__(GRID_T) void k_predict(BtArgs a) {
+    const int s = blockIdx.y;
+    const int i = blockIdx.x * GRID_T + threadIdx.x;
+    const BtCounters *c = a.cnt + s;
+    const int n_pool = c->n_pool, n_unc = c->n_unc;
+    const long long tb = (long long)s * a.CAP;
+    if (i < n_pool) {
+        const long long slot = tb + a.pool[tb + i];
+        KfState st;
+        load_kf(a.kf, slot, st);
+        if (st_of(a.meta[slot].flags) != ST_TRACKED) st.m[7] = 0;   // :41-42
+        kf_predict(st);
+        store_kf(a.kf, slot, st);
+        a.pool_box[tb + i] = xyah_mean_to_box(st.m[0], st.m[1], st.m[2], st.m[3]);
+    } else if (i < n_pool + n_unc) {
+        const int j = i - n_pool;
+        a.unc_box[tb + j] = kf_box(a.kf, tb + a.unc[tb + j]);   // unconfirmed: not predicted
+    }
+}
+
+__device__ __forceinline__ void take_detection(const BtArgs &a, long long slot, long long det,
+                                               int det_local, int fid) {
+    KfState st;
+    load_kf(a.kf, slot, st);
+    kf_update(st, a.det_xyah + det * 4);
+    store_kf(a.kf, slot, st);
+    TrackMeta m = a.meta[slot];
+    const bool reactivate = st_of(m.flags) != ST_TRACKED;
+    m.tracklet_len = reactivate ? 0 : m.tracklet_len + 1;
+    m.flags = (m.flags & ~FL_STATE) | ST_TRACKED | FL_ACTIVATED;
+    m.frame_id = fid;
+    m.score = a.det_conf[det];
+    m.cls = a.det_cls[det];
+    m.det_ind = det_local;
+    a.meta[slot] = m;
+}
+
+// ------------------------------------------------------------------------------------ k_stage1
+__global__ __launch_bounds__(GRID_T) void k_stage1(BtArgs a) {
+    const int s = blockIdx.y;
+    const int i = blockIdx.x * GRID_T + threadIdx.x;
+    const BtCounters *c = a.cnt + s;
+    const long long tb = (long long)s * a.CAP, db = (long long)s * a.MAXD;
+    if (i >= c->n_pool) return;
+    const int h = a.x1[tb + i];
+    int kind = 0;
+    if (h >= 0) {
+        const long long slot = tb + a.pool[tb + i];
+        kind = st_of(a.meta[slot].flags) == ST_TRACKED ? 1 : 2;   // update vs re_activate
+        const int d = a.high[db + h];
+        take_detection(a, slot, db + d, d, c->frame_id);
+    }
+    a.kind1[tb + i] = kind;
+}
+
+// ------------------------------------------------------------------------------------ k_prep23
+__global__ __launch_bounds__(BLK) void k_prep23(BtArgs a) {
+    __shared__ int wsum[32];
+    const int s = blockIdx.x;
+    BtCounters *c = a.cnt + s;
+    const long long tb = (long long)s * a.CAP, db = (long long)s * a.MAXD;
+    const int n_pool = c->n_pool, n_high = c->n_high;
+    int n_left = block_compact(
+        n_pool, wsum,
+        [&](int i) {
+            return a.x1[tb + i] < 0 && st_of(a.meta[tb + a.pool[tb + i]].flags) == ST_TRACKED;
+        },
+        [&](int i, int pos) {
+            a.left[tb + pos] = i;
+            a.left_box[tb + pos] = a.pool_box[tb + i];
+        });
+    int n_rest = block_compact(n_high, wsum, [&](int h) { return a.y1[db + h] < 0; },
+                               [&](int h, int pos) {
+                                   a.rest[db + pos] = h;
+                                   a.rest_box[db + pos] = a.high_box[db + h];
+                                   a.rest_score[db + pos] = a.high_score[db + h];
+                               });
+    if (threadIdx.x == 0) {
+        c->n_left = n_left;
+        c->n_rest = n_rest;
+    }
+}
+
+// ------------------------------------------------------------------------------------ k_stage23
+__global__ __launch_bounds__(GRID_T) void k_stage23(BtArgs a) {
+    const int s = blockIdx.y;
+    const int i = blockIdx.x * GRID_T + threadIdx.x;
+    const BtCounters *c = a.cnt + s;
+    const long long tb = (long long)s * a.CAP, db = (long long)s * a.MAXD;
+    const int n_left = c->n_left, n_unc = c->n_unc, fid = c->frame_id;
+    if (i < n_left) {
+        const long long slot = tb + a.pool[tb + a.left[tb + i]];
+        const int q = a.x2[tb + i];
+        if (q >= 0) {
+            const int d = a.second[db + q];
+            take_detection(a, slot, db + d, d, fid);
+            a.kind2[tb + i] = 1;
+        } else {
+            a.meta[slot].flags = (a.meta[slot].flags & ~FL_STATE) | ST_LOST;   // mark_lost
+            a.kind2[tb + i] = 0;
+        }
+    } else if (i < n_left + n_unc) {
+        const int j = i - n_left;
+        const long long slot = tb + a.unc[tb + j];
+        const int r = a.x3[tb + j];
+        if (r >= 0) {
+            const int d = a.high[db + a.rest[db + r]];
+            take_detection(a, slot, db + d, d, fid);
+        } else {
+            a.meta[slot].flags = (a.meta[slot].flags & ~FL_STATE) | ST_REMOVED | FL_REMOVED_NOW;
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------ k_finish
+__global__ __launch_bounds__(BLK) void k_finish(BtArgs a) {
+    __shared__ int wsum[32];
+    const int s = blockIdx.x, t = threadIdx.x;
+    BtCounters *c = a.cnt + s;
+    const long long tb = (long long)s * a.CAP, db = (long long)s * a.MAXD;
+    const int fid = c->frame_id;
+    const int n_tracked = c->n_tracked, n_lost = c->n_lost, n_pool = c->n_pool;
+    const int n_rest = c->n_rest, n_left = c->n_left, n_free = c->n_free;
+    const long long next_id = c->next_id;
+
+    // births in ascending order of the still-unmatched high detections (:242-248)
+    int n_births = block_compact(
+        n_rest, wsum,
+        [&](int j) { return a.y3[db + j] < 0 && a.rest_score[db + j] >= a.det_thresh; },
+        [&](int j, int pos) { a.birth[db + pos] = j; });
+    if (n_births > n_free) {
+        if (t == 0) atomicOr(&c->err, ERR_TRACK_CAPACITY);
+        n_births = n_free;
+    }
+    for (int b = t; b < n_births; b += BLK) {
+        const int slot = a.free_list[tb + b];
+        const int d = a.high[db + a.rest[db + a.birth[db + b]]];
+        KfState st;
+        kf_initiate(a.det_xyah + (db + d) * 4, st);
+        store_kf(a.kf, tb + slot, st);
+        TrackMeta m;
+        m.score = a.det_conf[db + d];
+        m.cls = a.det_cls[db + d];
+        m.id = next_id + 1 + b;
+        m.det_ind = d;
+        m.flags = ST_TRACKED | (fid == 1 ? FL_ACTIVATED : 0);
+        m.frame_id = fid;
+        m.start_frame = fid;
+        m.tracklet_len = 0;
+        m.pad = 0;
+        a.meta[tb + slot] = m;
+        a.newslot[tb + b] = slot;
+    }
+    // lost-track expiry (:250-253); end_frame == frame_id
+    for (int i = t; i < n_lost; i += BLK) {
+        const long long slot = tb + a.lost[tb + i];
+        TrackMeta m = a.meta[slot];
+        if (fid - m.frame_id > a.max_time_lost)
+            a.meta[slot].flags = (m.flags & ~FL_STATE) | ST_REMOVED | FL_REMOVED_NOW;
+    }
+    __syncthreads();
+    // tracked' = [Tracked survivors of tracked_stracks] ++ births ++ re-found (:257-261)
+    int n_t2 = block_compact(
+        n_tracked, wsum,
+        [&](int i) { return st_of(a.meta[tb + a.tracked[tb + i]].flags) == ST_TRACKED; },
+        [&](int i, int pos) { a.t2[tb + pos] = a.tracked[tb + i]; });
+    for (int b = t; b < n_births; b += BLK) a.t2[tb + n_t2 + b] = a.newslot[tb + b];
+    n_t2 += n_births;
+    n_t2 += block_compact(n_pool, wsum, [&](int i) { return a.kind1[tb + i] == 2; },
+                          [&](int i, int pos) { a.t2[tb + n_t2 + pos] = a.pool[tb + i]; });
+    // lost' = sub(lost, tracked') ++ newly lost, minus ids already in removed_stracks (:262-264)
+    int n_l2 = block_compact(
+        n_lost, wsum,
+        [&](int i) {
+            int f = a.meta[tb + a.lost[tb + i]].flags;
+            return st_of(f) != ST_TRACKED && !(f & FL_EVER_REMOVED);
+        },
+        [&](int i, int pos) { a.l2[tb + pos] = a.lost[tb + i]; });
+    n_l2 += block_compact(
+        n_left, wsum,
+        [&](int i) {
+            return a.kind2[tb + i] == 0 &&
+                   !(a.meta[tb + a.pool[tb + a.left[tb + i]]].flags & FL_EVER_REMOVED);
+        },
+        [&](int i, int pos) { a.l2[tb + n_l2 + pos] = a.pool[tb + a.left[tb + i]]; });
+    __syncthreads();
+    // this frame's removals join removed_stracks only now (:265)
+    for (int i = t; i < n_lost; i += BLK) {
+        const long long slot = tb + a.lost[tb + i];
+        int f = a.meta[slot].flags;
+        if (f & FL_REMOVED_NOW) a.meta[slot].flags = (f & ~FL_REMOVED_NOW) | FL_EVER_REMOVED;
+    }
+    for (int p = t; p < n_t2; p += BLK) {
+        const long long slot = tb + a.t2[tb + p];
+        a.tbox[tb + p] = kf_box(a.kf, slot);
+        a.tage[tb + p] = a.meta[slot].frame_id - a.meta[slot].start_frame;
+        a.dropA[tb + p] = 0;
+    }
+    for (int q = t; q < n_l2; q += BLK) {
+        const long long slot = tb + a.l2[tb + q];
+        a.lbox[tb + q] = kf_box(a.kf, slot);
+        a.lage[tb + q] = a.meta[slot].frame_id - a.meta[slot].start_frame;
+        a.dropB[tb + q] = 0;
+    }
+    if (t == 0) {
+        c->n_births = n_births;
+        c->next_id = next_id + n_births;
+        c->n_t2 = n_t2;
+        c->n_l2 = n_l2;
+    }
+}
+
+// ------------------------------------------------------------------------------------ k_dedup
+// remove_duplicate_stracks: every pair decides independently (set semantics), so the pairs can
+// be visited in any order.
+constexpr int DEDUP_ROWS_PER_WAVE = 4;
+constexpr int DEDUP_ROWS_PER_BLOCK = (GRID_T / WAVE) * DEDUP_ROWS_PER_WAVE;
+
+__global__ __launch_bounds__(GRID_T) void k_dedup(BtArgs a) {
+    const int s = blockIdx.y;
+    const BtCounters *c = a.cnt + s;
+    const int n_t2 = c->n_t2, n_l2 = c->n_l2;
+    const long long tb = (long long)s * a.CAP;
+    const int lane = lane_id(), wave = threadIdx.x / WAVE;
+    const int p0 = blockIdx.x * DEDUP_ROWS_PER_BLOCK + wave * DEDUP_ROWS_PER_WAVE;
+    if (p0 >= n_t2 || n_l2 == 0) return;
+    Box pb[DEDUP_ROWS_PER_WAVE];
+    int pa[DEDUP_ROWS_PER_WAVE];
+#pragma unroll
+    for (int r = 0; r < DEDUP_ROWS_PER_WAVE; ++r) {
+        int p = p0 + r < n_t2 ? p0 + r : p0;
+        pb[r] = a.tbox[tb + p];
+        pa[r] = a.tage[tb + p];
+    }
+    for (int q = lane; q < n_l2; q += WAVE) {
+        const Box lb = a.lbox[tb + q];
+        const int la = a.lage[tb + q];
+#pragma unroll
+        for (int r = 0; r < DEDUP_ROWS_PER_WAVE; ++r) {
+            if (p0 + r >= n_t2) continue;
+            if (!intersects(pb[r], lb)) continue;
+            if (1 - iou(pb[r], lb) < 0.15) {
+                if (pa[r] > la) a.dropB[tb + q] = 1;
+                else a.dropA[tb + p0 + r] = 1;
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------ k_output
+__global__ __launch_bounds__(BLK) void k_output(BtArgs a) {
+    __shared__ int wsum[32];
+    extern __shared__ __attribute__((aligned(16))) unsigned int live[];   // CAP bits
+    const int s = blockIdx.x, t = threadIdx.x;
+    BtCounters *c = a.cnt + s;
+    const long long tb = (long long)s * a.CAP;
+    const int n_t2 = c->n_t2, n_l2 = c->n_l2;
+    const int words = (a.CAP + 31) / 32;
+    for (int w = t; w < words; w += BLK) live[w] = 0u;
+    __syncthreads();
+    int n_tr = block_compact(n_t2, wsum, [&](int p) { return a.dropA[tb + p] == 0; },
+                             [&](int p, int pos) {
+                                 int slot = a.t2[tb + p];
+                                 a.tracked[tb + pos] = slot;
+                                 atomicOr(&live[slot >> 5], 1u << (slot & 31));
+                             });
+    int n_lo = block_compact(n_l2, wsum, [&](int q) { return a.dropB[tb + q] == 0; },
+                             [&](int q, int pos) {
+                                 int slot = a.l2[tb + q];
+                                 a.lost[tb + pos] = slot;
+                                 atomicOr(&live[slot >> 5], 1u << (slot & 31));
+                             });
+    __syncthreads();
+    double *out = a.out + tb * 8;
+    int n_out = block_compact(
+        n_tr, wsum, [&](int i) { return (a.meta[tb + a.tracked[tb + i]].flags & FL_ACTIVATED) != 0; },
+        [&](int i, int pos) {
+            const long long slot = tb + a.tracked[tb + i];
+            const Box b = kf_box(a.kf, slot);
+            const TrackMeta m = a.meta[slot];
+            double *o = out + (long long)pos * 8;
+            o[0] = b.x1; o[1] = b.y1; o[2] = b.x2; o[3] = b.y2;
+            o[4] = (double)m.id;
+            o[5] = m.score;
+            o[6] = m.cls;
+            o[7] = (double)m.det_ind;
+        });
+    int n_free = block_compact(a.CAP, wsum,
+                               [&](int slot) { return !((live[slot >> 5] >> (slot & 31)) & 1u); },
+                               [&](int slot, int pos) { a.free_list[tb + pos] = slot; });
+    if (t == 0) {
+        c->n_tracked = n_tr;
+        c->n_lost = n_lo;
+        c->n_free = n_free;
+        c->n_out = n_out;
+        if (a.out_counts) a.out_counts[s] = n_out;
+    }
+}
+
+// Rebuild the free-slot list of every stream from its tracked + lost lists (after a reserve).
+__global__ __launch_bounds__(BLK) void k_rebuild_free(BtArgs a) {
+    __shared__ int wsum[32];
+    extern __shared__ __attribute__((aligned(16))) unsigned int live[];
+    const int s = blockIdx.x, t = threadIdx.x;
+    BtCounters *c = a.cnt + s;
+    const long long tb = (long long)s * a.CAP;
+    const int words = (a.CAP + 31) / 32;
+    for (int w = t; w < words; w += BLK) live[w] = 0u;
+    __syncthreads();
+    for (int i = t; i < c->n_tracked; i += BLK) {
+        int slot = a.tracked[tb + i];
+        atomicOr(&live[slot >> 5], 1u << (slot & 31));
+    }
+    for (int i = t; i < c->n_lost; i += BLK) {
+        int slot = a.lost[tb + i];
+        atomicOr(&live[slot >> 5], 1u << (slot & 31));
+    }
+    __syncthreads();
+    int n_free = block_compact(a.CAP, wsum,
+                               [&](int slot) { return !((live[slot >> 5] >> (slot & 31)) & 1u); },
+                               [&](int slot, int pos) { a.free_list[tb + pos] = slot; });
+    if (t == 0) c->n_free = n_free;
+}
+
+__global__ void k_reset(BtArgs a) {
+    const int s = blockIdx.x;
+    const long long tb = (long long)s * a.CAP;
+    for (int i = threadIdx.x; i < a.CAP; i += blockDim.x) a.free_list[tb + i] = i;
+    if (threadIdx.x == 0) {
+        BtCounters z;
+        memset(&z, 0, sizeof(z));
+        z.n_free = a.CAP;
+        a.cnt[s] = z;
+    }
+}
+
+}  // namespace
+}  // namespace yta
+
+// ================================================================================== host engine
+using namespace yta;
+
+struct yta_bytetrack {
+    int device = 0, S = 0, CAP = 0, MAXD = 0;
+    long long edge_cap = 0;
+    yta_bytetrack_params prm{};
+    hipStream_t stream = nullptr;
+    std::vector<void *> allocs;
+    BtArgs a{};
+    // association buffers: stage 1 and 2 share pool A, stage 3 uses pool B
+    Edge *edgesA = nullptr, *edgesB = nullptr;
+    int *wsA = nullptr, *wsB = nullptr;
+    double *wsdA = nullptr, *wsdB = nullptr;
+    long long ws_i = 0, ws_d = 0;
+    int *err_dummy = nullptr;
+    // host staging
+    double *h_dets = nullptr;
+    long long h_dets_cap = 0;
+    int *h_off = nullptr;
+    BtCounters *h_cnt = nullptr;
+    double *d_det_in = nullptr;
+    long long d_det_cap = 0;
+    int *d_det_off = nullptr;
+    // optional per-kernel timing with HIP events on the engine stream
+    bool prof = false;
+    std::vector<hipEvent_t> ev;
+    size_t ev_used = 0;
+};
+
+namespace {
+
+template <typename T>
+int dalloc(yta_bytetrack *e, T **p, long long n) {
+    void *q = nullptr;
+    if (n <= 0) n = 1;
+    hipError_t err = hipMalloc(&q, sizeof(T) * (size_t)n);
+    if (err != hipSuccess) {
+        set_error("hipMalloc(%lld bytes) failed: %s", (long long)(sizeof(T) * n), hipGetErrorString(err));
+        return YTA_ERR_NOMEM;
+    }
+    e->allocs.push_back(q);
+    *p = static_cast<T *>(q);
+    return YTA_OK;
+}
+
+#define DALLOC(ptr, n)                          \
+    do {                                        \
+        int _rc = dalloc(e, &(ptr), (n));       \
+        if (_rc) return _rc;                    \
+    } while (0)
+
+int bt_alloc(yta_bytetrack *e) {
+    const long long S = e->S, CAP = e->CAP, MAXD = e->MAXD;
+    BtArgs &a = e->a;
+    a.S = e->S;
+    a.CAP = e->CAP;
+    a.MAXD = e->MAXD;
+    a.track_thresh = e->prm.track_thresh;
+    a.match_thresh = e->prm.match_thresh;
+    a.det_thresh = e->prm.track_thresh;
+    a.max_time_lost = (int)(e->prm.frame_rate / 30.0 * e->prm.track_buffer);   // :128-129
+    DALLOC(a.kf, S * CAP * KF_REC);
+    DALLOC(a.meta, S * CAP);
+    DALLOC(a.tracked, S * CAP);
+    DALLOC(a.lost, S * CAP);
+    DALLOC(a.free_list, S * CAP);
+    DALLOC(a.cnt, S);
+    DALLOC(a.det_box, S * MAXD);
+    DALLOC(a.det_xyah, S * MAXD * 4);
+    DALLOC(a.det_conf, S * MAXD);
+    DALLOC(a.det_cls, S * MAXD);
+    DALLOC(a.high, S * MAXD);
+    DALLOC(a.second, S * MAXD);
+    DALLOC(a.rest, S * MAXD);
+    DALLOC(a.birth, S * MAXD);
+    DALLOC(a.high_box, S * MAXD);
+    DALLOC(a.second_box, S * MAXD);
+    DALLOC(a.rest_box, S * MAXD);
+    DALLOC(a.high_score, S * MAXD);
+    DALLOC(a.rest_score, S * MAXD);
+    DALLOC(a.pool, S * CAP);
+    DALLOC(a.unc, S * CAP);
+    DALLOC(a.left, S * CAP);
+    DALLOC(a.t2, S * CAP);
+    DALLOC(a.l2, S * CAP);
+    DALLOC(a.kind1, S * CAP);
+    DALLOC(a.kind2, S * CAP);
+    DALLOC(a.dropA, S * CAP);
+    DALLOC(a.dropB, S * CAP);
+    DALLOC(a.newslot, S * CAP);
+    DALLOC(a.pool_box, S * CAP);
+    DALLOC(a.unc_box, S * CAP);
+    DALLOC(a.left_box, S * CAP);
+    DALLOC(a.tbox, S * CAP);
+    DALLOC(a.lbox, S * CAP);
+    DALLOC(a.tage, S * CAP);
+    DALLOC(a.lage, S * CAP);
+    DALLOC(a.x1, S * CAP);
+    DALLOC(a.x2, S * CAP);
+    DALLOC(a.x3, S * CAP);
+    DALLOC(a.y1, S * MAXD);
+    DALLOC(a.y2, S * MAXD);
+    DALLOC(a.y3, S * MAXD);
+    DALLOC(a.out, S * CAP * 8);
+    // association: worst-case edge pools (every pair a candidate) so no frame can overflow
+    e->edge_cap = CAP * MAXD;
+    e->ws_i = lap_ws_ints((int)CAP, (int)MAXD, e->edge_cap);
+    e->ws_d = lap_ws_doubles((int)CAP, (int)MAXD, e->edge_cap);
+    DALLOC(e->edgesA, S * e->edge_cap);
+    DALLOC(e->edgesB, S * e->edge_cap);
+    DALLOC(e->wsA, S * e->ws_i);
+    DALLOC(e->wsB, S * e->ws_i);
+    DALLOC(e->wsdA, S * e->ws_d);
+    DALLOC(e->wsdB, S * e->ws_d);
+    DALLOC(e->d_det_off, S + 1);
+    YTA_HIP(hipHostMalloc((void **)&e->h_off, sizeof(int) * (S + 1), hipHostMallocDefault));
+    YTA_HIP(hipHostMalloc((void **)&e->h_cnt, sizeof(BtCounters) * S, hipHostMallocDefault));
+    return YTA_OK;
+}
+
+constexpr int BT_PHASES = 14;   // see yta_bytetrack_profile_collect
+
+int mark(yta_bytetrack *e) {
+    if (!e->prof) return YTA_OK;
+    if (e->ev_used == e->ev.size()) {
+        hipEvent_t h;
+        YTA_HIP(hipEventCreate(&h));
+        e->ev.push_back(h);
+    }
+    YTA_HIP(hipEventRecord(e->ev[e->ev_used++], e->stream));
+    return YTA_OK;
+}
+
+#define MARK()                      \
+    do {                            \
+        int _m = mark(e);           \
+        if (_m) return _m;          \
+    } while (0)
+
+// One association stage over all S streams: edges + exact sparse solve -> x (rows), y (cols).
+int run_stage(yta_bytetrack *e, int stage, const Box *rows, const int *n_rows_field,
+              const Box *cols, const double *col_score, const int *n_cols_field, double thresh,
+              Edge *edges, int *ws, double *wsd, int *x, int *y) {
+    BtArgs &a = e->a;
+    const int cstride = (int)(sizeof(BtCounters) / sizeof(int));
+    ProblemSet ps{};
+    ps.rows = rows;
+    ps.rows_stride = a.CAP;
+    ps.n_rows = n_rows_field;
+    ps.n_rows_stride = cstride;
+    ps.cols = cols;
+    ps.cols_stride = a.MAXD;
+    ps.col_score = col_score;
+    ps.score_stride = a.MAXD;
+    ps.n_cols = n_cols_field;
+    ps.n_cols_stride = cstride;
+    ps.thresh = thresh;
+    ps.edges = edges;
+    ps.edges_stride = e->edge_cap;
+    ps.edge_cap = e->edge_cap;
+    ps.n_edges = &a.cnt[0].n_edges[stage];
+    ps.n_edges_stride = cstride;
+    ps.err = &a.cnt[0].err;
+    ps.err_stride = cstride;
+    ps.ws = ws;
+    ps.ws_stride = e->ws_i;
+    ps.wsd = wsd;
+    ps.wsd_stride = e->ws_d;
+    ps.max_rows = a.CAP;
+    ps.max_cols = a.MAXD;
+    ps.x = x;
+    ps.x_stride = a.CAP;
+    ps.y = y;
+    ps.y_stride = a.MAXD;
+    MARK();
+    YTA_HIP(launch_edges(ps, a.S, a.CAP, e->stream));
+    MARK();
+    YTA_HIP(launch_lap(ps, a.S, e->stream));
+    return YTA_OK;
+}
+
+int launch_pipeline(yta_bytetrack *e, const double *det_in, const int *det_off, double *out,
+                    int *out_counts) {
+    BtArgs &a = e->a;
+    a.det_in = det_in;
+    a.det_off = det_off;
+    a.out = out;
+    a.out_counts = out_counts;
+    const dim3 gt((a.CAP + GRID_T - 1) / GRID_T, a.S);
+    BtCounters *c0 = a.cnt;
+    MARK();
+    hipLaunchKernelGGL(k_begin, dim3(a.S), dim3(BLK), 0, e->stream, a);
+    YTA_HIP(hipGetLastError());
+    MARK();
+    hipLaunchKernelGGL(k_predict, gt, dim3(GRID_T), 0, e->stream, a);
+    YTA_HIP(hipGetLastError());
+    int rc = run_stage(e, 0, a.pool_box, &c0->n_pool, a.high_box, a.high_score, &c0->n_high,
+                       a.match_thresh, e->edgesA, e->wsA, e->wsdA, a.x1, a.y1);
+    if (rc) return rc;
+    MARK();
+    hipLaunchKernelGGL(k_stage1, gt, dim3(GRID_T), 0, e->stream, a);
+    YTA_HIP(hipGetLastError());
+    MARK();
+    hipLaunchKernelGGL(k_prep23, dim3(a.S), dim3(BLK), 0, e->stream, a);
+    YTA_HIP(hipGetLastError());
+    rc = run_stage(e, 1, a.left_box, &c0->n_left, a.second_box, nullptr, &c0->n_second, 0.5,
+                   e->edgesA, e->wsA, e->wsdA, a.x2, a.y2);
+    if (rc) return rc;
+    rc = run_stage(e, 2, a.unc_box, &c0->n_unc, a.rest_box, a.rest_score, &c0->n_rest, 0.7,
+                   e->edgesB, e->wsB, e->wsdB, a.x3, a.y3);
+    if (rc) return rc;
+    MARK();
+    hipLaunchKernelGGL(k_stage23, gt, dim3(GRID_T), 0, e->stream, a);
+    YTA_HIP(hipGetLastError());
+    MARK();
+    hipLaunchKernelGGL(k_finish, dim3(a.S), dim3(BLK), 0, e->stream, a);
+    YTA_HIP(hipGetLastError());
+    MARK();
+    const dim3 gd((a.CAP + DEDUP_ROWS_PER_BLOCK - 1) / DEDUP_ROWS_PER_BLOCK, a.S);
+    hipLaunchKernelGGL(k_dedup, gd, dim3(GRID_T), 0, e->stream, a);
+    YTA_HIP(hipGetLastError());
+    MARK();
+    const size_t live_bytes = sizeof(unsigned int) * ((a.CAP + 31) / 32);
+    hipLaunchKernelGGL(k_output, dim3(a.S), dim3(BLK), live_bytes, e->stream, a);
+    YTA_HIP(hipGetLastError());
+    MARK();
+    return YTA_OK;
+}
+
+void release_buffers(yta_bytetrack *e) {
+    for (void *p : e->allocs) (void)hipFree(p);
+    e->allocs.clear();
+    if (e->h_off) (void)hipHostFree(e->h_off);
+    if (e->h_cnt) (void)hipHostFree(e->h_cnt);
+    e->h_off = nullptr;
+    e->h_cnt = nullptr;
+}
+
+// Grow track capacity and/or max detections, keeping every stream's tracker state.
+int reserve(yta_bytetrack *e, int cap, int maxd) {
+    if (cap <= e->CAP && maxd <= e->MAXD) return YTA_OK;
+    cap = std::max(cap, e->CAP);
+    maxd = std::max(maxd, e->MAXD);
+    YTA_HIP(hipStreamSynchronize(e->stream));
+    yta_bytetrack *n = new (std::nothrow) yta_bytetrack();
+    YTA_CHECK(n, YTA_ERR_NOMEM, "out of host memory");
+    n->device = e->device;
+    n->S = e->S;
+    n->CAP = cap;
+    n->MAXD = maxd;
+    n->prm = e->prm;
+    n->stream = e->stream;
+    int rc = bt_alloc(n);
+    const size_t S = e->S, oc = e->CAP, nc = cap;
+    auto copy2d = [&](void *dst, size_t dpitch, const void *src, size_t spitch, size_t width,
+                      size_t height) -> int {
+        YTA_HIP(hipMemcpy2DAsync(dst, dpitch, src, spitch, width, height, hipMemcpyDeviceToDevice,
+                                 e->stream));
+        return YTA_OK;
+    };
+    if (!rc) rc = copy2d(n->a.kf, nc * KF_REC * 8, e->a.kf, oc * KF_REC * 8, oc * KF_REC * 8, S);
+    if (!rc) rc = copy2d(n->a.meta, nc * sizeof(TrackMeta), e->a.meta, oc * sizeof(TrackMeta),
+                         oc * sizeof(TrackMeta), S);
+    if (!rc) rc = copy2d(n->a.tracked, nc * 4, e->a.tracked, oc * 4, oc * 4, S);
+    if (!rc) rc = copy2d(n->a.lost, nc * 4, e->a.lost, oc * 4, oc * 4, S);
+    if (!rc) {
+        hipError_t he = hipMemcpyAsync(n->a.cnt, e->a.cnt, sizeof(BtCounters) * S,
+                                       hipMemcpyDeviceToDevice, e->stream);
+        if (he != hipSuccess) { set_error("reserve copy: %s", hipGetErrorString(he)); rc = YTA_ERR_HIP; }
+    }
+    if (!rc) {
+        const size_t live_bytes = sizeof(unsigned int) * ((nc + 31) / 32);
+        hipLaunchKernelGGL(k_rebuild_free, dim3(e->S), dim3(BLK), live_bytes, e->stream, n->a);
+        hipError_t he = hipGetLastError();
+        if (he == hipSuccess) he = hipStreamSynchronize(e->stream);
+        if (he != hipSuccess) { set_error("reserve: %s", hipGetErrorString(he)); rc = YTA_ERR_HIP; }
+    }
+    if (rc) {
+        n->stream = nullptr;
+        release_buffers(n);
+        delete n;
+        return rc;
+    }
+    memcpy(n->h_cnt, e->h_cnt, sizeof(BtCounters) * S);
+    release_buffers(e);
+    e->CAP = n->CAP;
+    e->MAXD = n->MAXD;
+    e->edge_cap = n->edge_cap;
+    e->allocs.swap(n->allocs);
+    e->a = n->a;
+    e->edgesA = n->edgesA; e->edgesB = n->edgesB;
+    e->wsA = n->wsA; e->wsB = n->wsB;
+    e->wsdA = n->wsdA; e->wsdB = n->wsdB;
+    e->ws_i = n->ws_i; e->ws_d = n->ws_d;
+    e->h_off = n->h_off; e->h_cnt = n->h_cnt;
+    e->d_det_off = n->d_det_off;
+    n->h_off = nullptr; n->h_cnt = nullptr; n->stream = nullptr;
+    delete n;
+    return YTA_OK;
+}
+
+int check_errors(yta_bytetrack *e) {
+    for (int s = 0; s < e->S; ++s) {
+        int err = e->h_cnt[s].err;
+        if (err) {
+            set_error("stream %d: device error flags 0x%x (%s%s%s%s)", s, err,
+                      err & ERR_EDGE_OVERFLOW ? "edge pool overflow " : "",
+                      err & ERR_SOLVER ? "assignment solver failure " : "",
+                      err & ERR_TRACK_CAPACITY ? "track capacity exceeded " : "",
+                      err & ERR_DET_CAPACITY ? "too many detections " : "");
+            return (err & (ERR_TRACK_CAPACITY | ERR_DET_CAPACITY | ERR_EDGE_OVERFLOW))
+                       ? YTA_ERR_CAPACITY : YTA_ERR_HIP;
+        }
+    }
+    return YTA_OK;
+}
+
+int read_counters(yta_bytetrack *e) {
+    YTA_HIP(hipMemcpyAsync(e->h_cnt, e->a.cnt, sizeof(BtCounters) * e->S, hipMemcpyDeviceToHost,
+                           e->stream));
+    YTA_HIP(hipStreamSynchronize(e->stream));
+    return YTA_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int yta_bytetrack_create(int device, int n_streams, int track_capacity, int max_dets,
+                         const yta_bytetrack_params *params, yta_bytetrack **engine) {
+    YTA_CHECK(engine && params, YTA_ERR_INVALID, "null engine/params");
+    YTA_CHECK(n_streams > 0 && track_capacity > 0 && max_dets > 0, YTA_ERR_INVALID,
+              "n_streams, track_capacity and max_dets must be positive");
+    YTA_CHECK(params->frame_rate > 0 && params->track_buffer >= 0, YTA_ERR_INVALID,
+              "frame_rate must be > 0 and track_buffer >= 0");
+    *engine = nullptr;
+    int rc = select_device(device);
+    if (rc) return rc;
+    yta_bytetrack *e = new (std::nothrow) yta_bytetrack();
+    YTA_CHECK(e, YTA_ERR_NOMEM, "out of host memory");
+    e->device = device;
+    e->S = n_streams;
+    e->CAP = track_capacity;
+    e->MAXD = max_dets;
+    e->prm = *params;
+    hipError_t he = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
+    if (he != hipSuccess) {
+        set_error("hipStreamCreate: %s", hipGetErrorString(he));
+        delete e;
+        return YTA_ERR_HIP;
+    }
+    rc = bt_alloc(e);
+    if (!rc) rc = yta_bytetrack_reset(e);
+    if (rc) {
+        yta_bytetrack_destroy(e);
+        return rc;
+    }
+    *engine = e;
+    return YTA_OK;
+}
+
+int yta_bytetrack_destroy(yta_bytetrack *e) {
+    if (!e) return YTA_OK;
+    (void)hipSetDevice(e->device);
+    if (e->stream) (void)hipStreamSynchronize(e->stream);
+    release_buffers(e);
+    if (e->h_dets) (void)hipHostFree(e->h_dets);
+    if (e->d_det_in) (void)hipFree(e->d_det_in);
+    for (hipEvent_t h : e->ev) (void)hipEventDestroy(h);
+    if (e->stream) (void)hipStreamDestroy(e->stream);
+    delete e;
+    return YTA_OK;
+}
+
+int yta_bytetrack_reset(yta_bytetrack *e) {
+    YTA_CHECK(e, YTA_ERR_INVALID, "null engine");
+    YTA_HIP(hipSetDevice(e->device));
+    hipLaunchKernelGGL(k_reset, dim3(e->S), dim3(256), 0, e->stream, e->a);
+    YTA_HIP(hipGetLastError());
+    YTA_HIP(hipMemsetAsync(e->a.meta, 0, sizeof(TrackMeta) * (size_t)e->S * e->CAP, e->stream));
+    YTA_HIP(hipStreamSynchronize(e->stream));
+    memset(e->h_cnt, 0, sizeof(BtCounters) * e->S);
+    return YTA_OK;
+}
+
+int yta_bytetrack_update(yta_bytetrack *e, const double *dets, const int *det_offsets,
+                         long long *next_id, double *out, int out_capacity, int *out_offsets) {
+    YTA_CHECK(e && det_offsets && out_offsets, YTA_ERR_INVALID, "null argument");
+    YTA_HIP(hipSetDevice(e->device));
+    const int S = e->S;
+    YTA_CHECK(det_offsets[0] == 0, YTA_ERR_INVALID, "det_offsets[0] must be 0");
+    int need_d = e->MAXD, need_c = e->CAP;
+    for (int s = 0; s < S; ++s) {
+        const int m = det_offsets[s + 1] - det_offsets[s];
+        YTA_CHECK(m >= 0, YTA_ERR_INVALID, "det_offsets must be non-decreasing");
+        need_d = std::max(need_d, m);
+        need_c = std::max(need_c, e->h_cnt[s].n_tracked + e->h_cnt[s].n_lost + m);
+    }
+    if (need_d > e->MAXD || need_c > e->CAP) {   // grow geometrically, keeping all state
+        int rc = reserve(e, need_c > e->CAP ? std::max(need_c, 2 * e->CAP) : e->CAP,
+                         need_d > e->MAXD ? std::max(need_d, 2 * e->MAXD) : e->MAXD);
+        if (rc) return rc;
+    }
+    const long long total = det_offsets[S];
+    YTA_CHECK(total == 0 || dets, YTA_ERR_INVALID, "null dets");
+    if (total > e->d_det_cap) {
+        if (e->d_det_in) (void)hipFree(e->d_det_in);
+        if (e->h_dets) (void)hipHostFree(e->h_dets);
+        e->d_det_in = nullptr;
+        e->h_dets = nullptr;
+        long long cap = std::max<long long>(total, 1024);
+        YTA_HIP(hipMalloc((void **)&e->d_det_in, sizeof(double) * 6 * cap));
+        YTA_HIP(hipHostMalloc((void **)&e->h_dets, sizeof(double) * 6 * cap, hipHostMallocDefault));
+        e->d_det_cap = cap;
+    }
+    if (total) {
+        memcpy(e->h_dets, dets, sizeof(double) * 6 * total);
+        YTA_HIP(hipMemcpyAsync(e->d_det_in, e->h_dets, sizeof(double) * 6 * total,
+                               hipMemcpyHostToDevice, e->stream));
+    }
+    memcpy(e->h_off, det_offsets, sizeof(int) * (S + 1));
+    YTA_HIP(hipMemcpyAsync(e->d_det_off, e->h_off, sizeof(int) * (S + 1), hipMemcpyHostToDevice,
+                           e->stream));
+    if (next_id) {
+        for (int s = 0; s < S; ++s) e->h_cnt[s].next_id = next_id[s];
+        YTA_HIP(hipMemcpy2DAsync(&e->a.cnt[0].next_id, sizeof(BtCounters), &e->h_cnt[0].next_id,
+                                 sizeof(BtCounters), sizeof(long long), S, hipMemcpyHostToDevice,
+                                 e->stream));
+    }
+    int rc = launch_pipeline(e, e->d_det_in, e->d_det_off, e->a.out, nullptr);
+    if (rc) return rc;
+    rc = read_counters(e);
+    if (rc) return rc;
+    rc = check_errors(e);
+    if (rc) return rc;
+    long long rows = 0;
+    out_offsets[0] = 0;
+    for (int s = 0; s < S; ++s) {
+        rows += e->h_cnt[s].n_out;
+        out_offsets[s + 1] = (int)rows;
+    }
+    YTA_CHECK(rows <= out_capacity, YTA_ERR_CAPACITY, "output needs %lld rows > capacity %d", rows,
+              out_capacity);
+    YTA_CHECK(rows == 0 || out, YTA_ERR_INVALID, "null out");
+    for (int s = 0; s < S; ++s) {
+        const int n = e->h_cnt[s].n_out;
+        if (n)
+            YTA_HIP(hipMemcpyAsync(out + (long long)out_offsets[s] * 8,
+                                   e->a.out + (long long)s * e->CAP * 8, sizeof(double) * 8 * n,
+                                   hipMemcpyDeviceToHost, e->stream));
+    }
+    YTA_HIP(hipStreamSynchronize(e->stream));
+    if (next_id)
+        for (int s = 0; s < S; ++s) next_id[s] = e->h_cnt[s].next_id;
+    return YTA_OK;
+}
+
+int yta_bytetrack_update_device(yta_bytetrack *e, const double *d_dets, const int *d_det_offsets,
+                                double *d_out, int *d_out_counts) {
+    YTA_CHECK(e && d_det_offsets && d_out, YTA_ERR_INVALID, "null argument");
+    return launch_pipeline(e, d_dets, d_det_offsets, d_out, d_out_counts);
+}
+
+int yta_bytetrack_sync(yta_bytetrack *e) {
+    YTA_CHECK(e, YTA_ERR_INVALID, "null engine");
+    int rc = read_counters(e);
+    if (rc) return rc;
+    return check_errors(e);
+}
+
+int yta_bytetrack_get_state(yta_bytetrack *e, int stream, int *n_tracks, long long *ints,
+                            double *mean, double *cov) {
+    YTA_CHECK(e && n_tracks && ints && mean && cov, YTA_ERR_INVALID, "null argument");
+    YTA_CHECK(stream >= 0 && stream < e->S, YTA_ERR_INVALID, "bad stream %d", stream);
+    YTA_HIP(hipSetDevice(e->device));
+    int rc = read_counters(e);
+    if (rc) return rc;
+    const BtCounters c = e->h_cnt[stream];
+    const long long tb = (long long)stream * e->CAP;
+    std::vector<int> tr(c.n_tracked), lo(c.n_lost);
+    std::vector<double> kf((size_t)e->CAP * KF_REC);
+    std::vector<TrackMeta> meta(e->CAP);
+    if (c.n_tracked)
+        YTA_HIP(hipMemcpy(tr.data(), e->a.tracked + tb, sizeof(int) * c.n_tracked, hipMemcpyDeviceToHost));
+    if (c.n_lost)
+        YTA_HIP(hipMemcpy(lo.data(), e->a.lost + tb, sizeof(int) * c.n_lost, hipMemcpyDeviceToHost));
+    YTA_HIP(hipMemcpy(kf.data(), e->a.kf + tb * KF_REC, sizeof(double) * KF_REC * e->CAP, hipMemcpyDeviceToHost));
+    YTA_HIP(hipMemcpy(meta.data(), e->a.meta + tb, sizeof(TrackMeta) * e->CAP, hipMemcpyDeviceToHost));
+    int n = 0;
+    for (int which = 0; which < 2; ++which) {
+        const std::vector<int> &lst = which ? lo : tr;
+        for (int slot : lst) {
+            const TrackMeta &m = meta[slot];
+            long long *ii = ints + (long long)n * 7;
+            ii[0] = which;
+            ii[1] = m.id;
+            ii[2] = m.flags & FL_STATE;
+            ii[3] = (m.flags & FL_ACTIVATED) ? 1 : 0;
+            ii[4] = m.frame_id;
+            ii[5] = m.start_frame;
+            ii[6] = m.tracklet_len;
+            const double *r = kf.data() + (size_t)slot * KF_REC;
+            for (int k = 0; k < 8; ++k) mean[(long long)n * 8 + k] = r[k];
+            for (int i = 0; i < 8; ++i)
+                for (int j = 0; j < 8; ++j) cov[(long long)n * 64 + i * 8 + j] = r[8 + pidx(i, j)];
+            ++n;
+        }
+    }
+    *n_tracks = n;
+    return YTA_OK;
+}
+
+int yta_bytetrack_reserve(yta_bytetrack *e, int track_capacity, int max_dets) {
+    YTA_CHECK(e, YTA_ERR_INVALID, "null engine");
+    YTA_HIP(hipSetDevice(e->device));
+    return reserve(e, track_capacity, max_dets);
+}
+
+int yta_bytetrack_capacity(yta_bytetrack *e, int *track_capacity, int *max_dets) {
+    YTA_CHECK(e && track_capacity && max_dets, YTA_ERR_INVALID, "null argument");
+    *track_capacity = e->CAP;
+    *max_dets = e->MAXD;
+    return YTA_OK;
+}
+
+int yta_bytetrack_profile(yta_bytetrack *e, int enable) {
+    YTA_CHECK(e, YTA_ERR_INVALID, "null engine");
+    YTA_HIP(hipStreamSynchronize(e->stream));
+    e->prof = enable != 0;
+    e->ev_used = 0;
+    return YTA_OK;
+}
+
+// Per-kernel time summed over the frames run since profiling was enabled / last collected:
+// ms[k] for the 14 launches of one frame in order (begin, predict, edges1, lap1, stage1, prep23,
+// edges2, lap2, edges3, lap3, stage23, finish, dedup, output); *frames = frames covered.
+int yta_bytetrack_profile_collect(yta_bytetrack *e, double *ms, int *frames) {
+    YTA_CHECK(e && ms && frames, YTA_ERR_INVALID, "null argument");
+    YTA_HIP(hipStreamSynchronize(e->stream));
+    const size_t per = BT_PHASES + 1;
+    for (int k = 0; k < BT_PHASES; ++k) ms[k] = 0.0;
+    *frames = (int)(e->ev_used / per);
+    for (int f = 0; f < *frames; ++f)
+        for (int k = 0; k < BT_PHASES; ++k) {
+            float t = 0.f;
+            YTA_HIP(hipEventElapsedTime(&t, e->ev[f * per + k], e->ev[f * per + k + 1]));
+            ms[k] += t;
+        }
+    e->ev_used = 0;
+    return YTA_OK;
+}
+
+int yta_bytetrack_hip_stream(yta_bytetrack *e, void **stream) {
+    YTA_CHECK(e && stream, YTA_ERR_INVALID, "null argument");
+    *stream = (void *)e->stream;
+    return YTA_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,73 @@
+// ByteTrack engine: device-resident state for S independent streams (see bytetrack.hip).
+#pragma once
+#include "assoc.hpp"
+#include "kf_xyah.hpp"
+
+namespace yta {
+
+// Track states (boxmot/trackers/bytetrack/basetrack.py:8-12) and flag bits.
+constexpr int ST_NEW = 0, ST_TRACKED = 1, ST_LOST = 2, ST_REMOVED = 3;
+constexpr int FL_STATE = 3;
+constexpr int FL_ACTIVATED = 4;      // STrack.is_activated
+constexpr int FL_EVER_REMOVED = 8;   // track_id is in BYTETracker.removed_stracks
+constexpr int FL_REMOVED_NOW = 16;   // marked removed in the current frame (joins removed_stracks at its end)
+
+constexpr int KF_REC = 48;           // doubles per Kalman record: mean 8 + packed cov 36 + pad (384 B)
+
+struct TrackMeta {                   // 48 B, one per slot
+    double score;
+    double cls;
+    long long id;
+    int det_ind;
+    int flags;
+    int frame_id;
+    int start_frame;
+    int tracklet_len;
+    int pad;
+};
+
+struct BtCounters {                  // one per stream, 128 B
+    long long next_id;               // last issued track id (BaseTrack._count)
+    int frame_id;
+    int n_tracked, n_lost, n_free;
+    int n_dets, n_high, n_second;
+    int n_pool, n_act, n_unc;
+    int n_left, n_rest, n_births;
+    int n_t2, n_l2, n_out;
+    int err;
+    int n_edges[3];
+    int pad[9];
+};
+static_assert(sizeof(BtCounters) == 128, "BtCounters layout");
+
+struct BtArgs {
+    int S, CAP, MAXD;
+    double track_thresh, match_thresh, det_thresh;
+    int max_time_lost;
+    // inputs
+    const double *det_in;     // packed rows of 6
+    const int *det_off;       // S+1
+    // persistent state
+    double *kf;               // [S*CAP][KF_REC]
+    TrackMeta *meta;          // [S*CAP]
+    int *tracked, *lost, *free_list;   // [S*CAP]
+    BtCounters *cnt;          // [S]
+    // per-frame: detections [S*MAXD]
+    Box *det_box;
+    double *det_xyah;         // [S*MAXD][4]
+    double *det_conf, *det_cls;
+    int *high, *second, *rest, *birth;
+    Box *high_box, *second_box, *rest_box;
+    double *high_score, *rest_score;
+    // per-frame: tracks [S*CAP]
+    int *pool, *unc, *left, *t2, *l2, *kind1, *kind2, *dropA, *dropB, *newslot;
+    Box *pool_box, *unc_box, *left_box, *tbox, *lbox;
+    int *tage, *lage;
+    // association results
+    int *x1, *y1, *x2, *y2, *x3, *y3;   // x*: [S*CAP], y*: [S*MAXD]
+    // outputs
+    double *out;              // [S*CAP][8]
+    int *out_counts;          // optional [S]
+};
+
+}  // namespace yta

@@ -1,0 +1,236 @@
+// Parity / known-answer entry points: the individual association and Kalman primitives on the
+// device, synchronous, host buffers in and out.  The tracker engine uses the same device
+// functions (geometry.hpp, kf_xyah.hpp, assoc.hip).
+#include <vector>
+
+#include "assoc.hpp"
+#include "kf_xyah.hpp"
+
+using namespace yta;
+
+namespace {
+
+__global__ void k_affinity(int kind, const Box *a, int na, const Box *b, int nb, double w,
+                           double h, double *out) {
+    const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= (long long)na * nb) return;
+    const int i = (int)(idx / nb), j = (int)(idx % nb);
+    const Box &p = a[i], &q = b[j];
+    double v;
+    switch (kind) {
+        case YTA_AFF_IOU: v = iou(p, q); break;
+        case YTA_AFF_GIOU: v = giou(p, q); break;
+        case YTA_AFF_DIOU: v = diou(p, q); break;
+        case YTA_AFF_CIOU: v = ciou(p, q); break;
+        default: v = centroid(p, q, w, h); break;
+    }
+    out[idx] = v;
+}
+
+__global__ void k_iou_distance(const Box *a, int na, const Box *b, int nb, const double *score,
+                               double *out) {
+    const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= (long long)na * nb) return;
+    const int i = (int)(idx / nb), j = (int)(idx % nb);
+    double d = 1 - iou(a[i], b[j]);
+    if (score) d = 1 - (1 - d) * score[j];
+    out[idx] = d;
+}
+
+__global__ void k_kf(int op, int n, const double *in_vec, double *mean, double *cov) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    KfState s;
+    if (op == 0) {
+        kf_initiate(in_vec + 4 * i, s);
+    } else {
+        for (int k = 0; k < 8; ++k) s.m[k] = mean[8 * i + k];
+        for (int r = 0; r < 8; ++r)
+            for (int c = r; c < 8; ++c) s.p[pidx(r, c)] = cov[64 * i + 8 * r + c];
+        if (op == 1) kf_predict(s);
+        else kf_update(s, in_vec + 4 * i);
+    }
+    for (int k = 0; k < 8; ++k) mean[8 * i + k] = s.m[k];
+    for (int r = 0; r < 8; ++r)
+        for (int c = 0; c < 8; ++c) cov[64 * i + 8 * r + c] = s.p[pidx(r, c)];
+}
+
+// cost matrix -> Box-free edge pool for the sparse solver (KAT path only)
+__global__ void k_dense_edges(const double *cost, int nr, int nc, double thresh, Edge *edges,
+                              int *n_edges) {
+    const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= (long long)nr * nc) return;
+    const double c = cost[idx];
+    if (c < thresh) {
+        int pos = atomicAdd(n_edges, 1);
+        Edge e;
+        e.row = (int)(idx / nc);
+        e.col = (int)(idx % nc);
+        e.cost = c;
+        edges[pos] = e;
+    }
+}
+
+struct DevBuf {
+    std::vector<void *> ptrs;
+    ~DevBuf() {
+        for (void *p : ptrs) (void)hipFree(p);
+    }
+    template <typename T>
+    hipError_t get(T **p, size_t n) {
+        void *q = nullptr;
+        hipError_t e = hipMalloc(&q, sizeof(T) * (n ? n : 1));
+        if (e == hipSuccess) ptrs.push_back(q);
+        *p = (T *)q;
+        return e;
+    }
+};
+
+}  // namespace
+
+extern "C" {
+
+int yta_box_affinity(int device, int kind, const double *a, int na, const double *b, int nb,
+                     double img_w, double img_h, double *out) {
+    YTA_CHECK(kind >= 0 && kind <= 4, YTA_ERR_INVALID, "unknown affinity kind %d", kind);
+    YTA_CHECK(na >= 0 && nb >= 0, YTA_ERR_INVALID, "negative size");
+    if ((long long)na * nb == 0) return YTA_OK;
+    YTA_CHECK(a && b && out, YTA_ERR_INVALID, "null buffer");
+    int rc = select_device(device);
+    if (rc) return rc;
+    DevBuf m;
+    Box *da, *db;
+    double *dout;
+    const long long n = (long long)na * nb;
+    YTA_HIP(m.get(&da, na));
+    YTA_HIP(m.get(&db, nb));
+    YTA_HIP(m.get(&dout, n));
+    YTA_HIP(hipMemcpy(da, a, sizeof(Box) * na, hipMemcpyHostToDevice));
+    YTA_HIP(hipMemcpy(db, b, sizeof(Box) * nb, hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(k_affinity, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, 0, kind, da, na,
+                       db, nb, img_w, img_h, dout);
+    YTA_HIP(hipGetLastError());
+    YTA_HIP(hipMemcpy(out, dout, sizeof(double) * n, hipMemcpyDeviceToHost));
+    if (kind == YTA_AFF_GIOU) {
+        // iou.py:58 asserts a positive enclosure; NaN marks the violation
+        for (long long k = 0; k < n; ++k)
+            YTA_CHECK(out[k] == out[k], YTA_ERR_INVALID, "giou: degenerate enclosing box");
+    }
+    return YTA_OK;
+}
+
+int yta_iou_distance(int device, const double *a, int na, const double *b, int nb,
+                     const double *scores, double *out) {
+    YTA_CHECK(na >= 0 && nb >= 0, YTA_ERR_INVALID, "negative size");
+    if ((long long)na * nb == 0) return YTA_OK;
+    YTA_CHECK(a && b && out, YTA_ERR_INVALID, "null buffer");
+    int rc = select_device(device);
+    if (rc) return rc;
+    DevBuf m;
+    Box *da, *db;
+    double *dout, *ds = nullptr;
+    const long long n = (long long)na * nb;
+    YTA_HIP(m.get(&da, na));
+    YTA_HIP(m.get(&db, nb));
+    YTA_HIP(m.get(&dout, n));
+    YTA_HIP(hipMemcpy(da, a, sizeof(Box) * na, hipMemcpyHostToDevice));
+    YTA_HIP(hipMemcpy(db, b, sizeof(Box) * nb, hipMemcpyHostToDevice));
+    if (scores) {
+        YTA_HIP(m.get(&ds, nb));
+        YTA_HIP(hipMemcpy(ds, scores, sizeof(double) * nb, hipMemcpyHostToDevice));
+    }
+    hipLaunchKernelGGL(k_iou_distance, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, 0, da, na,
+                       db, nb, ds, dout);
+    YTA_HIP(hipGetLastError());
+    YTA_HIP(hipMemcpy(out, dout, sizeof(double) * n, hipMemcpyDeviceToHost));
+    return YTA_OK;
+}
+
+static int kf_call(int device, int op, int n, const double *vec, double *mean, double *cov) {
+    YTA_CHECK(n >= 0, YTA_ERR_INVALID, "negative n");
+    if (n == 0) return YTA_OK;
+    YTA_CHECK(mean && cov && (op == 1 || vec), YTA_ERR_INVALID, "null buffer");
+    int rc = select_device(device);
+    if (rc) return rc;
+    DevBuf m;
+    double *dv = nullptr, *dm, *dc;
+    YTA_HIP(m.get(&dm, 8 * (size_t)n));
+    YTA_HIP(m.get(&dc, 64 * (size_t)n));
+    if (op != 1) {
+        YTA_HIP(m.get(&dv, 4 * (size_t)n));
+        YTA_HIP(hipMemcpy(dv, vec, sizeof(double) * 4 * n, hipMemcpyHostToDevice));
+    }
+    if (op != 0) {
+        YTA_HIP(hipMemcpy(dm, mean, sizeof(double) * 8 * n, hipMemcpyHostToDevice));
+        YTA_HIP(hipMemcpy(dc, cov, sizeof(double) * 64 * n, hipMemcpyHostToDevice));
+    }
+    hipLaunchKernelGGL(k_kf, dim3((n + 127) / 128), dim3(128), 0, 0, op, n, dv, dm, dc);
+    YTA_HIP(hipGetLastError());
+    YTA_HIP(hipMemcpy(mean, dm, sizeof(double) * 8 * n, hipMemcpyDeviceToHost));
+    YTA_HIP(hipMemcpy(cov, dc, sizeof(double) * 64 * n, hipMemcpyDeviceToHost));
+    return YTA_OK;
+}
+
+int yta_kf_xyah_initiate(int device, int n, const double *meas, double *mean, double *cov) {
+    return kf_call(device, 0, n, meas, mean, cov);
+}
+int yta_kf_xyah_predict(int device, int n, double *mean, double *cov) {
+    return kf_call(device, 1, n, nullptr, mean, cov);
+}
+int yta_kf_xyah_update(int device, int n, double *mean, double *cov, const double *z) {
+    return kf_call(device, 2, n, z, mean, cov);
+}
+
+int yta_lap_limited(int device, int nr, int nc, const double *cost, double cost_limit, int *x,
+                    int *y) {
+    YTA_CHECK(nr >= 0 && nc >= 0, YTA_ERR_INVALID, "negative size");
+    YTA_CHECK(cost_limit == cost_limit, YTA_ERR_INVALID, "cost_limit is NaN");
+    for (int i = 0; i < nr; ++i) x[i] = -1;
+    for (int j = 0; j < nc; ++j) y[j] = -1;
+    if ((long long)nr * nc == 0) return YTA_OK;
+    YTA_CHECK(cost && x && y, YTA_ERR_INVALID, "null buffer");
+    int rc = select_device(device);
+    if (rc) return rc;
+    DevBuf m;
+    const long long n = (long long)nr * nc;
+    double *dcost, *wsd;
+    Edge *edges;
+    int *ws, *dx, *dy, *cnt;   // cnt: [rows, cols, n_edges, err]
+    const long long E = n;
+    const long long wsi = lap_ws_ints(nr, nc, E), wsdn = lap_ws_doubles(nr, nc, E);
+    YTA_HIP(m.get(&dcost, n));
+    YTA_HIP(m.get(&edges, E));
+    YTA_HIP(m.get(&ws, wsi));
+    YTA_HIP(m.get(&wsd, wsdn));
+    YTA_HIP(m.get(&dx, nr));
+    YTA_HIP(m.get(&dy, nc));
+    YTA_HIP(m.get(&cnt, 4));
+    int h_cnt[4] = {nr, nc, 0, 0};
+    YTA_HIP(hipMemcpy(cnt, h_cnt, sizeof(h_cnt), hipMemcpyHostToDevice));
+    YTA_HIP(hipMemcpy(dcost, cost, sizeof(double) * n, hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(k_dense_edges, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, 0, dcost, nr,
+                       nc, cost_limit, edges, cnt + 2);
+    YTA_HIP(hipGetLastError());
+    ProblemSet ps{};
+    ps.n_rows = cnt;
+    ps.n_cols = cnt + 1;
+    ps.thresh = cost_limit;
+    ps.edges = edges;
+    ps.edge_cap = E;
+    ps.n_edges = cnt + 2;
+    ps.err = cnt + 3;
+    ps.ws = ws;
+    ps.wsd = wsd;
+    ps.max_rows = nr;
+    ps.max_cols = nc;
+    ps.x = dx;
+    ps.y = dy;
+    YTA_HIP(launch_lap(ps, 1, 0));
+    YTA_HIP(hipMemcpy(x, dx, sizeof(int) * nr, hipMemcpyDeviceToHost));
+    YTA_HIP(hipMemcpy(y, dy, sizeof(int) * nc, hipMemcpyDeviceToHost));
+    YTA_HIP(hipMemcpy(h_cnt, cnt, sizeof(h_cnt), hipMemcpyDeviceToHost));
+    YTA_CHECK(h_cnt[3] == 0, YTA_ERR_HIP, "assignment solver error flags 0x%x", h_cnt[3]);
+    return YTA_OK;
+}
+
+}  // extern "C"
