@@ -26,8 +26,9 @@ import numpy as np
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
-PHASES = ["begin", "predict", "edges1", "lap1", "stage1", "prep23", "edges2", "lap2", "edges3",
-          "lap3", "stage23", "finish", "dedup", "output"]
+PHASES = ["begin", "edges1", "lap1", "prep23", "edges23", "lap23", "apply", "finish"]
+STATS = ["dets", "high", "second", "pool", "act", "unc", "left", "rest", "births", "t2", "l2",
+         "tracked", "lost", "out", "edges1", "edges23"]
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # Canonical algorithmic bytes per update: ByteTrack 1024 x 1024
 BYTES_PER_UPDATE_1024 = 19_259_392
@@ -38,19 +39,25 @@ def algorithmic_bytes(n, m):
     return 4 * 576 * n + 56 * m + 16 * n * m + 64 * n
 
 
-def kernel_bytes(phase, n, m, streams):
-    """Algorithmic bytes one launch of `phase` moves for `streams` streams of n tracks x m dets
-    (DESIGN.md §Kernels): the KF kernels read+write the 352-B packed state per track; the cost /
-    edge kernel reads every track box and detection box+score once (the N x M cost itself is
-    never materialised: only c < cost_limit candidates are written)."""
-    per = {
-        "predict": 2 * 352 * n + 32 * n,
-        "stage1": 2 * 352 * n + 48 * n,
-        "edges1": 32 * n + 40 * m + 16 * n,
-        "lap1": 16 * n + 8 * (n + m),
-        "finish": 352 * m,
-    }.get(phase, 0)
-    return per * streams
+def kernel_bytes(phase, st):
+    """Algorithmic HBM bytes one launch of `phase` must move, from the last frame's counts summed
+    over streams.  Kalman record = 24 f64 (192 B), track meta = 48 B, box = 32 B,
+    detection row = 48 B, candidate edge = 16 B."""
+    pool, unc, high, dets = st["pool"], st["unc"], st["high"], st["dets"]
+    matched = st["tracked"]            # tracks updated this frame (upper bound: tracked list)
+    if phase == "apply":
+        # every pool track: KF state + meta read and written once, pool index + stage results read;
+        # every matched track: its detection's xyah / conf / cls read
+        return pool * (2 * 192 + 2 * 48 + 12) + unc * (48 + 8) + matched * 48
+    if phase == "begin":
+        return dets * (48 + 48 + 4) + high * (32 + 8 + 8) + pool * (64 + 48 + 32 + 4) + unc * 40
+    if phase == "edges1":
+        return pool * 32 + high * (32 + 8) + st["edges1"] * 16
+    if phase == "lap1":
+        return st["edges1"] * 16 + (pool + high) * 8
+    if phase == "finish":
+        return (st["t2"] + st["l2"]) * (32 + 48 + 12) + st["out"] * 64 + st["births"] * (192 + 48)
+    return 0
 
 
 def parse():
@@ -167,12 +174,19 @@ def main():
     value = calls / elapsed
     ms_per_step = 1000.0 * elapsed / args.steps
 
+    stats = (ctypes.c_longlong * 16)()
+    _lib.check(lib.yta_bytetrack_stats(h, stats))
+    st = {STATS[k]: int(stats[k]) for k in range(16)}
     if rank == 0:
-        dom = max((p for p in phase_ms if kernel_bytes(p, N, N, S)), key=lambda p: phase_ms[p])
+        # roofline kernel: the Kalman predict/update pass over every live track (HBM-bound)
+        dom = "apply"
         dom_ms = phase_ms[dom]
-        b = kernel_bytes(dom, N, N, S)
+        b = kernel_bytes(dom, st)
         achieved = b / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
         busiest = max(phase_ms, key=lambda p: phase_ms[p])
+        per_kernel = {p: {"ms": phase_ms[p], "alg_bytes": kernel_bytes(p, st),
+                          "gbs": (kernel_bytes(p, st) / (phase_ms[p] * 1e-3) / 1e9
+                                  if phase_ms[p] > 0 else 0.0)} for p in PHASES}
         cpu = None if args.no_cpu_baseline else cpu_baseline(N, args.cpu_frames, args.seed)
         line = {
             "metric": "tracker.update() calls/sec @ 1024 tracks×1024 dets; 1/2/4/8 MI355X",
@@ -187,7 +201,8 @@ def main():
                          "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                          "algorithmic_bytes_per_launch": b, "avg_launch_ms": dom_ms},
             "cpu_baseline": cpu,
-            "per_kernel_ms": phase_ms,
+            "per_kernel": per_kernel,
+            "frame_counts": st,
             "busiest_kernel": busiest,
             "single_stream_equiv_ms": ms_per_step,
             "algorithmic_bytes_per_update": algorithmic_bytes(N, N),

@@ -49,6 +49,12 @@ int yta_box_affinity(int device, int kind, const double *a, int na, const double
 int yta_iou_distance(int device, const double *a, int na, const double *b, int nb,
                      const double *scores, double *out);
 
+/* Grid-pruned pair search (the candidate machinery behind the tracker's association and
+ * duplicate removal): every (i, j) with 1 - IoU(a_i, b_j) < thresh, thresh <= 1; pairs[2k] = i,
+ * pairs[2k+1] = j in no particular order; *n_pairs = total found (only `cap` are written). */
+int yta_grid_pairs(int device, const double *a, int na, const double *b, int nb, double thresh,
+                   int *pairs, int cap, int *n_pairs);
+
 /* ---- ByteTrack Kalman filter, xyah state (parity / KAT entry points) -----------------------
  * mean: n x 8, cov: n x 8 x 8 (row-major, full matrices), meas / z: n x 4 [xc, yc, a, h]. */
 int yta_kf_xyah_initiate(int device, int n, const double *meas, double *mean, double *cov);
@@ -108,12 +114,20 @@ int yta_bytetrack_sync(yta_bytetrack *engine);      /* waits; reports device-sid
  * (64 f64).  *n_tracks receives the count; buffers must hold track_capacity entries. */
 int yta_bytetrack_get_state(yta_bytetrack *engine, int stream, int *n_tracks, long long *ints,
                             double *mean, double *cov);
-/* Measurement: when enabled, HIP events are recorded around each of the 14 launches of a frame on
+/* Measurement: when enabled, HIP events are recorded around each of the 8 launches of a frame on
  * the engine's stream; collect returns per-launch milliseconds summed over the covered frames in
- * launch order (begin, predict, edges1, lap1, stage1, prep23, edges2, lap2, edges3, lap3,
- * stage23, finish, dedup, output). */
+ * launch order (begin, edges1, lap1, prep23, edges23, lap23, apply, finish). */
 int yta_bytetrack_profile(yta_bytetrack *engine, int enable);
 int yta_bytetrack_profile_collect(yta_bytetrack *engine, double *ms, int *frames);
+/* Debug introspection of the last frame's duplicate removal (stream s): tracked' / lost' boxes
+ * (4 f64 each), ages (tracked' then lost'), drop flags (tracked' then lost').  Buffers hold
+ * track_capacity entries per list. */
+int yta_bytetrack_debug_dedup(yta_bytetrack *engine, int stream, int *n_t2, int *n_l2,
+                              double *tbox, double *lbox, int *ages, int *drops);
+/* Last frame's counts summed over streams (synchronises): dets, high, second, pool, activated,
+ * unconfirmed, leftovers, rest, births, tracked', lost', tracked, lost, output rows, stage-1
+ * candidate edges, stage-2+3 candidate edges (16 int64). */
+int yta_bytetrack_stats(yta_bytetrack *engine, long long *stats);
 /* Throughput helper: the engine's HIP stream (hipStream_t as void*) */
 int yta_bytetrack_hip_stream(yta_bytetrack *engine, void **stream);
 

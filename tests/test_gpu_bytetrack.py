@@ -102,6 +102,34 @@ def test_edge_cases_vs_oracle():
         _assert_rows(eng.update([d])[0], ref.update(d).reshape(-1, 8), f)
 
 
+@pytest.mark.parametrize("seed", [31, 32])
+def test_crowded_scene_vs_oracle(seed):
+    """Heavy overlap: large association components, many duplicate removals, dense grid cells."""
+    frames = [d for d, _ in make_frames(220, 25, seed=seed, canvas=260.0, speed_sigma=3.0,
+                                        turnover=0.08)]
+    eng = ByteTrackEngine(1, **KW)
+    ref = ByteTrackOracle(**KW)
+    for f, d in enumerate(frames):
+        _assert_rows(eng.update([d])[0], ref.update(d).reshape(-1, 8), (seed, f))
+
+
+def test_mixed_box_scales_vs_oracle():
+    """A few huge boxes among small ones (grid 'big' list) plus degenerate ones."""
+    rng = np.random.default_rng(8)
+    base = [d for d, _ in make_frames(150, 20, seed=9)]
+    frames = []
+    for d in base:
+        d = d.copy()
+        k = rng.choice(len(d), size=4, replace=False)
+        d[k, 2] = d[k, 0] + rng.uniform(300, 900, size=4)
+        d[k, 3] = d[k, 1] + rng.uniform(300, 900, size=4)
+        frames.append(d)
+    eng = ByteTrackEngine(1, **KW)
+    ref = ByteTrackOracle(**KW)
+    for f, d in enumerate(frames):
+        _assert_rows(eng.update([d])[0], ref.update(d).reshape(-1, 8), f)
+
+
 def test_capacity_growth_keeps_state():
     frames = [d for d, _ in make_frames(700, 8, seed=5)]
     eng = ByteTrackEngine(1, track_capacity=16, max_dets=8, **KW)   # forces several reserves

@@ -97,3 +97,41 @@ def test_lap_limited_empty():
     assert len(x) == 0 and np.all(y == -1)
     x, y = _lib.lap_limited(np.zeros((3, 0)), 0.8)
     assert np.all(x == -1) and len(y) == 0
+
+
+def _brute_pairs(a, b, thresh):
+    from oracle.geometry import iou_batch
+    if len(a) == 0 or len(b) == 0:
+        return np.zeros((0, 2), dtype=np.int32)
+    d = 1 - iou_batch(a, b)
+    i, j = np.nonzero(d < thresh)
+    p = np.stack([i, j], 1).astype(np.int32)
+    return p[np.lexsort((p[:, 1], p[:, 0]))]
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_grid_pairs_complete(seed):
+    """The grid prunes only non-intersecting pairs: results equal the brute-force IoU test."""
+    rng = np.random.default_rng(seed)
+    na, nb = rng.integers(1, 400, size=2)
+    canvas = rng.choice([60.0, 300.0, 2000.0])
+    def boxes(n):
+        xy = rng.uniform(0, canvas, size=(n, 2))
+        wh = rng.uniform(2, 64, size=(n, 2)) * rng.choice([1, 1, 1, 12], size=(n, 1))
+        return np.concatenate([xy, xy + wh], 1)
+    a, b = boxes(na), boxes(nb)
+    b[:3] = a[:3] + rng.normal(0, 1, size=(3, 4))
+    for thresh in (0.15, 0.5, 0.8, 1.0):
+        got = _lib.grid_pairs(a, b, thresh)
+        assert np.array_equal(got, _brute_pairs(a, b, thresh)), thresh
+
+
+def test_grid_pairs_mot17_dedup_case():
+    """The lost / tracked boxes of MOT17-02 frame 316 (a duplicate at IoU distance 0.129)."""
+    L = np.array([[430.97677576, 457.72682571, 460.54623113, 554.13059315],
+                  [848.0807521, 471.72410916, 911.79088983, 560.3342942],
+                  [539.63031215, 461.03830408, 563.40578585, 522.46247351],
+                  [550.07827234, 461.35683546, 573.58418471, 519.26254885]])
+    T = np.array([[548.52661677, 460.85409296, 572.20069217, 518.92964587]])
+    got = _lib.grid_pairs(T, L, 0.15)
+    assert np.array_equal(got, _brute_pairs(T, L, 0.15)) and len(got) == 1

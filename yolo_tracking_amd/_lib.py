@@ -51,6 +51,7 @@ _SIGS = {
     "yta_kf_xyah_initiate": ([_I, _I, _P, _P, _P], _I),
     "yta_kf_xyah_predict": ([_I, _I, _P, _P], _I),
     "yta_kf_xyah_update": ([_I, _I, _P, _P, _P], _I),
+    "yta_grid_pairs": ([_I, _P, _I, _P, _I, _D, _P, _I, _P], _I),
     "yta_lap_limited": ([_I, _I, _I, _P, _D, _P, _P], _I),
     "yta_bytetrack_create": ([_I, _I, _I, _I, _P, _P], _I),
     "yta_bytetrack_destroy": ([_P], _I),
@@ -63,6 +64,8 @@ _SIGS = {
     "yta_bytetrack_get_state": ([_P, _I, _P, _P, _P, _P], _I),
     "yta_bytetrack_profile": ([_P, _I], _I),
     "yta_bytetrack_profile_collect": ([_P, _P, _P], _I),
+    "yta_bytetrack_debug_dedup": ([_P, _I, _P, _P, _P, _P, _P, _P], _I),
+    "yta_bytetrack_stats": ([_P, _P], _I),
     "yta_bytetrack_hip_stream": ([_P, _P], _I),
 }
 
@@ -167,6 +170,22 @@ def kf_xyah_update(mean, cov, z, device=0):
     z = np.ascontiguousarray(z, dtype=np.float64).reshape(-1, 4)
     check(load_library().yta_kf_xyah_update(device, len(mean), ptr(mean), ptr(cov), ptr(z)))
     return mean, cov
+
+
+def grid_pairs(a, b, thresh, device=0):
+    """All (i, j) with 1 - IoU(a_i, b_j) < thresh, found through the device grid (sorted)."""
+    a = np.ascontiguousarray(a, dtype=np.float64).reshape(-1, 4)
+    b = np.ascontiguousarray(b, dtype=np.float64).reshape(-1, 4)
+    cap = max(16, 8 * (len(a) + len(b)))
+    while True:
+        pairs = np.empty((cap, 2), dtype=np.int32)
+        n = ctypes.c_int()
+        check(load_library().yta_grid_pairs(device, ptr(a), len(a), ptr(b), len(b), float(thresh),
+                                            ptr(pairs), cap, ctypes.byref(n)))
+        if n.value <= cap:
+            p = pairs[:n.value]
+            return p[np.lexsort((p[:, 1], p[:, 0]))]
+        cap = n.value
 
 
 def lap_limited(cost, cost_limit, device=0):

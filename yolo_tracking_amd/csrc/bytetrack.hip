@@ -1,19 +1,26 @@
 // ByteTrack update() for S independent streams on gfx950, all state resident in HBM.
 //
-// Follows boxmot/trackers/bytetrack/byte_tracker.py:132-325.  Per frame (every launch covers all
-// S streams; "block/stream" kernels do the order-preserving list algebra with block-wide scans):
-//   k_begin     [block/stream]  frame_id++, confidence split (:149-158), STrack box conversions
-//                               (:14-25), tracked -> activated / unconfirmed, pool = act ++ lost
-//   k_predict   [grid]          STrack.multi_predict over the pool (:35-48) + pool / unconfirmed boxes
-//   stage 1     edges + lap     iou_distance + fuse_score, lapjv cost_limit=match_thresh (:181-186)
-//   k_stage1    [grid]          Kalman update / re_activate of matched pool rows (:188-196)
-//   k_prep23    [block/stream]  leftovers = unmatched Tracked rows (:205-209); rest = unmatched dets (:229)
-//   stage 2 & 3 edges + lap     leftovers x low dets, IoU, 0.5 (:210-211); unconfirmed x rest, fused, 0.7 (:230-233)
-//   k_stage23   [grid]          stage-2/3 updates, mark lost (:222-226) / removed (:237-240)
-//   k_finish    [block/stream]  births (:242-248), lost expiry (:250-253), joint/sub list algebra
-//                               incl. the removed_stracks quirk (:257-265)
-//   k_dedup     [grid]          remove_duplicate_stracks pairs at IoU distance < 0.15 (:312-325)
-//   k_output    [block/stream]  final lists, output rows (:270-281), free-slot list
+// Follows boxmot/trackers/bytetrack/byte_tracker.py:132-325.  One frame = 8 launches, each
+// covering all S streams ("block/stream" kernels do the order-preserving list algebra with
+// block-wide scans; "grid" kernels spread per-track work over the whole chip):
+//   k_begin   [block/stream]  frame_id++, confidence split (:149-158), STrack box conversions
+//                             (:14-25), grids over high / low detections, tracked -> activated /
+//                             unconfirmed, pool = act ++ lost (:169-178), predicted pool boxes
+//                             (mean only, :35-48), unconfirmed boxes (not predicted)
+//   edges     [grid]          stage 1: pool x high, fused IoU (:181-183)
+//   lap       [block/stream]  lapjv cost_limit = match_thresh (:184-186)
+//   k_prep23  [block/stream]  leftovers = unmatched Tracked rows (:205-209), rest = unmatched
+//                             high dets (:229)
+//   edges     [grid]          stage 2: leftovers x low dets, IoU (:210); stage 3: unconfirmed x
+//                             rest, fused IoU (:230-232)
+//   lap       [block/problem] cost_limit 0.5 (:211) and 0.7 (:233)
+//   k_apply   [grid]          Kalman predict of every pool track + update of every matched track
+//                             (stages 1-3; :188-196, :212-220, :234-236), mark lost (:222-226) /
+//                             removed (:237-240); each track's state is read and written once
+//   k_finish  [block/stream]  births (:242-248), lost expiry (:250-253), joint/sub list algebra
+//                             incl. the removed_stracks quirk (:257-265), duplicate removal
+//                             (:312-325) through a grid over the lost list, output rows (:270-281),
+//                             free-slot list
 #include <algorithm>
 #include <cstring>
 #include <new>
@@ -24,15 +31,15 @@
 namespace yta {
 namespace {
 
-constexpr int BLK = 1024;   // block/stream kernels
-constexpr int GRID_T = 256; // grid kernels
+constexpr int BLK = 1024;    // block/stream kernels
+constexpr int GRID_T = 256;  // grid kernels
 
 __device__ __forceinline__ void load_kf(const double *kf, long long slot, KfState &s) {
     const double2 *src = reinterpret_cast<const double2 *>(kf + slot * KF_REC);
 #pragma unroll
-    for (int k = 0; k < 22; ++k) {
-        double2 v = src[k];
-        double *dst = k < 4 ? s.m + 2 * k : s.p + 2 * (k - 4);
+    for (int k = 0; k < 12; ++k) {
+        const double2 v = src[k];
+        double *dst = k < 4 ? s.m + 2 * k : s.c + 2 * (k - 4);
         dst[0] = v.x;
         dst[1] = v.y;
     }
@@ -41,22 +48,29 @@ __device__ __forceinline__ void load_kf(const double *kf, long long slot, KfStat
 __device__ __forceinline__ void store_kf(double *kf, long long slot, const KfState &s) {
     double2 *dst = reinterpret_cast<double2 *>(kf + slot * KF_REC);
 #pragma unroll
-    for (int k = 0; k < 22; ++k) {
-        const double *src = k < 4 ? s.m + 2 * k : s.p + 2 * (k - 4);
+    for (int k = 0; k < 12; ++k) {
+        const double *src = k < 4 ? s.m + 2 * k : s.c + 2 * (k - 4);
         dst[k] = make_double2(src[0], src[1]);
     }
 }
 
 __device__ __forceinline__ Box kf_box(const double *kf, long long slot) {
-    const double *m = kf + slot * KF_REC;
-    return xyah_mean_to_box(m[0], m[1], m[2], m[3]);
+    const double2 *m = reinterpret_cast<const double2 *>(kf + slot * KF_REC);
+    const double2 a = m[0], b = m[1];
+    return xyah_mean_to_box(a.x, a.y, b.x, b.y);
 }
 
 __device__ __forceinline__ int st_of(int flags) { return flags & FL_STATE; }
 
+__device__ __forceinline__ GridView grid_of(const BtGrid &g, int s) {
+    return GridView{g.hdr + s, g.cell + (long long)s * (GRID_MAX_CELLS + 1), g.items + s * g.cap,
+                    g.boxes + s * g.cap, g.big + s * g.cap};
+}
+
 // ------------------------------------------------------------------------------------ k_begin
 __global__ __launch_bounds__(BLK) void k_begin(BtArgs a) {
     __shared__ int wsum[32];
+    __shared__ GridScratch gs;
     const int s = blockIdx.x, t = threadIdx.x;
     BtCounters *c = a.cnt + s;
     const long long db = (long long)s * a.MAXD, tb = (long long)s * a.CAP;
@@ -66,39 +80,59 @@ __global__ __launch_bounds__(BLK) void k_begin(BtArgs a) {
         nd = nd < 0 ? 0 : a.MAXD;
     }
     const double *din = a.det_in + (long long)a.det_off[s] * 6;
+    const double thr = a.track_thresh;
     for (int i = t; i < nd; i += BLK) {
         const double *d = din + (long long)i * 6;
         double xywh[4];
-        det_xyxy_to_xywh(d, xywh);                    // STrack.__init__ (:16-18)
-        a.det_box[db + i] = xywh_to_box(xywh);        // STrack.xyxy with mean None (:105-106)
+        det_xyxy_to_xywh(d, xywh);                       // STrack.__init__ (:16-18)
         xywh_to_xyah(xywh, a.det_xyah + (db + i) * 4);
         a.det_conf[db + i] = d[4];
         a.det_cls[db + i] = d[5];
     }
-    __syncthreads();
-    const double thr = a.track_thresh;
+    block_sync();
     const double *conf = a.det_conf + db;
-    int n_high = block_compact(nd, wsum, [&](int i) { return conf[i] > thr; },
-                               [&](int i, int pos) {
-                                   a.high[db + pos] = i;
-                                   a.high_box[db + pos] = a.det_box[db + i];
-                                   a.high_score[db + pos] = conf[i];
-                               });
-    int n_second = block_compact(nd, wsum,
-                                 [&](int i) { return conf[i] > 0.1 && conf[i] < thr; },
-                                 [&](int i, int pos) {
-                                     a.second[db + pos] = i;
-                                     a.second_box[db + pos] = a.det_box[db + i];
-                                 });
+    auto det_box = [&](int i) {                          // STrack.xyxy with mean None (:105-106)
+        const double *d = din + (long long)i * 6;
+        double xywh[4];
+        det_xyxy_to_xywh(d, xywh);
+        return xywh_to_box(xywh);
+    };
+    const int n_high = block_compact(nd, wsum, [&](int i) { return conf[i] > thr; },
+                                     [&](int i, int pos) {
+                                         a.high[db + pos] = i;
+                                         a.high_box[db + pos] = det_box(i);
+                                         a.high_score[db + pos] = conf[i];
+                                     });
+    const int n_second = block_compact(nd, wsum,
+                                       [&](int i) { return conf[i] > 0.1 && conf[i] < thr; },
+                                       [&](int i, int pos) {
+                                           a.second[db + pos] = i;
+                                           a.second_box[db + pos] = det_box(i);
+                                       });
+    block_sync();
+    grid_build(n_high, [&](int i) { return a.high_box[db + i]; }, grid_of(a.grid_high, s), gs, wsum);
+    grid_build(n_second, [&](int i) { return a.second_box[db + i]; }, grid_of(a.grid_second, s), gs,
+               wsum);
     const int n_tracked = c->n_tracked, n_lost = c->n_lost;
     const int *tracked = a.tracked + tb;
-    int n_act = block_compact(n_tracked, wsum,
-                              [&](int i) { return (a.meta[tb + tracked[i]].flags & FL_ACTIVATED) != 0; },
-                              [&](int i, int pos) { a.pool[tb + pos] = tracked[i]; });
-    int n_unc = block_compact(n_tracked, wsum,
-                              [&](int i) { return (a.meta[tb + tracked[i]].flags & FL_ACTIVATED) == 0; },
-                              [&](int i, int pos) { a.unc[tb + pos] = tracked[i]; });
+    const int n_act = block_compact(
+        n_tracked, wsum, [&](int i) { return (a.meta[tb + tracked[i]].flags & FL_ACTIVATED) != 0; },
+        [&](int i, int pos) { a.pool[tb + pos] = tracked[i]; });
+    const int n_unc = block_compact(
+        n_tracked, wsum, [&](int i) { return (a.meta[tb + tracked[i]].flags & FL_ACTIVATED) == 0; },
+        [&](int i, int pos) { a.unc[tb + pos] = tracked[i]; });
     for (int i = t; i < n_lost; i += BLK) a.pool[tb + n_act + i] = a.lost[tb + i];
+    block_sync();
+    const int n_pool = n_act + n_lost;
+    // predicted boxes of the pool (STrack.multi_predict :35-48 zeroes vh of non-tracked tracks;
+    // the box needs the predicted mean only, the covariance is advanced in k_apply)
+    for (int i = t; i < n_pool; i += BLK) {
+        const long long slot = tb + a.pool[tb + i];
+        const double *m = a.kf + slot * KF_REC;
+        const double vh = st_of(a.meta[slot].flags) == ST_TRACKED ? m[7] : 0.0;
+        a.pool_box[tb + i] = xyah_mean_to_box(m[0] + m[4], m[1] + m[5], m[2] + m[6], m[3] + vh);
+    }
+    for (int j = t; j < n_unc; j += BLK) a.unc_box[tb + j] = kf_box(a.kf, tb + a.unc[tb + j]);
     if (t == 0) {
         c->frame_id += 1;
         c->n_dets = nd;
@@ -106,68 +140,12 @@ __global__ __launch_bounds__(BLK) void k_begin(BtArgs a) {
         c->n_second = n_second;
         c->n_act = n_act;
         c->n_unc = n_unc;
-        c->n_pool = n_act + n_lost;
+        c->n_pool = n_pool;
         c->n_left = 0;
         c->n_rest = 0;
         c->n_births = 0;
         c->n_edges[0] = c->n_edges[1] = c->n_edges[2] = 0;
     }
-}
-
-// ------------------------------------------------------------------------------------ k_predict
-__global__ __launch_bounds__(GRID_T) void k_predict(BtArgs a) {
-    const int s = blockIdx.y;
-    const int i = blockIdx.x * GRID_T + threadIdx.x;
-    const BtCounters *c = a.cnt + s;
-    const int n_pool = c->n_pool, n_unc = c->n_unc;
-    const long long tb = (long long)s * a.CAP;
-    if (i < n_pool) {
-        const long long slot = tb + a.pool[tb + i];
-        KfState st;
-        load_kf(a.kf, slot, st);
-        if (st_of(a.meta[slot].flags) != ST_TRACKED) st.m[7] = 0;   // :41-42
-        kf_predict(st);
-        store_kf(a.kf, slot, st);
-        a.pool_box[tb + i] = xyah_mean_to_box(st.m[0], st.m[1], st.m[2], st.m[3]);
-    } else if (i < n_pool + n_unc) {
-        const int j = i - n_pool;
-        a.unc_box[tb + j] = kf_box(a.kf, tb + a.unc[tb + j]);   // unconfirmed: not predicted
-    }
-}
-
-__device__ __forceinline__ void take_detection(const BtArgs &a, long long slot, long long det,
-                                               int det_local, int fid) {
-    KfState st;
-    load_kf(a.kf, slot, st);
-    kf_update(st, a.det_xyah + det * 4);
-    store_kf(a.kf, slot, st);
-    TrackMeta m = a.meta[slot];
-    const bool reactivate = st_of(m.flags) != ST_TRACKED;
-    m.tracklet_len = reactivate ? 0 : m.tracklet_len + 1;
-    m.flags = (m.flags & ~FL_STATE) | ST_TRACKED | FL_ACTIVATED;
-    m.frame_id = fid;
-    m.score = a.det_conf[det];
-    m.cls = a.det_cls[det];
-    m.det_ind = det_local;
-    a.meta[slot] = m;
-}
-
-// ------------------------------------------------------------------------------------ k_stage1
-__global__ __launch_bounds__(GRID_T) void k_stage1(BtArgs a) {
-    const int s = blockIdx.y;
-    const int i = blockIdx.x * GRID_T + threadIdx.x;
-    const BtCounters *c = a.cnt + s;
-    const long long tb = (long long)s * a.CAP, db = (long long)s * a.MAXD;
-    if (i >= c->n_pool) return;
-    const int h = a.x1[tb + i];
-    int kind = 0;
-    if (h >= 0) {
-        const long long slot = tb + a.pool[tb + i];
-        kind = st_of(a.meta[slot].flags) == ST_TRACKED ? 1 : 2;   // update vs re_activate
-        const int d = a.high[db + h];
-        take_detection(a, slot, db + d, d, c->frame_id);
-    }
-    a.kind1[tb + i] = kind;
 }
 
 // ------------------------------------------------------------------------------------ k_prep23
@@ -177,61 +155,103 @@ __global__ __launch_bounds__(BLK) void k_prep23(BtArgs a) {
     BtCounters *c = a.cnt + s;
     const long long tb = (long long)s * a.CAP, db = (long long)s * a.MAXD;
     const int n_pool = c->n_pool, n_high = c->n_high;
-    int n_left = block_compact(
+    for (int i = threadIdx.x; i < n_pool; i += BLK) a.left_of_pool[tb + i] = -1;
+    for (int h = threadIdx.x; h < n_high; h += BLK) a.rest_of_high[db + h] = -1;
+    block_sync();
+    const int n_left = block_compact(
         n_pool, wsum,
         [&](int i) {
             return a.x1[tb + i] < 0 && st_of(a.meta[tb + a.pool[tb + i]].flags) == ST_TRACKED;
         },
         [&](int i, int pos) {
             a.left[tb + pos] = i;
+            a.left_of_pool[tb + i] = pos;
             a.left_box[tb + pos] = a.pool_box[tb + i];
         });
-    int n_rest = block_compact(n_high, wsum, [&](int h) { return a.y1[db + h] < 0; },
-                               [&](int h, int pos) {
-                                   a.rest[db + pos] = h;
-                                   a.rest_box[db + pos] = a.high_box[db + h];
-                                   a.rest_score[db + pos] = a.high_score[db + h];
-                               });
+    const int n_rest = block_compact(n_high, wsum, [&](int h) { return a.y1[db + h] < 0; },
+                                     [&](int h, int pos) {
+                                         a.rest[db + pos] = h;
+                                         a.rest_of_high[db + h] = pos;
+                                         a.rest_box[db + pos] = a.high_box[db + h];
+                                         a.rest_score[db + pos] = a.high_score[db + h];
+                                     });
     if (threadIdx.x == 0) {
         c->n_left = n_left;
         c->n_rest = n_rest;
     }
 }
 
-// ------------------------------------------------------------------------------------ k_stage23
-__global__ __launch_bounds__(GRID_T) void k_stage23(BtArgs a) {
+// ------------------------------------------------------------------------------------ k_apply
+__device__ __forceinline__ void take_detection(const BtArgs &a, KfState &st, TrackMeta &m,
+                                               long long det, int det_local, int fid) {
+    kf_update(st, a.det_xyah + det * 4);
+    const bool reactivate = st_of(m.flags) != ST_TRACKED;
+    m.tracklet_len = reactivate ? 0 : m.tracklet_len + 1;
+    m.flags = (m.flags & ~FL_STATE) | ST_TRACKED | FL_ACTIVATED;
+    m.frame_id = fid;
+    m.score = a.det_conf[det];
+    m.cls = a.det_cls[det];
+    m.det_ind = det_local;
+}
+
+__global__ __launch_bounds__(GRID_T) void k_apply(BtArgs a) {
     const int s = blockIdx.y;
     const int i = blockIdx.x * GRID_T + threadIdx.x;
     const BtCounters *c = a.cnt + s;
+    const int n_pool = c->n_pool, n_unc = c->n_unc, fid = c->frame_id;
     const long long tb = (long long)s * a.CAP, db = (long long)s * a.MAXD;
-    const int n_left = c->n_left, n_unc = c->n_unc, fid = c->frame_id;
-    if (i < n_left) {
-        const long long slot = tb + a.pool[tb + a.left[tb + i]];
-        const int q = a.x2[tb + i];
-        if (q >= 0) {
-            const int d = a.second[db + q];
-            take_detection(a, slot, db + d, d, fid);
-            a.kind2[tb + i] = 1;
+    if (i < n_pool) {
+        const long long slot = tb + a.pool[tb + i];
+        KfState st;
+        load_kf(a.kf, slot, st);
+        TrackMeta m = a.meta[slot];
+        const bool tracked = st_of(m.flags) == ST_TRACKED;
+        if (!tracked) st.m[7] = 0;                                   // :41-42
+        kf_predict(st);
+        int kind = 0;
+        const int h = a.x1[tb + i];
+        if (h >= 0) {                                                // stage 1 (:188-196)
+            kind = tracked ? 1 : 2;
+            const int d = a.high[db + h];
+            take_detection(a, st, m, db + d, d, fid);
         } else {
-            a.meta[slot].flags = (a.meta[slot].flags & ~FL_STATE) | ST_LOST;   // mark_lost
-            a.kind2[tb + i] = 0;
+            const int L = a.left_of_pool[tb + i];
+            if (L >= 0) {
+                const int q = a.x2[tb + L];
+                if (q >= 0) {                                        // stage 2 (:212-220)
+                    const int d = a.second[db + q];
+                    take_detection(a, st, m, db + d, d, fid);
+                } else {
+                    m.flags = (m.flags & ~FL_STATE) | ST_LOST;       // mark_lost (:222-226)
+                }
+            }
         }
-    } else if (i < n_left + n_unc) {
-        const int j = i - n_left;
+        store_kf(a.kf, slot, st);
+        a.meta[slot] = m;
+        a.kind1[tb + i] = kind;
+    } else if (i < n_pool + n_unc) {
+        const int j = i - n_pool;
         const long long slot = tb + a.unc[tb + j];
+        TrackMeta m = a.meta[slot];
         const int r = a.x3[tb + j];
-        if (r >= 0) {
+        if (r >= 0) {                                                // stage 3 (:234-236)
+            KfState st;
+            load_kf(a.kf, slot, st);
             const int d = a.high[db + a.rest[db + r]];
-            take_detection(a, slot, db + d, d, fid);
+            take_detection(a, st, m, db + d, d, fid);
+            store_kf(a.kf, slot, st);
         } else {
-            a.meta[slot].flags = (a.meta[slot].flags & ~FL_STATE) | ST_REMOVED | FL_REMOVED_NOW;
+            m.flags = (m.flags & ~FL_STATE) | ST_REMOVED | FL_REMOVED_NOW;   // :237-240
         }
+        a.meta[slot] = m;
     }
 }
 
 // ------------------------------------------------------------------------------------ k_finish
 __global__ __launch_bounds__(BLK) void k_finish(BtArgs a) {
     __shared__ int wsum[32];
+    __shared__ GridScratch gs;
+    extern __shared__ __attribute__((aligned(16))) unsigned int live[];   // CAP bits
     const int s = blockIdx.x, t = threadIdx.x;
     BtCounters *c = a.cnt + s;
     const long long tb = (long long)s * a.CAP, db = (long long)s * a.MAXD;
@@ -266,22 +286,21 @@ __global__ __launch_bounds__(BLK) void k_finish(BtArgs a) {
         m.tracklet_len = 0;
         m.pad = 0;
         a.meta[tb + slot] = m;
-        a.newslot[tb + b] = slot;
     }
     // lost-track expiry (:250-253); end_frame == frame_id
     for (int i = t; i < n_lost; i += BLK) {
         const long long slot = tb + a.lost[tb + i];
-        TrackMeta m = a.meta[slot];
+        const TrackMeta m = a.meta[slot];
         if (fid - m.frame_id > a.max_time_lost)
             a.meta[slot].flags = (m.flags & ~FL_STATE) | ST_REMOVED | FL_REMOVED_NOW;
     }
-    __syncthreads();
+    block_sync();
     // tracked' = [Tracked survivors of tracked_stracks] ++ births ++ re-found (:257-261)
     int n_t2 = block_compact(
         n_tracked, wsum,
         [&](int i) { return st_of(a.meta[tb + a.tracked[tb + i]].flags) == ST_TRACKED; },
         [&](int i, int pos) { a.t2[tb + pos] = a.tracked[tb + i]; });
-    for (int b = t; b < n_births; b += BLK) a.t2[tb + n_t2 + b] = a.newslot[tb + b];
+    for (int b = t; b < n_births; b += BLK) a.t2[tb + n_t2 + b] = a.free_list[tb + b];
     n_t2 += n_births;
     n_t2 += block_compact(n_pool, wsum, [&](int i) { return a.kind1[tb + i] == 2; },
                           [&](int i, int pos) { a.t2[tb + n_t2 + pos] = a.pool[tb + i]; });
@@ -289,22 +308,22 @@ __global__ __launch_bounds__(BLK) void k_finish(BtArgs a) {
     int n_l2 = block_compact(
         n_lost, wsum,
         [&](int i) {
-            int f = a.meta[tb + a.lost[tb + i]].flags;
+            const int f = a.meta[tb + a.lost[tb + i]].flags;
             return st_of(f) != ST_TRACKED && !(f & FL_EVER_REMOVED);
         },
         [&](int i, int pos) { a.l2[tb + pos] = a.lost[tb + i]; });
     n_l2 += block_compact(
         n_left, wsum,
         [&](int i) {
-            return a.kind2[tb + i] == 0 &&
+            return a.x2[tb + i] < 0 &&
                    !(a.meta[tb + a.pool[tb + a.left[tb + i]]].flags & FL_EVER_REMOVED);
         },
         [&](int i, int pos) { a.l2[tb + n_l2 + pos] = a.pool[tb + a.left[tb + i]]; });
-    __syncthreads();
+    block_sync();
     // this frame's removals join removed_stracks only now (:265)
     for (int i = t; i < n_lost; i += BLK) {
         const long long slot = tb + a.lost[tb + i];
-        int f = a.meta[slot].flags;
+        const int f = a.meta[slot].flags;
         if (f & FL_REMOVED_NOW) a.meta[slot].flags = (f & ~FL_REMOVED_NOW) | FL_EVER_REMOVED;
     }
     for (int p = t; p < n_t2; p += BLK) {
@@ -319,96 +338,66 @@ __global__ __launch_bounds__(BLK) void k_finish(BtArgs a) {
         a.lage[tb + q] = a.meta[slot].frame_id - a.meta[slot].start_frame;
         a.dropB[tb + q] = 0;
     }
-    if (t == 0) {
-        c->n_births = n_births;
-        c->next_id = next_id + n_births;
-        c->n_t2 = n_t2;
-        c->n_l2 = n_l2;
-    }
-}
-
-// ------------------------------------------------------------------------------------ k_dedup
-// remove_duplicate_stracks: every pair decides independently (set semantics), so the pairs can
-// be visited in any order.
-constexpr int DEDUP_ROWS_PER_WAVE = 4;
-constexpr int DEDUP_ROWS_PER_BLOCK = (GRID_T / WAVE) * DEDUP_ROWS_PER_WAVE;
-
-__global__ __launch_bounds__(GRID_T) void k_dedup(BtArgs a) {
-    const int s = blockIdx.y;
-    const BtCounters *c = a.cnt + s;
-    const int n_t2 = c->n_t2, n_l2 = c->n_l2;
-    const long long tb = (long long)s * a.CAP;
-    const int lane = lane_id(), wave = threadIdx.x / WAVE;
-    const int p0 = blockIdx.x * DEDUP_ROWS_PER_BLOCK + wave * DEDUP_ROWS_PER_WAVE;
-    if (p0 >= n_t2 || n_l2 == 0) return;
-    Box pb[DEDUP_ROWS_PER_WAVE];
-    int pa[DEDUP_ROWS_PER_WAVE];
-#pragma unroll
-    for (int r = 0; r < DEDUP_ROWS_PER_WAVE; ++r) {
-        int p = p0 + r < n_t2 ? p0 + r : p0;
-        pb[r] = a.tbox[tb + p];
-        pa[r] = a.tage[tb + p];
-    }
-    for (int q = lane; q < n_l2; q += WAVE) {
-        const Box lb = a.lbox[tb + q];
-        const int la = a.lage[tb + q];
-#pragma unroll
-        for (int r = 0; r < DEDUP_ROWS_PER_WAVE; ++r) {
-            if (p0 + r >= n_t2) continue;
-            if (!intersects(pb[r], lb)) continue;
-            if (1 - iou(pb[r], lb) < 0.15) {
-                if (pa[r] > la) a.dropB[tb + q] = 1;
-                else a.dropA[tb + p0 + r] = 1;
-            }
+    block_sync();
+    // remove_duplicate_stracks (:312-325): set semantics, so pairs are visited in any order
+    if (n_t2 > 0 && n_l2 > 0) {
+        const GridView gv = grid_of(a.grid_lost, s);
+        grid_build(n_l2, [&](int q) { return a.lbox[tb + q]; }, gv, gs, wsum);
+        const GridHdr gh = gs.hdr;
+        for (int p = t; p < n_t2; p += BLK) {
+            const Box tbx = a.tbox[tb + p];
+            const int ta = a.tage[tb + p];
+            auto pair = [&](int q, const Box &lb) {
+                if (!intersects(tbx, lb)) return;
+                if (1 - iou(tbx, lb) < 0.15) {
+                    if (ta > a.lage[tb + q]) a.dropB[tb + q] = 1;
+                    else a.dropA[tb + p] = 1;
+                }
+            };
+            grid_query(gv, gh, tbx, pair, [&](int q) { pair(q, a.lbox[tb + q]); });
         }
     }
-}
-
-// ------------------------------------------------------------------------------------ k_output
-__global__ __launch_bounds__(BLK) void k_output(BtArgs a) {
-    __shared__ int wsum[32];
-    extern __shared__ __attribute__((aligned(16))) unsigned int live[];   // CAP bits
-    const int s = blockIdx.x, t = threadIdx.x;
-    BtCounters *c = a.cnt + s;
-    const long long tb = (long long)s * a.CAP;
-    const int n_t2 = c->n_t2, n_l2 = c->n_l2;
+    // final lists, output rows, free slots
     const int words = (a.CAP + 31) / 32;
-    for (int w = t; w < words; w += BLK) live[w] = 0u;
-    __syncthreads();
-    int n_tr = block_compact(n_t2, wsum, [&](int p) { return a.dropA[tb + p] == 0; },
-                             [&](int p, int pos) {
-                                 int slot = a.t2[tb + p];
-                                 a.tracked[tb + pos] = slot;
-                                 atomicOr(&live[slot >> 5], 1u << (slot & 31));
-                             });
-    int n_lo = block_compact(n_l2, wsum, [&](int q) { return a.dropB[tb + q] == 0; },
-                             [&](int q, int pos) {
-                                 int slot = a.l2[tb + q];
-                                 a.lost[tb + pos] = slot;
-                                 atomicOr(&live[slot >> 5], 1u << (slot & 31));
-                             });
-    __syncthreads();
+    for (int wd = t; wd < words; wd += BLK) live[wd] = 0u;
+    block_sync();
+    const int n_tr = block_compact(n_t2, wsum, [&](int p) { return a.dropA[tb + p] == 0; },
+                                   [&](int p, int pos) {
+                                       const int slot = a.t2[tb + p];
+                                       a.tracked[tb + pos] = slot;
+                                       atomicOr(&live[slot >> 5], 1u << (slot & 31));
+                                   });
+    const int n_lo = block_compact(n_l2, wsum, [&](int q) { return a.dropB[tb + q] == 0; },
+                                   [&](int q, int pos) {
+                                       const int slot = a.l2[tb + q];
+                                       a.lost[tb + pos] = slot;
+                                       atomicOr(&live[slot >> 5], 1u << (slot & 31));
+                                   });
+    block_sync();
     double *out = a.out + tb * 8;
-    int n_out = block_compact(
+    const int n_out = block_compact(
         n_tr, wsum, [&](int i) { return (a.meta[tb + a.tracked[tb + i]].flags & FL_ACTIVATED) != 0; },
         [&](int i, int pos) {
             const long long slot = tb + a.tracked[tb + i];
             const Box b = kf_box(a.kf, slot);
             const TrackMeta m = a.meta[slot];
-            double *o = out + (long long)pos * 8;
-            o[0] = b.x1; o[1] = b.y1; o[2] = b.x2; o[3] = b.y2;
-            o[4] = (double)m.id;
-            o[5] = m.score;
-            o[6] = m.cls;
-            o[7] = (double)m.det_ind;
+            double2 *o = reinterpret_cast<double2 *>(out + (long long)pos * 8);
+            o[0] = make_double2(b.x1, b.y1);
+            o[1] = make_double2(b.x2, b.y2);
+            o[2] = make_double2((double)m.id, m.score);
+            o[3] = make_double2(m.cls, (double)m.det_ind);
         });
-    int n_free = block_compact(a.CAP, wsum,
-                               [&](int slot) { return !((live[slot >> 5] >> (slot & 31)) & 1u); },
-                               [&](int slot, int pos) { a.free_list[tb + pos] = slot; });
+    const int n_fr = block_compact(a.CAP, wsum,
+                                   [&](int slot) { return !((live[slot >> 5] >> (slot & 31)) & 1u); },
+                                   [&](int slot, int pos) { a.free_list[tb + pos] = slot; });
     if (t == 0) {
+        c->n_births = n_births;
+        c->next_id = next_id + n_births;
+        c->n_t2 = n_t2;
+        c->n_l2 = n_l2;
         c->n_tracked = n_tr;
         c->n_lost = n_lo;
-        c->n_free = n_free;
+        c->n_free = n_fr;
         c->n_out = n_out;
         if (a.out_counts) a.out_counts[s] = n_out;
     }
@@ -423,19 +412,19 @@ __global__ __launch_bounds__(BLK) void k_rebuild_free(BtArgs a) {
     const long long tb = (long long)s * a.CAP;
     const int words = (a.CAP + 31) / 32;
     for (int w = t; w < words; w += BLK) live[w] = 0u;
-    __syncthreads();
+    block_sync();
     for (int i = t; i < c->n_tracked; i += BLK) {
-        int slot = a.tracked[tb + i];
+        const int slot = a.tracked[tb + i];
         atomicOr(&live[slot >> 5], 1u << (slot & 31));
     }
     for (int i = t; i < c->n_lost; i += BLK) {
-        int slot = a.lost[tb + i];
+        const int slot = a.lost[tb + i];
         atomicOr(&live[slot >> 5], 1u << (slot & 31));
     }
-    __syncthreads();
-    int n_free = block_compact(a.CAP, wsum,
-                               [&](int slot) { return !((live[slot >> 5] >> (slot & 31)) & 1u); },
-                               [&](int slot, int pos) { a.free_list[tb + pos] = slot; });
+    block_sync();
+    const int n_free = block_compact(a.CAP, wsum,
+                                     [&](int slot) { return !((live[slot >> 5] >> (slot & 31)) & 1u); },
+                                     [&](int slot, int pos) { a.free_list[tb + pos] = slot; });
     if (t == 0) c->n_free = n_free;
 }
 
@@ -464,15 +453,13 @@ struct yta_bytetrack {
     hipStream_t stream = nullptr;
     std::vector<void *> allocs;
     BtArgs a{};
-    // association buffers: stage 1 and 2 share pool A, stage 3 uses pool B
+    // association buffers: stages 1 and 2 share pool A, stage 3 uses pool B
     Edge *edgesA = nullptr, *edgesB = nullptr;
     int *wsA = nullptr, *wsB = nullptr;
     double *wsdA = nullptr, *wsdB = nullptr;
     long long ws_i = 0, ws_d = 0;
-    int *err_dummy = nullptr;
     // host staging
     double *h_dets = nullptr;
-    long long h_dets_cap = 0;
     int *h_off = nullptr;
     BtCounters *h_cnt = nullptr;
     double *d_det_in = nullptr;
@@ -486,13 +473,16 @@ struct yta_bytetrack {
 
 namespace {
 
+constexpr int BT_PHASES = 8;   // launches per frame, see yta_bytetrack_profile_collect
+
 template <typename T>
 int dalloc(yta_bytetrack *e, T **p, long long n) {
     void *q = nullptr;
     if (n <= 0) n = 1;
     hipError_t err = hipMalloc(&q, sizeof(T) * (size_t)n);
     if (err != hipSuccess) {
-        set_error("hipMalloc(%lld bytes) failed: %s", (long long)(sizeof(T) * n), hipGetErrorString(err));
+        set_error("hipMalloc(%lld bytes) failed: %s", (long long)(sizeof(T) * n),
+                  hipGetErrorString(err));
         return YTA_ERR_NOMEM;
     }
     e->allocs.push_back(q);
@@ -500,11 +490,21 @@ int dalloc(yta_bytetrack *e, T **p, long long n) {
     return YTA_OK;
 }
 
-#define DALLOC(ptr, n)                          \
-    do {                                        \
-        int _rc = dalloc(e, &(ptr), (n));       \
-        if (_rc) return _rc;                    \
+#define DALLOC(ptr, n)                    \
+    do {                                  \
+        int _rc = dalloc(e, &(ptr), (n)); \
+        if (_rc) return _rc;              \
     } while (0)
+
+int grid_alloc(yta_bytetrack *e, BtGrid &g, long long cap) {
+    g.cap = cap;
+    DALLOC(g.hdr, e->S);
+    DALLOC(g.cell, (long long)e->S * (GRID_MAX_CELLS + 1));
+    DALLOC(g.items, e->S * cap);
+    DALLOC(g.boxes, e->S * cap);
+    DALLOC(g.big, e->S * cap);
+    return YTA_OK;
+}
 
 int bt_alloc(yta_bytetrack *e) {
     const long long S = e->S, CAP = e->CAP, MAXD = e->MAXD;
@@ -514,7 +514,7 @@ int bt_alloc(yta_bytetrack *e) {
     a.MAXD = e->MAXD;
     a.track_thresh = e->prm.track_thresh;
     a.match_thresh = e->prm.match_thresh;
-    a.det_thresh = e->prm.track_thresh;
+    a.det_thresh = e->prm.track_thresh;                                        // :127
     a.max_time_lost = (int)(e->prm.frame_rate / 30.0 * e->prm.track_buffer);   // :128-129
     DALLOC(a.kf, S * CAP * KF_REC);
     DALLOC(a.meta, S * CAP);
@@ -522,7 +522,6 @@ int bt_alloc(yta_bytetrack *e) {
     DALLOC(a.lost, S * CAP);
     DALLOC(a.free_list, S * CAP);
     DALLOC(a.cnt, S);
-    DALLOC(a.det_box, S * MAXD);
     DALLOC(a.det_xyah, S * MAXD * 4);
     DALLOC(a.det_conf, S * MAXD);
     DALLOC(a.det_cls, S * MAXD);
@@ -530,21 +529,25 @@ int bt_alloc(yta_bytetrack *e) {
     DALLOC(a.second, S * MAXD);
     DALLOC(a.rest, S * MAXD);
     DALLOC(a.birth, S * MAXD);
+    DALLOC(a.rest_of_high, S * MAXD);
     DALLOC(a.high_box, S * MAXD);
     DALLOC(a.second_box, S * MAXD);
     DALLOC(a.rest_box, S * MAXD);
     DALLOC(a.high_score, S * MAXD);
     DALLOC(a.rest_score, S * MAXD);
+    int rc = grid_alloc(e, a.grid_high, MAXD);
+    if (!rc) rc = grid_alloc(e, a.grid_second, MAXD);
+    if (!rc) rc = grid_alloc(e, a.grid_lost, CAP);
+    if (rc) return rc;
     DALLOC(a.pool, S * CAP);
     DALLOC(a.unc, S * CAP);
     DALLOC(a.left, S * CAP);
+    DALLOC(a.left_of_pool, S * CAP);
     DALLOC(a.t2, S * CAP);
     DALLOC(a.l2, S * CAP);
     DALLOC(a.kind1, S * CAP);
-    DALLOC(a.kind2, S * CAP);
     DALLOC(a.dropA, S * CAP);
     DALLOC(a.dropB, S * CAP);
-    DALLOC(a.newslot, S * CAP);
     DALLOC(a.pool_box, S * CAP);
     DALLOC(a.unc_box, S * CAP);
     DALLOC(a.left_box, S * CAP);
@@ -559,7 +562,7 @@ int bt_alloc(yta_bytetrack *e) {
     DALLOC(a.y2, S * MAXD);
     DALLOC(a.y3, S * MAXD);
     DALLOC(a.out, S * CAP * 8);
-    // association: worst-case edge pools (every pair a candidate) so no frame can overflow
+    // association: worst-case edge pools (every pair a candidate), so no frame can overflow
     e->edge_cap = CAP * MAXD;
     e->ws_i = lap_ws_ints((int)CAP, (int)MAXD, e->edge_cap);
     e->ws_d = lap_ws_doubles((int)CAP, (int)MAXD, e->edge_cap);
@@ -575,8 +578,6 @@ int bt_alloc(yta_bytetrack *e) {
     return YTA_OK;
 }
 
-constexpr int BT_PHASES = 14;   // see yta_bytetrack_profile_collect
-
 int mark(yta_bytetrack *e) {
     if (!e->prof) return YTA_OK;
     if (e->ev_used == e->ev.size()) {
@@ -588,16 +589,16 @@ int mark(yta_bytetrack *e) {
     return YTA_OK;
 }
 
-#define MARK()                      \
-    do {                            \
-        int _m = mark(e);           \
-        if (_m) return _m;          \
+#define MARK()             \
+    do {                   \
+        int _m = mark(e);  \
+        if (_m) return _m; \
     } while (0)
 
-// One association stage over all S streams: edges + exact sparse solve -> x (rows), y (cols).
-int run_stage(yta_bytetrack *e, int stage, const Box *rows, const int *n_rows_field,
-              const Box *cols, const double *col_score, const int *n_cols_field, double thresh,
-              Edge *edges, int *ws, double *wsd, int *x, int *y) {
+ProblemSet make_problem(yta_bytetrack *e, int stage, const Box *rows, const int *n_rows_field,
+                        const Box *cols, const double *col_score, const int *n_cols_field,
+                        const BtGrid *grid, const int *remap, double thresh, Edge *edges, int *ws,
+                        double *wsd, int *x, int *y) {
     BtArgs &a = e->a;
     const int cstride = (int)(sizeof(BtCounters) / sizeof(int));
     ProblemSet ps{};
@@ -611,6 +612,17 @@ int run_stage(yta_bytetrack *e, int stage, const Box *rows, const int *n_rows_fi
     ps.score_stride = a.MAXD;
     ps.n_cols = n_cols_field;
     ps.n_cols_stride = cstride;
+    if (grid) {
+        ps.ghdr = grid->hdr;
+        ps.gcell = grid->cell;
+        ps.gcell_stride = GRID_MAX_CELLS + 1;
+        ps.gitems = grid->items;
+        ps.gboxes = grid->boxes;
+        ps.gbig = grid->big;
+        ps.gitems_stride = grid->cap;
+    }
+    ps.remap = remap;
+    ps.remap_stride = a.MAXD;
     ps.thresh = thresh;
     ps.edges = edges;
     ps.edges_stride = e->edge_cap;
@@ -629,11 +641,7 @@ int run_stage(yta_bytetrack *e, int stage, const Box *rows, const int *n_rows_fi
     ps.x_stride = a.CAP;
     ps.y = y;
     ps.y_stride = a.MAXD;
-    MARK();
-    YTA_HIP(launch_edges(ps, a.S, a.CAP, e->stream));
-    MARK();
-    YTA_HIP(launch_lap(ps, a.S, e->stream));
-    return YTA_OK;
+    return ps;
 }
 
 int launch_pipeline(yta_bytetrack *e, const double *det_in, const int *det_off, double *out,
@@ -643,42 +651,37 @@ int launch_pipeline(yta_bytetrack *e, const double *det_in, const int *det_off, 
     a.det_off = det_off;
     a.out = out;
     a.out_counts = out_counts;
-    const dim3 gt((a.CAP + GRID_T - 1) / GRID_T, a.S);
     BtCounters *c0 = a.cnt;
+    const ProblemSet s1 = make_problem(e, 0, a.pool_box, &c0->n_pool, a.high_box, a.high_score,
+                                       &c0->n_high, &a.grid_high, nullptr, a.match_thresh,
+                                       e->edgesA, e->wsA, e->wsdA, a.x1, a.y1);
+    const ProblemSet s2 = make_problem(e, 1, a.left_box, &c0->n_left, a.second_box, nullptr,
+                                       &c0->n_second, &a.grid_second, nullptr, 0.5, e->edgesA,
+                                       e->wsA, e->wsdA, a.x2, a.y2);
+    const ProblemSet s3 = make_problem(e, 2, a.unc_box, &c0->n_unc, a.rest_box, a.rest_score,
+                                       &c0->n_rest, &a.grid_high, a.rest_of_high, 0.7, e->edgesB,
+                                       e->wsB, e->wsdB, a.x3, a.y3);
     MARK();
     hipLaunchKernelGGL(k_begin, dim3(a.S), dim3(BLK), 0, e->stream, a);
     YTA_HIP(hipGetLastError());
     MARK();
-    hipLaunchKernelGGL(k_predict, gt, dim3(GRID_T), 0, e->stream, a);
-    YTA_HIP(hipGetLastError());
-    int rc = run_stage(e, 0, a.pool_box, &c0->n_pool, a.high_box, a.high_score, &c0->n_high,
-                       a.match_thresh, e->edgesA, e->wsA, e->wsdA, a.x1, a.y1);
-    if (rc) return rc;
+    YTA_HIP(launch_edges(s1, a.S, nullptr, 0, a.CAP, e->stream));
     MARK();
-    hipLaunchKernelGGL(k_stage1, gt, dim3(GRID_T), 0, e->stream, a);
-    YTA_HIP(hipGetLastError());
+    YTA_HIP(launch_lap(s1, a.S, nullptr, 0, e->stream));
     MARK();
     hipLaunchKernelGGL(k_prep23, dim3(a.S), dim3(BLK), 0, e->stream, a);
     YTA_HIP(hipGetLastError());
-    rc = run_stage(e, 1, a.left_box, &c0->n_left, a.second_box, nullptr, &c0->n_second, 0.5,
-                   e->edgesA, e->wsA, e->wsdA, a.x2, a.y2);
-    if (rc) return rc;
-    rc = run_stage(e, 2, a.unc_box, &c0->n_unc, a.rest_box, a.rest_score, &c0->n_rest, 0.7,
-                   e->edgesB, e->wsB, e->wsdB, a.x3, a.y3);
-    if (rc) return rc;
     MARK();
-    hipLaunchKernelGGL(k_stage23, gt, dim3(GRID_T), 0, e->stream, a);
-    YTA_HIP(hipGetLastError());
+    YTA_HIP(launch_edges(s2, a.S, &s3, a.S, a.CAP, e->stream));
     MARK();
-    hipLaunchKernelGGL(k_finish, dim3(a.S), dim3(BLK), 0, e->stream, a);
-    YTA_HIP(hipGetLastError());
+    YTA_HIP(launch_lap(s2, a.S, &s3, a.S, e->stream));
     MARK();
-    const dim3 gd((a.CAP + DEDUP_ROWS_PER_BLOCK - 1) / DEDUP_ROWS_PER_BLOCK, a.S);
-    hipLaunchKernelGGL(k_dedup, gd, dim3(GRID_T), 0, e->stream, a);
+    const dim3 gt((a.CAP + GRID_T - 1) / GRID_T, a.S);
+    hipLaunchKernelGGL(k_apply, gt, dim3(GRID_T), 0, e->stream, a);
     YTA_HIP(hipGetLastError());
     MARK();
     const size_t live_bytes = sizeof(unsigned int) * ((a.CAP + 31) / 32);
-    hipLaunchKernelGGL(k_output, dim3(a.S), dim3(BLK), live_bytes, e->stream, a);
+    hipLaunchKernelGGL(k_finish, dim3(a.S), dim3(BLK), live_bytes, e->stream, a);
     YTA_HIP(hipGetLastError());
     MARK();
     return YTA_OK;
@@ -723,14 +726,20 @@ int reserve(yta_bytetrack *e, int cap, int maxd) {
     if (!rc) {
         hipError_t he = hipMemcpyAsync(n->a.cnt, e->a.cnt, sizeof(BtCounters) * S,
                                        hipMemcpyDeviceToDevice, e->stream);
-        if (he != hipSuccess) { set_error("reserve copy: %s", hipGetErrorString(he)); rc = YTA_ERR_HIP; }
+        if (he != hipSuccess) {
+            set_error("reserve copy: %s", hipGetErrorString(he));
+            rc = YTA_ERR_HIP;
+        }
     }
     if (!rc) {
         const size_t live_bytes = sizeof(unsigned int) * ((nc + 31) / 32);
         hipLaunchKernelGGL(k_rebuild_free, dim3(e->S), dim3(BLK), live_bytes, e->stream, n->a);
         hipError_t he = hipGetLastError();
         if (he == hipSuccess) he = hipStreamSynchronize(e->stream);
-        if (he != hipSuccess) { set_error("reserve: %s", hipGetErrorString(he)); rc = YTA_ERR_HIP; }
+        if (he != hipSuccess) {
+            set_error("reserve: %s", hipGetErrorString(he));
+            rc = YTA_ERR_HIP;
+        }
     }
     if (rc) {
         n->stream = nullptr;
@@ -745,20 +754,27 @@ int reserve(yta_bytetrack *e, int cap, int maxd) {
     e->edge_cap = n->edge_cap;
     e->allocs.swap(n->allocs);
     e->a = n->a;
-    e->edgesA = n->edgesA; e->edgesB = n->edgesB;
-    e->wsA = n->wsA; e->wsB = n->wsB;
-    e->wsdA = n->wsdA; e->wsdB = n->wsdB;
-    e->ws_i = n->ws_i; e->ws_d = n->ws_d;
-    e->h_off = n->h_off; e->h_cnt = n->h_cnt;
+    e->edgesA = n->edgesA;
+    e->edgesB = n->edgesB;
+    e->wsA = n->wsA;
+    e->wsB = n->wsB;
+    e->wsdA = n->wsdA;
+    e->wsdB = n->wsdB;
+    e->ws_i = n->ws_i;
+    e->ws_d = n->ws_d;
+    e->h_off = n->h_off;
+    e->h_cnt = n->h_cnt;
     e->d_det_off = n->d_det_off;
-    n->h_off = nullptr; n->h_cnt = nullptr; n->stream = nullptr;
+    n->h_off = nullptr;
+    n->h_cnt = nullptr;
+    n->stream = nullptr;
     delete n;
     return YTA_OK;
 }
 
 int check_errors(yta_bytetrack *e) {
     for (int s = 0; s < e->S; ++s) {
-        int err = e->h_cnt[s].err;
+        const int err = e->h_cnt[s].err;
         if (err) {
             set_error("stream %d: device error flags 0x%x (%s%s%s%s)", s, err,
                       err & ERR_EDGE_OVERFLOW ? "edge pool overflow " : "",
@@ -766,7 +782,8 @@ int check_errors(yta_bytetrack *e) {
                       err & ERR_TRACK_CAPACITY ? "track capacity exceeded " : "",
                       err & ERR_DET_CAPACITY ? "too many detections " : "");
             return (err & (ERR_TRACK_CAPACITY | ERR_DET_CAPACITY | ERR_EDGE_OVERFLOW))
-                       ? YTA_ERR_CAPACITY : YTA_ERR_HIP;
+                       ? YTA_ERR_CAPACITY
+                       : YTA_ERR_HIP;
         }
     }
     return YTA_OK;
@@ -840,6 +857,19 @@ int yta_bytetrack_reset(yta_bytetrack *e) {
     return YTA_OK;
 }
 
+int yta_bytetrack_reserve(yta_bytetrack *e, int track_capacity, int max_dets) {
+    YTA_CHECK(e, YTA_ERR_INVALID, "null engine");
+    YTA_HIP(hipSetDevice(e->device));
+    return reserve(e, track_capacity, max_dets);
+}
+
+int yta_bytetrack_capacity(yta_bytetrack *e, int *track_capacity, int *max_dets) {
+    YTA_CHECK(e && track_capacity && max_dets, YTA_ERR_INVALID, "null argument");
+    *track_capacity = e->CAP;
+    *max_dets = e->MAXD;
+    return YTA_OK;
+}
+
 int yta_bytetrack_update(yta_bytetrack *e, const double *dets, const int *det_offsets,
                          long long *next_id, double *out, int out_capacity, int *out_offsets) {
     YTA_CHECK(e && det_offsets && out_offsets, YTA_ERR_INVALID, "null argument");
@@ -854,8 +884,8 @@ int yta_bytetrack_update(yta_bytetrack *e, const double *dets, const int *det_of
         need_c = std::max(need_c, e->h_cnt[s].n_tracked + e->h_cnt[s].n_lost + m);
     }
     if (need_d > e->MAXD || need_c > e->CAP) {   // grow geometrically, keeping all state
-        int rc = reserve(e, need_c > e->CAP ? std::max(need_c, 2 * e->CAP) : e->CAP,
-                         need_d > e->MAXD ? std::max(need_d, 2 * e->MAXD) : e->MAXD);
+        const int rc = reserve(e, need_c > e->CAP ? std::max(need_c, 2 * e->CAP) : e->CAP,
+                               need_d > e->MAXD ? std::max(need_d, 2 * e->MAXD) : e->MAXD);
         if (rc) return rc;
     }
     const long long total = det_offsets[S];
@@ -865,7 +895,8 @@ int yta_bytetrack_update(yta_bytetrack *e, const double *dets, const int *det_of
         if (e->h_dets) (void)hipHostFree(e->h_dets);
         e->d_det_in = nullptr;
         e->h_dets = nullptr;
-        long long cap = std::max<long long>(total, 1024);
+        e->d_det_cap = 0;
+        const long long cap = std::max<long long>(2 * total, 1024);
         YTA_HIP(hipMalloc((void **)&e->d_det_in, sizeof(double) * 6 * cap));
         YTA_HIP(hipHostMalloc((void **)&e->h_dets, sizeof(double) * 6 * cap, hipHostMallocDefault));
         e->d_det_cap = cap;
@@ -920,7 +951,7 @@ int yta_bytetrack_update_device(yta_bytetrack *e, const double *d_dets, const in
 
 int yta_bytetrack_sync(yta_bytetrack *e) {
     YTA_CHECK(e, YTA_ERR_INVALID, "null engine");
-    int rc = read_counters(e);
+    const int rc = read_counters(e);
     if (rc) return rc;
     return check_errors(e);
 }
@@ -930,7 +961,7 @@ int yta_bytetrack_get_state(yta_bytetrack *e, int stream, int *n_tracks, long lo
     YTA_CHECK(e && n_tracks && ints && mean && cov, YTA_ERR_INVALID, "null argument");
     YTA_CHECK(stream >= 0 && stream < e->S, YTA_ERR_INVALID, "bad stream %d", stream);
     YTA_HIP(hipSetDevice(e->device));
-    int rc = read_counters(e);
+    const int rc = read_counters(e);
     if (rc) return rc;
     const BtCounters c = e->h_cnt[stream];
     const long long tb = (long long)stream * e->CAP;
@@ -938,11 +969,14 @@ int yta_bytetrack_get_state(yta_bytetrack *e, int stream, int *n_tracks, long lo
     std::vector<double> kf((size_t)e->CAP * KF_REC);
     std::vector<TrackMeta> meta(e->CAP);
     if (c.n_tracked)
-        YTA_HIP(hipMemcpy(tr.data(), e->a.tracked + tb, sizeof(int) * c.n_tracked, hipMemcpyDeviceToHost));
+        YTA_HIP(hipMemcpy(tr.data(), e->a.tracked + tb, sizeof(int) * c.n_tracked,
+                          hipMemcpyDeviceToHost));
     if (c.n_lost)
         YTA_HIP(hipMemcpy(lo.data(), e->a.lost + tb, sizeof(int) * c.n_lost, hipMemcpyDeviceToHost));
-    YTA_HIP(hipMemcpy(kf.data(), e->a.kf + tb * KF_REC, sizeof(double) * KF_REC * e->CAP, hipMemcpyDeviceToHost));
-    YTA_HIP(hipMemcpy(meta.data(), e->a.meta + tb, sizeof(TrackMeta) * e->CAP, hipMemcpyDeviceToHost));
+    YTA_HIP(hipMemcpy(kf.data(), e->a.kf + tb * KF_REC, sizeof(double) * KF_REC * e->CAP,
+                      hipMemcpyDeviceToHost));
+    YTA_HIP(hipMemcpy(meta.data(), e->a.meta + tb, sizeof(TrackMeta) * e->CAP,
+                      hipMemcpyDeviceToHost));
     int n = 0;
     for (int which = 0; which < 2; ++which) {
         const std::vector<int> &lst = which ? lo : tr;
@@ -956,27 +990,15 @@ int yta_bytetrack_get_state(yta_bytetrack *e, int stream, int *n_tracks, long lo
             ii[4] = m.frame_id;
             ii[5] = m.start_frame;
             ii[6] = m.tracklet_len;
-            const double *r = kf.data() + (size_t)slot * KF_REC;
-            for (int k = 0; k < 8; ++k) mean[(long long)n * 8 + k] = r[k];
-            for (int i = 0; i < 8; ++i)
-                for (int j = 0; j < 8; ++j) cov[(long long)n * 64 + i * 8 + j] = r[8 + pidx(i, j)];
+            KfState st;
+            memcpy(st.m, kf.data() + (size_t)slot * KF_REC, sizeof(double) * 8);
+            memcpy(st.c, kf.data() + (size_t)slot * KF_REC + 8, sizeof(double) * 16);
+            for (int k = 0; k < 8; ++k) mean[(long long)n * 8 + k] = st.m[k];
+            kf_cov_full(st, cov + (long long)n * 64);
             ++n;
         }
     }
     *n_tracks = n;
-    return YTA_OK;
-}
-
-int yta_bytetrack_reserve(yta_bytetrack *e, int track_capacity, int max_dets) {
-    YTA_CHECK(e, YTA_ERR_INVALID, "null engine");
-    YTA_HIP(hipSetDevice(e->device));
-    return reserve(e, track_capacity, max_dets);
-}
-
-int yta_bytetrack_capacity(yta_bytetrack *e, int *track_capacity, int *max_dets) {
-    YTA_CHECK(e && track_capacity && max_dets, YTA_ERR_INVALID, "null argument");
-    *track_capacity = e->CAP;
-    *max_dets = e->MAXD;
     return YTA_OK;
 }
 
@@ -988,9 +1010,9 @@ int yta_bytetrack_profile(yta_bytetrack *e, int enable) {
     return YTA_OK;
 }
 
-// Per-kernel time summed over the frames run since profiling was enabled / last collected:
-// ms[k] for the 14 launches of one frame in order (begin, predict, edges1, lap1, stage1, prep23,
-// edges2, lap2, edges3, lap3, stage23, finish, dedup, output); *frames = frames covered.
+// Per-launch time summed over the frames run since profiling was enabled / last collected:
+// ms[k] for the 8 launches of one frame in order (begin, edges1, lap1, prep23, edges23, lap23,
+// apply, finish); *frames = frames covered.
 int yta_bytetrack_profile_collect(yta_bytetrack *e, double *ms, int *frames) {
     YTA_CHECK(e && ms && frames, YTA_ERR_INVALID, "null argument");
     YTA_HIP(hipStreamSynchronize(e->stream));
@@ -1004,6 +1026,42 @@ int yta_bytetrack_profile_collect(yta_bytetrack *e, double *ms, int *frames) {
             ms[k] += t;
         }
     e->ev_used = 0;
+    return YTA_OK;
+}
+
+int yta_bytetrack_debug_dedup(yta_bytetrack *e, int stream, int *n_t2, int *n_l2, double *tbox,
+                              double *lbox, int *ages, int *drops) {
+    YTA_CHECK(e && n_t2 && n_l2 && tbox && lbox && ages && drops, YTA_ERR_INVALID, "null argument");
+    YTA_HIP(hipSetDevice(e->device));
+    const int rc = read_counters(e);
+    if (rc) return rc;
+    const BtCounters c = e->h_cnt[stream];
+    const long long tb = (long long)stream * e->CAP;
+    *n_t2 = c.n_t2;
+    *n_l2 = c.n_l2;
+    YTA_HIP(hipMemcpy(tbox, e->a.tbox + tb, sizeof(Box) * c.n_t2, hipMemcpyDeviceToHost));
+    YTA_HIP(hipMemcpy(lbox, e->a.lbox + tb, sizeof(Box) * c.n_l2, hipMemcpyDeviceToHost));
+    YTA_HIP(hipMemcpy(ages, e->a.tage + tb, sizeof(int) * c.n_t2, hipMemcpyDeviceToHost));
+    YTA_HIP(hipMemcpy(ages + c.n_t2, e->a.lage + tb, sizeof(int) * c.n_l2, hipMemcpyDeviceToHost));
+    YTA_HIP(hipMemcpy(drops, e->a.dropA + tb, sizeof(int) * c.n_t2, hipMemcpyDeviceToHost));
+    YTA_HIP(hipMemcpy(drops + c.n_t2, e->a.dropB + tb, sizeof(int) * c.n_l2, hipMemcpyDeviceToHost));
+    return YTA_OK;
+}
+
+int yta_bytetrack_stats(yta_bytetrack *e, long long *stats) {
+    YTA_CHECK(e && stats, YTA_ERR_INVALID, "null argument");
+    YTA_HIP(hipSetDevice(e->device));
+    const int rc = read_counters(e);
+    if (rc) return rc;
+    for (int k = 0; k < 16; ++k) stats[k] = 0;
+    for (int s = 0; s < e->S; ++s) {
+        const BtCounters &c = e->h_cnt[s];
+        const long long v[16] = {c.n_dets, c.n_high, c.n_second, c.n_pool, c.n_act, c.n_unc,
+                                 c.n_left, c.n_rest, c.n_births, c.n_t2, c.n_l2, c.n_tracked,
+                                 c.n_lost, c.n_out, (long long)c.n_edges[0],
+                                 (long long)c.n_edges[1] + c.n_edges[2]};
+        for (int k = 0; k < 16; ++k) stats[k] += v[k];
+    }
     return YTA_OK;
 }
 

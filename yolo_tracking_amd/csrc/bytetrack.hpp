@@ -12,8 +12,6 @@ constexpr int FL_ACTIVATED = 4;      // STrack.is_activated
 constexpr int FL_EVER_REMOVED = 8;   // track_id is in BYTETracker.removed_stracks
 constexpr int FL_REMOVED_NOW = 16;   // marked removed in the current frame (joins removed_stracks at its end)
 
-constexpr int KF_REC = 48;           // doubles per Kalman record: mean 8 + packed cov 36 + pad (384 B)
-
 struct TrackMeta {                   // 48 B, one per slot
     double score;
     double cls;
@@ -40,6 +38,14 @@ struct BtCounters {                  // one per stream, 128 B
 };
 static_assert(sizeof(BtCounters) == 128, "BtCounters layout");
 
+struct BtGrid {                      // one grid per stream (hdr) + cell / item arrays
+    GridHdr *hdr;                    // [S]
+    int *cell;                       // [S][GRID_MAX_CELLS + 1]
+    int *items, *big;                // [S][cap]
+    Box *boxes;                      // [S][cap]
+    long long cap;
+};
+
 struct BtArgs {
     int S, CAP, MAXD;
     double track_thresh, match_thresh, det_thresh;
@@ -53,14 +59,14 @@ struct BtArgs {
     int *tracked, *lost, *free_list;   // [S*CAP]
     BtCounters *cnt;          // [S]
     // per-frame: detections [S*MAXD]
-    Box *det_box;
     double *det_xyah;         // [S*MAXD][4]
     double *det_conf, *det_cls;
-    int *high, *second, *rest, *birth;
+    int *high, *second, *rest, *birth, *rest_of_high;
     Box *high_box, *second_box, *rest_box;
     double *high_score, *rest_score;
+    BtGrid grid_high, grid_second, grid_lost;
     // per-frame: tracks [S*CAP]
-    int *pool, *unc, *left, *t2, *l2, *kind1, *kind2, *dropA, *dropB, *newslot;
+    int *pool, *unc, *left, *left_of_pool, *t2, *l2, *kind1, *dropA, *dropB;
     Box *pool_box, *unc_box, *left_box, *tbox, *lbox;
     int *tage, *lage;
     // association results

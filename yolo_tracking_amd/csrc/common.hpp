@@ -37,6 +37,15 @@ int select_device(int device);
 // ------------------------------------------------------------------ device helpers
 constexpr int WAVE = 64;
 
+// Block barrier for kernels that hand data between threads through GLOBAL memory: every wave
+// drains its outstanding vector-memory operations before the barrier.  (__syncthreads() alone
+// lowers to a bare s_barrier on gfx950 for workgroup scope; a global store still in flight could
+// then be overtaken by another thread's load of the same address after the barrier.)
+__device__ __forceinline__ void block_sync() {
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __syncthreads();
+}
+
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
 
 __device__ __forceinline__ unsigned long long lanemask_lt() {
@@ -56,7 +65,7 @@ __device__ __forceinline__ int block_exclusive_scan(int v, int *wsum, int *total
         if (lane >= off) incl += t;
     }
     if (lane == WAVE - 1) wsum[wid] = incl;
-    __syncthreads();
+    block_sync();
     if (threadIdx.x == 0) {
         int run = 0;
         for (int w = 0; w < nw; ++w) {

@@ -1,0 +1,214 @@
+// Uniform-grid binning of a box set, so a track only scores the detections it can intersect.
+//
+// Exactness.  A pair whose boxes do not intersect has IoU = +-0 (or NaN), hence 1 - IoU >= 1 and
+// 1 - (1 - (1 - IoU)) * s >= 1 for every cost threshold the reference uses (< 1): it can never be an
+// association candidate (assoc.hpp).  Boxes with a non-positive or non-finite width/height never
+// intersect anything and are left out.  The grid only skips pairs that provably do not intersect;
+// every visited pair is then scored with the exact float64 expression.
+//
+//  * cell size g = mean box size; a box goes to the cell of its top-left corner and its box is
+//    stored next to its id in cell order (one load per candidate);
+//  * boxes larger than 4 g go to a "big" list that every query scans, so the binned boxes have a
+//    small maximum width W and height H;
+//  * a query box T visits cells x in [cell(T.x1 - W - eps), cell(T.x2)] (same for y): a box D that
+//    intersects T has D.x1 < T.x2 and D.x1 = D.x2 - w(D) > T.x1 - W, cell() is monotone, and eps
+//    (1e-12 relative) covers the rounding of w(D) and of the subtraction.
+#pragma once
+#include "common.hpp"
+#include "geometry.hpp"
+
+namespace yta {
+
+constexpr int GRID_MAX_CELLS = 4096;
+
+struct GridHdr {
+    double ox, oy, inv_g, maxw, maxh, g;
+    int gx, gy, n_big, n_binned;
+};
+
+struct GridView {
+    GridHdr *hdr;
+    int *cell_start;   // GRID_MAX_CELLS + 1
+    int *ids;          // binned item ids, in cell order
+    Box *boxes;        // their boxes, same order
+    int *big;          // items scanned by every query
+};
+
+__host__ __device__ __forceinline__ bool box_usable(const Box &b) {
+    const double w = b.x2 - b.x1, h = b.y2 - b.y1;
+    return w > 0.0 && h > 0.0 && isfinite(b.x1) && isfinite(b.y1) && isfinite(b.x2) &&
+           isfinite(b.y2) && isfinite(w) && isfinite(h);
+}
+
+__device__ __forceinline__ int grid_cell_1d(double x, double o, double inv_g, int n) {
+    double f = floor((x - o) * inv_g);
+    f = f < 0.0 ? 0.0 : (f > (double)(n - 1) ? (double)(n - 1) : f);
+    return (int)f;
+}
+
+struct GridScratch {
+    int cnt[GRID_MAX_CELLS + 1];
+    double red[8 * 16];
+    GridHdr hdr;
+};
+
+// Block-wide min/max/sum of up to 6 values (per-wave partials through `red`).
+__device__ __forceinline__ void block_reduce6(double v[6], const bool is_min[6], double *red) {
+    for (int off = 32; off > 0; off >>= 1)
+        for (int k = 0; k < 6; ++k) {
+            const double o = __shfl_xor(v[k], off);
+            v[k] = is_min[k] == true ? fmin(v[k], o) : (k < 4 ? fmax(v[k], o) : v[k] + o);
+        }
+    const int wv = threadIdx.x / WAVE, nw = (blockDim.x + WAVE - 1) / WAVE;
+    if (lane_id() == 0)
+        for (int k = 0; k < 6; ++k) red[8 * wv + k] = v[k];
+    block_sync();
+    for (int k = 0; k < 6; ++k) {
+        double a = red[k];
+        for (int w = 1; w < nw; ++w) {
+            const double o = red[8 * w + k];
+            a = is_min[k] ? fmin(a, o) : (k < 4 ? fmax(a, o) : a + o);
+        }
+        v[k] = a;
+    }
+    block_sync();
+}
+
+// Block-wide build (every thread of the block calls it).  box(i) returns item i's box.
+template <typename BoxOf>
+__device__ void grid_build(int n, BoxOf box, GridView gv, GridScratch &gs, int *wsum) {
+    const int t = threadIdx.x, nt = blockDim.x;
+    // pass 1: mean size of the usable boxes
+    double v[6] = {0, 0, 0, 0, 0, 0};
+    const bool sum6[6] = {false, false, false, false, false, false};
+    for (int i = t; i < n; i += nt) {
+        const Box b = box(i);
+        if (!box_usable(b)) continue;
+        v[4] += fmax(b.x2 - b.x1, b.y2 - b.y1);
+        v[5] += 1.0;
+    }
+    block_reduce6(v, sum6, gs.red);
+    const double nb = v[5];
+    const double mean = nb > 0 ? v[4] / nb : 1.0;
+    const double bthr = 4.0 * mean;
+    // pass 2: extent of the binned top-left corners and their maximum width / height
+    double e[6] = {INFINITY, INFINITY, -INFINITY, -INFINITY, 0.0, 0.0};
+    const bool mins[6] = {true, true, false, false, false, false};
+    for (int i = t; i < n; i += nt) {
+        const Box b = box(i);
+        if (!box_usable(b) || b.x2 - b.x1 > bthr || b.y2 - b.y1 > bthr) continue;
+        e[0] = fmin(e[0], b.x1);
+        e[1] = fmin(e[1], b.y1);
+        e[2] = fmax(e[2], b.x2 - b.x1);   // max width  (slot 2, max)
+        e[3] = fmax(e[3], b.y2 - b.y1);   // max height (slot 3, max)
+        e[4] += 0.0;
+        e[5] += 0.0;
+    }
+    block_reduce6(e, mins, gs.red);
+    double f[6] = {-INFINITY, -INFINITY, 0, 0, 0, 0};
+    const bool maxs[6] = {false, false, false, false, false, false};
+    for (int i = t; i < n; i += nt) {
+        const Box b = box(i);
+        if (!box_usable(b) || b.x2 - b.x1 > bthr || b.y2 - b.y1 > bthr) continue;
+        f[0] = fmax(f[0], b.x1);
+        f[1] = fmax(f[1], b.y1);
+    }
+    block_reduce6(f, maxs, gs.red);
+    if (t == 0) {
+        GridHdr h;
+        h.maxw = e[2] > 0 ? e[2] : 0.0;
+        h.maxh = e[3] > 0 ? e[3] : 0.0;
+        if (!(f[0] >= e[0])) {   // nothing to bin
+            h.ox = h.oy = 0.0;
+            h.g = 1.0;
+            h.inv_g = 1.0;
+            h.gx = h.gy = 1;
+        } else {
+            double g = mean;
+            const double ex = f[0] - e[0], ey = f[1] - e[1];
+            double gxf = floor(ex / g) + 1.0, gyf = floor(ey / g) + 1.0;
+            while (gxf * gyf > (double)GRID_MAX_CELLS) {
+                g *= 1.25;
+                gxf = floor(ex / g) + 1.0;
+                gyf = floor(ey / g) + 1.0;
+            }
+            h.ox = e[0];
+            h.oy = e[1];
+            h.g = g;
+            h.inv_g = 1.0 / g;
+            h.gx = (int)gxf;
+            h.gy = (int)gyf;
+        }
+        h.n_big = 0;
+        h.n_binned = 0;
+        gs.hdr = h;
+    }
+    for (int c = t; c <= GRID_MAX_CELLS; c += nt) gs.cnt[c] = 0;
+    block_sync();
+    const GridHdr h = gs.hdr;
+    const int ncell = h.gx * h.gy;
+    for (int i = t; i < n; i += nt) {
+        const Box b = box(i);
+        if (!box_usable(b)) continue;
+        if (b.x2 - b.x1 > bthr || b.y2 - b.y1 > bthr) {
+            gv.big[atomicAdd(&gs.hdr.n_big, 1)] = i;
+            continue;
+        }
+        const int c = grid_cell_1d(b.y1, h.oy, h.inv_g, h.gy) * h.gx +
+                      grid_cell_1d(b.x1, h.ox, h.inv_g, h.gx);
+        atomicAdd(&gs.cnt[c], 1);
+    }
+    block_sync();
+    int run = 0;
+    for (int start = 0; start < ncell; start += nt) {
+        const int c = start + t;
+        const int cv = c < ncell ? gs.cnt[c] : 0;
+        int tot;
+        const int pos = block_exclusive_scan(cv, wsum, &tot);
+        if (c < ncell) {
+            gv.cell_start[c] = run + pos;
+            gs.cnt[c] = run + pos;
+        }
+        run += tot;
+    }
+    if (t == 0) {
+        gv.cell_start[ncell] = run;
+        gs.hdr.n_binned = run;
+        *gv.hdr = gs.hdr;
+    }
+    block_sync();
+    for (int i = t; i < n; i += nt) {
+        const Box b = box(i);
+        if (!box_usable(b) || b.x2 - b.x1 > bthr || b.y2 - b.y1 > bthr) continue;
+        const int c = grid_cell_1d(b.y1, h.oy, h.inv_g, h.gy) * h.gx +
+                      grid_cell_1d(b.x1, h.ox, h.inv_g, h.gx);
+        const int pos = atomicAdd(&gs.cnt[c], 1);
+        gv.ids[pos] = i;
+        gv.boxes[pos] = b;
+    }
+    block_sync();
+}
+
+// Visit every binned item that may intersect T: visit(id, box).  Big items: visit_big(id).
+template <typename Visit, typename VisitBig>
+__device__ __forceinline__ void grid_query(const GridView &gv, const GridHdr &h, const Box &T,
+                                           Visit visit, VisitBig visit_big) {
+    for (int k = 0; k < h.n_big; ++k) visit_big(gv.big[k]);
+    if (h.n_binned == 0) return;
+    if (!(T.x2 > T.x1 && T.y2 > T.y1)) return;   // also false for NaN: intersects nothing
+    const double lx = (T.x1 - h.maxw * (1.0 + 1e-12)) - (fabs(T.x1) + h.maxw) * 1e-12;
+    const double ly = (T.y1 - h.maxh * (1.0 + 1e-12)) - (fabs(T.y1) + h.maxh) * 1e-12;
+    const double fx1 = floor((T.x2 - h.ox) * h.inv_g), fy1 = floor((T.y2 - h.oy) * h.inv_g);
+    if (fx1 < 0.0 || fy1 < 0.0) return;
+    const int cx0 = grid_cell_1d(lx, h.ox, h.inv_g, h.gx);
+    const int cy0 = grid_cell_1d(ly, h.oy, h.inv_g, h.gy);
+    const int cx1 = fx1 > (double)(h.gx - 1) ? h.gx - 1 : (int)fx1;
+    const int cy1 = fy1 > (double)(h.gy - 1) ? h.gy - 1 : (int)fy1;
+    for (int cy = cy0; cy <= cy1; ++cy) {
+        const int base = cy * h.gx;
+        const int b = gv.cell_start[base + cx0], e = gv.cell_start[base + cx1 + 1];
+        for (int k = b; k < e; ++k) visit(gv.ids[k], gv.boxes[k]);   // cells of a row are contiguous
+    }
+}
+
+}  // namespace yta

@@ -4,6 +4,7 @@
 #include <vector>
 
 #include "assoc.hpp"
+#include "grid.hpp"
 #include "kf_xyah.hpp"
 
 using namespace yta;
@@ -45,14 +46,12 @@ __global__ void k_kf(int op, int n, const double *in_vec, double *mean, double *
         kf_initiate(in_vec + 4 * i, s);
     } else {
         for (int k = 0; k < 8; ++k) s.m[k] = mean[8 * i + k];
-        for (int r = 0; r < 8; ++r)
-            for (int c = r; c < 8; ++c) s.p[pidx(r, c)] = cov[64 * i + 8 * r + c];
+        kf_cov_pack(cov + 64 * i, s);   // the 2x2 blocks {j, j+4}; the rest is zero (kf_xyah.hpp)
         if (op == 1) kf_predict(s);
         else kf_update(s, in_vec + 4 * i);
     }
     for (int k = 0; k < 8; ++k) mean[8 * i + k] = s.m[k];
-    for (int r = 0; r < 8; ++r)
-        for (int c = 0; c < 8; ++c) cov[64 * i + 8 * r + c] = s.p[pidx(r, c)];
+    kf_cov_full(s, cov + 64 * i);
 }
 
 // cost matrix -> Box-free edge pool for the sparse solver (KAT path only)
@@ -68,6 +67,30 @@ __global__ void k_dense_edges(const double *cost, int nr, int nc, double thresh,
         e.col = (int)(idx % nc);
         e.cost = c;
         edges[pos] = e;
+    }
+}
+
+// One block: grid over b, then every a-box queries it; pairs with 1 - IoU < thresh are written
+// (the shape of remove_duplicate_stracks, byte_tracker.py:312-325).
+__global__ __launch_bounds__(1024) void k_grid_pairs(const Box *a, int na, const Box *b, int nb,
+                                                    double thresh, GridHdr *hdr, int *cell,
+                                                    int *ids, Box *boxes, int *big, int *pairs,
+                                                    int *n_pairs, int cap) {
+    __shared__ int wsum[32];
+    __shared__ GridScratch gs;
+    const GridView gv{hdr, cell, ids, boxes, big};
+    grid_build(nb, [&](int q) { return b[q]; }, gv, gs, wsum);
+    const GridHdr h = gs.hdr;
+    for (int p = threadIdx.x; p < na; p += blockDim.x) {
+        const Box T = a[p];
+        auto pair = [&](int q, const Box &lb) {
+            if (!intersects(T, lb)) return;
+            if (1 - iou(T, lb) < thresh) {
+                const int k = atomicAdd(n_pairs, 1);
+                if (k < cap) { pairs[2 * k] = p; pairs[2 * k + 1] = q; }
+            }
+        };
+        grid_query(gv, h, T, pair, [&](int q) { pair(q, b[q]); });
     }
 }
 
@@ -181,6 +204,39 @@ int yta_kf_xyah_update(int device, int n, double *mean, double *cov, const doubl
     return kf_call(device, 2, n, z, mean, cov);
 }
 
+int yta_grid_pairs(int device, const double *a, int na, const double *b, int nb, double thresh,
+                   int *pairs, int cap, int *n_pairs) {
+    YTA_CHECK(na >= 0 && nb >= 0 && cap >= 0 && n_pairs, YTA_ERR_INVALID, "bad argument");
+    *n_pairs = 0;
+    if (na == 0 || nb == 0) return YTA_OK;
+    YTA_CHECK(a && b && (cap == 0 || pairs), YTA_ERR_INVALID, "null buffer");
+    int rc = select_device(device);
+    if (rc) return rc;
+    DevBuf m;
+    Box *da, *db, *boxes;
+    GridHdr *hdr;
+    int *cell, *ids, *big, *dp, *dn;
+    YTA_HIP(m.get(&da, na));
+    YTA_HIP(m.get(&db, nb));
+    YTA_HIP(m.get(&hdr, 1));
+    YTA_HIP(m.get(&cell, GRID_MAX_CELLS + 1));
+    YTA_HIP(m.get(&ids, nb));
+    YTA_HIP(m.get(&boxes, nb));
+    YTA_HIP(m.get(&big, nb));
+    YTA_HIP(m.get(&dp, 2 * (size_t)(cap > 0 ? cap : 1)));
+    YTA_HIP(m.get(&dn, 1));
+    YTA_HIP(hipMemcpy(da, a, sizeof(Box) * na, hipMemcpyHostToDevice));
+    YTA_HIP(hipMemcpy(db, b, sizeof(Box) * nb, hipMemcpyHostToDevice));
+    YTA_HIP(hipMemset(dn, 0, sizeof(int)));
+    hipLaunchKernelGGL(k_grid_pairs, dim3(1), dim3(1024), 0, 0, da, na, db, nb, thresh, hdr, cell,
+                       ids, boxes, big, dp, dn, cap);
+    YTA_HIP(hipGetLastError());
+    YTA_HIP(hipMemcpy(n_pairs, dn, sizeof(int), hipMemcpyDeviceToHost));
+    const int n = *n_pairs < cap ? *n_pairs : cap;
+    if (n) YTA_HIP(hipMemcpy(pairs, dp, sizeof(int) * 2 * n, hipMemcpyDeviceToHost));
+    return YTA_OK;
+}
+
 int yta_lap_limited(int device, int nr, int nc, const double *cost, double cost_limit, int *x,
                     int *y) {
     YTA_CHECK(nr >= 0 && nc >= 0, YTA_ERR_INVALID, "negative size");
@@ -225,7 +281,7 @@ int yta_lap_limited(int device, int nr, int nc, const double *cost, double cost_
     ps.max_cols = nc;
     ps.x = dx;
     ps.y = dy;
-    YTA_HIP(launch_lap(ps, 1, 0));
+    YTA_HIP(launch_lap(ps, 1, nullptr, 0, 0));
     YTA_HIP(hipMemcpy(x, dx, sizeof(int) * nr, hipMemcpyDeviceToHost));
     YTA_HIP(hipMemcpy(y, dy, sizeof(int) * nc, hipMemcpyDeviceToHost));
     YTA_HIP(hipMemcpy(h_cnt, cnt, sizeof(h_cnt), hipMemcpyDeviceToHost));

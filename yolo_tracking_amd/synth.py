@@ -14,10 +14,10 @@ import numpy as np
 
 class SyntheticStream:
     def __init__(self, n_objects, seed, low_conf_frac=0.1, emb_dim=0, turnover=0.02,
-                 speed_sigma=1.5, jitter_sigma=0.5, shuffle=True):
+                 speed_sigma=1.5, jitter_sigma=0.5, shuffle=True, canvas=None):
         self.n = int(n_objects)
         self.rng = np.random.default_rng(seed)
-        self.canvas = 64.0 * np.sqrt(max(self.n, 1))
+        self.canvas = float(canvas) if canvas else 64.0 * np.sqrt(max(self.n, 1))
         self.low_conf_frac = float(low_conf_frac)
         self.emb_dim = int(emb_dim)
         self.turnover = float(turnover)
