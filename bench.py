@@ -26,9 +26,9 @@ import numpy as np
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
-PHASES = ["begin", "edges1", "lap1", "prep23", "edges23", "lap23", "apply", "finish"]
+PHASES = ["stage1", "stage23", "apply", "finish"]
 STATS = ["dets", "high", "second", "pool", "act", "unc", "left", "rest", "births", "t2", "l2",
-         "tracked", "lost", "out", "edges1", "edges23"]
+         "tracked", "lost", "out", "edges1", "edges23", "fallback1", "fallback23"]
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # Canonical algorithmic bytes per update: ByteTrack 1024 x 1024
 BYTES_PER_UPDATE_1024 = 19_259_392
@@ -49,12 +49,14 @@ def kernel_bytes(phase, st):
         # every pool track: KF state + meta read and written once, pool index + stage results read;
         # every matched track: its detection's xyah / conf / cls read
         return pool * (2 * 192 + 2 * 48 + 12) + unc * (48 + 8) + matched * 48
-    if phase == "begin":
-        return dets * (48 + 48 + 4) + high * (32 + 8 + 8) + pool * (64 + 48 + 32 + 4) + unc * 40
-    if phase == "edges1":
-        return pool * 32 + high * (32 + 8) + st["edges1"] * 16
-    if phase == "lap1":
-        return st["edges1"] * 16 + (pool + high) * 8
+    if phase == "stage1":
+        # dets read + converted rows written; high / low lists + boxes; tracked list, meta, the
+        # predicted mean of every pool track; pool / unconfirmed lists + boxes; stage-1 results
+        return (dets * (48 + 48) + high * (4 + 32 + 8 + 4) + st["second"] * (4 + 32)
+                + pool * (4 + 48 + 64 + 4 + 32 + 4) + unc * (4 + 48 + 64 + 4 + 32))
+    if phase == "stage23":
+        return (pool * (4 + 48 + 4) + high * (4 + 8 + 8) + st["left"] * (8 + 32 + 4)
+                + st["second"] * (32 + 4) + unc * (32 + 4) + st["rest"] * (4 + 32 + 8 + 4))
     if phase == "finish":
         return (st["t2"] + st["l2"]) * (32 + 48 + 12) + st["out"] * 64 + st["births"] * (192 + 48)
     return 0
@@ -174,9 +176,9 @@ def main():
     value = calls / elapsed
     ms_per_step = 1000.0 * elapsed / args.steps
 
-    stats = (ctypes.c_longlong * 16)()
+    stats = (ctypes.c_longlong * len(STATS))()
     _lib.check(lib.yta_bytetrack_stats(h, stats))
-    st = {STATS[k]: int(stats[k]) for k in range(16)}
+    st = {STATS[k]: int(stats[k]) for k in range(len(STATS))}
     if rank == 0:
         # roofline kernel: the Kalman predict/update pass over every live track (HBM-bound)
         dom = "apply"

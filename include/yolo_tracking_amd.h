@@ -114,9 +114,9 @@ int yta_bytetrack_sync(yta_bytetrack *engine);      /* waits; reports device-sid
  * (64 f64).  *n_tracks receives the count; buffers must hold track_capacity entries. */
 int yta_bytetrack_get_state(yta_bytetrack *engine, int stream, int *n_tracks, long long *ints,
                             double *mean, double *cov);
-/* Measurement: when enabled, HIP events are recorded around each of the 8 launches of a frame on
+/* Measurement: when enabled, HIP events are recorded around each of the 4 launches of a frame on
  * the engine's stream; collect returns per-launch milliseconds summed over the covered frames in
- * launch order (begin, edges1, lap1, prep23, edges23, lap23, apply, finish). */
+ * launch order (stage1, stage23, apply, finish). */
 int yta_bytetrack_profile(yta_bytetrack *engine, int enable);
 int yta_bytetrack_profile_collect(yta_bytetrack *engine, double *ms, int *frames);
 /* Debug introspection of the last frame's duplicate removal (stream s): tracked' / lost' boxes
@@ -126,8 +126,13 @@ int yta_bytetrack_debug_dedup(yta_bytetrack *engine, int stream, int *n_t2, int 
                               double *tbox, double *lbox, int *ages, int *drops);
 /* Last frame's counts summed over streams (synchronises): dets, high, second, pool, activated,
  * unconfirmed, leftovers, rest, births, tracked', lost', tracked, lost, output rows, stage-1
- * candidate edges, stage-2+3 candidate edges (16 int64). */
+ * candidate edges, stage-2+3 candidate edges, then the cumulative number of stream-frames whose
+ * stage-1 / stage-2+3 association did not fit in LDS and ran over global memory (18 int64). */
 int yta_bytetrack_stats(yta_bytetrack *engine, long long *stats);
+/* Tuning / testing: bytes of LDS the association kernels may use per stream (default 72 KiB,
+ * at most 150 KiB); a stream-frame that does not fit runs over global memory.  0 forces the
+ * global-memory path for every stream. */
+int yta_bytetrack_set_lds(yta_bytetrack *engine, int bytes);
 /* Throughput helper: the engine's HIP stream (hipStream_t as void*) */
 int yta_bytetrack_hip_stream(yta_bytetrack *engine, void **stream);
 

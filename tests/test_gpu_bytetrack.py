@@ -179,3 +179,46 @@ def test_headline_size_vs_oracle():
     ref = ByteTrackOracle(**KW)
     for f, d in enumerate(frames):
         _assert_rows(eng.update([d])[0], ref.update(d).reshape(-1, 8), f)
+
+
+@pytest.mark.parametrize("lds", [0, 16 * 1024])
+def test_global_memory_association_path(golden_dir, lds):
+    """The association kernels redo a stream-frame over global memory when its problem does not
+    fit in the LDS arena; lds=0 forces that path everywhere, 16 KiB mixes both within a frame."""
+    g = np.load(os.path.join(golden_dir, "bytetrack_synth.npz"))
+    case = "n1024_s13"
+    dets, dc = g[f"{case}__dets"], g[f"{case}__det_counts"]
+    oc, out = g[f"{case}__out_counts"], g[f"{case}__out"]
+    eng = ByteTrackEngine(1, **KW)
+    eng.set_lds(lds)
+    o0 = r0 = 0
+    for f, n in enumerate(dc):
+        got = eng.update([dets[o0:o0 + n]])[0]
+        _assert_rows(got, out[r0:r0 + oc[f]], (case, f))
+        o0 += n
+        r0 += oc[f]
+    st = eng.stats()
+    assert st["fallback1"] > 0
+    if lds == 0:
+        assert st["fallback1"] == len(dc) and st["fallback23"] == len(dc)
+
+
+def test_pileup_large_components_vs_oracle():
+    """Dense pile-up: association components beyond one wavefront (global-slab solver)."""
+    frames = [d for d, _ in make_frames(160, 12, seed=77, canvas=70.0, speed_sigma=2.0,
+                                        turnover=0.05)]
+    eng = ByteTrackEngine(1, **KW)
+    ref = ByteTrackOracle(**KW)
+    for f, d in enumerate(frames):
+        _assert_rows(eng.update([d])[0], ref.update(d).reshape(-1, 8), f)
+
+
+def test_headline_size_runs_in_lds():
+    """At the benchmark size (1024 x 1024) every stage fits the default LDS arena."""
+    frames = [d for d, _ in make_frames(1024, 6, seed=14)]
+    eng = ByteTrackEngine(2, track_capacity=2048, max_dets=1024, **KW)
+    for d in frames:
+        eng.update([d, d])
+    st = eng.stats()
+    assert st["edges1"] > 0
+    assert st["fallback1"] == 0 and st["fallback23"] == 0, st

@@ -67,6 +67,7 @@ _SIGS = {
     "yta_bytetrack_debug_dedup": ([_P, _I, _P, _P, _P, _P, _P, _P], _I),
     "yta_bytetrack_stats": ([_P, _P], _I),
     "yta_bytetrack_hip_stream": ([_P, _P], _I),
+    "yta_bytetrack_set_lds": ([_P, _I], _I),
 }
 
 EXPORTED_SYMBOLS = tuple(_SIGS)

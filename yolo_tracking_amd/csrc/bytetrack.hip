@@ -32,6 +32,7 @@ namespace yta {
 namespace {
 
 constexpr int BLK = 1024;    // block/stream kernels
+constexpr int BLK_WAVES = BLK / WAVE;
 constexpr int GRID_T = 256;  // grid kernels
 
 __device__ __forceinline__ void load_kf(const double *kf, long long slot, KfState &s) {
@@ -67,11 +68,27 @@ __device__ __forceinline__ GridView grid_of(const BtGrid &g, int s) {
                     g.boxes + s * g.cap, g.big + s * g.cap};
 }
 
-// ------------------------------------------------------------------------------------ k_begin
-__global__ __launch_bounds__(BLK) void k_begin(BtArgs a) {
-    __shared__ int wsum[32];
-    __shared__ GridScratch gs;
-    const int s = blockIdx.x, t = threadIdx.x;
+// ------------------------------------------------------------------------------------ k_stage1
+// Per stream: frame_id++, confidence split (:149-158), STrack box conversions (:14-25),
+// tracked -> activated / unconfirmed, pool = act ++ lost (:169-178), predicted pool boxes (mean
+// only, multi_predict :35-48 zeroes vh of non-tracked tracks; the covariance is advanced in
+// k_apply), unconfirmed boxes (not predicted), then stage 1: pool x high detections, fused IoU
+// (:181-183), lapjv with cost_limit = match_thresh (:184-186).
+__device__ __forceinline__ LapSlab slab_of(const BtArgs &a, int s) {
+    LapSlab l = a.slab;
+    const int nw = blockDim.x / WAVE;
+    l.i += (long long)s * nw * l.i_stride;
+    l.d += (long long)s * nw * l.d_stride;
+    return l;
+}
+
+struct StageShared {
+    AssocShared as;
+};
+
+__device__ __forceinline__ bool stage1_body(const BtArgs &a, int s, Arena &ar, StageShared &sh) {
+    int *wsum = sh.as.lap.wsum;
+    const int t = threadIdx.x, nt = blockDim.x;
     BtCounters *c = a.cnt + s;
     const long long db = (long long)s * a.MAXD, tb = (long long)s * a.CAP;
     int nd = a.det_off[s + 1] - a.det_off[s];
@@ -81,7 +98,7 @@ __global__ __launch_bounds__(BLK) void k_begin(BtArgs a) {
     }
     const double *din = a.det_in + (long long)a.det_off[s] * 6;
     const double thr = a.track_thresh;
-    for (int i = t; i < nd; i += BLK) {
+    for (int i = t; i < nd; i += nt) {
         const double *d = din + (long long)i * 6;
         double xywh[4];
         det_xyxy_to_xywh(d, xywh);                       // STrack.__init__ (:16-18)
@@ -109,10 +126,6 @@ __global__ __launch_bounds__(BLK) void k_begin(BtArgs a) {
                                            a.second[db + pos] = i;
                                            a.second_box[db + pos] = det_box(i);
                                        });
-    block_sync();
-    grid_build(n_high, [&](int i) { return a.high_box[db + i]; }, grid_of(a.grid_high, s), gs, wsum);
-    grid_build(n_second, [&](int i) { return a.second_box[db + i]; }, grid_of(a.grid_second, s), gs,
-               wsum);
     const int n_tracked = c->n_tracked, n_lost = c->n_lost;
     const int *tracked = a.tracked + tb;
     const int n_act = block_compact(
@@ -121,18 +134,23 @@ __global__ __launch_bounds__(BLK) void k_begin(BtArgs a) {
     const int n_unc = block_compact(
         n_tracked, wsum, [&](int i) { return (a.meta[tb + tracked[i]].flags & FL_ACTIVATED) == 0; },
         [&](int i, int pos) { a.unc[tb + pos] = tracked[i]; });
-    for (int i = t; i < n_lost; i += BLK) a.pool[tb + n_act + i] = a.lost[tb + i];
+    for (int i = t; i < n_lost; i += nt) a.pool[tb + n_act + i] = a.lost[tb + i];
     block_sync();
     const int n_pool = n_act + n_lost;
-    // predicted boxes of the pool (STrack.multi_predict :35-48 zeroes vh of non-tracked tracks;
-    // the box needs the predicted mean only, the covariance is advanced in k_apply)
-    for (int i = t; i < n_pool; i += BLK) {
+    for (int i = t; i < n_pool; i += nt) {
         const long long slot = tb + a.pool[tb + i];
         const double *m = a.kf + slot * KF_REC;
         const double vh = st_of(a.meta[slot].flags) == ST_TRACKED ? m[7] : 0.0;
         a.pool_box[tb + i] = xyah_mean_to_box(m[0] + m[4], m[1] + m[5], m[2] + m[6], m[3] + vh);
     }
-    for (int j = t; j < n_unc; j += BLK) a.unc_box[tb + j] = kf_box(a.kf, tb + a.unc[tb + j]);
+    for (int j = t; j < n_unc; j += nt) a.unc_box[tb + j] = kf_box(a.kf, tb + a.unc[tb + j]);
+    block_sync();
+    const bool ok = assoc_block(
+        n_pool, [&](int i) { return a.pool_box[tb + i]; }, n_high,
+        [&](int j) { return a.high_box[db + j]; }, true,
+        [&](int j) { return a.high_score[db + j]; }, a.match_thresh, a.x1 + tb, a.y1 + db, &c->err,
+        &c->n_edges[0], ar, slab_of(a, s), sh.as);
+    if (!ok) return false;
     if (t == 0) {
         c->frame_id += 1;
         c->n_dets = nd;
@@ -144,19 +162,21 @@ __global__ __launch_bounds__(BLK) void k_begin(BtArgs a) {
         c->n_left = 0;
         c->n_rest = 0;
         c->n_births = 0;
-        c->n_edges[0] = c->n_edges[1] = c->n_edges[2] = 0;
     }
+    return true;
 }
 
-// ------------------------------------------------------------------------------------ k_prep23
-__global__ __launch_bounds__(BLK) void k_prep23(BtArgs a) {
-    __shared__ int wsum[32];
-    const int s = blockIdx.x;
+// ------------------------------------------------------------------------------------ k_stage23
+// Per stream: leftovers = unmatched Tracked pool rows (:205-209) x low detections, IoU, cost_limit
+// 0.5 (:210-211); rest = unmatched high detections (:229); unconfirmed x rest, fused IoU,
+// cost_limit 0.7 (:230-233).
+__device__ __forceinline__ bool stage23_body(const BtArgs &a, int s, Arena &ar, StageShared &sh) {
+    int *wsum = sh.as.lap.wsum;
+    const int t = threadIdx.x, nt = blockDim.x;
     BtCounters *c = a.cnt + s;
     const long long tb = (long long)s * a.CAP, db = (long long)s * a.MAXD;
-    const int n_pool = c->n_pool, n_high = c->n_high;
-    for (int i = threadIdx.x; i < n_pool; i += BLK) a.left_of_pool[tb + i] = -1;
-    for (int h = threadIdx.x; h < n_high; h += BLK) a.rest_of_high[db + h] = -1;
+    const int n_pool = c->n_pool, n_high = c->n_high, n_second = c->n_second, n_unc = c->n_unc;
+    for (int i = t; i < n_pool; i += nt) a.left_of_pool[tb + i] = -1;
     block_sync();
     const int n_left = block_compact(
         n_pool, wsum,
@@ -166,19 +186,62 @@ __global__ __launch_bounds__(BLK) void k_prep23(BtArgs a) {
         [&](int i, int pos) {
             a.left[tb + pos] = i;
             a.left_of_pool[tb + i] = pos;
-            a.left_box[tb + pos] = a.pool_box[tb + i];
         });
     const int n_rest = block_compact(n_high, wsum, [&](int h) { return a.y1[db + h] < 0; },
                                      [&](int h, int pos) {
                                          a.rest[db + pos] = h;
-                                         a.rest_of_high[db + h] = pos;
-                                         a.rest_box[db + pos] = a.high_box[db + h];
                                          a.rest_score[db + pos] = a.high_score[db + h];
                                      });
-    if (threadIdx.x == 0) {
+    block_sync();
+    const LapSlab slab = slab_of(a, s);
+    bool ok = assoc_block(
+        n_left, [&](int k) { return a.pool_box[tb + a.left[tb + k]]; }, n_second,
+        [&](int q) { return a.second_box[db + q]; }, false, [&](int) { return 1.0; }, 0.5,
+        a.x2 + tb, a.y2 + db, &c->err, &c->n_edges[1], ar, slab, sh.as);
+    if (!ok) return false;
+    ar.reset();
+    ok = assoc_block(
+        n_unc, [&](int j) { return a.unc_box[tb + j]; }, n_rest,
+        [&](int r) { return a.high_box[db + a.rest[db + r]]; }, true,
+        [&](int r) { return a.rest_score[db + r]; }, 0.7, a.x3 + tb, a.y3 + db, &c->err,
+        &c->n_edges[2], ar, slab, sh.as);
+    if (!ok) return false;
+    if (t == 0) {
         c->n_left = n_left;
         c->n_rest = n_rest;
     }
+    return true;
+}
+
+// LDS first; a frame whose association does not fit is redone over the stream's global arena
+// (both bodies only write values that the redo rewrites identically, and bump the frame counter
+// only on success).
+__global__ __launch_bounds__(BLK) void k_stage1(BtArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    __shared__ StageShared sh;
+    const int s = blockIdx.x;
+    {
+        Arena ar(smem, a.lds_bytes);
+        if (stage1_body(a, s, ar, sh)) return;
+    }
+    block_sync();
+    if (threadIdx.x == 0) a.cnt[s].n_fallback[0] += 1;
+    Arena ag(a.ws + s * a.ws_stride, a.ws_stride);
+    if (!stage1_body(a, s, ag, sh) && threadIdx.x == 0) atomicOr(&a.cnt[s].err, ERR_EDGE_OVERFLOW);
+}
+
+__global__ __launch_bounds__(BLK) void k_stage23(BtArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    __shared__ StageShared sh;
+    const int s = blockIdx.x;
+    {
+        Arena ar(smem, a.lds_bytes);
+        if (stage23_body(a, s, ar, sh)) return;
+    }
+    block_sync();
+    if (threadIdx.x == 0) a.cnt[s].n_fallback[1] += 1;
+    Arena ag(a.ws + s * a.ws_stride, a.ws_stride);
+    if (!stage23_body(a, s, ag, sh) && threadIdx.x == 0) atomicOr(&a.cnt[s].err, ERR_EDGE_OVERFLOW);
 }
 
 // ------------------------------------------------------------------------------------ k_apply
@@ -448,16 +511,10 @@ using namespace yta;
 
 struct yta_bytetrack {
     int device = 0, S = 0, CAP = 0, MAXD = 0;
-    long long edge_cap = 0;
     yta_bytetrack_params prm{};
     hipStream_t stream = nullptr;
     std::vector<void *> allocs;
     BtArgs a{};
-    // association buffers: stages 1 and 2 share pool A, stage 3 uses pool B
-    Edge *edgesA = nullptr, *edgesB = nullptr;
-    int *wsA = nullptr, *wsB = nullptr;
-    double *wsdA = nullptr, *wsdB = nullptr;
-    long long ws_i = 0, ws_d = 0;
     // host staging
     double *h_dets = nullptr;
     int *h_off = nullptr;
@@ -473,7 +530,8 @@ struct yta_bytetrack {
 
 namespace {
 
-constexpr int BT_PHASES = 8;   // launches per frame, see yta_bytetrack_profile_collect
+constexpr int BT_PHASES = 4;   // launches per frame, see yta_bytetrack_profile_collect
+constexpr size_t BT_LDS_BYTES = 72 * 1024;   // dynamic LDS of the stage kernels
 
 template <typename T>
 int dalloc(yta_bytetrack *e, T **p, long long n) {
@@ -529,15 +587,11 @@ int bt_alloc(yta_bytetrack *e) {
     DALLOC(a.second, S * MAXD);
     DALLOC(a.rest, S * MAXD);
     DALLOC(a.birth, S * MAXD);
-    DALLOC(a.rest_of_high, S * MAXD);
     DALLOC(a.high_box, S * MAXD);
     DALLOC(a.second_box, S * MAXD);
-    DALLOC(a.rest_box, S * MAXD);
     DALLOC(a.high_score, S * MAXD);
     DALLOC(a.rest_score, S * MAXD);
-    int rc = grid_alloc(e, a.grid_high, MAXD);
-    if (!rc) rc = grid_alloc(e, a.grid_second, MAXD);
-    if (!rc) rc = grid_alloc(e, a.grid_lost, CAP);
+    int rc = grid_alloc(e, a.grid_lost, CAP);
     if (rc) return rc;
     DALLOC(a.pool, S * CAP);
     DALLOC(a.unc, S * CAP);
@@ -550,7 +604,6 @@ int bt_alloc(yta_bytetrack *e) {
     DALLOC(a.dropB, S * CAP);
     DALLOC(a.pool_box, S * CAP);
     DALLOC(a.unc_box, S * CAP);
-    DALLOC(a.left_box, S * CAP);
     DALLOC(a.tbox, S * CAP);
     DALLOC(a.lbox, S * CAP);
     DALLOC(a.tage, S * CAP);
@@ -562,16 +615,17 @@ int bt_alloc(yta_bytetrack *e) {
     DALLOC(a.y2, S * MAXD);
     DALLOC(a.y3, S * MAXD);
     DALLOC(a.out, S * CAP * 8);
-    // association: worst-case edge pools (every pair a candidate), so no frame can overflow
-    e->edge_cap = CAP * MAXD;
-    e->ws_i = lap_ws_ints((int)CAP, (int)MAXD, e->edge_cap);
-    e->ws_d = lap_ws_doubles((int)CAP, (int)MAXD, e->edge_cap);
-    DALLOC(e->edgesA, S * e->edge_cap);
-    DALLOC(e->edgesB, S * e->edge_cap);
-    DALLOC(e->wsA, S * e->ws_i);
-    DALLOC(e->wsB, S * e->ws_i);
-    DALLOC(e->wsdA, S * e->ws_d);
-    DALLOC(e->wsdB, S * e->ws_d);
+    // association: LDS arena first; the global fallback arena holds the worst case (every pair a
+    // candidate edge), so no frame can overflow it
+    a.lds_bytes = BT_LDS_BYTES;
+    a.ws_stride = (assoc_arena_bytes(CAP, MAXD, CAP * MAXD) + 255) & ~255LL;
+    DALLOC(a.ws, S * a.ws_stride);
+    a.slab.R = (int)CAP;
+    a.slab.C = (int)MAXD;
+    a.slab.i_stride = lap_slab_ints((int)CAP, (int)MAXD);
+    a.slab.d_stride = lap_slab_doubles((int)CAP, (int)MAXD);
+    DALLOC(a.slab.i, S * BLK_WAVES * a.slab.i_stride);
+    DALLOC(a.slab.d, S * BLK_WAVES * a.slab.d_stride);
     DALLOC(e->d_det_off, S + 1);
     YTA_HIP(hipHostMalloc((void **)&e->h_off, sizeof(int) * (S + 1), hipHostMallocDefault));
     YTA_HIP(hipHostMalloc((void **)&e->h_cnt, sizeof(BtCounters) * S, hipHostMallocDefault));
@@ -595,53 +649,12 @@ int mark(yta_bytetrack *e) {
         if (_m) return _m; \
     } while (0)
 
-ProblemSet make_problem(yta_bytetrack *e, int stage, const Box *rows, const int *n_rows_field,
-                        const Box *cols, const double *col_score, const int *n_cols_field,
-                        const BtGrid *grid, const int *remap, double thresh, Edge *edges, int *ws,
-                        double *wsd, int *x, int *y) {
-    BtArgs &a = e->a;
-    const int cstride = (int)(sizeof(BtCounters) / sizeof(int));
-    ProblemSet ps{};
-    ps.rows = rows;
-    ps.rows_stride = a.CAP;
-    ps.n_rows = n_rows_field;
-    ps.n_rows_stride = cstride;
-    ps.cols = cols;
-    ps.cols_stride = a.MAXD;
-    ps.col_score = col_score;
-    ps.score_stride = a.MAXD;
-    ps.n_cols = n_cols_field;
-    ps.n_cols_stride = cstride;
-    if (grid) {
-        ps.ghdr = grid->hdr;
-        ps.gcell = grid->cell;
-        ps.gcell_stride = GRID_MAX_CELLS + 1;
-        ps.gitems = grid->items;
-        ps.gboxes = grid->boxes;
-        ps.gbig = grid->big;
-        ps.gitems_stride = grid->cap;
-    }
-    ps.remap = remap;
-    ps.remap_stride = a.MAXD;
-    ps.thresh = thresh;
-    ps.edges = edges;
-    ps.edges_stride = e->edge_cap;
-    ps.edge_cap = e->edge_cap;
-    ps.n_edges = &a.cnt[0].n_edges[stage];
-    ps.n_edges_stride = cstride;
-    ps.err = &a.cnt[0].err;
-    ps.err_stride = cstride;
-    ps.ws = ws;
-    ps.ws_stride = e->ws_i;
-    ps.wsd = wsd;
-    ps.wsd_stride = e->ws_d;
-    ps.max_rows = a.CAP;
-    ps.max_cols = a.MAXD;
-    ps.x = x;
-    ps.x_stride = a.CAP;
-    ps.y = y;
-    ps.y_stride = a.MAXD;
-    return ps;
+int set_lds_limits() {
+    YTA_HIP(hipFuncSetAttribute((const void *)k_stage1, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)BT_LDS_BYTES));
+    YTA_HIP(hipFuncSetAttribute((const void *)k_stage23, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)BT_LDS_BYTES));
+    return YTA_OK;
 }
 
 int launch_pipeline(yta_bytetrack *e, const double *det_in, const int *det_off, double *out,
@@ -651,30 +664,12 @@ int launch_pipeline(yta_bytetrack *e, const double *det_in, const int *det_off, 
     a.det_off = det_off;
     a.out = out;
     a.out_counts = out_counts;
-    BtCounters *c0 = a.cnt;
-    const ProblemSet s1 = make_problem(e, 0, a.pool_box, &c0->n_pool, a.high_box, a.high_score,
-                                       &c0->n_high, &a.grid_high, nullptr, a.match_thresh,
-                                       e->edgesA, e->wsA, e->wsdA, a.x1, a.y1);
-    const ProblemSet s2 = make_problem(e, 1, a.left_box, &c0->n_left, a.second_box, nullptr,
-                                       &c0->n_second, &a.grid_second, nullptr, 0.5, e->edgesA,
-                                       e->wsA, e->wsdA, a.x2, a.y2);
-    const ProblemSet s3 = make_problem(e, 2, a.unc_box, &c0->n_unc, a.rest_box, a.rest_score,
-                                       &c0->n_rest, &a.grid_high, a.rest_of_high, 0.7, e->edgesB,
-                                       e->wsB, e->wsdB, a.x3, a.y3);
     MARK();
-    hipLaunchKernelGGL(k_begin, dim3(a.S), dim3(BLK), 0, e->stream, a);
+    hipLaunchKernelGGL(k_stage1, dim3(a.S), dim3(BLK), a.lds_bytes, e->stream, a);
     YTA_HIP(hipGetLastError());
     MARK();
-    YTA_HIP(launch_edges(s1, a.S, nullptr, 0, a.CAP, e->stream));
-    MARK();
-    YTA_HIP(launch_lap(s1, a.S, nullptr, 0, e->stream));
-    MARK();
-    hipLaunchKernelGGL(k_prep23, dim3(a.S), dim3(BLK), 0, e->stream, a);
+    hipLaunchKernelGGL(k_stage23, dim3(a.S), dim3(BLK), a.lds_bytes, e->stream, a);
     YTA_HIP(hipGetLastError());
-    MARK();
-    YTA_HIP(launch_edges(s2, a.S, &s3, a.S, a.CAP, e->stream));
-    MARK();
-    YTA_HIP(launch_lap(s2, a.S, &s3, a.S, e->stream));
     MARK();
     const dim3 gt((a.CAP + GRID_T - 1) / GRID_T, a.S);
     hipLaunchKernelGGL(k_apply, gt, dim3(GRID_T), 0, e->stream, a);
@@ -751,17 +746,9 @@ int reserve(yta_bytetrack *e, int cap, int maxd) {
     release_buffers(e);
     e->CAP = n->CAP;
     e->MAXD = n->MAXD;
-    e->edge_cap = n->edge_cap;
     e->allocs.swap(n->allocs);
+    n->a.lds_bytes = e->a.lds_bytes;
     e->a = n->a;
-    e->edgesA = n->edgesA;
-    e->edgesB = n->edgesB;
-    e->wsA = n->wsA;
-    e->wsB = n->wsB;
-    e->wsdA = n->wsdA;
-    e->wsdB = n->wsdB;
-    e->ws_i = n->ws_i;
-    e->ws_d = n->ws_d;
     e->h_off = n->h_off;
     e->h_cnt = n->h_cnt;
     e->d_det_off = n->d_det_off;
@@ -824,6 +811,7 @@ int yta_bytetrack_create(int device, int n_streams, int track_capacity, int max_
         return YTA_ERR_HIP;
     }
     rc = bt_alloc(e);
+    if (!rc) rc = set_lds_limits();
     if (!rc) rc = yta_bytetrack_reset(e);
     if (rc) {
         yta_bytetrack_destroy(e);
@@ -1011,8 +999,8 @@ int yta_bytetrack_profile(yta_bytetrack *e, int enable) {
 }
 
 // Per-launch time summed over the frames run since profiling was enabled / last collected:
-// ms[k] for the 8 launches of one frame in order (begin, edges1, lap1, prep23, edges23, lap23,
-// apply, finish); *frames = frames covered.
+// ms[k] for the 4 launches of one frame in order (stage1, stage23, apply, finish); *frames =
+// frames covered.
 int yta_bytetrack_profile_collect(yta_bytetrack *e, double *ms, int *frames) {
     YTA_CHECK(e && ms && frames, YTA_ERR_INVALID, "null argument");
     YTA_HIP(hipStreamSynchronize(e->stream));
@@ -1053,15 +1041,30 @@ int yta_bytetrack_stats(yta_bytetrack *e, long long *stats) {
     YTA_HIP(hipSetDevice(e->device));
     const int rc = read_counters(e);
     if (rc) return rc;
-    for (int k = 0; k < 16; ++k) stats[k] = 0;
+    constexpr int NS = 18;
+    for (int k = 0; k < NS; ++k) stats[k] = 0;
     for (int s = 0; s < e->S; ++s) {
         const BtCounters &c = e->h_cnt[s];
-        const long long v[16] = {c.n_dets, c.n_high, c.n_second, c.n_pool, c.n_act, c.n_unc,
+        const long long v[NS] = {c.n_dets, c.n_high, c.n_second, c.n_pool, c.n_act, c.n_unc,
                                  c.n_left, c.n_rest, c.n_births, c.n_t2, c.n_l2, c.n_tracked,
                                  c.n_lost, c.n_out, (long long)c.n_edges[0],
-                                 (long long)c.n_edges[1] + c.n_edges[2]};
-        for (int k = 0; k < 16; ++k) stats[k] += v[k];
+                                 (long long)c.n_edges[1] + c.n_edges[2], c.n_fallback[0],
+                                 c.n_fallback[1]};
+        for (int k = 0; k < NS; ++k) stats[k] += v[k];
     }
+    return YTA_OK;
+}
+
+int yta_bytetrack_set_lds(yta_bytetrack *e, int bytes) {
+    YTA_CHECK(e, YTA_ERR_INVALID, "null engine");
+    YTA_CHECK(bytes >= 0 && bytes <= 150 * 1024, YTA_ERR_INVALID, "LDS bytes must be in [0, 150 KiB]");
+    YTA_HIP(hipSetDevice(e->device));
+    YTA_HIP(hipStreamSynchronize(e->stream));
+    e->a.lds_bytes = (size_t)bytes & ~(size_t)15;
+    YTA_HIP(hipFuncSetAttribute((const void *)k_stage1, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)std::max<size_t>(e->a.lds_bytes, BT_LDS_BYTES)));
+    YTA_HIP(hipFuncSetAttribute((const void *)k_stage23, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)std::max<size_t>(e->a.lds_bytes, BT_LDS_BYTES)));
     return YTA_OK;
 }
 

@@ -34,7 +34,8 @@ struct BtCounters {                  // one per stream, 128 B
     int n_t2, n_l2, n_out;
     int err;
     int n_edges[3];
-    int pad[9];
+    int n_fallback[2];               // cumulative: association redone over global memory
+    int pad[7];
 };
 static_assert(sizeof(BtCounters) == 128, "BtCounters layout");
 
@@ -61,16 +62,21 @@ struct BtArgs {
     // per-frame: detections [S*MAXD]
     double *det_xyah;         // [S*MAXD][4]
     double *det_conf, *det_cls;
-    int *high, *second, *rest, *birth, *rest_of_high;
-    Box *high_box, *second_box, *rest_box;
+    int *high, *second, *rest, *birth;
+    Box *high_box, *second_box;
     double *high_score, *rest_score;
-    BtGrid grid_high, grid_second, grid_lost;
+    BtGrid grid_lost;
     // per-frame: tracks [S*CAP]
     int *pool, *unc, *left, *left_of_pool, *t2, *l2, *kind1, *dropA, *dropB;
-    Box *pool_box, *unc_box, *left_box, *tbox, *lbox;
+    Box *pool_box, *unc_box, *tbox, *lbox;
     int *tage, *lage;
     // association results
     int *x1, *y1, *x2, *y2, *x3, *y3;   // x*: [S*CAP], y*: [S*MAXD]
+    // association workspace: LDS arena size, per-stream global fallback arena, solver slabs
+    size_t lds_bytes;
+    unsigned char *ws;
+    long long ws_stride;
+    LapSlab slab;             // per stream: (threads / 64) slabs
     // outputs
     double *out;              // [S*CAP][8]
     int *out_counts;          // optional [S]

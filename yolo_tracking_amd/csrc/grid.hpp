@@ -16,10 +16,11 @@
 #pragma once
 #include "common.hpp"
 #include "geometry.hpp"
+#include "lap.hpp"
 
 namespace yta {
 
-constexpr int GRID_MAX_CELLS = 4096;
+constexpr int GRID_MAX_CELLS = 2048;
 
 struct GridHdr {
     double ox, oy, inv_g, maxw, maxh, g;
@@ -47,142 +48,128 @@ __device__ __forceinline__ int grid_cell_1d(double x, double o, double inv_g, in
 }
 
 struct GridScratch {
-    int cnt[GRID_MAX_CELLS + 1];
     double red[8 * 16];
     GridHdr hdr;
 };
 
-// Block-wide min/max/sum of up to 6 values (per-wave partials through `red`).
-__device__ __forceinline__ void block_reduce6(double v[6], const bool is_min[6], double *red) {
+// Block-wide reduction of 6 values; op[k]: 0 = min, 1 = max, 2 = sum (per-wave partials in `red`).
+__device__ __forceinline__ void block_reduce6(double v[6], const int op[6], double *red) {
+    auto comb = [&](int k, double a, double b) {
+        return op[k] == 0 ? fmin(a, b) : (op[k] == 1 ? fmax(a, b) : a + b);
+    };
     for (int off = 32; off > 0; off >>= 1)
-        for (int k = 0; k < 6; ++k) {
-            const double o = __shfl_xor(v[k], off);
-            v[k] = is_min[k] == true ? fmin(v[k], o) : (k < 4 ? fmax(v[k], o) : v[k] + o);
-        }
+        for (int k = 0; k < 6; ++k) v[k] = comb(k, v[k], __shfl_xor(v[k], off));
     const int wv = threadIdx.x / WAVE, nw = (blockDim.x + WAVE - 1) / WAVE;
     if (lane_id() == 0)
         for (int k = 0; k < 6; ++k) red[8 * wv + k] = v[k];
     block_sync();
     for (int k = 0; k < 6; ++k) {
         double a = red[k];
-        for (int w = 1; w < nw; ++w) {
-            const double o = red[8 * w + k];
-            a = is_min[k] ? fmin(a, o) : (k < 4 ? fmax(a, o) : a + o);
-        }
+        for (int w = 1; w < nw; ++w) a = comb(k, a, red[8 * w + k]);
         v[k] = a;
     }
     block_sync();
 }
 
 // Block-wide build (every thread of the block calls it).  box(i) returns item i's box.
+// gv.cell_start needs GRID_MAX_CELLS + 1 entries, gv.ids / gv.boxes / gv.big n entries.
 template <typename BoxOf>
 __device__ void grid_build(int n, BoxOf box, GridView gv, GridScratch &gs, int *wsum) {
     const int t = threadIdx.x, nt = blockDim.x;
     // pass 1: mean size of the usable boxes
     double v[6] = {0, 0, 0, 0, 0, 0};
-    const bool sum6[6] = {false, false, false, false, false, false};
+    const int sums[6] = {2, 2, 2, 2, 2, 2};
     for (int i = t; i < n; i += nt) {
         const Box b = box(i);
         if (!box_usable(b)) continue;
         v[4] += fmax(b.x2 - b.x1, b.y2 - b.y1);
         v[5] += 1.0;
     }
-    block_reduce6(v, sum6, gs.red);
+    block_reduce6(v, sums, gs.red);
     const double nb = v[5];
     const double mean = nb > 0 ? v[4] / nb : 1.0;
     const double bthr = 4.0 * mean;
+    auto binned = [&](const Box &b) {
+        return box_usable(b) && !(b.x2 - b.x1 > bthr) && !(b.y2 - b.y1 > bthr);
+    };
     // pass 2: extent of the binned top-left corners and their maximum width / height
-    double e[6] = {INFINITY, INFINITY, -INFINITY, -INFINITY, 0.0, 0.0};
-    const bool mins[6] = {true, true, false, false, false, false};
+    double e[6] = {INFINITY, INFINITY, -INFINITY, -INFINITY, -INFINITY, -INFINITY};
+    const int ops[6] = {0, 0, 1, 1, 1, 1};
     for (int i = t; i < n; i += nt) {
         const Box b = box(i);
-        if (!box_usable(b) || b.x2 - b.x1 > bthr || b.y2 - b.y1 > bthr) continue;
+        if (!binned(b)) continue;
         e[0] = fmin(e[0], b.x1);
         e[1] = fmin(e[1], b.y1);
-        e[2] = fmax(e[2], b.x2 - b.x1);   // max width  (slot 2, max)
-        e[3] = fmax(e[3], b.y2 - b.y1);   // max height (slot 3, max)
-        e[4] += 0.0;
-        e[5] += 0.0;
+        e[2] = fmax(e[2], b.x1);
+        e[3] = fmax(e[3], b.y1);
+        e[4] = fmax(e[4], b.x2 - b.x1);
+        e[5] = fmax(e[5], b.y2 - b.y1);
     }
-    block_reduce6(e, mins, gs.red);
-    double f[6] = {-INFINITY, -INFINITY, 0, 0, 0, 0};
-    const bool maxs[6] = {false, false, false, false, false, false};
-    for (int i = t; i < n; i += nt) {
-        const Box b = box(i);
-        if (!box_usable(b) || b.x2 - b.x1 > bthr || b.y2 - b.y1 > bthr) continue;
-        f[0] = fmax(f[0], b.x1);
-        f[1] = fmax(f[1], b.y1);
-    }
-    block_reduce6(f, maxs, gs.red);
-    if (t == 0) {
-        GridHdr h;
-        h.maxw = e[2] > 0 ? e[2] : 0.0;
-        h.maxh = e[3] > 0 ? e[3] : 0.0;
-        if (!(f[0] >= e[0])) {   // nothing to bin
-            h.ox = h.oy = 0.0;
-            h.g = 1.0;
-            h.inv_g = 1.0;
-            h.gx = h.gy = 1;
-        } else {
-            double g = mean;
-            const double ex = f[0] - e[0], ey = f[1] - e[1];
-            double gxf = floor(ex / g) + 1.0, gyf = floor(ey / g) + 1.0;
-            while (gxf * gyf > (double)GRID_MAX_CELLS) {
-                g *= 1.25;
-                gxf = floor(ex / g) + 1.0;
-                gyf = floor(ey / g) + 1.0;
-            }
-            h.ox = e[0];
-            h.oy = e[1];
-            h.g = g;
-            h.inv_g = 1.0 / g;
-            h.gx = (int)gxf;
-            h.gy = (int)gyf;
+    block_reduce6(e, ops, gs.red);
+    GridHdr h;
+    h.maxw = e[4] > 0 ? e[4] : 0.0;
+    h.maxh = e[5] > 0 ? e[5] : 0.0;
+    if (!(e[2] >= e[0])) {   // nothing to bin
+        h.ox = h.oy = 0.0;
+        h.g = 1.0;
+        h.inv_g = 1.0;
+        h.gx = h.gy = 1;
+    } else {
+        double g = mean;
+        const double ex = e[2] - e[0], ey = e[3] - e[1];
+        double gxf = floor(ex / g) + 1.0, gyf = floor(ey / g) + 1.0;
+        while (gxf * gyf > (double)GRID_MAX_CELLS) {
+            g *= 1.25;
+            gxf = floor(ex / g) + 1.0;
+            gyf = floor(ey / g) + 1.0;
         }
-        h.n_big = 0;
-        h.n_binned = 0;
-        gs.hdr = h;
+        h.ox = e[0];
+        h.oy = e[1];
+        h.g = g;
+        h.inv_g = 1.0 / g;
+        h.gx = (int)gxf;
+        h.gy = (int)gyf;
     }
-    for (int c = t; c <= GRID_MAX_CELLS; c += nt) gs.cnt[c] = 0;
-    block_sync();
-    const GridHdr h = gs.hdr;
+    h.n_big = 0;
+    h.n_binned = 0;
+    if (t == 0) gs.hdr = h;
     const int ncell = h.gx * h.gy;
+    int *cs = gv.cell_start;
+    for (int c = t; c <= ncell; c += nt) cs[c] = 0;
+    block_sync();
+    auto cell_of = [&](const Box &b) {
+        return grid_cell_1d(b.y1, h.oy, h.inv_g, h.gy) * h.gx + grid_cell_1d(b.x1, h.ox, h.inv_g, h.gx);
+    };
+    // counts land in cs[c + 1]; the exclusive scan leaves start(c) there, and the scatter's cursor
+    // increments turn it into end(c) = start(c + 1), so cs[c] = start(c) afterwards
     for (int i = t; i < n; i += nt) {
         const Box b = box(i);
         if (!box_usable(b)) continue;
-        if (b.x2 - b.x1 > bthr || b.y2 - b.y1 > bthr) {
+        if (!binned(b)) {
             gv.big[atomicAdd(&gs.hdr.n_big, 1)] = i;
             continue;
         }
-        const int c = grid_cell_1d(b.y1, h.oy, h.inv_g, h.gy) * h.gx +
-                      grid_cell_1d(b.x1, h.ox, h.inv_g, h.gx);
-        atomicAdd(&gs.cnt[c], 1);
+        atomicAdd(&cs[cell_of(b) + 1], 1);
     }
     block_sync();
     int run = 0;
     for (int start = 0; start < ncell; start += nt) {
         const int c = start + t;
-        const int cv = c < ncell ? gs.cnt[c] : 0;
+        const int cv = c < ncell ? ald(cs + c + 1) : 0;
         int tot;
         const int pos = block_exclusive_scan(cv, wsum, &tot);
-        if (c < ncell) {
-            gv.cell_start[c] = run + pos;
-            gs.cnt[c] = run + pos;
-        }
+        if (c < ncell) cs[c + 1] = run + pos;
         run += tot;
     }
     if (t == 0) {
-        gv.cell_start[ncell] = run;
         gs.hdr.n_binned = run;
-        *gv.hdr = gs.hdr;
+        if (gv.hdr) *gv.hdr = gs.hdr;
     }
     block_sync();
     for (int i = t; i < n; i += nt) {
         const Box b = box(i);
-        if (!box_usable(b) || b.x2 - b.x1 > bthr || b.y2 - b.y1 > bthr) continue;
-        const int c = grid_cell_1d(b.y1, h.oy, h.inv_g, h.gy) * h.gx +
-                      grid_cell_1d(b.x1, h.ox, h.inv_g, h.gx);
-        const int pos = atomicAdd(&gs.cnt[c], 1);
+        if (!binned(b)) continue;
+        const int pos = atomicAdd(&cs[cell_of(b) + 1], 1);
         gv.ids[pos] = i;
         gv.boxes[pos] = b;
     }
@@ -206,7 +193,7 @@ __device__ __forceinline__ void grid_query(const GridView &gv, const GridHdr &h,
     const int cy1 = fy1 > (double)(h.gy - 1) ? h.gy - 1 : (int)fy1;
     for (int cy = cy0; cy <= cy1; ++cy) {
         const int base = cy * h.gx;
-        const int b = gv.cell_start[base + cx0], e = gv.cell_start[base + cx1 + 1];
+        const int b = ald(gv.cell_start + base + cx0), e = ald(gv.cell_start + base + cx1 + 1);
         for (int k = b; k < e; ++k) visit(gv.ids[k], gv.boxes[k]);   // cells of a row are contiguous
     }
 }

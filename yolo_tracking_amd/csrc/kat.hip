@@ -54,20 +54,62 @@ __global__ void k_kf(int op, int n, const double *in_vec, double *mean, double *
     kf_cov_full(s, cov + 64 * i);
 }
 
-// cost matrix -> Box-free edge pool for the sparse solver (KAT path only)
-__global__ void k_dense_edges(const double *cost, int nr, int nc, double thresh, Edge *edges,
-                              int *n_edges) {
-    const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= (long long)nr * nc) return;
-    const double c = cost[idx];
-    if (c < thresh) {
-        int pos = atomicAdd(n_edges, 1);
-        Edge e;
-        e.row = (int)(idx / nc);
-        e.col = (int)(idx % nc);
-        e.cost = c;
-        edges[pos] = e;
+// Dense cost matrix -> CSR of the entries below the limit -> lap_block (one block).  LDS arena
+// first, the global one if the problem does not fit (the KAT suite exercises both).
+__device__ __forceinline__ bool lap_dense_body(const double *cost, int nr, int nc, double thresh,
+                                               int *X, int *Y, int *err, Arena &ar,
+                                               const LapSlab &slab, LapShared &sh) {
+    const int t = threadIdx.x, nt = blockDim.x;
+    int *row_off = ar.alloc_top<int>(nr + 1);
+    int *col_deg = ar.alloc_top<int>(nc);
+    if (ar.fail) return false;
+    for (int j = t; j < nc; j += nt) col_deg[j] = 0;
+    int run = 0;
+    for (int start = 0; start < nr; start += nt) {
+        const int i = start + t;
+        int cnt = 0;
+        if (i < nr)
+            for (int j = 0; j < nc; ++j) cnt += cost[(long long)i * nc + j] < thresh;
+        int tot;
+        const int pos = block_exclusive_scan(cnt, sh.wsum, &tot);
+        if (i < nr) row_off[i] = run + pos;
+        run += tot;
     }
+    if (t == 0) row_off[nr] = run;
+    int *csr_col = ar.alloc_top<int>(run);
+    double *csr_cost = ar.alloc_top<double>(run);
+    if (ar.fail) return false;
+    block_sync();
+    for (int i = t; i < nr; i += nt) {
+        int k = row_off[i];
+        for (int j = 0; j < nc; ++j) {
+            const double c = cost[(long long)i * nc + j];
+            if (c < thresh) {
+                csr_col[k] = j;
+                csr_cost[k] = c;
+                ++k;
+                atomicAdd(&col_deg[j], 1);
+            }
+        }
+    }
+    block_sync();
+    return lap_block(nr, nc, row_off, csr_col, csr_cost, col_deg, thresh, X, Y, err, ar, slab, sh);
+}
+
+__global__ __launch_bounds__(1024) void k_lap_dense(const double *cost, int nr, int nc,
+                                                    double thresh, int *X, int *Y, int *err,
+                                                    size_t lds_bytes, unsigned char *ws,
+                                                    size_t ws_bytes, LapSlab slab) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    __shared__ LapShared sh;
+    {
+        Arena ar(smem, lds_bytes);
+        if (lap_dense_body(cost, nr, nc, thresh, X, Y, err, ar, slab, sh)) return;
+    }
+    block_sync();
+    Arena ag(ws, ws_bytes);
+    if (!lap_dense_body(cost, nr, nc, thresh, X, Y, err, ag, slab, sh) && threadIdx.x == 0)
+        atomicOr(err, ERR_EDGE_OVERFLOW);
 }
 
 // One block: grid over b, then every a-box queries it; pairs with 1 - IoU < thresh are written
@@ -241,51 +283,46 @@ int yta_lap_limited(int device, int nr, int nc, const double *cost, double cost_
                     int *y) {
     YTA_CHECK(nr >= 0 && nc >= 0, YTA_ERR_INVALID, "negative size");
     YTA_CHECK(cost_limit == cost_limit, YTA_ERR_INVALID, "cost_limit is NaN");
+    YTA_CHECK((nr == 0 || x) && (nc == 0 || y), YTA_ERR_INVALID, "null buffer");
     for (int i = 0; i < nr; ++i) x[i] = -1;
     for (int j = 0; j < nc; ++j) y[j] = -1;
     if ((long long)nr * nc == 0) return YTA_OK;
-    YTA_CHECK(cost && x && y, YTA_ERR_INVALID, "null buffer");
+    YTA_CHECK(cost, YTA_ERR_INVALID, "null buffer");
     int rc = select_device(device);
     if (rc) return rc;
     DevBuf m;
     const long long n = (long long)nr * nc;
-    double *dcost, *wsd;
-    Edge *edges;
-    int *ws, *dx, *dy, *cnt;   // cnt: [rows, cols, n_edges, err]
-    const long long E = n;
-    const long long wsi = lap_ws_ints(nr, nc, E), wsdn = lap_ws_doubles(nr, nc, E);
+    constexpr int THREADS = 1024, WAVES = THREADS / WAVE;
+    constexpr size_t LDS = 64 * 1024;
+    double *dcost;
+    int *dx, *dy, *derr;
+    unsigned char *ws;
+    LapSlab slab;
+    const size_t ws_bytes = (size_t)(((4LL * (nr + 1) + 4LL * nc + 12 * n) +
+                                      4LL * 8 * (nr + nc + 1) + 64 * 16 + 255) & ~255LL);
+    slab.R = nr;
+    slab.C = nc;
+    slab.i_stride = lap_slab_ints(nr, nc);
+    slab.d_stride = lap_slab_doubles(nr, nc);
     YTA_HIP(m.get(&dcost, n));
-    YTA_HIP(m.get(&edges, E));
-    YTA_HIP(m.get(&ws, wsi));
-    YTA_HIP(m.get(&wsd, wsdn));
     YTA_HIP(m.get(&dx, nr));
     YTA_HIP(m.get(&dy, nc));
-    YTA_HIP(m.get(&cnt, 4));
-    int h_cnt[4] = {nr, nc, 0, 0};
-    YTA_HIP(hipMemcpy(cnt, h_cnt, sizeof(h_cnt), hipMemcpyHostToDevice));
+    YTA_HIP(m.get(&derr, 1));
+    YTA_HIP(m.get(&ws, ws_bytes));
+    YTA_HIP(m.get(&slab.i, WAVES * slab.i_stride));
+    YTA_HIP(m.get(&slab.d, WAVES * slab.d_stride));
+    YTA_HIP(hipMemset(derr, 0, sizeof(int)));
     YTA_HIP(hipMemcpy(dcost, cost, sizeof(double) * n, hipMemcpyHostToDevice));
-    hipLaunchKernelGGL(k_dense_edges, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, 0, dcost, nr,
-                       nc, cost_limit, edges, cnt + 2);
+    YTA_HIP(hipFuncSetAttribute((const void *)k_lap_dense,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS));
+    hipLaunchKernelGGL(k_lap_dense, dim3(1), dim3(THREADS), LDS, 0, dcost, nr, nc, cost_limit, dx,
+                       dy, derr, LDS, ws, ws_bytes, slab);
     YTA_HIP(hipGetLastError());
-    ProblemSet ps{};
-    ps.n_rows = cnt;
-    ps.n_cols = cnt + 1;
-    ps.thresh = cost_limit;
-    ps.edges = edges;
-    ps.edge_cap = E;
-    ps.n_edges = cnt + 2;
-    ps.err = cnt + 3;
-    ps.ws = ws;
-    ps.wsd = wsd;
-    ps.max_rows = nr;
-    ps.max_cols = nc;
-    ps.x = dx;
-    ps.y = dy;
-    YTA_HIP(launch_lap(ps, 1, nullptr, 0, 0));
+    int herr = 0;
     YTA_HIP(hipMemcpy(x, dx, sizeof(int) * nr, hipMemcpyDeviceToHost));
     YTA_HIP(hipMemcpy(y, dy, sizeof(int) * nc, hipMemcpyDeviceToHost));
-    YTA_HIP(hipMemcpy(h_cnt, cnt, sizeof(h_cnt), hipMemcpyDeviceToHost));
-    YTA_CHECK(h_cnt[3] == 0, YTA_ERR_HIP, "assignment solver error flags 0x%x", h_cnt[3]);
+    YTA_HIP(hipMemcpy(&herr, derr, sizeof(int), hipMemcpyDeviceToHost));
+    YTA_CHECK(herr == 0, YTA_ERR_HIP, "assignment solver error flags 0x%x", herr);
     return YTA_OK;
 }
 

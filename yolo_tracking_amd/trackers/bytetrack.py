@@ -57,6 +57,18 @@ class ByteTrackEngine:
     def reserve(self, track_capacity, max_dets):
         _lib.check(self.lib.yta_bytetrack_reserve(self._h, int(track_capacity), int(max_dets)))
 
+    def set_lds(self, nbytes):
+        """LDS bytes per stream for the association kernels (0: always over global memory)."""
+        _lib.check(self.lib.yta_bytetrack_set_lds(self._h, int(nbytes)))
+
+    def stats(self):
+        """Last frame's counts summed over streams (see yta_bytetrack_stats)."""
+        names = ["dets", "high", "second", "pool", "act", "unc", "left", "rest", "births", "t2",
+                 "l2", "tracked", "lost", "out", "edges1", "edges23", "fallback1", "fallback23"]
+        buf = (ctypes.c_longlong * len(names))()
+        _lib.check(self.lib.yta_bytetrack_stats(self._h, buf))
+        return {k: int(buf[i]) for i, k in enumerate(names)}
+
     def update(self, dets_per_stream, next_id=None):
         """dets_per_stream: list of S float64 (M_s, 6) arrays.  next_id: optional int64 (S,) array
         of last-issued IDs, updated in place.  Returns a list of S (K_s, 8) arrays."""
