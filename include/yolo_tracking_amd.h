@@ -62,6 +62,10 @@ int yta_kf_xyah_initiate(int device, int n, const double *meas, double *mean, do
 int yta_kf_xyah_predict(int device, int n, double *mean, double *cov);
 int yta_kf_xyah_update(int device, int n, double *mean, double *cov, const double *z);
 
+/* Device self-test of the block-wide scan / reduction primitives the kernels are built on (DPP
+ * cross-lane operations) at several block sizes.  0 when every result matches a serial answer. */
+int yta_selftest(int device);
+
 /* ---- linear assignment with lapx cost_limit semantics -------------------------------------
  * Minimises sum(matched cost) + cost_limit/2 * (#unmatched rows + #unmatched cols); x[r] = col or
  * -1, y[c] = row or -1 (lap.lapjv(cost, extend_cost=True, cost_limit=cost_limit)). */
@@ -129,7 +133,7 @@ int yta_bytetrack_debug_dedup(yta_bytetrack *engine, int stream, int *n_t2, int 
  * candidate edges, stage-2+3 candidate edges, then the cumulative number of stream-frames whose
  * stage-1 / stage-2+3 association did not fit in LDS and ran over global memory (18 int64). */
 int yta_bytetrack_stats(yta_bytetrack *engine, long long *stats);
-/* Tuning / testing: bytes of LDS the association kernels may use per stream (default 72 KiB,
+/* Tuning / testing: bytes of LDS the association kernels may use per stream (default 150 KiB,
  * at most 150 KiB); a stream-frame that does not fit runs over global memory.  0 forces the
  * global-memory path for every stream. */
 int yta_bytetrack_set_lds(yta_bytetrack *engine, int bytes);

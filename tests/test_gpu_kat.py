@@ -135,3 +135,9 @@ def test_grid_pairs_mot17_dedup_case():
     T = np.array([[548.52661677, 460.85409296, 572.20069217, 518.92964587]])
     got = _lib.grid_pairs(T, L, 0.15)
     assert np.array_equal(got, _brute_pairs(T, L, 0.15)) and len(got) == 1
+
+
+def test_block_primitives_selftest():
+    """DPP wave scans / row and wave reductions behind every block-wide scan and reduction."""
+    lib = _lib.load_library()
+    _lib.check(lib.yta_selftest(0))

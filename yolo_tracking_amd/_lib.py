@@ -10,7 +10,8 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libyta.so")
+# YTA_LIBRARY: an alternative build of the same library (tuning experiments, tools/)
+LIB_PATH = os.environ.get("YTA_LIBRARY") or os.path.join(_HERE, "libyta.so")
 
 YTA_OK = 0
 YTA_ERR_INVALID = -1
@@ -68,6 +69,7 @@ _SIGS = {
     "yta_bytetrack_stats": ([_P, _P], _I),
     "yta_bytetrack_hip_stream": ([_P, _P], _I),
     "yta_bytetrack_set_lds": ([_P, _I], _I),
+    "yta_selftest": ([_I], _I),
 }
 
 EXPORTED_SYMBOLS = tuple(_SIGS)

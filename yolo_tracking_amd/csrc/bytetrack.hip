@@ -31,9 +31,21 @@
 namespace yta {
 namespace {
 
-constexpr int BLK = 1024;    // block/stream kernels
-constexpr int BLK_WAVES = BLK / WAVE;
-constexpr int GRID_T = 256;  // grid kernels
+// Threads per block of the block/stream kernels.  k_stage1 is one long latency-bound chain per
+// stream: the widest block shortens it.  k_stage23 (small problems) and k_finish run better as
+// several narrower blocks per CU.
+#ifndef YTA_BLK1
+#define YTA_BLK1 1024
+#endif
+#ifndef YTA_BLK23
+#define YTA_BLK23 256
+#endif
+#ifndef YTA_BLKF
+#define YTA_BLKF 256
+#endif
+constexpr int BLK1 = YTA_BLK1, BLK23 = YTA_BLK23, BLKF = YTA_BLKF;
+constexpr int BLK_MAX = 1024;
+constexpr int SLAB_WAVES = BLK_MAX / WAVE;   // solver slabs per stream (any block size)
 
 __device__ __forceinline__ void load_kf(const double *kf, long long slot, KfState &s) {
     const double2 *src = reinterpret_cast<const double2 *>(kf + slot * KF_REC);
@@ -65,7 +77,7 @@ __device__ __forceinline__ int st_of(int flags) { return flags & FL_STATE; }
 
 __device__ __forceinline__ GridView grid_of(const BtGrid &g, int s) {
     return GridView{g.hdr + s, g.cell + (long long)s * (GRID_MAX_CELLS + 1), g.items + s * g.cap,
-                    g.boxes + s * g.cap, g.big + s * g.cap};
+                    g.boxes + s * g.cap, g.fbox + s * g.cap, nullptr, g.big + s * g.cap};
 }
 
 // ------------------------------------------------------------------------------------ k_stage1
@@ -76,9 +88,8 @@ __device__ __forceinline__ GridView grid_of(const BtGrid &g, int s) {
 // (:181-183), lapjv with cost_limit = match_thresh (:184-186).
 __device__ __forceinline__ LapSlab slab_of(const BtArgs &a, int s) {
     LapSlab l = a.slab;
-    const int nw = blockDim.x / WAVE;
-    l.i += (long long)s * nw * l.i_stride;
-    l.d += (long long)s * nw * l.d_stride;
+    l.i += (long long)s * SLAB_WAVES * l.i_stride;
+    l.d += (long long)s * SLAB_WAVES * l.d_stride;
     return l;
 }
 
@@ -107,6 +118,7 @@ __device__ __forceinline__ bool stage1_body(const BtArgs &a, int s, Arena &ar, S
         a.det_cls[db + i] = d[5];
     }
     block_sync();
+    YTA_STAMP(1);
     const double *conf = a.det_conf + db;
     auto det_box = [&](int i) {                          // STrack.xyxy with mean None (:105-106)
         const double *d = din + (long long)i * 6;
@@ -126,6 +138,7 @@ __device__ __forceinline__ bool stage1_body(const BtArgs &a, int s, Arena &ar, S
                                            a.second[db + pos] = i;
                                            a.second_box[db + pos] = det_box(i);
                                        });
+    YTA_STAMP(2);
     const int n_tracked = c->n_tracked, n_lost = c->n_lost;
     const int *tracked = a.tracked + tb;
     const int n_act = block_compact(
@@ -136,6 +149,7 @@ __device__ __forceinline__ bool stage1_body(const BtArgs &a, int s, Arena &ar, S
         [&](int i, int pos) { a.unc[tb + pos] = tracked[i]; });
     for (int i = t; i < n_lost; i += nt) a.pool[tb + n_act + i] = a.lost[tb + i];
     block_sync();
+    YTA_STAMP(3);
     const int n_pool = n_act + n_lost;
     for (int i = t; i < n_pool; i += nt) {
         const long long slot = tb + a.pool[tb + i];
@@ -145,6 +159,7 @@ __device__ __forceinline__ bool stage1_body(const BtArgs &a, int s, Arena &ar, S
     }
     for (int j = t; j < n_unc; j += nt) a.unc_box[tb + j] = kf_box(a.kf, tb + a.unc[tb + j]);
     block_sync();
+    YTA_STAMP(4);
     const bool ok = assoc_block(
         n_pool, [&](int i) { return a.pool_box[tb + i]; }, n_high,
         [&](int j) { return a.high_box[db + j]; }, true,
@@ -193,6 +208,7 @@ __device__ __forceinline__ bool stage23_body(const BtArgs &a, int s, Arena &ar, 
                                          a.rest_score[db + pos] = a.high_score[db + h];
                                      });
     block_sync();
+    YTA_STAMP(4);
     const LapSlab slab = slab_of(a, s);
     bool ok = assoc_block(
         n_left, [&](int k) { return a.pool_box[tb + a.left[tb + k]]; }, n_second,
@@ -200,6 +216,7 @@ __device__ __forceinline__ bool stage23_body(const BtArgs &a, int s, Arena &ar, 
         a.x2 + tb, a.y2 + db, &c->err, &c->n_edges[1], ar, slab, sh.as);
     if (!ok) return false;
     ar.reset();
+    YTA_STAMP_BASE(40);
     ok = assoc_block(
         n_unc, [&](int j) { return a.unc_box[tb + j]; }, n_rest,
         [&](int r) { return a.high_box[db + a.rest[db + r]]; }, true,
@@ -216,10 +233,12 @@ __device__ __forceinline__ bool stage23_body(const BtArgs &a, int s, Arena &ar, 
 // LDS first; a frame whose association does not fit is redone over the stream's global arena
 // (both bodies only write values that the redo rewrites identically, and bump the frame counter
 // only on success).
-__global__ __launch_bounds__(BLK) void k_stage1(BtArgs a) {
+__global__ __launch_bounds__(BLK1) void k_stage1(BtArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     __shared__ StageShared sh;
     const int s = blockIdx.x;
+    YTA_STAMP_BASE(0);
+    YTA_STAMP(0);
     {
         Arena ar(smem, a.lds_bytes);
         if (stage1_body(a, s, ar, sh)) return;
@@ -230,12 +249,14 @@ __global__ __launch_bounds__(BLK) void k_stage1(BtArgs a) {
     if (!stage1_body(a, s, ag, sh) && threadIdx.x == 0) atomicOr(&a.cnt[s].err, ERR_EDGE_OVERFLOW);
 }
 
-__global__ __launch_bounds__(BLK) void k_stage23(BtArgs a) {
+__global__ __launch_bounds__(BLK23) void k_stage23(BtArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     __shared__ StageShared sh;
     const int s = blockIdx.x;
+    YTA_STAMP_BASE(20);
+    YTA_STAMP(0);
     {
-        Arena ar(smem, a.lds_bytes);
+        Arena ar(smem, a.lds_bytes23);
         if (stage23_body(a, s, ar, sh)) return;
     }
     block_sync();
@@ -257,61 +278,133 @@ __device__ __forceinline__ void take_detection(const BtArgs &a, KfState &st, Tra
     m.det_ind = det_local;
 }
 
-__global__ __launch_bounds__(GRID_T) void k_apply(BtArgs a) {
-    const int s = blockIdx.y;
-    const int i = blockIdx.x * GRID_T + threadIdx.x;
+// Records move between HBM and LDS in whole 16-B pieces with consecutive lanes on consecutive
+// pieces of a record (full-line reads and writes); each thread then runs the Kalman step of one
+// track out of LDS.  Piece p < 12 is the Kalman record, 12..14 the 48-B meta.
+constexpr int APPLY_T = 128;              // tracks (= threads) per block
+constexpr int REC_PIECES = KF_REC / 2 + 3;
+
+__global__ __launch_bounds__(APPLY_T) void k_apply(BtArgs a) {
+    __shared__ double2 rec[APPLY_T][REC_PIECES];
+    __shared__ int s_slot[APPLY_T];
+    __shared__ int s_wmask[APPLY_T];      // bit 0: write the Kalman record, bit 1: write the meta
+    const int s = blockIdx.y, t = threadIdx.x;
     const BtCounters *c = a.cnt + s;
     const int n_pool = c->n_pool, n_unc = c->n_unc, fid = c->frame_id;
+    const int i0 = blockIdx.x * APPLY_T;
+    const int n_items = n_pool + n_unc;
+    if (i0 >= n_items) return;                                       // block-uniform
+    const int nloc = n_items - i0 < APPLY_T ? n_items - i0 : APPLY_T;
     const long long tb = (long long)s * a.CAP, db = (long long)s * a.MAXD;
-    if (i < n_pool) {
-        const long long slot = tb + a.pool[tb + i];
-        KfState st;
-        load_kf(a.kf, slot, st);
-        TrackMeta m = a.meta[slot];
-        const bool tracked = st_of(m.flags) == ST_TRACKED;
-        if (!tracked) st.m[7] = 0;                                   // :41-42
-        kf_predict(st);
-        int kind = 0;
-        const int h = a.x1[tb + i];
-        if (h >= 0) {                                                // stage 1 (:188-196)
-            kind = tracked ? 1 : 2;
-            const int d = a.high[db + h];
-            take_detection(a, st, m, db + d, d, fid);
-        } else {
-            const int L = a.left_of_pool[tb + i];
-            if (L >= 0) {
-                const int q = a.x2[tb + L];
-                if (q >= 0) {                                        // stage 2 (:212-220)
-                    const int d = a.second[db + q];
-                    take_detection(a, st, m, db + d, d, fid);
-                } else {
-                    m.flags = (m.flags & ~FL_STATE) | ST_LOST;       // mark_lost (:222-226)
+    const int i = i0 + t;
+    // per-track decision (small loads only)
+    // act: 0 predict only, 1 predict + stage-1 update, 2 predict + stage-2 update, 3 predict +
+    // mark lost, 4 update (unconfirmed, stage 3), 5 remove (unconfirmed)
+    int slot = -1, det = -1, act = 0;
+    if (t < nloc) {
+        if (i < n_pool) {
+            slot = a.pool[tb + i];
+            const int h = a.x1[tb + i];
+            if (h >= 0) {                                            // stage 1 (:188-196)
+                act = 1;
+                det = a.high[db + h];
+            } else {
+                const int L = a.left_of_pool[tb + i];
+                if (L >= 0) {
+                    const int q = a.x2[tb + L];
+                    if (q >= 0) {                                    // stage 2 (:212-220)
+                        act = 2;
+                        det = a.second[db + q];
+                    } else {
+                        act = 3;                                     // mark_lost (:222-226)
+                    }
                 }
             }
-        }
-        store_kf(a.kf, slot, st);
-        a.meta[slot] = m;
-        a.kind1[tb + i] = kind;
-    } else if (i < n_pool + n_unc) {
-        const int j = i - n_pool;
-        const long long slot = tb + a.unc[tb + j];
-        TrackMeta m = a.meta[slot];
-        const int r = a.x3[tb + j];
-        if (r >= 0) {                                                // stage 3 (:234-236)
-            KfState st;
-            load_kf(a.kf, slot, st);
-            const int d = a.high[db + a.rest[db + r]];
-            take_detection(a, st, m, db + d, d, fid);
-            store_kf(a.kf, slot, st);
         } else {
-            m.flags = (m.flags & ~FL_STATE) | ST_REMOVED | FL_REMOVED_NOW;   // :237-240
+            const int j = i - n_pool;
+            slot = a.unc[tb + j];
+            const int r = a.x3[tb + j];
+            if (r >= 0) {                                            // stage 3 (:234-236)
+                act = 4;
+                det = a.high[db + a.rest[db + r]];
+            } else {
+                act = 5;                                             // :237-240
+            }
         }
-        a.meta[slot] = m;
+        s_slot[t] = slot;
+    }
+    __syncthreads();
+    // cooperative load
+    const double2 *kf2 = reinterpret_cast<const double2 *>(a.kf);
+    const double2 *meta2 = reinterpret_cast<const double2 *>(a.meta);
+    for (int p = t; p < nloc * REC_PIECES; p += APPLY_T) {
+        const int r = p / REC_PIECES, k = p - r * REC_PIECES;
+        const long long sl = tb + s_slot[r];
+        rec[r][k] = k < 12 ? kf2[sl * 12 + k] : meta2[sl * 3 + (k - 12)];
+    }
+    __syncthreads();
+    if (t < nloc) {
+        KfState st;
+        double *row = reinterpret_cast<double *>(rec[t]);
+        TrackMeta m;
+        memcpy(&m, row + KF_REC, sizeof(TrackMeta));
+        int wmask = 0;
+        if (act <= 3) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) st.m[k] = row[k];
+#pragma unroll
+            for (int k = 0; k < 16; ++k) st.c[k] = row[8 + k];
+            const bool tracked = st_of(m.flags) == ST_TRACKED;
+            if (!tracked) st.m[7] = 0;                               // :41-42
+            kf_predict(st);
+            wmask = 1;
+            if (act == 1 || act == 2) {
+                take_detection(a, st, m, db + det, det, fid);
+                wmask = 3;
+            } else if (act == 3) {
+                m.flags = (m.flags & ~FL_STATE) | ST_LOST;
+                wmask = 3;
+            }
+            // stage-1 outcome for the tracked' list order: 1 tracked -> updated, 2 re-found
+            a.kind1[tb + i] = act == 1 ? (tracked ? 1 : 2) : 0;
+        } else if (act == 4) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) st.m[k] = row[k];
+#pragma unroll
+            for (int k = 0; k < 16; ++k) st.c[k] = row[8 + k];
+            take_detection(a, st, m, db + det, det, fid);
+            wmask = 3;
+        } else {
+            m.flags = (m.flags & ~FL_STATE) | ST_REMOVED | FL_REMOVED_NOW;
+            wmask = 2;
+        }
+        if (wmask & 1) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) row[k] = st.m[k];
+#pragma unroll
+            for (int k = 0; k < 16; ++k) row[8 + k] = st.c[k];
+        }
+        if (wmask & 2) memcpy(row + KF_REC, &m, sizeof(TrackMeta));
+        s_wmask[t] = wmask;
+    }
+    __syncthreads();
+    // cooperative store of what changed
+    double2 *kfw = reinterpret_cast<double2 *>(a.kf);
+    double2 *metaw = reinterpret_cast<double2 *>(a.meta);
+    for (int p = t; p < nloc * REC_PIECES; p += APPLY_T) {
+        const int r = p / REC_PIECES, k = p - r * REC_PIECES;
+        const int wm = s_wmask[r];
+        const long long sl = tb + s_slot[r];
+        if (k < 12) {
+            if (wm & 1) kfw[sl * 12 + k] = rec[r][k];
+        } else if (wm & 2) {
+            metaw[sl * 3 + (k - 12)] = rec[r][k];
+        }
     }
 }
 
 // ------------------------------------------------------------------------------------ k_finish
-__global__ __launch_bounds__(BLK) void k_finish(BtArgs a) {
+__global__ __launch_bounds__(BLKF) void k_finish(BtArgs a) {
     __shared__ int wsum[32];
     __shared__ GridScratch gs;
     extern __shared__ __attribute__((aligned(16))) unsigned int live[];   // CAP bits
@@ -332,7 +425,7 @@ __global__ __launch_bounds__(BLK) void k_finish(BtArgs a) {
         if (t == 0) atomicOr(&c->err, ERR_TRACK_CAPACITY);
         n_births = n_free;
     }
-    for (int b = t; b < n_births; b += BLK) {
+    for (int b = t; b < n_births; b += (int)blockDim.x) {
         const int slot = a.free_list[tb + b];
         const int d = a.high[db + a.rest[db + a.birth[db + b]]];
         KfState st;
@@ -351,7 +444,7 @@ __global__ __launch_bounds__(BLK) void k_finish(BtArgs a) {
         a.meta[tb + slot] = m;
     }
     // lost-track expiry (:250-253); end_frame == frame_id
-    for (int i = t; i < n_lost; i += BLK) {
+    for (int i = t; i < n_lost; i += (int)blockDim.x) {
         const long long slot = tb + a.lost[tb + i];
         const TrackMeta m = a.meta[slot];
         if (fid - m.frame_id > a.max_time_lost)
@@ -363,7 +456,7 @@ __global__ __launch_bounds__(BLK) void k_finish(BtArgs a) {
         n_tracked, wsum,
         [&](int i) { return st_of(a.meta[tb + a.tracked[tb + i]].flags) == ST_TRACKED; },
         [&](int i, int pos) { a.t2[tb + pos] = a.tracked[tb + i]; });
-    for (int b = t; b < n_births; b += BLK) a.t2[tb + n_t2 + b] = a.free_list[tb + b];
+    for (int b = t; b < n_births; b += (int)blockDim.x) a.t2[tb + n_t2 + b] = a.free_list[tb + b];
     n_t2 += n_births;
     n_t2 += block_compact(n_pool, wsum, [&](int i) { return a.kind1[tb + i] == 2; },
                           [&](int i, int pos) { a.t2[tb + n_t2 + pos] = a.pool[tb + i]; });
@@ -384,18 +477,18 @@ __global__ __launch_bounds__(BLK) void k_finish(BtArgs a) {
         [&](int i, int pos) { a.l2[tb + n_l2 + pos] = a.pool[tb + a.left[tb + i]]; });
     block_sync();
     // this frame's removals join removed_stracks only now (:265)
-    for (int i = t; i < n_lost; i += BLK) {
+    for (int i = t; i < n_lost; i += (int)blockDim.x) {
         const long long slot = tb + a.lost[tb + i];
         const int f = a.meta[slot].flags;
         if (f & FL_REMOVED_NOW) a.meta[slot].flags = (f & ~FL_REMOVED_NOW) | FL_EVER_REMOVED;
     }
-    for (int p = t; p < n_t2; p += BLK) {
+    for (int p = t; p < n_t2; p += (int)blockDim.x) {
         const long long slot = tb + a.t2[tb + p];
         a.tbox[tb + p] = kf_box(a.kf, slot);
         a.tage[tb + p] = a.meta[slot].frame_id - a.meta[slot].start_frame;
         a.dropA[tb + p] = 0;
     }
-    for (int q = t; q < n_l2; q += BLK) {
+    for (int q = t; q < n_l2; q += (int)blockDim.x) {
         const long long slot = tb + a.l2[tb + q];
         a.lbox[tb + q] = kf_box(a.kf, slot);
         a.lage[tb + q] = a.meta[slot].frame_id - a.meta[slot].start_frame;
@@ -405,9 +498,10 @@ __global__ __launch_bounds__(BLK) void k_finish(BtArgs a) {
     // remove_duplicate_stracks (:312-325): set semantics, so pairs are visited in any order
     if (n_t2 > 0 && n_l2 > 0) {
         const GridView gv = grid_of(a.grid_lost, s);
-        grid_build(n_l2, [&](int q) { return a.lbox[tb + q]; }, gv, gs, wsum);
+        grid_build(n_l2, [&](int q) { return a.lbox[tb + q]; }, [](int) { return 1.0; }, gv, gs,
+                   wsum);
         const GridHdr gh = gs.hdr;
-        for (int p = t; p < n_t2; p += BLK) {
+        for (int p = t; p < n_t2; p += (int)blockDim.x) {
             const Box tbx = a.tbox[tb + p];
             const int ta = a.tage[tb + p];
             auto pair = [&](int q, const Box &lb) {
@@ -417,12 +511,13 @@ __global__ __launch_bounds__(BLK) void k_finish(BtArgs a) {
                     else a.dropA[tb + p] = 1;
                 }
             };
-            grid_query(gv, gh, tbx, pair, [&](int q) { pair(q, a.lbox[tb + q]); });
+            grid_query(gv, gh, tbx, [&](int k) { pair(gv.ids[k], gv.boxes[k]); },
+                       [&](int q) { pair(q, a.lbox[tb + q]); });
         }
     }
     // final lists, output rows, free slots
     const int words = (a.CAP + 31) / 32;
-    for (int wd = t; wd < words; wd += BLK) live[wd] = 0u;
+    for (int wd = t; wd < words; wd += (int)blockDim.x) live[wd] = 0u;
     block_sync();
     const int n_tr = block_compact(n_t2, wsum, [&](int p) { return a.dropA[tb + p] == 0; },
                                    [&](int p, int pos) {
@@ -467,20 +562,20 @@ __global__ __launch_bounds__(BLK) void k_finish(BtArgs a) {
 }
 
 // Rebuild the free-slot list of every stream from its tracked + lost lists (after a reserve).
-__global__ __launch_bounds__(BLK) void k_rebuild_free(BtArgs a) {
+__global__ __launch_bounds__(BLKF) void k_rebuild_free(BtArgs a) {
     __shared__ int wsum[32];
     extern __shared__ __attribute__((aligned(16))) unsigned int live[];
     const int s = blockIdx.x, t = threadIdx.x;
     BtCounters *c = a.cnt + s;
     const long long tb = (long long)s * a.CAP;
     const int words = (a.CAP + 31) / 32;
-    for (int w = t; w < words; w += BLK) live[w] = 0u;
+    for (int w = t; w < words; w += (int)blockDim.x) live[w] = 0u;
     block_sync();
-    for (int i = t; i < c->n_tracked; i += BLK) {
+    for (int i = t; i < c->n_tracked; i += (int)blockDim.x) {
         const int slot = a.tracked[tb + i];
         atomicOr(&live[slot >> 5], 1u << (slot & 31));
     }
-    for (int i = t; i < c->n_lost; i += BLK) {
+    for (int i = t; i < c->n_lost; i += (int)blockDim.x) {
         const int slot = a.lost[tb + i];
         atomicOr(&live[slot >> 5], 1u << (slot & 31));
     }
@@ -531,7 +626,8 @@ struct yta_bytetrack {
 namespace {
 
 constexpr int BT_PHASES = 4;   // launches per frame, see yta_bytetrack_profile_collect
-constexpr size_t BT_LDS_BYTES = 72 * 1024;   // dynamic LDS of the stage kernels
+constexpr size_t BT_LDS_BYTES = 150 * 1024;   // k_stage1 arena (one 1024-thread block per CU)
+constexpr size_t BT_LDS23_BYTES = 32 * 1024;  // k_stage23 arena (several blocks per CU)
 
 template <typename T>
 int dalloc(yta_bytetrack *e, T **p, long long n) {
@@ -560,6 +656,7 @@ int grid_alloc(yta_bytetrack *e, BtGrid &g, long long cap) {
     DALLOC(g.cell, (long long)e->S * (GRID_MAX_CELLS + 1));
     DALLOC(g.items, e->S * cap);
     DALLOC(g.boxes, e->S * cap);
+    DALLOC(g.fbox, e->S * cap);
     DALLOC(g.big, e->S * cap);
     return YTA_OK;
 }
@@ -618,14 +715,15 @@ int bt_alloc(yta_bytetrack *e) {
     // association: LDS arena first; the global fallback arena holds the worst case (every pair a
     // candidate edge), so no frame can overflow it
     a.lds_bytes = BT_LDS_BYTES;
+    a.lds_bytes23 = BT_LDS23_BYTES;
     a.ws_stride = (assoc_arena_bytes(CAP, MAXD, CAP * MAXD) + 255) & ~255LL;
     DALLOC(a.ws, S * a.ws_stride);
     a.slab.R = (int)CAP;
     a.slab.C = (int)MAXD;
     a.slab.i_stride = lap_slab_ints((int)CAP, (int)MAXD);
     a.slab.d_stride = lap_slab_doubles((int)CAP, (int)MAXD);
-    DALLOC(a.slab.i, S * BLK_WAVES * a.slab.i_stride);
-    DALLOC(a.slab.d, S * BLK_WAVES * a.slab.d_stride);
+    DALLOC(a.slab.i, S * SLAB_WAVES * a.slab.i_stride);
+    DALLOC(a.slab.d, S * SLAB_WAVES * a.slab.d_stride);
     DALLOC(e->d_det_off, S + 1);
     YTA_HIP(hipHostMalloc((void **)&e->h_off, sizeof(int) * (S + 1), hipHostMallocDefault));
     YTA_HIP(hipHostMalloc((void **)&e->h_cnt, sizeof(BtCounters) * S, hipHostMallocDefault));
@@ -665,18 +763,18 @@ int launch_pipeline(yta_bytetrack *e, const double *det_in, const int *det_off, 
     a.out = out;
     a.out_counts = out_counts;
     MARK();
-    hipLaunchKernelGGL(k_stage1, dim3(a.S), dim3(BLK), a.lds_bytes, e->stream, a);
+    hipLaunchKernelGGL(k_stage1, dim3(a.S), dim3(BLK1), a.lds_bytes, e->stream, a);
     YTA_HIP(hipGetLastError());
     MARK();
-    hipLaunchKernelGGL(k_stage23, dim3(a.S), dim3(BLK), a.lds_bytes, e->stream, a);
+    hipLaunchKernelGGL(k_stage23, dim3(a.S), dim3(BLK23), a.lds_bytes23, e->stream, a);
     YTA_HIP(hipGetLastError());
     MARK();
-    const dim3 gt((a.CAP + GRID_T - 1) / GRID_T, a.S);
-    hipLaunchKernelGGL(k_apply, gt, dim3(GRID_T), 0, e->stream, a);
+    const dim3 gt((a.CAP + APPLY_T - 1) / APPLY_T, a.S);
+    hipLaunchKernelGGL(k_apply, gt, dim3(APPLY_T), 0, e->stream, a);
     YTA_HIP(hipGetLastError());
     MARK();
     const size_t live_bytes = sizeof(unsigned int) * ((a.CAP + 31) / 32);
-    hipLaunchKernelGGL(k_finish, dim3(a.S), dim3(BLK), live_bytes, e->stream, a);
+    hipLaunchKernelGGL(k_finish, dim3(a.S), dim3(BLKF), live_bytes, e->stream, a);
     YTA_HIP(hipGetLastError());
     MARK();
     return YTA_OK;
@@ -728,7 +826,7 @@ int reserve(yta_bytetrack *e, int cap, int maxd) {
     }
     if (!rc) {
         const size_t live_bytes = sizeof(unsigned int) * ((nc + 31) / 32);
-        hipLaunchKernelGGL(k_rebuild_free, dim3(e->S), dim3(BLK), live_bytes, e->stream, n->a);
+        hipLaunchKernelGGL(k_rebuild_free, dim3(e->S), dim3(BLKF), live_bytes, e->stream, n->a);
         hipError_t he = hipGetLastError();
         if (he == hipSuccess) he = hipStreamSynchronize(e->stream);
         if (he != hipSuccess) {
@@ -748,6 +846,7 @@ int reserve(yta_bytetrack *e, int cap, int maxd) {
     e->MAXD = n->MAXD;
     e->allocs.swap(n->allocs);
     n->a.lds_bytes = e->a.lds_bytes;
+    n->a.lds_bytes23 = e->a.lds_bytes23;
     e->a = n->a;
     e->h_off = n->h_off;
     e->h_cnt = n->h_cnt;
@@ -1061,6 +1160,7 @@ int yta_bytetrack_set_lds(yta_bytetrack *e, int bytes) {
     YTA_HIP(hipSetDevice(e->device));
     YTA_HIP(hipStreamSynchronize(e->stream));
     e->a.lds_bytes = (size_t)bytes & ~(size_t)15;
+    e->a.lds_bytes23 = std::min(e->a.lds_bytes, BT_LDS23_BYTES);
     YTA_HIP(hipFuncSetAttribute((const void *)k_stage1, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)std::max<size_t>(e->a.lds_bytes, BT_LDS_BYTES)));
     YTA_HIP(hipFuncSetAttribute((const void *)k_stage23, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -1073,5 +1173,12 @@ int yta_bytetrack_hip_stream(yta_bytetrack *e, void **stream) {
     *stream = (void *)e->stream;
     return YTA_OK;
 }
+
+#ifdef YTA_STAMPS
+int yta_debug_stamps(unsigned long long *out) {
+    YTA_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 128));
+    return YTA_OK;
+}
+#endif
 
 }  // extern "C"

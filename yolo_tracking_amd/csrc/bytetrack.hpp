@@ -24,6 +24,8 @@ struct TrackMeta {                   // 48 B, one per slot
     int pad;
 };
 
+static_assert(sizeof(TrackMeta) == 48, "TrackMeta layout");
+
 struct BtCounters {                  // one per stream, 128 B
     long long next_id;               // last issued track id (BaseTrack._count)
     int frame_id;
@@ -44,6 +46,7 @@ struct BtGrid {                      // one grid per stream (hdr) + cell / item 
     int *cell;                       // [S][GRID_MAX_CELLS + 1]
     int *items, *big;                // [S][cap]
     Box *boxes;                      // [S][cap]
+    float4 *fbox;                    // [S][cap]
     long long cap;
 };
 
@@ -73,7 +76,7 @@ struct BtArgs {
     // association results
     int *x1, *y1, *x2, *y2, *x3, *y3;   // x*: [S*CAP], y*: [S*MAXD]
     // association workspace: LDS arena size, per-stream global fallback arena, solver slabs
-    size_t lds_bytes;
+    size_t lds_bytes, lds_bytes23;   // arenas of k_stage1 / k_stage23
     unsigned char *ws;
     long long ws_stride;
     LapSlab slab;             // per stream: (threads / 64) slabs

@@ -46,46 +46,118 @@ __device__ __forceinline__ void block_sync() {
     __syncthreads();
 }
 
+// Diagnostic build only (-DYTA_STAMPS, tools/diag_stamps.py): wall-clock stamps (100 MHz) of
+// block 0's phases, read back with yta_debug_stamps.
+#ifdef YTA_STAMPS
+static __device__ unsigned long long g_stamps[128];
+static __device__ int g_stamp_off;
+#define YTA_STAMP(k)                                                                        \
+    do {                                                                                    \
+        if (blockIdx.x == 0 && threadIdx.x == 0) g_stamps[g_stamp_off + (k)] = wall_clock64(); \
+    } while (0)
+#define YTA_STAMP_BASE(b)                                        \
+    do {                                                         \
+        if (blockIdx.x == 0 && threadIdx.x == 0) g_stamp_off = (b); \
+    } while (0)
+#define YTA_STAMP_ABS(k)                                                       \
+    do {                                                                       \
+        if (blockIdx.x == 0 && threadIdx.x == 0) g_stamps[(k)] = wall_clock64(); \
+    } while (0)
+#else
+#define YTA_STAMP(k) \
+    do {             \
+    } while (0)
+#define YTA_STAMP_BASE(b) \
+    do {                  \
+    } while (0)
+#define YTA_STAMP_ABS(k) \
+    do {                 \
+    } while (0)
+#endif
+
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
 
 __device__ __forceinline__ unsigned long long lanemask_lt() {
     return (1ull << lane_id()) - 1ull;
 }
 
-// Exclusive prefix sum over the whole block (blockDim.x multiple of 64, <= 1024).  `wsum` is a
-// shared scratch of >= 17 ints.  Returns the exclusive prefix; *total gets the block sum.
+// ------------------------------------------------------------------ DPP cross-lane primitives
+// gfx950 (GFX9 DPP): quad_perm, row_shr:n (0x110+n), row_ror:n (0x120+n), row_bcast:15 (0x142),
+// row_bcast:31 (0x143).  All lanes of the wave must be active.
+template <int CTRL>
+__device__ __forceinline__ int dpp_i32(int v) {
+    return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false);
+}
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+    const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+    const unsigned lo = (unsigned)dpp_i32<CTRL>((int)(unsigned)b);
+    const unsigned hi = (unsigned)dpp_i32<CTRL>((int)(unsigned)(b >> 32));
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+__device__ __forceinline__ double readlane_f64(double v, int lane) {
+    const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)b, lane);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(b >> 32), lane);
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
+// Inclusive prefix sum over the 64 lanes.
+__device__ __forceinline__ int wave_inclusive_scan(int x) {
+    const int l = lane_id(), rl = l & 15;
+    int t;
+    t = dpp_i32<0x111>(x); if (rl >= 1) x += t;
+    t = dpp_i32<0x112>(x); if (rl >= 2) x += t;
+    t = dpp_i32<0x114>(x); if (rl >= 4) x += t;
+    t = dpp_i32<0x118>(x); if (rl >= 8) x += t;
+    t = dpp_i32<0x142>(x); if ((l & 31) >= 16) x += t;
+    t = dpp_i32<0x143>(x); if (l >= 32) x += t;
+    return x;
+}
+
+enum { RED_MIN = 0, RED_MAX = 1, RED_SUM = 2 };
+__device__ __forceinline__ double red_op(int op, double a, double b) {
+    return op == RED_MIN ? fmin(a, b) : (op == RED_MAX ? fmax(a, b) : a + b);
+}
+__device__ __forceinline__ double red_ident(int op) {
+    return op == RED_MIN ? INFINITY : (op == RED_MAX ? -INFINITY : 0.0);
+}
+// All-reduce within each 16-lane row (every lane of the row gets the row's result).
+__device__ __forceinline__ double row_allreduce(int op, double v) {
+    v = red_op(op, v, dpp_f64<0xB1>(v));    // quad_perm [1,0,3,2]
+    v = red_op(op, v, dpp_f64<0x4E>(v));    // quad_perm [2,3,0,1]
+    v = red_op(op, v, dpp_f64<0x124>(v));   // row_ror:4
+    v = red_op(op, v, dpp_f64<0x128>(v));   // row_ror:8
+    return v;
+}
+// Wave-uniform reduction of the 64 lanes.
+__device__ __forceinline__ double wave_reduce(int op, double v) {
+    v = row_allreduce(op, v);
+    return red_op(op, red_op(op, readlane_f64(v, 0), readlane_f64(v, 16)),
+                  red_op(op, readlane_f64(v, 32), readlane_f64(v, 48)));
+}
+
+// Exclusive prefix sum over the whole block (blockDim.x a multiple of 64, <= 1024).  `wsum` is a
+// shared scratch of >= 16 ints.  Returns the exclusive prefix; *total gets the block sum.
 __device__ __forceinline__ int block_exclusive_scan(int v, int *wsum, int *total) {
     const int lane = lane_id();
     const int wid = threadIdx.x / WAVE;
-    const int nw = (blockDim.x + WAVE - 1) / WAVE;
-    int incl = v;
-#pragma unroll
-    for (int off = 1; off < WAVE; off <<= 1) {
-        int t = __shfl_up(incl, off, WAVE);
-        if (lane >= off) incl += t;
-    }
+    const int nw = blockDim.x / WAVE;
+    const int incl = wave_inclusive_scan(v);
     if (lane == WAVE - 1) wsum[wid] = incl;
     block_sync();
-    if (threadIdx.x == 0) {
-        int run = 0;
-        for (int w = 0; w < nw; ++w) {
-            int t = wsum[w];
-            wsum[w] = run;
-            run += t;
-        }
-        wsum[16] = run;
-    }
-    __syncthreads();
-    int excl = incl - v + wsum[wid];
-    if (total) *total = wsum[16];
-    __syncthreads();
-    return excl;
+    int p = lane < nw ? wsum[lane] : 0;
+    p = wave_inclusive_scan(p);
+    const int before = wid > 0 ? __builtin_amdgcn_readlane(p, wid - 1) : 0;
+    if (total) *total = __builtin_amdgcn_readlane(p, nw - 1);
+    __syncthreads();   // wsum is reused by the next scan
+    return incl - v + before;
 }
 
 // Order-preserving compaction of indices [0, n) where pred(i) holds, appended to out[*]
 // starting at `base`.  All threads of the block must call it.  Returns the count.
 template <typename Pred, typename Emit>
-__device__ int block_compact(int n, int *wsum, Pred pred, Emit emit) {
+__device__ __forceinline__ int block_compact(int n, int *wsum, Pred pred, Emit emit) {
     int count = 0;
     for (int start = 0; start < n; start += blockDim.x) {
         int i = start + threadIdx.x;

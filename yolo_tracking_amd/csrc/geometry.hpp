@@ -33,11 +33,14 @@ __host__ __device__ __forceinline__ Overlap overlap(const Box &a, const Box &b) 
 
 __host__ __device__ __forceinline__ double iou(const Box &a, const Box &b) { return overlap(a, b).iou; }
 
-// True when the intersection is non-empty.  If false, iou() is +-0 or NaN, so every
-// "1 - iou < thresh" test with thresh <= 1 fails: such pairs can never be association edges.
+// True when the intersection is non-empty, i.e. np_min(x2) - np_max(x1) > 0 on both axes.  If
+// false, iou() is +-0 or NaN, so every "1 - iou < thresh" test with thresh <= 1 fails: such pairs
+// can never be association edges.  Written as plain comparisons, which is the same predicate for
+// every input: with a NaN both forms are false; otherwise min - max > 0 <=> min > max (the
+// difference of two distinct doubles never rounds to 0, inf - inf = NaN fails like inf > inf).
 __host__ __device__ __forceinline__ bool intersects(const Box &a, const Box &b) {
-    return np_min(a.x2, b.x2) - np_max(a.x1, b.x1) > 0.0 &&
-           np_min(a.y2, b.y2) - np_max(a.y1, b.y1) > 0.0;
+    return a.x2 > a.x1 && a.x2 > b.x1 && b.x2 > a.x1 && b.x2 > b.x1 &&
+           a.y2 > a.y1 && a.y2 > b.y1 && b.y2 > a.y1 && b.y2 > b.y1;
 }
 
 // iou.py:28-62.  Returns NaN where the reference would raise on its enclosure assert (:58); the

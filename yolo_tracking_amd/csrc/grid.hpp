@@ -22,18 +22,40 @@ namespace yta {
 
 constexpr int GRID_MAX_CELLS = 2048;
 
+// Cell budget for n items: about two cells per item (fewer cells only coarsen the pruning).
+__host__ __device__ __forceinline__ int grid_cells_for(int n) {
+    const int c = 2 * n + 16;
+    return c < GRID_MAX_CELLS ? c : GRID_MAX_CELLS;
+}
+
 struct GridHdr {
     double ox, oy, inv_g, maxw, maxh, g;
     int gx, gy, n_big, n_binned;
 };
 
 struct GridView {
-    GridHdr *hdr;
+    GridHdr *hdr;      // optional copy of the header (global)
     int *cell_start;   // GRID_MAX_CELLS + 1
     int *ids;          // binned item ids, in cell order
     Box *boxes;        // their boxes, same order
+    float4 *fbox;      // the same boxes rounded outward to float (x1, y1 down; x2, y2 up)
+    double *w;         // optional per-item weight, same order (nullptr: none)
     int *big;          // items scanned by every query
 };
+
+// float bounds that contain the double value: the prefilter on them never rejects a pair whose
+// double boxes intersect (x2 > x1' implies up(x2) >= x2 > x1' >= down(x1'); NaN fails both)
+__device__ __forceinline__ float f_down(double x) {
+    const float f = (float)x;
+    return (double)f > x ? nextafterf(f, -INFINITY) : f;
+}
+__device__ __forceinline__ float f_up(double x) {
+    const float f = (float)x;
+    return (double)f < x ? nextafterf(f, INFINITY) : f;
+}
+__device__ __forceinline__ float4 box_outward(const Box &b) {
+    return make_float4(f_down(b.x1), f_down(b.y1), f_up(b.x2), f_up(b.y2));
+}
 
 __host__ __device__ __forceinline__ bool box_usable(const Box &b) {
     const double w = b.x2 - b.x1, h = b.y2 - b.y1;
@@ -52,33 +74,29 @@ struct GridScratch {
     GridHdr hdr;
 };
 
-// Block-wide reduction of 6 values; op[k]: 0 = min, 1 = max, 2 = sum (per-wave partials in `red`).
+// Block-wide reduction of 6 values; op[k]: RED_MIN / RED_MAX / RED_SUM.  Per-wave partials go
+// through `red` (>= 8 * 16 doubles); every wave then reduces the partials itself.
 __device__ __forceinline__ void block_reduce6(double v[6], const int op[6], double *red) {
-    auto comb = [&](int k, double a, double b) {
-        return op[k] == 0 ? fmin(a, b) : (op[k] == 1 ? fmax(a, b) : a + b);
-    };
-    for (int off = 32; off > 0; off >>= 1)
-        for (int k = 0; k < 6; ++k) v[k] = comb(k, v[k], __shfl_xor(v[k], off));
-    const int wv = threadIdx.x / WAVE, nw = (blockDim.x + WAVE - 1) / WAVE;
-    if (lane_id() == 0)
+    const int wv = threadIdx.x / WAVE, nw = blockDim.x / WAVE, lane = lane_id();
+    for (int k = 0; k < 6; ++k) v[k] = wave_reduce(op[k], v[k]);
+    if (lane == 0)
         for (int k = 0; k < 6; ++k) red[8 * wv + k] = v[k];
     block_sync();
-    for (int k = 0; k < 6; ++k) {
-        double a = red[k];
-        for (int w = 1; w < nw; ++w) a = comb(k, a, red[8 * w + k]);
-        v[k] = a;
-    }
-    block_sync();
+    for (int k = 0; k < 6; ++k)
+        v[k] = wave_reduce(op[k], lane < nw ? red[8 * lane + k] : red_ident(op[k]));
+    __syncthreads();   // red is reused
 }
 
-// Block-wide build (every thread of the block calls it).  box(i) returns item i's box.
-// gv.cell_start needs GRID_MAX_CELLS + 1 entries, gv.ids / gv.boxes / gv.big n entries.
-template <typename BoxOf>
-__device__ void grid_build(int n, BoxOf box, GridView gv, GridScratch &gs, int *wsum) {
+// Block-wide build (every thread of the block calls it).  box(i) returns item i's box, wof(i) its
+// weight (stored only when gv.w is set).  gv.cell_start needs GRID_MAX_CELLS + 1 entries, gv.ids /
+// gv.boxes / gv.w / gv.big n entries, gv.cell_start grid_cells_for(n) + 1.
+template <typename BoxOf, typename WOf>
+__device__ __forceinline__ void grid_build(int n, BoxOf box, WOf wof, GridView gv, GridScratch &gs, int *wsum) {
     const int t = threadIdx.x, nt = blockDim.x;
+    YTA_STAMP_ABS(110);
     // pass 1: mean size of the usable boxes
     double v[6] = {0, 0, 0, 0, 0, 0};
-    const int sums[6] = {2, 2, 2, 2, 2, 2};
+    const int sums[6] = {RED_SUM, RED_SUM, RED_SUM, RED_SUM, RED_SUM, RED_SUM};
     for (int i = t; i < n; i += nt) {
         const Box b = box(i);
         if (!box_usable(b)) continue;
@@ -86,6 +104,7 @@ __device__ void grid_build(int n, BoxOf box, GridView gv, GridScratch &gs, int *
         v[5] += 1.0;
     }
     block_reduce6(v, sums, gs.red);
+    YTA_STAMP_ABS(111);
     const double nb = v[5];
     const double mean = nb > 0 ? v[4] / nb : 1.0;
     const double bthr = 4.0 * mean;
@@ -94,7 +113,7 @@ __device__ void grid_build(int n, BoxOf box, GridView gv, GridScratch &gs, int *
     };
     // pass 2: extent of the binned top-left corners and their maximum width / height
     double e[6] = {INFINITY, INFINITY, -INFINITY, -INFINITY, -INFINITY, -INFINITY};
-    const int ops[6] = {0, 0, 1, 1, 1, 1};
+    const int ops[6] = {RED_MIN, RED_MIN, RED_MAX, RED_MAX, RED_MAX, RED_MAX};
     for (int i = t; i < n; i += nt) {
         const Box b = box(i);
         if (!binned(b)) continue;
@@ -106,6 +125,7 @@ __device__ void grid_build(int n, BoxOf box, GridView gv, GridScratch &gs, int *
         e[5] = fmax(e[5], b.y2 - b.y1);
     }
     block_reduce6(e, ops, gs.red);
+    YTA_STAMP_ABS(112);
     GridHdr h;
     h.maxw = e[4] > 0 ? e[4] : 0.0;
     h.maxh = e[5] > 0 ? e[5] : 0.0;
@@ -118,7 +138,8 @@ __device__ void grid_build(int n, BoxOf box, GridView gv, GridScratch &gs, int *
         double g = mean;
         const double ex = e[2] - e[0], ey = e[3] - e[1];
         double gxf = floor(ex / g) + 1.0, gyf = floor(ey / g) + 1.0;
-        while (gxf * gyf > (double)GRID_MAX_CELLS) {
+        const double max_cells = (double)grid_cells_for(n);
+        while (gxf * gyf > max_cells) {
             g *= 1.25;
             gxf = floor(ex / g) + 1.0;
             gyf = floor(ey / g) + 1.0;
@@ -137,6 +158,7 @@ __device__ void grid_build(int n, BoxOf box, GridView gv, GridScratch &gs, int *
     int *cs = gv.cell_start;
     for (int c = t; c <= ncell; c += nt) cs[c] = 0;
     block_sync();
+    YTA_STAMP_ABS(113);
     auto cell_of = [&](const Box &b) {
         return grid_cell_1d(b.y1, h.oy, h.inv_g, h.gy) * h.gx + grid_cell_1d(b.x1, h.ox, h.inv_g, h.gx);
     };
@@ -152,6 +174,7 @@ __device__ void grid_build(int n, BoxOf box, GridView gv, GridScratch &gs, int *
         atomicAdd(&cs[cell_of(b) + 1], 1);
     }
     block_sync();
+    YTA_STAMP_ABS(114);
     int run = 0;
     for (int start = 0; start < ncell; start += nt) {
         const int c = start + t;
@@ -166,17 +189,23 @@ __device__ void grid_build(int n, BoxOf box, GridView gv, GridScratch &gs, int *
         if (gv.hdr) *gv.hdr = gs.hdr;
     }
     block_sync();
+    YTA_STAMP_ABS(115);
     for (int i = t; i < n; i += nt) {
         const Box b = box(i);
         if (!binned(b)) continue;
         const int pos = atomicAdd(&cs[cell_of(b) + 1], 1);
         gv.ids[pos] = i;
         gv.boxes[pos] = b;
+        gv.fbox[pos] = box_outward(b);
+        if (gv.w) gv.w[pos] = wof(i);
     }
     block_sync();
+    YTA_STAMP_ABS(116);
 }
 
-// Visit every binned item that may intersect T: visit(id, box).  Big items: visit_big(id).
+// Visit every binned item that may intersect T: visit(k) with k its position in cell order (ids,
+// boxes, w at k); the float prefilter has passed, the caller applies the exact test.  Big items:
+// visit_big(id).
 template <typename Visit, typename VisitBig>
 __device__ __forceinline__ void grid_query(const GridView &gv, const GridHdr &h, const Box &T,
                                            Visit visit, VisitBig visit_big) {
@@ -191,10 +220,14 @@ __device__ __forceinline__ void grid_query(const GridView &gv, const GridHdr &h,
     const int cy0 = grid_cell_1d(ly, h.oy, h.inv_g, h.gy);
     const int cx1 = fx1 > (double)(h.gx - 1) ? h.gx - 1 : (int)fx1;
     const int cy1 = fy1 > (double)(h.gy - 1) ? h.gy - 1 : (int)fy1;
+    const float4 tf = box_outward(T);
     for (int cy = cy0; cy <= cy1; ++cy) {
         const int base = cy * h.gx;
         const int b = ald(gv.cell_start + base + cx0), e = ald(gv.cell_start + base + cx1 + 1);
-        for (int k = b; k < e; ++k) visit(gv.ids[k], gv.boxes[k]);   // cells of a row are contiguous
+        for (int k = b; k < e; ++k) {   // the cells of a grid row are contiguous
+            const float4 f = gv.fbox[k];
+            if (f.z > tf.x && tf.z > f.x && f.w > tf.y && tf.w > f.y) visit(k);
+        }
     }
 }
 

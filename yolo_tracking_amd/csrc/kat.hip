@@ -116,12 +116,12 @@ __global__ __launch_bounds__(1024) void k_lap_dense(const double *cost, int nr, 
 // (the shape of remove_duplicate_stracks, byte_tracker.py:312-325).
 __global__ __launch_bounds__(1024) void k_grid_pairs(const Box *a, int na, const Box *b, int nb,
                                                     double thresh, GridHdr *hdr, int *cell,
-                                                    int *ids, Box *boxes, int *big, int *pairs,
-                                                    int *n_pairs, int cap) {
+                                                    int *ids, Box *boxes, float4 *fbox, int *big,
+                                                    int *pairs, int *n_pairs, int cap) {
     __shared__ int wsum[32];
     __shared__ GridScratch gs;
-    const GridView gv{hdr, cell, ids, boxes, big};
-    grid_build(nb, [&](int q) { return b[q]; }, gv, gs, wsum);
+    const GridView gv{hdr, cell, ids, boxes, fbox, nullptr, big};
+    grid_build(nb, [&](int q) { return b[q]; }, [](int) { return 1.0; }, gv, gs, wsum);
     const GridHdr h = gs.hdr;
     for (int p = threadIdx.x; p < na; p += blockDim.x) {
         const Box T = a[p];
@@ -132,7 +132,37 @@ __global__ __launch_bounds__(1024) void k_grid_pairs(const Box *a, int na, const
                 if (k < cap) { pairs[2 * k] = p; pairs[2 * k + 1] = q; }
             }
         };
-        grid_query(gv, h, T, pair, [&](int q) { pair(q, b[q]); });
+        grid_query(gv, h, T, [&](int k) { pair(gv.ids[k], gv.boxes[k]); },
+                   [&](int q) { pair(q, b[q]); });
+    }
+}
+
+// Self-test of the block primitives (DPP scans / reductions) against serial answers.
+__device__ __forceinline__ int st_val(int u, int trial) {
+    return (int)(((unsigned)u * 2654435761u + (unsigned)trial * 40503u) >> 28) % 5 - (trial == 3);
+}
+__global__ __launch_bounds__(1024) void k_selftest(int *err) {
+    __shared__ int wsum[32];
+    __shared__ GridScratch gs;
+    const int t = threadIdx.x, nt = blockDim.x;
+    for (int trial = 0; trial < 6; ++trial) {
+        const int v = st_val(t, trial);
+        int tot;
+        const int ex = block_exclusive_scan(v, wsum, &tot);
+        int e = 0, all = 0, mn = 1 << 30, mx = -(1 << 30);
+        for (int u = 0; u < nt; ++u) {
+            const int vu = st_val(u, trial);
+            if (u < t) e += vu;
+            all += vu;
+            mn = vu < mn ? vu : mn;
+            mx = vu > mx ? vu : mx;
+        }
+        if (ex != e || tot != all) atomicOr(err, 1);
+        double r[6] = {(double)v, (double)v, (double)v, (double)-v, (double)v, 1.0};
+        const int ops[6] = {RED_MIN, RED_MAX, RED_SUM, RED_MIN, RED_SUM, RED_SUM};
+        block_reduce6(r, ops, gs.red);
+        if (r[0] != mn || r[1] != mx || r[2] != all || r[3] != -mx || r[4] != all || r[5] != nt)
+            atomicOr(err, 2);
     }
 }
 
@@ -256,6 +286,7 @@ int yta_grid_pairs(int device, const double *a, int na, const double *b, int nb,
     if (rc) return rc;
     DevBuf m;
     Box *da, *db, *boxes;
+    float4 *fbox;
     GridHdr *hdr;
     int *cell, *ids, *big, *dp, *dn;
     YTA_HIP(m.get(&da, na));
@@ -264,6 +295,7 @@ int yta_grid_pairs(int device, const double *a, int na, const double *b, int nb,
     YTA_HIP(m.get(&cell, GRID_MAX_CELLS + 1));
     YTA_HIP(m.get(&ids, nb));
     YTA_HIP(m.get(&boxes, nb));
+    YTA_HIP(m.get(&fbox, nb));
     YTA_HIP(m.get(&big, nb));
     YTA_HIP(m.get(&dp, 2 * (size_t)(cap > 0 ? cap : 1)));
     YTA_HIP(m.get(&dn, 1));
@@ -271,11 +303,27 @@ int yta_grid_pairs(int device, const double *a, int na, const double *b, int nb,
     YTA_HIP(hipMemcpy(db, b, sizeof(Box) * nb, hipMemcpyHostToDevice));
     YTA_HIP(hipMemset(dn, 0, sizeof(int)));
     hipLaunchKernelGGL(k_grid_pairs, dim3(1), dim3(1024), 0, 0, da, na, db, nb, thresh, hdr, cell,
-                       ids, boxes, big, dp, dn, cap);
+                       ids, boxes, fbox, big, dp, dn, cap);
     YTA_HIP(hipGetLastError());
     YTA_HIP(hipMemcpy(n_pairs, dn, sizeof(int), hipMemcpyDeviceToHost));
     const int n = *n_pairs < cap ? *n_pairs : cap;
     if (n) YTA_HIP(hipMemcpy(pairs, dp, sizeof(int) * 2 * n, hipMemcpyDeviceToHost));
+    return YTA_OK;
+}
+
+int yta_selftest(int device) {
+    int rc = select_device(device);
+    if (rc) return rc;
+    DevBuf m;
+    int *derr;
+    YTA_HIP(m.get(&derr, 1));
+    YTA_HIP(hipMemset(derr, 0, sizeof(int)));
+    for (int threads : {64, 128, 256, 512, 960, 1024})
+        hipLaunchKernelGGL(k_selftest, dim3(1), dim3(threads), 0, 0, derr);
+    YTA_HIP(hipGetLastError());
+    int herr = 0;
+    YTA_HIP(hipMemcpy(&herr, derr, sizeof(int), hipMemcpyDeviceToHost));
+    YTA_CHECK(herr == 0, YTA_ERR_HIP, "block primitive self-test failed (flags 0x%x)", herr);
     return YTA_OK;
 }
 

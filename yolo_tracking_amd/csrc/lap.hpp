@@ -63,6 +63,22 @@ struct Arena {
         lo += b;
         return p;
     }
+    // optional caches: nullptr (and no failure) when the space is not there
+    template <typename T>
+    __device__ __forceinline__ T *try_alloc(long long n) {
+        const size_t b = round(n, sizeof(T));
+        if (fail || b > hi - lo) return nullptr;
+        T *p = (T *)(base + lo);
+        lo += b;
+        return p;
+    }
+    template <typename T>
+    __device__ __forceinline__ T *try_alloc_top(long long n) {
+        const size_t b = round(n, sizeof(T));
+        if (fail || b > hi - lo) return nullptr;
+        hi -= b;
+        return (T *)(base + hi);
+    }
     template <typename T>
     __device__ __forceinline__ T *alloc_top(long long n) {
         const size_t b = round(n, sizeof(T));
@@ -129,8 +145,7 @@ __device__ __forceinline__ void solve_seg(int k, int l, const int *rows_in, cons
             }
             // argmin: lower distance, then a free column, then the lower lane
             double bd = (lane < V && !vis) ? d : INFINITY;
-#pragma unroll
-            for (int off = W / 2; off > 0; off >>= 1) bd = fmin(bd, __shfl_xor(bd, off, W));
+            bd = W == 16 ? row_allreduce(RED_MIN, bd) : wave_reduce(RED_MIN, bd);
             if (!(bd < INFINITY)) { if (lane == 0) atomicOr(err, ERR_SOLVER); return; }
             const bool cand = lane < V && !vis && d == bd;
             const unsigned long long mfree = __ballot(cand && y < 0) & segmask;
@@ -324,6 +339,7 @@ __device__ __forceinline__ bool lap_block(int nr, int nc, const int *row_off, co
     for (int n = t; n < N; n += nt) parent[n] = n;
     if (t == 0) { sh.cnt[0] = 0; sh.cnt[1] = 0; }
     block_sync();
+    YTA_STAMP(8);
     // P1: single-edge components matched outright, every other edge united
     for (int i = t; i < nr; i += nt) {
         const int b = row_off[i], e = row_off[i + 1];
@@ -338,6 +354,7 @@ __device__ __forceinline__ bool lap_block(int nr, int nc, const int *row_off, co
         }
     }
     block_sync();
+    YTA_STAMP(9);
     // P2: roots of the complex nodes (full path compression: a concurrent find only ever sees a
     // parent replaced by one of its ancestors), counts of complex nodes and of components
     auto complex_node = [&](int n) {
@@ -360,6 +377,7 @@ __device__ __forceinline__ bool lap_block(int nr, int nc, const int *row_off, co
         }
     }
     block_sync();
+    YTA_STAMP(10);
     const int ncx = sh.cnt[0], ncomp = sh.cnt[1];
     if (ncomp == 0) return true;
     int *cnodes = ar.alloc<int>(ncx);
@@ -389,6 +407,7 @@ __device__ __forceinline__ bool lap_block(int nr, int nc, const int *row_off, co
     }
     for (int c = t; c < ncomp; c += nt) { kc[c] = 0; lc[c] = 0; }
     block_sync();
+    YTA_STAMP(11);
     // P4: per-component row / column counts, offsets, members (roots are ascending: binary search)
     auto comp_of = [&](int n) {
         const int r = ald(parent + n);
@@ -430,6 +449,7 @@ __device__ __forceinline__ bool lap_block(int nr, int nc, const int *row_off, co
     }
     if (t == 0) { sh.cnt[0] = 0; sh.cnt[1] = 0; sh.cnt[2] = 0; }
     block_sync();
+    YTA_STAMP(12);
     // P5: classify and solve.  After the gather kc[c] = end of rows, lc[c] = end of columns.  The
     // members of a component are in ascending order within rows and within columns only after a
     // sort: atomics scattered them, so each component sorts its (few) members first.
@@ -469,7 +489,17 @@ __device__ __forceinline__ bool lap_block(int nr, int nc, const int *row_off, co
         }
     }
     block_sync();
+    YTA_STAMP(13);
     const int n16 = sh.cnt[0], n64 = sh.cnt[1], nbig = sh.cnt[2];
+#ifdef YTA_STAMPS
+    if (blockIdx.x == 0 && t == 0) {
+        g_stamps[g_stamp_off + 15] = n16;
+        g_stamps[g_stamp_off + 16] = n64;
+        g_stamps[g_stamp_off + 17] = nbig;
+        g_stamps[g_stamp_off + 18] = E;
+        g_stamps[g_stamp_off + 19] = ncx;
+    }
+#endif
     const int wave = t / WAVE, lane = lane_id(), nwaves = nt / WAVE;
     for (int q = wave * 4 + (lane >> 4); q - (lane >> 4) < n16; q += nwaves * 4) {
         if (q < n16) {
@@ -497,6 +527,7 @@ __device__ __forceinline__ bool lap_block(int nr, int nc, const int *row_off, co
                     thresh, X, Y, err);
     }
     block_sync();
+    YTA_STAMP(14);
     return true;
 }
 
