@@ -123,11 +123,6 @@ int yta_bytetrack_get_state(yta_bytetrack *engine, int stream, int *n_tracks, lo
  * launch order (stage1, stage23, apply, finish). */
 int yta_bytetrack_profile(yta_bytetrack *engine, int enable);
 int yta_bytetrack_profile_collect(yta_bytetrack *engine, double *ms, int *frames);
-/* Debug introspection of the last frame's duplicate removal (stream s): tracked' / lost' boxes
- * (4 f64 each), ages (tracked' then lost'), drop flags (tracked' then lost').  Buffers hold
- * track_capacity entries per list. */
-int yta_bytetrack_debug_dedup(yta_bytetrack *engine, int stream, int *n_t2, int *n_l2,
-                              double *tbox, double *lbox, int *ages, int *drops);
 /* Last frame's counts summed over streams (synchronises): dets, high, second, pool, activated,
  * unconfirmed, leftovers, rest, births, tracked', lost', tracked, lost, output rows, stage-1
  * candidate edges, stage-2+3 candidate edges, then the cumulative number of stream-frames whose

@@ -78,8 +78,9 @@ def main():
     show(st, 20, {4: "left/rest lists", **{k: v for k, v in STAGE1.items() if k >= 5}},
          "k_stage23 stage 2")
     show(st, 40, {k: v for k, v in STAGE1.items() if k >= 5}, "k_stage23 stage 3")
-    show(st, 100, {1: "query traversal", 2: "+ intersects", 3: "+ cost (full)", 4: "row boxes only"},
-         "stage-1 pass variants")
+    show(st, 80, {1: "zero bits", 2: "births", 3: "expiry", 4: "t2/l2 lists", 5: "dedup grid",
+                  6: "dedup queries", 7: "final lists", 8: "output rows", 9: "free list"},
+         "k_finish")
     show(st, 110, {1: "mean reduce", 2: "extent reduce", 3: "zero cells", 4: "count",
                   5: "cell scan", 6: "scatter"}, "grid_build (last call)")
 

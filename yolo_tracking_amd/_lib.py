@@ -65,7 +65,6 @@ _SIGS = {
     "yta_bytetrack_get_state": ([_P, _I, _P, _P, _P, _P], _I),
     "yta_bytetrack_profile": ([_P, _I], _I),
     "yta_bytetrack_profile_collect": ([_P, _P, _P], _I),
-    "yta_bytetrack_debug_dedup": ([_P, _I, _P, _P, _P, _P, _P, _P], _I),
     "yta_bytetrack_stats": ([_P, _P], _I),
     "yta_bytetrack_hip_stream": ([_P, _P], _I),
     "yta_bytetrack_set_lds": ([_P, _I], _I),

@@ -47,17 +47,6 @@ constexpr int BLK1 = YTA_BLK1, BLK23 = YTA_BLK23, BLKF = YTA_BLKF;
 constexpr int BLK_MAX = 1024;
 constexpr int SLAB_WAVES = BLK_MAX / WAVE;   // solver slabs per stream (any block size)
 
-__device__ __forceinline__ void load_kf(const double *kf, long long slot, KfState &s) {
-    const double2 *src = reinterpret_cast<const double2 *>(kf + slot * KF_REC);
-#pragma unroll
-    for (int k = 0; k < 12; ++k) {
-        const double2 v = src[k];
-        double *dst = k < 4 ? s.m + 2 * k : s.c + 2 * (k - 4);
-        dst[0] = v.x;
-        dst[1] = v.y;
-    }
-}
-
 __device__ __forceinline__ void store_kf(double *kf, long long slot, const KfState &s) {
     double2 *dst = reinterpret_cast<double2 *>(kf + slot * KF_REC);
 #pragma unroll
@@ -75,10 +64,6 @@ __device__ __forceinline__ Box kf_box(const double *kf, long long slot) {
 
 __device__ __forceinline__ int st_of(int flags) { return flags & FL_STATE; }
 
-__device__ __forceinline__ GridView grid_of(const BtGrid &g, int s) {
-    return GridView{g.hdr + s, g.cell + (long long)s * (GRID_MAX_CELLS + 1), g.items + s * g.cap,
-                    g.boxes + s * g.cap, g.fbox + s * g.cap, nullptr, g.big + s * g.cap};
-}
 
 // ------------------------------------------------------------------------------------ k_stage1
 // Per stream: frame_id++, confidence split (:149-158), STrack box conversions (:14-25),
@@ -280,12 +265,12 @@ __device__ __forceinline__ void take_detection(const BtArgs &a, KfState &st, Tra
 
 // Records move between HBM and LDS in whole 16-B pieces with consecutive lanes on consecutive
 // pieces of a record (full-line reads and writes); each thread then runs the Kalman step of one
-// track out of LDS.  Piece p < 12 is the Kalman record, 12..14 the 48-B meta.
+// track out of LDS.  Pieces 0-11: the Kalman record (mean, then covariance), 12-14: the meta.
 constexpr int APPLY_T = 128;              // tracks (= threads) per block
 constexpr int REC_PIECES = KF_REC / 2 + 3;
 
 __global__ __launch_bounds__(APPLY_T) void k_apply(BtArgs a) {
-    __shared__ double2 rec[APPLY_T][REC_PIECES];
+    __shared__ double2 rec[APPLY_T][REC_PIECES];   // 60-dword rows: no bank conflicts
     __shared__ int s_slot[APPLY_T];
     __shared__ int s_wmask[APPLY_T];      // bit 0: write the Kalman record, bit 1: write the meta
     const int s = blockIdx.y, t = threadIdx.x;
@@ -404,17 +389,38 @@ __global__ __launch_bounds__(APPLY_T) void k_apply(BtArgs a) {
 }
 
 // ------------------------------------------------------------------------------------ k_finish
-__global__ __launch_bounds__(BLKF) void k_finish(BtArgs a) {
-    __shared__ int wsum[32];
-    __shared__ GridScratch gs;
-    extern __shared__ __attribute__((aligned(16))) unsigned int live[];   // CAP bits
-    const int s = blockIdx.x, t = threadIdx.x;
+// Per stream: births (:242-248), lost expiry (:250-253), joint/sub list algebra incl. the
+// removed_stracks quirk (:257-265), duplicate removal (:312-325) through a grid over lost' (in an
+// LDS arena, or the stream's global workspace when lost' is too large), output rows (:270-281),
+// free slots.  Live / drop flags are LDS bitsets.
+struct FinishShared {
+    GridScratch gs;
+    int wsum[32];
+};
+
+__host__ __device__ inline long long dedup_arena_bytes(long long n) {
+    return 4 * (grid_cells_for((int)(n < GRID_MAX_CELLS ? n : GRID_MAX_CELLS)) + 1) +
+           n * (4 + 32 + 16 + 4) + 5 * 16;
+}
+
+__device__ __forceinline__ int track_age(const BtArgs &a, long long slot) {
+    return a.meta[slot].frame_id - a.meta[slot].start_frame;   // STrack.end_frame - start_frame
+}
+
+__device__ __forceinline__ void finish_body(const BtArgs &a, int s, unsigned *bits, Arena &ar,
+                                            FinishShared &sh) {
+    int *wsum = sh.wsum;
+    const int t = threadIdx.x, nt = blockDim.x;
     BtCounters *c = a.cnt + s;
     const long long tb = (long long)s * a.CAP, db = (long long)s * a.MAXD;
     const int fid = c->frame_id;
     const int n_tracked = c->n_tracked, n_lost = c->n_lost, n_pool = c->n_pool;
     const int n_rest = c->n_rest, n_left = c->n_left, n_free = c->n_free;
     const long long next_id = c->next_id;
+    const int words = (a.CAP + 31) / 32;
+    unsigned *live = bits, *dropA = bits + words, *dropB = bits + 2 * words;
+    for (int w = t; w < 3 * words; w += nt) bits[w] = 0u;
+    YTA_STAMP(1);
 
     // births in ascending order of the still-unmatched high detections (:242-248)
     int n_births = block_compact(
@@ -425,7 +431,7 @@ __global__ __launch_bounds__(BLKF) void k_finish(BtArgs a) {
         if (t == 0) atomicOr(&c->err, ERR_TRACK_CAPACITY);
         n_births = n_free;
     }
-    for (int b = t; b < n_births; b += (int)blockDim.x) {
+    for (int b = t; b < n_births; b += nt) {
         const int slot = a.free_list[tb + b];
         const int d = a.high[db + a.rest[db + a.birth[db + b]]];
         KfState st;
@@ -443,20 +449,22 @@ __global__ __launch_bounds__(BLKF) void k_finish(BtArgs a) {
         m.pad = 0;
         a.meta[tb + slot] = m;
     }
+    YTA_STAMP(2);
     // lost-track expiry (:250-253); end_frame == frame_id
-    for (int i = t; i < n_lost; i += (int)blockDim.x) {
+    for (int i = t; i < n_lost; i += nt) {
         const long long slot = tb + a.lost[tb + i];
         const TrackMeta m = a.meta[slot];
         if (fid - m.frame_id > a.max_time_lost)
             a.meta[slot].flags = (m.flags & ~FL_STATE) | ST_REMOVED | FL_REMOVED_NOW;
     }
     block_sync();
+    YTA_STAMP(3);
     // tracked' = [Tracked survivors of tracked_stracks] ++ births ++ re-found (:257-261)
     int n_t2 = block_compact(
         n_tracked, wsum,
         [&](int i) { return st_of(a.meta[tb + a.tracked[tb + i]].flags) == ST_TRACKED; },
         [&](int i, int pos) { a.t2[tb + pos] = a.tracked[tb + i]; });
-    for (int b = t; b < n_births; b += (int)blockDim.x) a.t2[tb + n_t2 + b] = a.free_list[tb + b];
+    for (int b = t; b < n_births; b += nt) a.t2[tb + n_t2 + b] = a.free_list[tb + b];
     n_t2 += n_births;
     n_t2 += block_compact(n_pool, wsum, [&](int i) { return a.kind1[tb + i] == 2; },
                           [&](int i, int pos) { a.t2[tb + n_t2 + pos] = a.pool[tb + i]; });
@@ -476,78 +484,111 @@ __global__ __launch_bounds__(BLKF) void k_finish(BtArgs a) {
         },
         [&](int i, int pos) { a.l2[tb + n_l2 + pos] = a.pool[tb + a.left[tb + i]]; });
     block_sync();
+    YTA_STAMP(4);
     // this frame's removals join removed_stracks only now (:265)
-    for (int i = t; i < n_lost; i += (int)blockDim.x) {
+    for (int i = t; i < n_lost; i += nt) {
         const long long slot = tb + a.lost[tb + i];
         const int f = a.meta[slot].flags;
         if (f & FL_REMOVED_NOW) a.meta[slot].flags = (f & ~FL_REMOVED_NOW) | FL_EVER_REMOVED;
     }
-    for (int p = t; p < n_t2; p += (int)blockDim.x) {
-        const long long slot = tb + a.t2[tb + p];
-        a.tbox[tb + p] = kf_box(a.kf, slot);
-        a.tage[tb + p] = a.meta[slot].frame_id - a.meta[slot].start_frame;
-        a.dropA[tb + p] = 0;
-    }
-    for (int q = t; q < n_l2; q += (int)blockDim.x) {
-        const long long slot = tb + a.l2[tb + q];
-        a.lbox[tb + q] = kf_box(a.kf, slot);
-        a.lage[tb + q] = a.meta[slot].frame_id - a.meta[slot].start_frame;
-        a.dropB[tb + q] = 0;
-    }
-    block_sync();
-    // remove_duplicate_stracks (:312-325): set semantics, so pairs are visited in any order
+    // remove_duplicate_stracks (:312-325): pairs with 1 - IoU < 0.15 drop the younger track (set
+    // semantics, so pairs are visited in any order)
     if (n_t2 > 0 && n_l2 > 0) {
-        const GridView gv = grid_of(a.grid_lost, s);
-        grid_build(n_l2, [&](int q) { return a.lbox[tb + q]; }, [](int) { return 1.0; }, gv, gs,
-                   wsum);
-        const GridHdr gh = gs.hdr;
-        for (int p = t; p < n_t2; p += (int)blockDim.x) {
-            const Box tbx = a.tbox[tb + p];
-            const int ta = a.tage[tb + p];
-            auto pair = [&](int q, const Box &lb) {
-                if (!intersects(tbx, lb)) return;
-                if (1 - iou(tbx, lb) < 0.15) {
-                    if (ta > a.lage[tb + q]) a.dropB[tb + q] = 1;
-                    else a.dropA[tb + p] = 1;
-                }
-            };
-            grid_query(gv, gh, tbx, [&](int k) { pair(gv.ids[k], gv.boxes[k]); },
-                       [&](int q) { pair(q, a.lbox[tb + q]); });
+        const int ncell = grid_cells_for(n_l2);
+        GridView gv{nullptr, ar.alloc<int>(ncell + 1), ar.alloc<int>(n_l2), ar.alloc<Box>(n_l2),
+                    ar.alloc<float4>(n_l2), nullptr, ar.alloc<int>(n_l2)};
+        Box *lcache = ar.try_alloc<Box>(n_l2);
+        auto lbox = [&](int q) { return kf_box(a.kf, tb + a.l2[tb + q]); };
+        if (lcache) {
+            for (int q = t; q < n_l2; q += nt) lcache[q] = lbox(q);
+            block_sync();
+            grid_build(n_l2, [&](int q) { return lcache[q]; }, [](int) { return 1.0; }, gv, sh.gs,
+                       wsum);
+        } else {
+            grid_build(n_l2, lbox, [](int) { return 1.0; }, gv, sh.gs, wsum);
         }
+        const GridHdr gh = sh.gs.hdr;
+        YTA_STAMP(5);
+        struct TBox {
+            long long slot;
+            Box b;
+        };
+        batched_for<4>(
+            n_t2,
+            [&](int p) {
+                TBox v;
+                v.slot = tb + a.t2[tb + p];
+                v.b = kf_box(a.kf, v.slot);
+                return v;
+            },
+            [&](int p, const TBox &v) {
+                const Box &tbx = v.b;
+                auto pair = [&](int q, const Box &lb) {
+                    if (!intersects(tbx, lb)) return;
+                    if (1 - iou(tbx, lb) < 0.15) {
+                        if (track_age(a, v.slot) > track_age(a, tb + a.l2[tb + q]))
+                            atomicOr(&dropB[q >> 5], 1u << (q & 31));
+                        else
+                            atomicOr(&dropA[p >> 5], 1u << (p & 31));
+                    }
+                };
+                grid_query(gv, gh, tbx, [&](int k) { pair(gv.ids[k], gv.boxes[k]); },
+                           [&](int q) { pair(q, lbox(q)); });
+            });
     }
-    // final lists, output rows, free slots
-    const int words = (a.CAP + 31) / 32;
-    for (int wd = t; wd < words; wd += (int)blockDim.x) live[wd] = 0u;
     block_sync();
-    const int n_tr = block_compact(n_t2, wsum, [&](int p) { return a.dropA[tb + p] == 0; },
+    YTA_STAMP(6);
+    // final lists, output rows, free slots
+    const int n_tr = block_compact(n_t2, wsum, [&](int p) { return !((dropA[p >> 5] >> (p & 31)) & 1u); },
                                    [&](int p, int pos) {
                                        const int slot = a.t2[tb + p];
                                        a.tracked[tb + pos] = slot;
                                        atomicOr(&live[slot >> 5], 1u << (slot & 31));
                                    });
-    const int n_lo = block_compact(n_l2, wsum, [&](int q) { return a.dropB[tb + q] == 0; },
+    const int n_lo = block_compact(n_l2, wsum, [&](int q) { return !((dropB[q >> 5] >> (q & 31)) & 1u); },
                                    [&](int q, int pos) {
                                        const int slot = a.l2[tb + q];
                                        a.lost[tb + pos] = slot;
                                        atomicOr(&live[slot >> 5], 1u << (slot & 31));
                                    });
     block_sync();
+    YTA_STAMP(7);
     double *out = a.out + tb * 8;
+    ar.lo = 0;   // the dedup grid is dead: its arena holds the output slot list
+    int *outslot = reinterpret_cast<int *>(ar.base);
+    const bool os_arena = ar.hi >= (size_t)4 * (n_tr > 0 ? n_tr : 1);
     const int n_out = block_compact(
         n_tr, wsum, [&](int i) { return (a.meta[tb + a.tracked[tb + i]].flags & FL_ACTIVATED) != 0; },
         [&](int i, int pos) {
-            const long long slot = tb + a.tracked[tb + i];
-            const Box b = kf_box(a.kf, slot);
-            const TrackMeta m = a.meta[slot];
-            double2 *o = reinterpret_cast<double2 *>(out + (long long)pos * 8);
-            o[0] = make_double2(b.x1, b.y1);
-            o[1] = make_double2(b.x2, b.y2);
-            o[2] = make_double2((double)m.id, m.score);
-            o[3] = make_double2(m.cls, (double)m.det_ind);
+            if (os_arena) outslot[pos] = a.tracked[tb + i];
+            else a.t2[tb + pos] = a.tracked[tb + i];   // t2 is dead: reuse as the slot list
         });
+    block_sync();
+    struct Row {
+        Box b;
+        TrackMeta m;
+    };
+    batched_for<4>(
+        n_out,
+        [&](int pos) {
+            const long long slot = tb + (os_arena ? outslot[pos] : a.t2[tb + pos]);
+            Row r;
+            r.b = kf_box(a.kf, slot);
+            r.m = a.meta[slot];
+            return r;
+        },
+        [&](int pos, const Row &r) {
+            double2 *o = reinterpret_cast<double2 *>(out + (long long)pos * 8);
+            o[0] = make_double2(r.b.x1, r.b.y1);
+            o[1] = make_double2(r.b.x2, r.b.y2);
+            o[2] = make_double2((double)r.m.id, r.m.score);
+            o[3] = make_double2(r.m.cls, (double)r.m.det_ind);
+        });
+    YTA_STAMP(8);
     const int n_fr = block_compact(a.CAP, wsum,
                                    [&](int slot) { return !((live[slot >> 5] >> (slot & 31)) & 1u); },
                                    [&](int slot, int pos) { a.free_list[tb + pos] = slot; });
+    YTA_STAMP(9);
     if (t == 0) {
         c->n_births = n_births;
         c->next_id = next_id + n_births;
@@ -558,6 +599,27 @@ __global__ __launch_bounds__(BLKF) void k_finish(BtArgs a) {
         c->n_free = n_fr;
         c->n_out = n_out;
         if (a.out_counts) a.out_counts[s] = n_out;
+    }
+}
+
+__global__ __launch_bounds__(BLKF) void k_finish(BtArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char fsmem[];
+    __shared__ FinishShared sh;
+    const int s = blockIdx.x;
+    const int words = (a.CAP + 31) / 32;
+    const size_t bits_bytes = ((size_t)12 * words + 15) & ~(size_t)15;
+    unsigned *bits = reinterpret_cast<unsigned *>(fsmem);
+    // the dedup grid's arena: LDS when lost' (<= lost + leftovers) fits, else global
+    YTA_STAMP_BASE(80);
+    YTA_STAMP(0);
+    const BtCounters *c = a.cnt + s;
+    const long long need = dedup_arena_bytes(c->n_lost + c->n_left);
+    if (need <= (long long)a.lds_bytes_f) {
+        Arena ar(fsmem + bits_bytes, a.lds_bytes_f);
+        finish_body(a, s, bits, ar, sh);
+    } else {
+        Arena ag(a.ws + s * a.ws_stride, a.ws_stride);
+        finish_body(a, s, bits, ag, sh);
     }
 }
 
@@ -628,6 +690,7 @@ namespace {
 constexpr int BT_PHASES = 4;   // launches per frame, see yta_bytetrack_profile_collect
 constexpr size_t BT_LDS_BYTES = 150 * 1024;   // k_stage1 arena (one 1024-thread block per CU)
 constexpr size_t BT_LDS23_BYTES = 32 * 1024;  // k_stage23 arena (several blocks per CU)
+constexpr size_t BT_LDSF_BYTES = 20 * 1024;   // k_finish dedup arena (several blocks per CU)
 
 template <typename T>
 int dalloc(yta_bytetrack *e, T **p, long long n) {
@@ -649,17 +712,6 @@ int dalloc(yta_bytetrack *e, T **p, long long n) {
         int _rc = dalloc(e, &(ptr), (n)); \
         if (_rc) return _rc;              \
     } while (0)
-
-int grid_alloc(yta_bytetrack *e, BtGrid &g, long long cap) {
-    g.cap = cap;
-    DALLOC(g.hdr, e->S);
-    DALLOC(g.cell, (long long)e->S * (GRID_MAX_CELLS + 1));
-    DALLOC(g.items, e->S * cap);
-    DALLOC(g.boxes, e->S * cap);
-    DALLOC(g.fbox, e->S * cap);
-    DALLOC(g.big, e->S * cap);
-    return YTA_OK;
-}
 
 int bt_alloc(yta_bytetrack *e) {
     const long long S = e->S, CAP = e->CAP, MAXD = e->MAXD;
@@ -688,8 +740,6 @@ int bt_alloc(yta_bytetrack *e) {
     DALLOC(a.second_box, S * MAXD);
     DALLOC(a.high_score, S * MAXD);
     DALLOC(a.rest_score, S * MAXD);
-    int rc = grid_alloc(e, a.grid_lost, CAP);
-    if (rc) return rc;
     DALLOC(a.pool, S * CAP);
     DALLOC(a.unc, S * CAP);
     DALLOC(a.left, S * CAP);
@@ -697,14 +747,8 @@ int bt_alloc(yta_bytetrack *e) {
     DALLOC(a.t2, S * CAP);
     DALLOC(a.l2, S * CAP);
     DALLOC(a.kind1, S * CAP);
-    DALLOC(a.dropA, S * CAP);
-    DALLOC(a.dropB, S * CAP);
     DALLOC(a.pool_box, S * CAP);
     DALLOC(a.unc_box, S * CAP);
-    DALLOC(a.tbox, S * CAP);
-    DALLOC(a.lbox, S * CAP);
-    DALLOC(a.tage, S * CAP);
-    DALLOC(a.lage, S * CAP);
     DALLOC(a.x1, S * CAP);
     DALLOC(a.x2, S * CAP);
     DALLOC(a.x3, S * CAP);
@@ -716,6 +760,7 @@ int bt_alloc(yta_bytetrack *e) {
     // candidate edge), so no frame can overflow it
     a.lds_bytes = BT_LDS_BYTES;
     a.lds_bytes23 = BT_LDS23_BYTES;
+    a.lds_bytes_f = BT_LDSF_BYTES;
     a.ws_stride = (assoc_arena_bytes(CAP, MAXD, CAP * MAXD) + 255) & ~255LL;
     DALLOC(a.ws, S * a.ws_stride);
     a.slab.R = (int)CAP;
@@ -773,8 +818,8 @@ int launch_pipeline(yta_bytetrack *e, const double *det_in, const int *det_off, 
     hipLaunchKernelGGL(k_apply, gt, dim3(APPLY_T), 0, e->stream, a);
     YTA_HIP(hipGetLastError());
     MARK();
-    const size_t live_bytes = sizeof(unsigned int) * ((a.CAP + 31) / 32);
-    hipLaunchKernelGGL(k_finish, dim3(a.S), dim3(BLKF), live_bytes, e->stream, a);
+    const size_t bits_bytes = ((size_t)12 * ((a.CAP + 31) / 32) + 15) & ~(size_t)15;
+    hipLaunchKernelGGL(k_finish, dim3(a.S), dim3(BLKF), bits_bytes + a.lds_bytes_f, e->stream, a);
     YTA_HIP(hipGetLastError());
     MARK();
     return YTA_OK;
@@ -847,6 +892,7 @@ int reserve(yta_bytetrack *e, int cap, int maxd) {
     e->allocs.swap(n->allocs);
     n->a.lds_bytes = e->a.lds_bytes;
     n->a.lds_bytes23 = e->a.lds_bytes23;
+    n->a.lds_bytes_f = e->a.lds_bytes_f;
     e->a = n->a;
     e->h_off = n->h_off;
     e->h_cnt = n->h_cnt;
@@ -1116,25 +1162,6 @@ int yta_bytetrack_profile_collect(yta_bytetrack *e, double *ms, int *frames) {
     return YTA_OK;
 }
 
-int yta_bytetrack_debug_dedup(yta_bytetrack *e, int stream, int *n_t2, int *n_l2, double *tbox,
-                              double *lbox, int *ages, int *drops) {
-    YTA_CHECK(e && n_t2 && n_l2 && tbox && lbox && ages && drops, YTA_ERR_INVALID, "null argument");
-    YTA_HIP(hipSetDevice(e->device));
-    const int rc = read_counters(e);
-    if (rc) return rc;
-    const BtCounters c = e->h_cnt[stream];
-    const long long tb = (long long)stream * e->CAP;
-    *n_t2 = c.n_t2;
-    *n_l2 = c.n_l2;
-    YTA_HIP(hipMemcpy(tbox, e->a.tbox + tb, sizeof(Box) * c.n_t2, hipMemcpyDeviceToHost));
-    YTA_HIP(hipMemcpy(lbox, e->a.lbox + tb, sizeof(Box) * c.n_l2, hipMemcpyDeviceToHost));
-    YTA_HIP(hipMemcpy(ages, e->a.tage + tb, sizeof(int) * c.n_t2, hipMemcpyDeviceToHost));
-    YTA_HIP(hipMemcpy(ages + c.n_t2, e->a.lage + tb, sizeof(int) * c.n_l2, hipMemcpyDeviceToHost));
-    YTA_HIP(hipMemcpy(drops, e->a.dropA + tb, sizeof(int) * c.n_t2, hipMemcpyDeviceToHost));
-    YTA_HIP(hipMemcpy(drops + c.n_t2, e->a.dropB + tb, sizeof(int) * c.n_l2, hipMemcpyDeviceToHost));
-    return YTA_OK;
-}
-
 int yta_bytetrack_stats(yta_bytetrack *e, long long *stats) {
     YTA_CHECK(e && stats, YTA_ERR_INVALID, "null argument");
     YTA_HIP(hipSetDevice(e->device));
@@ -1161,6 +1188,7 @@ int yta_bytetrack_set_lds(yta_bytetrack *e, int bytes) {
     YTA_HIP(hipStreamSynchronize(e->stream));
     e->a.lds_bytes = (size_t)bytes & ~(size_t)15;
     e->a.lds_bytes23 = std::min(e->a.lds_bytes, BT_LDS23_BYTES);
+    e->a.lds_bytes_f = std::min(e->a.lds_bytes, BT_LDSF_BYTES);
     YTA_HIP(hipFuncSetAttribute((const void *)k_stage1, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)std::max<size_t>(e->a.lds_bytes, BT_LDS_BYTES)));
     YTA_HIP(hipFuncSetAttribute((const void *)k_stage23, hipFuncAttributeMaxDynamicSharedMemorySize,

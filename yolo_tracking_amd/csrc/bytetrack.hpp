@@ -41,14 +41,6 @@ struct BtCounters {                  // one per stream, 128 B
 };
 static_assert(sizeof(BtCounters) == 128, "BtCounters layout");
 
-struct BtGrid {                      // one grid per stream (hdr) + cell / item arrays
-    GridHdr *hdr;                    // [S]
-    int *cell;                       // [S][GRID_MAX_CELLS + 1]
-    int *items, *big;                // [S][cap]
-    Box *boxes;                      // [S][cap]
-    float4 *fbox;                    // [S][cap]
-    long long cap;
-};
 
 struct BtArgs {
     int S, CAP, MAXD;
@@ -68,15 +60,13 @@ struct BtArgs {
     int *high, *second, *rest, *birth;
     Box *high_box, *second_box;
     double *high_score, *rest_score;
-    BtGrid grid_lost;
     // per-frame: tracks [S*CAP]
-    int *pool, *unc, *left, *left_of_pool, *t2, *l2, *kind1, *dropA, *dropB;
-    Box *pool_box, *unc_box, *tbox, *lbox;
-    int *tage, *lage;
+    int *pool, *unc, *left, *left_of_pool, *t2, *l2, *kind1;
+    Box *pool_box, *unc_box;
     // association results
     int *x1, *y1, *x2, *y2, *x3, *y3;   // x*: [S*CAP], y*: [S*MAXD]
     // association workspace: LDS arena size, per-stream global fallback arena, solver slabs
-    size_t lds_bytes, lds_bytes23;   // arenas of k_stage1 / k_stage23
+    size_t lds_bytes, lds_bytes23, lds_bytes_f;   // arenas of k_stage1 / k_stage23 / k_finish
     unsigned char *ws;
     long long ws_stride;
     LapSlab slab;             // per stream: (threads / 64) slabs

@@ -154,20 +154,53 @@ __device__ __forceinline__ int block_exclusive_scan(int v, int *wsum, int *total
     return incl - v + before;
 }
 
-// Order-preserving compaction of indices [0, n) where pred(i) holds, appended to out[*]
-// starting at `base`.  All threads of the block must call it.  Returns the count.
+// Order-preserving compaction of indices [0, n) where pred(i) holds: emit(i, position).  All
+// threads of the block must call it.  Returns the count.  Each thread owns a contiguous run of
+// up to 32 indices (predicate bits in a register), so one block scan covers n <= 32 * blockDim;
+// beyond that the range is processed in such super-chunks.
 template <typename Pred, typename Emit>
 __device__ __forceinline__ int block_compact(int n, int *wsum, Pred pred, Emit emit) {
+    const int nt = blockDim.x, t = threadIdx.x;
     int count = 0;
-    for (int start = 0; start < n; start += blockDim.x) {
-        int i = start + threadIdx.x;
-        int f = (i < n && pred(i)) ? 1 : 0;
+    for (int base = 0; base < n; base += 32 * nt) {
+        const int m = n - base < 32 * nt ? n - base : 32 * nt;
+        const int per = (m + nt - 1) / nt;
+        const int lo = base + t * per;
+        const int hi = lo + per < base + m ? lo + per : base + m;
+        unsigned bits = 0;
+        for (int i = lo; i < hi; ++i)
+            if (pred(i)) bits |= 1u << (i - lo);
         int tot;
-        int pos = block_exclusive_scan(f, wsum, &tot);
-        if (f) emit(i, count + pos);
+        int pos = count + block_exclusive_scan(__popc(bits), wsum, &tot);
+        while (bits) {
+            const int k = __ffs(bits) - 1;
+            bits &= bits - 1;
+            emit(lo + k, pos++);
+        }
         count += tot;
     }
     return count;
+}
+
+// Strided loop over [0, n) that issues the loads of B iterations before using any of them, so
+// their latencies overlap: load(i) -> value, use(i, value).
+template <int B, typename Load, typename Use>
+__device__ __forceinline__ void batched_for(int n, Load load, Use use) {
+    const int t = threadIdx.x, nt = blockDim.x;
+    using V = decltype(load(0));
+    for (int base = t; base < n; base += B * nt) {
+        V v[B];
+#pragma unroll
+        for (int b = 0; b < B; ++b) {
+            const int i = base + b * nt;
+            if (i < n) v[b] = load(i);
+        }
+#pragma unroll
+        for (int b = 0; b < B; ++b) {
+            const int i = base + b * nt;
+            if (i < n) use(i, v[b]);
+        }
+    }
 }
 
 // NumPy's np.maximum / np.minimum for float64 (NaN-propagating; first operand wins on ties).
