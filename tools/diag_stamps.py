@@ -78,6 +78,8 @@ def main():
     show(st, 20, {4: "left/rest lists", **{k: v for k, v in STAGE1.items() if k >= 5}},
          "k_stage23 stage 2")
     show(st, 40, {k: v for k, v in STAGE1.items() if k >= 5}, "k_stage23 stage 3")
+    show(st, 100, {1: "rows + scan", 2: "+ traversal/prefilter", 3: "+ exact test",
+                   4: "full count"}, "stage-1 pass-1 variants (each a full pass)")
     show(st, 80, {1: "zero bits", 2: "births", 3: "expiry", 4: "t2/l2 lists", 5: "dedup grid",
                   6: "dedup queries", 7: "final lists", 8: "output rows", 9: "free list"},
          "k_finish")

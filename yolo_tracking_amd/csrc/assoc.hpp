@@ -34,7 +34,7 @@ struct AssocShared {     // static LDS of a kernel that calls assoc_block
 // Arena bytes that suffice for one assoc_block with <= R rows, <= C columns and <= E edges (the
 // global-memory fallback arena is sized with this and E = R * C).
 __host__ __device__ inline long long assoc_arena_bytes(long long R, long long C, long long E) {
-    const long long grid = 4 * (GRID_MAX_CELLS + 1) + C * (4 + 32 + 16 + 8 + 4) + 6 * 16 +
+    const long long grid = 4 * (GRID_MAX_CELLS + 1) + C * (4 + 32 + 8 + 4) + 5 * 16 +
                            1024 * 20 + 2 * 16;   // + overflow list
     const long long top = 4 * (R + 1) + 4 * C + 12 * E + 3 * 16;
     const long long lap = 4 * (R + C) * 3 + 4 * 5 * (R + C + 1) + 8 * 16;
@@ -74,12 +74,11 @@ __device__ __forceinline__ bool assoc_block(int nr, RowBox rowbox, int nc, ColBo
     const int t = threadIdx.x, nt = blockDim.x;
     const bool use_grid = thresh <= 1.0 && nr > 0 && nc > 0;
     const size_t lo0 = ar.lo;
-    GridView gv{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+    GridView gv{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
     if (use_grid) {
         gv.cell_start = ar.alloc<int>(grid_cells_for(nc) + 1);
         gv.ids = ar.alloc<int>(nc);
         gv.boxes = ar.alloc<Box>(nc);
-        gv.fbox = ar.alloc<float4>(nc);
         gv.w = fused ? ar.alloc<double>(nc) : nullptr;
         gv.big = ar.alloc<int>(nc);
     }
@@ -119,26 +118,30 @@ __device__ __forceinline__ bool assoc_block(int nr, RowBox rowbox, int nc, ColBo
     YTA_STAMP(5);
 
     // every candidate (j, cost) of row box rb with cost < thresh
+    auto cost_of = [&](const Box &rb, const Box &cb, double w) {
+        const double dist = 1 - iou(rb, cb);                              // matching.py:117
+        return fused ? 1 - (1 - dist) * w : dist;                         // matching.py:216-220
+    };
     auto for_each_edge = [&](const Box &rb, auto &&f) {
-        auto score = [&](const Box &cb, double w, int j) {
-            const double dist = 1 - iou(rb, cb);
-            const double cost = fused ? 1 - (1 - dist) * w : dist;
-            if (cost < thresh) f(j, cost);
-        };
-        if (use_grid) {
-            grid_query(
-                gv, gh, rb,
-                [&](int k) {
-                    const Box cb = gv.boxes[k];
-                    if (intersects(rb, cb)) score(cb, fused ? gv.w[k] : 1.0, gv.ids[k]);
-                },
-                [&](int j) {
-                    const Box cb = colbox(j);
-                    if (intersects(rb, cb)) score(cb, fused ? colscore(j) : 1.0, j);
-                });
-        } else {
-            for (int j = 0; j < nc; ++j) score(colbox(j), fused ? colscore(j) : 1.0, j);
+        if (!use_grid) {
+            for (int j = 0; j < nc; ++j) {
+                const double c = cost_of(rb, colbox(j), fused ? colscore(j) : 1.0);
+                if (c < thresh) f(j, c);
+            }
+            return;
         }
+        grid_query(
+            gv, gh, rb,
+            [&](int j, const Box &cb, double w) {
+                const double c = cost_of(rb, cb, w);
+                if (c < thresh) f(j, c);
+            },
+            [&](int j) {
+                const Box cb = colbox(j);
+                if (!intersects(rb, cb)) return;
+                const double c = cost_of(rb, cb, fused ? colscore(j) : 1.0);
+                if (c < thresh) f(j, c);
+            });
     };
     // pass 1: edges per row (rows strided over the threads, chunk by chunk) -> row offsets.  The
     // first KC edges of a row in the first two chunks stay in registers; every other edge goes
@@ -150,6 +153,55 @@ __device__ __forceinline__ bool assoc_block(int nr, RowBox rowbox, int nc, ColBo
     const int ovf_n_cap = ovf_c ? ovf_cap : 0;
     if (t == 0) { sh.lap.cnt[2] = 0; sh.lap.cnt[3] = 0; }
     block_sync();
+#ifdef YTA_STAMPS
+    if (g_stamp_off == 0 && use_grid) {   // diagnostic variants of pass 1 (block 0, stage 1)
+        int sink = 0;
+        YTA_STAMP_ABS(100);
+        for (int start = 0; start < nr; start += nt) {   // rows + scan only
+            const int i = start + t;
+            int cnt = 0;
+            if (i < nr) cnt = rowbox(i).x1 > 0.0;
+            int tot;
+            sink += block_exclusive_scan(cnt, sh.lap.wsum, &tot);
+        }
+        block_sync();
+        YTA_STAMP_ABS(101);
+        for (int start = 0; start < nr; start += nt) {   // + traversal with the float prefilter
+            const int i = start + t;
+            int cnt = 0;
+            if (i < nr)
+                grid_query(gv, gh, rowbox(i), [&](int, const Box &, double) { ++cnt; },
+                           [&](int j) { ++cnt; });
+            int tot;
+            sink += block_exclusive_scan(cnt, sh.lap.wsum, &tot);
+        }
+        block_sync();
+        YTA_STAMP_ABS(102);
+        for (int start = 0; start < nr; start += nt) {   // + exact intersection test
+            const int i = start + t;
+            int cnt = 0;
+            if (i < nr) {
+                const Box rb = rowbox(i);
+                grid_query(gv, gh, rb, [&](int, const Box &cb, double) { cnt += cb.x1 < rb.x2; },
+                           [&](int j) { ++cnt; });
+            }
+            int tot;
+            sink += block_exclusive_scan(cnt, sh.lap.wsum, &tot);
+        }
+        block_sync();
+        YTA_STAMP_ABS(103);
+        for (int start = 0; start < nr; start += nt) {   // full edge count
+            const int i = start + t;
+            int cnt = 0;
+            if (i < nr) for_each_edge(rowbox(i), [&](int, double) { ++cnt; });
+            int tot;
+            sink += block_exclusive_scan(cnt, sh.lap.wsum, &tot);
+        }
+        block_sync();
+        YTA_STAMP_ABS(104);
+        if (sink == 123456789) g_stamps[105] = sink;
+    }
+#endif
     EdgeCache ea, eb;
     ea.n = eb.n = 0;
     int run = 0;

@@ -400,7 +400,7 @@ struct FinishShared {
 
 __host__ __device__ inline long long dedup_arena_bytes(long long n) {
     return 4 * (grid_cells_for((int)(n < GRID_MAX_CELLS ? n : GRID_MAX_CELLS)) + 1) +
-           n * (4 + 32 + 16 + 4) + 5 * 16;
+           n * (4 + 32 + 4) + 4 * 16;
 }
 
 __device__ __forceinline__ int track_age(const BtArgs &a, long long slot) {
@@ -496,7 +496,7 @@ __device__ __forceinline__ void finish_body(const BtArgs &a, int s, unsigned *bi
     if (n_t2 > 0 && n_l2 > 0) {
         const int ncell = grid_cells_for(n_l2);
         GridView gv{nullptr, ar.alloc<int>(ncell + 1), ar.alloc<int>(n_l2), ar.alloc<Box>(n_l2),
-                    ar.alloc<float4>(n_l2), nullptr, ar.alloc<int>(n_l2)};
+                    nullptr, ar.alloc<int>(n_l2)};
         Box *lcache = ar.try_alloc<Box>(n_l2);
         auto lbox = [&](int q) { return kf_box(a.kf, tb + a.l2[tb + q]); };
         if (lcache) {
@@ -532,7 +532,7 @@ __device__ __forceinline__ void finish_body(const BtArgs &a, int s, unsigned *bi
                             atomicOr(&dropA[p >> 5], 1u << (p & 31));
                     }
                 };
-                grid_query(gv, gh, tbx, [&](int k) { pair(gv.ids[k], gv.boxes[k]); },
+                grid_query(gv, gh, tbx, [&](int q, const Box &lb, double) { pair(q, lb); },
                            [&](int q) { pair(q, lbox(q)); });
             });
     }

@@ -38,24 +38,10 @@ struct GridView {
     int *cell_start;   // GRID_MAX_CELLS + 1
     int *ids;          // binned item ids, in cell order
     Box *boxes;        // their boxes, same order
-    float4 *fbox;      // the same boxes rounded outward to float (x1, y1 down; x2, y2 up)
     double *w;         // optional per-item weight, same order (nullptr: none)
     int *big;          // items scanned by every query
 };
 
-// float bounds that contain the double value: the prefilter on them never rejects a pair whose
-// double boxes intersect (x2 > x1' implies up(x2) >= x2 > x1' >= down(x1'); NaN fails both)
-__device__ __forceinline__ float f_down(double x) {
-    const float f = (float)x;
-    return (double)f > x ? nextafterf(f, -INFINITY) : f;
-}
-__device__ __forceinline__ float f_up(double x) {
-    const float f = (float)x;
-    return (double)f < x ? nextafterf(f, INFINITY) : f;
-}
-__device__ __forceinline__ float4 box_outward(const Box &b) {
-    return make_float4(f_down(b.x1), f_down(b.y1), f_up(b.x2), f_up(b.y2));
-}
 
 __host__ __device__ __forceinline__ bool box_usable(const Box &b) {
     const double w = b.x2 - b.x1, h = b.y2 - b.y1;
@@ -196,20 +182,20 @@ __device__ __forceinline__ void grid_build(int n, BoxOf box, WOf wof, GridView g
         const int pos = atomicAdd(&cs[cell_of(b) + 1], 1);
         gv.ids[pos] = i;
         gv.boxes[pos] = b;
-        gv.fbox[pos] = box_outward(b);
         if (gv.w) gv.w[pos] = wof(i);
     }
     block_sync();
     YTA_STAMP_ABS(116);
 }
 
-// Visit every binned item that may intersect T: visit(k) with k its position in cell order (ids,
-// boxes, w at k); the float prefilter has passed, the caller applies the exact test.  Big items:
-// visit_big(id).
-template <typename Visit, typename VisitBig>
-__device__ __forceinline__ void grid_query(const GridView &gv, const GridHdr &h, const Box &T,
-                                           Visit visit, VisitBig visit_big) {
-    for (int k = 0; k < h.n_big; ++k) visit_big(gv.big[k]);
+// grid_scan: every binned item whose box intersects T (exact float64 test): hit(k, id, box, w)
+// with k its position in cell order (w = 1 without weights).  Software-pipelined: the next cell
+// row's range is loaded while this one is scanned, and two candidates' box / id / weight are
+// loaded together before either is tested (one LDS round trip per pair).
+// grid_query: the same plus visit_big(id) for every big item (unfiltered).
+template <typename Hit>
+__device__ __forceinline__ void grid_scan(const GridView &gv, const GridHdr &h, const Box &T,
+                                          Hit hit) {
     if (h.n_binned == 0) return;
     if (!(T.x2 > T.x1 && T.y2 > T.y1)) return;   // also false for NaN: intersects nothing
     const double lx = (T.x1 - h.maxw * (1.0 + 1e-12)) - (fabs(T.x1) + h.maxw) * 1e-12;
@@ -220,15 +206,37 @@ __device__ __forceinline__ void grid_query(const GridView &gv, const GridHdr &h,
     const int cy0 = grid_cell_1d(ly, h.oy, h.inv_g, h.gy);
     const int cx1 = fx1 > (double)(h.gx - 1) ? h.gx - 1 : (int)fx1;
     const int cy1 = fy1 > (double)(h.gy - 1) ? h.gy - 1 : (int)fy1;
-    const float4 tf = box_outward(T);
+    auto wt = [&](int k) { return gv.w ? gv.w[k] : 1.0; };
+    int b = ald(gv.cell_start + cy0 * h.gx + cx0), e = ald(gv.cell_start + cy0 * h.gx + cx1 + 1);
     for (int cy = cy0; cy <= cy1; ++cy) {
-        const int base = cy * h.gx;
-        const int b = ald(gv.cell_start + base + cx0), e = ald(gv.cell_start + base + cx1 + 1);
-        for (int k = b; k < e; ++k) {   // the cells of a grid row are contiguous
-            const float4 f = gv.fbox[k];
-            if (f.z > tf.x && tf.z > f.x && f.w > tf.y && tf.w > f.y) visit(k);
+        int nb = 0, ne = 0;
+        if (cy < cy1) {
+            const int base = (cy + 1) * h.gx;
+            nb = ald(gv.cell_start + base + cx0);
+            ne = ald(gv.cell_start + base + cx1 + 1);
         }
+        int k = b;
+        for (; k + 1 < e; k += 2) {   // the cells of a grid row are contiguous
+            const Box b0 = gv.boxes[k], b1 = gv.boxes[k + 1];
+            const int i0 = gv.ids[k], i1 = gv.ids[k + 1];
+            const double w0 = wt(k), w1 = wt(k + 1);
+            if (intersects(T, b0)) hit(k, i0, b0, w0);
+            if (intersects(T, b1)) hit(k + 1, i1, b1, w1);
+        }
+        if (k < e) {
+            const Box b0 = gv.boxes[k];
+            if (intersects(T, b0)) hit(k, gv.ids[k], b0, wt(k));
+        }
+        b = nb;
+        e = ne;
     }
+}
+
+template <typename Visit, typename VisitBig>
+__device__ __forceinline__ void grid_query(const GridView &gv, const GridHdr &h, const Box &T,
+                                           Visit visit, VisitBig visit_big) {
+    for (int k = 0; k < h.n_big; ++k) visit_big(gv.big[k]);
+    grid_scan(gv, h, T, [&](int, int id, const Box &b, double w) { visit(id, b, w); });
 }
 
 }  // namespace yta

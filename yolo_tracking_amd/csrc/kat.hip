@@ -116,11 +116,11 @@ __global__ __launch_bounds__(1024) void k_lap_dense(const double *cost, int nr, 
 // (the shape of remove_duplicate_stracks, byte_tracker.py:312-325).
 __global__ __launch_bounds__(1024) void k_grid_pairs(const Box *a, int na, const Box *b, int nb,
                                                     double thresh, GridHdr *hdr, int *cell,
-                                                    int *ids, Box *boxes, float4 *fbox, int *big,
+                                                    int *ids, Box *boxes, int *big,
                                                     int *pairs, int *n_pairs, int cap) {
     __shared__ int wsum[32];
     __shared__ GridScratch gs;
-    const GridView gv{hdr, cell, ids, boxes, fbox, nullptr, big};
+    const GridView gv{hdr, cell, ids, boxes, nullptr, big};
     grid_build(nb, [&](int q) { return b[q]; }, [](int) { return 1.0; }, gv, gs, wsum);
     const GridHdr h = gs.hdr;
     for (int p = threadIdx.x; p < na; p += blockDim.x) {
@@ -132,7 +132,7 @@ __global__ __launch_bounds__(1024) void k_grid_pairs(const Box *a, int na, const
                 if (k < cap) { pairs[2 * k] = p; pairs[2 * k + 1] = q; }
             }
         };
-        grid_query(gv, h, T, [&](int k) { pair(gv.ids[k], gv.boxes[k]); },
+        grid_query(gv, h, T, [&](int q, const Box &lb, double) { pair(q, lb); },
                    [&](int q) { pair(q, b[q]); });
     }
 }
@@ -286,7 +286,6 @@ int yta_grid_pairs(int device, const double *a, int na, const double *b, int nb,
     if (rc) return rc;
     DevBuf m;
     Box *da, *db, *boxes;
-    float4 *fbox;
     GridHdr *hdr;
     int *cell, *ids, *big, *dp, *dn;
     YTA_HIP(m.get(&da, na));
@@ -295,7 +294,6 @@ int yta_grid_pairs(int device, const double *a, int na, const double *b, int nb,
     YTA_HIP(m.get(&cell, GRID_MAX_CELLS + 1));
     YTA_HIP(m.get(&ids, nb));
     YTA_HIP(m.get(&boxes, nb));
-    YTA_HIP(m.get(&fbox, nb));
     YTA_HIP(m.get(&big, nb));
     YTA_HIP(m.get(&dp, 2 * (size_t)(cap > 0 ? cap : 1)));
     YTA_HIP(m.get(&dn, 1));
@@ -303,7 +301,7 @@ int yta_grid_pairs(int device, const double *a, int na, const double *b, int nb,
     YTA_HIP(hipMemcpy(db, b, sizeof(Box) * nb, hipMemcpyHostToDevice));
     YTA_HIP(hipMemset(dn, 0, sizeof(int)));
     hipLaunchKernelGGL(k_grid_pairs, dim3(1), dim3(1024), 0, 0, da, na, db, nb, thresh, hdr, cell,
-                       ids, boxes, fbox, big, dp, dn, cap);
+                       ids, boxes, big, dp, dn, cap);
     YTA_HIP(hipGetLastError());
     YTA_HIP(hipMemcpy(n_pairs, dn, sizeof(int), hipMemcpyDeviceToHost));
     const int n = *n_pairs < cap ? *n_pairs : cap;
