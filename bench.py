@@ -62,12 +62,26 @@ def kernel_bytes(phase, st):
     return 0
 
 
+def pmc_traffic(streams, n):
+    """HBM bytes per launch of the roofline kernel from the committed rocprofv3 PMC summary
+    (profiles/roofline_traffic.json, FETCH_SIZE x 2 + WRITE_SIZE in separate passes), when it
+    was measured on this same workload; else None."""
+    f = os.path.join(REPO, "profiles", "roofline_traffic.json")
+    try:
+        d = json.load(open(f))
+    except (OSError, ValueError):
+        return None, None
+    if d.get("streams") == streams and d.get("n") == n:
+        return d["hbm_bytes_per_launch"], d.get("tag")
+    return None, None
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=30)
     p.add_argument("--warmup", type=int, default=5)
-    p.add_argument("--streams", type=int, default=64, help="streams per GPU")
+    p.add_argument("--streams", type=int, default=1024, help="streams per GPU")
     p.add_argument("--n", type=int, default=1024, help="tracks = detections per frame")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-frames", type=int, default=40)
@@ -190,6 +204,7 @@ def main():
                           "gbs": (kernel_bytes(p, st) / (phase_ms[p] * 1e-3) / 1e9
                                   if phase_ms[p] > 0 else 0.0)} for p in PHASES}
         cpu = None if args.no_cpu_baseline else cpu_baseline(N, args.cpu_frames, args.seed)
+        traffic, traffic_tag = pmc_traffic(S, N)
         line = {
             "metric": "tracker.update() calls/sec @ 1024 tracks×1024 dets; 1/2/4/8 MI355X",
             "value": value, "unit": "calls/s", "n_gpus": world, "steps": args.steps,
@@ -200,7 +215,9 @@ def main():
                        "parallelism": f"stream-sharded x{world}"},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "traffic_source": (f"profiles/{traffic_tag}_summary.json (rocprofv3 "
+                                            "FETCH_SIZE x2 + WRITE_SIZE)" if traffic else None),
                          "algorithmic_bytes_per_launch": b, "avg_launch_ms": dom_ms},
             "cpu_baseline": cpu,
             "per_kernel": per_kernel,

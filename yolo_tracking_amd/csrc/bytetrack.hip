@@ -127,10 +127,10 @@ __device__ __forceinline__ bool stage1_body(const BtArgs &a, int s, Arena &ar, S
     const int n_tracked = c->n_tracked, n_lost = c->n_lost;
     const int *tracked = a.tracked + tb;
     const int n_act = block_compact(
-        n_tracked, wsum, [&](int i) { return (a.meta[tb + tracked[i]].flags & FL_ACTIVATED) != 0; },
+        n_tracked, wsum, [&](int i) { return (a.flags[tb + tracked[i]] & FL_ACTIVATED) != 0; },
         [&](int i, int pos) { a.pool[tb + pos] = tracked[i]; });
     const int n_unc = block_compact(
-        n_tracked, wsum, [&](int i) { return (a.meta[tb + tracked[i]].flags & FL_ACTIVATED) == 0; },
+        n_tracked, wsum, [&](int i) { return (a.flags[tb + tracked[i]] & FL_ACTIVATED) == 0; },
         [&](int i, int pos) { a.unc[tb + pos] = tracked[i]; });
     for (int i = t; i < n_lost; i += nt) a.pool[tb + n_act + i] = a.lost[tb + i];
     block_sync();
@@ -139,7 +139,7 @@ __device__ __forceinline__ bool stage1_body(const BtArgs &a, int s, Arena &ar, S
     for (int i = t; i < n_pool; i += nt) {
         const long long slot = tb + a.pool[tb + i];
         const double *m = a.kf + slot * KF_REC;
-        const double vh = st_of(a.meta[slot].flags) == ST_TRACKED ? m[7] : 0.0;
+        const double vh = st_of(a.flags[slot]) == ST_TRACKED ? m[7] : 0.0;
         a.pool_box[tb + i] = xyah_mean_to_box(m[0] + m[4], m[1] + m[5], m[2] + m[6], m[3] + vh);
     }
     for (int j = t; j < n_unc; j += nt) a.unc_box[tb + j] = kf_box(a.kf, tb + a.unc[tb + j]);
@@ -181,7 +181,7 @@ __device__ __forceinline__ bool stage23_body(const BtArgs &a, int s, Arena &ar, 
     const int n_left = block_compact(
         n_pool, wsum,
         [&](int i) {
-            return a.x1[tb + i] < 0 && st_of(a.meta[tb + a.pool[tb + i]].flags) == ST_TRACKED;
+            return a.x1[tb + i] < 0 && st_of(a.flags[tb + a.pool[tb + i]]) == ST_TRACKED;
         },
         [&](int i, int pos) {
             a.left[tb + pos] = i;
@@ -252,11 +252,11 @@ __global__ __launch_bounds__(BLK23) void k_stage23(BtArgs a) {
 
 // ------------------------------------------------------------------------------------ k_apply
 __device__ __forceinline__ void take_detection(const BtArgs &a, KfState &st, TrackMeta &m,
-                                               long long det, int det_local, int fid) {
+                                               int &flags, long long det, int det_local, int fid) {
     kf_update(st, a.det_xyah + det * 4);
-    const bool reactivate = st_of(m.flags) != ST_TRACKED;
+    const bool reactivate = st_of(flags) != ST_TRACKED;
     m.tracklet_len = reactivate ? 0 : m.tracklet_len + 1;
-    m.flags = (m.flags & ~FL_STATE) | ST_TRACKED | FL_ACTIVATED;
+    flags = (flags & ~FL_STATE) | ST_TRACKED | FL_ACTIVATED;
     m.frame_id = fid;
     m.score = a.det_conf[det];
     m.cls = a.det_cls[det];
@@ -317,7 +317,10 @@ __global__ __launch_bounds__(APPLY_T) void k_apply(BtArgs a) {
             }
         }
         s_slot[t] = slot;
+        // pieces this track rewrites: bit 0 the Kalman record, bit 1 the meta
+        s_wmask[t] = act == 5 ? 0 : (act == 1 || act == 2 || act == 4 ? 3 : 1);
     }
+    const int flags0 = t < nloc ? a.flags[tb + slot] : 0;
     __syncthreads();
     // cooperative load
     const double2 *kf2 = reinterpret_cast<const double2 *>(a.kf);
@@ -325,7 +328,7 @@ __global__ __launch_bounds__(APPLY_T) void k_apply(BtArgs a) {
     for (int p = t; p < nloc * REC_PIECES; p += APPLY_T) {
         const int r = p / REC_PIECES, k = p - r * REC_PIECES;
         const long long sl = tb + s_slot[r];
-        rec[r][k] = k < 12 ? kf2[sl * 12 + k] : meta2[sl * 3 + (k - 12)];
+        rec[r][k] = k < 12 ? kf2[sl * 12 + k] : meta2[sl * 3 + (k - 12)];   // whole records
     }
     __syncthreads();
     if (t < nloc) {
@@ -333,22 +336,22 @@ __global__ __launch_bounds__(APPLY_T) void k_apply(BtArgs a) {
         double *row = reinterpret_cast<double *>(rec[t]);
         TrackMeta m;
         memcpy(&m, row + KF_REC, sizeof(TrackMeta));
+        int flags = flags0;
         int wmask = 0;
         if (act <= 3) {
 #pragma unroll
             for (int k = 0; k < 8; ++k) st.m[k] = row[k];
 #pragma unroll
             for (int k = 0; k < 16; ++k) st.c[k] = row[8 + k];
-            const bool tracked = st_of(m.flags) == ST_TRACKED;
+            const bool tracked = st_of(flags) == ST_TRACKED;
             if (!tracked) st.m[7] = 0;                               // :41-42
             kf_predict(st);
             wmask = 1;
             if (act == 1 || act == 2) {
-                take_detection(a, st, m, db + det, det, fid);
+                take_detection(a, st, m, flags, db + det, det, fid);
                 wmask = 3;
             } else if (act == 3) {
-                m.flags = (m.flags & ~FL_STATE) | ST_LOST;
-                wmask = 3;
+                flags = (flags & ~FL_STATE) | ST_LOST;
             }
             // stage-1 outcome for the tracked' list order: 1 tracked -> updated, 2 re-found
             a.kind1[tb + i] = act == 1 ? (tracked ? 1 : 2) : 0;
@@ -357,12 +360,12 @@ __global__ __launch_bounds__(APPLY_T) void k_apply(BtArgs a) {
             for (int k = 0; k < 8; ++k) st.m[k] = row[k];
 #pragma unroll
             for (int k = 0; k < 16; ++k) st.c[k] = row[8 + k];
-            take_detection(a, st, m, db + det, det, fid);
+            take_detection(a, st, m, flags, db + det, det, fid);
             wmask = 3;
         } else {
-            m.flags = (m.flags & ~FL_STATE) | ST_REMOVED | FL_REMOVED_NOW;
-            wmask = 2;
+            flags = (flags & ~FL_STATE) | ST_REMOVED | FL_REMOVED_NOW;
         }
+        if (flags != flags0) a.flags[tb + slot] = flags;
         if (wmask & 1) {
 #pragma unroll
             for (int k = 0; k < 8; ++k) row[k] = st.m[k];
@@ -370,7 +373,6 @@ __global__ __launch_bounds__(APPLY_T) void k_apply(BtArgs a) {
             for (int k = 0; k < 16; ++k) row[8 + k] = st.c[k];
         }
         if (wmask & 2) memcpy(row + KF_REC, &m, sizeof(TrackMeta));
-        s_wmask[t] = wmask;
     }
     __syncthreads();
     // cooperative store of what changed
@@ -442,7 +444,8 @@ __device__ __forceinline__ void finish_body(const BtArgs &a, int s, unsigned *bi
         m.cls = a.det_cls[db + d];
         m.id = next_id + 1 + b;
         m.det_ind = d;
-        m.flags = ST_TRACKED | (fid == 1 ? FL_ACTIVATED : 0);
+        m.spare = 0;
+        a.flags[tb + slot] = ST_TRACKED | (fid == 1 ? FL_ACTIVATED : 0);
         m.frame_id = fid;
         m.start_frame = fid;
         m.tracklet_len = 0;
@@ -453,16 +456,15 @@ __device__ __forceinline__ void finish_body(const BtArgs &a, int s, unsigned *bi
     // lost-track expiry (:250-253); end_frame == frame_id
     for (int i = t; i < n_lost; i += nt) {
         const long long slot = tb + a.lost[tb + i];
-        const TrackMeta m = a.meta[slot];
-        if (fid - m.frame_id > a.max_time_lost)
-            a.meta[slot].flags = (m.flags & ~FL_STATE) | ST_REMOVED | FL_REMOVED_NOW;
+        if (fid - a.meta[slot].frame_id > a.max_time_lost)
+            a.flags[slot] = (a.flags[slot] & ~FL_STATE) | ST_REMOVED | FL_REMOVED_NOW;
     }
     block_sync();
     YTA_STAMP(3);
     // tracked' = [Tracked survivors of tracked_stracks] ++ births ++ re-found (:257-261)
     int n_t2 = block_compact(
         n_tracked, wsum,
-        [&](int i) { return st_of(a.meta[tb + a.tracked[tb + i]].flags) == ST_TRACKED; },
+        [&](int i) { return st_of(a.flags[tb + a.tracked[tb + i]]) == ST_TRACKED; },
         [&](int i, int pos) { a.t2[tb + pos] = a.tracked[tb + i]; });
     for (int b = t; b < n_births; b += nt) a.t2[tb + n_t2 + b] = a.free_list[tb + b];
     n_t2 += n_births;
@@ -472,7 +474,7 @@ __device__ __forceinline__ void finish_body(const BtArgs &a, int s, unsigned *bi
     int n_l2 = block_compact(
         n_lost, wsum,
         [&](int i) {
-            const int f = a.meta[tb + a.lost[tb + i]].flags;
+            const int f = a.flags[tb + a.lost[tb + i]];
             return st_of(f) != ST_TRACKED && !(f & FL_EVER_REMOVED);
         },
         [&](int i, int pos) { a.l2[tb + pos] = a.lost[tb + i]; });
@@ -480,7 +482,7 @@ __device__ __forceinline__ void finish_body(const BtArgs &a, int s, unsigned *bi
         n_left, wsum,
         [&](int i) {
             return a.x2[tb + i] < 0 &&
-                   !(a.meta[tb + a.pool[tb + a.left[tb + i]]].flags & FL_EVER_REMOVED);
+                   !(a.flags[tb + a.pool[tb + a.left[tb + i]]] & FL_EVER_REMOVED);
         },
         [&](int i, int pos) { a.l2[tb + n_l2 + pos] = a.pool[tb + a.left[tb + i]]; });
     block_sync();
@@ -488,8 +490,8 @@ __device__ __forceinline__ void finish_body(const BtArgs &a, int s, unsigned *bi
     // this frame's removals join removed_stracks only now (:265)
     for (int i = t; i < n_lost; i += nt) {
         const long long slot = tb + a.lost[tb + i];
-        const int f = a.meta[slot].flags;
-        if (f & FL_REMOVED_NOW) a.meta[slot].flags = (f & ~FL_REMOVED_NOW) | FL_EVER_REMOVED;
+        const int f = a.flags[slot];
+        if (f & FL_REMOVED_NOW) a.flags[slot] = (f & ~FL_REMOVED_NOW) | FL_EVER_REMOVED;
     }
     // remove_duplicate_stracks (:312-325): pairs with 1 - IoU < 0.15 drop the younger track (set
     // semantics, so pairs are visited in any order)
@@ -558,7 +560,7 @@ __device__ __forceinline__ void finish_body(const BtArgs &a, int s, unsigned *bi
     int *outslot = reinterpret_cast<int *>(ar.base);
     const bool os_arena = ar.hi >= (size_t)4 * (n_tr > 0 ? n_tr : 1);
     const int n_out = block_compact(
-        n_tr, wsum, [&](int i) { return (a.meta[tb + a.tracked[tb + i]].flags & FL_ACTIVATED) != 0; },
+        n_tr, wsum, [&](int i) { return (a.flags[tb + a.tracked[tb + i]] & FL_ACTIVATED) != 0; },
         [&](int i, int pos) {
             if (os_arena) outslot[pos] = a.tracked[tb + i];
             else a.t2[tb + pos] = a.tracked[tb + i];   // t2 is dead: reuse as the slot list
@@ -725,6 +727,7 @@ int bt_alloc(yta_bytetrack *e) {
     a.max_time_lost = (int)(e->prm.frame_rate / 30.0 * e->prm.track_buffer);   // :128-129
     DALLOC(a.kf, S * CAP * KF_REC);
     DALLOC(a.meta, S * CAP);
+    DALLOC(a.flags, S * CAP);
     DALLOC(a.tracked, S * CAP);
     DALLOC(a.lost, S * CAP);
     DALLOC(a.free_list, S * CAP);
@@ -859,6 +862,7 @@ int reserve(yta_bytetrack *e, int cap, int maxd) {
     if (!rc) rc = copy2d(n->a.kf, nc * KF_REC * 8, e->a.kf, oc * KF_REC * 8, oc * KF_REC * 8, S);
     if (!rc) rc = copy2d(n->a.meta, nc * sizeof(TrackMeta), e->a.meta, oc * sizeof(TrackMeta),
                          oc * sizeof(TrackMeta), S);
+    if (!rc) rc = copy2d(n->a.flags, nc * 4, e->a.flags, oc * 4, oc * 4, S);
     if (!rc) rc = copy2d(n->a.tracked, nc * 4, e->a.tracked, oc * 4, oc * 4, S);
     if (!rc) rc = copy2d(n->a.lost, nc * 4, e->a.lost, oc * 4, oc * 4, S);
     if (!rc) {
@@ -985,6 +989,7 @@ int yta_bytetrack_reset(yta_bytetrack *e) {
     hipLaunchKernelGGL(k_reset, dim3(e->S), dim3(256), 0, e->stream, e->a);
     YTA_HIP(hipGetLastError());
     YTA_HIP(hipMemsetAsync(e->a.meta, 0, sizeof(TrackMeta) * (size_t)e->S * e->CAP, e->stream));
+    YTA_HIP(hipMemsetAsync(e->a.flags, 0, sizeof(int) * (size_t)e->S * e->CAP, e->stream));
     YTA_HIP(hipStreamSynchronize(e->stream));
     memset(e->h_cnt, 0, sizeof(BtCounters) * e->S);
     return YTA_OK;
@@ -1101,6 +1106,7 @@ int yta_bytetrack_get_state(yta_bytetrack *e, int stream, int *n_tracks, long lo
     std::vector<int> tr(c.n_tracked), lo(c.n_lost);
     std::vector<double> kf((size_t)e->CAP * KF_REC);
     std::vector<TrackMeta> meta(e->CAP);
+    std::vector<int> flags(e->CAP);
     if (c.n_tracked)
         YTA_HIP(hipMemcpy(tr.data(), e->a.tracked + tb, sizeof(int) * c.n_tracked,
                           hipMemcpyDeviceToHost));
@@ -1110,6 +1116,7 @@ int yta_bytetrack_get_state(yta_bytetrack *e, int stream, int *n_tracks, long lo
                       hipMemcpyDeviceToHost));
     YTA_HIP(hipMemcpy(meta.data(), e->a.meta + tb, sizeof(TrackMeta) * e->CAP,
                       hipMemcpyDeviceToHost));
+    YTA_HIP(hipMemcpy(flags.data(), e->a.flags + tb, sizeof(int) * e->CAP, hipMemcpyDeviceToHost));
     int n = 0;
     for (int which = 0; which < 2; ++which) {
         const std::vector<int> &lst = which ? lo : tr;
@@ -1118,8 +1125,8 @@ int yta_bytetrack_get_state(yta_bytetrack *e, int stream, int *n_tracks, long lo
             long long *ii = ints + (long long)n * 7;
             ii[0] = which;
             ii[1] = m.id;
-            ii[2] = m.flags & FL_STATE;
-            ii[3] = (m.flags & FL_ACTIVATED) ? 1 : 0;
+            ii[2] = flags[slot] & FL_STATE;
+            ii[3] = (flags[slot] & FL_ACTIVATED) ? 1 : 0;
             ii[4] = m.frame_id;
             ii[5] = m.start_frame;
             ii[6] = m.tracklet_len;

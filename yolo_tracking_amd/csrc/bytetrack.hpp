@@ -17,7 +17,7 @@ struct TrackMeta {                   // 48 B, one per slot
     double cls;
     long long id;
     int det_ind;
-    int flags;
+    int spare;                       // (the state flags live in BtArgs::flags)
     int frame_id;
     int start_frame;
     int tracklet_len;
@@ -52,6 +52,7 @@ struct BtArgs {
     // persistent state
     double *kf;               // [S*CAP][KF_REC]
     TrackMeta *meta;          // [S*CAP]
+    int *flags;               // [S*CAP] state + FL_* bits, dense: every list scan reads these
     int *tracked, *lost, *free_list;   // [S*CAP]
     BtCounters *cnt;          // [S]
     // per-frame: detections [S*MAXD]
