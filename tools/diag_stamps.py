@@ -20,7 +20,7 @@ sys.path.insert(0, REPO)
 CSRC = os.path.join(REPO, "yolo_tracking_amd", "csrc")
 OUT = os.path.join(REPO, "tools", "_diag", "libyta_diag.so")
 
-STAGE1 = {1: "dets convert", 2: "high/second lists", 3: "act/unc/pool lists", 4: "pool boxes",
+STAGE1 = {2: "dets pass", 4: "tracked/lost pass",
           5: "grid build", 6: "edges pass 1", 7: "edges pass 2", 8: "lap init", 9: "lap P1 union",
           10: "lap P2 roots", 11: "lap P3 lists", 12: "lap P4 gather", 13: "lap classify",
           14: "lap solve"}
@@ -78,13 +78,11 @@ def main():
     show(st, 20, {4: "left/rest lists", **{k: v for k, v in STAGE1.items() if k >= 5}},
          "k_stage23 stage 2")
     show(st, 40, {k: v for k, v in STAGE1.items() if k >= 5}, "k_stage23 stage 3")
-    show(st, 100, {1: "rows + scan", 2: "+ traversal/prefilter", 3: "+ exact test",
-                   4: "full count"}, "stage-1 pass-1 variants (each a full pass)")
     show(st, 80, {1: "zero bits", 2: "births", 3: "expiry", 4: "t2/l2 lists", 5: "dedup grid",
                   6: "dedup queries", 7: "final lists", 8: "output rows", 9: "free list"},
          "k_finish")
-    show(st, 110, {1: "mean reduce", 2: "extent reduce", 3: "zero cells", 4: "count",
-                  5: "cell scan", 6: "scatter"}, "grid_build (last call)")
+    show(st, 110, {1: "reduce", 2: "zero cells", 3: "count", 5: "cell scan", 6: "scatter"},
+         "grid_build (last call)")
 
 
 if __name__ == "__main__":

@@ -70,7 +70,9 @@ template <typename RowBox, typename ColBox, typename ColScore>
 __device__ __forceinline__ bool assoc_block(int nr, RowBox rowbox, int nc, ColBox colbox,
                                             bool fused, ColScore colscore, double thresh, int *X,
                                             int *Y, int *err, int *n_edges, Arena &ar,
-                                            const LapSlab &slab, AssocShared &sh) {
+                                            const LapSlab &slab, AssocShared &sh,
+                                            const Box *ext_cbox = nullptr,
+                                            const double *ext_cw = nullptr) {
     const int t = threadIdx.x, nt = blockDim.x;
     const bool use_grid = thresh <= 1.0 && nr > 0 && nc > 0;
     const size_t lo0 = ar.lo;
@@ -86,7 +88,9 @@ __device__ __forceinline__ bool assoc_block(int nr, RowBox rowbox, int nc, ColBo
     int *col_deg = ar.alloc_top<int>(nc);
     if (ar.fail) return false;
     const size_t hi0 = ar.hi;
-    Box *ccache = use_grid ? ar.try_alloc_top<Box>(nc) : nullptr;
+    // column boxes / weights staged in the arena: by the caller (ext_*), else here if room
+    const bool ext = ext_cbox && (!fused || ext_cw);
+    Box *ccache = ext ? nullptr : (use_grid ? ar.try_alloc_top<Box>(nc) : nullptr);
     double *wcache = nullptr;
     if (ccache && fused) {
         wcache = ar.try_alloc_top<double>(nc);
@@ -102,12 +106,14 @@ __device__ __forceinline__ bool assoc_block(int nr, RowBox rowbox, int nc, ColBo
             if (wcache) wcache[j] = colscore(j);
         }
     }
+    const Box *cb_src = ext ? ext_cbox : ccache;
+    const double *cw_src = ext ? ext_cw : wcache;
     if (use_grid) {
         block_sync();
-        if (ccache)
+        if (cb_src)
             grid_build(
-                nc, [&](int j) { return ccache[j]; },
-                [&](int j) { return wcache ? wcache[j] : 1.0; }, gv, sh.gs, sh.lap.wsum);
+                nc, [&](int j) { return cb_src[j]; },
+                [&](int j) { return cw_src ? cw_src[j] : 1.0; }, gv, sh.gs, sh.lap.wsum);
         else
             grid_build(
                 nc, [&](int j) { return colbox(j); },
@@ -153,55 +159,6 @@ __device__ __forceinline__ bool assoc_block(int nr, RowBox rowbox, int nc, ColBo
     const int ovf_n_cap = ovf_c ? ovf_cap : 0;
     if (t == 0) { sh.lap.cnt[2] = 0; sh.lap.cnt[3] = 0; }
     block_sync();
-#ifdef YTA_STAMPS
-    if (g_stamp_off == 0 && use_grid) {   // diagnostic variants of pass 1 (block 0, stage 1)
-        int sink = 0;
-        YTA_STAMP_ABS(100);
-        for (int start = 0; start < nr; start += nt) {   // rows + scan only
-            const int i = start + t;
-            int cnt = 0;
-            if (i < nr) cnt = rowbox(i).x1 > 0.0;
-            int tot;
-            sink += block_exclusive_scan(cnt, sh.lap.wsum, &tot);
-        }
-        block_sync();
-        YTA_STAMP_ABS(101);
-        for (int start = 0; start < nr; start += nt) {   // + traversal with the float prefilter
-            const int i = start + t;
-            int cnt = 0;
-            if (i < nr)
-                grid_query(gv, gh, rowbox(i), [&](int, const Box &, double) { ++cnt; },
-                           [&](int j) { ++cnt; });
-            int tot;
-            sink += block_exclusive_scan(cnt, sh.lap.wsum, &tot);
-        }
-        block_sync();
-        YTA_STAMP_ABS(102);
-        for (int start = 0; start < nr; start += nt) {   // + exact intersection test
-            const int i = start + t;
-            int cnt = 0;
-            if (i < nr) {
-                const Box rb = rowbox(i);
-                grid_query(gv, gh, rb, [&](int, const Box &cb, double) { cnt += cb.x1 < rb.x2; },
-                           [&](int j) { ++cnt; });
-            }
-            int tot;
-            sink += block_exclusive_scan(cnt, sh.lap.wsum, &tot);
-        }
-        block_sync();
-        YTA_STAMP_ABS(103);
-        for (int start = 0; start < nr; start += nt) {   // full edge count
-            const int i = start + t;
-            int cnt = 0;
-            if (i < nr) for_each_edge(rowbox(i), [&](int, double) { ++cnt; });
-            int tot;
-            sink += block_exclusive_scan(cnt, sh.lap.wsum, &tot);
-        }
-        block_sync();
-        YTA_STAMP_ABS(104);
-        if (sink == 123456789) g_stamps[105] = sink;
-    }
-#endif
     EdgeCache ea, eb;
     ea.n = eb.n = 0;
     int run = 0;

@@ -94,62 +94,85 @@ __device__ __forceinline__ bool stage1_body(const BtArgs &a, int s, Arena &ar, S
     }
     const double *din = a.det_in + (long long)a.det_off[s] * 6;
     const double thr = a.track_thresh;
-    for (int i = t; i < nd; i += nt) {
-        const double *d = din + (long long)i * 6;
-        double xywh[4];
-        det_xyxy_to_xywh(d, xywh);                       // STrack.__init__ (:16-18)
-        xywh_to_xyah(xywh, a.det_xyah + (db + i) * 4);
-        a.det_conf[db + i] = d[4];
-        a.det_cls[db + i] = d[5];
-    }
-    block_sync();
-    YTA_STAMP(1);
-    const double *conf = a.det_conf + db;
     auto det_box = [&](int i) {                          // STrack.xyxy with mean None (:105-106)
         const double *d = din + (long long)i * 6;
         double xywh[4];
         det_xyxy_to_xywh(d, xywh);
         return xywh_to_box(xywh);
     };
-    const int n_high = block_compact(nd, wsum, [&](int i) { return conf[i] > thr; },
-                                     [&](int i, int pos) {
-                                         a.high[db + pos] = i;
-                                         a.high_box[db + pos] = det_box(i);
-                                         a.high_score[db + pos] = conf[i];
-                                     });
-    const int n_second = block_compact(nd, wsum,
-                                       [&](int i) { return conf[i] > 0.1 && conf[i] < thr; },
-                                       [&](int i, int pos) {
-                                           a.second[db + pos] = i;
-                                           a.second_box[db + pos] = det_box(i);
-                                       });
+    // the high detections' boxes / scores staged in the arena for the stage-1 grid (top end,
+    // sized for every detection; skipped when the arena has no room)
+    Box *hbox = ar.try_alloc_top<Box>(nd);
+    double *hw = hbox ? ar.try_alloc_top<double>(nd) : nullptr;
+    if (!hw) hbox = nullptr;
+    // detections: STrack conversions (:16-18) and the confidence split (:149-158), one pass
+    const int2 hs = block_compact2(
+        nd, wsum,
+        [&](int i) {
+            const double *d = din + (long long)i * 6;
+            double xywh[4];
+            det_xyxy_to_xywh(d, xywh);
+            xywh_to_xyah(xywh, a.det_xyah + (db + i) * 4);
+            const double conf = d[4];
+            a.det_conf[db + i] = conf;
+            a.det_cls[db + i] = d[5];
+            return conf > thr ? 1 : (conf > 0.1 && conf < thr ? 2 : 0);
+        },
+        [&](int i, int cat, int pos) {
+            const Box b = det_box(i);
+            if (cat == 1) {
+                const double conf = din[(long long)i * 6 + 4];
+                a.high[db + pos] = i;
+                a.high_box[db + pos] = b;
+                a.high_score[db + pos] = conf;
+                if (hbox) {
+                    hbox[pos] = b;
+                    hw[pos] = conf;
+                }
+            } else {
+                a.second[db + pos] = i;
+                a.second_box[db + pos] = b;
+            }
+        });
+    const int n_high = hs.x, n_second = hs.y;
     YTA_STAMP(2);
+    // tracked -> activated (pool head) / unconfirmed (:169-178), with their boxes: predicted for
+    // the pool (mean only; multi_predict :35-48 zeroes vh of non-tracked tracks, the covariance is
+    // advanced in k_apply), current for the unconfirmed (not predicted)
     const int n_tracked = c->n_tracked, n_lost = c->n_lost;
     const int *tracked = a.tracked + tb;
-    const int n_act = block_compact(
-        n_tracked, wsum, [&](int i) { return (a.flags[tb + tracked[i]] & FL_ACTIVATED) != 0; },
-        [&](int i, int pos) { a.pool[tb + pos] = tracked[i]; });
-    const int n_unc = block_compact(
-        n_tracked, wsum, [&](int i) { return (a.flags[tb + tracked[i]] & FL_ACTIVATED) == 0; },
-        [&](int i, int pos) { a.unc[tb + pos] = tracked[i]; });
-    for (int i = t; i < n_lost; i += nt) a.pool[tb + n_act + i] = a.lost[tb + i];
-    block_sync();
-    YTA_STAMP(3);
-    const int n_pool = n_act + n_lost;
-    for (int i = t; i < n_pool; i += nt) {
-        const long long slot = tb + a.pool[tb + i];
+    auto pred_box = [&](long long slot) {
         const double *m = a.kf + slot * KF_REC;
         const double vh = st_of(a.flags[slot]) == ST_TRACKED ? m[7] : 0.0;
-        a.pool_box[tb + i] = xyah_mean_to_box(m[0] + m[4], m[1] + m[5], m[2] + m[6], m[3] + vh);
+        return xyah_mean_to_box(m[0] + m[4], m[1] + m[5], m[2] + m[6], m[3] + vh);
+    };
+    const int2 au = block_compact2(
+        n_tracked, wsum,
+        [&](int i) { return (a.flags[tb + tracked[i]] & FL_ACTIVATED) ? 1 : 2; },
+        [&](int i, int cat, int pos) {
+            const int slot = tracked[i];
+            if (cat == 1) {
+                a.pool[tb + pos] = slot;
+                a.pool_box[tb + pos] = pred_box(tb + slot);
+            } else {
+                a.unc[tb + pos] = slot;
+                a.unc_box[tb + pos] = kf_box(a.kf, tb + slot);
+            }
+        });
+    const int n_act = au.x, n_unc = au.y;
+    for (int i = t; i < n_lost; i += nt) {
+        const int slot = a.lost[tb + i];
+        a.pool[tb + n_act + i] = slot;
+        a.pool_box[tb + n_act + i] = pred_box(tb + slot);
     }
-    for (int j = t; j < n_unc; j += nt) a.unc_box[tb + j] = kf_box(a.kf, tb + a.unc[tb + j]);
+    const int n_pool = n_act + n_lost;
     block_sync();
     YTA_STAMP(4);
     const bool ok = assoc_block(
         n_pool, [&](int i) { return a.pool_box[tb + i]; }, n_high,
         [&](int j) { return a.high_box[db + j]; }, true,
         [&](int j) { return a.high_score[db + j]; }, a.match_thresh, a.x1 + tb, a.y1 + db, &c->err,
-        &c->n_edges[0], ar, slab_of(a, s), sh.as);
+        &c->n_edges[0], ar, slab_of(a, s), sh.as, hbox, hw);
     if (!ok) return false;
     if (t == 0) {
         c->frame_id += 1;

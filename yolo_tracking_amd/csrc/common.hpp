@@ -182,6 +182,43 @@ __device__ __forceinline__ int block_compact(int n, int *wsum, Pred pred, Emit e
     return count;
 }
 
+// Two order-preserving compactions of [0, n) in one pass (one block scan of packed counts):
+// cat(i) -> 0 (neither), 1 or 2; emit(i, cat, position within its category).  Returns the two
+// counts.  Same ownership scheme as block_compact.
+template <typename Cat, typename Emit>
+__device__ __forceinline__ int2 block_compact2(int n, int *wsum, Cat cat, Emit emit) {
+    const int nt = blockDim.x, t = threadIdx.x;
+    int c1 = 0, c2 = 0;
+    for (int base = 0; base < n; base += 32 * nt) {
+        const int m = n - base < 32 * nt ? n - base : 32 * nt;
+        const int per = (m + nt - 1) / nt;
+        const int lo = base + t * per;
+        const int hi = lo + per < base + m ? lo + per : base + m;
+        unsigned b1 = 0, b2 = 0;
+        for (int i = lo; i < hi; ++i) {
+            const int c = cat(i);
+            if (c == 1) b1 |= 1u << (i - lo);
+            else if (c == 2) b2 |= 1u << (i - lo);
+        }
+        int tot;   // counts <= 32 * 1024 each: 16 bits apiece
+        const int ex = block_exclusive_scan(__popc(b1) | (__popc(b2) << 16), wsum, &tot);
+        int p1 = c1 + (ex & 0xFFFF), p2 = c2 + (ex >> 16);
+        while (b1 | b2) {
+            const int k1 = b1 ? __ffs(b1) - 1 : 32, k2 = b2 ? __ffs(b2) - 1 : 32;
+            if (k1 < k2) {
+                b1 &= b1 - 1;
+                emit(lo + k1, 1, p1++);
+            } else {
+                b2 &= b2 - 1;
+                emit(lo + k2, 2, p2++);
+            }
+        }
+        c1 += tot & 0xFFFF;
+        c2 += tot >> 16;
+    }
+    return make_int2(c1, c2);
+}
+
 // Strided loop over [0, n) that issues the loads of B iterations before using any of them, so
 // their latencies overlap: load(i) -> value, use(i, value).
 template <int B, typename Load, typename Use>

@@ -58,6 +58,7 @@ __device__ __forceinline__ int grid_cell_1d(double x, double o, double inv_g, in
 struct GridScratch {
     double red[8 * 16];
     GridHdr hdr;
+    unsigned long long maxw_bits, maxh_bits;   // max binned width / height (positive doubles)
 };
 
 // Block-wide reduction of 6 values; op[k]: RED_MIN / RED_MAX / RED_SUM.  Per-wave partials go
@@ -74,55 +75,50 @@ __device__ __forceinline__ void block_reduce6(double v[6], const int op[6], doub
 }
 
 // Block-wide build (every thread of the block calls it).  box(i) returns item i's box, wof(i) its
-// weight (stored only when gv.w is set).  gv.cell_start needs GRID_MAX_CELLS + 1 entries, gv.ids /
-// gv.boxes / gv.w / gv.big n entries, gv.cell_start grid_cells_for(n) + 1.
+// weight (stored only when gv.w is set).  gv.cell_start needs grid_cells_for(n) + 1 entries,
+// gv.ids / gv.boxes / gv.w / gv.big n entries.
+//   1. one block reduction over the usable boxes: mean size, extent of the top-left corners
+//   2. count per cell (items larger than 4 x mean go to the big list instead); the maximum
+//      width / height of the binned items by 64-bit LDS atomicMax on their bit patterns
+//   3. one block scan of the cell counts, 4. scatter
 template <typename BoxOf, typename WOf>
-__device__ __forceinline__ void grid_build(int n, BoxOf box, WOf wof, GridView gv, GridScratch &gs, int *wsum) {
+__device__ __forceinline__ void grid_build(int n, BoxOf box, WOf wof, GridView gv, GridScratch &gs,
+                                           int *wsum) {
     const int t = threadIdx.x, nt = blockDim.x;
     YTA_STAMP_ABS(110);
-    // pass 1: mean size of the usable boxes
-    double v[6] = {0, 0, 0, 0, 0, 0};
-    const int sums[6] = {RED_SUM, RED_SUM, RED_SUM, RED_SUM, RED_SUM, RED_SUM};
+    double v[6] = {0.0, 0.0, INFINITY, INFINITY, -INFINITY, -INFINITY};
+    const int ops[6] = {RED_SUM, RED_SUM, RED_MIN, RED_MIN, RED_MAX, RED_MAX};
     for (int i = t; i < n; i += nt) {
         const Box b = box(i);
         if (!box_usable(b)) continue;
-        v[4] += fmax(b.x2 - b.x1, b.y2 - b.y1);
-        v[5] += 1.0;
+        v[0] += fmax(b.x2 - b.x1, b.y2 - b.y1);
+        v[1] += 1.0;
+        v[2] = fmin(v[2], b.x1);
+        v[3] = fmin(v[3], b.y1);
+        v[4] = fmax(v[4], b.x1);
+        v[5] = fmax(v[5], b.y1);
     }
-    block_reduce6(v, sums, gs.red);
+    if (t == 0) {
+        gs.maxw_bits = 0ull;
+        gs.maxh_bits = 0ull;
+        gs.hdr.n_big = 0;
+    }
+    block_reduce6(v, ops, gs.red);
     YTA_STAMP_ABS(111);
-    const double nb = v[5];
-    const double mean = nb > 0 ? v[4] / nb : 1.0;
+    const double mean = v[1] > 0 ? v[0] / v[1] : 1.0;
     const double bthr = 4.0 * mean;
     auto binned = [&](const Box &b) {
         return box_usable(b) && !(b.x2 - b.x1 > bthr) && !(b.y2 - b.y1 > bthr);
     };
-    // pass 2: extent of the binned top-left corners and their maximum width / height
-    double e[6] = {INFINITY, INFINITY, -INFINITY, -INFINITY, -INFINITY, -INFINITY};
-    const int ops[6] = {RED_MIN, RED_MIN, RED_MAX, RED_MAX, RED_MAX, RED_MAX};
-    for (int i = t; i < n; i += nt) {
-        const Box b = box(i);
-        if (!binned(b)) continue;
-        e[0] = fmin(e[0], b.x1);
-        e[1] = fmin(e[1], b.y1);
-        e[2] = fmax(e[2], b.x1);
-        e[3] = fmax(e[3], b.y1);
-        e[4] = fmax(e[4], b.x2 - b.x1);
-        e[5] = fmax(e[5], b.y2 - b.y1);
-    }
-    block_reduce6(e, ops, gs.red);
-    YTA_STAMP_ABS(112);
     GridHdr h;
-    h.maxw = e[4] > 0 ? e[4] : 0.0;
-    h.maxh = e[5] > 0 ? e[5] : 0.0;
-    if (!(e[2] >= e[0])) {   // nothing to bin
+    if (!(v[4] >= v[2])) {   // nothing usable
         h.ox = h.oy = 0.0;
         h.g = 1.0;
         h.inv_g = 1.0;
         h.gx = h.gy = 1;
     } else {
         double g = mean;
-        const double ex = e[2] - e[0], ey = e[3] - e[1];
+        const double ex = v[4] - v[2], ey = v[5] - v[3];
         double gxf = floor(ex / g) + 1.0, gyf = floor(ey / g) + 1.0;
         const double max_cells = (double)grid_cells_for(n);
         while (gxf * gyf > max_cells) {
@@ -130,26 +126,24 @@ __device__ __forceinline__ void grid_build(int n, BoxOf box, WOf wof, GridView g
             gxf = floor(ex / g) + 1.0;
             gyf = floor(ey / g) + 1.0;
         }
-        h.ox = e[0];
-        h.oy = e[1];
+        h.ox = v[2];
+        h.oy = v[3];
         h.g = g;
         h.inv_g = 1.0 / g;
         h.gx = (int)gxf;
         h.gy = (int)gyf;
     }
-    h.n_big = 0;
-    h.n_binned = 0;
-    if (t == 0) gs.hdr = h;
     const int ncell = h.gx * h.gy;
     int *cs = gv.cell_start;
     for (int c = t; c <= ncell; c += nt) cs[c] = 0;
     block_sync();
-    YTA_STAMP_ABS(113);
+    YTA_STAMP_ABS(112);
     auto cell_of = [&](const Box &b) {
         return grid_cell_1d(b.y1, h.oy, h.inv_g, h.gy) * h.gx + grid_cell_1d(b.x1, h.ox, h.inv_g, h.gx);
     };
     // counts land in cs[c + 1]; the exclusive scan leaves start(c) there, and the scatter's cursor
     // increments turn it into end(c) = start(c + 1), so cs[c] = start(c) afterwards
+    double mw = 0.0, mh = 0.0;
     for (int i = t; i < n; i += nt) {
         const Box b = box(i);
         if (!box_usable(b)) continue;
@@ -157,22 +151,38 @@ __device__ __forceinline__ void grid_build(int n, BoxOf box, WOf wof, GridView g
             gv.big[atomicAdd(&gs.hdr.n_big, 1)] = i;
             continue;
         }
+        mw = fmax(mw, b.x2 - b.x1);
+        mh = fmax(mh, b.y2 - b.y1);
         atomicAdd(&cs[cell_of(b) + 1], 1);
     }
-    block_sync();
-    YTA_STAMP_ABS(114);
-    int run = 0;
-    for (int start = 0; start < ncell; start += nt) {
-        const int c = start + t;
-        const int cv = c < ncell ? ald(cs + c + 1) : 0;
-        int tot;
-        const int pos = block_exclusive_scan(cv, wsum, &tot);
-        if (c < ncell) cs[c + 1] = run + pos;
-        run += tot;
+    mw = wave_reduce(RED_MAX, mw);
+    mh = wave_reduce(RED_MAX, mh);
+    if (lane_id() == 0) {
+        atomicMax(&gs.maxw_bits, (unsigned long long)__double_as_longlong(mw));
+        atomicMax(&gs.maxh_bits, (unsigned long long)__double_as_longlong(mh));
     }
-    if (t == 0) {
-        gs.hdr.n_binned = run;
-        if (gv.hdr) *gv.hdr = gs.hdr;
+    block_sync();
+    YTA_STAMP_ABS(113);
+    {   // one scan: every thread owns a contiguous run of cells
+        const int per = (ncell + nt - 1) / nt;
+        const int c0 = t * per, c1 = c0 + per < ncell ? c0 + per : ncell;
+        int mine = 0;
+        for (int c = c0; c < c1; ++c) mine += ald(cs + c + 1);
+        int tot;
+        int run = block_exclusive_scan(mine, wsum, &tot);
+        for (int c = c0; c < c1; ++c) {
+            const int k = ald(cs + c + 1);
+            cs[c + 1] = run;
+            run += k;
+        }
+        if (t == 0) {
+            h.n_big = gs.hdr.n_big;
+            h.n_binned = tot;
+            h.maxw = __longlong_as_double((long long)gs.maxw_bits);
+            h.maxh = __longlong_as_double((long long)gs.maxh_bits);
+            gs.hdr = h;
+            if (gv.hdr) *gv.hdr = h;
+        }
     }
     block_sync();
     YTA_STAMP_ABS(115);

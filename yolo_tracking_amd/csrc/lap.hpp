@@ -389,21 +389,35 @@ __device__ __forceinline__ bool lap_block(int nr, int nc, const int *row_off, co
     int *queue = ar.alloc<int>(ncomp);
     int *big_q = ar.alloc<int>(ncomp);
     if (ar.fail) return false;
-    // P3: complex nodes and roots in node order
-    {
-        int run = 0, runr = 0;
-        for (int start = 0; start < N; start += nt) {
-            const int n = start + t;
-            const bool cx = n < N && complex_node(n);
-            const bool rt = cx && ald(parent + n) == n;
-            int tot, totr;
-            const int pos = block_exclusive_scan(cx ? 1 : 0, sh.wsum, &tot);
-            const int posr = block_exclusive_scan(rt ? 1 : 0, sh.wsum, &totr);
-            if (cx) cnodes[run + pos] = n;
-            if (rt) roots[runr + posr] = n;
-            run += tot;
-            runr += totr;
+    // P3: complex nodes and roots in node order (each thread a contiguous run of nodes, one block
+    // scan of the packed counts)
+    for (int base = 0; base < N; base += 32 * nt) {
+        const int m = N - base < 32 * nt ? N - base : 32 * nt;
+        const int per = (m + nt - 1) / nt;
+        const int lo = base + t * per;
+        const int hi = lo + per < base + m ? lo + per : base + m;
+        unsigned bc = 0, br = 0;
+        for (int n = lo; n < hi; ++n) {
+            if (!complex_node(n)) continue;
+            bc |= 1u << (n - lo);
+            if (ald(parent + n) == n) br |= 1u << (n - lo);
         }
+        int tot;
+        const int ex = block_exclusive_scan(__popc(bc) | (__popc(br) << 16), sh.wsum, &tot);
+        int pc = (base == 0 ? 0 : sh.cnt[2]) + (ex & 0xFFFF);
+        int pr = (base == 0 ? 0 : sh.cnt[3]) + (ex >> 16);
+        while (bc) {
+            const int k = __ffs(bc) - 1;
+            bc &= bc - 1;
+            cnodes[pc++] = lo + k;
+            if ((br >> k) & 1u) roots[pr++] = lo + k;
+        }
+        block_sync();
+        if (t == 0) {
+            sh.cnt[2] = (base == 0 ? 0 : sh.cnt[2]) + (tot & 0xFFFF);
+            sh.cnt[3] = (base == 0 ? 0 : sh.cnt[3]) + (tot >> 16);
+        }
+        block_sync();
     }
     for (int c = t; c < ncomp; c += nt) { kc[c] = 0; lc[c] = 0; }
     block_sync();
