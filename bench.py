@@ -76,6 +76,42 @@ def pmc_traffic(streams, n):
     return None, None
 
 
+# ---------------------------------------------------------------- multi-rank harness (N > 1)
+def stream_seeds(seed, rank, streams):
+    """Rank r owns streams [r*S, (r+1)*S): disjoint seeds, so ranks shard the job (weak scaling)."""
+    return [seed + rank * streams + s for s in range(streams)]
+
+
+def timed_region(run_steps, sync, dist):
+    """Barrier + device sync on both sides of the timed region; returns this rank's seconds."""
+    sync()
+    if dist:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    run_steps()
+    sync()
+    if dist:
+        dist.barrier()
+    sync()
+    return time.perf_counter() - t0
+
+
+def max_over_ranks(elapsed, dist, device):
+    """The job's time is the slowest rank's (all_reduce MAX; RCCL on the GPU box, gloo in tests)."""
+    if not dist:
+        return elapsed
+    import torch
+    t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def aggregate_rate(world, streams, steps, elapsed):
+    """Whole-job update calls per second over all ranks."""
+    return world * streams * steps / elapsed
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -136,7 +172,7 @@ def main():
     F = args.warmup + args.steps
     # synthetic frames for this rank's streams, staged in HBM: [F][S*N][6] + offsets
     t_gen = time.time()
-    per_stream = [gen_stream_frames(N, F, args.seed + rank * S + s) for s in range(S)]
+    per_stream = [gen_stream_frames(N, F, sd) for sd in stream_seeds(args.seed, rank, S)]
     host = np.stack([np.concatenate([per_stream[s][f] for s in range(S)]) for f in range(F)])
     off = np.array([[sum(len(per_stream[q][f]) for q in range(s)) for s in range(S + 1)]
                     for f in range(F)], dtype=np.int32)
@@ -164,30 +200,19 @@ def main():
         step(f)
     _lib.check(lib.yta_bytetrack_sync(h))
     _lib.check(lib.yta_bytetrack_profile(h, 1))
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for f in range(args.warmup, F):
-        step(f)
-    _lib.check(lib.yta_bytetrack_sync(h))
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
+    def run_steps():
+        for f in range(args.warmup, F):
+            step(f)
+        _lib.check(lib.yta_bytetrack_sync(h))
+
+    elapsed = timed_region(run_steps, torch.cuda.synchronize, dist)
     ms = (ctypes.c_double * len(PHASES))()
     nfr = ctypes.c_int()
     _lib.check(lib.yta_bytetrack_profile_collect(h, ms, ctypes.byref(nfr)))
     phase_ms = {PHASES[k]: ms[k] / max(nfr.value, 1) for k in range(len(PHASES))}
 
-    if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    calls = world * S * args.steps
-    value = calls / elapsed
+    elapsed = max_over_ranks(elapsed, dist, "cuda")
+    value = aggregate_rate(world, S, args.steps, elapsed)
     ms_per_step = 1000.0 * elapsed / args.steps
 
     stats = (ctypes.c_longlong * len(STATS))()

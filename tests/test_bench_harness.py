@@ -1,0 +1,59 @@
+"""CPU: the N > 1 bench harness (stream sharding, barrier-bracketed timing, max over ranks) with
+world_size 2 over gloo — the same functions bench.py runs over RCCL on the GPU box."""
+import os
+import socket
+import sys
+import time
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+import bench  # noqa: E402
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        S, steps = 3, 4
+        seeds = bench.stream_seeds(1000, rank, S)
+        every = [None] * world
+        dist.all_gather_object(every, seeds)
+        # rank 1 is deliberately slower: the job time must be the slowest rank's
+        el = bench.timed_region(lambda: time.sleep(0.05 + 0.15 * rank), lambda: None, dist)
+        job = bench.max_over_ranks(el, dist, "cpu")
+        q.put((rank, every, el, job, bench.aggregate_rate(world, S, steps, job)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_harness_gloo():
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    seeds = res[0][1]
+    flat = [x for r in seeds for x in r]
+    assert len(set(flat)) == len(flat)            # disjoint stream shards
+    assert seeds[1][0] == seeds[0][-1] + 1        # contiguous global stream numbering
+    jobs = {r[3] for r in res}
+    assert len(jobs) == 1                         # every rank reports the same (max) time
+    job = jobs.pop()
+    assert job >= max(r[2] for r in res) - 1e-9 and job >= 0.2
+    assert res[0][4] == pytest.approx(world * 3 * 4 / job)
