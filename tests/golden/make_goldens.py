@@ -10,6 +10,12 @@ Fixtures (data only — inputs and the reference's outputs):
                            with the final Kalman state of every live track.
   G3 kat_*.npz             known-answer vectors: IoU family, fuse_score, ByteTrack KF
                            initiate / multi_predict / update, lapjv with and without cost_limit.
+  G4 botsort_synth.npz     BoT-SORT (botsort.yaml parameters) on seeded synthetic streams with
+                           embeddings (fake ReID = harness rows / global norm, fake CMC = harness
+                           warp: identity or SURVEY §8(d)'s fixed affine), final Kalman states and
+                           smoothed features.  Every embedding-threshold comparison and every LAP
+                           cost is margin-checked (> 1e-6 from its threshold), so a tolerance-level
+                           difference in float32 embedding arithmetic cannot flip an assignment.
 Every LAP call made while generating is tie-checked: the problem is re-solved on the row- and
 column-reversed matrix and the matched real pairs must be identical; otherwise the fixture is
 rejected (lapx's own tie-breaking is unpinned because lapx is not installed).
@@ -236,12 +242,123 @@ def make_g3():
     print("G3 written")
 
 
+# ------------------------------------------------------------------ G4: BoT-SORT
+BOTSORT_YAML = dict(track_high_thresh=0.33824964456239337, track_low_thresh=0.1,
+                    new_track_thresh=0.21144301345190655, track_buffer=60,
+                    match_thresh=0.22734550911325851, proximity_thresh=0.5945380911899254,
+                    appearance_thresh=0.4818211117541298, frame_rate=30)   # botsort.yaml
+CMC_AFFINE = np.array([[1.0, 1e-3, 0.5], [-1e-3, 1.0, -0.3]])
+BOTSORT_CASES = [  # (name, n_objects, n_frames, seed, emb_dim, warp, extra kwargs)
+    ("bs_n64_d32", 64, 30, 41, 32, None, {}),
+    ("bs_n256_d64", 256, 20, 42, 64, None, {}),
+    ("bs_n256_d64_cmc", 256, 20, 43, 64, CMC_AFFINE, {}),
+    ("bs_n128_fuse", 128, 25, 44, 32, None, {"fuse_first_associate": True}),
+    ("bs_n128_noreid", 128, 25, 45, 0, None, {"with_reid": False}),
+    ("bs_n512_d128", 512, 4, 46, 128, None, {}),
+]
+MARGIN = {"min": np.inf}
+
+
+def _margin(vals, thr):
+    v = np.asarray(vals, dtype=np.float64).ravel()
+    v = v[np.isfinite(v)]
+    if v.size:
+        MARGIN["min"] = min(MARGIN["min"], float(np.min(np.abs(v - thr))))
+
+
+def make_g4():
+    bs = refshim.load_botsort()
+    H = refshim.Harness
+    mod = bs.bot_sort
+    orig_emb = mod.embedding_distance
+
+    CHECK_IOU = {"on": False}
+    orig_iou = mod.iou_distance
+
+    def emb_checked(tracks, dets, metric="cosine"):
+        e = orig_emb(tracks, dets, metric)
+        if e.size:   # only entries the proximity mask leaves in play can change a cost
+            live = orig_iou(tracks, dets) <= BOTSORT_YAML["proximity_thresh"]
+            h = (e / 2.0)[live]
+            for thr in (BOTSORT_YAML["appearance_thresh"], BOTSORT_YAML["match_thresh"], 0.7):
+                _margin(h, thr)
+        return e
+
+    def iou_checked(a, b):
+        d = orig_iou(a, b)
+        if CHECK_IOU["on"]:   # Kalman states under a non-identity warp are not bit-exact
+            for thr in (0.5, 0.7, 0.15, BOTSORT_YAML["proximity_thresh"],
+                        BOTSORT_YAML["match_thresh"]):
+                _margin(d, thr)
+        return d
+
+    mod.embedding_distance, mod.iou_distance = emb_checked, iou_checked
+    out = {}
+    try:
+        for name, n, nf, seed, D, warp, extra in BOTSORT_CASES:
+            frames = make_frames(n, nf, seed, emb_dim=max(D, 1))
+            before = dict(TIES)
+            MARGIN["min"] = np.inf
+            kw = dict(BOTSORT_YAML, **extra)
+            t = mod.BoTSORT(None, "cpu", False, **kw)
+            H.high_thresh = kw["track_high_thresh"]
+            H.warp = np.eye(2, 3) if warp is None else warp
+            CHECK_IOU["on"] = warp is not None
+            outs = []
+            img = np.zeros((8, 8, 3), np.uint8)
+            for dets, embs in frames:
+                H.dets, H.feats = dets, embs
+                outs.append(np.asarray(t.update(dets, img), dtype=np.float64).reshape(-1, 8))
+            ties = TIES["ties"] - before["ties"]
+            assert ties == 0, f"{name}: {ties} tied LAP calls"
+            assert MARGIN["min"] > 1e-6, f"{name}: threshold margin {MARGIN['min']}"
+            counts, rows = pack_outputs(outs)
+            # inputs are regenerated by the tests from (n, frames, seed, D) with
+            # yolo_tracking_amd.synth; the checksums pin that generator
+            out[f"{name}__gen"] = np.array([n, nf, seed, D], np.int64)
+            out[f"{name}__in_sum"] = np.array(
+                [float(np.sum([d.sum() for d, _ in frames])),
+                 float(np.sum([e.astype(np.float64).sum() for _, e in frames])) if D else 0.0])
+            out[f"{name}__warp"] = np.asarray(H.warp, dtype=np.float64)
+            out[f"{name}__params"] = np.array([kw["track_high_thresh"], kw["track_low_thresh"],
+                                               kw["new_track_thresh"], kw["track_buffer"],
+                                               kw["match_thresh"], kw["proximity_thresh"],
+                                               kw["appearance_thresh"], kw["frame_rate"],
+                                               float(kw.get("fuse_first_associate", False)),
+                                               float(kw.get("with_reid", True))])
+            out[f"{name}__out_counts"] = counts
+            out[f"{name}__out"] = rows
+            recs = [(tag, s) for lst, tag in ((t.tracked_stracks, 0), (t.lost_stracks, 1))
+                    for s in lst]
+            out[f"{name}__st_list"] = np.array([r[0] for r in recs], np.int64)
+            out[f"{name}__st_id"] = np.array([r[1].id for r in recs], np.int64)
+            out[f"{name}__st_state"] = np.array([r[1].state for r in recs], np.int64)
+            out[f"{name}__st_act"] = np.array([int(r[1].is_activated) for r in recs], np.int64)
+            out[f"{name}__st_frame"] = np.array([r[1].frame_id for r in recs], np.int64)
+            out[f"{name}__st_start"] = np.array([r[1].start_frame for r in recs], np.int64)
+            out[f"{name}__st_len"] = np.array([r[1].tracklet_len for r in recs], np.int64)
+            out[f"{name}__st_mean"] = np.array([r[1].mean for r in recs]).reshape(-1, 8)
+            out[f"{name}__st_cov"] = np.array([r[1].covariance for r in recs]).reshape(-1, 8, 8)
+            if D:
+                out[f"{name}__st_feat"] = np.array([r[1].smooth_feat for r in recs],
+                                                   np.float32).reshape(-1, D)
+            print(f"G4 {name}: out_rows={len(rows)} live={len(t.tracked_stracks)}+"
+                  f"{len(t.lost_stracks)} lap_calls={TIES['calls'] - before['calls']} "
+                  f"min_margin={MARGIN['min']:.3g}")
+    finally:
+        mod.embedding_distance, mod.iou_distance = orig_emb, orig_iou
+    out["cases"] = np.array([c[0] for c in BOTSORT_CASES])
+    np.savez_compressed(os.path.join(HERE, "botsort_synth.npz"), **out)
+
+
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["g1", "g2", "g3"]
+    which = sys.argv[1:] or ["g1", "g2", "g3", "g4"]
     if "g3" in which:
         make_g3()
     if "g1" in which:
         make_g1()
     if "g2" in which:
         make_g2()
+    if "g4" in which:
+        make_g4()
     print(f"LAP calls {TIES['calls']}, tied {TIES['ties']}")

@@ -8,7 +8,11 @@ run on the GPU box (the reference does not exist there).  Recipe from SURVEY.md 
   3. `filterpy.common.reshape_z/pretty_str` + `filterpy.stats.logpdf` — shape-only helpers, no
      arithmetic (ocsort_kf.py:105-106);
   4. a `lap` module whose `lapjv` restates lapx's extend_cost / cost_limit contract on top of
-     scipy.optimize.linear_sum_assignment (lapx itself is not installed).
+     scipy.optimize.linear_sum_assignment (lapx itself is not installed);
+  5. for BoT-SORT: a fake `boxmot.appearance.reid_multibackend` whose
+     get_features returns harness-supplied rows divided by their global Frobenius norm (as
+     reid_multibackend.py:310), and a fake `boxmot.motion.cmc.sof.SparseOptFlow` returning a
+     harness-supplied 2x3 warp.
 """
 import os
 import sys
@@ -99,6 +103,65 @@ def _install_shims():
         pkg = types.ModuleType("boxmot")
         pkg.__path__ = [os.path.join(REF, "boxmot")]
         sys.modules["boxmot"] = pkg
+
+
+class Harness:
+    """Per-frame inputs the fake ReID / CMC modules hand to the reference."""
+    feats = None           # (M, D) float32 raw embeddings of the frame's detections
+    high_thresh = 0.5      # BoT-SORT track_high_thresh (rows the reference asks features for)
+    dets = None
+    warp = np.eye(2, 3)
+
+
+def _install_botsort_shims():
+    if "boxmot.appearance.reid_multibackend" in sys.modules:
+        return
+    app = types.ModuleType("boxmot.appearance")
+    app.__path__ = []
+    rmb = types.ModuleType("boxmot.appearance.reid_multibackend")
+
+    class ReIDDetectMultiBackend:
+        def __init__(self, weights=None, device=None, fp16=False):
+            pass
+
+        def get_features(self, xyxys, img):
+            if xyxys.size != 0:
+                m = Harness.dets[:, 4] > Harness.high_thresh
+                features = Harness.feats[m]
+                assert np.array_equal(Harness.dets[m, :4], xyxys)
+            else:
+                features = np.array([])
+            return features / np.linalg.norm(features)          # reid_multibackend.py:310
+
+    rmb.ReIDDetectMultiBackend = ReIDDetectMultiBackend
+    cmc = types.ModuleType("boxmot.motion.cmc")
+    cmc.__path__ = []
+    sof = types.ModuleType("boxmot.motion.cmc.sof")
+
+    class SparseOptFlow:
+        def __init__(self, *a, **k):
+            pass
+
+        def apply(self, img, dets):
+            return np.array(Harness.warp, dtype=np.float64)
+
+    sof.SparseOptFlow = SparseOptFlow
+    sys.modules["boxmot.appearance"] = app
+    sys.modules["boxmot.appearance.reid_multibackend"] = rmb
+    sys.modules["boxmot.motion.cmc"] = cmc
+    sys.modules["boxmot.motion.cmc.sof"] = sof
+
+
+def load_botsort():
+    """Reference BoT-SORT modules (with the fake ReID / CMC of step 5)."""
+    _install_shims()
+    _install_botsort_shims()
+    import importlib
+    ns = types.SimpleNamespace()
+    ns.bot_sort = importlib.import_module("boxmot.trackers.botsort.bot_sort")
+    ns.basetrack = importlib.import_module("boxmot.trackers.botsort.basetrack")
+    ns.botsort_kf = importlib.import_module("boxmot.motion.kalman_filters.botsort_kf")
+    return ns
 
 
 def load():

@@ -101,3 +101,54 @@ def test_reference_kat_bytetrack_output():
         out = t.update(det)
         assert out.shape == (2, 8)
     np.testing.assert_allclose(det, np.delete(out, [4, 7], axis=1), atol=1, rtol=7e-3)
+
+
+# ------------------------------------------------------------------ BoT-SORT (G4)
+def botsort_case(g, name):
+    """Inputs of a G4 case regenerated from its seed, checked against the stored checksums;
+    returns (frames [(dets, embs)], params dict, warp)."""
+    from yolo_tracking_amd.synth import make_frames
+    n, nf, seed, D = (int(x) for x in g[f"{name}__gen"])
+    frames = make_frames(n, nf, seed, emb_dim=max(D, 1))
+    sums = g[f"{name}__in_sum"]
+    assert float(np.sum([d.sum() for d, _ in frames])) == sums[0]
+    if D:
+        assert float(np.sum([e.astype(np.float64).sum() for _, e in frames])) == sums[1]
+    p = g[f"{name}__params"]
+    params = dict(track_high_thresh=p[0], track_low_thresh=p[1], new_track_thresh=p[2],
+                  track_buffer=int(p[3]), match_thresh=p[4], proximity_thresh=p[5],
+                  appearance_thresh=p[6], frame_rate=int(p[7]),
+                  fuse_first_associate=bool(p[8]), with_reid=bool(p[9]))
+    return frames, params, g[f"{name}__warp"], D
+
+
+def reid_features(dets, embs, high_thresh):
+    """What ReIDDetectMultiBackend.get_features returns for the high detections: their rows
+    divided by the global Frobenius norm (reid_multibackend.py:310)."""
+    f = embs[dets[:, 4] > high_thresh]
+    return f / np.linalg.norm(f)
+
+
+@pytest.mark.parametrize("name", ["bs_n64_d32", "bs_n256_d64", "bs_n256_d64_cmc", "bs_n128_fuse",
+                                  "bs_n128_noreid", "bs_n512_d128"])
+def test_botsort_oracle_matches_reference(golden_dir, name):
+    from oracle.botsort import BoTSORTOracle
+    g = np.load(os.path.join(golden_dir, "botsort_synth.npz"))
+    frames, params, warp, D = botsort_case(g, name)
+    t = BoTSORTOracle(**params)
+    oc, out = g[f"{name}__out_counts"], g[f"{name}__out"]
+    r0 = 0
+    for f, (dets, embs) in enumerate(frames):
+        feats = reid_features(dets, embs, params["track_high_thresh"]) if D else None
+        got = t.update(dets, feats, warp).reshape(-1, 8)
+        exp = out[r0:r0 + oc[f]]
+        assert got.shape == exp.shape, (name, f)
+        assert np.array_equal(got, exp), (name, f)
+        r0 += oc[f]
+    recs = [(tag, s) for lst, tag in ((t.tracked, 0), (t.lost, 1)) for s in lst]
+    assert np.array_equal([r[1].track_id for r in recs], g[f"{name}__st_id"])
+    assert np.array_equal(np.array([r[1].mean for r in recs]).reshape(-1, 8), g[f"{name}__st_mean"])
+    assert np.array_equal(np.array([r[1].cov for r in recs]).reshape(-1, 8, 8), g[f"{name}__st_cov"])
+    if D:
+        assert np.array_equal(np.array([r[1].smooth_feat for r in recs], np.float32).reshape(-1, D),
+                              g[f"{name}__st_feat"])
