@@ -9,6 +9,10 @@
  * What each entry point replaces in the reference (BoxMOT 10.0.51, /root/reference):
  *   yta_bytetrack_*          boxmot/trackers/bytetrack/byte_tracker.py:114-281  BYTETracker.__init__/update
  *                            (created by boxmot/tracker_zoo.py:56-64 create_tracker('bytetrack', ...))
+ *   yta_botsort_*            boxmot/trackers/botsort/bot_sort.py:185-420  BoTSORT.__init__/update
+ *                            (created by boxmot/tracker_zoo.py:66-81 create_tracker('botsort', ...));
+ *                            the ReID forward pass (reid_multibackend.py:303-311) and the CMC
+ *                            estimator (sof.py) stay outside: their outputs are inputs here
  *   yta_box_affinity         boxmot/utils/iou.py:6-188  iou/giou/diou/ciou/centroid_batch
  *   yta_iou_distance         boxmot/utils/matching.py:94-119 iou_distance (+ fuse_score :213-221)
  *   yta_kf_xyah_initiate     boxmot/motion/kalman_filters/bytetrack_kf.py:55-86
@@ -134,6 +138,45 @@ int yta_bytetrack_stats(yta_bytetrack *engine, long long *stats);
 int yta_bytetrack_set_lds(yta_bytetrack *engine, int bytes);
 /* Throughput helper: the engine's HIP stream (hipStream_t as void*) */
 int yta_bytetrack_hip_stream(yta_bytetrack *engine, void **stream);
+
+/* ---- BoT-SORT engine: S independent streams ----------------------------------------------
+ * The same engine object as ByteTrack (yta_bytetrack_destroy / reset / reserve / capacity / sync /
+ * get_state / profile / stats / set_lds / hip_stream all apply; get_state's mean is xywh) with
+ * BoT-SORT's association (IoU + gated cosine appearance cost), xywh Kalman filter, feature EMA
+ * and class vote.  IDs start from 0 per stream at creation (BaseTrack.clear_count, :205). */
+typedef struct yta_bytetrack yta_botsort;
+typedef struct {
+    double track_high_thresh;     /* botsort.yaml / ctor default 0.5  */
+    double track_low_thresh;      /* 0.1  */
+    double new_track_thresh;      /* 0.6  */
+    double match_thresh;          /* 0.8  */
+    double proximity_thresh;      /* 0.5  */
+    double appearance_thresh;     /* 0.25 */
+    int track_buffer;             /* 30   */
+    int frame_rate;               /* 30   */
+    int fuse_first_associate;     /* 0    */
+    int with_reid;                /* 1: feat_dim-wide float32 ReID features per high detection */
+} yta_botsort_params;
+
+int yta_botsort_create(int device, int n_streams, int track_capacity, int max_dets, int feat_dim,
+                       const yta_botsort_params *params, yta_botsort **engine);
+/* Host-buffer update (synchronous).  dets / det_offsets / next_id / out / out_offsets as
+ * yta_bytetrack_update.  feats: for each stream in order, the rows get_features returned for its
+ * detections with conf > track_high_thresh, in detection order (float32, feat_dim wide; NULL
+ * when with_reid is 0).  warps: S camera-motion 2x3 affines (row-major) or NULL for identity;
+ * this version accepts only identity warps (YTA_ERR_INVALID otherwise). */
+int yta_botsort_update(yta_botsort *engine, const double *dets, const int *det_offsets,
+                       const float *feats, const double *warps, long long *next_id, double *out,
+                       int out_capacity, int *out_offsets);
+/* Device-resident update (asynchronous, identity warps): d_feats holds feat_dim floats per
+ * detection row of d_dets (only the high rows are read). */
+int yta_botsort_update_device(yta_botsort *engine, const double *d_dets, const int *d_det_offsets,
+                              const float *d_feats, double *d_out, int *d_out_counts);
+/* Parity introspection, in yta_bytetrack_get_state's track order: smoothed features
+ * (feat_dim floats per track, may be NULL), class histograms (8 x (class, summed score) float64
+ * per track, may be NULL) and their entry counts (may be NULL). */
+int yta_botsort_get_features(yta_botsort *engine, int stream, int *n_tracks, float *feats,
+                             double *cls_hist, int *n_cls);
 
 #ifdef __cplusplus
 }

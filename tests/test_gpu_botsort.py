@@ -1,0 +1,116 @@
+"""GPU: the device-resident BoT-SORT engine against the reference goldens (G4) and the oracle.
+
+Bar: output rows (ids, boxes, scores, classes, det_ind), track lists and Kalman states bit-exact
+on the identity-warp cases; smoothed features within float32 rounding (the engine sums squares in
+float64 where the reference's OpenBLAS sdot sums in float32 lanes: rtol 1e-5, atol 1e-6).
+"""
+import os
+
+import numpy as np
+import pytest
+
+from oracle.botsort import BoTSORTOracle
+from test_oracle_golden import botsort_case, reid_features
+from yolo_tracking_amd import _lib, create_tracker, get_tracker_config
+from yolo_tracking_amd.synth import make_frames
+from yolo_tracking_amd.trackers.botsort import BaseTrack, BoTSORT, BoTSORTEngine
+
+pytestmark = pytest.mark.gpu
+
+IDENTITY_CASES = ["bs_n64_d32", "bs_n256_d64", "bs_n128_fuse", "bs_n128_noreid", "bs_n512_d128"]
+
+
+def _engine(params, D, **kw):
+    return BoTSORTEngine(1, feat_dim=max(D, 1), **params, **kw)
+
+
+def _check_state(eng, g, name, D):
+    st = eng.state(0)
+    assert np.array_equal(st["list"], g[f"{name}__st_list"])
+    assert np.array_equal(st["id"], g[f"{name}__st_id"])
+    assert np.array_equal(st["state"], g[f"{name}__st_state"])
+    assert np.array_equal(st["activated"], g[f"{name}__st_act"])
+    assert np.array_equal(st["frame_id"], g[f"{name}__st_frame"])
+    assert np.array_equal(st["start_frame"], g[f"{name}__st_start"])
+    assert np.array_equal(st["tracklet_len"], g[f"{name}__st_len"])
+    assert np.array_equal(st["mean"], g[f"{name}__st_mean"])
+    assert np.array_equal(st["cov"], g[f"{name}__st_cov"])
+    if D:
+        feats, _, _ = eng.features(0)
+        np.testing.assert_allclose(feats, g[f"{name}__st_feat"], rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("name", IDENTITY_CASES)
+@pytest.mark.parametrize("lds", [None, 0])
+def test_botsort_golden(golden_dir, name, lds):
+    g = np.load(os.path.join(golden_dir, "botsort_synth.npz"))
+    frames, params, warp, D = botsort_case(g, name)
+    eng = _engine(params, D)
+    if lds is not None:
+        eng.set_lds(lds)               # every association over the global-memory arena
+    oc, out = g[f"{name}__out_counts"], g[f"{name}__out"]
+    r0 = 0
+    for f, (dets, embs) in enumerate(frames):
+        feats = reid_features(dets, embs, params["track_high_thresh"]) if D else None
+        got = eng.update([dets], [feats])[0]
+        exp = out[r0:r0 + oc[f]]
+        assert got.shape == exp.shape, (name, f, got.shape, exp.shape)
+        assert np.array_equal(got, exp), (name, f)
+        r0 += oc[f]
+    _check_state(eng, g, name, D)
+
+
+def test_botsort_cmc_warp_rejected(golden_dir):
+    """Non-identity camera-motion warps are not on the device path yet: refused loudly."""
+    g = np.load(os.path.join(golden_dir, "botsort_synth.npz"))
+    frames, params, warp, D = botsort_case(g, "bs_n256_d64_cmc")
+    eng = _engine(params, D)
+    dets, embs = frames[0]
+    with pytest.raises(_lib.YTAError):
+        eng.update([dets], [reid_features(dets, embs, params["track_high_thresh"])],
+                   warps=np.asarray(warp)[None])
+
+
+def test_botsort_python_surface(golden_dir):
+    """create_tracker('botsort') + update(dets, img, embs): the reference's call shape."""
+    g = np.load(os.path.join(golden_dir, "botsort_synth.npz"))
+    name = "bs_n64_d32"
+    frames, params, warp, D = botsort_case(g, name)
+    t = BoTSORT(None, "cuda:0", False, **params)
+    oc, out = g[f"{name}__out_counts"], g[f"{name}__out"]
+    img = np.zeros((8, 8, 3), np.uint8)
+    r0 = 0
+    for f, (dets, embs) in enumerate(frames):
+        hi = dets[:, 4] > params["track_high_thresh"]
+        e = np.zeros((len(dets), D), np.float32)
+        e[hi] = reid_features(dets, embs, params["track_high_thresh"])
+        got = np.asarray(t.update(dets, img, embs=e)).reshape(-1, 8)
+        assert np.array_equal(got, out[r0:r0 + oc[f]]), f
+        r0 += oc[f]
+    assert [v.track_id for v in t.tracked_stracks + t.lost_stracks] == list(g[f"{name}__st_id"])
+    # create_tracker wires the YAML keys and a ReID producer passed as reid_weights
+    class Reid:
+        def get_features(self, xyxys, img):
+            return np.ones((len(xyxys), 16), np.float32)
+    tz = create_tracker("botsort", get_tracker_config("botsort"), Reid(), "0", False, False)
+    r = tz.update(frames[0][0], img)
+    assert r.ndim == 2 and r.shape[1] == 8
+    assert BaseTrack._count == len(r)
+
+
+def test_botsort_multistream_matches_oracle():
+    """S streams in one engine, each its own seed, against the oracle stream by stream."""
+    S, n, nf, D = 4, 64, 12, 32
+    params = dict(track_high_thresh=0.5, track_low_thresh=0.1, new_track_thresh=0.6,
+                  track_buffer=30, match_thresh=0.8, proximity_thresh=0.5,
+                  appearance_thresh=0.25, frame_rate=30)
+    streams = [make_frames(n, nf, 100 + s, emb_dim=D) for s in range(S)]
+    eng = BoTSORTEngine(S, feat_dim=D, **params)
+    ors = [BoTSORTOracle(**params) for _ in range(S)]
+    for f in range(nf):
+        dets = [streams[s][f][0] for s in range(S)]
+        feats = [reid_features(dets[s], streams[s][f][1], 0.5) for s in range(S)]
+        got = eng.update(dets, feats)
+        for s in range(S):
+            exp = ors[s].update(dets[s], feats[s]).reshape(-1, 8)
+            assert np.array_equal(got[s], exp), (s, f)

@@ -11,8 +11,10 @@ __version__ = "10.0.51+mi355x.1"
 
 from .tracker_zoo import create_tracker, get_tracker_config  # noqa: E402
 from .trackers.bytetrack import BYTETracker, ByteTrackEngine  # noqa: E402
+from .trackers.botsort import BoTSORT, BoTSORTEngine  # noqa: E402
 
 TRACKERS = ["bytetrack", "botsort", "strongsort", "ocsort", "deepocsort", "hybridsort"]
 
-__all__ = ("__version__", "BYTETracker", "ByteTrackEngine", "create_tracker",
+__all__ = ("__version__", "BYTETracker", "ByteTrackEngine", "BoTSORT", "BoTSORTEngine",
+           "create_tracker",
            "get_tracker_config", "TRACKERS")

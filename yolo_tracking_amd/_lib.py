@@ -37,6 +37,15 @@ class BtParams(ctypes.Structure):
                 ("track_buffer", ctypes.c_int), ("frame_rate", ctypes.c_int)]
 
 
+class BotParams(ctypes.Structure):
+    """yta_botsort_params (include/yolo_tracking_amd.h)."""
+    _fields_ = [("track_high_thresh", ctypes.c_double), ("track_low_thresh", ctypes.c_double),
+                ("new_track_thresh", ctypes.c_double), ("match_thresh", ctypes.c_double),
+                ("proximity_thresh", ctypes.c_double), ("appearance_thresh", ctypes.c_double),
+                ("track_buffer", ctypes.c_int), ("frame_rate", ctypes.c_int),
+                ("fuse_first_associate", ctypes.c_int), ("with_reid", ctypes.c_int)]
+
+
 _lib = None
 
 _P = ctypes.c_void_p
@@ -69,6 +78,10 @@ _SIGS = {
     "yta_bytetrack_hip_stream": ([_P, _P], _I),
     "yta_bytetrack_set_lds": ([_P, _I], _I),
     "yta_selftest": ([_I], _I),
+    "yta_botsort_create": ([_I, _I, _I, _I, _I, _P, _P], _I),
+    "yta_botsort_update": ([_P, _P, _P, _P, _P, _P, _P, _I, _P], _I),
+    "yta_botsort_update_device": ([_P, _P, _P, _P, _P, _P], _I),
+    "yta_botsort_get_features": ([_P, _I, _P, _P, _P, _P], _I),
 }
 
 EXPORTED_SYMBOLS = tuple(_SIGS)

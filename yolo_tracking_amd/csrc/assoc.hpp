@@ -239,3 +239,209 @@ __device__ __forceinline__ bool assoc_block(int nr, RowBox rowbox, int nc, ColBo
 }
 
 }  // namespace yta
+
+namespace yta {
+
+// ------------------------------------------------------------------ IoU + appearance (BoT-SORT)
+// Cosine distance of two float32 feature rows in float64 (scipy cdist 'cosine':
+// 1 - u.v / (|u| |v|)), by one 16-lane row group: every lane accumulates a strided share, the
+// row group reduces with DPP.  Returns the value on every lane of the group.
+template <typename ColElem>
+__device__ __forceinline__ double cosine_dist16(const float *u, ColElem v, int D) {
+    const int l16 = lane_id() & 15;
+    double d = 0.0, nu = 0.0, nv = 0.0;
+    for (int k = l16; k < D; k += 16) {
+        const double a = (double)u[k], b = (double)v(k);
+        d += a * b;
+        nu += a * a;
+        nv += b * b;
+    }
+    d = row_allreduce(RED_SUM, d);
+    nu = row_allreduce(RED_SUM, nu);
+    nv = row_allreduce(RED_SUM, nv);
+    return 1 - d / (sqrt(nu) * sqrt(nv));
+}
+
+// One association problem whose cost is BoT-SORT's min(iou cost, gated appearance cost)
+// (bot_sort.py:307-322, :355-370):
+//   iou_d = 1 - IoU; mask = iou_d > prox; c = fused ? 1 - (1 - iou_d) * score : iou_d
+//   emb = max(0, cosine) / 2; emb > app -> 1; masked -> 1; cost = min(c, emb); edge iff < thresh
+// With prox < 1 and thresh <= 1 only intersecting pairs can be edges (emb needs iou_d <= prox),
+// so candidates come from the column grid (else every pair is visited).  Pass A (a thread per
+// row) records direct edges (masked pairs whose IoU cost alone is below thresh) and pending pairs
+// (the appearance cost is needed); pass B computes the pending pairs' cosine distances, one
+// 16-lane group per pair.  Edges are collected in a list at the arena's top end, then laid out
+// as CSR where the grid and the pending list were, each row sorted by column (run-to-run
+// deterministic whatever order the atomics produced).
+// Arena: the lists take what the grid leaves (LDS), or every pair (the global fallback arena,
+// sized by assoc_emb_arena_bytes).
+// rowfeat(i) -> const float* (smoothed track feature row); colfeat(j) -> accessor whose (k) is
+// the k-th element of column j's (normalised) feature.
+__host__ __device__ inline long long assoc_emb_arena_bytes(long long R, long long C) {
+    const long long P = R * C;
+    const long long grid = 4 * (GRID_MAX_CELLS + 1) + C * (4 + 32 + 8 + 4) + 5 * 16;
+    const long long lists = 8 * P + 16 * P + 2 * 16;
+    const long long lap = 12 * P + 4 * (R + C) * 3 + 4 * 5 * (R + C + 1) + 10 * 16;
+    return (grid + lists > lap + 16 * P ? grid + lists : lap + 16 * P) + 4 * (R + 1) + 4 * C +
+           512;
+}
+
+template <typename RowBox, typename ColBox, typename ColScore, typename RowFeat, typename ColFeat>
+__device__ __forceinline__ bool assoc_block_emb(int nr, RowBox rowbox, int nc, ColBox colbox,
+                                                bool fused, ColScore colscore, RowFeat rowfeat,
+                                                ColFeat colfeat, int D, double prox, double app,
+                                                double thresh, int *X, int *Y, int *err,
+                                                int *n_edges, Arena &ar, const LapSlab &slab,
+                                                AssocShared &sh) {
+    const int t = threadIdx.x, nt = blockDim.x;
+    const bool use_grid = prox < 1.0 && thresh <= 1.0 && nr > 0 && nc > 0;
+    const size_t lo0 = ar.lo;
+    GridView gv{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+    if (use_grid) {
+        gv.cell_start = ar.alloc<int>(grid_cells_for(nc) + 1);
+        gv.ids = ar.alloc<int>(nc);
+        gv.boxes = ar.alloc<Box>(nc);
+        gv.w = fused ? ar.alloc<double>(nc) : nullptr;
+        gv.big = ar.alloc<int>(nc);
+    }
+    int *row_off = ar.alloc_top<int>(nr + 1);
+    int *col_deg = ar.alloc_top<int>(nc);
+    if (ar.fail) return false;
+    const size_t hi_rows = ar.hi;
+    const long long pairs = (long long)nr * nc;
+    const long long avail = (long long)ar.hi - (long long)ar.lo - 64;
+    long long pcap = avail > 0 ? avail / 24 : 0;
+    pcap = pcap < pairs ? pcap : pairs;
+    long long ecap = avail > 0 ? (avail - 8 * pcap) / 16 : 0;
+    ecap = ecap < pairs ? ecap : pairs;
+    int2 *pend = ar.alloc<int2>(pcap);
+    int2 *edge = ar.alloc_top<int2>(ecap);
+    double *edge_c = ar.alloc_top<double>(ecap);
+    if (ar.fail) return false;
+    for (int i = t; i <= nr; i += nt) row_off[i] = 0;
+    for (int j = t; j < nc; j += nt) col_deg[j] = 0;
+    if (t == 0) { sh.lap.cnt[0] = 0; sh.lap.cnt[1] = 0; sh.lap.cnt[2] = 0; }
+    if (use_grid) {
+        block_sync();
+        grid_build(
+            nc, colbox, [&](int j) { return fused ? colscore(j) : 1.0; }, gv, sh.gs, sh.lap.wsum);
+    }
+    block_sync();
+    const GridHdr gh = sh.gs.hdr;
+    auto push_edge = [&](int i, int j, double c) {
+        const int p = atomicAdd(&sh.lap.cnt[1], 1);
+        if (p < ecap) {
+            edge[p] = make_int2(i, j);
+            edge_c[p] = c;
+            atomicAdd(&row_off[i + 1], 1);
+            atomicAdd(&col_deg[j], 1);
+        } else {
+            sh.lap.cnt[2] = 1;   // overflow: the caller redoes the frame over the global arena
+        }
+    };
+    auto iou_cost = [&](const Box &rb, const Box &cb, double w, double &d) {
+        d = 1 - iou(rb, cb);                                        // matching.py:117
+        return fused ? 1 - (1 - d) * w : d;                         // matching.py:216-220
+    };
+    auto pair = [&](int i, const Box &rb, int j, const Box &cb, double w) {
+        double d;
+        const double c = iou_cost(rb, cb, w, d);
+        if (d > prox) {                                             // emb masked to 1 (:319)
+            const double m = np_min(c, 1.0);
+            if (m < thresh) push_edge(i, j, m);
+        } else {
+            const int p = atomicAdd(&sh.lap.cnt[0], 1);
+            if (p < pcap) pend[p] = make_int2(i, j);
+            else sh.lap.cnt[2] = 1;
+        }
+    };
+    // pass A
+    for (int i = t; i < nr; i += nt) {
+        const Box rb = rowbox(i);
+        if (use_grid) {
+            grid_query(
+                gv, gh, rb, [&](int j, const Box &cb, double w) { pair(i, rb, j, cb, w); },
+                [&](int j) {
+                    const Box cb = colbox(j);
+                    if (intersects(rb, cb)) pair(i, rb, j, cb, fused ? colscore(j) : 1.0);
+                });
+        } else {
+            for (int j = 0; j < nc; ++j) pair(i, rb, j, colbox(j), fused ? colscore(j) : 1.0);
+        }
+    }
+    block_sync();
+    if (sh.lap.cnt[2]) return false;
+    const int n_pend = sh.lap.cnt[0];
+    // pass B: appearance cost of the pending pairs, one 16-lane group each
+    {
+        const int groups = nt / 16, g = t / 16;
+        for (int p = g; p < n_pend; p += groups) {
+            const int2 ij = pend[p];
+            const auto cf = colfeat(ij.y);
+            const double cd = cosine_dist16(rowfeat(ij.x), cf, D);
+            if ((lane_id() & 15) == 0) {
+                double emb = np_max(0.0, cd) / 2.0;                 // matching.py:164-166
+                if (emb > app) emb = 1.0;                           // bot_sort.py:318
+                double d;
+                const double c = iou_cost(rowbox(ij.x), colbox(ij.y),
+                                          fused ? colscore(ij.y) : 1.0, d);
+                const double cost = np_min(c, emb);                 // bot_sort.py:320
+                if (cost < thresh) push_edge(ij.x, ij.y, cost);
+            }
+        }
+    }
+    block_sync();
+    if (sh.lap.cnt[2]) return false;
+    const int E = sh.lap.cnt[1];
+    if (t == 0) *n_edges = E;
+    // row starts: exclusive scan of the counts (per-thread runs of rows)
+    {
+        const int per = (nr + nt - 1) / nt;
+        const int r0 = t * per < nr ? t * per : nr, r1 = r0 + per < nr ? r0 + per : nr;
+        int mine = 0;
+        for (int r = r0; r < r1; ++r) mine += ald(row_off + r + 1);
+        int tot;
+        int run = block_exclusive_scan(mine, sh.lap.wsum, &tot);
+        block_sync();
+        for (int r = r0; r < r1; ++r) {
+            const int k = ald(row_off + r + 1);
+            row_off[r + 1] = run;   // start of row r: the cursor, its end after the scatter
+            run += k;
+        }
+    }
+    ar.lo = lo0;   // the grid and the pending list are dead
+    int *csr_col = ar.alloc<int>(E);
+    double *csr_cost = ar.alloc<double>(E);
+    if (ar.fail) return false;
+    block_sync();
+    for (int e = t; e < E; e += nt) {
+        const int2 ij = edge[e];
+        const int k = atomicAdd(&row_off[ij.x + 1], 1);
+        csr_col[k] = ij.y;
+        csr_cost[k] = edge_c[e];
+    }
+    block_sync();
+    // the row ends came from atomics (L2): drop any stale L1 lines before plain loads of them
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    ar.hi = hi_rows;   // the edge list is dead
+    for (int r = t; r < nr; r += nt) {   // rows in column order (insertion sort, ~1 edge/row)
+        const int b = r == 0 ? 0 : ald(row_off + r), en = ald(row_off + r + 1);
+        for (int k = b + 1; k < en; ++k) {
+            const int cj = csr_col[k];
+            const double cc = csr_cost[k];
+            int q = k - 1;
+            while (q >= b && csr_col[q] > cj) {
+                csr_col[q + 1] = csr_col[q];
+                csr_cost[q + 1] = csr_cost[q];
+                --q;
+            }
+            csr_col[q + 1] = cj;
+            csr_cost[q + 1] = cc;
+        }
+    }
+    block_sync();
+    return lap_block(nr, nc, row_off, csr_col, csr_cost, col_deg, thresh, X, Y, err, ar, slab,
+                     sh.lap);
+}
+
+}  // namespace yta

@@ -56,10 +56,32 @@ __device__ __forceinline__ void store_kf(double *kf, long long slot, const KfSta
     }
 }
 
+// STrack.xyxy of a track's current mean: ByteTrack (xc, yc, a, h) (byte_tracker.py:100-111),
+// BoT-SORT (xc, yc, w, h) (bot_sort.py:173-182)
+template <int V>
 __device__ __forceinline__ Box kf_box(const double *kf, long long slot) {
     const double2 *m = reinterpret_cast<const double2 *>(kf + slot * KF_REC);
     const double2 a = m[0], b = m[1];
+    if (V == VAR_BOTSORT) {
+        const double xywh[4] = {a.x, a.y, b.x, b.y};
+        return xywh_to_box(xywh);
+    }
     return xyah_mean_to_box(a.x, a.y, b.x, b.y);
+}
+
+template <int V> constexpr int kf_model() { return V == VAR_BOTSORT ? KF_XYWH : KF_XYAH; }
+
+// A detection's normalised ReID feature as the reference holds it: the row e of get_features,
+// divided in place by its norm twice at STrack construction (bot_sort.py:40-48):
+// curr_feat = (e / n1) / n2, elementwise in float32.
+struct DetFeat {
+    const float *e;
+    float n1, n2;
+    __device__ __forceinline__ float operator()(int k) const { return (e[k] / n1) / n2; }
+};
+__device__ __forceinline__ DetFeat det_feat(const BtArgs &a, int s, long long db, int d) {
+    const float *fn = a.det_fn + (db + d) * 4;
+    return DetFeat{a.det_feat + ((long long)a.det_off[s] + d) * a.D, fn[0], fn[1]};
 }
 
 __device__ __forceinline__ int st_of(int flags) { return flags & FL_STATE; }
@@ -82,6 +104,7 @@ struct StageShared {
     AssocShared as;
 };
 
+template <int V>
 __device__ __forceinline__ bool stage1_body(const BtArgs &a, int s, Arena &ar, StageShared &sh) {
     int *wsum = sh.as.lap.wsum;
     const int t = threadIdx.x, nt = blockDim.x;
@@ -112,11 +135,20 @@ __device__ __forceinline__ bool stage1_body(const BtArgs &a, int s, Arena &ar, S
             const double *d = din + (long long)i * 6;
             double xywh[4];
             det_xyxy_to_xywh(d, xywh);
-            xywh_to_xyah(xywh, a.det_xyah + (db + i) * 4);
+            double *z = a.det_xyah + (db + i) * 4;
+            if (V == VAR_BOTSORT) {
+                z[0] = xywh[0];
+                z[1] = xywh[1];
+                z[2] = xywh[2];
+                z[3] = xywh[3];
+            } else {
+                xywh_to_xyah(xywh, z);
+            }
             const double conf = d[4];
             a.det_conf[db + i] = conf;
             a.det_cls[db + i] = d[5];
-            return conf > thr ? 1 : (conf > 0.1 && conf < thr ? 2 : 0);
+            // byte_tracker.py:149-158 (low bound 0.1) / bot_sort.py:263-269 (track_low_thresh)
+            return conf > thr ? 1 : (conf > a.low_thresh && conf < thr ? 2 : 0);
         },
         [&](int i, int cat, int pos) {
             const Box b = det_box(i);
@@ -143,7 +175,12 @@ __device__ __forceinline__ bool stage1_body(const BtArgs &a, int s, Arena &ar, S
     const int *tracked = a.tracked + tb;
     auto pred_box = [&](long long slot) {
         const double *m = a.kf + slot * KF_REC;
-        const double vh = st_of(a.flags[slot]) == ST_TRACKED ? m[7] : 0.0;
+        const bool trk = st_of(a.flags[slot]) == ST_TRACKED;
+        const double vh = trk ? m[7] : 0.0;
+        if (V == VAR_BOTSORT) {   // multi_predict zeroes vw and vh of non-tracked (:80-93)
+            const double p[4] = {m[0] + m[4], m[1] + m[5], m[2] + (trk ? m[6] : 0.0), m[3] + vh};
+            return xywh_to_box(p);
+        }
         return xyah_mean_to_box(m[0] + m[4], m[1] + m[5], m[2] + m[6], m[3] + vh);
     };
     const int2 au = block_compact2(
@@ -156,7 +193,7 @@ __device__ __forceinline__ bool stage1_body(const BtArgs &a, int s, Arena &ar, S
                 a.pool_box[tb + pos] = pred_box(tb + slot);
             } else {
                 a.unc[tb + pos] = slot;
-                a.unc_box[tb + pos] = kf_box(a.kf, tb + slot);
+                a.unc_box[tb + pos] = kf_box<V>(a.kf, tb + slot);
             }
         });
     const int n_act = au.x, n_unc = au.y;
@@ -168,11 +205,22 @@ __device__ __forceinline__ bool stage1_body(const BtArgs &a, int s, Arena &ar, S
     const int n_pool = n_act + n_lost;
     block_sync();
     YTA_STAMP(4);
-    const bool ok = assoc_block(
-        n_pool, [&](int i) { return a.pool_box[tb + i]; }, n_high,
-        [&](int j) { return a.high_box[db + j]; }, true,
-        [&](int j) { return a.high_score[db + j]; }, a.match_thresh, a.x1 + tb, a.y1 + db, &c->err,
-        &c->n_edges[0], ar, slab_of(a, s), sh.as, hbox, hw);
+    bool ok;
+    if (V == VAR_BOTSORT && a.D > 0)   // min(iou, gated appearance) (bot_sort.py:307-322)
+        ok = assoc_block_emb(
+            n_pool, [&](int i) { return a.pool_box[tb + i]; }, n_high,
+            [&](int j) { return a.high_box[db + j]; }, a.fuse_first != 0,
+            [&](int j) { return a.high_score[db + j]; },
+            [&](int i) { return a.feat + (tb + a.pool[tb + i]) * a.D; },
+            [&](int j) { return det_feat(a, s, db, a.high[db + j]); }, a.D, a.prox_thresh,
+            a.app_thresh, a.match_thresh, a.x1 + tb, a.y1 + db, &c->err, &c->n_edges[0], ar,
+            slab_of(a, s), sh.as);
+    else   // ByteTrack: fused IoU (:181-183); BoT-SORT without ReID: IoU, fused if fuse_first
+        ok = assoc_block(
+            n_pool, [&](int i) { return a.pool_box[tb + i]; }, n_high,
+            [&](int j) { return a.high_box[db + j]; }, V == VAR_BYTETRACK || a.fuse_first != 0,
+            [&](int j) { return a.high_score[db + j]; }, a.match_thresh, a.x1 + tb, a.y1 + db,
+            &c->err, &c->n_edges[0], ar, slab_of(a, s), sh.as, hbox, hw);
     if (!ok) return false;
     if (t == 0) {
         c->frame_id += 1;
@@ -193,6 +241,7 @@ __device__ __forceinline__ bool stage1_body(const BtArgs &a, int s, Arena &ar, S
 // Per stream: leftovers = unmatched Tracked pool rows (:205-209) x low detections, IoU, cost_limit
 // 0.5 (:210-211); rest = unmatched high detections (:229); unconfirmed x rest, fused IoU,
 // cost_limit 0.7 (:230-233).
+template <int V>
 __device__ __forceinline__ bool stage23_body(const BtArgs &a, int s, Arena &ar, StageShared &sh) {
     int *wsum = sh.as.lap.wsum;
     const int t = threadIdx.x, nt = blockDim.x;
@@ -225,11 +274,21 @@ __device__ __forceinline__ bool stage23_body(const BtArgs &a, int s, Arena &ar, 
     if (!ok) return false;
     ar.reset();
     YTA_STAMP_BASE(40);
-    ok = assoc_block(
-        n_unc, [&](int j) { return a.unc_box[tb + j]; }, n_rest,
-        [&](int r) { return a.high_box[db + a.rest[db + r]]; }, true,
-        [&](int r) { return a.rest_score[db + r]; }, 0.7, a.x3 + tb, a.y3 + db, &c->err,
-        &c->n_edges[2], ar, slab, sh.as);
+    if (V == VAR_BOTSORT && a.D > 0)   // bot_sort.py:355-370
+        ok = assoc_block_emb(
+            n_unc, [&](int j) { return a.unc_box[tb + j]; }, n_rest,
+            [&](int r) { return a.high_box[db + a.rest[db + r]]; }, true,
+            [&](int r) { return a.rest_score[db + r]; },
+            [&](int j) { return a.feat + (tb + a.unc[tb + j]) * a.D; },
+            [&](int r) { return det_feat(a, s, db, a.high[db + a.rest[db + r]]); }, a.D,
+            a.prox_thresh, a.app_thresh, 0.7, a.x3 + tb, a.y3 + db, &c->err, &c->n_edges[2], ar,
+            slab, sh.as);
+    else
+        ok = assoc_block(
+            n_unc, [&](int j) { return a.unc_box[tb + j]; }, n_rest,
+            [&](int r) { return a.high_box[db + a.rest[db + r]]; }, true,
+            [&](int r) { return a.rest_score[db + r]; }, 0.7, a.x3 + tb, a.y3 + db, &c->err,
+            &c->n_edges[2], ar, slab, sh.as);
     if (!ok) return false;
     if (t == 0) {
         c->n_left = n_left;
@@ -241,6 +300,7 @@ __device__ __forceinline__ bool stage23_body(const BtArgs &a, int s, Arena &ar, 
 // LDS first; a frame whose association does not fit is redone over the stream's global arena
 // (both bodies only write values that the redo rewrites identically, and bump the frame counter
 // only on success).
+template <int V>
 __global__ __launch_bounds__(BLK1) void k_stage1(BtArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     __shared__ StageShared sh;
@@ -249,14 +309,15 @@ __global__ __launch_bounds__(BLK1) void k_stage1(BtArgs a) {
     YTA_STAMP(0);
     {
         Arena ar(smem, a.lds_bytes);
-        if (stage1_body(a, s, ar, sh)) return;
+        if (stage1_body<V>(a, s, ar, sh)) return;
     }
     block_sync();
     if (threadIdx.x == 0) a.cnt[s].n_fallback[0] += 1;
     Arena ag(a.ws + s * a.ws_stride, a.ws_stride);
-    if (!stage1_body(a, s, ag, sh) && threadIdx.x == 0) atomicOr(&a.cnt[s].err, ERR_EDGE_OVERFLOW);
+    if (!stage1_body<V>(a, s, ag, sh) && threadIdx.x == 0) atomicOr(&a.cnt[s].err, ERR_EDGE_OVERFLOW);
 }
 
+template <int V>
 __global__ __launch_bounds__(BLK23) void k_stage23(BtArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     __shared__ StageShared sh;
@@ -265,18 +326,54 @@ __global__ __launch_bounds__(BLK23) void k_stage23(BtArgs a) {
     YTA_STAMP(0);
     {
         Arena ar(smem, a.lds_bytes23);
-        if (stage23_body(a, s, ar, sh)) return;
+        if (stage23_body<V>(a, s, ar, sh)) return;
     }
     block_sync();
     if (threadIdx.x == 0) a.cnt[s].n_fallback[1] += 1;
     Arena ag(a.ws + s * a.ws_stride, a.ws_stride);
-    if (!stage23_body(a, s, ag, sh) && threadIdx.x == 0) atomicOr(&a.cnt[s].err, ERR_EDGE_OVERFLOW);
+    if (!stage23_body<V>(a, s, ag, sh) && threadIdx.x == 0) atomicOr(&a.cnt[s].err, ERR_EDGE_OVERFLOW);
 }
 
 // ------------------------------------------------------------------------------------ k_apply
+// BoT-SORT STrack.update_cls (bot_sort.py:50-67): per-class summed scores, the first strict
+// maximum wins; a class not seen before is appended and taken as is.
+__device__ __forceinline__ double vote_cls(double2 *h, int &n, double cls, double score,
+                                           int *err) {
+    double out = cls;
+    if (n > 0) {
+        double maxf = 0.0;
+        bool found = false;
+        for (int e = 0; e < n; ++e) {
+            double2 c = h[e];
+            if (cls == c.x) {
+                c.y += score;
+                h[e] = c;
+                found = true;
+            }
+            if (c.y > maxf) {
+                maxf = c.y;
+                out = c.x;
+            }
+        }
+        if (!found) {
+            if (n < CLS_K) h[n++] = make_double2(cls, score);
+            else atomicOr(err, ERR_CLS_HIST);
+            out = cls;
+        }
+    } else {
+        h[0] = make_double2(cls, score);
+        n = 1;
+    }
+    return out;
+}
+
+// STrack.update / re_activate (byte_tracker.py:70-98; bot_sort.py:125-170) minus the feature EMA
+// (k_ema)
+template <int V>
 __device__ __forceinline__ void take_detection(const BtArgs &a, KfState &st, TrackMeta &m,
-                                               int &flags, long long det, int det_local, int fid) {
-    kf_update(st, a.det_xyah + det * 4);
+                                               int &flags, long long det, int det_local, int fid,
+                                               long long slot, int *err) {
+    kf_update<kf_model<V>()>(st, a.det_xyah + det * 4);
     const bool reactivate = st_of(flags) != ST_TRACKED;
     m.tracklet_len = reactivate ? 0 : m.tracklet_len + 1;
     flags = (flags & ~FL_STATE) | ST_TRACKED | FL_ACTIVATED;
@@ -284,6 +381,7 @@ __device__ __forceinline__ void take_detection(const BtArgs &a, KfState &st, Tra
     m.score = a.det_conf[det];
     m.cls = a.det_cls[det];
     m.det_ind = det_local;
+    if (V == VAR_BOTSORT) m.cls = vote_cls(a.cls_hist + slot * CLS_K, m.n_cls, m.cls, m.score, err);
 }
 
 // Records move between HBM and LDS in whole 16-B pieces with consecutive lanes on consecutive
@@ -292,12 +390,13 @@ __device__ __forceinline__ void take_detection(const BtArgs &a, KfState &st, Tra
 constexpr int APPLY_T = 128;              // tracks (= threads) per block
 constexpr int REC_PIECES = KF_REC / 2 + 3;
 
+template <int V>
 __global__ __launch_bounds__(APPLY_T) void k_apply(BtArgs a) {
     __shared__ double2 rec[APPLY_T][REC_PIECES];   // 60-dword rows: no bank conflicts
     __shared__ int s_slot[APPLY_T];
     __shared__ int s_wmask[APPLY_T];      // bit 0: write the Kalman record, bit 1: write the meta
     const int s = blockIdx.y, t = threadIdx.x;
-    const BtCounters *c = a.cnt + s;
+    BtCounters *c = a.cnt + s;
     const int n_pool = c->n_pool, n_unc = c->n_unc, fid = c->frame_id;
     const int i0 = blockIdx.x * APPLY_T;
     const int n_items = n_pool + n_unc;
@@ -308,13 +407,14 @@ __global__ __launch_bounds__(APPLY_T) void k_apply(BtArgs a) {
     // per-track decision (small loads only)
     // act: 0 predict only, 1 predict + stage-1 update, 2 predict + stage-2 update, 3 predict +
     // mark lost, 4 update (unconfirmed, stage 3), 5 remove (unconfirmed)
-    int slot = -1, det = -1, act = 0;
+    int slot = -1, det = -1, act = 0, hpos = -1;
     if (t < nloc) {
         if (i < n_pool) {
             slot = a.pool[tb + i];
             const int h = a.x1[tb + i];
             if (h >= 0) {                                            // stage 1 (:188-196)
                 act = 1;
+                hpos = h;
                 det = a.high[db + h];
             } else {
                 const int L = a.left_of_pool[tb + i];
@@ -334,12 +434,15 @@ __global__ __launch_bounds__(APPLY_T) void k_apply(BtArgs a) {
             const int r = a.x3[tb + j];
             if (r >= 0) {                                            // stage 3 (:234-236)
                 act = 4;
-                det = a.high[db + a.rest[db + r]];
+                hpos = a.rest[db + r];
+                det = a.high[db + hpos];
             } else {
                 act = 5;                                             // :237-240
             }
         }
         s_slot[t] = slot;
+        // BoT-SORT: tracks taking a high detection also take its feature (k_ema)
+        if (V == VAR_BOTSORT && a.D > 0) a.ema_job[tb + i] = hpos;
         // pieces this track rewrites: bit 0 the Kalman record, bit 1 the meta
         s_wmask[t] = act == 5 ? 0 : (act == 1 || act == 2 || act == 4 ? 3 : 1);
     }
@@ -367,11 +470,14 @@ __global__ __launch_bounds__(APPLY_T) void k_apply(BtArgs a) {
 #pragma unroll
             for (int k = 0; k < 16; ++k) st.c[k] = row[8 + k];
             const bool tracked = st_of(flags) == ST_TRACKED;
-            if (!tracked) st.m[7] = 0;                               // :41-42
-            kf_predict(st);
+            if (!tracked) {                                          // :41-42 / bot_sort.py:85-87
+                st.m[7] = 0;
+                if (V == VAR_BOTSORT) st.m[6] = 0;
+            }
+            kf_predict<kf_model<V>()>(st);
             wmask = 1;
             if (act == 1 || act == 2) {
-                take_detection(a, st, m, flags, db + det, det, fid);
+                take_detection<V>(a, st, m, flags, db + det, det, fid, tb + slot, &c->err);
                 wmask = 3;
             } else if (act == 3) {
                 flags = (flags & ~FL_STATE) | ST_LOST;
@@ -383,7 +489,7 @@ __global__ __launch_bounds__(APPLY_T) void k_apply(BtArgs a) {
             for (int k = 0; k < 8; ++k) st.m[k] = row[k];
 #pragma unroll
             for (int k = 0; k < 16; ++k) st.c[k] = row[8 + k];
-            take_detection(a, st, m, flags, db + det, det, fid);
+            take_detection<V>(a, st, m, flags, db + det, det, fid, tb + slot, &c->err);
             wmask = 3;
         } else {
             flags = (flags & ~FL_STATE) | ST_REMOVED | FL_REMOVED_NOW;
@@ -413,6 +519,79 @@ __global__ __launch_bounds__(APPLY_T) void k_apply(BtArgs a) {
     }
 }
 
+// ------------------------------------------------------------------------------ k_feat / k_ema
+// BoT-SORT features, one wave per row.  Norms follow np.linalg.norm on a float32 row (the sum of
+// squares rounded to float32, then sqrt in float32); the sum is accumulated in float64 here,
+// where OpenBLAS sdot accumulates in float32 lanes, so a norm may differ from the reference's in
+// its last bit (the parity tests compare features with a tolerance).
+__device__ __forceinline__ float f32_norm(double sumsq) { return sqrtf((float)sumsq); }
+
+// k_feat: per high detection (conf > track_high_thresh, the stage-1 predicate) the norms of the
+// in-place normalisations the reference applies to its row: n1 = |e|, n2 = |e/n1| (STrack
+// construction, :40-48) and n3 = |(e/n1)/n2| (when a track takes it, :40-41).
+constexpr int FEAT_T = 256;
+__global__ __launch_bounds__(FEAT_T) void k_feat(BtArgs a) {
+    const int s = blockIdx.y, lane = lane_id();
+    const int d = blockIdx.x * (FEAT_T / WAVE) + threadIdx.x / WAVE;
+    const int nd = min(a.det_off[s + 1] - a.det_off[s], a.MAXD);
+    if (d >= nd) return;
+    const long long row = (long long)a.det_off[s] + d;
+    if (!(a.det_in[row * 6 + 4] > a.track_thresh)) return;
+    const float *e = a.det_feat + row * a.D;
+    double q = 0.0;
+    for (int k = lane; k < a.D; k += WAVE) q += (double)e[k] * (double)e[k];
+    const float n1 = f32_norm(wave_reduce(RED_SUM, q));
+    q = 0.0;
+    for (int k = lane; k < a.D; k += WAVE) {
+        const float f = e[k] / n1;
+        q += (double)f * (double)f;
+    }
+    const float n2 = f32_norm(wave_reduce(RED_SUM, q));
+    q = 0.0;
+    for (int k = lane; k < a.D; k += WAVE) {
+        const float f = (e[k] / n1) / n2;
+        q += (double)f * (double)f;
+    }
+    const float n3 = f32_norm(wave_reduce(RED_SUM, q));
+    if (lane == 0) {
+        float *fn = a.det_fn + ((long long)s * a.MAXD + d) * 4;
+        fn[0] = n1;
+        fn[1] = n2;
+        fn[2] = n3;
+        fn[3] = 0.f;
+    }
+}
+
+// k_ema: update_features of every track that took a high detection this frame (bot_sort.py:40-48):
+// f = curr / |curr| with curr = (e/n1)/n2, smooth = 0.9 * smooth + 0.1 * f (float32), then
+// smooth /= |smooth|.
+constexpr int EMA_T = 256;
+__global__ __launch_bounds__(EMA_T) void k_ema(BtArgs a) {
+    const int s = blockIdx.y, lane = lane_id();
+    const BtCounters *c = a.cnt + s;
+    const int n_pool = c->n_pool, n_items = n_pool + c->n_unc;
+    const int item = blockIdx.x * (EMA_T / WAVE) + threadIdx.x / WAVE;
+    if (item >= n_items) return;
+    const long long tb = (long long)s * a.CAP, db = (long long)s * a.MAXD;
+    const int h = a.ema_job[tb + item];
+    if (h < 0) return;
+    const int slot = item < n_pool ? a.pool[tb + item] : a.unc[tb + item - n_pool];
+    const int d = a.high[db + h];
+    const float *fn = a.det_fn + (db + d) * 4;
+    const float n1 = fn[0], n2 = fn[1], n3 = fn[2];
+    const float *e = a.det_feat + ((long long)a.det_off[s] + d) * a.D;
+    float *sm = a.feat + (tb + slot) * a.D;
+    double q = 0.0;
+    for (int k = lane; k < a.D; k += WAVE) {
+        const float f = ((e[k] / n1) / n2) / n3;
+        const float v = 0.9f * sm[k] + 0.1f * f;
+        sm[k] = v;
+        q += (double)v * (double)v;
+    }
+    const float nrm = f32_norm(wave_reduce(RED_SUM, q));
+    for (int k = lane; k < a.D; k += WAVE) sm[k] = sm[k] / nrm;
+}
+
 // ------------------------------------------------------------------------------------ k_finish
 // Per stream: births (:242-248), lost expiry (:250-253), joint/sub list algebra incl. the
 // removed_stracks quirk (:257-265), duplicate removal (:312-325) through a grid over lost' (in an
@@ -432,6 +611,7 @@ __device__ __forceinline__ int track_age(const BtArgs &a, long long slot) {
     return a.meta[slot].frame_id - a.meta[slot].start_frame;   // STrack.end_frame - start_frame
 }
 
+template <int V>
 __device__ __forceinline__ void finish_body(const BtArgs &a, int s, unsigned *bits, Arena &ar,
                                             FinishShared &sh) {
     int *wsum = sh.wsum;
@@ -460,20 +640,33 @@ __device__ __forceinline__ void finish_body(const BtArgs &a, int s, unsigned *bi
         const int slot = a.free_list[tb + b];
         const int d = a.high[db + a.rest[db + a.birth[db + b]]];
         KfState st;
-        kf_initiate(a.det_xyah + (db + d) * 4, st);
+        kf_initiate<kf_model<V>()>(a.det_xyah + (db + d) * 4, st);
         store_kf(a.kf, tb + slot, st);
         TrackMeta m;
         m.score = a.det_conf[db + d];
         m.cls = a.det_cls[db + d];
         m.id = next_id + 1 + b;
         m.det_ind = d;
-        m.spare = 0;
+        m.n_cls = 0;
+        if (V == VAR_BOTSORT) {   // the detection's own STrack: cls_hist [[cls, score]] (:28)
+            a.cls_hist[(tb + slot) * CLS_K] = make_double2(m.cls, m.score);
+            m.n_cls = 1;
+        }
         a.flags[tb + slot] = ST_TRACKED | (fid == 1 ? FL_ACTIVATED : 0);
         m.frame_id = fid;
         m.start_frame = fid;
         m.tracklet_len = 0;
         m.pad = 0;
         a.meta[tb + slot] = m;
+    }
+    if (V == VAR_BOTSORT && a.D > 0) {   // smooth_feat of a birth = its detection's curr_feat
+        const int lane = lane_id(), nw = nt / WAVE;
+        for (int b = t / WAVE; b < n_births; b += nw) {
+            const int slot = a.free_list[tb + b];
+            const DetFeat f = det_feat(a, s, db, a.high[db + a.rest[db + a.birth[db + b]]]);
+            float *dst = a.feat + (tb + slot) * a.D;
+            for (int k = lane; k < a.D; k += WAVE) dst[k] = f(k);
+        }
     }
     YTA_STAMP(2);
     // lost-track expiry (:250-253); end_frame == frame_id
@@ -523,7 +716,7 @@ __device__ __forceinline__ void finish_body(const BtArgs &a, int s, unsigned *bi
         GridView gv{nullptr, ar.alloc<int>(ncell + 1), ar.alloc<int>(n_l2), ar.alloc<Box>(n_l2),
                     nullptr, ar.alloc<int>(n_l2)};
         Box *lcache = ar.try_alloc<Box>(n_l2);
-        auto lbox = [&](int q) { return kf_box(a.kf, tb + a.l2[tb + q]); };
+        auto lbox = [&](int q) { return kf_box<V>(a.kf, tb + a.l2[tb + q]); };
         if (lcache) {
             for (int q = t; q < n_l2; q += nt) lcache[q] = lbox(q);
             block_sync();
@@ -543,7 +736,7 @@ __device__ __forceinline__ void finish_body(const BtArgs &a, int s, unsigned *bi
             [&](int p) {
                 TBox v;
                 v.slot = tb + a.t2[tb + p];
-                v.b = kf_box(a.kf, v.slot);
+                v.b = kf_box<V>(a.kf, v.slot);
                 return v;
             },
             [&](int p, const TBox &v) {
@@ -598,7 +791,7 @@ __device__ __forceinline__ void finish_body(const BtArgs &a, int s, unsigned *bi
         [&](int pos) {
             const long long slot = tb + (os_arena ? outslot[pos] : a.t2[tb + pos]);
             Row r;
-            r.b = kf_box(a.kf, slot);
+            r.b = kf_box<V>(a.kf, slot);
             r.m = a.meta[slot];
             return r;
         },
@@ -627,6 +820,7 @@ __device__ __forceinline__ void finish_body(const BtArgs &a, int s, unsigned *bi
     }
 }
 
+template <int V>
 __global__ __launch_bounds__(BLKF) void k_finish(BtArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char fsmem[];
     __shared__ FinishShared sh;
@@ -641,10 +835,10 @@ __global__ __launch_bounds__(BLKF) void k_finish(BtArgs a) {
     const long long need = dedup_arena_bytes(c->n_lost + c->n_left);
     if (need <= (long long)a.lds_bytes_f) {
         Arena ar(fsmem + bits_bytes, a.lds_bytes_f);
-        finish_body(a, s, bits, ar, sh);
+        finish_body<V>(a, s, bits, ar, sh);
     } else {
         Arena ag(a.ws + s * a.ws_stride, a.ws_stride);
-        finish_body(a, s, bits, ag, sh);
+        finish_body<V>(a, s, bits, ag, sh);
     }
 }
 
@@ -693,7 +887,12 @@ using namespace yta;
 
 struct yta_bytetrack {
     int device = 0, S = 0, CAP = 0, MAXD = 0;
+    int variant = VAR_BYTETRACK, D = 0;
     yta_bytetrack_params prm{};
+    yta_botsort_params bprm{};
+    // BoT-SORT: per-frame ReID rows aligned with the detections (host staging + device)
+    float *h_feat = nullptr, *d_feat_in = nullptr;
+    long long feat_cap = 0;
     hipStream_t stream = nullptr;
     std::vector<void *> allocs;
     BtArgs a{};
@@ -744,10 +943,25 @@ int bt_alloc(yta_bytetrack *e) {
     a.S = e->S;
     a.CAP = e->CAP;
     a.MAXD = e->MAXD;
-    a.track_thresh = e->prm.track_thresh;
-    a.match_thresh = e->prm.match_thresh;
-    a.det_thresh = e->prm.track_thresh;                                        // :127
-    a.max_time_lost = (int)(e->prm.frame_rate / 30.0 * e->prm.track_buffer);   // :128-129
+    if (e->variant == VAR_BOTSORT) {   // bot_sort.py:185-229
+        const yta_botsort_params &b = e->bprm;
+        a.track_thresh = b.track_high_thresh;
+        a.low_thresh = b.track_low_thresh;
+        a.det_thresh = b.new_track_thresh;
+        a.match_thresh = b.match_thresh;
+        a.max_time_lost = (int)(b.frame_rate / 30.0 * b.track_buffer);
+        a.prox_thresh = b.proximity_thresh;
+        a.app_thresh = b.appearance_thresh;
+        a.fuse_first = b.fuse_first_associate;
+        a.D = e->D;
+    } else {
+        a.track_thresh = e->prm.track_thresh;
+        a.low_thresh = 0.1;                                                      // :150
+        a.match_thresh = e->prm.match_thresh;
+        a.det_thresh = e->prm.track_thresh;                                      // :127
+        a.max_time_lost = (int)(e->prm.frame_rate / 30.0 * e->prm.track_buffer); // :128-129
+        a.D = 0;
+    }
     DALLOC(a.kf, S * CAP * KF_REC);
     DALLOC(a.meta, S * CAP);
     DALLOC(a.flags, S * CAP);
@@ -782,12 +996,23 @@ int bt_alloc(yta_bytetrack *e) {
     DALLOC(a.y2, S * MAXD);
     DALLOC(a.y3, S * MAXD);
     DALLOC(a.out, S * CAP * 8);
+    if (e->variant == VAR_BOTSORT) {
+        DALLOC(a.cls_hist, S * CAP * CLS_K);
+        if (e->D > 0) {
+            DALLOC(a.feat, S * CAP * e->D);
+            DALLOC(a.det_fn, S * MAXD * 4);
+            DALLOC(a.ema_job, S * CAP);
+        }
+    }
     // association: LDS arena first; the global fallback arena holds the worst case (every pair a
     // candidate edge), so no frame can overflow it
     a.lds_bytes = BT_LDS_BYTES;
     a.lds_bytes23 = BT_LDS23_BYTES;
     a.lds_bytes_f = BT_LDSF_BYTES;
-    a.ws_stride = (assoc_arena_bytes(CAP, MAXD, CAP * MAXD) + 255) & ~255LL;
+    a.ws_stride = assoc_arena_bytes(CAP, MAXD, CAP * MAXD);
+    if (e->variant == VAR_BOTSORT && e->D > 0)
+        a.ws_stride = std::max(a.ws_stride, assoc_emb_arena_bytes(CAP, MAXD));
+    a.ws_stride = (a.ws_stride + 255) & ~255LL;
     DALLOC(a.ws, S * a.ws_stride);
     a.slab.R = (int)CAP;
     a.slab.C = (int)MAXD;
@@ -818,37 +1043,61 @@ int mark(yta_bytetrack *e) {
         if (_m) return _m; \
     } while (0)
 
-int set_lds_limits() {
-    YTA_HIP(hipFuncSetAttribute((const void *)k_stage1, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)BT_LDS_BYTES));
-    YTA_HIP(hipFuncSetAttribute((const void *)k_stage23, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)BT_LDS_BYTES));
+int set_lds_limits(size_t bytes) {
+    const int b = (int)bytes;
+    for (const void *k : {(const void *)k_stage1<VAR_BYTETRACK>, (const void *)k_stage1<VAR_BOTSORT>,
+                          (const void *)k_stage23<VAR_BYTETRACK>,
+                          (const void *)k_stage23<VAR_BOTSORT>})
+        YTA_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, b));
+    return YTA_OK;
+}
+
+// One frame of every stream: 4 launches (ByteTrack), + k_feat and k_ema (BoT-SORT with ReID).
+// Profiling marks bracket the phases stage1 (k_feat + k_stage1), stage23, apply (k_apply +
+// k_ema), finish.
+template <int V>
+int launch_frame(yta_bytetrack *e) {
+    BtArgs &a = e->a;
+    const bool reid = V == VAR_BOTSORT && a.D > 0;
+    MARK();
+    if (reid) {
+        const dim3 gf((a.MAXD + FEAT_T / WAVE - 1) / (FEAT_T / WAVE), a.S);
+        hipLaunchKernelGGL(k_feat, gf, dim3(FEAT_T), 0, e->stream, a);
+        YTA_HIP(hipGetLastError());
+    }
+    hipLaunchKernelGGL(k_stage1<V>, dim3(a.S), dim3(BLK1), a.lds_bytes, e->stream, a);
+    YTA_HIP(hipGetLastError());
+    MARK();
+    hipLaunchKernelGGL(k_stage23<V>, dim3(a.S), dim3(BLK23), a.lds_bytes23, e->stream, a);
+    YTA_HIP(hipGetLastError());
+    MARK();
+    const dim3 gt((a.CAP + APPLY_T - 1) / APPLY_T, a.S);
+    hipLaunchKernelGGL(k_apply<V>, gt, dim3(APPLY_T), 0, e->stream, a);
+    YTA_HIP(hipGetLastError());
+    if (reid) {
+        const dim3 ge((a.CAP + EMA_T / WAVE - 1) / (EMA_T / WAVE), a.S);
+        hipLaunchKernelGGL(k_ema, ge, dim3(EMA_T), 0, e->stream, a);
+        YTA_HIP(hipGetLastError());
+    }
+    MARK();
+    const size_t bits_bytes = ((size_t)12 * ((a.CAP + 31) / 32) + 15) & ~(size_t)15;
+    hipLaunchKernelGGL(k_finish<V>, dim3(a.S), dim3(BLKF), bits_bytes + a.lds_bytes_f, e->stream,
+                       a);
+    YTA_HIP(hipGetLastError());
+    MARK();
     return YTA_OK;
 }
 
 int launch_pipeline(yta_bytetrack *e, const double *det_in, const int *det_off, double *out,
-                    int *out_counts) {
+                    int *out_counts, const float *det_feat = nullptr) {
     BtArgs &a = e->a;
     a.det_in = det_in;
     a.det_off = det_off;
     a.out = out;
     a.out_counts = out_counts;
-    MARK();
-    hipLaunchKernelGGL(k_stage1, dim3(a.S), dim3(BLK1), a.lds_bytes, e->stream, a);
-    YTA_HIP(hipGetLastError());
-    MARK();
-    hipLaunchKernelGGL(k_stage23, dim3(a.S), dim3(BLK23), a.lds_bytes23, e->stream, a);
-    YTA_HIP(hipGetLastError());
-    MARK();
-    const dim3 gt((a.CAP + APPLY_T - 1) / APPLY_T, a.S);
-    hipLaunchKernelGGL(k_apply, gt, dim3(APPLY_T), 0, e->stream, a);
-    YTA_HIP(hipGetLastError());
-    MARK();
-    const size_t bits_bytes = ((size_t)12 * ((a.CAP + 31) / 32) + 15) & ~(size_t)15;
-    hipLaunchKernelGGL(k_finish, dim3(a.S), dim3(BLKF), bits_bytes + a.lds_bytes_f, e->stream, a);
-    YTA_HIP(hipGetLastError());
-    MARK();
-    return YTA_OK;
+    a.det_feat = det_feat;
+    return e->variant == VAR_BOTSORT ? launch_frame<VAR_BOTSORT>(e)
+                                     : launch_frame<VAR_BYTETRACK>(e);
 }
 
 void release_buffers(yta_bytetrack *e) {
@@ -873,6 +1122,9 @@ int reserve(yta_bytetrack *e, int cap, int maxd) {
     n->CAP = cap;
     n->MAXD = maxd;
     n->prm = e->prm;
+    n->variant = e->variant;
+    n->D = e->D;
+    n->bprm = e->bprm;
     n->stream = e->stream;
     int rc = bt_alloc(n);
     const size_t S = e->S, oc = e->CAP, nc = cap;
@@ -886,6 +1138,13 @@ int reserve(yta_bytetrack *e, int cap, int maxd) {
     if (!rc) rc = copy2d(n->a.meta, nc * sizeof(TrackMeta), e->a.meta, oc * sizeof(TrackMeta),
                          oc * sizeof(TrackMeta), S);
     if (!rc) rc = copy2d(n->a.flags, nc * 4, e->a.flags, oc * 4, oc * 4, S);
+    if (!rc && e->a.cls_hist)
+        rc = copy2d(n->a.cls_hist, nc * CLS_K * 16, e->a.cls_hist, oc * CLS_K * 16,
+                    oc * CLS_K * 16, S);
+    if (!rc && e->a.feat) {
+        const size_t row = (size_t)e->D * 4;
+        rc = copy2d(n->a.feat, nc * row, e->a.feat, oc * row, oc * row, S);
+    }
     if (!rc) rc = copy2d(n->a.tracked, nc * 4, e->a.tracked, oc * 4, oc * 4, S);
     if (!rc) rc = copy2d(n->a.lost, nc * 4, e->a.lost, oc * 4, oc * 4, S);
     if (!rc) {
@@ -935,12 +1194,13 @@ int check_errors(yta_bytetrack *e) {
     for (int s = 0; s < e->S; ++s) {
         const int err = e->h_cnt[s].err;
         if (err) {
-            set_error("stream %d: device error flags 0x%x (%s%s%s%s)", s, err,
+            set_error("stream %d: device error flags 0x%x (%s%s%s%s%s)", s, err,
                       err & ERR_EDGE_OVERFLOW ? "edge pool overflow " : "",
                       err & ERR_SOLVER ? "assignment solver failure " : "",
                       err & ERR_TRACK_CAPACITY ? "track capacity exceeded " : "",
-                      err & ERR_DET_CAPACITY ? "too many detections " : "");
-            return (err & (ERR_TRACK_CAPACITY | ERR_DET_CAPACITY | ERR_EDGE_OVERFLOW))
+                      err & ERR_DET_CAPACITY ? "too many detections " : "",
+                      err & ERR_CLS_HIST ? "class histogram full " : "");
+            return (err & (ERR_TRACK_CAPACITY | ERR_DET_CAPACITY | ERR_EDGE_OVERFLOW | ERR_CLS_HIST))
                        ? YTA_ERR_CAPACITY
                        : YTA_ERR_HIP;
         }
@@ -955,17 +1215,12 @@ int read_counters(yta_bytetrack *e) {
     return YTA_OK;
 }
 
-}  // namespace
 
-extern "C" {
-
-int yta_bytetrack_create(int device, int n_streams, int track_capacity, int max_dets,
-                         const yta_bytetrack_params *params, yta_bytetrack **engine) {
-    YTA_CHECK(engine && params, YTA_ERR_INVALID, "null engine/params");
+template <typename Init>
+int create_engine(int device, int n_streams, int track_capacity, int max_dets,
+                  yta_bytetrack **engine, Init init) {
     YTA_CHECK(n_streams > 0 && track_capacity > 0 && max_dets > 0, YTA_ERR_INVALID,
               "n_streams, track_capacity and max_dets must be positive");
-    YTA_CHECK(params->frame_rate > 0 && params->track_buffer >= 0, YTA_ERR_INVALID,
-              "frame_rate must be > 0 and track_buffer >= 0");
     *engine = nullptr;
     int rc = select_device(device);
     if (rc) return rc;
@@ -975,7 +1230,7 @@ int yta_bytetrack_create(int device, int n_streams, int track_capacity, int max_
     e->S = n_streams;
     e->CAP = track_capacity;
     e->MAXD = max_dets;
-    e->prm = *params;
+    init(e);
     hipError_t he = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
     if (he != hipSuccess) {
         set_error("hipStreamCreate: %s", hipGetErrorString(he));
@@ -983,7 +1238,7 @@ int yta_bytetrack_create(int device, int n_streams, int track_capacity, int max_
         return YTA_ERR_HIP;
     }
     rc = bt_alloc(e);
-    if (!rc) rc = set_lds_limits();
+    if (!rc) rc = set_lds_limits(BT_LDS_BYTES);
     if (!rc) rc = yta_bytetrack_reset(e);
     if (rc) {
         yta_bytetrack_destroy(e);
@@ -993,46 +1248,11 @@ int yta_bytetrack_create(int device, int n_streams, int track_capacity, int max_
     return YTA_OK;
 }
 
-int yta_bytetrack_destroy(yta_bytetrack *e) {
-    if (!e) return YTA_OK;
-    (void)hipSetDevice(e->device);
-    if (e->stream) (void)hipStreamSynchronize(e->stream);
-    release_buffers(e);
-    if (e->h_dets) (void)hipHostFree(e->h_dets);
-    if (e->d_det_in) (void)hipFree(e->d_det_in);
-    for (hipEvent_t h : e->ev) (void)hipEventDestroy(h);
-    if (e->stream) (void)hipStreamDestroy(e->stream);
-    delete e;
-    return YTA_OK;
-}
-
-int yta_bytetrack_reset(yta_bytetrack *e) {
-    YTA_CHECK(e, YTA_ERR_INVALID, "null engine");
-    YTA_HIP(hipSetDevice(e->device));
-    hipLaunchKernelGGL(k_reset, dim3(e->S), dim3(256), 0, e->stream, e->a);
-    YTA_HIP(hipGetLastError());
-    YTA_HIP(hipMemsetAsync(e->a.meta, 0, sizeof(TrackMeta) * (size_t)e->S * e->CAP, e->stream));
-    YTA_HIP(hipMemsetAsync(e->a.flags, 0, sizeof(int) * (size_t)e->S * e->CAP, e->stream));
-    YTA_HIP(hipStreamSynchronize(e->stream));
-    memset(e->h_cnt, 0, sizeof(BtCounters) * e->S);
-    return YTA_OK;
-}
-
-int yta_bytetrack_reserve(yta_bytetrack *e, int track_capacity, int max_dets) {
-    YTA_CHECK(e, YTA_ERR_INVALID, "null engine");
-    YTA_HIP(hipSetDevice(e->device));
-    return reserve(e, track_capacity, max_dets);
-}
-
-int yta_bytetrack_capacity(yta_bytetrack *e, int *track_capacity, int *max_dets) {
-    YTA_CHECK(e && track_capacity && max_dets, YTA_ERR_INVALID, "null argument");
-    *track_capacity = e->CAP;
-    *max_dets = e->MAXD;
-    return YTA_OK;
-}
-
-int yta_bytetrack_update(yta_bytetrack *e, const double *dets, const int *det_offsets,
-                         long long *next_id, double *out, int out_capacity, int *out_offsets) {
+// Host-buffer update shared by both trackers.  feats (BoT-SORT with ReID): per stream, the rows
+// get_features returned for that stream's high detections (conf > track_high_thresh, in
+// detection order), streams concatenated; staged here aligned with the detection rows.
+int update_host(yta_bytetrack *e, const double *dets, const int *det_offsets, const float *feats,
+                long long *next_id, double *out, int out_capacity, int *out_offsets) {
     YTA_CHECK(e && det_offsets && out_offsets, YTA_ERR_INVALID, "null argument");
     YTA_HIP(hipSetDevice(e->device));
     const int S = e->S;
@@ -1067,6 +1287,30 @@ int yta_bytetrack_update(yta_bytetrack *e, const double *dets, const int *det_of
         YTA_HIP(hipMemcpyAsync(e->d_det_in, e->h_dets, sizeof(double) * 6 * total,
                                hipMemcpyHostToDevice, e->stream));
     }
+    const int D = e->a.D;
+    if (D > 0 && total) {
+        if (total > e->feat_cap) {
+            if (e->d_feat_in) (void)hipFree(e->d_feat_in);
+            if (e->h_feat) (void)hipHostFree(e->h_feat);
+            e->d_feat_in = nullptr;
+            e->h_feat = nullptr;
+            e->feat_cap = 0;
+            const long long cap = std::max<long long>(2 * total, 1024);
+            YTA_HIP(hipMalloc((void **)&e->d_feat_in, sizeof(float) * D * cap));
+            YTA_HIP(hipHostMalloc((void **)&e->h_feat, sizeof(float) * D * cap,
+                                  hipHostMallocDefault));
+            e->feat_cap = cap;
+        }
+        long long k = 0;   // next high row of feats
+        for (long long r = 0; r < total; ++r)
+            if (dets[r * 6 + 4] > e->a.track_thresh) {
+                YTA_CHECK(feats, YTA_ERR_INVALID, "null feats with high detections");
+                memcpy(e->h_feat + r * D, feats + k * D, sizeof(float) * D);
+                ++k;
+            }
+        YTA_HIP(hipMemcpyAsync(e->d_feat_in, e->h_feat, sizeof(float) * D * total,
+                               hipMemcpyHostToDevice, e->stream));
+    }
     memcpy(e->h_off, det_offsets, sizeof(int) * (S + 1));
     YTA_HIP(hipMemcpyAsync(e->d_det_off, e->h_off, sizeof(int) * (S + 1), hipMemcpyHostToDevice,
                            e->stream));
@@ -1076,7 +1320,7 @@ int yta_bytetrack_update(yta_bytetrack *e, const double *dets, const int *det_of
                                  sizeof(BtCounters), sizeof(long long), S, hipMemcpyHostToDevice,
                                  e->stream));
     }
-    int rc = launch_pipeline(e, e->d_det_in, e->d_det_off, e->a.out, nullptr);
+    int rc = launch_pipeline(e, e->d_det_in, e->d_det_off, e->a.out, nullptr, e->d_feat_in);
     if (rc) return rc;
     rc = read_counters(e);
     if (rc) return rc;
@@ -1102,6 +1346,82 @@ int yta_bytetrack_update(yta_bytetrack *e, const double *dets, const int *det_of
     if (next_id)
         for (int s = 0; s < S; ++s) next_id[s] = e->h_cnt[s].next_id;
     return YTA_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int yta_bytetrack_create(int device, int n_streams, int track_capacity, int max_dets,
+                         const yta_bytetrack_params *params, yta_bytetrack **engine) {
+    YTA_CHECK(engine && params, YTA_ERR_INVALID, "null engine/params");
+    YTA_CHECK(params->frame_rate > 0 && params->track_buffer >= 0, YTA_ERR_INVALID,
+              "frame_rate must be > 0 and track_buffer >= 0");
+    yta_bytetrack_params prm = *params;
+    return create_engine(device, n_streams, track_capacity, max_dets, engine,
+                         [&](yta_bytetrack *e) { e->prm = prm; });
+}
+
+int yta_botsort_create(int device, int n_streams, int track_capacity, int max_dets, int feat_dim,
+                       const yta_botsort_params *params, yta_botsort **engine) {
+    YTA_CHECK(engine && params, YTA_ERR_INVALID, "null engine/params");
+    YTA_CHECK(params->frame_rate > 0 && params->track_buffer >= 0, YTA_ERR_INVALID,
+              "frame_rate must be > 0 and track_buffer >= 0");
+    YTA_CHECK(params->with_reid == 0 || feat_dim > 0, YTA_ERR_INVALID,
+              "with_reid needs feat_dim > 0");
+    yta_botsort_params prm = *params;
+    const int D = prm.with_reid ? feat_dim : 0;
+    return create_engine(device, n_streams, track_capacity, max_dets, engine,
+                         [&](yta_bytetrack *e) {
+                             e->variant = VAR_BOTSORT;
+                             e->bprm = prm;
+                             e->D = D;
+                         });
+}
+
+int yta_bytetrack_destroy(yta_bytetrack *e) {
+    if (!e) return YTA_OK;
+    (void)hipSetDevice(e->device);
+    if (e->stream) (void)hipStreamSynchronize(e->stream);
+    release_buffers(e);
+    if (e->h_dets) (void)hipHostFree(e->h_dets);
+    if (e->d_det_in) (void)hipFree(e->d_det_in);
+    if (e->h_feat) (void)hipHostFree(e->h_feat);
+    if (e->d_feat_in) (void)hipFree(e->d_feat_in);
+    for (hipEvent_t h : e->ev) (void)hipEventDestroy(h);
+    if (e->stream) (void)hipStreamDestroy(e->stream);
+    delete e;
+    return YTA_OK;
+}
+
+int yta_bytetrack_reset(yta_bytetrack *e) {
+    YTA_CHECK(e, YTA_ERR_INVALID, "null engine");
+    YTA_HIP(hipSetDevice(e->device));
+    hipLaunchKernelGGL(k_reset, dim3(e->S), dim3(256), 0, e->stream, e->a);
+    YTA_HIP(hipGetLastError());
+    YTA_HIP(hipMemsetAsync(e->a.meta, 0, sizeof(TrackMeta) * (size_t)e->S * e->CAP, e->stream));
+    YTA_HIP(hipMemsetAsync(e->a.flags, 0, sizeof(int) * (size_t)e->S * e->CAP, e->stream));
+    YTA_HIP(hipStreamSynchronize(e->stream));
+    memset(e->h_cnt, 0, sizeof(BtCounters) * e->S);
+    return YTA_OK;
+}
+
+int yta_bytetrack_reserve(yta_bytetrack *e, int track_capacity, int max_dets) {
+    YTA_CHECK(e, YTA_ERR_INVALID, "null engine");
+    YTA_HIP(hipSetDevice(e->device));
+    return reserve(e, track_capacity, max_dets);
+}
+
+int yta_bytetrack_capacity(yta_bytetrack *e, int *track_capacity, int *max_dets) {
+    YTA_CHECK(e && track_capacity && max_dets, YTA_ERR_INVALID, "null argument");
+    *track_capacity = e->CAP;
+    *max_dets = e->MAXD;
+    return YTA_OK;
+}
+
+int yta_bytetrack_update(yta_bytetrack *e, const double *dets, const int *det_offsets,
+                         long long *next_id, double *out, int out_capacity, int *out_offsets) {
+    return update_host(e, dets, det_offsets, nullptr, next_id, out, out_capacity, out_offsets);
 }
 
 int yta_bytetrack_update_device(yta_bytetrack *e, const double *d_dets, const int *d_det_offsets,
@@ -1219,16 +1539,76 @@ int yta_bytetrack_set_lds(yta_bytetrack *e, int bytes) {
     e->a.lds_bytes = (size_t)bytes & ~(size_t)15;
     e->a.lds_bytes23 = std::min(e->a.lds_bytes, BT_LDS23_BYTES);
     e->a.lds_bytes_f = std::min(e->a.lds_bytes, BT_LDSF_BYTES);
-    YTA_HIP(hipFuncSetAttribute((const void *)k_stage1, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)std::max<size_t>(e->a.lds_bytes, BT_LDS_BYTES)));
-    YTA_HIP(hipFuncSetAttribute((const void *)k_stage23, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)std::max<size_t>(e->a.lds_bytes, BT_LDS_BYTES)));
-    return YTA_OK;
+    return set_lds_limits(std::max<size_t>(e->a.lds_bytes, BT_LDS_BYTES));
 }
 
 int yta_bytetrack_hip_stream(yta_bytetrack *e, void **stream) {
     YTA_CHECK(e && stream, YTA_ERR_INVALID, "null argument");
     *stream = (void *)e->stream;
+    return YTA_OK;
+}
+
+static bool identity_warps(const double *w, int S) {
+    if (!w) return true;
+    for (int s = 0; s < S; ++s) {
+        const double *h = w + 6LL * s;
+        if (!(h[0] == 1.0 && h[1] == 0.0 && h[2] == 0.0 && h[3] == 0.0 && h[4] == 1.0 &&
+              h[5] == 0.0))
+            return false;
+    }
+    return true;
+}
+
+int yta_botsort_update(yta_botsort *e, const double *dets, const int *det_offsets,
+                       const float *feats, const double *warps, long long *next_id, double *out,
+                       int out_capacity, int *out_offsets) {
+    YTA_CHECK(e && e->variant == VAR_BOTSORT, YTA_ERR_INVALID, "not a BoT-SORT engine");
+    YTA_CHECK(identity_warps(warps, e->S), YTA_ERR_INVALID,
+              "camera-motion warps other than the identity are not supported yet");
+    return update_host(e, dets, det_offsets, feats, next_id, out, out_capacity, out_offsets);
+}
+
+int yta_botsort_update_device(yta_botsort *e, const double *d_dets, const int *d_det_offsets,
+                              const float *d_feats, double *d_out, int *d_out_counts) {
+    YTA_CHECK(e && e->variant == VAR_BOTSORT && d_det_offsets && d_out, YTA_ERR_INVALID,
+              "null argument / not a BoT-SORT engine");
+    YTA_CHECK(e->D == 0 || d_feats, YTA_ERR_INVALID, "null feats");
+    return launch_pipeline(e, d_dets, d_det_offsets, d_out, d_out_counts, d_feats);
+}
+
+int yta_botsort_get_features(yta_botsort *e, int stream, int *n_tracks, float *feats,
+                             double *cls_hist, int *n_cls) {
+    YTA_CHECK(e && e->variant == VAR_BOTSORT && n_tracks, YTA_ERR_INVALID,
+              "null argument / not a BoT-SORT engine");
+    YTA_CHECK(stream >= 0 && stream < e->S, YTA_ERR_INVALID, "bad stream %d", stream);
+    YTA_HIP(hipSetDevice(e->device));
+    const int rc = read_counters(e);
+    if (rc) return rc;
+    const BtCounters c = e->h_cnt[stream];
+    const long long tb = (long long)stream * e->CAP;
+    std::vector<int> lst(c.n_tracked + c.n_lost);
+    if (c.n_tracked)
+        YTA_HIP(hipMemcpy(lst.data(), e->a.tracked + tb, sizeof(int) * c.n_tracked,
+                          hipMemcpyDeviceToHost));
+    if (c.n_lost)
+        YTA_HIP(hipMemcpy(lst.data() + c.n_tracked, e->a.lost + tb, sizeof(int) * c.n_lost,
+                          hipMemcpyDeviceToHost));
+    std::vector<TrackMeta> meta(e->CAP);
+    YTA_HIP(hipMemcpy(meta.data(), e->a.meta + tb, sizeof(TrackMeta) * e->CAP,
+                      hipMemcpyDeviceToHost));
+    const int D = e->D;
+    int n = 0;
+    for (int slot : lst) {
+        if (feats && D)
+            YTA_HIP(hipMemcpy(feats + (long long)n * D, e->a.feat + (tb + slot) * D,
+                              sizeof(float) * D, hipMemcpyDeviceToHost));
+        if (cls_hist)
+            YTA_HIP(hipMemcpy(cls_hist + (long long)n * CLS_K * 2, e->a.cls_hist + (tb + slot) * CLS_K,
+                              sizeof(double2) * CLS_K, hipMemcpyDeviceToHost));
+        if (n_cls) n_cls[n] = meta[slot].n_cls;
+        ++n;
+    }
+    *n_tracks = n;
     return YTA_OK;
 }
 

@@ -1,4 +1,5 @@
-// ByteTrack engine: device-resident state for S independent streams (see bytetrack.hip).
+// Tracker engine (ByteTrack, BoT-SORT): device-resident state for S independent streams (see
+// bytetrack.hip).
 #pragma once
 #include "assoc.hpp"
 #include "kf_xyah.hpp"
@@ -17,7 +18,7 @@ struct TrackMeta {                   // 48 B, one per slot
     double cls;
     long long id;
     int det_ind;
-    int spare;                       // (the state flags live in BtArgs::flags)
+    int n_cls;                       // BoT-SORT: entries of the class histogram (update_cls)
     int frame_id;
     int start_frame;
     int tracklet_len;
@@ -42,10 +43,25 @@ struct BtCounters {                  // one per stream, 128 B
 static_assert(sizeof(BtCounters) == 128, "BtCounters layout");
 
 
+// Tracker variants (template parameter V of the kernels).
+constexpr int VAR_BYTETRACK = 0, VAR_BOTSORT = 1;
+constexpr int CLS_K = 8;             // BoT-SORT class-histogram entries per track
+
 struct BtArgs {
     int S, CAP, MAXD;
-    double track_thresh, match_thresh, det_thresh;
+    double track_thresh, match_thresh, det_thresh;   // det_thresh: births (BoT-SORT new_track_thresh)
+    double low_thresh;        // second-stage lower confidence bound (ByteTrack 0.1)
     int max_time_lost;
+    // BoT-SORT
+    double prox_thresh, app_thresh;
+    int fuse_first;           // fuse_first_associate
+    int D;                    // appearance feature length (0: with_reid off)
+    const float *det_feat;    // per frame: [rows of det_in][D] ReID features (high rows read)
+    float *det_fn;            // [S*MAXD][4] per high detection: the norms n1, n2, n3 of its row
+    float *feat;              // [S*CAP][D] smoothed track features
+    double2 *cls_hist;        // [S*CAP][CLS_K] (class, summed score)
+    int *ema_job;             // [S*CAP] per k_apply item: high position of the detection taken
+                              // with its feature, else -1
     // inputs
     const double *det_in;     // packed rows of 6
     const int *det_off;       // S+1
@@ -56,7 +72,7 @@ struct BtArgs {
     int *tracked, *lost, *free_list;   // [S*CAP]
     BtCounters *cnt;          // [S]
     // per-frame: detections [S*MAXD]
-    double *det_xyah;         // [S*MAXD][4]
+    double *det_xyah;         // [S*MAXD][4] Kalman measurement (ByteTrack xyah, BoT-SORT xywh)
     double *det_conf, *det_cls;
     int *high, *second, *rest, *birth;
     Box *high_box, *second_box;

@@ -1,5 +1,8 @@
-// ByteTrack constant-velocity Kalman filter in (xc, yc, a, h) space, float64, one track per thread.
-// Follows boxmot/motion/kalman_filters/bytetrack_kf.py:40-226.
+// Constant-velocity Kalman filters of ByteTrack (state (xc, yc, a, h), bytetrack_kf.py:40-226) and
+// BoT-SORT (state (xc, yc, w, h), botsort_kf.py:21-226), float64, one track per thread.  The two
+// differ only in their noise terms (template parameter M: KF_XYAH / KF_XYWH):
+//   XYAH: every std scales with the height h = mean[3]; the aspect terms are constants
+//   XYWH: x / w terms scale with the width w = mean[2], y / h terms with the height
 //
 // Layout.  initiate() builds a diagonal covariance (:85), Q and R are diagonal (:117, :148) and F
 // couples only position i with velocity i+4 (:44-46).  Hence every covariance the reference ever
@@ -22,17 +25,31 @@ namespace yta {
 constexpr double KF_W_POS = 1.0 / 20;    // bytetrack_kf.py:52
 constexpr double KF_W_VEL = 1.0 / 160;   // bytetrack_kf.py:53
 constexpr int KF_REC = 24;               // doubles per stored track
+constexpr int KF_XYAH = 0, KF_XYWH = 1;   // noise models
+
+// Per-axis standard deviations (before squaring) from a mean / measurement (n = 4 each):
+// scale(i) = h for XYAH, (w, h, w, h)[i] for XYWH.
+template <int M>
+__host__ __device__ __forceinline__ double kf_scale(const double *v, int i) {
+    return M == KF_XYWH ? ((i & 1) ? v[3] : v[2]) : v[3];
+}
 
 struct KfState {
     double m[8];
     double c[16];
 };
 
-// bytetrack_kf.py:55-86
+// bytetrack_kf.py:55-86 / botsort_kf.py:43-73
+template <int M = KF_XYAH>
 __host__ __device__ inline void kf_initiate(const double *z, KfState &s) {
-    const double h = z[3];
-    const double sp[4] = {2 * KF_W_POS * h, 2 * KF_W_POS * h, 1e-2, 2 * KF_W_POS * h};
-    const double sv[4] = {10 * KF_W_VEL * h, 10 * KF_W_VEL * h, 1e-5, 10 * KF_W_VEL * h};
+    double sp[4], sv[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const double g = kf_scale<M>(z, i);
+        const bool aspect = M == KF_XYAH && i == 2;
+        sp[i] = aspect ? 1e-2 : 2 * KF_W_POS * g;
+        sv[i] = aspect ? 1e-5 : 10 * KF_W_VEL * g;
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         s.m[i] = z[i];
@@ -53,11 +70,17 @@ __host__ __device__ inline void kf_predict_mean(const double *m, double *out) {
     }
 }
 
-// bytetrack_kf.py:155-192 (multi_predict) for one track.
+// bytetrack_kf.py:155-192 / botsort_kf.py:150-190 (multi_predict) for one track.
+template <int M = KF_XYAH>
 __host__ __device__ inline void kf_predict(KfState &s) {
-    const double h = s.m[3];
-    const double sp[4] = {KF_W_POS * h, KF_W_POS * h, 1e-2, KF_W_POS * h};
-    const double sv[4] = {KF_W_VEL * h, KF_W_VEL * h, 1e-5, KF_W_VEL * h};
+    double sp[4], sv[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const double g = kf_scale<M>(s.m, i);
+        const bool aspect = M == KF_XYAH && i == 2;
+        sp[i] = aspect ? 1e-2 : KF_W_POS * g;
+        sv[i] = aspect ? 1e-5 : KF_W_VEL * g;
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const double pp = s.c[4 * i], pv = s.c[4 * i + 1], vp = s.c[4 * i + 2], vv = s.c[4 * i + 3];
@@ -69,10 +92,13 @@ __host__ __device__ inline void kf_predict(KfState &s) {
     }
 }
 
-// bytetrack_kf.py:194-226 (+ project :126-153).
+// bytetrack_kf.py:194-226 (+ project :126-153) / botsort_kf.py:192-226 (+ project :110-148).
+template <int M = KF_XYAH>
 __host__ __device__ inline void kf_update(KfState &s, const double *z) {
-    const double h = s.m[3];
-    const double r[4] = {KF_W_POS * h, KF_W_POS * h, 1e-1, KF_W_POS * h};
+    double r[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+        r[i] = (M == KF_XYAH && i == 2) ? 1e-1 : KF_W_POS * kf_scale<M>(s.m, i);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const double pp = s.c[4 * i], pv = s.c[4 * i + 1], vp = s.c[4 * i + 2], vv = s.c[4 * i + 3];

@@ -31,6 +31,7 @@ constexpr int ERR_EDGE_OVERFLOW = 1;   // workspace too small for the frame (cap
 constexpr int ERR_SOLVER = 2;
 constexpr int ERR_TRACK_CAPACITY = 4;
 constexpr int ERR_DET_CAPACITY = 8;
+constexpr int ERR_CLS_HIST = 16;       // a BoT-SORT track voted over more than CLS_K classes
 
 __device__ __forceinline__ int ald(const int *p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -24,7 +24,18 @@ def create_tracker(tracker_type, tracker_config, reid_weights, device, half, per
         return BYTETracker(track_thresh=cfg.track_thresh, match_thresh=cfg.match_thresh,
                            track_buffer=cfg.track_buffer, frame_rate=cfg.frame_rate,
                            device=device)
-    if tracker_type in ("ocsort", "botsort", "deepocsort", "hybridsort", "strongsort"):
+    if tracker_type == "botsort":
+        from .trackers.botsort import BoTSORT
+        # reid_weights names the reference's ReID model (outside the hot path); an object with
+        # get_features(xyxys, img) passed in its place is used as the feature producer
+        reid = reid_weights if hasattr(reid_weights, "get_features") else None
+        return BoTSORT(reid_weights, device, half, track_high_thresh=cfg.track_high_thresh,
+                       track_low_thresh=cfg.track_low_thresh,
+                       new_track_thresh=cfg.new_track_thresh, track_buffer=cfg.track_buffer,
+                       match_thresh=cfg.match_thresh, proximity_thresh=cfg.proximity_thresh,
+                       appearance_thresh=cfg.appearance_thresh, cmc_method=cfg.cmc_method,
+                       frame_rate=cfg.frame_rate, reid=reid)
+    if tracker_type in ("ocsort", "deepocsort", "hybridsort", "strongsort"):
         raise NotImplementedError(
             f"{tracker_type}: not yet on the MI355X path in this build (ByteTrack is); see DESIGN.md")
     print("No such tracker")
