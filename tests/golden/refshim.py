@@ -175,4 +175,5 @@ def load():
     ns.matching = importlib.import_module("boxmot.utils.matching")
     ns.iou = importlib.import_module("boxmot.utils.iou")
     ns.ops = importlib.import_module("boxmot.utils.ops")
+    ns.ocsort = importlib.import_module("boxmot.trackers.ocsort.ocsort")
     return ns

@@ -152,3 +152,70 @@ def test_botsort_oracle_matches_reference(golden_dir, name):
     if D:
         assert np.array_equal(np.array([r[1].smooth_feat for r in recs], np.float32).reshape(-1, D),
                               g[f"{name}__st_feat"])
+
+
+# ------------------------------------------------------------------ OCSORT (G5)
+OCSORT_CASES = ["oc_n64_giou", "oc_n256_giou", "oc_n128_iou_mh3", "oc_n128_diou", "oc_n128_ciou",
+                "oc_n96_centroid", "oc_n128_byte", "oc_n64_dt5"]
+
+
+def ocsort_case(g, name):
+    """Inputs of a G5 case regenerated from its seed (checksum-pinned); returns
+    (frames [dets], img_shape, OCSortOracle kwargs)."""
+    from yolo_tracking_amd.synth import make_frames
+    n, nf, seed = (int(x) for x in g[f"{name}__gen"])
+    low, drop = (float(x) for x in g[f"{name}__stream"])
+    frames = [d for d, _ in make_frames(n, nf, seed, low_conf_frac=low, drop_frac=drop)]
+    assert float(np.sum([d.sum() for d in frames])) == g[f"{name}__in_sum"][0]
+    p = g[f"{name}__params"]
+    kw = dict(det_thresh=float(p[0]), max_age=int(p[1]), min_hits=int(p[2]),
+              asso_threshold=float(p[3]), delta_t=int(p[4]), inertia=float(p[5]),
+              use_byte=bool(p[6]), asso_func=str(g[f"{name}__asso"]))
+    return frames, tuple(int(v) for v in g[f"{name}__img"]), kw
+
+
+def golden_outputs(g, name):
+    oc, out = g[f"{name}__out_counts"], g[f"{name}__out"]
+    offs = np.concatenate([[0], np.cumsum(oc)])
+    return [out[offs[f]:offs[f + 1]] for f in range(len(oc))]
+
+
+def canonical_equal(outs_a, outs_b):
+    """Equal up to the numbering of same-frame births (rows matched by det_ind, one id
+    bijection over the stream); see tests/golden/make_goldens.py."""
+    fwd, bwd = {}, {}
+    for a, b in zip(outs_a, outs_b):
+        if a.shape != b.shape:
+            return False
+        if not len(a):
+            continue
+        a = a[np.argsort(a[:, 7], kind="stable")]
+        b = b[np.argsort(b[:, 7], kind="stable")]
+        if not np.array_equal(a[:, [0, 1, 2, 3, 5, 6, 7]], b[:, [0, 1, 2, 3, 5, 6, 7]]):
+            return False
+        for ia, ib in zip(a[:, 4], b[:, 4]):
+            if fwd.setdefault(ia, ib) != ib or bwd.setdefault(ib, ia) != ia:
+                return False
+    return True
+
+
+@pytest.mark.parametrize("name", OCSORT_CASES)
+def test_ocsort_oracle_matches_reference(golden_dir, name):
+    from oracle.ocsort import OCSortOracle
+    g = np.load(os.path.join(golden_dir, "ocsort_synth.npz"))
+    frames, img_shape, kw = ocsort_case(g, name)
+    t = OCSortOracle(**kw)
+    got = [np.asarray(t.update(d, img_shape), dtype=np.float64).reshape(-1, 8) for d in frames]
+    exp = golden_outputs(g, name)
+    assert canonical_equal(got, exp)
+    x = np.array([k.kf.x.ravel() for k in t.trackers]).reshape(-1, 7)
+    P = np.array([k.kf.P for k in t.trackers]).reshape(-1, 7, 7)
+    if bool(g[f"{name}__exact"]):
+        assert all(np.array_equal(a, b) for a, b in zip(got, exp))
+        assert np.array_equal([k.id for k in t.trackers], g[f"{name}__st_id"])
+        assert np.array_equal(x, g[f"{name}__st_x"])
+        assert np.array_equal(P, g[f"{name}__st_P"])
+    else:   # same tracker states, possibly listed in another birth order
+        ox, gx = np.lexsort(x.T[::-1]), np.lexsort(g[f"{name}__st_x"].T[::-1])
+        assert np.array_equal(x[ox], g[f"{name}__st_x"][gx])
+        assert np.array_equal(P[ox], g[f"{name}__st_P"][gx])

@@ -14,7 +14,7 @@ import numpy as np
 
 class SyntheticStream:
     def __init__(self, n_objects, seed, low_conf_frac=0.1, emb_dim=0, turnover=0.02,
-                 speed_sigma=1.5, jitter_sigma=0.5, shuffle=True, canvas=None):
+                 speed_sigma=1.5, jitter_sigma=0.5, shuffle=True, canvas=None, drop_frac=0.0):
         self.n = int(n_objects)
         self.rng = np.random.default_rng(seed)
         self.canvas = float(canvas) if canvas else 64.0 * np.sqrt(max(self.n, 1))
@@ -24,6 +24,8 @@ class SyntheticStream:
         self.speed_sigma = float(speed_sigma)
         self.jitter_sigma = float(jitter_sigma)
         self.shuffle = shuffle
+        self.drop_frac = float(drop_frac)   # missed detections per frame (drawn last, so 0 keeps
+                                            # every other draw of the stream unchanged)
         r = self.rng
         self.wh = r.uniform(16.0, 64.0, size=(self.n, 2))
         self.ctr = r.uniform(0.0, self.canvas, size=(self.n, 2))
@@ -67,6 +69,8 @@ class SyntheticStream:
         dets[:, 4] = conf
         dets[:, 5] = 0.0
         order = r.permutation(self.n) if self.shuffle else np.arange(self.n)
+        if self.drop_frac > 0:
+            order = order[r.random(self.n) >= self.drop_frac]
         dets = dets[order]
         embs = self.emb[order].copy() if self.emb is not None else None
         return dets, embs
