@@ -76,6 +76,12 @@ int yta_selftest(int device);
 int yta_lap_limited(int device, int nr, int nc, const double *cost, double cost_limit, int *x,
                     int *y);
 
+/* Padded dense assignment (association.py:20-28: lap.lapjv(cost, extend_cost=True), OCSORT
+ * family): zero-padded to max(nr, nc) square, every row / column of the smaller side matched;
+ * x[r] = col or -1, y[c] = row or -1.  The same operation and tie-breaking sequence as the
+ * restated lapjv (oracle/lapjv.c). */
+int yta_lap_padded(int device, int nr, int nc, const double *cost, int *x, int *y);
+
 /* ---- ByteTrack engine: S independent streams, state resident in HBM -----------------------
  * One engine = S trackers with identical parameters (BYTETracker(track_thresh, match_thresh,
  * track_buffer, frame_rate)).  Stream s keeps its own tracks and its own ID counter. */

@@ -63,6 +63,7 @@ _SIGS = {
     "yta_kf_xyah_update": ([_I, _I, _P, _P, _P], _I),
     "yta_grid_pairs": ([_I, _P, _I, _P, _I, _D, _P, _I, _P], _I),
     "yta_lap_limited": ([_I, _I, _I, _P, _D, _P, _P], _I),
+    "yta_lap_padded": ([_I, _I, _I, _P, _P, _P], _I),
     "yta_bytetrack_create": ([_I, _I, _I, _I, _P, _P], _I),
     "yta_bytetrack_destroy": ([_P], _I),
     "yta_bytetrack_reset": ([_P], _I),
@@ -201,6 +202,16 @@ def grid_pairs(a, b, thresh, device=0):
             p = pairs[:n.value]
             return p[np.lexsort((p[:, 1], p[:, 0]))]
         cap = n.value
+
+
+def lap_padded(cost, device=0):
+    """lap.lapjv(cost, extend_cost=True) -> (x, y) (association.py:20-28)."""
+    c = np.ascontiguousarray(cost, dtype=np.float64)
+    nr, nc = c.shape
+    x = np.empty(nr, dtype=np.int32)
+    y = np.empty(nc, dtype=np.int32)
+    check(load_library().yta_lap_padded(device, nr, nc, ptr(c), ptr(x), ptr(y)))
+    return x, y
 
 
 def lap_limited(cost, cost_limit, device=0):

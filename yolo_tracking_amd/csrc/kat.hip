@@ -6,6 +6,7 @@
 #include "assoc.hpp"
 #include "grid.hpp"
 #include "kf_xyah.hpp"
+#include "lap_dense.hpp"
 
 using namespace yta;
 
@@ -110,6 +111,30 @@ __global__ __launch_bounds__(1024) void k_lap_dense(const double *cost, int nr, 
     Arena ag(ws, ws_bytes);
     if (!lap_dense_body(cost, nr, nc, thresh, X, Y, err, ag, slab, sh) && threadIdx.x == 0)
         atomicOr(err, ERR_EDGE_OVERFLOW);
+}
+
+// One wave: the padded dense solve of association.py:20-28 (lapjv(cost, extend_cost=True)).
+// Work arrays in LDS (n <= LAP_PADDED_LDS_N) or in the global buffer `gws`.
+constexpr int LAP_PADDED_LDS_N = 1536;
+__global__ __launch_bounds__(64) void k_lap_padded(const double *cost, int nr, int nc, int *X,
+                                                   int *Y, int *err, unsigned char *gws) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int n = nr > nc ? nr : nc;
+    unsigned char *base = n <= LAP_PADDED_LDS_N ? smem : gws;
+    DenseLapWs w;
+    w.v = reinterpret_cast<double *>(base);
+    w.d = w.v + n;
+    w.x = reinterpret_cast<int *>(w.d + n);
+    w.y = w.x + n;
+    w.free_rows = w.y + n;
+    w.cols = w.free_rows + n;
+    w.pred = w.cols + n;
+    w.aux = w.pred + n;
+    auto c = [&](int r, int k) { return r < nr && k < nc ? cost[(long long)r * nc + k] : 0.0; };
+    const int rc = lap_dense_wave(n, c, w);
+    if (rc && lane_id() == 0) atomicOr(err, ERR_SOLVER);
+    for (int r = lane_id(); r < nr; r += WAVE) X[r] = w.x[r] < nc ? w.x[r] : -1;
+    for (int k = lane_id(); k < nc; k += WAVE) Y[k] = w.y[k] < nr ? w.y[k] : -1;
 }
 
 // One block: grid over b, then every a-box queries it; pairs with 1 - IoU < thresh are written
@@ -369,6 +394,43 @@ int yta_lap_limited(int device, int nr, int nc, const double *cost, double cost_
     YTA_HIP(hipMemcpy(y, dy, sizeof(int) * nc, hipMemcpyDeviceToHost));
     YTA_HIP(hipMemcpy(&herr, derr, sizeof(int), hipMemcpyDeviceToHost));
     YTA_CHECK(herr == 0, YTA_ERR_HIP, "assignment solver error flags 0x%x", herr);
+    return YTA_OK;
+}
+
+int yta_lap_padded(int device, int nr, int nc, const double *cost, int *x, int *y) {
+    YTA_CHECK(nr >= 0 && nc >= 0, YTA_ERR_INVALID, "negative size");
+    YTA_CHECK((nr == 0 || x) && (nc == 0 || y), YTA_ERR_INVALID, "null buffer");
+    for (int i = 0; i < nr; ++i) x[i] = -1;
+    for (int j = 0; j < nc; ++j) y[j] = -1;
+    if (nr == 0 && nc == 0) return YTA_OK;
+    YTA_CHECK((long long)nr * nc == 0 || cost, YTA_ERR_INVALID, "null buffer");
+    int rc = select_device(device);
+    if (rc) return rc;
+    DevBuf m;
+    const long long n = nr > nc ? nr : nc;
+    double *dcost = nullptr;
+    int *dx, *dy, *derr;
+    unsigned char *gws;
+    const size_t ws = (size_t)dense_lap_ws_bytes(n);
+    if ((long long)nr * nc) YTA_HIP(m.get(&dcost, (long long)nr * nc));
+    YTA_HIP(m.get(&dx, nr > 0 ? nr : 1));
+    YTA_HIP(m.get(&dy, nc > 0 ? nc : 1));
+    YTA_HIP(m.get(&derr, 1));
+    YTA_HIP(m.get(&gws, ws));
+    YTA_HIP(hipMemset(derr, 0, sizeof(int)));
+    if (dcost)
+        YTA_HIP(hipMemcpy(dcost, cost, sizeof(double) * nr * nc, hipMemcpyHostToDevice));
+    const size_t lds = n <= LAP_PADDED_LDS_N ? ws : 0;
+    YTA_HIP(hipFuncSetAttribute((const void *)k_lap_padded,
+                                hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)dense_lap_ws_bytes(LAP_PADDED_LDS_N)));
+    hipLaunchKernelGGL(k_lap_padded, dim3(1), dim3(64), lds, 0, dcost, nr, nc, dx, dy, derr, gws);
+    YTA_HIP(hipGetLastError());
+    int herr = 0;
+    if (nr) YTA_HIP(hipMemcpy(x, dx, sizeof(int) * nr, hipMemcpyDeviceToHost));
+    if (nc) YTA_HIP(hipMemcpy(y, dy, sizeof(int) * nc, hipMemcpyDeviceToHost));
+    YTA_HIP(hipMemcpy(&herr, derr, sizeof(int), hipMemcpyDeviceToHost));
+    YTA_CHECK(herr == 0, YTA_ERR_HIP, "padded assignment solver error flags 0x%x", herr);
     return YTA_OK;
 }
 
