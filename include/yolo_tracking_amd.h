@@ -13,6 +13,12 @@
  *                            (created by boxmot/tracker_zoo.py:66-81 create_tracker('botsort', ...));
  *                            the ReID forward pass (reid_multibackend.py:303-311) and the CMC
  *                            estimator (sof.py) stay outside: their outputs are inputs here
+ *   yta_ocsort_*             boxmot/trackers/ocsort/ocsort.py:188-379  OCSort.__init__/update
+ *                            (created by boxmot/tracker_zoo.py:42-55 create_tracker('ocsort', ...))
+ *   yta_lap_padded           boxmot/utils/association.py:20-28 linear_assignment -> lap.lapjv(cost,
+ *                            extend_cost=True)
+ *   yta_kf7_run              boxmot/motion/kalman_filters/ocsort_kf.py:339-526 predict / update incl.
+ *                            freeze / unfreeze (observation-centric re-update)
  *   yta_box_affinity         boxmot/utils/iou.py:6-188  iou/giou/diou/ciou/centroid_batch
  *   yta_iou_distance         boxmot/utils/matching.py:94-119 iou_distance (+ fuse_score :213-221)
  *   yta_kf_xyah_initiate     boxmot/motion/kalman_filters/bytetrack_kf.py:55-86
@@ -183,6 +189,57 @@ int yta_botsort_update_device(yta_botsort *engine, const double *d_dets, const i
  * per track, may be NULL) and their entry counts (may be NULL). */
 int yta_botsort_get_features(yta_botsort *engine, int stream, int *n_tracks, float *feats,
                              double *cls_hist, int *n_cls);
+
+/* ---- OCSORT engine: S independent streams ------------------------------------------------
+ * OCSort(per_class, det_thresh, max_age, min_hits, asso_threshold, delta_t, asso_func, inertia,
+ * use_byte) per stream; the KalmanBoxTracker.count ID counter per stream (next_id in / out as
+ * for ByteTrack; the Python front-end shares one counter per process like the reference). */
+typedef struct yta_ocsort yta_ocsort;
+#define YTA_ASSO_IOU 0
+#define YTA_ASSO_GIOU 1
+#define YTA_ASSO_DIOU 2
+#define YTA_ASSO_CIOU 3
+#define YTA_ASSO_CENTROID 4
+typedef struct {
+    double det_thresh;       /* ocsort.yaml: 0      (ctor default 0.2)  */
+    int max_age;             /* 30                                      */
+    int min_hits;            /* 1                   (ctor default 3)    */
+    double asso_threshold;   /* iou_thresh 0.3                          */
+    int delta_t;             /* 3  (1..8)                               */
+    int asso_func;           /* YTA_ASSO_*: giou    (ctor default iou)  */
+    double inertia;          /* 0.2                                     */
+    int use_byte;            /* 0                                       */
+} yta_ocsort_params;
+
+int yta_ocsort_create(int device, int n_streams, int track_capacity, int max_dets,
+                      const yta_ocsort_params *params, yta_ocsort **engine);
+int yta_ocsort_destroy(yta_ocsort *engine);
+int yta_ocsort_reset(yta_ocsort *engine);
+int yta_ocsort_capacity(yta_ocsort *engine, int *track_capacity, int *max_dets);
+/* Host-buffer update (synchronous): dets / det_offsets / next_id / out / out_offsets as
+ * yta_bytetrack_update; img_wh: S x (width, height) of the frames (img.shape[1], img.shape[0];
+ * read by the centroid cost only, may be NULL otherwise).  Output rows per stream in the
+ * reference's order (reversed tracker list), id = tracker id + 1. */
+int yta_ocsort_update(yta_ocsort *engine, const double *dets, const int *det_offsets,
+                      const int *img_wh, long long *next_id, double *out, int out_capacity,
+                      int *out_offsets);
+/* Device-resident update (asynchronous): d_out holds S * track_capacity rows x 8. */
+int yta_ocsort_update_device(yta_ocsort *engine, const double *d_dets, const int *d_det_offsets,
+                             const int *d_img_wh, double *d_out, int *d_out_counts);
+int yta_ocsort_sync(yta_ocsort *engine);
+/* Parity introspection, tracker-list order: ints 7 x int64 per tracker (id, age, hits,
+ * hit_streak, time_since_update, kf.observed, kf.attr_saved is not None), x (7 f64), P (49 f64). */
+int yta_ocsort_get_state(yta_ocsort *engine, int stream, int *n_tracks, long long *ints,
+                         double *x, double *P);
+/* Last frame's counts summed over streams: dets, first-round dets, BYTE dets, live trackers,
+ * output rows, births, LAP calls, fast-path frames (8 int64). */
+int yta_ocsort_stats(yta_ocsort *engine, long long *stats);
+int yta_ocsort_hip_stream(yta_ocsort *engine, void **stream);
+/* OCSORT Kalman KAT: n tracks initialised from z0 (n x 4, [u, v, s, r]) run `steps` steps of
+ * predict + update(z[step] (n x 4 per step); a NaN first value = update(None)), freeze /
+ * unfreeze included; final x (n x 7) and full P (n x 49). */
+int yta_kf7_run(int device, int n, int steps, const double *z0, const double *z, double *x_out,
+                double *P_out);
 
 #ifdef __cplusplus
 }

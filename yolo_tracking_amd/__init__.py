@@ -12,9 +12,11 @@ __version__ = "10.0.51+mi355x.1"
 from .tracker_zoo import create_tracker, get_tracker_config  # noqa: E402
 from .trackers.bytetrack import BYTETracker, ByteTrackEngine  # noqa: E402
 from .trackers.botsort import BoTSORT, BoTSORTEngine  # noqa: E402
+from .trackers.ocsort import OCSort, OCSortEngine  # noqa: E402
 
 TRACKERS = ["bytetrack", "botsort", "strongsort", "ocsort", "deepocsort", "hybridsort"]
 
-__all__ = ("__version__", "BYTETracker", "ByteTrackEngine", "BoTSORT", "BoTSORTEngine",
+__all__ = ("__version__", "BYTETracker", "ByteTrackEngine", "BoTSORT", "BoTSORTEngine", "OCSort",
+           "OCSortEngine",
            "create_tracker",
            "get_tracker_config", "TRACKERS")

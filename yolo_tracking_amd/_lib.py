@@ -46,6 +46,16 @@ class BotParams(ctypes.Structure):
                 ("fuse_first_associate", ctypes.c_int), ("with_reid", ctypes.c_int)]
 
 
+class OcParams(ctypes.Structure):
+    """yta_ocsort_params (include/yolo_tracking_amd.h)."""
+    _fields_ = [("det_thresh", ctypes.c_double), ("max_age", ctypes.c_int),
+                ("min_hits", ctypes.c_int), ("asso_threshold", ctypes.c_double),
+                ("delta_t", ctypes.c_int), ("asso_func", ctypes.c_int),
+                ("inertia", ctypes.c_double), ("use_byte", ctypes.c_int)]
+
+
+ASSO_FUNCS = {"iou": 0, "giou": 1, "diou": 2, "ciou": 3, "centroid": 4}
+
 _lib = None
 
 _P = ctypes.c_void_p
@@ -83,6 +93,17 @@ _SIGS = {
     "yta_botsort_update": ([_P, _P, _P, _P, _P, _P, _P, _I, _P], _I),
     "yta_botsort_update_device": ([_P, _P, _P, _P, _P, _P], _I),
     "yta_botsort_get_features": ([_P, _I, _P, _P, _P, _P], _I),
+    "yta_ocsort_create": ([_I, _I, _I, _I, _P, _P], _I),
+    "yta_ocsort_destroy": ([_P], _I),
+    "yta_ocsort_reset": ([_P], _I),
+    "yta_ocsort_capacity": ([_P, _P, _P], _I),
+    "yta_ocsort_update": ([_P, _P, _P, _P, _P, _P, _I, _P], _I),
+    "yta_ocsort_update_device": ([_P, _P, _P, _P, _P, _P], _I),
+    "yta_ocsort_sync": ([_P], _I),
+    "yta_ocsort_get_state": ([_P, _I, _P, _P, _P, _P], _I),
+    "yta_ocsort_stats": ([_P, _P], _I),
+    "yta_ocsort_hip_stream": ([_P, _P], _I),
+    "yta_kf7_run": ([_I, _I, _I, _P, _P, _P, _P], _I),
 }
 
 EXPORTED_SYMBOLS = tuple(_SIGS)
@@ -202,6 +223,17 @@ def grid_pairs(a, b, thresh, device=0):
             p = pairs[:n.value]
             return p[np.lexsort((p[:, 1], p[:, 0]))]
         cap = n.value
+
+
+def kf7_run(z0, z, device=0):
+    """OCSORT Kalman KAT (yta_kf7_run): z0 (n, 4), z (steps, n, 4) with NaN rows = missed."""
+    z0 = np.ascontiguousarray(z0, dtype=np.float64).reshape(-1, 4)
+    n = len(z0)
+    z = np.ascontiguousarray(z, dtype=np.float64).reshape(-1, n, 4)
+    x = np.empty((n, 7))
+    P = np.empty((n, 7, 7))
+    check(load_library().yta_kf7_run(device, n, len(z), ptr(z0), ptr(z), ptr(x), ptr(P)))
+    return x, P
 
 
 def lap_padded(cost, device=0):

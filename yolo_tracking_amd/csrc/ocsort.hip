@@ -1,0 +1,1118 @@
+// OCSORT update() for S independent streams on gfx950, all tracker state resident in HBM.
+//
+// Follows boxmot/trackers/ocsort/ocsort.py:188-379 with boxmot/utils/association.py:8-28,
+// :111-201 and the live paths of ocsort_kf.py (kf_ocsort.hpp).  One frame = one launch of
+// k_ocsort (one block per stream) whose phases keep the reference's list semantics:
+//   A  predict every tracker (x[6] clamp, Kalman predict, age / hit_streak / time_since_update,
+//      :168-181), predicted boxes; trackers whose box has a NaN are dropped (:254-264)
+//   B  per-column association inputs in tracker order: box, velocity (or 0), k_previous_obs
+//      (:14-22), last observation
+//   C  detections: conf > det_thresh (first / OCR rounds), 0.1 < conf < det_thresh (BYTE round)
+//   D  dense asso (iou / giou / diou / ciou / centroid, dets x trackers) and the OCSORT cost
+//      -(asso + angle), angle = ((valid * (pi/2 - |acos(clip(v . dir))|) / pi) * inertia) * score
+//   E  fast path when every row and column has at most one asso > thr (and one has exactly one),
+//      else the padded dense LAP (lap_dense.hpp, one wave); matches filtered by asso >= thr; the
+//      unmatched lists in the reference's order (scan order, then the filtered pairs)
+//   F  BYTE round (use_byte) and G  OCR round: asso of the leftovers (OCR: against the trackers'
+//      last observations), LAP on -asso when its max exceeds thr, lists replaced by the sorted
+//      set differences (np.setdiff1d)
+//   H  tracker updates, one thread per tracker: velocity from the observation delta_t ages back,
+//      observation ring, Kalman update with the observation-centric re-update (freeze on the first
+//      miss, restore + virtual-trajectory replay on re-acquisition)
+//   I  births in unmatched-list order; J  output rows in reversed tracker order, then trackers
+//      unseen for more than max_age frames are dropped.
+#include <algorithm>
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "geometry.hpp"
+#include "kf_ocsort.hpp"
+#include "lap.hpp"
+#include "lap_dense.hpp"
+
+namespace yta {
+namespace {
+
+constexpr int OC_T = 256;          // threads per stream block
+constexpr int OC_DT_MAX = 8;       // delta_t capacity of the observation ring
+constexpr int OC_LDS_LAP_N = 1536; // dense LAP work arrays in LDS up to this n
+
+constexpr int OF_OBSERVED = 1;     // KalmanFilter.observed
+constexpr int OF_SAVED = 2;        // KalmanFilter.attr_saved is not None
+constexpr int OF_VELOCITY = 4;     // velocity is not None
+constexpr int ERR_GIOU = 32;       // giou enclosure assert (iou.py:58)
+
+struct OcTrack {                   // one slot
+    Kf7 kf;                        // live filter
+    Kf7 fz;                        // frozen copy (freeze, ocsort_kf.py:383-387)
+    double hist_z[4];              // last non-None entry of history_obs
+    double last_obs[5];            // last_observation (placeholder -1s)
+    double vel[2];                 // velocity (dy, dx)
+    double conf, cls;
+    double obs[OC_DT_MAX][5];      // ring of the latest delta_t observations
+    long long id;
+    int obs_age[OC_DT_MAX];
+    int obs_n;                     // observations inserted so far (ring position = n % delta_t)
+    int det_ind, age, hits, hit_streak, tsu, flags, hist_since;
+};
+
+struct OcCounters {                // one per stream
+    long long next_id;             // KalmanBoxTracker.count
+    int frame;
+    int n_trk, n_free;
+    int n_dets, n_high, n_second, n_out, n_births;
+    int lap_calls, fast_path;
+    int err;
+    int pad[18];
+};
+static_assert(sizeof(OcCounters) == 128, "OcCounters layout");
+
+struct OcArgs {
+    int S, CAP, MAXD;
+    double det_thresh, thr, inertia;
+    int max_age, min_hits, delta_t, asso, use_byte;
+    const double *det_in;          // packed rows of 6
+    const int *det_off;            // S + 1
+    const int *img_wh;             // S x (w, h) or null
+    OcTrack *rec;                  // [S*CAP]
+    int *list, *free_list;         // [S*CAP]
+    OcCounters *cnt;
+    // per frame
+    int *hi_row, *lo_row;          // [S*MAXD] input rows of the first / BYTE detections
+    Box *cbox;                     // [S*CAP] predicted boxes (tracker order)
+    double *cvel, *ckobs, *clast;  // [S*CAP] x 2 / 5 / 5
+    int *nan_flag;                 // [S*CAP]
+    double *mat, *mat2;            // [S*MAXD*CAP] asso, cost
+    int *rmatch;                   // [S*MAXD] first-round column of each row (-1)
+    int *cmatched;                 // [S*CAP]
+    int *udet, *utrk, *tmp;        // [S*(MAXD+CAP)]
+    int *upd;                      // [S*CAP] update source per tracker: input row, -1 none
+    unsigned char *lap_ws;         // per stream (n > OC_LDS_LAP_N)
+    long long lap_ws_stride;
+    double *out;                   // [S*CAP*8]
+    int *out_counts;
+};
+
+__device__ __forceinline__ double asso_of(int kind, const Box &d, const Box &t, double w, double h) {
+    switch (kind) {
+        case 0: return iou(d, t);
+        case 1: return giou(d, t);
+        case 2: return diou(d, t);
+        case 3: return ciou(d, t);
+        default: return centroid(d, t, w, h);
+    }
+}
+
+__device__ __forceinline__ Box box5(const double *b) { return Box{b[0], b[1], b[2], b[3]}; }
+
+// k_previous_obs (ocsort.py:14-22) from the ring
+__device__ __forceinline__ void k_prev_obs(const OcTrack &r, int dt, double *o) {
+    if (r.obs_n == 0) {
+        for (int k = 0; k < 5; ++k) o[k] = -1.0;
+        return;
+    }
+    const int m = r.obs_n < dt ? r.obs_n : dt;
+    for (int i = 0; i < dt; ++i) {
+        const int want = r.age - (dt - i);
+        for (int e = 0; e < m; ++e)
+            if (r.obs_age[e] == want) {
+                for (int k = 0; k < 5; ++k) o[k] = r.obs[e][k];
+                return;
+            }
+    }
+    for (int k = 0; k < 5; ++k) o[k] = r.last_obs[k];   // the newest observation
+}
+
+// KalmanBoxTracker.update (ocsort.py:130-166) + KalmanFilter.update (ocsort_kf.py:437-526)
+__device__ void tracker_update(OcTrack &r, const double *det, int det_local, int dt) {
+    if (!det) {                                   // update(None)
+        r.det_ind = -1;
+        if (r.flags & OF_OBSERVED) {              // freeze on the first miss
+            r.fz = r.kf;
+            r.flags |= OF_SAVED;
+        }
+        r.flags &= ~OF_OBSERVED;
+        r.hist_since += 1;
+        return;
+    }
+    double bbox[5] = {det[0], det[1], det[2], det[3], det[4]};
+    r.det_ind = det_local;
+    r.conf = bbox[4];
+    r.cls = det[5];
+    if (np_sum5(r.last_obs) >= 0) {
+        const double *prev = r.last_obs;
+        const int m = r.obs_n < dt ? r.obs_n : dt;
+        bool found = false;
+        for (int i = 0; i < dt && !found; ++i) {
+            const int want = r.age - (dt - i);
+            for (int e = 0; e < m; ++e)
+                if (r.obs_age[e] == want) {
+                    prev = r.obs[e];
+                    found = true;
+                    break;
+                }
+        }
+        // speed_direction (ocsort.py:57-62)
+        const double cx1 = (prev[0] + prev[2]) / 2.0, cy1 = (prev[1] + prev[3]) / 2.0;
+        const double cx2 = (bbox[0] + bbox[2]) / 2.0, cy2 = (bbox[1] + bbox[3]) / 2.0;
+        const double sy = cy2 - cy1, sx = cx2 - cx1;
+        const double nrm = sqrt(sy * sy + sx * sx) + 1e-6;
+        r.vel[0] = sy / nrm;
+        r.vel[1] = sx / nrm;
+        r.flags |= OF_VELOCITY;
+    }
+    for (int k = 0; k < 5; ++k) r.last_obs[k] = bbox[k];
+    const int slot = r.obs_n % dt;
+    for (int k = 0; k < 5; ++k) r.obs[slot][k] = bbox[k];
+    r.obs_age[slot] = r.age;
+    r.obs_n += 1;
+    r.tsu = 0;
+    r.hits += 1;
+    r.hit_streak += 1;
+    double z[4];
+    oc_bbox_to_z(bbox, z);
+    if (!(r.flags & OF_OBSERVED) && (r.flags & OF_SAVED)) {
+        // unfreeze: restore, replay the virtual trajectory from the last kept observation
+        r.kf = r.fz;
+        r.flags &= ~OF_SAVED;   // the restored attr_saved is the one before the freeze: None
+        kf7_replay(r.kf, r.hist_z, z, r.hist_since + 1, r.hist_z);
+    } else {
+        for (int k = 0; k < 4; ++k) r.hist_z[k] = z[k];
+    }
+    r.hist_since = 0;
+    r.flags |= OF_OBSERVED;
+    kf7_correct(r.kf, z);
+}
+
+struct OcShared {
+    int wsum[32];
+    int cnt[8];
+    double red[OC_T / WAVE];
+};
+
+// Block max of v (wave reductions, then wave 0).
+__device__ __forceinline__ double block_max(double v, OcShared &sh) {
+    v = wave_reduce(RED_MAX, v);
+    if (lane_id() == 0) sh.red[threadIdx.x / WAVE] = v;
+    block_sync();
+    double m = -INFINITY;
+    for (int w = 0; w < (int)blockDim.x / WAVE; ++w) m = fmax(m, sh.red[w]);
+    block_sync();
+    return m;
+}
+
+// association.py:20-28 on an na x nb matrix held by `cost_of` (dummy entries 0): wave 0 solves,
+// x[r] = column or -1 written to `rx`.
+template <typename Cost>
+__device__ __forceinline__ void padded_lap(int na, int nb, Cost cost_of, int *rx,
+                                           unsigned char *lds, unsigned char *gws, int *err) {
+    const int n = na > nb ? na : nb;
+    if (threadIdx.x < WAVE && n > 0) {
+        unsigned char *base = n <= OC_LDS_LAP_N ? lds : gws;
+        DenseLapWs w;
+        w.v = reinterpret_cast<double *>(base);
+        w.d = w.v + n;
+        w.x = reinterpret_cast<int *>(w.d + n);
+        w.y = w.x + n;
+        w.free_rows = w.y + n;
+        w.cols = w.free_rows + n;
+        w.pred = w.cols + n;
+        w.aux = w.pred + n;
+        auto c = [&](int r, int k) { return r < na && k < nb ? cost_of(r, k) : 0.0; };
+        if (lap_dense_wave(n, c, w) && lane_id() == 0) atomicOr(err, ERR_SOLVER);
+        for (int r = lane_id(); r < na; r += WAVE) rx[r] = w.x[r] < nb ? w.x[r] : -1;
+    }
+    block_sync();
+}
+
+__global__ __launch_bounds__(OC_T) void k_ocsort(OcArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    __shared__ OcShared sh;
+    const int s = blockIdx.x, t = threadIdx.x, nt = blockDim.x;
+    OcCounters *c = a.cnt + s;
+    const long long tb = (long long)s * a.CAP, db = (long long)s * a.MAXD;
+    const long long mb = (long long)s * (a.MAXD > 4 ? a.MAXD : 4) * a.CAP;
+    const long long ub = (long long)s * (a.MAXD + a.CAP);
+    unsigned char *gws = a.lap_ws + s * a.lap_ws_stride;
+    int nd = a.det_off[s + 1] - a.det_off[s];
+    if (nd > a.MAXD || nd < 0) {
+        if (t == 0) atomicOr(&c->err, ERR_DET_CAPACITY);
+        nd = nd < 0 ? 0 : a.MAXD;
+    }
+    const double *din = a.det_in + (long long)a.det_off[s] * 6;
+    const double img_w = a.img_wh ? (double)a.img_wh[2 * s] : 0.0;
+    const double img_h = a.img_wh ? (double)a.img_wh[2 * s + 1] : 0.0;
+    const int frame = c->frame + 1;
+    int n_trk = c->n_trk;
+    const int dt = a.delta_t;
+    int *list = a.list + tb;
+
+    // ---- A: predict (:250-264)
+    for (int i = t; i < n_trk; i += nt) {
+        OcTrack &r = a.rec[tb + list[i]];
+        if (r.kf.x[6] + r.kf.x[2] <= 0) r.kf.x[6] *= 0.0;
+        kf7_predict(r.kf);
+        r.age += 1;
+        if (r.tsu > 0) r.hit_streak = 0;
+        r.tsu += 1;
+        double b[4];
+        oc_x_to_bbox(r.kf.x, b);
+        a.nan_flag[tb + i] = (b[0] != b[0]) || (b[1] != b[1]) || (b[2] != b[2]) || (b[3] != b[3]);
+        a.cbox[tb + i] = Box{b[0], b[1], b[2], b[3]};
+    }
+    block_sync();
+    // ---- B: drop NaN trackers (order kept), free their slots; column inputs in tracker order
+    {
+        int n_free = c->n_free;
+        const int n_nan = block_compact(n_trk, sh.wsum, [&](int i) { return a.nan_flag[tb + i] != 0; },
+                                        [&](int i, int pos) { a.tmp[ub + pos] = list[i]; });
+        for (int k = t; k < n_nan; k += nt) a.free_list[tb + n_free + k] = a.tmp[ub + k];
+        n_free += n_nan;
+        block_sync();
+        const int n_keep = block_compact(n_trk, sh.wsum, [&](int i) { return a.nan_flag[tb + i] == 0; },
+                                         [&](int i, int pos) {
+                                             a.tmp[ub + pos] = list[i];
+                                             a.upd[tb + pos] = i;   // its old position
+                                         });
+        block_sync();
+        Box *bscratch = reinterpret_cast<Box *>(a.mat2 + mb);
+        for (int j = t; j < n_keep; j += nt) {
+            const OcTrack &r = a.rec[tb + a.tmp[ub + j]];
+            bscratch[j] = a.cbox[tb + a.upd[tb + j]];
+            double ko[5];
+            k_prev_obs(r, dt, ko);
+            for (int k = 0; k < 5; ++k) {
+                a.ckobs[(tb + j) * 5 + k] = ko[k];
+                a.clast[(tb + j) * 5 + k] = r.last_obs[k];
+            }
+            const bool hv = (r.flags & OF_VELOCITY) != 0;
+            a.cvel[(tb + j) * 2] = hv ? r.vel[0] : 0.0;
+            a.cvel[(tb + j) * 2 + 1] = hv ? r.vel[1] : 0.0;
+        }
+        block_sync();
+        for (int j = t; j < n_keep; j += nt) {
+            list[j] = a.tmp[ub + j];
+            a.cbox[tb + j] = bscratch[j];
+            a.cmatched[tb + j] = 0;
+            a.nan_flag[tb + j] = 0;
+        }
+        n_trk = n_keep;
+        if (t == 0) c->n_free = n_free;
+        block_sync();
+    }
+    for (int j = t; j < n_trk; j += nt) a.upd[tb + j] = -1;
+    // ---- C: detection split (:241-247)
+    const int n_hi = block_compact(nd, sh.wsum, [&](int i) { return din[i * 6 + 4] > a.det_thresh; },
+                                   [&](int i, int pos) { a.hi_row[db + pos] = i; });
+    const int n_lo = block_compact(
+        nd, sh.wsum,
+        [&](int i) { const double cf = din[i * 6 + 4]; return cf > 0.1 && cf < a.det_thresh; },
+        [&](int i, int pos) { a.lo_row[db + pos] = i; });
+    block_sync();
+    auto hbox = [&](int i) { return box5(din + (long long)a.hi_row[db + i] * 6); };
+    double *mat = a.mat + mb, *mat2 = a.mat2 + mb;
+    int *udet = a.udet + ub, *utrk = a.utrk + ub;
+    int n_ud = 0, n_ut = 0;
+    bool giou_bad = false;
+
+    // ---- D / E: first round (association.py:111-201)
+    if (n_trk == 0) {
+        for (int i = t; i < n_hi; i += nt) udet[i] = i;
+        n_ud = n_hi;
+        n_ut = 0;
+        if (t == 0) { c->fast_path = 0; c->lap_calls = 0; }
+    } else {
+        if (t < 8) sh.cnt[t] = 0;
+        for (int i = t; i < n_hi; i += nt) a.rmatch[db + i] = 0;
+        block_sync();
+        const long long nm = (long long)n_hi * n_trk;
+        int local_over = 0;
+        for (long long q = t; q < nm; q += nt) {
+            const int i = (int)(q / n_trk), j = (int)(q % n_trk);
+            const double *dr = din + (long long)a.hi_row[db + i] * 6;
+            const double v = asso_of(a.asso, box5(dr), a.cbox[tb + j], img_w, img_h);
+            if (a.asso == 1 && v != v) giou_bad = true;
+            // speed_direction_batch (:8-17): k-obs centre -> detection centre
+            const double *ko = a.ckobs + (tb + j) * 5;
+            const double dx = (dr[0] + dr[2]) / 2.0 - (ko[0] + ko[2]) / 2.0;
+            const double dy = (dr[1] + dr[3]) / 2.0 - (ko[1] + ko[3]) / 2.0;
+            const double nrm = sqrt(dx * dx + dy * dy) + 1e-6;
+            const double X = dx / nrm, Y = dy / nrm;
+            const double vy = a.cvel[(tb + j) * 2], vx = a.cvel[(tb + j) * 2 + 1];
+            double cs = vx * X + vy * Y;
+            cs = np_min(np_max(cs, -1.0), 1.0);
+            const double ang = (M_PI / 2.0 - fabs(acos(cs))) / M_PI;
+            const double valid = ko[4] < 0 ? 0.0 : 1.0;
+            const double angle = ((valid * ang) * a.inertia) * dr[4];
+            mat[q] = v;
+            mat2[q] = -((v + angle) + 0.0);
+            if (v > a.thr) {   // per-row / per-column counts (the fast-path test, :156-159)
+                ++local_over;
+                atomicAdd(&a.rmatch[db + i], 1);
+                atomicAdd(&a.cmatched[tb + j], 1);
+            }
+        }
+        if (local_over) atomicAdd(&sh.cnt[0], local_over);
+        block_sync();
+        int bad = 0;
+        for (int i = t; i < n_hi; i += nt) bad |= ald(a.rmatch + db + i) > 1;
+        for (int j = t; j < n_trk; j += nt) bad |= ald(a.cmatched + tb + j) > 1;
+        if (bad) atomicOr(&sh.cnt[1], 1);
+        block_sync();
+        const bool fast = sh.cnt[1] == 0 && sh.cnt[0] > 0;
+        if (fast) {
+            for (int i = t; i < n_hi; i += nt) {
+                int col = -1;
+                if (ald(a.rmatch + db + i) == 1)
+                    for (int j = 0; j < n_trk; ++j)
+                        if (mat[(long long)i * n_trk + j] > a.thr) { col = j; break; }
+                a.rmatch[db + i] = col;
+            }
+            block_sync();
+        } else if (n_hi > 0) {
+            block_sync();
+            padded_lap(n_hi, n_trk, [&](int r, int k) { return mat2[(long long)r * n_trk + k]; },
+                       a.rmatch + db, lds, gws, &c->err);
+        }
+        if (t == 0) { c->fast_path = fast; c->lap_calls = (fast || n_hi == 0) ? 0 : 1; }
+        // matched columns; unmatched lists: scan order, then the filtered pairs in row order
+        for (int j = t; j < n_trk; j += nt) a.cmatched[tb + j] = 0;
+        block_sync();
+        for (int i = t; i < n_hi; i += nt) {
+            const int col = a.rmatch[db + i];
+            if (col >= 0) a.cmatched[tb + col] = 1;
+        }
+        block_sync();
+        n_ud = block_compact(n_hi, sh.wsum, [&](int i) { return a.rmatch[db + i] < 0; },
+                             [&](int i, int pos) { udet[pos] = i; });
+        n_ut = block_compact(n_trk, sh.wsum, [&](int j) { return a.cmatched[tb + j] == 0; },
+                             [&](int j, int pos) { utrk[pos] = j; });
+        auto filtered = [&](int i) {
+            const int col = a.rmatch[db + i];
+            return col >= 0 && mat[(long long)i * n_trk + col] < a.thr;
+        };
+        const int nf = block_compact(n_hi, sh.wsum, filtered, [&](int i, int pos) {
+            udet[n_ud + pos] = i;
+            utrk[n_ut + pos] = a.rmatch[db + i];
+        });
+        for (int i = t; i < n_hi; i += nt) {
+            const int col = a.rmatch[db + i];
+            if (col >= 0 && !filtered(i)) a.upd[tb + col] = a.hi_row[db + i];
+        }
+        n_ud += nf;
+        n_ut += nf;
+        block_sync();
+    }
+    if (giou_bad) atomicOr(&c->err, ERR_GIOU);
+
+    // ---- F: BYTE round (:289-313)
+    if (a.use_byte && n_lo > 0 && n_ut > 0) {
+        const long long nm = (long long)n_lo * n_ut;
+        double mx = -INFINITY;
+        for (long long q = t; q < nm; q += nt) {
+            const int p = (int)(q / n_ut), k = (int)(q % n_ut);
+            const double v = asso_of(a.asso, box5(din + (long long)a.lo_row[db + p] * 6),
+                                     a.cbox[tb + utrk[k]], img_w, img_h);
+            if (a.asso == 1 && v != v) atomicOr(&c->err, ERR_GIOU);
+            mat[q] = v;
+            mx = np_max(mx, v);
+        }
+        block_sync();
+        mx = block_max(mx, sh);
+        if (mx > a.thr) {
+            padded_lap(n_lo, n_ut, [&](int r, int k) { return -mat[(long long)r * n_ut + k]; },
+                       a.rmatch + db, lds, gws, &c->err);
+            for (int k = t; k < n_ut; k += nt) a.tmp[ub + k] = 0;   // taken flags
+            block_sync();
+            for (int p = t; p < n_lo; p += nt) {
+                const int k = a.rmatch[db + p];
+                if (k >= 0 && !(mat[(long long)p * n_ut + k] < a.thr)) {
+                    a.upd[tb + utrk[k]] = a.lo_row[db + p];
+                    a.tmp[ub + k] = 1;
+                }
+            }
+            block_sync();
+            // setdiff1d: the remaining tracker indices, sorted
+            for (int k = t; k < n_ut; k += nt) a.nan_flag[tb + utrk[k]] = a.tmp[ub + k] ? 0 : 1;
+            block_sync();
+            n_ut = block_compact(n_trk, sh.wsum, [&](int j) { return a.nan_flag[tb + j] == 1; },
+                                 [&](int j, int pos) { utrk[pos] = j; });
+            for (int j = t; j < n_trk; j += nt) a.nan_flag[tb + j] = 0;
+            if (t == 0) c->lap_calls += 1;
+            block_sync();
+        }
+    }
+    // ---- G: OCR round (:315-342)
+    if (n_ud > 0 && n_ut > 0) {
+        const long long nm = (long long)n_ud * n_ut;
+        double mx = -INFINITY;
+        for (long long q = t; q < nm; q += nt) {
+            const int p = (int)(q / n_ut), k = (int)(q % n_ut);
+            const Box lb = box5(a.clast + (tb + utrk[k]) * 5);
+            const double v = asso_of(a.asso, hbox(udet[p]), lb, img_w, img_h);
+            if (a.asso == 1 && v != v) atomicOr(&c->err, ERR_GIOU);
+            mat[q] = v;
+            mx = np_max(mx, v);
+        }
+        block_sync();
+        mx = block_max(mx, sh);
+        if (mx > a.thr) {
+            padded_lap(n_ud, n_ut, [&](int r, int k) { return -mat[(long long)r * n_ut + k]; },
+                       a.rmatch + db, lds, gws, &c->err);
+            // removed dets / trackers -> flags, then sorted set differences
+            for (int i = t; i < n_hi; i += nt) a.tmp[ub + i] = 0;
+            for (int j = t; j < n_trk; j += nt) a.nan_flag[tb + j] = 0;
+            block_sync();
+            for (int p = t; p < n_ud; p += nt) a.tmp[ub + udet[p]] = 1;        // in udet
+            for (int k = t; k < n_ut; k += nt) a.nan_flag[tb + utrk[k]] = 1;   // in utrk
+            block_sync();
+            for (int p = t; p < n_ud; p += nt) {
+                const int k = a.rmatch[db + p];
+                if (k >= 0 && !(mat[(long long)p * n_ut + k] < a.thr)) {
+                    a.upd[tb + utrk[k]] = a.hi_row[db + udet[p]];
+                    a.tmp[ub + udet[p]] = 0;
+                    a.nan_flag[tb + utrk[k]] = 0;
+                }
+            }
+            block_sync();
+            n_ud = block_compact(n_hi, sh.wsum, [&](int i) { return a.tmp[ub + i] == 1; },
+                                 [&](int i, int pos) { udet[pos] = i; });
+            n_ut = block_compact(n_trk, sh.wsum, [&](int j) { return a.nan_flag[tb + j] == 1; },
+                                 [&](int j, int pos) { utrk[pos] = j; });
+            for (int j = t; j < n_trk; j += nt) a.nan_flag[tb + j] = 0;
+            if (t == 0) c->lap_calls += 1;
+            block_sync();
+        }
+    }
+    // ---- H: tracker updates (matched: det row; the rest: None)
+    for (int j = t; j < n_trk; j += nt) {
+        OcTrack &r = a.rec[tb + list[j]];
+        const int row = a.upd[tb + j];
+        tracker_update(r, row >= 0 ? din + (long long)row * 6 : nullptr, row, dt);
+    }
+    block_sync();
+    // ---- I: births in unmatched-list order (:347-349)
+    int n_free = c->n_free;
+    int n_b = n_ud;
+    if (n_b > n_free) {
+        if (t == 0) atomicOr(&c->err, ERR_TRACK_CAPACITY);
+        n_b = n_free;
+    }
+    const long long next_id = c->next_id;
+    for (int b = t; b < n_b; b += nt) {
+        const int slot = a.free_list[tb + n_free - 1 - b];
+        const double *dr = din + (long long)a.hi_row[db + udet[b]] * 6;
+        OcTrack r;
+        double z[4];
+        oc_bbox_to_z(dr, z);
+        kf7_init(z, r.kf);
+        r.fz = r.kf;
+        for (int k = 0; k < 4; ++k) r.hist_z[k] = 0.0;
+        for (int k = 0; k < 5; ++k) r.last_obs[k] = -1.0;
+        r.vel[0] = r.vel[1] = 0.0;
+        r.conf = dr[4];
+        r.cls = dr[5];
+        r.id = next_id + b;
+        r.obs_n = 0;
+        for (int e = 0; e < OC_DT_MAX; ++e) r.obs_age[e] = -1;
+        r.det_ind = a.hi_row[db + udet[b]];
+        r.age = r.hits = r.hit_streak = r.tsu = 0;
+        r.flags = 0;
+        r.hist_since = 0;
+        a.rec[tb + slot] = r;
+        list[n_trk + b] = slot;
+    }
+    n_free -= n_b;
+    n_trk += n_b;
+    block_sync();
+    // ---- J: outputs in reversed tracker order, then drop trackers unseen > max_age (:350-379)
+    double *out = a.out + tb * 8;
+    const int n_out = block_compact(
+        n_trk, sh.wsum,
+        [&](int q) {
+            const OcTrack &r = a.rec[tb + list[n_trk - 1 - q]];
+            return r.tsu < 1 && (r.hit_streak >= a.min_hits || frame <= a.min_hits);
+        },
+        [&](int q, int pos) {
+            const OcTrack &r = a.rec[tb + list[n_trk - 1 - q]];
+            double b[4];
+            if (np_sum5(r.last_obs) < 0) oc_x_to_bbox(r.kf.x, b);
+            else for (int k = 0; k < 4; ++k) b[k] = r.last_obs[k];
+            double *o = out + (long long)pos * 8;
+            o[0] = b[0];
+            o[1] = b[1];
+            o[2] = b[2];
+            o[3] = b[3];
+            o[4] = (double)(r.id + 1);
+            o[5] = r.conf;
+            o[6] = r.cls;
+            o[7] = (double)r.det_ind;
+        });
+    const int n_dead = block_compact(n_trk, sh.wsum,
+                                     [&](int j) { return a.rec[tb + list[j]].tsu > a.max_age; },
+                                     [&](int j, int pos) { a.tmp[ub + pos] = list[j]; });
+    for (int k = t; k < n_dead; k += nt) a.free_list[tb + n_free + k] = a.tmp[ub + k];
+    block_sync();
+    const int n_live = block_compact(n_trk, sh.wsum,
+                                     [&](int j) { return a.rec[tb + list[j]].tsu <= a.max_age; },
+                                     [&](int j, int pos) { a.tmp[ub + pos] = list[j]; });
+    block_sync();
+    for (int j = t; j < n_live; j += nt) list[j] = a.tmp[ub + j];
+    if (t == 0) {
+        c->frame = frame;
+        c->n_trk = n_live;
+        c->n_free = n_free + n_dead;
+        c->n_dets = nd;
+        c->n_high = n_hi;
+        c->n_second = n_lo;
+        c->n_out = n_out;
+        c->n_births = n_b;
+        c->next_id = next_id + n_b;
+        if (a.out_counts) a.out_counts[s] = n_out;
+    }
+}
+
+__global__ void k_oc_reset(OcArgs a) {
+    const int s = blockIdx.x;
+    const long long tb = (long long)s * a.CAP;
+    // births pop from the end of the free list: store it descending so slots fill from 0
+    for (int i = threadIdx.x; i < a.CAP; i += blockDim.x) a.free_list[tb + i] = a.CAP - 1 - i;
+    if (threadIdx.x == 0) {
+        OcCounters z;
+        memset(&z, 0, sizeof(z));
+        z.n_free = a.CAP;
+        a.cnt[s] = z;
+    }
+}
+
+}  // namespace
+}  // namespace yta
+
+// ================================================================================== host engine
+using namespace yta;
+
+struct yta_ocsort {
+    int device = 0, S = 0, CAP = 0, MAXD = 0;
+    yta_ocsort_params prm{};
+    hipStream_t stream = nullptr;
+    std::vector<void *> allocs;
+    OcArgs a{};
+    double *h_dets = nullptr, *d_det_in = nullptr;
+    long long det_cap = 0;
+    int *h_off = nullptr, *d_off = nullptr, *h_wh = nullptr, *d_wh = nullptr;
+    OcCounters *h_cnt = nullptr;
+    size_t lds = 0;
+};
+
+namespace {
+
+template <typename T>
+int oc_dalloc(yta_ocsort *e, T **p, long long n) {
+    void *q = nullptr;
+    if (n <= 0) n = 1;
+    hipError_t err = hipMalloc(&q, sizeof(T) * (size_t)n);
+    if (err != hipSuccess) {
+        set_error("hipMalloc(%lld bytes) failed: %s", (long long)(sizeof(T) * n),
+                  hipGetErrorString(err));
+        return YTA_ERR_NOMEM;
+    }
+    e->allocs.push_back(q);
+    *p = static_cast<T *>(q);
+    return YTA_OK;
+}
+
+#define OCALLOC(ptr, n)                      \
+    do {                                     \
+        int _rc = oc_dalloc(e, &(ptr), (n)); \
+        if (_rc) return _rc;                 \
+    } while (0)
+
+int oc_alloc(yta_ocsort *e) {
+    const long long S = e->S, CAP = e->CAP, MAXD = e->MAXD;
+    OcArgs &a = e->a;
+    const yta_ocsort_params &p = e->prm;
+    a.S = e->S;
+    a.CAP = e->CAP;
+    a.MAXD = e->MAXD;
+    a.det_thresh = p.det_thresh;
+    a.thr = p.asso_threshold;
+    a.inertia = p.inertia;
+    a.max_age = p.max_age;
+    a.min_hits = p.min_hits;
+    a.delta_t = p.delta_t;
+    a.asso = p.asso_func;
+    a.use_byte = p.use_byte;
+    OCALLOC(a.rec, S * CAP);
+    OCALLOC(a.list, S * CAP);
+    OCALLOC(a.free_list, S * CAP);
+    OCALLOC(a.cnt, S);
+    OCALLOC(a.hi_row, S * MAXD);
+    OCALLOC(a.lo_row, S * MAXD);
+    OCALLOC(a.cbox, S * CAP);
+    OCALLOC(a.cvel, S * CAP * 2);
+    OCALLOC(a.ckobs, S * CAP * 5);
+    OCALLOC(a.clast, S * CAP * 5);
+    OCALLOC(a.nan_flag, S * CAP);
+    const long long mat = std::max<long long>(MAXD * CAP, 4 * CAP);   // (mat2 doubles as a Box
+    OCALLOC(a.mat, S * mat);                                            //  scratch of CAP boxes)
+    OCALLOC(a.mat2, S * mat);
+    OCALLOC(a.rmatch, S * MAXD);
+    OCALLOC(a.cmatched, S * CAP);
+    OCALLOC(a.udet, S * (MAXD + CAP));
+    OCALLOC(a.utrk, S * (MAXD + CAP));
+    OCALLOC(a.tmp, S * (MAXD + CAP));
+    OCALLOC(a.upd, S * CAP);
+    OCALLOC(a.out, S * CAP * 8);
+    const long long n = std::max(CAP, MAXD);
+    a.lap_ws_stride = n > OC_LDS_LAP_N ? ((dense_lap_ws_bytes(n) + 255) & ~255LL) : 256;
+    OCALLOC(a.lap_ws, S * a.lap_ws_stride);
+    e->lds = (size_t)dense_lap_ws_bytes(std::min<long long>(n, OC_LDS_LAP_N));
+    OCALLOC(e->d_off, S + 1);
+    OCALLOC(e->d_wh, 2 * S);
+    YTA_HIP(hipHostMalloc((void **)&e->h_off, sizeof(int) * (S + 1), hipHostMallocDefault));
+    YTA_HIP(hipHostMalloc((void **)&e->h_wh, sizeof(int) * 2 * S, hipHostMallocDefault));
+    YTA_HIP(hipHostMalloc((void **)&e->h_cnt, sizeof(OcCounters) * S, hipHostMallocDefault));
+    YTA_HIP(hipFuncSetAttribute((const void *)k_ocsort, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)dense_lap_ws_bytes(OC_LDS_LAP_N)));
+    return YTA_OK;
+}
+
+void oc_release(yta_ocsort *e) {
+    for (void *p : e->allocs) (void)hipFree(p);
+    e->allocs.clear();
+    if (e->h_off) (void)hipHostFree(e->h_off);
+    if (e->h_wh) (void)hipHostFree(e->h_wh);
+    if (e->h_cnt) (void)hipHostFree(e->h_cnt);
+    e->h_off = e->h_wh = nullptr;
+    e->h_cnt = nullptr;
+}
+
+int oc_launch(yta_ocsort *e, const double *d_dets, const int *d_off, const int *d_wh, double *out,
+              int *out_counts) {
+    OcArgs &a = e->a;
+    a.det_in = d_dets;
+    a.det_off = d_off;
+    a.img_wh = d_wh;
+    a.out = out;
+    a.out_counts = out_counts;
+    hipLaunchKernelGGL(k_ocsort, dim3(a.S), dim3(OC_T), e->lds, e->stream, a);
+    YTA_HIP(hipGetLastError());
+    return YTA_OK;
+}
+
+int oc_read_counters(yta_ocsort *e) {
+    YTA_HIP(hipMemcpyAsync(e->h_cnt, e->a.cnt, sizeof(OcCounters) * e->S, hipMemcpyDeviceToHost,
+                           e->stream));
+    YTA_HIP(hipStreamSynchronize(e->stream));
+    return YTA_OK;
+}
+
+int oc_check_errors(yta_ocsort *e) {
+    for (int s = 0; s < e->S; ++s) {
+        const int err = e->h_cnt[s].err;
+        if (err) {
+            set_error("stream %d: device error flags 0x%x (%s%s%s%s)", s, err,
+                      err & ERR_GIOU ? "giou enclosure not positive (iou.py:58 assert) " : "",
+                      err & ERR_SOLVER ? "assignment solver failure " : "",
+                      err & ERR_TRACK_CAPACITY ? "track capacity exceeded " : "",
+                      err & ERR_DET_CAPACITY ? "too many detections " : "");
+            return (err & (ERR_TRACK_CAPACITY | ERR_DET_CAPACITY)) ? YTA_ERR_CAPACITY
+                   : (err & ERR_GIOU)                              ? YTA_ERR_INVALID
+                                                                   : YTA_ERR_HIP;
+        }
+    }
+    return YTA_OK;
+}
+
+// Grow capacity (tracks per stream / detections per stream), keeping every stream's state.
+int oc_reserve(yta_ocsort *e, int cap, int maxd) {
+    if (cap <= e->CAP && maxd <= e->MAXD) return YTA_OK;
+    cap = std::max(cap, e->CAP);
+    maxd = std::max(maxd, e->MAXD);
+    YTA_HIP(hipStreamSynchronize(e->stream));
+    yta_ocsort *n = new (std::nothrow) yta_ocsort();
+    YTA_CHECK(n, YTA_ERR_NOMEM, "out of host memory");
+    n->device = e->device;
+    n->S = e->S;
+    n->CAP = cap;
+    n->MAXD = maxd;
+    n->prm = e->prm;
+    n->stream = e->stream;
+    int rc = oc_alloc(n);
+    const size_t S = e->S, oc = e->CAP, nc = cap;
+    auto copy2d = [&](void *dst, size_t dp, const void *src, size_t sp, size_t w) -> int {
+        YTA_HIP(hipMemcpy2DAsync(dst, dp, src, sp, w, S, hipMemcpyDeviceToDevice, e->stream));
+        return YTA_OK;
+    };
+    if (!rc) rc = copy2d(n->a.rec, nc * sizeof(OcTrack), e->a.rec, oc * sizeof(OcTrack),
+                         oc * sizeof(OcTrack));
+    if (!rc) rc = copy2d(n->a.list, nc * 4, e->a.list, oc * 4, oc * 4);
+    if (!rc) {
+        // free slots: the old free list, then the new slots [oc, nc) (popped from the end:
+        // written so the lowest new slot is used first after the old ones)
+        std::vector<int> fl(nc * S);
+        std::vector<int> old(oc * S);
+        std::vector<OcCounters> cnt(S);
+        hipError_t he = hipMemcpyAsync(old.data(), e->a.free_list, sizeof(int) * oc * S,
+                                       hipMemcpyDeviceToHost, e->stream);
+        if (he == hipSuccess)
+            he = hipMemcpyAsync(cnt.data(), e->a.cnt, sizeof(OcCounters) * S,
+                                hipMemcpyDeviceToHost, e->stream);
+        if (he == hipSuccess) he = hipStreamSynchronize(e->stream);
+        if (he != hipSuccess) {
+            set_error("reserve: %s", hipGetErrorString(he));
+            rc = YTA_ERR_HIP;
+        } else {
+            for (size_t s = 0; s < S; ++s) {
+                int k = 0;
+                for (int q = (int)nc - 1; q >= (int)oc; --q) fl[s * nc + k++] = q;
+                for (int q = 0; q < cnt[s].n_free; ++q) fl[s * nc + k++] = old[s * oc + q];
+                cnt[s].n_free = k;
+            }
+            he = hipMemcpy(n->a.free_list, fl.data(), sizeof(int) * nc * S, hipMemcpyHostToDevice);
+            if (he == hipSuccess)
+                he = hipMemcpy(n->a.cnt, cnt.data(), sizeof(OcCounters) * S,
+                               hipMemcpyHostToDevice);
+            if (he != hipSuccess) {
+                set_error("reserve: %s", hipGetErrorString(he));
+                rc = YTA_ERR_HIP;
+            }
+        }
+    }
+    if (rc) {
+        n->stream = nullptr;
+        oc_release(n);
+        delete n;
+        return rc;
+    }
+    memcpy(n->h_cnt, e->h_cnt, sizeof(OcCounters) * S);
+    oc_release(e);
+    e->CAP = n->CAP;
+    e->MAXD = n->MAXD;
+    e->allocs.swap(n->allocs);
+    e->a = n->a;
+    e->lds = n->lds;
+    e->h_off = n->h_off;
+    e->h_wh = n->h_wh;
+    e->h_cnt = n->h_cnt;
+    e->d_off = n->d_off;
+    e->d_wh = n->d_wh;
+    n->h_off = n->h_wh = nullptr;
+    n->h_cnt = nullptr;
+    n->stream = nullptr;
+    delete n;
+    return YTA_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int yta_ocsort_create(int device, int n_streams, int track_capacity, int max_dets,
+                      const yta_ocsort_params *params, yta_ocsort **engine) {
+    YTA_CHECK(engine && params, YTA_ERR_INVALID, "null engine/params");
+    YTA_CHECK(n_streams > 0 && track_capacity > 0 && max_dets > 0, YTA_ERR_INVALID,
+              "n_streams, track_capacity and max_dets must be positive");
+    YTA_CHECK(params->delta_t >= 1 && params->delta_t <= OC_DT_MAX, YTA_ERR_INVALID,
+              "delta_t must be in [1, %d]", OC_DT_MAX);
+    YTA_CHECK(params->asso_func >= 0 && params->asso_func <= 4, YTA_ERR_INVALID,
+              "asso_func must be 0..4 (iou, giou, diou, ciou, centroid)");
+    YTA_CHECK(!(params->use_byte && params->asso_func == 4), YTA_ERR_INVALID,
+              "use_byte with centroid: the reference calls centroid_batch without w, h "
+              "(ocsort.py:292) and raises");
+    *engine = nullptr;
+    int rc = select_device(device);
+    if (rc) return rc;
+    yta_ocsort *e = new (std::nothrow) yta_ocsort();
+    YTA_CHECK(e, YTA_ERR_NOMEM, "out of host memory");
+    e->device = device;
+    e->S = n_streams;
+    e->CAP = track_capacity;
+    e->MAXD = max_dets;
+    e->prm = *params;
+    hipError_t he = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
+    if (he != hipSuccess) {
+        set_error("hipStreamCreate: %s", hipGetErrorString(he));
+        delete e;
+        return YTA_ERR_HIP;
+    }
+    rc = oc_alloc(e);
+    if (!rc) rc = yta_ocsort_reset(e);
+    if (rc) {
+        yta_ocsort_destroy(e);
+        return rc;
+    }
+    *engine = e;
+    return YTA_OK;
+}
+
+int yta_ocsort_destroy(yta_ocsort *e) {
+    if (!e) return YTA_OK;
+    (void)hipSetDevice(e->device);
+    if (e->stream) (void)hipStreamSynchronize(e->stream);
+    oc_release(e);
+    if (e->h_dets) (void)hipHostFree(e->h_dets);
+    if (e->d_det_in) (void)hipFree(e->d_det_in);
+    if (e->stream) (void)hipStreamDestroy(e->stream);
+    delete e;
+    return YTA_OK;
+}
+
+int yta_ocsort_reset(yta_ocsort *e) {
+    YTA_CHECK(e, YTA_ERR_INVALID, "null engine");
+    YTA_HIP(hipSetDevice(e->device));
+    hipLaunchKernelGGL(k_oc_reset, dim3(e->S), dim3(256), 0, e->stream, e->a);
+    YTA_HIP(hipGetLastError());
+    YTA_HIP(hipStreamSynchronize(e->stream));
+    memset(e->h_cnt, 0, sizeof(OcCounters) * e->S);
+    return YTA_OK;
+}
+
+int yta_ocsort_capacity(yta_ocsort *e, int *track_capacity, int *max_dets) {
+    YTA_CHECK(e && track_capacity && max_dets, YTA_ERR_INVALID, "null argument");
+    *track_capacity = e->CAP;
+    *max_dets = e->MAXD;
+    return YTA_OK;
+}
+
+int yta_ocsort_update(yta_ocsort *e, const double *dets, const int *det_offsets,
+                      const int *img_wh, long long *next_id, double *out, int out_capacity,
+                      int *out_offsets) {
+    YTA_CHECK(e && det_offsets && out_offsets, YTA_ERR_INVALID, "null argument");
+    YTA_HIP(hipSetDevice(e->device));
+    const int S = e->S;
+    YTA_CHECK(det_offsets[0] == 0, YTA_ERR_INVALID, "det_offsets[0] must be 0");
+    YTA_CHECK(img_wh || e->prm.asso_func != 4, YTA_ERR_INVALID, "centroid needs img_wh");
+    int need_d = e->MAXD, need_c = e->CAP;
+    for (int s = 0; s < S; ++s) {
+        const int m = det_offsets[s + 1] - det_offsets[s];
+        YTA_CHECK(m >= 0, YTA_ERR_INVALID, "det_offsets must be non-decreasing");
+        need_d = std::max(need_d, m);
+        need_c = std::max(need_c, e->h_cnt[s].n_trk + m);
+    }
+    if (need_d > e->MAXD || need_c > e->CAP) {
+        const int rc = oc_reserve(e, need_c > e->CAP ? std::max(need_c, 2 * e->CAP) : e->CAP,
+                                  need_d > e->MAXD ? std::max(need_d, 2 * e->MAXD) : e->MAXD);
+        if (rc) return rc;
+    }
+    const long long total = det_offsets[S];
+    YTA_CHECK(total == 0 || dets, YTA_ERR_INVALID, "null dets");
+    if (total > e->det_cap) {
+        if (e->d_det_in) (void)hipFree(e->d_det_in);
+        if (e->h_dets) (void)hipHostFree(e->h_dets);
+        e->d_det_in = nullptr;
+        e->h_dets = nullptr;
+        e->det_cap = 0;
+        const long long cap = std::max<long long>(2 * total, 1024);
+        YTA_HIP(hipMalloc((void **)&e->d_det_in, sizeof(double) * 6 * cap));
+        YTA_HIP(hipHostMalloc((void **)&e->h_dets, sizeof(double) * 6 * cap, hipHostMallocDefault));
+        e->det_cap = cap;
+    }
+    if (total) {
+        memcpy(e->h_dets, dets, sizeof(double) * 6 * total);
+        YTA_HIP(hipMemcpyAsync(e->d_det_in, e->h_dets, sizeof(double) * 6 * total,
+                               hipMemcpyHostToDevice, e->stream));
+    }
+    memcpy(e->h_off, det_offsets, sizeof(int) * (S + 1));
+    YTA_HIP(hipMemcpyAsync(e->d_off, e->h_off, sizeof(int) * (S + 1), hipMemcpyHostToDevice,
+                           e->stream));
+    if (img_wh) {
+        memcpy(e->h_wh, img_wh, sizeof(int) * 2 * S);
+        YTA_HIP(hipMemcpyAsync(e->d_wh, e->h_wh, sizeof(int) * 2 * S, hipMemcpyHostToDevice,
+                               e->stream));
+    }
+    if (next_id) {
+        for (int s = 0; s < S; ++s) e->h_cnt[s].next_id = next_id[s];
+        YTA_HIP(hipMemcpy2DAsync(&e->a.cnt[0].next_id, sizeof(OcCounters), &e->h_cnt[0].next_id,
+                                 sizeof(OcCounters), sizeof(long long), S, hipMemcpyHostToDevice,
+                                 e->stream));
+    }
+    int rc = oc_launch(e, e->d_det_in, e->d_off, img_wh ? e->d_wh : nullptr, e->a.out, nullptr);
+    if (rc) return rc;
+    rc = oc_read_counters(e);
+    if (rc) return rc;
+    rc = oc_check_errors(e);
+    if (rc) return rc;
+    long long rows = 0;
+    out_offsets[0] = 0;
+    for (int s = 0; s < S; ++s) {
+        rows += e->h_cnt[s].n_out;
+        out_offsets[s + 1] = (int)rows;
+    }
+    YTA_CHECK(rows <= out_capacity, YTA_ERR_CAPACITY, "output needs %lld rows > capacity %d", rows,
+              out_capacity);
+    YTA_CHECK(rows == 0 || out, YTA_ERR_INVALID, "null out");
+    for (int s = 0; s < S; ++s) {
+        const int n = e->h_cnt[s].n_out;
+        if (n)
+            YTA_HIP(hipMemcpyAsync(out + (long long)out_offsets[s] * 8,
+                                   e->a.out + (long long)s * e->CAP * 8, sizeof(double) * 8 * n,
+                                   hipMemcpyDeviceToHost, e->stream));
+    }
+    YTA_HIP(hipStreamSynchronize(e->stream));
+    if (next_id)
+        for (int s = 0; s < S; ++s) next_id[s] = e->h_cnt[s].next_id;
+    return YTA_OK;
+}
+
+int yta_ocsort_update_device(yta_ocsort *e, const double *d_dets, const int *d_det_offsets,
+                             const int *d_img_wh, double *d_out, int *d_out_counts) {
+    YTA_CHECK(e && d_det_offsets && d_out, YTA_ERR_INVALID, "null argument");
+    YTA_CHECK(d_img_wh || e->prm.asso_func != 4, YTA_ERR_INVALID, "centroid needs img_wh");
+    return oc_launch(e, d_dets, d_det_offsets, d_img_wh, d_out, d_out_counts);
+}
+
+int yta_ocsort_sync(yta_ocsort *e) {
+    YTA_CHECK(e, YTA_ERR_INVALID, "null engine");
+    const int rc = oc_read_counters(e);
+    if (rc) return rc;
+    return oc_check_errors(e);
+}
+
+int yta_ocsort_get_state(yta_ocsort *e, int stream, int *n_tracks, long long *ints, double *x,
+                         double *P) {
+    YTA_CHECK(e && n_tracks && ints && x && P, YTA_ERR_INVALID, "null argument");
+    YTA_CHECK(stream >= 0 && stream < e->S, YTA_ERR_INVALID, "bad stream %d", stream);
+    YTA_HIP(hipSetDevice(e->device));
+    const int rc = oc_read_counters(e);
+    if (rc) return rc;
+    const OcCounters c = e->h_cnt[stream];
+    const long long tb = (long long)stream * e->CAP;
+    std::vector<int> lst(c.n_trk);
+    std::vector<OcTrack> rec(e->CAP);
+    if (c.n_trk)
+        YTA_HIP(hipMemcpy(lst.data(), e->a.list + tb, sizeof(int) * c.n_trk, hipMemcpyDeviceToHost));
+    YTA_HIP(hipMemcpy(rec.data(), e->a.rec + tb, sizeof(OcTrack) * e->CAP, hipMemcpyDeviceToHost));
+    for (int i = 0; i < c.n_trk; ++i) {
+        const OcTrack &r = rec[lst[i]];
+        long long *ii = ints + 7LL * i;
+        ii[0] = r.id;
+        ii[1] = r.age;
+        ii[2] = r.hits;
+        ii[3] = r.hit_streak;
+        ii[4] = r.tsu;
+        ii[5] = (r.flags & OF_OBSERVED) ? 1 : 0;
+        ii[6] = (r.flags & OF_SAVED) ? 1 : 0;
+        for (int k = 0; k < 7; ++k) x[7LL * i + k] = r.kf.x[k];
+        double *M = P + 49LL * i;
+        for (int k = 0; k < 49; ++k) M[k] = 0.0;
+        for (int g = 0; g < 3; ++g) {
+            const int a0 = g, b0 = g + 4;
+            M[a0 * 7 + a0] = r.kf.p[4 * g];
+            M[a0 * 7 + b0] = r.kf.p[4 * g + 1];
+            M[b0 * 7 + a0] = r.kf.p[4 * g + 2];
+            M[b0 * 7 + b0] = r.kf.p[4 * g + 3];
+        }
+        M[3 * 7 + 3] = r.kf.p[12];
+    }
+    *n_tracks = c.n_trk;
+    return YTA_OK;
+}
+
+// Last frame's counts summed over streams: dets, first-round dets, BYTE dets, live trackers,
+// output rows, births, LAP calls, fast-path frames (8 int64).
+int yta_ocsort_stats(yta_ocsort *e, long long *stats) {
+    YTA_CHECK(e && stats, YTA_ERR_INVALID, "null argument");
+    const int rc = oc_read_counters(e);
+    if (rc) return rc;
+    for (int k = 0; k < 8; ++k) stats[k] = 0;
+    for (int s = 0; s < e->S; ++s) {
+        const OcCounters &c = e->h_cnt[s];
+        const long long v[8] = {c.n_dets, c.n_high, c.n_second, c.n_trk,
+                                c.n_out, c.n_births, c.lap_calls, c.fast_path};
+        for (int k = 0; k < 8; ++k) stats[k] += v[k];
+    }
+    return YTA_OK;
+}
+
+int yta_ocsort_hip_stream(yta_ocsort *e, void **stream) {
+    YTA_CHECK(e && stream, YTA_ERR_INVALID, "null argument");
+    *stream = (void *)e->stream;
+    return YTA_OK;
+}
+
+// Kalman KAT: n tracks run `steps` steps of predict + update from z[step][track] (4 values; a
+// NaN first value = missed update, i.e. update(None)); track i starts from z0[i].  Final x (7)
+// and full P (49) per track.
+int yta_kf7_run(int device, int n, int steps, const double *z0, const double *z, double *x_out,
+                double *P_out);
+
+}  // extern "C"
+
+namespace {
+__global__ void k_kf7_run(int n, int steps, const double *z0, const double *z, double *xo,
+                          double *Po) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    Kf7 kf, fz;
+    kf7_init(z0 + 4LL * i, kf);
+    fz = kf;
+    double hz[4] = {0, 0, 0, 0};
+    bool observed = false, saved = false;
+    int since = 0;
+    for (int st = 0; st < steps; ++st) {
+        kf7_predict(kf);
+        const double *zz = z + (4LL * n) * st + 4LL * i;
+        if (zz[0] != zz[0]) {
+            if (observed) { fz = kf; saved = true; }
+            observed = false;
+            since += 1;
+            continue;
+        }
+        if (!observed && saved) {
+            kf = fz;
+            saved = false;
+            kf7_replay(kf, hz, zz, since + 1, hz);
+        } else {
+            for (int k = 0; k < 4; ++k) hz[k] = zz[k];
+        }
+        since = 0;
+        observed = true;
+        kf7_correct(kf, zz);
+    }
+    for (int k = 0; k < 7; ++k) xo[7LL * i + k] = kf.x[k];
+    double *M = Po + 49LL * i;
+    for (int k = 0; k < 49; ++k) M[k] = 0.0;
+    for (int g = 0; g < 3; ++g) {
+        M[g * 7 + g] = kf.p[4 * g];
+        M[g * 7 + g + 4] = kf.p[4 * g + 1];
+        M[(g + 4) * 7 + g] = kf.p[4 * g + 2];
+        M[(g + 4) * 7 + g + 4] = kf.p[4 * g + 3];
+    }
+    M[24] = kf.p[12];
+}
+}  // namespace
+
+extern "C" int yta_kf7_run(int device, int n, int steps, const double *z0, const double *z,
+                           double *x_out, double *P_out) {
+    YTA_CHECK(n >= 0 && steps >= 0, YTA_ERR_INVALID, "negative size");
+    if (n == 0) return YTA_OK;
+    YTA_CHECK(z0 && (steps == 0 || z) && x_out && P_out, YTA_ERR_INVALID, "null buffer");
+    int rc = select_device(device);
+    if (rc) return rc;
+    double *d_z0 = nullptr, *d_z = nullptr, *d_x = nullptr, *d_P = nullptr;
+    auto cleanup = [&]() {
+        if (d_z0) (void)hipFree(d_z0);
+        if (d_z) (void)hipFree(d_z);
+        if (d_x) (void)hipFree(d_x);
+        if (d_P) (void)hipFree(d_P);
+    };
+    hipError_t he = hipMalloc(&d_z0, sizeof(double) * 4 * n);
+    if (he == hipSuccess) he = hipMalloc(&d_z, sizeof(double) * 4 * n * (steps ? steps : 1));
+    if (he == hipSuccess) he = hipMalloc(&d_x, sizeof(double) * 7 * n);
+    if (he == hipSuccess) he = hipMalloc(&d_P, sizeof(double) * 49 * n);
+    if (he == hipSuccess) he = hipMemcpy(d_z0, z0, sizeof(double) * 4 * n, hipMemcpyHostToDevice);
+    if (he == hipSuccess && steps)
+        he = hipMemcpy(d_z, z, sizeof(double) * 4 * n * steps, hipMemcpyHostToDevice);
+    if (he == hipSuccess) {
+        hipLaunchKernelGGL(k_kf7_run, dim3((n + 63) / 64), dim3(64), 0, 0, n, steps, d_z0, d_z, d_x,
+                           d_P);
+        he = hipGetLastError();
+    }
+    if (he == hipSuccess) he = hipMemcpy(x_out, d_x, sizeof(double) * 7 * n, hipMemcpyDeviceToHost);
+    if (he == hipSuccess) he = hipMemcpy(P_out, d_P, sizeof(double) * 49 * n, hipMemcpyDeviceToHost);
+    cleanup();
+    YTA_CHECK(he == hipSuccess, YTA_ERR_HIP, "kf7 KAT: %s", hipGetErrorString(he));
+    return YTA_OK;
+}

@@ -35,7 +35,13 @@ def create_tracker(tracker_type, tracker_config, reid_weights, device, half, per
                        match_thresh=cfg.match_thresh, proximity_thresh=cfg.proximity_thresh,
                        appearance_thresh=cfg.appearance_thresh, cmc_method=cfg.cmc_method,
                        frame_rate=cfg.frame_rate, reid=reid)
-    if tracker_type in ("ocsort", "deepocsort", "hybridsort", "strongsort"):
+    if tracker_type == "ocsort":
+        from .trackers.ocsort import OCSort
+        return OCSort(per_class, det_thresh=cfg.det_thresh, max_age=cfg.max_age,
+                      min_hits=cfg.min_hits, asso_threshold=cfg.iou_thresh, delta_t=cfg.delta_t,
+                      asso_func=cfg.asso_func, inertia=cfg.inertia, use_byte=cfg.use_byte,
+                      device=device)
+    if tracker_type in ("deepocsort", "hybridsort", "strongsort"):
         raise NotImplementedError(
             f"{tracker_type}: not yet on the MI355X path in this build (ByteTrack is); see DESIGN.md")
     print("No such tracker")
