@@ -1,0 +1,172 @@
+#!/usr/bin/env python3
+"""Per-config throughput of the other trackers (BASELINE.json configs 2 and 3).
+
+    python tools/bench_tracker.py --tracker ocsort  [--n 256]  [--streams 1] [--steps 50]
+    python tools/bench_tracker.py --tracker botsort [--n 1024] [--dim 512] [--streams 1]
+
+A step = one update() frame of every stream (SURVEY.md §8(d) synthetic streams; OCSORT with
+ocsort.yaml parameters and no low-confidence detections, BoT-SORT with botsort.yaml parameters
+and D-dim float32 embeddings through the get_features convention), inputs staged in HBM, the
+engine's device-buffer entry point, K timed frames bracketed by device syncs.  The CPU baseline
+is the oracle restatement of the same tracker on one core over a bounded sample of the stream.
+bench.py (the driver's contract) measures the ByteTrack headline; this tool is for DESIGN.md.
+"""
+import argparse
+import ctypes
+import json
+import os
+import subprocess
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+OCSORT_YAML = dict(det_thresh=0.0, max_age=30, min_hits=1, asso_threshold=0.3, delta_t=3,
+                   asso_func="giou", inertia=0.2, use_byte=False)
+BOTSORT_YAML = dict(track_high_thresh=0.33824964456239337, track_low_thresh=0.1,
+                    new_track_thresh=0.21144301345190655, track_buffer=60,
+                    match_thresh=0.22734550911325851, proximity_thresh=0.5945380911899254,
+                    appearance_thresh=0.4818211117541298, frame_rate=30)
+
+
+def reid_rows(dets, embs, thr):
+    f = embs[dets[:, 4] > thr]
+    return (f / np.linalg.norm(f)).astype(np.float32) if len(f) else f
+
+
+def cpu_leg(code, timeout=900):
+    env = dict(os.environ, OMP_NUM_THREADS="1", OPENBLAS_NUM_THREADS="1", MKL_NUM_THREADS="1")
+    try:
+        r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
+                           timeout=timeout)
+        return json.loads(r.stdout.strip().splitlines()[-1])
+    except Exception as exc:
+        return {"error": str(exc)}
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--tracker", choices=["ocsort", "botsort"], required=True)
+    p.add_argument("--n", type=int, default=None)
+    p.add_argument("--dim", type=int, default=512)
+    p.add_argument("--streams", type=int, default=1)
+    p.add_argument("--steps", type=int, default=50)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--cpu-frames", type=int, default=None)
+    p.add_argument("--seed", type=int, default=2000)
+    args = p.parse_args()
+    import torch
+    from yolo_tracking_amd import _lib
+    from yolo_tracking_amd.synth import SyntheticStream, make_frames
+    S = args.streams
+    F = args.warmup + args.steps
+    oc = args.tracker == "ocsort"
+    N = args.n or (256 if oc else 1024)
+    D = 0 if oc else args.dim
+    kw_stream = dict(low_conf_frac=0.0) if oc else dict(emb_dim=D)
+    streams = [make_frames(N, F, args.seed + s, **kw_stream) for s in range(S)]
+    dets = np.stack([np.concatenate([streams[s][f][0] for s in range(S)]) for f in range(F)])
+    off = np.array([[sum(len(streams[q][f][0]) for q in range(s)) for s in range(S + 1)]
+                    for f in range(F)], dtype=np.int32)
+    d_dets = torch.from_numpy(dets).cuda()
+    d_off = torch.from_numpy(off).cuda()
+    row_bytes = dets.shape[1] * 6 * 8
+    if oc:
+        from yolo_tracking_amd.trackers.ocsort import OCSortEngine
+        eng = OCSortEngine(S, **OCSORT_YAML, track_capacity=2 * N, max_dets=N)
+        shape = SyntheticStream(N, args.seed, **kw_stream).img_shape
+        d_wh = torch.tensor([[shape[1], shape[0]]] * S, dtype=torch.int32).cuda()
+        cap, _ = eng.capacity()
+        d_out = torch.empty((S * cap, 8), dtype=torch.float64, device="cuda")
+        fn, sync = eng.lib.yta_ocsort_update_device, eng.lib.yta_ocsort_sync
+
+        def step(f):
+            _lib.check(fn(eng.handle, ctypes.c_void_p(d_dets.data_ptr() + f * row_bytes),
+                          ctypes.c_void_p(d_off.data_ptr() + f * (S + 1) * 4),
+                          ctypes.c_void_p(d_wh.data_ptr()), ctypes.c_void_p(d_out.data_ptr()),
+                          None))
+    else:
+        from yolo_tracking_amd.trackers.botsort import BoTSORTEngine
+        eng = BoTSORTEngine(S, feat_dim=D, **BOTSORT_YAML, track_capacity=2 * N, max_dets=N)
+        # ReID rows aligned with the detections (the high rows carry get_features' output)
+        feats = np.zeros((F, dets.shape[1], D), np.float32)
+        for f in range(F):
+            r0 = 0
+            for s in range(S):
+                d, e = streams[s][f]
+                hi = d[:, 4] > BOTSORT_YAML["track_high_thresh"]
+                blk = np.zeros((len(d), D), np.float32)
+                blk[hi] = reid_rows(d, e, BOTSORT_YAML["track_high_thresh"])
+                feats[f, r0:r0 + len(d)] = blk
+                r0 += len(d)
+        d_feat = torch.from_numpy(feats).cuda()
+        feat_bytes = dets.shape[1] * D * 4
+        cap, _ = eng.capacity()
+        d_out = torch.empty((S * cap, 8), dtype=torch.float64, device="cuda")
+        fn, sync = eng.lib.yta_botsort_update_device, eng.lib.yta_bytetrack_sync
+
+        def step(f):
+            _lib.check(fn(eng.handle, ctypes.c_void_p(d_dets.data_ptr() + f * row_bytes),
+                          ctypes.c_void_p(d_off.data_ptr() + f * (S + 1) * 4),
+                          ctypes.c_void_p(d_feat.data_ptr() + f * feat_bytes),
+                          ctypes.c_void_p(d_out.data_ptr()), None))
+    for f in range(args.warmup):
+        step(f)
+    _lib.check(sync(eng.handle))
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for f in range(args.warmup, F):
+        step(f)
+    _lib.check(sync(eng.handle))
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    value = S * args.steps / el
+    stats = eng.stats()
+    # CPU leg: the oracle on stream 0, 1 thread, bounded sample
+    cf = args.cpu_frames or (30 if oc else 6)
+    if oc:
+        code = ("import sys,time,json; sys.path.insert(0,%r)\n"
+                "from oracle.ocsort import OCSortOracle\n"
+                "from yolo_tracking_amd.synth import make_frames, SyntheticStream\n"
+                "fr=[d for d,_ in make_frames(%d,%d,%d,low_conf_frac=0.0)]\n"
+                "sh=SyntheticStream(%d,%d,low_conf_frac=0.0).img_shape\n"
+                "t=OCSortOracle(**%r); t.update(fr[0],sh)\n"
+                "t0=time.perf_counter()\n"
+                "for d in fr[1:]: t.update(d,sh)\n"
+                "print(json.dumps({'frames':len(fr)-1,'seconds':time.perf_counter()-t0}))\n"
+                % (REPO, N, cf + 1, args.seed, N, args.seed, OCSORT_YAML))
+    else:
+        code = ("import sys,time,json; sys.path.insert(0,%r)\n"
+                "import numpy as np\n"
+                "from oracle.botsort import BoTSORTOracle\n"
+                "from yolo_tracking_amd.synth import make_frames\n"
+                "fr=make_frames(%d,%d,%d,emb_dim=%d)\n"
+                "kw=%r\n"
+                "def rows(d,e):\n"
+                "    f=e[d[:,4]>kw['track_high_thresh']]; return f/np.linalg.norm(f)\n"
+                "t=BoTSORTOracle(**kw); t.update(fr[0][0],rows(*fr[0]))\n"
+                "t0=time.perf_counter()\n"
+                "for d,e in fr[1:]: t.update(d,rows(d,e))\n"
+                "print(json.dumps({'frames':len(fr)-1,'seconds':time.perf_counter()-t0}))\n"
+                % (REPO, N, cf + 1, args.seed, D, BOTSORT_YAML))
+    res = cpu_leg(code)
+    cpu = ({"value": res["frames"] / res["seconds"], "unit": "calls/s", "cores": 1, "kind": "port",
+            "sample": f"oracle {args.tracker} 1 stream {N}x{N}, frames 2..{cf + 1} of seed "
+                      f"{args.seed}, {res['seconds']:.1f} s, 1 thread"}
+           if "frames" in res else {"value": None, "sample": res.get("error")})
+    line = {"metric": f"{args.tracker} tracker.update() calls/sec @ {N} tracks x {N} dets",
+            "value": value, "unit": "calls/s", "n_gpus": 1, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": 1000 * el / args.steps,
+            "higher_is_better": True, "dtype": "f64", "data": "synthetic",
+            "config": {"workload": f"{args.tracker} {N}x{N}" + (f" D={D}" if D else "")
+                                   + f", {S} streams, inputs resident in HBM",
+                       "streams": S},
+            "cpu_baseline": cpu, "frame_counts": stats}
+    print(json.dumps(line))
+
+
+if __name__ == "__main__":
+    main()

@@ -63,7 +63,14 @@ static __device__ int g_stamp_off;
     do {                                                                       \
         if (blockIdx.x == 0 && threadIdx.x == 0) g_stamps[(k)] = wall_clock64(); \
     } while (0)
+#define YTA_COUNT(k)                                                           \
+    do {                                                                       \
+        if (blockIdx.x == 0 && threadIdx.x == 0) g_stamps[(k)] += 1;            \
+    } while (0)
 #else
+#define YTA_COUNT(k) \
+    do {             \
+    } while (0)
 #define YTA_STAMP(k) \
     do {             \
     } while (0)

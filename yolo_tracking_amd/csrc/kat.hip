@@ -121,17 +121,9 @@ __global__ __launch_bounds__(64) void k_lap_padded(const double *cost, int nr, i
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int n = nr > nc ? nr : nc;
     unsigned char *base = n <= LAP_PADDED_LDS_N ? smem : gws;
-    DenseLapWs w;
-    w.v = reinterpret_cast<double *>(base);
-    w.d = w.v + n;
-    w.x = reinterpret_cast<int *>(w.d + n);
-    w.y = w.x + n;
-    w.free_rows = w.y + n;
-    w.cols = w.free_rows + n;
-    w.pred = w.cols + n;
-    w.aux = w.pred + n;
-    auto c = [&](int r, int k) { return r < nr && k < nc ? cost[(long long)r * nc + k] : 0.0; };
-    const int rc = lap_dense_wave(n, c, w);
+    const DenseLapWs w = dense_lap_ws(base, n);
+    const LapMat M{cost, nr, nc, false};
+    const int rc = n <= LAP_PADDED_LDS_N ? lap_dense_wave<true>(n, M, w) : lap_dense_wave<false>(n, M, w);
     if (rc && lane_id() == 0) atomicOr(err, ERR_SOLVER);
     for (int r = lane_id(); r < nr; r += WAVE) X[r] = w.x[r] < nc ? w.x[r] : -1;
     for (int k = lane_id(); k < nc; k += WAVE) Y[k] = w.y[k] < nr ? w.y[k] : -1;

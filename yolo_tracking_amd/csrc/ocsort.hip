@@ -2,7 +2,8 @@
 //
 // Follows boxmot/trackers/ocsort/ocsort.py:188-379 with boxmot/utils/association.py:8-28,
 // :111-201 and the live paths of ocsort_kf.py (kf_ocsort.hpp).  One frame = one launch of
-// k_ocsort (one block per stream) whose phases keep the reference's list semantics:
+// three kernels (k_oc_pre: A-C, one block per stream; k_oc_cost: D over the whole chip;
+// k_oc_assoc: E-J, one block per stream) whose phases keep the reference's list semantics:
 //   A  predict every tracker (x[6] clamp, Kalman predict, age / hit_streak / time_since_update,
 //      :168-181), predicted boxes; trackers whose box has a NaN are dropped (:254-264)
 //   B  per-column association inputs in tracker order: box, velocity (or 0), k_previous_obs
@@ -202,31 +203,29 @@ __device__ __forceinline__ double block_max(double v, OcShared &sh) {
     return m;
 }
 
-// association.py:20-28 on an na x nb matrix held by `cost_of` (dummy entries 0): wave 0 solves,
-// x[r] = column or -1 written to `rx`.
-template <typename Cost>
-__device__ __forceinline__ void padded_lap(int na, int nb, Cost cost_of, int *rx,
-                                           unsigned char *lds, unsigned char *gws, int *err) {
-    const int n = na > nb ? na : nb;
+// association.py:20-28 on the padded problem M: wave 0 solves, x[r] = column or -1 -> rx.
+// The solver is one dependent chain of row reads; the matrix was written by k_oc_cost on every
+// XCD, so the whole block first streams it once (coalesced) into this XCD's L2.
+__device__ __forceinline__ void padded_lap(const LapMat &M, int *rx, unsigned char *lds,
+                                           unsigned char *gws, int *err) {
+    const int n = M.na > M.nb ? M.na : M.nb;
+    {
+        const long long cnt = (long long)M.na * M.nb;
+        double acc = 0.0;
+        for (long long q = threadIdx.x; q < cnt; q += blockDim.x) acc += M.m[q];
+        if (acc == 1.2345e300) rx[0] = -7;   // keeps the loads; never true for cost matrices
+        block_sync();
+    }
     if (threadIdx.x < WAVE && n > 0) {
-        unsigned char *base = n <= OC_LDS_LAP_N ? lds : gws;
-        DenseLapWs w;
-        w.v = reinterpret_cast<double *>(base);
-        w.d = w.v + n;
-        w.x = reinterpret_cast<int *>(w.d + n);
-        w.y = w.x + n;
-        w.free_rows = w.y + n;
-        w.cols = w.free_rows + n;
-        w.pred = w.cols + n;
-        w.aux = w.pred + n;
-        auto c = [&](int r, int k) { return r < na && k < nb ? cost_of(r, k) : 0.0; };
-        if (lap_dense_wave(n, c, w) && lane_id() == 0) atomicOr(err, ERR_SOLVER);
-        for (int r = lane_id(); r < na; r += WAVE) rx[r] = w.x[r] < nb ? w.x[r] : -1;
+        const DenseLapWs w = dense_lap_ws(n <= OC_LDS_LAP_N ? lds : gws, n);
+        const int rc = n <= OC_LDS_LAP_N ? lap_dense_wave<true>(n, M, w) : lap_dense_wave<false>(n, M, w);
+        if (rc && lane_id() == 0) atomicOr(err, ERR_SOLVER);
+        for (int r = lane_id(); r < M.na; r += WAVE) rx[r] = w.x[r] < M.nb ? w.x[r] : -1;
     }
     block_sync();
 }
 
-__global__ __launch_bounds__(OC_T) void k_ocsort(OcArgs a) {
+__global__ __launch_bounds__(OC_T) void k_oc_pre(OcArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     __shared__ OcShared sh;
     const int s = blockIdx.x, t = threadIdx.x, nt = blockDim.x;
@@ -247,6 +246,8 @@ __global__ __launch_bounds__(OC_T) void k_ocsort(OcArgs a) {
     int n_trk = c->n_trk;
     const int dt = a.delta_t;
     int *list = a.list + tb;
+    YTA_STAMP_BASE(0);
+    YTA_STAMP(0);
 
     // ---- A: predict (:250-264)
     for (int i = t; i < n_trk; i += nt) {
@@ -263,6 +264,7 @@ __global__ __launch_bounds__(OC_T) void k_ocsort(OcArgs a) {
     }
     block_sync();
     // ---- B: drop NaN trackers (order kept), free their slots; column inputs in tracker order
+    YTA_STAMP(1);
     {
         int n_free = c->n_free;
         const int n_nan = block_compact(n_trk, sh.wsum, [&](int i) { return a.nan_flag[tb + i] != 0; },
@@ -303,6 +305,7 @@ __global__ __launch_bounds__(OC_T) void k_ocsort(OcArgs a) {
     }
     for (int j = t; j < n_trk; j += nt) a.upd[tb + j] = -1;
     // ---- C: detection split (:241-247)
+    YTA_STAMP(2);
     const int n_hi = block_compact(nd, sh.wsum, [&](int i) { return din[i * 6 + 4] > a.det_thresh; },
                                    [&](int i, int pos) { a.hi_row[db + pos] = i; });
     const int n_lo = block_compact(
@@ -310,11 +313,90 @@ __global__ __launch_bounds__(OC_T) void k_ocsort(OcArgs a) {
         [&](int i) { const double cf = din[i * 6 + 4]; return cf > 0.1 && cf < a.det_thresh; },
         [&](int i, int pos) { a.lo_row[db + pos] = i; });
     block_sync();
+    for (int i = t; i < n_hi; i += nt) a.rmatch[db + i] = 0;
+    if (t == 0) {
+        c->n_trk = n_trk;          // NaN-culled
+        c->n_high = n_hi;
+        c->n_second = n_lo;
+    }
+    (void)img_w;
+    (void)img_h;
+    (void)frame;
+    (void)lds;
+    (void)gws;
+}
+
+// k_oc_cost: the first round's dense asso / cost matrices of every stream over the whole chip
+// (association.py:111-150; costs -(asso + angle), :155-170), with the per-row / per-column counts
+// of asso > thr that decide the fast path (:156-159).
+__global__ __launch_bounds__(OC_T) void k_oc_cost(OcArgs a) {
+    const int s = blockIdx.y;
+    OcCounters *c = a.cnt + s;
+    const int n_trk = c->n_trk, n_hi = c->n_high;
+    const long long nm = (long long)n_hi * n_trk;
+    const long long tb = (long long)s * a.CAP, db = (long long)s * a.MAXD;
+    const long long mb = (long long)s * (a.MAXD > 4 ? a.MAXD : 4) * a.CAP;
+    const double *din = a.det_in + (long long)a.det_off[s] * 6;
+    const double img_w = a.img_wh ? (double)a.img_wh[2 * s] : 0.0;
+    const double img_h = a.img_wh ? (double)a.img_wh[2 * s + 1] : 0.0;
+    double *mat = a.mat + mb, *mat2 = a.mat2 + mb;
+    bool giou_bad = false;
+    for (long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x; q < nm;
+         q += (long long)gridDim.x * blockDim.x) {
+        const int i = (int)(q / n_trk), j = (int)(q % n_trk);
+        const double *dr = din + (long long)a.hi_row[db + i] * 6;
+        const double v = asso_of(a.asso, box5(dr), a.cbox[tb + j], img_w, img_h);
+        if (a.asso == 1 && v != v) giou_bad = true;
+        // speed_direction_batch (:8-17): k-obs centre -> detection centre
+        const double *ko = a.ckobs + (tb + j) * 5;
+        const double dx = (dr[0] + dr[2]) / 2.0 - (ko[0] + ko[2]) / 2.0;
+        const double dy = (dr[1] + dr[3]) / 2.0 - (ko[1] + ko[3]) / 2.0;
+        const double nrm = sqrt(dx * dx + dy * dy) + 1e-6;
+        const double X = dx / nrm, Y = dy / nrm;
+        const double vy = a.cvel[(tb + j) * 2], vx = a.cvel[(tb + j) * 2 + 1];
+        double cs = vx * X + vy * Y;
+        cs = np_min(np_max(cs, -1.0), 1.0);
+        const double ang = (M_PI / 2.0 - fabs(acos(cs))) / M_PI;
+        const double valid = ko[4] < 0 ? 0.0 : 1.0;
+        const double angle = ((valid * ang) * a.inertia) * dr[4];
+        mat[q] = v;
+        mat2[q] = -((v + angle) + 0.0);
+        if (v > a.thr) {
+            atomicAdd(&a.rmatch[db + i], 1);
+            atomicAdd(&a.cmatched[tb + j], 1);
+        }
+    }
+    if (giou_bad) atomicOr(&c->err, ERR_GIOU);
+}
+
+__global__ __launch_bounds__(OC_T) void k_oc_assoc(OcArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    __shared__ OcShared sh;
+    const int s = blockIdx.x, t = threadIdx.x, nt = blockDim.x;
+    OcCounters *c = a.cnt + s;
+    const long long tb = (long long)s * a.CAP, db = (long long)s * a.MAXD;
+    const long long mb = (long long)s * (a.MAXD > 4 ? a.MAXD : 4) * a.CAP;
+    const long long ub = (long long)s * (a.MAXD + a.CAP);
+    unsigned char *gws = a.lap_ws + s * a.lap_ws_stride;
+    int nd = a.det_off[s + 1] - a.det_off[s];
+    if (nd > a.MAXD || nd < 0) {
+        if (t == 0) atomicOr(&c->err, ERR_DET_CAPACITY);
+        nd = nd < 0 ? 0 : a.MAXD;
+    }
+    const double *din = a.det_in + (long long)a.det_off[s] * 6;
+    const double img_w = a.img_wh ? (double)a.img_wh[2 * s] : 0.0;
+    const double img_h = a.img_wh ? (double)a.img_wh[2 * s + 1] : 0.0;
+    const int frame = c->frame + 1;
+    int n_trk = c->n_trk;
+    const int n_hi = c->n_high, n_lo = c->n_second;
+    const int dt = a.delta_t;
+    int *list = a.list + tb;
+    YTA_STAMP_BASE(40);
+    YTA_STAMP(0);
     auto hbox = [&](int i) { return box5(din + (long long)a.hi_row[db + i] * 6); };
     double *mat = a.mat + mb, *mat2 = a.mat2 + mb;
     int *udet = a.udet + ub, *utrk = a.utrk + ub;
     int n_ud = 0, n_ut = 0;
-    bool giou_bad = false;
 
     // ---- D / E: first round (association.py:111-201)
     if (n_trk == 0) {
@@ -324,42 +406,18 @@ __global__ __launch_bounds__(OC_T) void k_ocsort(OcArgs a) {
         if (t == 0) { c->fast_path = 0; c->lap_calls = 0; }
     } else {
         if (t < 8) sh.cnt[t] = 0;
-        for (int i = t; i < n_hi; i += nt) a.rmatch[db + i] = 0;
         block_sync();
-        const long long nm = (long long)n_hi * n_trk;
-        int local_over = 0;
-        for (long long q = t; q < nm; q += nt) {
-            const int i = (int)(q / n_trk), j = (int)(q % n_trk);
-            const double *dr = din + (long long)a.hi_row[db + i] * 6;
-            const double v = asso_of(a.asso, box5(dr), a.cbox[tb + j], img_w, img_h);
-            if (a.asso == 1 && v != v) giou_bad = true;
-            // speed_direction_batch (:8-17): k-obs centre -> detection centre
-            const double *ko = a.ckobs + (tb + j) * 5;
-            const double dx = (dr[0] + dr[2]) / 2.0 - (ko[0] + ko[2]) / 2.0;
-            const double dy = (dr[1] + dr[3]) / 2.0 - (ko[1] + ko[3]) / 2.0;
-            const double nrm = sqrt(dx * dx + dy * dy) + 1e-6;
-            const double X = dx / nrm, Y = dy / nrm;
-            const double vy = a.cvel[(tb + j) * 2], vx = a.cvel[(tb + j) * 2 + 1];
-            double cs = vx * X + vy * Y;
-            cs = np_min(np_max(cs, -1.0), 1.0);
-            const double ang = (M_PI / 2.0 - fabs(acos(cs))) / M_PI;
-            const double valid = ko[4] < 0 ? 0.0 : 1.0;
-            const double angle = ((valid * ang) * a.inertia) * dr[4];
-            mat[q] = v;
-            mat2[q] = -((v + angle) + 0.0);
-            if (v > a.thr) {   // per-row / per-column counts (the fast-path test, :156-159)
-                ++local_over;
-                atomicAdd(&a.rmatch[db + i], 1);
-                atomicAdd(&a.cmatched[tb + j], 1);
-            }
+        int over = 0, bad = 0;
+        for (int i = t; i < n_hi; i += nt) {
+            const int k = ald(a.rmatch + db + i);
+            over += k;
+            bad |= k > 1;
         }
-        if (local_over) atomicAdd(&sh.cnt[0], local_over);
-        block_sync();
-        int bad = 0;
-        for (int i = t; i < n_hi; i += nt) bad |= ald(a.rmatch + db + i) > 1;
         for (int j = t; j < n_trk; j += nt) bad |= ald(a.cmatched + tb + j) > 1;
+        if (over) atomicAdd(&sh.cnt[0], over);
         if (bad) atomicOr(&sh.cnt[1], 1);
         block_sync();
+        YTA_STAMP(3);
         const bool fast = sh.cnt[1] == 0 && sh.cnt[0] > 0;
         if (fast) {
             for (int i = t; i < n_hi; i += nt) {
@@ -372,9 +430,9 @@ __global__ __launch_bounds__(OC_T) void k_ocsort(OcArgs a) {
             block_sync();
         } else if (n_hi > 0) {
             block_sync();
-            padded_lap(n_hi, n_trk, [&](int r, int k) { return mat2[(long long)r * n_trk + k]; },
-                       a.rmatch + db, lds, gws, &c->err);
+            padded_lap(LapMat{mat2, n_hi, n_trk, false}, a.rmatch + db, lds, gws, &c->err);
         }
+        YTA_STAMP(4);
         if (t == 0) { c->fast_path = fast; c->lap_calls = (fast || n_hi == 0) ? 0 : 1; }
         // matched columns; unmatched lists: scan order, then the filtered pairs in row order
         for (int j = t; j < n_trk; j += nt) a.cmatched[tb + j] = 0;
@@ -404,9 +462,9 @@ __global__ __launch_bounds__(OC_T) void k_ocsort(OcArgs a) {
         n_ut += nf;
         block_sync();
     }
-    if (giou_bad) atomicOr(&c->err, ERR_GIOU);
 
     // ---- F: BYTE round (:289-313)
+    YTA_STAMP(5);
     if (a.use_byte && n_lo > 0 && n_ut > 0) {
         const long long nm = (long long)n_lo * n_ut;
         double mx = -INFINITY;
@@ -421,8 +479,7 @@ __global__ __launch_bounds__(OC_T) void k_ocsort(OcArgs a) {
         block_sync();
         mx = block_max(mx, sh);
         if (mx > a.thr) {
-            padded_lap(n_lo, n_ut, [&](int r, int k) { return -mat[(long long)r * n_ut + k]; },
-                       a.rmatch + db, lds, gws, &c->err);
+            padded_lap(LapMat{mat, n_lo, n_ut, true}, a.rmatch + db, lds, gws, &c->err);
             for (int k = t; k < n_ut; k += nt) a.tmp[ub + k] = 0;   // taken flags
             block_sync();
             for (int p = t; p < n_lo; p += nt) {
@@ -444,6 +501,7 @@ __global__ __launch_bounds__(OC_T) void k_ocsort(OcArgs a) {
         }
     }
     // ---- G: OCR round (:315-342)
+    YTA_STAMP(6);
     if (n_ud > 0 && n_ut > 0) {
         const long long nm = (long long)n_ud * n_ut;
         double mx = -INFINITY;
@@ -458,8 +516,7 @@ __global__ __launch_bounds__(OC_T) void k_ocsort(OcArgs a) {
         block_sync();
         mx = block_max(mx, sh);
         if (mx > a.thr) {
-            padded_lap(n_ud, n_ut, [&](int r, int k) { return -mat[(long long)r * n_ut + k]; },
-                       a.rmatch + db, lds, gws, &c->err);
+            padded_lap(LapMat{mat, n_ud, n_ut, true}, a.rmatch + db, lds, gws, &c->err);
             // removed dets / trackers -> flags, then sorted set differences
             for (int i = t; i < n_hi; i += nt) a.tmp[ub + i] = 0;
             for (int j = t; j < n_trk; j += nt) a.nan_flag[tb + j] = 0;
@@ -486,6 +543,7 @@ __global__ __launch_bounds__(OC_T) void k_ocsort(OcArgs a) {
         }
     }
     // ---- H: tracker updates (matched: det row; the rest: None)
+    YTA_STAMP(7);
     for (int j = t; j < n_trk; j += nt) {
         OcTrack &r = a.rec[tb + list[j]];
         const int row = a.upd[tb + j];
@@ -493,6 +551,7 @@ __global__ __launch_bounds__(OC_T) void k_ocsort(OcArgs a) {
     }
     block_sync();
     // ---- I: births in unmatched-list order (:347-349)
+    YTA_STAMP(8);
     int n_free = c->n_free;
     int n_b = n_ud;
     if (n_b > n_free) {
@@ -527,6 +586,7 @@ __global__ __launch_bounds__(OC_T) void k_ocsort(OcArgs a) {
     n_trk += n_b;
     block_sync();
     // ---- J: outputs in reversed tracker order, then drop trackers unseen > max_age (:350-379)
+    YTA_STAMP(9);
     double *out = a.out + tb * 8;
     const int n_out = block_compact(
         n_trk, sh.wsum,
@@ -559,6 +619,7 @@ __global__ __launch_bounds__(OC_T) void k_ocsort(OcArgs a) {
                                      [&](int j, int pos) { a.tmp[ub + pos] = list[j]; });
     block_sync();
     for (int j = t; j < n_live; j += nt) list[j] = a.tmp[ub + j];
+    YTA_STAMP(10);
     if (t == 0) {
         c->frame = frame;
         c->n_trk = n_live;
@@ -673,7 +734,7 @@ int oc_alloc(yta_ocsort *e) {
     YTA_HIP(hipHostMalloc((void **)&e->h_off, sizeof(int) * (S + 1), hipHostMallocDefault));
     YTA_HIP(hipHostMalloc((void **)&e->h_wh, sizeof(int) * 2 * S, hipHostMallocDefault));
     YTA_HIP(hipHostMalloc((void **)&e->h_cnt, sizeof(OcCounters) * S, hipHostMallocDefault));
-    YTA_HIP(hipFuncSetAttribute((const void *)k_ocsort, hipFuncAttributeMaxDynamicSharedMemorySize,
+    YTA_HIP(hipFuncSetAttribute((const void *)k_oc_assoc, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)dense_lap_ws_bytes(OC_LDS_LAP_N)));
     return YTA_OK;
 }
@@ -696,7 +757,14 @@ int oc_launch(yta_ocsort *e, const double *d_dets, const int *d_off, const int *
     a.img_wh = d_wh;
     a.out = out;
     a.out_counts = out_counts;
-    hipLaunchKernelGGL(k_ocsort, dim3(a.S), dim3(OC_T), e->lds, e->stream, a);
+    hipLaunchKernelGGL(k_oc_pre, dim3(a.S), dim3(OC_T), 0, e->stream, a);
+    YTA_HIP(hipGetLastError());
+    const long long per = ((long long)a.MAXD * a.CAP + OC_T - 1) / OC_T;
+    const long long cap = std::max<long long>(4, 4096 / a.S);
+    hipLaunchKernelGGL(k_oc_cost, dim3((unsigned)std::max<long long>(1, std::min(per, cap)), a.S),
+                       dim3(OC_T), 0, e->stream, a);
+    YTA_HIP(hipGetLastError());
+    hipLaunchKernelGGL(k_oc_assoc, dim3(a.S), dim3(OC_T), e->lds, e->stream, a);
     YTA_HIP(hipGetLastError());
     return YTA_OK;
 }
@@ -1031,6 +1099,13 @@ int yta_ocsort_hip_stream(yta_ocsort *e, void **stream) {
     *stream = (void *)e->stream;
     return YTA_OK;
 }
+
+#ifdef YTA_STAMPS
+int yta_ocsort_debug_stamps(unsigned long long *out) {
+    YTA_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 128));
+    return YTA_OK;
+}
+#endif
 
 // Kalman KAT: n tracks run `steps` steps of predict + update from z[step][track] (4 values; a
 // NaN first value = missed update, i.e. update(None)); track i starts from z0[i].  Final x (7)
