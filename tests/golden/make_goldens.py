@@ -461,8 +461,109 @@ def make_g5():
     np.savez_compressed(os.path.join(HERE, "ocsort_synth.npz"), **out)
 
 
+# ------------------------------------------------------------------ G6: DeepOCSORT
+DEEPOCSORT_YAML = dict(det_thresh=0.0, max_age=30, min_hits=1, iou_threshold=0.3, delta_t=3,
+                       asso_func="giou", inertia=0.2, w_association_emb=0.75,
+                       alpha_fixed_emb=0.95, aw_param=0.5, embedding_off=False, cmc_off=False,
+                       aw_off=False)                                    # deepocsort.yaml
+DEEPOCSORT_CASES = [  # (name, n_objects, n_frames, seed, emb_dim, warp, stream kw, tracker kw)
+    ("dos_n64_d32", 64, 30, 61, 32, None, dict(drop_frac=0.05), {}),
+    ("dos_n128_d64_cmc", 128, 20, 62, 64, CMC_AFFINE, dict(drop_frac=0.05), {}),
+    ("dos_n128_noemb", 128, 20, 63, 0, None, dict(drop_frac=0.05), dict(embedding_off=True)),
+    ("dos_n96_d32_awoff", 96, 20, 64, 32, None, dict(drop_frac=0.05), dict(aw_off=True)),
+    ("dos_n64_dt5_iou", 64, 40, 65, 32, CMC_AFFINE, dict(drop_frac=0.15),
+     dict(delta_t=5, asso_func="iou", det_thresh=0.3, min_hits=3)),
+    ("dos_n256_d64", 256, 10, 66, 64, None, dict(drop_frac=0.05), {}),
+]
+
+
+def _deepocsort_lockstep(frames, img_shape, kw, warp, outs):
+    """As _oracle_lockstep, with every padded LAP cost perturbed by 1e-6 relative noise (covers a
+    float32 vs float64 embedding product, ~1e-7) and order-reversed."""
+    import oracle.deepocsort as dos
+    orig = dos.linear_assignment_padded
+    rng = np.random.default_rng(9)
+
+    def perturbed(cost):
+        c = np.asarray(cost, np.float64)
+        c = c * (1.0 + 1e-6 * rng.standard_normal(c.shape))
+        m = orig(c[::-1, ::-1])
+        if m.size == 0:
+            return m
+        m = np.stack([c.shape[0] - 1 - m[:, 0], c.shape[1] - 1 - m[:, 1]], axis=1)
+        return m[np.argsort(m[:, 0])]
+
+    exact = None
+    for lap_fn in (orig, perturbed):
+        dos.linear_assignment_padded = lap_fn
+        try:
+            t = dos.DeepOCSortOracle(**kw)
+            got = [np.asarray(t.update(d, img_shape, f, warp), dtype=np.float64).reshape(-1, 8)
+                   for d, f in frames]
+        finally:
+            dos.linear_assignment_padded = orig
+        assert canonical_equal(got, outs), lap_fn.__name__
+        if exact is None:
+            exact = all(np.array_equal(g, o) for g, o in zip(got, outs))
+    return exact
+
+
+def make_g6():
+    ns = refshim.load_deepocsort()
+    H = refshim.Harness
+    mod = ns.deep_ocsort
+    out = {}
+    for name, n, nf, seed, D, warp, skw, tkw in DEEPOCSORT_CASES:
+        skw = dict(skw)
+        skw.setdefault("low_conf_frac", 0.0)
+        frames = make_frames(n, nf, seed, emb_dim=max(D, 1), **skw)
+        from yolo_tracking_amd.synth import SyntheticStream
+        img_shape = SyntheticStream(n, seed, emb_dim=max(D, 1), **skw).img_shape
+        kw = dict(DEEPOCSORT_YAML, **tkw)
+        H.high_thresh = kw["det_thresh"]
+        H.warp = np.eye(2, 3) if warp is None else warp
+        t = mod.DeepOCSort(None, "cpu", False, per_class=False, **kw)
+        img = np.zeros((img_shape[0], img_shape[1], 3), np.uint8)
+        outs, feats = [], []
+        for dets, embs in frames:
+            H.dets, H.feats = dets, embs
+            m = dets[:, 4] > kw["det_thresh"]
+            f = embs[m]
+            feats.append((f / np.linalg.norm(f)) if (len(f) and D) else None)
+            outs.append(np.asarray(t.update(dets, img), dtype=np.float64).reshape(-1, 8))
+        exact = _deepocsort_lockstep([(d, f) for (d, _), f in zip(frames, feats)], img_shape, kw,
+                                     None if warp is None else warp, outs)
+        counts, rows = pack_outputs(outs)
+        out[f"{name}__gen"] = np.array([n, nf, seed, D], np.int64)
+        out[f"{name}__stream"] = np.array([skw["low_conf_frac"], skw.get("drop_frac", 0.0)])
+        out[f"{name}__in_sum"] = np.array([float(np.sum([d.sum() for d, _ in frames])),
+                                           float(np.sum([e.astype(np.float64).sum()
+                                                         for _, e in frames])) if D else 0.0])
+        out[f"{name}__img"] = np.array(img_shape[:2], np.int64)
+        out[f"{name}__warp"] = np.asarray(H.warp, dtype=np.float64)
+        out[f"{name}__params"] = np.array([kw["det_thresh"], kw["max_age"], kw["min_hits"],
+                                           kw["iou_threshold"], kw["delta_t"], kw["inertia"],
+                                           kw["w_association_emb"], kw["alpha_fixed_emb"],
+                                           kw["aw_param"], float(kw["embedding_off"]),
+                                           float(kw["cmc_off"]), float(kw["aw_off"])])
+        out[f"{name}__asso"] = np.array(kw["asso_func"])
+        out[f"{name}__exact"] = np.array(exact)
+        out[f"{name}__out_counts"] = counts
+        out[f"{name}__out"] = rows
+        trk = t.trackers
+        out[f"{name}__st_id"] = np.array([k.id for k in trk], np.int64)
+        out[f"{name}__st_x"] = np.array([k.kf.x.ravel() for k in trk]).reshape(-1, 8)
+        out[f"{name}__st_P"] = np.array([k.kf.P for k in trk]).reshape(-1, 8, 8)
+        if D:
+            out[f"{name}__st_emb"] = np.array([np.asarray(k.emb, np.float64) for k in trk]
+                                              ).reshape(-1, D)
+        print(f"G6 {name}: out_rows={len(rows)} live={len(trk)} oracle_exact={exact}")
+    out["cases"] = np.array([c[0] for c in DEEPOCSORT_CASES])
+    np.savez_compressed(os.path.join(HERE, "deepocsort_synth.npz"), **out)
+
+
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["g1", "g2", "g3", "g4", "g5"]
+    which = sys.argv[1:] or ["g1", "g2", "g3", "g4", "g5", "g6"]
     if "g3" in which:
         make_g3()
     if "g1" in which:
@@ -473,4 +574,6 @@ if __name__ == "__main__":
         make_g4()
     if "g5" in which:
         make_g5()
+    if "g6" in which:
+        make_g6()
     print(f"LAP calls {TIES['calls']}, tied {TIES['ties']}")

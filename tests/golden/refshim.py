@@ -146,6 +146,7 @@ def _install_botsort_shims():
             return np.array(Harness.warp, dtype=np.float64)
 
     sof.SparseOptFlow = SparseOptFlow
+    cmc.get_cmc_method = lambda name: SparseOptFlow       # DeepOCSort: get_cmc_method('sof')()
     sys.modules["boxmot.appearance"] = app
     sys.modules["boxmot.appearance.reid_multibackend"] = rmb
     sys.modules["boxmot.motion.cmc"] = cmc
@@ -161,6 +162,16 @@ def load_botsort():
     ns.bot_sort = importlib.import_module("boxmot.trackers.botsort.bot_sort")
     ns.basetrack = importlib.import_module("boxmot.trackers.botsort.basetrack")
     ns.botsort_kf = importlib.import_module("boxmot.motion.kalman_filters.botsort_kf")
+    return ns
+
+
+def load_deepocsort():
+    """Reference DeepOCSORT modules (fake ReID / CMC of step 5)."""
+    _install_shims()
+    _install_botsort_shims()
+    import importlib
+    ns = types.SimpleNamespace()
+    ns.deep_ocsort = importlib.import_module("boxmot.trackers.deepocsort.deep_ocsort")
     return ns
 
 

@@ -219,3 +219,56 @@ def test_ocsort_oracle_matches_reference(golden_dir, name):
         ox, gx = np.lexsort(x.T[::-1]), np.lexsort(g[f"{name}__st_x"].T[::-1])
         assert np.array_equal(x[ox], g[f"{name}__st_x"][gx])
         assert np.array_equal(P[ox], g[f"{name}__st_P"][gx])
+
+
+# ------------------------------------------------------------------ DeepOCSORT (G6)
+DEEPOCSORT_CASES = ["dos_n64_d32", "dos_n128_d64_cmc", "dos_n128_noemb", "dos_n96_d32_awoff",
+                    "dos_n64_dt5_iou", "dos_n256_d64"]
+
+
+def deepocsort_case(g, name):
+    """Inputs of a G6 case regenerated from its seed (checksum-pinned): (frames [(dets, feats)],
+    img_shape, DeepOCSortOracle kwargs, warp or None, D)."""
+    from yolo_tracking_amd.synth import make_frames
+    n, nf, seed, D = (int(x) for x in g[f"{name}__gen"])
+    low, drop = (float(x) for x in g[f"{name}__stream"])
+    raw = make_frames(n, nf, seed, emb_dim=max(D, 1), low_conf_frac=low, drop_frac=drop)
+    sums = g[f"{name}__in_sum"]
+    assert float(np.sum([d.sum() for d, _ in raw])) == sums[0]
+    if D:
+        assert float(np.sum([e.astype(np.float64).sum() for _, e in raw])) == sums[1]
+    p = g[f"{name}__params"]
+    kw = dict(det_thresh=float(p[0]), max_age=int(p[1]), min_hits=int(p[2]),
+              iou_threshold=float(p[3]), delta_t=int(p[4]), inertia=float(p[5]),
+              w_association_emb=float(p[6]), alpha_fixed_emb=float(p[7]), aw_param=float(p[8]),
+              embedding_off=bool(p[9]), cmc_off=bool(p[10]), aw_off=bool(p[11]),
+              asso_func=str(g[f"{name}__asso"]))
+    frames = []
+    for d, e in raw:
+        f = e[d[:, 4] > kw["det_thresh"]]
+        frames.append((d, f / np.linalg.norm(f) if (len(f) and D) else None))
+    warp = g[f"{name}__warp"]
+    warp = None if np.array_equal(warp, np.eye(2, 3)) else warp
+    return frames, tuple(int(v) for v in g[f"{name}__img"]), kw, warp, D
+
+
+@pytest.mark.parametrize("name", DEEPOCSORT_CASES)
+def test_deepocsort_oracle_matches_reference(golden_dir, name):
+    from oracle.deepocsort import DeepOCSortOracle
+    g = np.load(os.path.join(golden_dir, "deepocsort_synth.npz"))
+    frames, img_shape, kw, warp, D = deepocsort_case(g, name)
+    t = DeepOCSortOracle(**kw)
+    got = [np.asarray(t.update(d, img_shape, f, warp), dtype=np.float64).reshape(-1, 8)
+           for d, f in frames]
+    exp = golden_outputs(g, name)
+    assert canonical_equal(got, exp)
+    assert bool(g[f"{name}__exact"])
+    assert all(np.array_equal(a, b) for a, b in zip(got, exp))
+    assert np.array_equal([k.id for k in t.trackers], g[f"{name}__st_id"])
+    assert np.array_equal(np.array([k.kf.x.ravel() for k in t.trackers]).reshape(-1, 8),
+                          g[f"{name}__st_x"])
+    assert np.array_equal(np.array([k.kf.P for k in t.trackers]).reshape(-1, 8, 8),
+                          g[f"{name}__st_P"])
+    if D:
+        assert np.array_equal(np.array([np.asarray(k.emb, np.float64) for k in t.trackers]
+                                       ).reshape(-1, D), g[f"{name}__st_emb"])
