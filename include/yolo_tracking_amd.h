@@ -15,6 +15,9 @@
  *                            estimator (sof.py) stay outside: their outputs are inputs here
  *   yta_ocsort_*             boxmot/trackers/ocsort/ocsort.py:188-379  OCSort.__init__/update
  *                            (created by boxmot/tracker_zoo.py:42-55 create_tracker('ocsort', ...))
+ *   yta_deepocsort_*         boxmot/trackers/deepocsort/deep_ocsort.py:308-520  DeepOCSort.__init__/
+ *                            update (created by boxmot/tracker_zoo.py:83-99); ReID and CMC outside
+ *   yta_kf8_run              deep_ocsort.py:103-293 KalmanBoxTracker (new KF) + deepocsort_kf.py
  *   yta_lap_padded           boxmot/utils/association.py:20-28 linear_assignment -> lap.lapjv(cost,
  *                            extend_cost=True)
  *   yta_kf7_run              boxmot/motion/kalman_filters/ocsort_kf.py:339-526 predict / update incl.
@@ -240,6 +243,67 @@ int yta_ocsort_hip_stream(yta_ocsort *engine, void **stream);
  * unfreeze included; final x (n x 7) and full P (n x 49). */
 int yta_kf7_run(int device, int n, int steps, const double *z0, const double *z, double *x_out,
                 double *P_out);
+
+/* ---- DeepOCSORT engine: S independent streams --------------------------------------------
+ * DeepOCSort(det_thresh, max_age, min_hits, iou_threshold, delta_t, asso_func, inertia,
+ * w_association_emb, alpha_fixed_emb, aw_param, embedding_off, cmc_off, aw_off) per stream
+ * (boxmot/trackers/deepocsort/deep_ocsort.py:308-520; per_class is stored but unused by the
+ * reference's update).  The ReID forward pass (:387 get_features) and the CMC estimator (:391
+ * cmc.apply) stay outside: their outputs are inputs here.  KalmanBoxTracker.count starts at 1
+ * and ids are reported as stored (no +1). */
+typedef struct yta_deepocsort yta_deepocsort;
+typedef struct {
+    double det_thresh;          /* deepocsort.yaml: 0   (ctor default 0.3); must be < 1 */
+    int max_age;                /* 30                                                  */
+    int min_hits;               /* 1                    (ctor default 3)               */
+    double iou_threshold;       /* iou_thresh 0.3                                      */
+    int delta_t;                /* 3  (0..8)                                           */
+    int asso_func;              /* YTA_ASSO_*: giou     (ctor default iou)             */
+    double inertia;             /* 0.2                                                 */
+    double w_association_emb;   /* 0.5 (create_tracker does not pass the yaml's 0.75)  */
+    double alpha_fixed_emb;     /* 0.95                                                */
+    double aw_param;            /* 0.5                                                 */
+    int embedding_off;          /* 0                                                   */
+    int cmc_off;                /* 0                                                   */
+    int aw_off;                 /* 0                                                   */
+} yta_deepocsort_params;
+
+int yta_deepocsort_create(int device, int n_streams, int track_capacity, int max_dets,
+                          int feat_dim, const yta_deepocsort_params *params,
+                          yta_deepocsort **engine);
+int yta_deepocsort_destroy(yta_deepocsort *engine);
+int yta_deepocsort_reset(yta_deepocsort *engine);
+int yta_deepocsort_capacity(yta_deepocsort *engine, int *track_capacity, int *max_dets);
+/* Host-buffer update (synchronous).  dets / det_offsets / next_id / out / out_offsets as
+ * yta_ocsort_update; feats: feat_dim float32 per detection with conf > det_thresh, in input order
+ * (what get_features returns for dets[conf > det_thresh]); warps: S x 6 float64 row-major 2x3
+ * affines from the CMC estimator (NULL = identity for every stream); img_wh as yta_ocsort_update. */
+int yta_deepocsort_update(yta_deepocsort *engine, const double *dets, const int *det_offsets,
+                          const float *feats, const double *warps, const int *img_wh,
+                          long long *next_id, double *out, int out_capacity, int *out_offsets);
+/* Device-resident update (asynchronous).  d_feats holds feat_dim float32 for EVERY input row
+ * (rows at or below det_thresh are ignored); d_warps S x 6 or NULL; d_out S * track_capacity
+ * rows x 8. */
+int yta_deepocsort_update_device(yta_deepocsort *engine, const double *d_dets,
+                                 const int *d_det_offsets, const float *d_feats,
+                                 const double *d_warps, const int *d_img_wh, double *d_out,
+                                 int *d_out_counts);
+int yta_deepocsort_sync(yta_deepocsort *engine);
+/* Parity introspection, tracker-list order: ints 7 x int64 per tracker (id, age, hits,
+ * hit_streak, time_since_update, kf.observed, frozen), x (8 f64), P (64 f64), emb (feat_dim f64
+ * per tracker; may be NULL). */
+int yta_deepocsort_get_state(yta_deepocsort *engine, int stream, int *n_tracks, long long *ints,
+                             double *x, double *P, double *emb);
+/* Last frame's counts summed over streams: dets, kept dets, 0, live trackers, output rows,
+ * births, LAP calls, fast-path frames (8 int64). */
+int yta_deepocsort_stats(yta_deepocsort *engine, long long *stats);
+int yta_deepocsort_hip_stream(yta_deepocsort *engine, void **stream);
+/* DeepOCSORT Kalman KAT (deep_ocsort.py:103-136, 198-293 new-KF branch): n tracks initialised
+ * from boxes b0 (n x 4, x1 y1 x2 y2) run `steps` steps of [affine (warps: steps x n x 6, NULL =
+ * none)], predict + update(b[step] (n x 4); a NaN first value = update(None)) with the reference's
+ * clamps, Q(w, h), R(w, h), freeze / unfreeze replay; final x (n x 8) and full P (n x 64). */
+int yta_kf8_run(int device, int n, int steps, const double *b0, const double *b,
+                const double *warps, double *x_out, double *P_out);
 
 #ifdef __cplusplus
 }

@@ -54,6 +54,17 @@ class OcParams(ctypes.Structure):
                 ("inertia", ctypes.c_double), ("use_byte", ctypes.c_int)]
 
 
+class DocParams(ctypes.Structure):
+    """yta_deepocsort_params (include/yolo_tracking_amd.h)."""
+    _fields_ = [("det_thresh", ctypes.c_double), ("max_age", ctypes.c_int),
+                ("min_hits", ctypes.c_int), ("iou_threshold", ctypes.c_double),
+                ("delta_t", ctypes.c_int), ("asso_func", ctypes.c_int),
+                ("inertia", ctypes.c_double), ("w_association_emb", ctypes.c_double),
+                ("alpha_fixed_emb", ctypes.c_double), ("aw_param", ctypes.c_double),
+                ("embedding_off", ctypes.c_int), ("cmc_off", ctypes.c_int),
+                ("aw_off", ctypes.c_int)]
+
+
 ASSO_FUNCS = {"iou": 0, "giou": 1, "diou": 2, "ciou": 3, "centroid": 4}
 
 _lib = None
@@ -104,6 +115,17 @@ _SIGS = {
     "yta_ocsort_stats": ([_P, _P], _I),
     "yta_ocsort_hip_stream": ([_P, _P], _I),
     "yta_kf7_run": ([_I, _I, _I, _P, _P, _P, _P], _I),
+    "yta_deepocsort_create": ([_I, _I, _I, _I, _I, _P, _P], _I),
+    "yta_deepocsort_destroy": ([_P], _I),
+    "yta_deepocsort_reset": ([_P], _I),
+    "yta_deepocsort_capacity": ([_P, _P, _P], _I),
+    "yta_deepocsort_update": ([_P, _P, _P, _P, _P, _P, _P, _P, _I, _P], _I),
+    "yta_deepocsort_update_device": ([_P, _P, _P, _P, _P, _P, _P, _P], _I),
+    "yta_deepocsort_sync": ([_P], _I),
+    "yta_deepocsort_get_state": ([_P, _I, _P, _P, _P, _P, _P], _I),
+    "yta_deepocsort_stats": ([_P, _P], _I),
+    "yta_deepocsort_hip_stream": ([_P, _P], _I),
+    "yta_kf8_run": ([_I, _I, _I, _P, _P, _P, _P, _P], _I),
 }
 
 EXPORTED_SYMBOLS = tuple(_SIGS)
@@ -233,6 +255,19 @@ def kf7_run(z0, z, device=0):
     x = np.empty((n, 7))
     P = np.empty((n, 7, 7))
     check(load_library().yta_kf7_run(device, n, len(z), ptr(z0), ptr(z), ptr(x), ptr(P)))
+    return x, P
+
+
+def kf8_run(b0, b, warps=None, device=0):
+    """DeepOCSORT KalmanBoxTracker KAT (yta_kf8_run): b0 (n, 4) boxes, b (steps, n, 4) with NaN
+    rows = missed, warps (steps, n, 2, 3) or None."""
+    b0 = np.ascontiguousarray(b0, dtype=np.float64).reshape(-1, 4)
+    n = len(b0)
+    b = np.ascontiguousarray(b, dtype=np.float64).reshape(-1, n, 4)
+    w = None if warps is None else np.ascontiguousarray(warps, dtype=np.float64).reshape(-1, n, 6)
+    x = np.empty((n, 8))
+    P = np.empty((n, 8, 8))
+    check(load_library().yta_kf8_run(device, n, len(b), ptr(b0), ptr(b), ptr(w), ptr(x), ptr(P)))
     return x, P
 
 

@@ -41,8 +41,15 @@ def create_tracker(tracker_type, tracker_config, reid_weights, device, half, per
                       min_hits=cfg.min_hits, asso_threshold=cfg.iou_thresh, delta_t=cfg.delta_t,
                       asso_func=cfg.asso_func, inertia=cfg.inertia, use_byte=cfg.use_byte,
                       device=device)
-    if tracker_type in ("deepocsort", "hybridsort", "strongsort"):
+    if tracker_type == "deepocsort":
+        from .trackers.deepocsort import DeepOCSort
+        reid = reid_weights if hasattr(reid_weights, "get_features") else None
+        return DeepOCSort(reid_weights, device, half, per_class, det_thresh=cfg.det_thresh,
+                          max_age=cfg.max_age, min_hits=cfg.min_hits,
+                          iou_threshold=cfg.iou_thresh, delta_t=cfg.delta_t,
+                          asso_func=cfg.asso_func, inertia=cfg.inertia, reid=reid)
+    if tracker_type in ("hybridsort", "strongsort"):
         raise NotImplementedError(
-            f"{tracker_type}: not yet on the MI355X path in this build (ByteTrack is); see DESIGN.md")
+            f"{tracker_type}: not yet on the MI355X path in this build; see DESIGN.md")
     print("No such tracker")
     exit()
