@@ -81,10 +81,11 @@ def main():
         lines.append(f"| {k} | {v['calls']} | {v['avg_us']:.2f} | {v['total_pct']:.2f} | "
                      f"{'%.4g' % hb if hb else '-'} | {'%.0f' % v['hbm_gbs'] if hb else '-'} |")
     open(os.path.join(here, f"{args.tag}_summary.md"), "w").write("\n".join(lines) + "\n")
-    if "k_apply" in stats and "hbm_bytes_corrected" in stats["k_apply"]:
+    ka = next((k for k in stats if k.split("<")[0] == "k_apply"), None)
+    if ka and "hbm_bytes_corrected" in stats[ka]:
         json.dump({"tag": args.tag, "streams": args.streams, "n": args.n, "kernel": "k_apply",
-                   "hbm_bytes_per_launch": stats["k_apply"]["hbm_bytes_corrected"],
-                   "avg_us_rocprof": stats["k_apply"]["avg_us"]},
+                   "hbm_bytes_per_launch": stats[ka]["hbm_bytes_corrected"],
+                   "avg_us_rocprof": stats[ka]["avg_us"]},
                   open(os.path.join(here, "roofline_traffic.json"), "w"), indent=1)
     print("\n".join(lines))
 
