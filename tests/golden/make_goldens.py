@@ -562,8 +562,128 @@ def make_g6():
     np.savez_compressed(os.path.join(HERE, "deepocsort_synth.npz"), **out)
 
 
+# ------------------------------------------------------------------ G7: HybridSORT
+HYBRIDSORT_YAML = dict(det_thresh=0.0, max_age=30, min_hits=1, iou_threshold=0.3, delta_t=3,
+                       asso_func="giou", inertia=0.2)                    # hybridsort.yaml
+HYBRIDSORT_CASES = [  # (name, n_objects, n_frames, seed, emb_dim, stream kw, tracker kw)
+    ("hs_n64_d32", 64, 30, 71, 32, dict(drop_frac=0.05), {}),
+    ("hs_n128_d64", 128, 20, 72, 64, dict(drop_frac=0.05), {}),
+    ("hs_n96_dt5_iou", 96, 30, 73, 32, dict(drop_frac=0.15, low_conf_frac=0.1),
+     dict(delta_t=5, asso_func="iou", det_thresh=0.3, min_hits=3)),
+    ("hs_n64_cls3", 64, 25, 74, 32, dict(drop_frac=0.05, n_classes=3), {}),
+    ("hs_n96_diou_long", 96, 60, 75, 32, dict(drop_frac=0.3), dict(asso_func="diou", max_age=8)),
+    ("hs_n256_d64", 256, 10, 76, 64, dict(drop_frac=0.05), {}),
+]
+
+
+def _hybridsort_lockstep(frames, kw, outs):
+    """As _deepocsort_lockstep for HybridSORT (per-class calls included): the oracle must
+    reproduce the reference with every padded LAP cost perturbed by 1e-6 relative noise and
+    order-reversed; returns whether it matched exactly (birth order included)."""
+    import oracle.hybridsort as hs
+    orig = hs.linear_assignment_padded
+    rng = np.random.default_rng(11)
+
+    def perturbed(cost):
+        c = np.asarray(cost, np.float64)
+        c = c * (1.0 + 1e-6 * rng.standard_normal(c.shape))
+        m = orig(c[::-1, ::-1])
+        if m.size == 0:
+            return m
+        m = np.stack([c.shape[0] - 1 - m[:, 0], c.shape[1] - 1 - m[:, 1]], axis=1)
+        return m[np.argsort(m[:, 0])]
+
+    exact = None
+    for lap_fn in (orig, perturbed):
+        hs.linear_assignment_padded = lap_fn
+        try:
+            t = hs.HybridSortOracle(**kw)
+            got = [np.asarray(hs.per_class_update(t, d, e), dtype=np.float64).reshape(-1, 8)
+                   for d, e in frames]
+        finally:
+            hs.linear_assignment_padded = orig
+        assert canonical_equal(got, outs), lap_fn.__name__
+        if exact is None:
+            exact = all(np.array_equal(g, o) for g, o in zip(got, outs))
+    return exact
+
+
+EMB_MARGIN = {"min": np.inf}
+
+
+def make_g7():
+    ns = refshim.load_hybridsort()
+    H = refshim.Harness
+    mod = ns.hybridsort
+    asc = sys.modules["boxmot.trackers.hybridsort.association"]
+    orig_assoc = asc.associate_4_points_with_score_with_reid
+
+    def assoc_checked(*a, **k):
+        # every matched pair's embedding cost must sit > 1e-6 from the correction threshold
+        m, ud, ut = orig_assoc(*a, **k)
+        emb = k.get("emb_cost")
+        if emb is not None and emb.size:
+            d = np.abs(emb - k["longterm_reid_correction_thresh"])
+            EMB_MARGIN["min"] = min(EMB_MARGIN["min"], float(d.min()))
+            assert d.min() > 1e-6, "embedding cost within 1e-6 of the correction threshold"
+        return m, ud, ut
+
+    mod.associate_4_points_with_score_with_reid = assoc_checked
+    out = {}
+    import builtins
+    for name, n, nf, seed, D, skw, tkw in HYBRIDSORT_CASES:
+        skw = dict(skw)
+        skw.setdefault("low_conf_frac", 0.0)
+        frames = make_frames(n, nf, seed, emb_dim=D, **skw)
+        from yolo_tracking_amd.synth import SyntheticStream
+        img_shape = SyntheticStream(n, seed, emb_dim=D, **skw).img_shape
+        kw = dict(HYBRIDSORT_YAML, **tkw)
+        H.match_boxes = True
+        t = mod.HybridSORT(None, "cpu", False, det_thresh=kw["det_thresh"], max_age=kw["max_age"],
+                           min_hits=kw["min_hits"], iou_threshold=kw["iou_threshold"],
+                           delta_t=kw["delta_t"], asso_func=kw["asso_func"],
+                           inertia=kw["inertia"])
+        img = np.zeros((img_shape[0], img_shape[1], 3), np.uint8)
+        outs = []
+        pr = builtins.print
+        builtins.print = lambda *a, **k: None          # the reference prints every correction
+        try:
+            for dets, embs in frames:
+                H.dets, H.feats = dets, embs
+                outs.append(np.asarray(t.update(dets, img), dtype=np.float64).reshape(-1, 8))
+        finally:
+            builtins.print = pr
+        exact = _hybridsort_lockstep(frames, kw, outs)
+        counts, rows = pack_outputs(outs)
+        out[f"{name}__gen"] = np.array([n, nf, seed, D], np.int64)
+        out[f"{name}__stream"] = np.array([skw["low_conf_frac"], skw.get("drop_frac", 0.0),
+                                           skw.get("n_classes", 1)])
+        out[f"{name}__in_sum"] = np.array([float(np.sum([d.sum() for d, _ in frames])),
+                                           float(np.sum([e.astype(np.float64).sum()
+                                                         for _, e in frames]))])
+        out[f"{name}__params"] = np.array([kw["det_thresh"], kw["max_age"], kw["min_hits"],
+                                           kw["iou_threshold"], kw["delta_t"], kw["inertia"]])
+        out[f"{name}__asso"] = np.array(kw["asso_func"])
+        out[f"{name}__exact"] = np.array(exact)
+        out[f"{name}__out_counts"] = counts
+        out[f"{name}__out"] = rows
+        trk = t.trackers
+        out[f"{name}__st_id"] = np.array([k.id for k in trk], np.int64)
+        out[f"{name}__st_x"] = np.array([k.kf.x.ravel() for k in trk]).reshape(-1, 9)
+        out[f"{name}__st_P"] = np.array([k.kf.P for k in trk]).reshape(-1, 9, 9)
+        out[f"{name}__st_int"] = np.array([[k.age, k.hits, k.hit_streak, k.time_since_update,
+                                            int(k.kf.observed), int(k.kf.attr_saved is not None)]
+                                           for k in trk], np.int64).reshape(-1, 6)
+        out[f"{name}__st_feat"] = np.array([np.asarray(k.smooth_feat, np.float32) for k in trk]
+                                           ).reshape(-1, D)
+        print(f"G7 {name}: out_rows={len(rows)} live={len(trk)} oracle_exact={exact} "
+              f"emb_margin={EMB_MARGIN['min']:.2e}")
+    out["cases"] = np.array([c[0] for c in HYBRIDSORT_CASES])
+    np.savez_compressed(os.path.join(HERE, "hybridsort_synth.npz"), **out)
+
+
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["g1", "g2", "g3", "g4", "g5", "g6"]
+    which = sys.argv[1:] or ["g1", "g2", "g3", "g4", "g5", "g6", "g7"]
     if "g3" in which:
         make_g3()
     if "g1" in which:
@@ -576,4 +696,6 @@ if __name__ == "__main__":
         make_g5()
     if "g6" in which:
         make_g6()
+    if "g7" in which:
+        make_g7()
     print(f"LAP calls {TIES['calls']}, tied {TIES['ties']}")

@@ -111,6 +111,8 @@ class Harness:
     high_thresh = 0.5      # BoT-SORT track_high_thresh (rows the reference asks features for)
     dets = None
     warp = np.eye(2, 3)
+    match_boxes = False    # HybridSORT: get_features sees every row of each per-class call;
+                           # its rows are found by box (the global norm is over those rows)
 
 
 def _install_botsort_shims():
@@ -125,6 +127,11 @@ def _install_botsort_shims():
             pass
 
         def get_features(self, xyxys, img):
+            if Harness.match_boxes:
+                where = {tuple(b): k for k, b in enumerate(Harness.dets[:, :4])}
+                idx = [where[tuple(b)] for b in np.asarray(xyxys).reshape(-1, 4)]
+                features = Harness.feats[idx]
+                return features / np.linalg.norm(features)
             if xyxys.size != 0:
                 m = Harness.dets[:, 4] > Harness.high_thresh
                 features = Harness.feats[m]
@@ -172,6 +179,17 @@ def load_deepocsort():
     import importlib
     ns = types.SimpleNamespace()
     ns.deep_ocsort = importlib.import_module("boxmot.trackers.deepocsort.deep_ocsort")
+    return ns
+
+
+def load_hybridsort():
+    """Reference HybridSORT modules (fake ReID of step 5; its ECC CMC is off, hybridsort.py:360)."""
+    _install_shims()
+    _install_botsort_shims()
+    import importlib
+    ns = types.SimpleNamespace()
+    ns.hybridsort = importlib.import_module("boxmot.trackers.hybridsort.hybridsort")
+    ns.kf = importlib.import_module("boxmot.motion.kalman_filters.hybridsort_kf")
     return ns
 
 

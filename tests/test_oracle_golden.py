@@ -272,3 +272,45 @@ def test_deepocsort_oracle_matches_reference(golden_dir, name):
     if D:
         assert np.array_equal(np.array([np.asarray(k.emb, np.float64) for k in t.trackers]
                                        ).reshape(-1, D), g[f"{name}__st_emb"])
+
+
+HYBRIDSORT_CASES = ["hs_n64_d32", "hs_n128_d64", "hs_n96_dt5_iou", "hs_n64_cls3",
+                    "hs_n96_diou_long", "hs_n256_d64"]
+
+
+def hybridsort_case(g, name):
+    """Inputs of a G7 case regenerated from its seed (checksum-pinned): (frames [(dets, raw
+    embeddings of every row)], HybridSortOracle kwargs, D)."""
+    from yolo_tracking_amd.synth import make_frames
+    n, nf, seed, D = (int(x) for x in g[f"{name}__gen"])
+    low, drop, ncls = (float(x) for x in g[f"{name}__stream"])
+    raw = make_frames(n, nf, seed, emb_dim=D, low_conf_frac=low, drop_frac=drop,
+                      n_classes=int(ncls))
+    sums = g[f"{name}__in_sum"]
+    assert float(np.sum([d.sum() for d, _ in raw])) == sums[0]
+    assert float(np.sum([e.astype(np.float64).sum() for _, e in raw])) == sums[1]
+    p = g[f"{name}__params"]
+    kw = dict(det_thresh=float(p[0]), max_age=int(p[1]), min_hits=int(p[2]),
+              iou_threshold=float(p[3]), delta_t=int(p[4]), inertia=float(p[5]),
+              asso_func=str(g[f"{name}__asso"]))
+    return raw, kw, D
+
+
+@pytest.mark.parametrize("name", HYBRIDSORT_CASES)
+def test_hybridsort_oracle_matches_reference(golden_dir, name):
+    from oracle.hybridsort import HybridSortOracle, per_class_update
+    g = np.load(os.path.join(golden_dir, "hybridsort_synth.npz"))
+    frames, kw, D = hybridsort_case(g, name)
+    t = HybridSortOracle(**kw)
+    got = [np.asarray(per_class_update(t, d, e), dtype=np.float64).reshape(-1, 8)
+           for d, e in frames]
+    exp = golden_outputs(g, name)
+    assert bool(g[f"{name}__exact"])
+    assert all(np.array_equal(a, b) for a, b in zip(got, exp))
+    assert np.array_equal([k.id for k in t.trackers], g[f"{name}__st_id"])
+    assert np.array_equal(np.array([k.kf.x.ravel() for k in t.trackers]).reshape(-1, 9),
+                          g[f"{name}__st_x"])
+    assert np.array_equal(np.array([k.kf.P for k in t.trackers]).reshape(-1, 9, 9),
+                          g[f"{name}__st_P"])
+    assert np.array_equal(np.array([k.smooth_feat for k in t.trackers]).reshape(-1, D),
+                          g[f"{name}__st_feat"])

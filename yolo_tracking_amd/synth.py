@@ -14,7 +14,7 @@ import numpy as np
 
 class SyntheticStream:
     def __init__(self, n_objects, seed, low_conf_frac=0.1, emb_dim=0, turnover=0.02,
-                 speed_sigma=1.5, jitter_sigma=0.5, shuffle=True, canvas=None, drop_frac=0.0):
+                 speed_sigma=1.5, jitter_sigma=0.5, shuffle=True, canvas=None, drop_frac=0.0, n_classes=1):
         self.n = int(n_objects)
         self.rng = np.random.default_rng(seed)
         self.canvas = float(canvas) if canvas else 64.0 * np.sqrt(max(self.n, 1))
@@ -26,6 +26,7 @@ class SyntheticStream:
         self.shuffle = shuffle
         self.drop_frac = float(drop_frac)   # missed detections per frame (drawn last, so 0 keeps
                                             # every other draw of the stream unchanged)
+        self.n_classes = int(n_classes)     # object k has class k % n_classes (no draw)
         r = self.rng
         self.wh = r.uniform(16.0, 64.0, size=(self.n, 2))
         self.ctr = r.uniform(0.0, self.canvas, size=(self.n, 2))
@@ -67,7 +68,7 @@ class SyntheticStream:
         dets = np.empty((self.n, 6), dtype=np.float64)
         dets[:, :4] = box
         dets[:, 4] = conf
-        dets[:, 5] = 0.0
+        dets[:, 5] = (np.arange(self.n) % self.n_classes).astype(np.float64)
         order = r.permutation(self.n) if self.shuffle else np.arange(self.n)
         if self.drop_frac > 0:
             order = order[r.random(self.n) >= self.drop_frac]
