@@ -18,6 +18,11 @@
  *   yta_deepocsort_*         boxmot/trackers/deepocsort/deep_ocsort.py:308-520  DeepOCSort.__init__/
  *                            update (created by boxmot/tracker_zoo.py:83-99); ReID and CMC outside
  *   yta_kf8_run              deep_ocsort.py:103-293 KalmanBoxTracker (new KF) + deepocsort_kf.py
+ *   yta_hybridsort_*         boxmot/trackers/hybridsort/hybridsort.py:329-570  HybridSORT.__init__/
+ *                            update without its PerClassDecorator (the host replays it call by
+ *                            call, boxmot/utils/__init__.py:22-61; created by
+ *                            boxmot/tracker_zoo.py:100-114); ReID outside
+ *   yta_kf9_run              hybridsort.py:106-320 KalmanBoxTracker + hybridsort_kf.py:339-528
  *   yta_lap_padded           boxmot/utils/association.py:20-28 linear_assignment -> lap.lapjv(cost,
  *                            extend_cost=True)
  *   yta_kf7_run              boxmot/motion/kalman_filters/ocsort_kf.py:339-526 predict / update incl.
@@ -304,6 +309,63 @@ int yta_deepocsort_hip_stream(yta_deepocsort *engine, void **stream);
  * clamps, Q(w, h), R(w, h), freeze / unfreeze replay; final x (n x 8) and full P (n x 64). */
 int yta_kf8_run(int device, int n, int steps, const double *b0, const double *b,
                 const double *warps, double *x_out, double *P_out);
+
+/* ---- HybridSORT engine: S independent streams --------------------------------------------
+ * HybridSORT(det_thresh, max_age, min_hits, iou_threshold, delta_t, asso_func, inertia) per stream
+ * (boxmot/trackers/hybridsort/hybridsort.py:329-570) with its hard-wired association settings
+ * (:346-360: TCM weight 0, ReID weight 1.3, long-term ReID weight 0 with the 0.4 correction, no
+ * BYTE round, no ECC).  One update call = one undecorated HybridSORT.update: the per-class
+ * decorator's calls (one per class, each over all trackers) are issued by the caller.  The ReID
+ * forward pass (:394 get_features) stays outside: its rows are inputs here.  KalmanBoxTracker.count
+ * starts at 0 and ids are reported + 1; det_ind reports the detection's score (dets0[:, 6]). */
+typedef struct yta_hybridsort yta_hybridsort;
+typedef struct {
+    double det_thresh;          /* hybridsort.yaml: 0                                      */
+    int max_age;                /* 30                                                      */
+    int min_hits;               /* 1                                                       */
+    double iou_threshold;       /* iou_thresh 0.3                                          */
+    int delta_t;                /* 3  (0..8)                                               */
+    int asso_func;              /* YTA_ASSO_IOU..YTA_ASSO_CIOU: giou (centroid: the reference
+                                   calls the asso function without the image size, :516)   */
+    double inertia;             /* 0.2                                                     */
+} yta_hybridsort_params;
+
+int yta_hybridsort_create(int device, int n_streams, int track_capacity, int max_dets,
+                          int feat_dim, const yta_hybridsort_params *params,
+                          yta_hybridsort **engine);
+int yta_hybridsort_destroy(yta_hybridsort *engine);
+int yta_hybridsort_reset(yta_hybridsort *engine);
+int yta_hybridsort_capacity(yta_hybridsort *engine, int *track_capacity, int *max_dets);
+/* Host-buffer update (synchronous).  dets / det_offsets / next_id / out / out_offsets as
+ * yta_ocsort_update; feats: feat_dim float32 for EVERY input row, in input order (what
+ * get_features returns for the call's boxes). */
+int yta_hybridsort_update(yta_hybridsort *engine, const double *dets, const int *det_offsets,
+                          const float *feats, long long *next_id, double *out, int out_capacity,
+                          int *out_offsets);
+/* Device-resident update (asynchronous): d_feats feat_dim float32 per input row; d_out
+ * S * track_capacity rows x 8; d_out_counts S ints (may be NULL). */
+int yta_hybridsort_update_device(yta_hybridsort *engine, const double *d_dets,
+                                 const int *d_det_offsets, const float *d_feats, double *d_out,
+                                 int *d_out_counts);
+int yta_hybridsort_sync(yta_hybridsort *engine);
+/* Parity introspection, tracker-list order: ints 6 x int64 per tracker (id, age, hits,
+ * hit_streak, time_since_update, kf.observed), dbl 3 x f64 (conf, cls, det_ind), x (9 f64),
+ * P (81 f64), feat (feat_dim float32 smooth_feat per tracker; may be NULL). */
+int yta_hybridsort_get_state(yta_hybridsort *engine, int stream, int *n_tracks, long long *ints,
+                             double *dbl, double *x, double *P, float *feat);
+/* The cls of every live tracker of a stream in list order (PerClassDecorator's active classes,
+ * boxmot/utils/__init__.py:38). */
+int yta_hybridsort_classes(yta_hybridsort *engine, int stream, double *cls, int cap, int *n);
+/* Last frame's counts summed over streams: dets, kept dets, live trackers, output rows, births,
+ * LAP calls, long-term corrections, feature jobs (8 int64). */
+int yta_hybridsort_stats(yta_hybridsort *engine, long long *stats);
+int yta_hybridsort_hip_stream(yta_hybridsort *engine, void **stream);
+/* HybridSORT Kalman KAT (hybridsort.py:112-320): n tracks initialised from rows b0 (n x 5:
+ * x1 y1 x2 y2 score) run `steps` steps of predict (velocity clamp) + update(b[step] (n x 5); a
+ * NaN first value = update(None)) with the freeze / unfreeze replay; final x (n x 9) and full P
+ * (n x 81). */
+int yta_kf9_run(int device, int n, int steps, const double *b0, const double *b, double *x_out,
+                double *P_out);
 
 #ifdef __cplusplus
 }

@@ -322,7 +322,9 @@ class HybridSortOracle:
         for every detection (reid_multibackend.py:310 global norm already applied)."""
         self.frame_count += 1
         scores = dets[:, 4]
-        dets_embs = np.array(feats, dtype=np.float32).reshape(len(dets), -1)
+        dets_embs = np.array(feats, dtype=np.float32)
+        if dets_embs.ndim != 2:
+            dets_embs = dets_embs.reshape(len(dets), -1)
         dets0 = np.concatenate((dets, np.expand_dims(scores, axis=-1)), axis=1)
         dets5 = np.concatenate((dets[:, :4], np.expand_dims(scores, axis=-1)), axis=1)
         remain = scores > self.det_thresh
@@ -401,7 +403,9 @@ def per_class_update(tracker, dets, raw, get_features=get_features_norm):
     """PerClassDecorator (boxmot/utils/__init__.py:22-61) around HybridSortOracle.update: one call
     per class of the union of active and detected classes, in the iteration order of that Python
     set, each with the get_features output of its own rows; every call predicts all trackers."""
-    raw = np.asarray(raw, dtype=np.float32).reshape(len(dets), -1)
+    raw = np.asarray(raw, dtype=np.float32)
+    if raw.ndim != 2:
+        raw = raw.reshape(len(dets), -1)
     if dets.size == 0:
         return tracker.update(dets, get_features(raw))
     dets_dict = {c: np.array([d for d in dets if d[5] == c]) for c in set(d[5] for d in dets)}

@@ -3,6 +3,8 @@
 
     python tools/bench_tracker.py --tracker ocsort  [--n 256]  [--streams 1] [--steps 50]
     python tools/bench_tracker.py --tracker botsort [--n 1024] [--dim 512] [--streams 1]
+    python tools/bench_tracker.py --tracker deepocsort [--n 2048] [--dim 512] [--streams 1]
+    python tools/bench_tracker.py --tracker hybridsort [--n 4096] [--dim 512] [--streams 8]
 
 A step = one update() frame of every stream (SURVEY.md §8(d) synthetic streams; OCSORT with
 ocsort.yaml parameters and no low-confidence detections, BoT-SORT with botsort.yaml parameters
@@ -30,6 +32,12 @@ BOTSORT_YAML = dict(track_high_thresh=0.33824964456239337, track_low_thresh=0.1,
                     new_track_thresh=0.21144301345190655, track_buffer=60,
                     match_thresh=0.22734550911325851, proximity_thresh=0.5945380911899254,
                     appearance_thresh=0.4818211117541298, frame_rate=30)
+DEEPOCSORT_YAML = dict(det_thresh=0.0, max_age=30, min_hits=1, iou_threshold=0.3, delta_t=3,
+                       asso_func="giou", inertia=0.2)          # create_tracker's arguments
+HYBRIDSORT_YAML = dict(det_thresh=0.0, max_age=30, min_hits=1, iou_threshold=0.3, delta_t=3,
+                       asso_func="giou", inertia=0.2)
+CMC_AFFINE = [[1.0, 1e-3, 0.5], [-1e-3, 1.0, -0.3]]
+DEFAULT_N = {"ocsort": 256, "botsort": 1024, "deepocsort": 2048, "hybridsort": 4096}
 
 
 def reid_rows(dets, embs, thr):
@@ -49,7 +57,8 @@ def cpu_leg(code, timeout=900):
 
 def main():
     p = argparse.ArgumentParser()
-    p.add_argument("--tracker", choices=["ocsort", "botsort"], required=True)
+    p.add_argument("--tracker", choices=["ocsort", "botsort", "deepocsort", "hybridsort"],
+                   required=True)
     p.add_argument("--n", type=int, default=None)
     p.add_argument("--dim", type=int, default=512)
     p.add_argument("--streams", type=int, default=1)
@@ -64,9 +73,12 @@ def main():
     S = args.streams
     F = args.warmup + args.steps
     oc = args.tracker == "ocsort"
-    N = args.n or (256 if oc else 1024)
+    fam = args.tracker in ("deepocsort", "hybridsort")
+    N = args.n or DEFAULT_N[args.tracker]
     D = 0 if oc else args.dim
     kw_stream = dict(low_conf_frac=0.0) if oc else dict(emb_dim=D)
+    if fam:
+        kw_stream["low_conf_frac"] = 0.0
     streams = [make_frames(N, F, args.seed + s, **kw_stream) for s in range(S)]
     dets = np.stack([np.concatenate([streams[s][f][0] for s in range(S)]) for f in range(F)])
     off = np.array([[sum(len(streams[q][f][0]) for q in range(s)) for s in range(S + 1)]
@@ -88,6 +100,45 @@ def main():
                           ctypes.c_void_p(d_off.data_ptr() + f * (S + 1) * 4),
                           ctypes.c_void_p(d_wh.data_ptr()), ctypes.c_void_p(d_out.data_ptr()),
                           None))
+    elif fam:
+        # get_features rows of every detection (all rows kept at det_thresh 0), global norm per
+        # stream-frame (reid_multibackend.py:310)
+        feats = np.zeros((F, dets.shape[1], D), np.float32)
+        for f in range(F):
+            r0 = 0
+            for s in range(S):
+                d, e = streams[s][f]
+                feats[f, r0:r0 + len(d)] = e / np.linalg.norm(e)
+                r0 += len(d)
+        d_feat = torch.from_numpy(feats).cuda()
+        del feats
+        feat_bytes = dets.shape[1] * D * 4
+        if args.tracker == "deepocsort":
+            from yolo_tracking_amd.trackers.deepocsort import DeepOCSortEngine
+            eng = DeepOCSortEngine(S, feat_dim=D, **DEEPOCSORT_YAML, track_capacity=2 * N,
+                                   max_dets=N)
+            d_warp = torch.tensor([CMC_AFFINE] * S, dtype=torch.float64).cuda()
+            shape = SyntheticStream(N, args.seed, **kw_stream).img_shape
+            d_wh = torch.tensor([[shape[1], shape[0]]] * S, dtype=torch.int32).cuda()
+            fn, sync = eng.lib.yta_deepocsort_update_device, eng.lib.yta_deepocsort_sync
+        else:
+            from yolo_tracking_amd.trackers.hybridsort import HybridSortEngine
+            eng = HybridSortEngine(S, feat_dim=D, **HYBRIDSORT_YAML, track_capacity=2 * N,
+                                   max_dets=N)
+            fn, sync = eng.lib.yta_hybridsort_update_device, eng.lib.yta_hybridsort_sync
+        cap, _ = eng.capacity()
+        d_out = torch.empty((S * cap, 8), dtype=torch.float64, device="cuda")
+
+        def step(f):
+            pd = ctypes.c_void_p(d_dets.data_ptr() + f * row_bytes)
+            po = ctypes.c_void_p(d_off.data_ptr() + f * (S + 1) * 4)
+            pf = ctypes.c_void_p(d_feat.data_ptr() + f * feat_bytes)
+            if args.tracker == "deepocsort":
+                _lib.check(fn(eng.handle, pd, po, pf, ctypes.c_void_p(d_warp.data_ptr()),
+                              ctypes.c_void_p(d_wh.data_ptr()), ctypes.c_void_p(d_out.data_ptr()),
+                              None))
+            else:
+                _lib.check(fn(eng.handle, pd, po, pf, ctypes.c_void_p(d_out.data_ptr()), None))
     else:
         from yolo_tracking_amd.trackers.botsort import BoTSORTEngine
         eng = BoTSORTEngine(S, feat_dim=D, **BOTSORT_YAML, track_capacity=2 * N, max_dets=N)
@@ -126,8 +177,34 @@ def main():
     value = S * args.steps / el
     stats = eng.stats()
     # CPU leg: the oracle on stream 0, 1 thread, bounded sample
-    cf = args.cpu_frames or (30 if oc else 6)
-    if oc:
+    cf = args.cpu_frames if args.cpu_frames is not None else (30 if oc else (2 if fam else 6))
+    if cf == 0:
+        code = None
+    elif args.tracker == "deepocsort":
+        code = ("import sys,time,json; sys.path.insert(0,%r)\n"
+                "import numpy as np\n"
+                "from oracle.deepocsort import DeepOCSortOracle\n"
+                "from yolo_tracking_amd.synth import make_frames, SyntheticStream\n"
+                "fr=make_frames(%d,%d,%d,emb_dim=%d,low_conf_frac=0.0)\n"
+                "sh=SyntheticStream(%d,%d,emb_dim=%d,low_conf_frac=0.0).img_shape\n"
+                "w=np.array(%r)\n"
+                "t=DeepOCSortOracle(**%r); t.update(fr[0][0],sh,fr[0][1]/np.linalg.norm(fr[0][1]),w)\n"
+                "t0=time.perf_counter()\n"
+                "for d,e in fr[1:]: t.update(d,sh,e/np.linalg.norm(e),w)\n"
+                "print(json.dumps({'frames':len(fr)-1,'seconds':time.perf_counter()-t0}))\n"
+                % (REPO, N, cf + 1, args.seed, D, N, args.seed, D, CMC_AFFINE, DEEPOCSORT_YAML))
+    elif args.tracker == "hybridsort":
+        code = ("import sys,time,json; sys.path.insert(0,%r)\n"
+                "import numpy as np\n"
+                "from oracle.hybridsort import HybridSortOracle\n"
+                "from yolo_tracking_amd.synth import make_frames\n"
+                "fr=make_frames(%d,%d,%d,emb_dim=%d,low_conf_frac=0.0)\n"
+                "t=HybridSortOracle(**%r); t.update(fr[0][0],fr[0][1]/np.linalg.norm(fr[0][1]))\n"
+                "t0=time.perf_counter()\n"
+                "for d,e in fr[1:]: t.update(d,e/np.linalg.norm(e))\n"
+                "print(json.dumps({'frames':len(fr)-1,'seconds':time.perf_counter()-t0}))\n"
+                % (REPO, N, cf + 1, args.seed, D, HYBRIDSORT_YAML))
+    elif oc:
         code = ("import sys,time,json; sys.path.insert(0,%r)\n"
                 "from oracle.ocsort import OCSortOracle\n"
                 "from yolo_tracking_amd.synth import make_frames, SyntheticStream\n"
@@ -152,7 +229,7 @@ def main():
                 "for d,e in fr[1:]: t.update(d,rows(d,e))\n"
                 "print(json.dumps({'frames':len(fr)-1,'seconds':time.perf_counter()-t0}))\n"
                 % (REPO, N, cf + 1, args.seed, D, BOTSORT_YAML))
-    res = cpu_leg(code)
+    res = cpu_leg(code) if code else {"error": "skipped (--cpu-frames 0)"}
     cpu = ({"value": res["frames"] / res["seconds"], "unit": "calls/s", "cores": 1, "kind": "port",
             "sample": f"oracle {args.tracker} 1 stream {N}x{N}, frames 2..{cf + 1} of seed "
                       f"{args.seed}, {res['seconds']:.1f} s, 1 thread"}

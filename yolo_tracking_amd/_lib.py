@@ -65,6 +65,14 @@ class DocParams(ctypes.Structure):
                 ("aw_off", ctypes.c_int)]
 
 
+class HsParams(ctypes.Structure):
+    """yta_hybridsort_params (include/yolo_tracking_amd.h)."""
+    _fields_ = [("det_thresh", ctypes.c_double), ("max_age", ctypes.c_int),
+                ("min_hits", ctypes.c_int), ("iou_threshold", ctypes.c_double),
+                ("delta_t", ctypes.c_int), ("asso_func", ctypes.c_int),
+                ("inertia", ctypes.c_double)]
+
+
 ASSO_FUNCS = {"iou": 0, "giou": 1, "diou": 2, "ciou": 3, "centroid": 4}
 
 _lib = None
@@ -126,6 +134,18 @@ _SIGS = {
     "yta_deepocsort_stats": ([_P, _P], _I),
     "yta_deepocsort_hip_stream": ([_P, _P], _I),
     "yta_kf8_run": ([_I, _I, _I, _P, _P, _P, _P, _P], _I),
+    "yta_hybridsort_create": ([_I, _I, _I, _I, _I, _P, _P], _I),
+    "yta_hybridsort_destroy": ([_P], _I),
+    "yta_hybridsort_reset": ([_P], _I),
+    "yta_hybridsort_capacity": ([_P, _P, _P], _I),
+    "yta_hybridsort_update": ([_P, _P, _P, _P, _P, _P, _I, _P], _I),
+    "yta_hybridsort_update_device": ([_P, _P, _P, _P, _P, _P], _I),
+    "yta_hybridsort_sync": ([_P], _I),
+    "yta_hybridsort_get_state": ([_P, _I, _P, _P, _P, _P, _P, _P], _I),
+    "yta_hybridsort_classes": ([_P, _I, _P, _I, _P], _I),
+    "yta_hybridsort_stats": ([_P, _P], _I),
+    "yta_hybridsort_hip_stream": ([_P, _P], _I),
+    "yta_kf9_run": ([_I, _I, _I, _P, _P, _P, _P], _I),
 }
 
 EXPORTED_SYMBOLS = tuple(_SIGS)
@@ -268,6 +288,18 @@ def kf8_run(b0, b, warps=None, device=0):
     x = np.empty((n, 8))
     P = np.empty((n, 8, 8))
     check(load_library().yta_kf8_run(device, n, len(b), ptr(b0), ptr(b), ptr(w), ptr(x), ptr(P)))
+    return x, P
+
+
+def kf9_run(b0, b, device=0):
+    """HybridSORT KalmanBoxTracker KAT (yta_kf9_run): b0 (n, 5) rows x1 y1 x2 y2 score, b
+    (steps, n, 5) with NaN rows = missed."""
+    b0 = np.ascontiguousarray(b0, dtype=np.float64).reshape(-1, 5)
+    n = len(b0)
+    b = np.ascontiguousarray(b, dtype=np.float64).reshape(-1, n, 5)
+    x = np.empty((n, 9))
+    P = np.empty((n, 9, 9))
+    check(load_library().yta_kf9_run(device, n, len(b), ptr(b0), ptr(b), ptr(x), ptr(P)))
     return x, P
 
 

@@ -1,0 +1,1269 @@
+// HybridSORT update() for S independent streams on gfx950, all tracker state resident in HBM.
+//
+// Follows boxmot/trackers/hybridsort/hybridsort.py:373-570 (HybridSORT.update without its
+// PerClassDecorator, which the host side replays call by call) with the association of
+// boxmot/trackers/hybridsort/association.py:495-581 as HybridSORT configures it (hard-wired,
+// hybridsort.py:346-360): TCM weight 0, ReID weight 1.3 on the short-term embedding cost,
+// long-term ReID weight 0, long-term correction at 0.4, no BYTE round (hybridsort.yaml).  One
+// frame (one undecorated update call) =
+//   k_hs_pre     [block/stream]  predict every tracker (:296-320: velocity clamp, 9-d Kalman
+//                                predict, kalman / simple scores), NaN cull (:406-416), column
+//                                inputs (box, kalman score, 4 corner velocities, k-previous and
+//                                last observations), confidence split (:391-404)
+//   k_hs_emb     [grid]          stage-1 cost tiles: dets_feats x smooth_feats on f64 MFMA
+//                                (v_mfma_f64_16x16x4_f64) with the row norms, cosine distance
+//                                max(0, 1 - uv / sqrt(uu vv)) (association.py:667-684), and in the
+//                                same epilogue the asso function, the four corner angle costs
+//                                (:314-383, :507-518) and the fused cost
+//                                -(iou + angle) + 1.3 emb (:531-539)
+//   k_hs_assoc   [block/stream]  padded LAP (lapx semantics, no limit), long-term correction
+//                                (:557-567), tracker updates (Kalman + ORU replay, corner
+//                                velocities, observations), OCR round on the last observations
+//                                (:512-542), misses, births, outputs in reversed tracker order,
+//                                removal (:544-570)
+//   k_hs_ema     [grid]          update_features of first-round matches (EMA alpha 0.8, float32)
+//                                and the smooth features of births (:197-214)
+#include <algorithm>
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "kf_hybrid.hpp"
+#include "kf_ocsort.hpp"   // np_sum5
+#include "ocsort_common.hpp"
+
+namespace yta {
+namespace {
+
+constexpr int HF_CPRE = 8;          // confidence_pre is not None
+constexpr int ERR_INF_ROW = 64;     // a predicted box with an inf but no NaN (the reference's
+                                    // trks / trackers lists would disagree, hybridsort.py:412-416)
+constexpr int HS_RING = OC_DT_MAX + 1;
+constexpr double HS_TRACK_THRESH = 0.6;     // predict(track_thresh=0.6) (:296)
+constexpr double HS_EG_WEIGHT = 1.3;        // EG_weight_high_score (:347)
+constexpr double HS_CORR_THRESH = 0.4;      // longterm_reid_correction_thresh (:355)
+
+struct HsTrack {
+    Kf9 kf;
+    Kf9 fz;                         // frozen filter (attr_saved x / P)
+    double hist_z[5];               // the filter's last measurement kept in history_obs
+    double last_obs[5];
+    double vel[8];                  // velocity_lt, _rt, _lb, _rb: (dy, dx) each
+    double conf, cls, det_ind;      // det_ind holds the detection's score (dets0[:, 6])
+    double confidence, conf_pre;
+    double obs[HS_RING][5];
+    long long id;
+    int obs_age[HS_RING];
+    int obs_n;
+    int age, hits, hit_streak, tsu, flags, hist_since;
+};
+
+struct HsCounters {
+    long long next_id;
+    int frame;
+    int n_trk, n_free;
+    int n_dets, n_high, n_out, n_births;
+    int lap_calls, corrections;
+    int n_ema;
+    int err;
+    int pad[18];
+};
+static_assert(sizeof(HsCounters) == 128, "HsCounters layout");
+
+// per-tracker association inputs, one 160-B record (k_hs_pre -> k_hs_emb / k_hs_assoc)
+struct HsCol {
+    double box[4];
+    double kscore;                  // clip(x[3], 0.6, 1)
+    double kobs[5];                 // k_previous_obs
+    double vel[8];
+    double valid;                   // k_previous_obs[4] >= 0 (valid_mask)
+    double pad;
+};
+
+struct HsArgs {
+    int S, CAP, MAXD, D;
+    double det_thresh, thr, inertia;
+    int max_age, min_hits, delta_t, asso;
+    const double *det_in;
+    const int *det_off;
+    const float *det_feat;          // [rows of det_in][D] get_features output
+    HsTrack *rec;                   // [S*CAP]
+    float *feat;                    // [S*CAP][D] smooth_feat (float32)
+    int *list, *free_list;          // [S*CAP]
+    HsCounters *cnt;
+    // per frame
+    int *hi_row;                    // [S*MAXD]
+    HsCol *col;                     // [S*CAP]
+    double *clast;                  // [S*CAP][5] last observations
+    int *nan_flag, *cslot;          // [S*CAP]
+    double *cost, *emat;            // [S*MAXD*CAP]
+    int *rmatch, *cmatched;
+    int *udet, *utrk, *tmp;         // [S*(MAXD+CAP)]
+    int *upd;                       // [S*CAP] kept-detection index updating each tracker or -1
+    int *ema_slot, *ema_row;        // [S*(CAP+MAXD)] feature jobs: slot, kept index (birth: ~p)
+    unsigned char *lap_ws;
+    long long lap_ws_stride;
+    double *out;
+    int *out_counts;
+};
+
+__device__ __forceinline__ long long hs_mb(const HsArgs &a, int s) {
+    return (long long)s * (a.MAXD > 4 ? a.MAXD : 4) * a.CAP;
+}
+
+// corner (x column, y column) of velocity_lt, _rt, _lb, _rb (hybridsort.py:74-103,
+// association.py:338-383)
+__device__ __forceinline__ int hs_cx(int c) { return c < 2 ? 0 : 2; }
+__device__ __forceinline__ int hs_cy(int c) { return (c & 1) ? 3 : 1; }
+
+// speed_direction_{lt,rt,lb,rb}(prev, cur) (hybridsort.py:74-103) -> (dy, dx)
+__device__ __forceinline__ void hs_dir(const double *p, const double *b, int c, double &vy,
+                                       double &vx) {
+    const double cx1 = p[hs_cx(c)], cy1 = p[hs_cy(c)];
+    const double cx2 = b[hs_cx(c)], cy2 = b[hs_cy(c)];
+    const double sy = cy2 - cy1, sx = cx2 - cx1;
+    const double nrm = sqrt(sy * sy + sx * sx) + 1e-6;
+    vy = sy / nrm;
+    vx = sx / nrm;
+}
+
+// k_previous_obs (hybridsort.py:22-30) from the ring
+__device__ __forceinline__ void hs_prev_obs(const HsTrack &r, int dt, double *o) {
+    if (r.obs_n == 0) {
+        for (int k = 0; k < 5; ++k) o[k] = -1.0;
+        return;
+    }
+    const int m = r.obs_n < HS_RING ? r.obs_n : HS_RING;
+    for (int i = 0; i < dt; ++i) {
+        const int want = r.age - (dt - i);
+        for (int e = 0; e < m; ++e)
+            if (r.obs_age[e] == want) {
+                for (int k = 0; k < 5; ++k) o[k] = r.obs[e][k];
+                return;
+            }
+    }
+    const int newest = (r.obs_n - 1) % HS_RING;
+    for (int k = 0; k < 5; ++k) o[k] = r.obs[newest][k];
+}
+
+// KalmanBoxTracker.update (hybridsort.py:230-294) + KalmanFilter.update (hybridsort_kf.py:439-528).
+// bbox = dets[p] (x1, y1, x2, y2, score); cls / det_ind = dets0[p, 5] / dets0[p, 6].
+__device__ void hs_update(HsTrack &r, const double *bbox, double cls, double det_ind, int dt) {
+    if (!bbox) {
+        if (r.flags & OF_OBSERVED) {          // freeze
+            r.fz = r.kf;
+            r.flags |= OF_SAVED;
+        }
+        r.flags &= ~(OF_OBSERVED | HF_CPRE);  // confidence_pre = None
+        r.hist_since += 1;
+        return;
+    }
+    r.conf = bbox[4];
+    r.cls = cls;
+    r.det_ind = det_ind;
+    if (np_sum5(r.last_obs) >= 0) {
+        const int m = r.obs_n < HS_RING ? r.obs_n : HS_RING;
+        bool found = false;
+        double acc[8];
+        for (int i = 0; i < dt; ++i) {        // every stored observation within delta_t (no break)
+            const int want = r.age - i - 1;
+            for (int e = 0; e < m; ++e)
+                if (r.obs_age[e] == want) {
+                    for (int c = 0; c < 4; ++c) {
+                        double vy, vx;
+                        hs_dir(r.obs[e], bbox, c, vy, vx);
+                        if (found) {
+                            acc[2 * c] = acc[2 * c] + vy;
+                            acc[2 * c + 1] = acc[2 * c + 1] + vx;
+                        } else {
+                            acc[2 * c] = vy;
+                            acc[2 * c + 1] = vx;
+                        }
+                    }
+                    found = true;
+                    break;
+                }
+        }
+        if (!found)
+            for (int c = 0; c < 4; ++c) hs_dir(r.last_obs, bbox, c, acc[2 * c], acc[2 * c + 1]);
+        for (int k = 0; k < 8; ++k) r.vel[k] = acc[k];
+        r.flags |= OF_VELOCITY;
+    }
+    for (int k = 0; k < 5; ++k) r.last_obs[k] = bbox[k];
+    const int slot = r.obs_n % HS_RING;
+    for (int k = 0; k < 5; ++k) r.obs[slot][k] = bbox[k];
+    r.obs_age[slot] = r.age;
+    r.obs_n += 1;
+    r.tsu = 0;
+    r.hits += 1;
+    r.hit_streak += 1;
+    double z[5];
+    hs_bbox_to_z(bbox, z);
+    if (!(r.flags & OF_OBSERVED) && (r.flags & OF_SAVED)) {   // unfreeze: restore, replay
+        r.kf = r.fz;
+        r.flags &= ~OF_SAVED;
+        kf9_replay(r.kf, r.hist_z, z, r.hist_since + 1, r.hist_z);
+    } else {
+        for (int k = 0; k < 5; ++k) r.hist_z[k] = z[k];
+    }
+    r.hist_since = 0;
+    r.flags |= OF_OBSERVED;
+    kf9_correct(r.kf, z);
+    r.conf_pre = r.confidence;                // confidence_pre = confidence (never None here)
+    r.flags |= HF_CPRE;
+    r.confidence = bbox[4];
+}
+
+// KalmanBoxTracker.predict (hybridsort.py:296-320): returns the predicted box; kalman / simple
+// scores through ks / ss
+__device__ void hs_predict(HsTrack &r, double *b, double &ks, double &ss) {
+    if (r.kf.x[7] + r.kf.x[2] <= 0) r.kf.x[7] = r.kf.x[7] * 0.0;
+    kf9_predict(r.kf);
+    r.age += 1;
+    if (r.tsu > 0) r.hit_streak = 0;
+    r.tsu += 1;
+    hs_x_to_bbox(r.kf.x, b);
+    ks = np_min(np_max(r.kf.x[3], HS_TRACK_THRESH), 1.0);
+    const bool pre = (r.flags & HF_CPRE) && r.conf_pre != 0.0;   // `if not self.confidence_pre`
+    const double v = pre ? r.confidence - (r.conf_pre - r.confidence) : r.confidence;
+    ss = np_min(np_max(v, 0.1), HS_TRACK_THRESH);
+}
+
+// KalmanBoxTracker.__init__ (hybridsort.py:112-194)
+__device__ void hs_birth(HsTrack &out, const double *bbox, double cls, double det_ind, long long id) {
+    HsTrack r;
+    double z[5];
+    hs_bbox_to_z(bbox, z);
+    kf9_init(z, r.kf);
+    r.fz = r.kf;
+    for (int k = 0; k < 5; ++k) {
+        r.hist_z[k] = 0.0;
+        r.last_obs[k] = -1.0;
+    }
+    for (int k = 0; k < 8; ++k) r.vel[k] = 0.0;
+    r.conf = bbox[4];
+    r.cls = cls;
+    r.det_ind = det_ind;
+    r.confidence = bbox[4];
+    r.conf_pre = 0.0;
+    r.id = id;
+    r.obs_n = 0;
+    for (int e = 0; e < HS_RING; ++e) r.obs_age[e] = -1;
+    r.age = r.hits = r.hit_streak = r.tsu = 0;
+    r.flags = 0;
+    r.hist_since = 0;
+    out = r;
+}
+
+__global__ __launch_bounds__(OC_T) void k_hs_pre(HsArgs a) {
+    __shared__ OcShared sh;
+    const int s = blockIdx.x, t = threadIdx.x, nt = blockDim.x;
+    HsCounters *c = a.cnt + s;
+    const long long tb = (long long)s * a.CAP, db = (long long)s * a.MAXD;
+    const long long ub = (long long)s * (a.MAXD + a.CAP);
+    int nd = a.det_off[s + 1] - a.det_off[s];
+    if (nd > a.MAXD || nd < 0) {
+        if (t == 0) atomicOr(&c->err, ERR_DET_CAPACITY);
+        nd = nd < 0 ? 0 : a.MAXD;
+    }
+    const double *din = a.det_in + (long long)a.det_off[s] * 6;
+    int n_trk = c->n_trk;
+    const int dt = a.delta_t;
+    int *list = a.list + tb;
+    HsCol *col = a.col + tb;
+    // predict (:406-413): boxes and scores into the column records (by list position)
+    for (int i = t; i < n_trk; i += nt) {
+        HsTrack &r = a.rec[tb + list[i]];
+        double b[4], ks, ss;
+        hs_predict(r, b, ks, ss);
+        const double sc = r.kf.x[3];
+        const bool nan = (b[0] != b[0]) || (b[1] != b[1]) || (b[2] != b[2]) || (b[3] != b[3]) ||
+                         (sc != sc);
+        if (!nan && !(fabs(b[0]) < INFINITY && fabs(b[1]) < INFINITY && fabs(b[2]) < INFINITY &&
+                      fabs(b[3]) < INFINITY && fabs(sc) < INFINITY))
+            atomicOr(&c->err, ERR_INF_ROW);
+        a.nan_flag[tb + i] = nan;
+        HsCol &q = col[i];
+        for (int k = 0; k < 4; ++k) q.box[k] = b[k];
+        q.kscore = ks;
+        (void)ss;   // simple score: trks[:, 5], read only by the BYTE round (use_byte = False)
+    }
+    block_sync();
+    {
+        int n_free = c->n_free;
+        const int n_nan = block_compact(n_trk, sh.wsum, [&](int i) { return a.nan_flag[tb + i] != 0; },
+                                        [&](int i, int pos) { a.tmp[ub + pos] = list[i]; });
+        for (int k = t; k < n_nan; k += nt) a.free_list[tb + n_free + k] = a.tmp[ub + k];
+        n_free += n_nan;
+        block_sync();
+        const int n_keep = block_compact(n_trk, sh.wsum, [&](int i) { return a.nan_flag[tb + i] == 0; },
+                                         [&](int i, int pos) {
+                                             a.tmp[ub + pos] = list[i];
+                                             a.upd[tb + pos] = i;
+                                         });
+        block_sync();
+        // kept trackers' column records, compacted (scratch: the cost matrix)
+        HsCol *scratch = reinterpret_cast<HsCol *>(a.cost + hs_mb(a, s));
+        for (int j = t; j < n_keep; j += nt) {
+            const HsTrack &r = a.rec[tb + a.tmp[ub + j]];
+            HsCol q = col[a.upd[tb + j]];
+            double ko[5];
+            hs_prev_obs(r, dt, ko);
+            for (int k = 0; k < 5; ++k) q.kobs[k] = ko[k];
+            const bool hv = (r.flags & OF_VELOCITY) != 0;
+            for (int k = 0; k < 8; ++k) q.vel[k] = hv ? r.vel[k] : 0.0;
+            q.valid = ko[4] < 0 ? 0.0 : 1.0;
+            q.pad = 0.0;
+            scratch[j] = q;
+            for (int k = 0; k < 5; ++k) a.clast[(tb + j) * 5 + k] = r.last_obs[k];
+        }
+        block_sync();
+        for (int j = t; j < n_keep; j += nt) {
+            list[j] = a.tmp[ub + j];
+            a.cslot[tb + j] = a.tmp[ub + j];
+            col[j] = scratch[j];
+            a.cmatched[tb + j] = 0;
+            a.nan_flag[tb + j] = 0;
+            a.upd[tb + j] = -1;
+        }
+        n_trk = n_keep;
+        if (t == 0) c->n_free = n_free;
+        block_sync();
+    }
+    // detections kept for association (:401-404)
+    const int n_hi = block_compact(nd, sh.wsum, [&](int i) { return din[i * 6 + 4] > a.det_thresh; },
+                                   [&](int i, int pos) { a.hi_row[db + pos] = i; });
+    for (int i = t; i < n_hi; i += nt) a.rmatch[db + i] = -1;
+    if (t == 0) {
+        c->n_trk = n_trk;
+        c->n_high = n_hi;
+        c->n_dets = nd;
+    }
+}
+
+// ---------------------------------------------------------------------------------- k_hs_emb
+// 64 (detections) x 64 (trackers) cost tiles per block, 4 waves of 32 x 32 (2 x 2 MFMA tiles of
+// v_mfma_f64_16x16x4_f64: A[l&15][k = l>>4], B[k = l>>4][l&15], D[row (l>>4) + 4 r][col l&15]).
+// The embedding dimension streams through LDS in chunks of 32 (float32 -> float64 on the way),
+// with the row norms accumulated from the same chunks.
+typedef double dbl4 __attribute__((ext_vector_type(4)));
+constexpr int HE_TILE = 64, HE_KC = 32, HE_LD = HE_KC + 1;
+
+struct HsDetCol {                   // per detection row of the tile
+    double box[4], score;
+};
+
+__global__ __launch_bounds__(256) void k_hs_emb(HsArgs a) {
+    __shared__ double As[HE_TILE * HE_LD], Bs[HE_TILE * HE_LD];
+    __shared__ double nA[HE_TILE], nB[HE_TILE];
+    __shared__ HsDetCol dcol[HE_TILE];
+    __shared__ HsCol tcol[HE_TILE];
+    const int s = blockIdx.z;
+    const HsCounters *c = a.cnt + s;
+    const int n_trk = c->n_trk, n_hi = c->n_high, D = a.D;
+    const int r0 = blockIdx.y * HE_TILE, c0 = blockIdx.x * HE_TILE;
+    if (r0 >= n_hi || c0 >= n_trk) return;                   // block-uniform
+    const long long tb = (long long)s * a.CAP, db = (long long)s * a.MAXD, mb = hs_mb(a, s);
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int wr = (w >> 1) * 32, wc = (w & 1) * 32;
+    // staging: thread t loads 8 consecutive k of row t >> 2 (A: detection, B: tracker)
+    const int lr = t >> 2, lk = (t & 3) * 8;
+    const bool a_ok = r0 + lr < n_hi, b_ok = c0 + lr < n_trk;
+    const float *arow = a_ok ? a.det_feat + ((long long)a.det_off[s] + a.hi_row[db + r0 + lr]) * D
+                             : nullptr;
+    const float *brow = b_ok ? a.feat + (tb + a.cslot[tb + c0 + lr]) * D : nullptr;
+    double qa = 0.0, qb = 0.0;
+    dbl4 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = dbl4{0.0, 0.0, 0.0, 0.0};
+    for (int k0 = 0; k0 < D; k0 += HE_KC) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int k = k0 + lk + u;
+            const double av = (a_ok && k < D) ? (double)arow[k] : 0.0;
+            const double bv = (b_ok && k < D) ? (double)brow[k] : 0.0;
+            qa += av * av;
+            qb += bv * bv;
+            As[lr * HE_LD + lk + u] = av;
+            Bs[lr * HE_LD + lk + u] = bv;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int ks = 0; ks < HE_KC; ks += 4) {
+            const int kk = ks + (lane >> 4);
+            double af[2], bf[2];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) af[i] = As[(wr + 16 * i + (lane & 15)) * HE_LD + kk];
+#pragma unroll
+            for (int j = 0; j < 2; ++j) bf[j] = Bs[(wc + 16 * j + (lane & 15)) * HE_LD + kk];
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[i], bf[j], acc[i][j], 0, 0, 0);
+        }
+        __syncthreads();
+    }
+    // row norms (4 threads per row)
+    qa += __shfl_xor(qa, 1);
+    qa += __shfl_xor(qa, 2);
+    qb += __shfl_xor(qb, 1);
+    qb += __shfl_xor(qb, 2);
+    if ((t & 3) == 0) {
+        nA[lr] = qa;
+        nB[lr] = qb;
+    }
+    if (t < HE_TILE) {
+        const int p = r0 + t;
+        if (p < n_hi) {
+            const double *dr = a.det_in + ((long long)a.det_off[s] + a.hi_row[db + p]) * 6;
+            HsDetCol dc;
+            for (int k = 0; k < 4; ++k) dc.box[k] = dr[k];
+            dc.score = dr[4];
+            dcol[t] = dc;
+        }
+    } else if (t < 2 * HE_TILE) {
+        const int j = c0 + t - HE_TILE;
+        if (j < n_trk) {   // 20 doubles, copied as such (a struct copy goes through scratch)
+            const double *src = reinterpret_cast<const double *>(a.col + tb + j);
+            double *dst = reinterpret_cast<double *>(tcol + (t - HE_TILE));
+#pragma unroll
+            for (int k = 0; k < (int)(sizeof(HsCol) / 8); ++k) dst[k] = src[k];
+        }
+    }
+    __syncthreads();
+    // epilogue: cosine distance, asso function, corner angle costs, fused cost
+    bool giou_bad = false;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr) {
+                const int lrow = wr + 16 * i + (lane >> 4) + 4 * rr;
+                const int lcol = wc + 16 * j + (lane & 15);
+                const int p = r0 + lrow, q = c0 + lcol;
+                if (p >= n_hi || q >= n_trk) continue;
+                const double uv = acc[i][j][rr];
+                const double emb = np_max(0.0, 1.0 - uv / sqrt(nA[lrow] * nB[lcol]));
+                const HsDetCol &dc = dcol[lrow];
+                const HsCol &tc = tcol[lcol];
+                const Box db_{dc.box[0], dc.box[1], dc.box[2], dc.box[3]};
+                const Box tb_{tc.box[0], tc.box[1], tc.box[2], tc.box[3]};
+                const double v = asso_of(a.asso, db_, tb_, 0.0, 0.0);
+                if (a.asso == 1 && v != v) giou_bad = true;
+                double angle = 0.0;
+                for (int cc = 0; cc < 4; ++cc) {
+                    const double dx = dc.box[hs_cx(cc)] - tc.kobs[hs_cx(cc)];
+                    const double dy = dc.box[hs_cy(cc)] - tc.kobs[hs_cy(cc)];
+                    const double nrm = sqrt(dx * dx + dy * dy) + 1e-6;
+                    const double X = dx / nrm, Y = dy / nrm;
+                    double cs = tc.vel[2 * cc + 1] * X + tc.vel[2 * cc] * Y;
+                    cs = np_min(np_max(cs, -1.0), 1.0);
+                    const double ang = (M_PI / 2.0 - fabs(acos(cs))) / M_PI;
+                    const double term = ((tc.valid * ang) * a.inertia) * dc.score;
+                    angle = cc == 0 ? term : angle + term;
+                }
+                double cost = -(v + angle);
+                cost = cost + HS_EG_WEIGHT * emb;
+                cost = cost + 0.0;                            // + 0 * long-term cost
+                const long long o = mb + (long long)p * n_trk + q;
+                a.emat[o] = emb;
+                a.cost[o] = cost;
+            }
+    if (giou_bad) atomicOr(&a.cnt[s].err, ERR_GIOU);
+}
+
+// -------------------------------------------------------------------------------- k_hs_assoc
+__global__ __launch_bounds__(OC_T) void k_hs_assoc(HsArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    __shared__ OcShared sh;
+    const int s = blockIdx.x, t = threadIdx.x, nt = blockDim.x;
+    HsCounters *c = a.cnt + s;
+    const long long tb = (long long)s * a.CAP, db = (long long)s * a.MAXD, mb = hs_mb(a, s);
+    const long long ub = (long long)s * (a.MAXD + a.CAP);
+    unsigned char *gws = a.lap_ws + s * a.lap_ws_stride;
+    const double *din = a.det_in + (long long)a.det_off[s] * 6;
+    const int frame = c->frame + 1;
+    int n_trk = c->n_trk;
+    const int n_hi = c->n_high;
+    const int dt = a.delta_t;
+    int *list = a.list + tb;
+    const HsCol *col = a.col + tb;
+    double *cost = a.cost + mb, *emat = a.emat + mb;
+    int *udet = a.udet + ub, *utrk = a.utrk + ub;
+    int n_ud = 0, n_ut = 0;
+    int n_corr = 0;
+    // dets[p] (x1, y1, x2, y2, score) of kept detection p: input row hi_row[p]
+    auto hrow = [&](int p) { return din + (long long)a.hi_row[db + p] * 6; };
+    // ---- first round (association.py:495-581)
+    if (n_trk == 0 || n_hi == 0) {
+        for (int i = t; i < n_hi; i += nt) udet[i] = i;
+        for (int j = t; j < n_trk; j += nt) utrk[j] = j;
+        n_ud = n_hi;
+        n_ut = n_trk;
+        if (t == 0) c->lap_calls = 0;
+        block_sync();
+    } else {
+        block_sync();
+        padded_lap(LapMat{cost, n_hi, n_trk, false}, a.rmatch + db, lds, gws, &c->err);
+        if (t == 0) c->lap_calls = 1;
+        for (int j = t; j < n_trk; j += nt) a.cmatched[tb + j] = 0;
+        block_sync();
+        for (int i = t; i < n_hi; i += nt) {
+            const int k = a.rmatch[db + i];
+            if (k >= 0) a.cmatched[tb + k] = 1;
+        }
+        block_sync();
+        n_ud = block_compact(n_hi, sh.wsum, [&](int i) { return a.rmatch[db + i] < 0; },
+                             [&](int i, int pos) { udet[pos] = i; });
+        n_ut = block_compact(n_trk, sh.wsum, [&](int j) { return a.cmatched[tb + j] == 0; },
+                             [&](int j, int pos) { utrk[pos] = j; });
+        // long-term correction (:557-567): emb > 0.4 and iou - |kalman score - score| < thr
+        auto corrected = [&](int i) {
+            const int k = a.rmatch[db + i];
+            if (k < 0) return false;
+            const double e = emat[(long long)i * n_trk + k];
+            if (!(e > HS_CORR_THRESH)) return false;
+            const double *dr = hrow(i);
+            const HsCol &q = col[k];
+            const double v = asso_of(a.asso, box5(dr), Box{q.box[0], q.box[1], q.box[2], q.box[3]},
+                                     0.0, 0.0);
+            const double sd = fabs(q.kscore - dr[4]);
+            return (v - sd) < a.thr;
+        };
+        n_corr = block_compact(n_hi, sh.wsum, corrected, [&](int i, int pos) {
+            udet[n_ud + pos] = i;
+            utrk[n_ut + pos] = a.rmatch[db + i];
+        });
+        for (int i = t; i < n_hi; i += nt) {
+            const int k = a.rmatch[db + i];
+            if (k >= 0 && !corrected(i)) a.upd[tb + k] = i;
+        }
+        n_ud += n_corr;
+        n_ut += n_corr;
+        block_sync();
+    }
+    // first-round updates with features (:462-464); feature jobs for k_hs_ema
+    const long long eb = (long long)s * (a.CAP + a.MAXD);
+    const int n_upd = block_compact(n_trk, sh.wsum, [&](int j) { return a.upd[tb + j] >= 0; },
+                                    [&](int j, int pos) {
+                                        a.ema_slot[eb + pos] = list[j];
+                                        a.ema_row[eb + pos] = a.upd[tb + j];
+                                    });
+    for (int j = t; j < n_trk; j += nt) {
+        const int p = a.upd[tb + j];
+        if (p >= 0) {
+            // cls / det_ind from dets0 row p of the input (filtered position, :464)
+            hs_update(a.rec[tb + list[j]], hrow(p), din[(long long)p * 6 + 5],
+                      din[(long long)p * 6 + 4], dt);
+        }
+    }
+    block_sync();
+    // ---- OCR round (:512-542): asso_func(left dets, last observations), no feature update
+    if (n_ud > 0 && n_ut > 0) {
+        const long long nm = (long long)n_ud * n_ut;
+        double mx = -INFINITY;
+        double *mat = emat;   // the embedding costs are no longer needed
+        for (long long q = t; q < nm; q += nt) {
+            const int p = (int)(q / n_ut), k = (int)(q % n_ut);
+            const Box lb = box5(a.clast + (tb + utrk[k]) * 5);
+            const double v = asso_of(a.asso, box5(hrow(udet[p])), lb, 0.0, 0.0);
+            if (a.asso == 1 && v != v) atomicOr(&c->err, ERR_GIOU);
+            mat[q] = v;
+            mx = np_max(mx, v);
+        }
+        block_sync();
+        mx = block_max(mx, sh);
+        if (mx > a.thr) {
+            padded_lap(LapMat{mat, n_ud, n_ut, true}, a.rmatch + db, lds, gws, &c->err);
+            for (int i = t; i < n_hi; i += nt) a.tmp[ub + i] = 0;
+            for (int j = t; j < n_trk; j += nt) a.nan_flag[tb + j] = 0;
+            block_sync();
+            for (int p = t; p < n_ud; p += nt) a.tmp[ub + udet[p]] = 1;
+            for (int k = t; k < n_ut; k += nt) a.nan_flag[tb + utrk[k]] = 1;
+            block_sync();
+            for (int p = t; p < n_ud; p += nt) {
+                const int k = a.rmatch[db + p];
+                if (k >= 0 && !(mat[(long long)p * n_ut + k] < a.thr)) {
+                    const int di = udet[p], tj = utrk[k];
+                    hs_update(a.rec[tb + list[tj]], hrow(di), din[(long long)di * 6 + 5],
+                              din[(long long)di * 6 + 4], dt);
+                    a.tmp[ub + di] = 0;
+                    a.nan_flag[tb + tj] = 0;
+                }
+            }
+            block_sync();
+            n_ud = block_compact(n_hi, sh.wsum, [&](int i) { return a.tmp[ub + i] == 1; },
+                                 [&](int i, int pos) { udet[pos] = i; });
+            n_ut = block_compact(n_trk, sh.wsum, [&](int j) { return a.nan_flag[tb + j] == 1; },
+                                 [&](int j, int pos) { utrk[pos] = j; });
+            for (int j = t; j < n_trk; j += nt) a.nan_flag[tb + j] = 0;
+            if (t == 0) c->lap_calls += 1;
+            block_sync();
+        }
+    }
+    // ---- misses (:544-545)
+    for (int k = t; k < n_ut; k += nt) hs_update(a.rec[tb + list[utrk[k]]], nullptr, 0.0, 0.0, dt);
+    block_sync();
+    // ---- births in unmatched-list order (:548-550)
+    int n_free = c->n_free;
+    int n_b = n_ud;
+    if (n_b > n_free) {
+        if (t == 0) atomicOr(&c->err, ERR_TRACK_CAPACITY);
+        n_b = n_free;
+    }
+    const long long next_id = c->next_id;
+    for (int b = t; b < n_b; b += nt) {
+        const int slot = a.free_list[tb + n_free - 1 - b];
+        const int p = udet[b];
+        hs_birth(a.rec[tb + slot], hrow(p), din[(long long)p * 6 + 5], din[(long long)p * 6 + 4],
+                 next_id + b);
+        list[n_trk + b] = slot;
+        a.ema_slot[eb + n_upd + b] = slot;
+        a.ema_row[eb + n_upd + b] = ~p;
+    }
+    n_free -= n_b;
+    n_trk += n_b;
+    block_sync();
+    // ---- outputs in reversed tracker order, then removal (:551-570); ids + 1 (:563)
+    double *out = a.out + tb * 8;
+    const int n_out = block_compact(
+        n_trk, sh.wsum,
+        [&](int q) {
+            const HsTrack &r = a.rec[tb + list[n_trk - 1 - q]];
+            return r.tsu < 1 && (r.hit_streak >= a.min_hits || frame <= a.min_hits);
+        },
+        [&](int q, int pos) {
+            const HsTrack &r = a.rec[tb + list[n_trk - 1 - q]];
+            double b[4];
+            if (np_sum5(r.last_obs) < 0) hs_x_to_bbox(r.kf.x, b);
+            else for (int k = 0; k < 4; ++k) b[k] = r.last_obs[k];
+            double *o = out + (long long)pos * 8;
+            o[0] = b[0];
+            o[1] = b[1];
+            o[2] = b[2];
+            o[3] = b[3];
+            o[4] = (double)(r.id + 1);
+            o[5] = r.conf;
+            o[6] = r.cls;
+            o[7] = r.det_ind;
+        });
+    const int n_dead = block_compact(n_trk, sh.wsum,
+                                     [&](int j) { return a.rec[tb + list[j]].tsu > a.max_age; },
+                                     [&](int j, int pos) { a.tmp[ub + pos] = list[j]; });
+    for (int k = t; k < n_dead; k += nt) a.free_list[tb + n_free + k] = a.tmp[ub + k];
+    block_sync();
+    const int n_live = block_compact(n_trk, sh.wsum,
+                                     [&](int j) { return a.rec[tb + list[j]].tsu <= a.max_age; },
+                                     [&](int j, int pos) { a.tmp[ub + pos] = list[j]; });
+    block_sync();
+    for (int j = t; j < n_live; j += nt) list[j] = a.tmp[ub + j];
+    if (t == 0) {
+        c->frame = frame;
+        c->n_trk = n_live;
+        c->n_free = n_free + n_dead;
+        c->n_out = n_out;
+        c->n_births = n_b;
+        c->n_ema = n_upd + n_b;
+        c->corrections = n_corr;
+        c->next_id = next_id + n_b;
+        if (a.out_counts) a.out_counts[s] = n_out;
+    }
+}
+
+// ---------------------------------------------------------------------------------- k_hs_ema
+// update_features (hybridsort.py:197-214), float32 as the reference: f = e / |e| (in place on the
+// detection's row), smooth = 0.8 smooth + 0.2 f, smooth /= |smooth|; a birth's smooth_feat is its
+// row normalised twice (feat is smooth_feat).  Norms: np.linalg.norm of a float32 row, the sum of
+// squares accumulated in float64 here (OpenBLAS sdot sums in float32 lanes, so a norm may differ
+// from the reference's in its last bit; the tests compare features with a tolerance).  One wave
+// per job.
+__device__ __forceinline__ float hs_f32_norm(double sumsq) { return sqrtf((float)sumsq); }
+
+__global__ __launch_bounds__(256) void k_hs_ema(HsArgs a) {
+    const int s = blockIdx.y, lane = lane_id();
+    const HsCounters *c = a.cnt + s;
+    const int job = blockIdx.x * 4 + threadIdx.x / WAVE;
+    if (job >= c->n_ema) return;
+    const long long tb = (long long)s * a.CAP, db = (long long)s * a.MAXD;
+    const long long eb = (long long)s * (a.CAP + a.MAXD);
+    const int slot = a.ema_slot[eb + job], code = a.ema_row[eb + job];
+    const int p = code >= 0 ? code : ~code;
+    const float *e = a.det_feat + ((long long)a.det_off[s] + a.hi_row[db + p]) * a.D;
+    float *sm = a.feat + (tb + slot) * a.D;
+    double q = 0.0;
+    for (int k = lane; k < a.D; k += WAVE) q += (double)e[k] * (double)e[k];
+    const float n1 = hs_f32_norm(wave_reduce(RED_SUM, q));
+    q = 0.0;
+    if (code < 0) {
+        for (int k = lane; k < a.D; k += WAVE) {
+            const float f = e[k] / n1;
+            q += (double)f * (double)f;
+        }
+        const float n2 = hs_f32_norm(wave_reduce(RED_SUM, q));
+        for (int k = lane; k < a.D; k += WAVE) sm[k] = (e[k] / n1) / n2;
+        return;
+    }
+    for (int k = lane; k < a.D; k += WAVE) {
+        const float f = e[k] / n1;
+        const float v = 0.8f * sm[k] + 0.2f * f;
+        sm[k] = v;
+        q += (double)v * (double)v;
+    }
+    const float nrm = hs_f32_norm(wave_reduce(RED_SUM, q));
+    for (int k = lane; k < a.D; k += WAVE) sm[k] = sm[k] / nrm;
+}
+
+// KalmanBoxTracker KAT: one thread per track, steps of predict, update(box | None)
+__global__ void k_kf9_run(int n, int steps, const double *b0, const double *b, double *x_out,
+                          double *P_out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    HsTrack r;
+    hs_birth(r, b0 + 5LL * i, 0.0, 0.0, 0);
+    for (int st = 0; st < steps; ++st) {
+        double bb[4], ks, ss;
+        hs_predict(r, bb, ks, ss);
+        const double *z = b + ((long long)st * n + i) * 5;
+        hs_update(r, z[0] != z[0] ? nullptr : z, 0.0, 0.0, 3);
+    }
+    for (int k = 0; k < 9; ++k) x_out[9LL * i + k] = r.kf.x[k];
+    double *M = P_out + 81LL * i;
+    for (int k = 0; k < 81; ++k) M[k] = 0.0;
+    for (int g = 0; g < 4; ++g) {
+        M[g * 9 + g] = r.kf.p[4 * g];
+        M[g * 9 + g + 5] = r.kf.p[4 * g + 1];
+        M[(g + 5) * 9 + g] = r.kf.p[4 * g + 2];
+        M[(g + 5) * 9 + g + 5] = r.kf.p[4 * g + 3];
+    }
+    M[4 * 9 + 4] = r.kf.p[16];
+}
+
+__global__ void k_hs_reset(HsArgs a) {
+    const int s = blockIdx.x;
+    const long long tb = (long long)s * a.CAP;
+    for (int i = threadIdx.x; i < a.CAP; i += blockDim.x) a.free_list[tb + i] = a.CAP - 1 - i;
+    if (threadIdx.x == 0) {
+        HsCounters z;
+        memset(&z, 0, sizeof(z));
+        z.n_free = a.CAP;
+        z.next_id = 0;                         // KalmanBoxTracker.count = 0 (:361)
+        a.cnt[s] = z;
+    }
+}
+
+}  // namespace
+}  // namespace yta
+
+// ================================================================================== host engine
+using namespace yta;
+
+struct yta_hybridsort {
+    int device = 0, S = 0, CAP = 0, MAXD = 0, D = 0;
+    yta_hybridsort_params prm{};
+    hipStream_t stream = nullptr;
+    std::vector<void *> allocs;
+    HsArgs a{};
+    double *h_dets = nullptr, *d_det_in = nullptr;
+    long long det_cap = 0;
+    float *h_feat = nullptr, *d_feat = nullptr;
+    long long feat_cap = 0;
+    int *h_off = nullptr, *d_off = nullptr;
+    HsCounters *h_cnt = nullptr;
+    size_t lds = 0;
+};
+
+namespace {
+
+template <typename T>
+int hs_dalloc(yta_hybridsort *e, T **p, long long n) {
+    void *q = nullptr;
+    if (n <= 0) n = 1;
+    hipError_t err = hipMalloc(&q, sizeof(T) * (size_t)n);
+    if (err != hipSuccess) {
+        set_error("hipMalloc(%lld bytes) failed: %s", (long long)(sizeof(T) * n),
+                  hipGetErrorString(err));
+        return YTA_ERR_NOMEM;
+    }
+    e->allocs.push_back(q);
+    *p = static_cast<T *>(q);
+    return YTA_OK;
+}
+
+#define HSALLOC(ptr, n)                      \
+    do {                                     \
+        int _rc = hs_dalloc(e, &(ptr), (n)); \
+        if (_rc) return _rc;                 \
+    } while (0)
+
+int hs_alloc(yta_hybridsort *e) {
+    const long long S = e->S, CAP = e->CAP, MAXD = e->MAXD, D = e->D;
+    HsArgs &a = e->a;
+    const yta_hybridsort_params &p = e->prm;
+    a.S = e->S;
+    a.CAP = e->CAP;
+    a.MAXD = e->MAXD;
+    a.D = e->D;
+    a.det_thresh = p.det_thresh;
+    a.thr = p.iou_threshold;
+    a.inertia = p.inertia;
+    a.max_age = p.max_age;
+    a.min_hits = p.min_hits;
+    a.delta_t = p.delta_t;
+    a.asso = p.asso_func;
+    HSALLOC(a.rec, S * CAP);
+    HSALLOC(a.feat, S * CAP * D);
+    HSALLOC(a.list, S * CAP);
+    HSALLOC(a.free_list, S * CAP);
+    HSALLOC(a.cnt, S);
+    HSALLOC(a.hi_row, S * MAXD);
+    HSALLOC(a.col, S * CAP);
+    HSALLOC(a.clast, S * CAP * 5);
+    HSALLOC(a.nan_flag, S * CAP);
+    HSALLOC(a.cslot, S * CAP);
+    // the cost matrix doubles as the column-record scratch of k_hs_pre (CAP records of 160 B)
+    const long long mat = std::max<long long>(MAXD, (long long)sizeof(HsCol) / 8) * CAP;
+    HSALLOC(a.cost, S * mat);
+    HSALLOC(a.emat, S * mat);
+    HSALLOC(a.rmatch, S * MAXD);
+    HSALLOC(a.cmatched, S * CAP);
+    HSALLOC(a.udet, S * (MAXD + CAP));
+    HSALLOC(a.utrk, S * (MAXD + CAP));
+    HSALLOC(a.tmp, S * (MAXD + CAP));
+    HSALLOC(a.upd, S * CAP);
+    HSALLOC(a.ema_slot, S * (MAXD + CAP));
+    HSALLOC(a.ema_row, S * (MAXD + CAP));
+    HSALLOC(a.out, S * CAP * 8);
+    const long long n = std::max(CAP, MAXD);
+    a.lap_ws_stride = n > OC_LDS_LAP_N ? ((dense_lap_ws_bytes(n) + 255) & ~255LL) : 256;
+    HSALLOC(a.lap_ws, S * a.lap_ws_stride);
+    e->lds = (size_t)dense_lap_ws_bytes(std::min<long long>(n, OC_LDS_LAP_N));
+    HSALLOC(e->d_off, S + 1);
+    YTA_HIP(hipHostMalloc((void **)&e->h_off, sizeof(int) * (S + 1), hipHostMallocDefault));
+    YTA_HIP(hipHostMalloc((void **)&e->h_cnt, sizeof(HsCounters) * S, hipHostMallocDefault));
+    YTA_HIP(hipFuncSetAttribute((const void *)k_hs_assoc,
+                                hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)dense_lap_ws_bytes(OC_LDS_LAP_N)));
+    return YTA_OK;
+}
+
+void hs_release(yta_hybridsort *e) {
+    for (void *p : e->allocs) (void)hipFree(p);
+    e->allocs.clear();
+    if (e->h_off) (void)hipHostFree(e->h_off);
+    if (e->h_cnt) (void)hipHostFree(e->h_cnt);
+    e->h_off = nullptr;
+    e->h_cnt = nullptr;
+}
+
+int hs_launch(yta_hybridsort *e, const double *d_dets, const int *d_off, const float *d_feat,
+              double *out, int *out_counts) {
+    HsArgs &a = e->a;
+    a.det_in = d_dets;
+    a.det_off = d_off;
+    a.det_feat = d_feat;
+    a.out = out;
+    a.out_counts = out_counts;
+    hipLaunchKernelGGL(k_hs_pre, dim3(a.S), dim3(OC_T), 0, e->stream, a);
+    YTA_HIP(hipGetLastError());
+    const dim3 ge((a.CAP + HE_TILE - 1) / HE_TILE, (a.MAXD + HE_TILE - 1) / HE_TILE, a.S);
+    hipLaunchKernelGGL(k_hs_emb, ge, dim3(256), 0, e->stream, a);
+    YTA_HIP(hipGetLastError());
+    hipLaunchKernelGGL(k_hs_assoc, dim3(a.S), dim3(OC_T), e->lds, e->stream, a);
+    YTA_HIP(hipGetLastError());
+    const dim3 gj((a.CAP + a.MAXD + 3) / 4, a.S);
+    hipLaunchKernelGGL(k_hs_ema, gj, dim3(256), 0, e->stream, a);
+    YTA_HIP(hipGetLastError());
+    return YTA_OK;
+}
+
+int hs_read_counters(yta_hybridsort *e) {
+    YTA_HIP(hipMemcpyAsync(e->h_cnt, e->a.cnt, sizeof(HsCounters) * e->S, hipMemcpyDeviceToHost,
+                           e->stream));
+    YTA_HIP(hipStreamSynchronize(e->stream));
+    return YTA_OK;
+}
+
+int hs_check_errors(yta_hybridsort *e) {
+    for (int s = 0; s < e->S; ++s) {
+        const int err = e->h_cnt[s].err;
+        if (err) {
+            set_error("stream %d: device error flags 0x%x (%s%s%s%s%s)", s, err,
+                      err & ERR_GIOU ? "giou enclosure not positive (iou.py:58 assert) " : "",
+                      err & ERR_SOLVER ? "assignment solver failure " : "",
+                      err & ERR_TRACK_CAPACITY ? "track capacity exceeded " : "",
+                      err & ERR_DET_CAPACITY ? "too many detections " : "",
+                      err & ERR_INF_ROW ? "infinite predicted box without NaN " : "");
+            return (err & (ERR_TRACK_CAPACITY | ERR_DET_CAPACITY)) ? YTA_ERR_CAPACITY
+                   : (err & (ERR_GIOU | ERR_INF_ROW))               ? YTA_ERR_INVALID
+                                                                   : YTA_ERR_HIP;
+        }
+    }
+    return YTA_OK;
+}
+
+int hs_reserve(yta_hybridsort *e, int cap, int maxd) {
+    if (cap <= e->CAP && maxd <= e->MAXD) return YTA_OK;
+    cap = std::max(cap, e->CAP);
+    maxd = std::max(maxd, e->MAXD);
+    YTA_HIP(hipStreamSynchronize(e->stream));
+    yta_hybridsort *n = new (std::nothrow) yta_hybridsort();
+    YTA_CHECK(n, YTA_ERR_NOMEM, "out of host memory");
+    n->device = e->device;
+    n->S = e->S;
+    n->CAP = cap;
+    n->MAXD = maxd;
+    n->D = e->D;
+    n->prm = e->prm;
+    n->stream = e->stream;
+    int rc = hs_alloc(n);
+    const size_t S = e->S, oc = e->CAP, nc = cap, Dd = e->D;
+    auto copy2d = [&](void *dst, size_t dp, const void *src, size_t sp, size_t w) -> int {
+        YTA_HIP(hipMemcpy2DAsync(dst, dp, src, sp, w, S, hipMemcpyDeviceToDevice, e->stream));
+        return YTA_OK;
+    };
+    if (!rc) rc = copy2d(n->a.rec, nc * sizeof(HsTrack), e->a.rec, oc * sizeof(HsTrack),
+                         oc * sizeof(HsTrack));
+    if (!rc) rc = copy2d(n->a.feat, nc * Dd * 4, e->a.feat, oc * Dd * 4, oc * Dd * 4);
+    if (!rc) rc = copy2d(n->a.list, nc * 4, e->a.list, oc * 4, oc * 4);
+    if (!rc) {
+        std::vector<int> fl(nc * S), old(oc * S);
+        std::vector<HsCounters> cnt(S);
+        hipError_t he = hipMemcpyAsync(old.data(), e->a.free_list, sizeof(int) * oc * S,
+                                       hipMemcpyDeviceToHost, e->stream);
+        if (he == hipSuccess)
+            he = hipMemcpyAsync(cnt.data(), e->a.cnt, sizeof(HsCounters) * S,
+                                hipMemcpyDeviceToHost, e->stream);
+        if (he == hipSuccess) he = hipStreamSynchronize(e->stream);
+        if (he == hipSuccess) {
+            for (size_t s = 0; s < S; ++s) {
+                int k = 0;
+                for (int q = (int)nc - 1; q >= (int)oc; --q) fl[s * nc + k++] = q;
+                for (int q = 0; q < cnt[s].n_free; ++q) fl[s * nc + k++] = old[s * oc + q];
+                cnt[s].n_free = k;
+            }
+            he = hipMemcpy(n->a.free_list, fl.data(), sizeof(int) * nc * S, hipMemcpyHostToDevice);
+            if (he == hipSuccess)
+                he = hipMemcpy(n->a.cnt, cnt.data(), sizeof(HsCounters) * S,
+                               hipMemcpyHostToDevice);
+        }
+        if (he != hipSuccess) {
+            set_error("reserve: %s", hipGetErrorString(he));
+            rc = YTA_ERR_HIP;
+        }
+    }
+    if (rc) {
+        n->stream = nullptr;
+        hs_release(n);
+        delete n;
+        return rc;
+    }
+    memcpy(n->h_cnt, e->h_cnt, sizeof(HsCounters) * S);
+    hs_release(e);
+    e->CAP = n->CAP;
+    e->MAXD = n->MAXD;
+    e->allocs.swap(n->allocs);
+    e->a = n->a;
+    e->lds = n->lds;
+    e->h_off = n->h_off;
+    e->h_cnt = n->h_cnt;
+    e->d_off = n->d_off;
+    n->h_off = nullptr;
+    n->h_cnt = nullptr;
+    n->stream = nullptr;
+    delete n;
+    return YTA_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int yta_hybridsort_create(int device, int n_streams, int track_capacity, int max_dets,
+                          int feat_dim, const yta_hybridsort_params *params,
+                          yta_hybridsort **engine) {
+    YTA_CHECK(engine && params, YTA_ERR_INVALID, "null engine/params");
+    YTA_CHECK(n_streams > 0 && track_capacity > 0 && max_dets > 0, YTA_ERR_INVALID,
+              "n_streams, track_capacity and max_dets must be positive");
+    YTA_CHECK(params->delta_t >= 0 && params->delta_t <= OC_DT_MAX, YTA_ERR_INVALID,
+              "delta_t must be in [0, %d]", OC_DT_MAX);
+    YTA_CHECK(params->asso_func >= 0 && params->asso_func <= 3, YTA_ERR_INVALID,
+              "asso_func must be 0..3 (iou, giou, diou, ciou): HybridSORT calls it without the "
+              "image size centroid needs (hybridsort.py:516)");
+    YTA_CHECK(feat_dim > 0, YTA_ERR_INVALID, "HybridSORT needs embeddings (feat_dim > 0)");
+    *engine = nullptr;
+    int rc = select_device(device);
+    if (rc) return rc;
+    yta_hybridsort *e = new (std::nothrow) yta_hybridsort();
+    YTA_CHECK(e, YTA_ERR_NOMEM, "out of host memory");
+    e->device = device;
+    e->S = n_streams;
+    e->CAP = track_capacity;
+    e->MAXD = max_dets;
+    e->D = feat_dim;
+    e->prm = *params;
+    hipError_t he = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
+    if (he != hipSuccess) {
+        set_error("hipStreamCreate: %s", hipGetErrorString(he));
+        delete e;
+        return YTA_ERR_HIP;
+    }
+    rc = hs_alloc(e);
+    if (!rc) rc = yta_hybridsort_reset(e);
+    if (rc) {
+        yta_hybridsort_destroy(e);
+        return rc;
+    }
+    *engine = e;
+    return YTA_OK;
+}
+
+int yta_hybridsort_destroy(yta_hybridsort *e) {
+    if (!e) return YTA_OK;
+    (void)hipSetDevice(e->device);
+    if (e->stream) (void)hipStreamSynchronize(e->stream);
+    hs_release(e);
+    if (e->h_dets) (void)hipHostFree(e->h_dets);
+    if (e->d_det_in) (void)hipFree(e->d_det_in);
+    if (e->h_feat) (void)hipHostFree(e->h_feat);
+    if (e->d_feat) (void)hipFree(e->d_feat);
+    if (e->stream) (void)hipStreamDestroy(e->stream);
+    delete e;
+    return YTA_OK;
+}
+
+int yta_hybridsort_reset(yta_hybridsort *e) {
+    YTA_CHECK(e, YTA_ERR_INVALID, "null engine");
+    YTA_HIP(hipSetDevice(e->device));
+    hipLaunchKernelGGL(k_hs_reset, dim3(e->S), dim3(256), 0, e->stream, e->a);
+    YTA_HIP(hipGetLastError());
+    YTA_HIP(hipStreamSynchronize(e->stream));
+    memset(e->h_cnt, 0, sizeof(HsCounters) * e->S);
+    return YTA_OK;
+}
+
+int yta_hybridsort_capacity(yta_hybridsort *e, int *track_capacity, int *max_dets) {
+    YTA_CHECK(e && track_capacity && max_dets, YTA_ERR_INVALID, "null argument");
+    *track_capacity = e->CAP;
+    *max_dets = e->MAXD;
+    return YTA_OK;
+}
+
+int yta_hybridsort_update(yta_hybridsort *e, const double *dets, const int *det_offsets,
+                          const float *feats, long long *next_id, double *out, int out_capacity,
+                          int *out_offsets) {
+    YTA_CHECK(e && det_offsets && out_offsets, YTA_ERR_INVALID, "null argument");
+    YTA_HIP(hipSetDevice(e->device));
+    const int S = e->S;
+    YTA_CHECK(det_offsets[0] == 0, YTA_ERR_INVALID, "det_offsets[0] must be 0");
+    int need_d = e->MAXD, need_c = e->CAP;
+    for (int s = 0; s < S; ++s) {
+        const int m = det_offsets[s + 1] - det_offsets[s];
+        YTA_CHECK(m >= 0, YTA_ERR_INVALID, "det_offsets must be non-decreasing");
+        need_d = std::max(need_d, m);
+        need_c = std::max(need_c, e->h_cnt[s].n_trk + m);
+    }
+    if (need_d > e->MAXD || need_c > e->CAP) {
+        const int rc = hs_reserve(e, need_c > e->CAP ? std::max(need_c, 2 * e->CAP) : e->CAP,
+                                  need_d > e->MAXD ? std::max(need_d, 2 * e->MAXD) : e->MAXD);
+        if (rc) return rc;
+    }
+    const long long total = det_offsets[S];
+    YTA_CHECK(total == 0 || (dets && feats), YTA_ERR_INVALID, "null dets / feats");
+    const int D = e->D;
+    if (total > e->det_cap) {
+        if (e->d_det_in) (void)hipFree(e->d_det_in);
+        if (e->h_dets) (void)hipHostFree(e->h_dets);
+        if (e->d_feat) (void)hipFree(e->d_feat);
+        if (e->h_feat) (void)hipHostFree(e->h_feat);
+        e->d_det_in = nullptr;
+        e->h_dets = nullptr;
+        e->d_feat = nullptr;
+        e->h_feat = nullptr;
+        e->det_cap = 0;
+        const long long cap = std::max<long long>(2 * total, 1024);
+        YTA_HIP(hipMalloc((void **)&e->d_det_in, sizeof(double) * 6 * cap));
+        YTA_HIP(hipHostMalloc((void **)&e->h_dets, sizeof(double) * 6 * cap, hipHostMallocDefault));
+        YTA_HIP(hipMalloc((void **)&e->d_feat, sizeof(float) * D * cap));
+        YTA_HIP(hipHostMalloc((void **)&e->h_feat, sizeof(float) * D * cap, hipHostMallocDefault));
+        e->det_cap = cap;
+    }
+    if (total) {
+        memcpy(e->h_dets, dets, sizeof(double) * 6 * total);
+        YTA_HIP(hipMemcpyAsync(e->d_det_in, e->h_dets, sizeof(double) * 6 * total,
+                               hipMemcpyHostToDevice, e->stream));
+        memcpy(e->h_feat, feats, sizeof(float) * D * total);
+        YTA_HIP(hipMemcpyAsync(e->d_feat, e->h_feat, sizeof(float) * D * total,
+                               hipMemcpyHostToDevice, e->stream));
+    }
+    memcpy(e->h_off, det_offsets, sizeof(int) * (S + 1));
+    YTA_HIP(hipMemcpyAsync(e->d_off, e->h_off, sizeof(int) * (S + 1), hipMemcpyHostToDevice,
+                           e->stream));
+    if (next_id) {
+        for (int s = 0; s < S; ++s) e->h_cnt[s].next_id = next_id[s];
+        YTA_HIP(hipMemcpy2DAsync(&e->a.cnt[0].next_id, sizeof(HsCounters), &e->h_cnt[0].next_id,
+                                 sizeof(HsCounters), sizeof(long long), S, hipMemcpyHostToDevice,
+                                 e->stream));
+    }
+    int rc = hs_launch(e, e->d_det_in, e->d_off, e->d_feat, e->a.out, nullptr);
+    if (rc) return rc;
+    rc = hs_read_counters(e);
+    if (rc) return rc;
+    rc = hs_check_errors(e);
+    if (rc) return rc;
+    long long rows = 0;
+    out_offsets[0] = 0;
+    for (int s = 0; s < S; ++s) {
+        rows += e->h_cnt[s].n_out;
+        out_offsets[s + 1] = (int)rows;
+    }
+    YTA_CHECK(rows <= out_capacity, YTA_ERR_CAPACITY, "output needs %lld rows > capacity %d", rows,
+              out_capacity);
+    YTA_CHECK(rows == 0 || out, YTA_ERR_INVALID, "null out");
+    for (int s = 0; s < S; ++s) {
+        const int n = e->h_cnt[s].n_out;
+        if (n)
+            YTA_HIP(hipMemcpyAsync(out + (long long)out_offsets[s] * 8,
+                                   e->a.out + (long long)s * e->CAP * 8, sizeof(double) * 8 * n,
+                                   hipMemcpyDeviceToHost, e->stream));
+    }
+    YTA_HIP(hipStreamSynchronize(e->stream));
+    if (next_id)
+        for (int s = 0; s < S; ++s) next_id[s] = e->h_cnt[s].next_id;
+    return YTA_OK;
+}
+
+int yta_hybridsort_update_device(yta_hybridsort *e, const double *d_dets, const int *d_det_offsets,
+                                 const float *d_feats, double *d_out, int *d_out_counts) {
+    YTA_CHECK(e && d_det_offsets && d_out && d_feats, YTA_ERR_INVALID, "null argument");
+    return hs_launch(e, d_dets, d_det_offsets, d_feats, d_out, d_out_counts);
+}
+
+int yta_hybridsort_sync(yta_hybridsort *e) {
+    YTA_CHECK(e, YTA_ERR_INVALID, "null engine");
+    const int rc = hs_read_counters(e);
+    if (rc) return rc;
+    return hs_check_errors(e);
+}
+
+int yta_hybridsort_get_state(yta_hybridsort *e, int stream, int *n_tracks, long long *ints,
+                             double *dbl, double *x, double *P, float *feat) {
+    YTA_CHECK(e && n_tracks && ints && dbl && x && P, YTA_ERR_INVALID, "null argument");
+    YTA_CHECK(stream >= 0 && stream < e->S, YTA_ERR_INVALID, "bad stream %d", stream);
+    YTA_HIP(hipSetDevice(e->device));
+    const int rc = hs_read_counters(e);
+    if (rc) return rc;
+    const HsCounters c = e->h_cnt[stream];
+    const long long tb = (long long)stream * e->CAP;
+    std::vector<int> lst(c.n_trk);
+    std::vector<HsTrack> rec(e->CAP);
+    if (c.n_trk)
+        YTA_HIP(hipMemcpy(lst.data(), e->a.list + tb, sizeof(int) * c.n_trk, hipMemcpyDeviceToHost));
+    YTA_HIP(hipMemcpy(rec.data(), e->a.rec + tb, sizeof(HsTrack) * e->CAP, hipMemcpyDeviceToHost));
+    for (int i = 0; i < c.n_trk; ++i) {
+        const HsTrack &r = rec[lst[i]];
+        long long *ii = ints + 6LL * i;
+        ii[0] = r.id;
+        ii[1] = r.age;
+        ii[2] = r.hits;
+        ii[3] = r.hit_streak;
+        ii[4] = r.tsu;
+        ii[5] = (r.flags & OF_OBSERVED) ? 1 : 0;
+        double *dd = dbl + 3LL * i;
+        dd[0] = r.conf;
+        dd[1] = r.cls;
+        dd[2] = r.det_ind;
+        for (int k = 0; k < 9; ++k) x[9LL * i + k] = r.kf.x[k];
+        double *M = P + 81LL * i;
+        for (int k = 0; k < 81; ++k) M[k] = 0.0;
+        for (int g = 0; g < 4; ++g) {
+            M[g * 9 + g] = r.kf.p[4 * g];
+            M[g * 9 + g + 5] = r.kf.p[4 * g + 1];
+            M[(g + 5) * 9 + g] = r.kf.p[4 * g + 2];
+            M[(g + 5) * 9 + g + 5] = r.kf.p[4 * g + 3];
+        }
+        M[4 * 9 + 4] = r.kf.p[16];
+        if (feat)
+            YTA_HIP(hipMemcpy(feat + (long long)i * e->D, e->a.feat + (tb + lst[i]) * e->D,
+                              sizeof(float) * e->D, hipMemcpyDeviceToHost));
+    }
+    *n_tracks = c.n_trk;
+    return YTA_OK;
+}
+
+int yta_hybridsort_classes(yta_hybridsort *e, int stream, double *cls, int cap, int *n) {
+    YTA_CHECK(e && n && (cls || cap == 0), YTA_ERR_INVALID, "null argument");
+    YTA_CHECK(stream >= 0 && stream < e->S, YTA_ERR_INVALID, "bad stream %d", stream);
+    YTA_HIP(hipSetDevice(e->device));
+    const int rc = hs_read_counters(e);
+    if (rc) return rc;
+    const int nt = e->h_cnt[stream].n_trk;
+    YTA_CHECK(nt <= cap, YTA_ERR_CAPACITY, "%d trackers > capacity %d", nt, cap);
+    const long long tb = (long long)stream * e->CAP;
+    std::vector<int> lst(nt);
+    if (nt)
+        YTA_HIP(hipMemcpy(lst.data(), e->a.list + tb, sizeof(int) * nt, hipMemcpyDeviceToHost));
+    for (int i = 0; i < nt; ++i)
+        YTA_HIP(hipMemcpy(cls + i, (const char *)(e->a.rec + tb + lst[i]) + offsetof(HsTrack, cls),
+                          sizeof(double), hipMemcpyDeviceToHost));
+    *n = nt;
+    return YTA_OK;
+}
+
+int yta_hybridsort_stats(yta_hybridsort *e, long long *stats) {
+    YTA_CHECK(e && stats, YTA_ERR_INVALID, "null argument");
+    const int rc = hs_read_counters(e);
+    if (rc) return rc;
+    for (int k = 0; k < 8; ++k) stats[k] = 0;
+    for (int s = 0; s < e->S; ++s) {
+        const HsCounters &c = e->h_cnt[s];
+        const long long v[8] = {c.n_dets, c.n_high, c.n_trk, c.n_out, c.n_births, c.lap_calls,
+                                c.corrections, c.n_ema};
+        for (int k = 0; k < 8; ++k) stats[k] += v[k];
+    }
+    return YTA_OK;
+}
+
+int yta_kf9_run(int device, int n, int steps, const double *b0, const double *b, double *x_out,
+                double *P_out) {
+    YTA_CHECK(n > 0 && steps >= 0 && b0 && (b || steps == 0) && x_out && P_out, YTA_ERR_INVALID,
+              "bad arguments");
+    int rc = select_device(device);
+    if (rc) return rc;
+    double *d_b0 = nullptr, *d_b = nullptr, *d_x = nullptr, *d_P = nullptr;
+    const size_t nb = sizeof(double) * 5 * (size_t)n * std::max(steps, 1);
+    hipError_t he = hipMalloc((void **)&d_b0, sizeof(double) * 5 * n);
+    if (he == hipSuccess) he = hipMalloc((void **)&d_b, nb);
+    if (he == hipSuccess) he = hipMalloc((void **)&d_x, sizeof(double) * 9 * n);
+    if (he == hipSuccess) he = hipMalloc((void **)&d_P, sizeof(double) * 81 * n);
+    if (he == hipSuccess) he = hipMemcpy(d_b0, b0, sizeof(double) * 5 * n, hipMemcpyHostToDevice);
+    if (he == hipSuccess && steps)
+        he = hipMemcpy(d_b, b, sizeof(double) * 5 * (size_t)n * steps, hipMemcpyHostToDevice);
+    if (he == hipSuccess) {
+        hipLaunchKernelGGL(k_kf9_run, dim3((n + 63) / 64), dim3(64), 0, 0, n, steps, d_b0, d_b,
+                           d_x, d_P);
+        he = hipGetLastError();
+    }
+    if (he == hipSuccess) he = hipMemcpy(x_out, d_x, sizeof(double) * 9 * n, hipMemcpyDeviceToHost);
+    if (he == hipSuccess) he = hipMemcpy(P_out, d_P, sizeof(double) * 81 * n, hipMemcpyDeviceToHost);
+    (void)hipFree(d_b0);
+    (void)hipFree(d_b);
+    (void)hipFree(d_x);
+    (void)hipFree(d_P);
+    if (he != hipSuccess) {
+        set_error("yta_kf9_run: %s", hipGetErrorString(he));
+        return YTA_ERR_HIP;
+    }
+    return YTA_OK;
+}
+
+int yta_hybridsort_hip_stream(yta_hybridsort *e, void **stream) {
+    YTA_CHECK(e && stream, YTA_ERR_INVALID, "null argument");
+    *stream = (void *)e->stream;
+    return YTA_OK;
+}
+
+}  // extern "C"

@@ -48,7 +48,14 @@ def create_tracker(tracker_type, tracker_config, reid_weights, device, half, per
                           max_age=cfg.max_age, min_hits=cfg.min_hits,
                           iou_threshold=cfg.iou_thresh, delta_t=cfg.delta_t,
                           asso_func=cfg.asso_func, inertia=cfg.inertia, reid=reid)
-    if tracker_type in ("hybridsort", "strongsort"):
+    if tracker_type == "hybridsort":
+        from .trackers.hybridsort import HybridSORT
+        reid = reid_weights if hasattr(reid_weights, "get_features") else None
+        return HybridSORT(reid_weights, device, half, det_thresh=cfg.det_thresh,
+                          max_age=cfg.max_age, min_hits=cfg.min_hits,
+                          iou_threshold=cfg.iou_thresh, delta_t=cfg.delta_t,
+                          asso_func=cfg.asso_func, inertia=cfg.inertia, reid=reid)
+    if tracker_type == "strongsort":
         raise NotImplementedError(
             f"{tracker_type}: not yet on the MI355X path in this build; see DESIGN.md")
     print("No such tracker")
