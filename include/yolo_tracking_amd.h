@@ -25,6 +25,8 @@
  *   yta_kf9_run              hybridsort.py:106-320 KalmanBoxTracker + hybridsort_kf.py:339-528
  *   yta_lap_padded           boxmot/utils/association.py:20-28 linear_assignment -> lap.lapjv(cost,
  *                            extend_cost=True)
+ *   yta_lap_rect             the same call's optimum where ties cannot change the tracker result
+ *                            (association.py:20-28 at ocsort.py:266-291, :315-342)
  *   yta_kf7_run              boxmot/motion/kalman_filters/ocsort_kf.py:339-526 predict / update incl.
  *                            freeze / unfreeze (observation-centric re-update)
  *   yta_box_affinity         boxmot/utils/iou.py:6-188  iou/giou/diou/ciou/centroid_batch
@@ -95,6 +97,13 @@ int yta_lap_limited(int device, int nr, int nc, const double *cost, double cost_
  * x[r] = col or -1, y[c] = row or -1.  The same operation and tie-breaking sequence as the
  * restated lapjv (oracle/lapjv.c). */
 int yta_lap_padded(int device, int nr, int nc, const double *cost, int *x, int *y);
+
+/* The optimum of the same padded problem by the rectangular solver the OCSORT-family engines use
+ * where the result does not depend on lapjv's tie-breaking (lap_rect.hpp): warm
+ * start from row minima, shortest augmenting paths with bound pruning.  Every row / column of the
+ * smaller side is matched; equal to yta_lap_padded whenever the optimum is unique.  At most 8192
+ * entries on the larger side. */
+int yta_lap_rect(int device, int nr, int nc, const double *cost, int *x, int *y);
 
 /* ---- ByteTrack engine: S independent streams, state resident in HBM -----------------------
  * One engine = S trackers with identical parameters (BYTETracker(track_thresh, match_thresh,

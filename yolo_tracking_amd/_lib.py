@@ -93,6 +93,7 @@ _SIGS = {
     "yta_grid_pairs": ([_I, _P, _I, _P, _I, _D, _P, _I, _P], _I),
     "yta_lap_limited": ([_I, _I, _I, _P, _D, _P, _P], _I),
     "yta_lap_padded": ([_I, _I, _I, _P, _P, _P], _I),
+    "yta_lap_rect": ([_I, _I, _I, _P, _P, _P], _I),
     "yta_bytetrack_create": ([_I, _I, _I, _I, _P, _P], _I),
     "yta_bytetrack_destroy": ([_P], _I),
     "yta_bytetrack_reset": ([_P], _I),
@@ -310,6 +311,16 @@ def lap_padded(cost, device=0):
     x = np.empty(nr, dtype=np.int32)
     y = np.empty(nc, dtype=np.int32)
     check(load_library().yta_lap_padded(device, nr, nc, ptr(c), ptr(x), ptr(y)))
+    return x, y
+
+
+def lap_rect(cost, device=0):
+    """The padded problem's optimum by the OCSORT-family rectangular solver (lap_rect.hpp)."""
+    c = np.ascontiguousarray(cost, dtype=np.float64)
+    nr, nc = c.shape
+    x = np.empty(nr, dtype=np.int32)
+    y = np.empty(nc, dtype=np.int32)
+    check(load_library().yta_lap_rect(device, nr, nc, ptr(c), ptr(x), ptr(y)))
     return x, y
 
 

@@ -85,6 +85,8 @@ struct DocArgs {
     int *ema_slot, *ema_row;        // [S*(CAP+MAXD)] embedding jobs: slot, input row (birth: ~row)
     unsigned char *lap_ws;
     long long lap_ws_stride;
+    double *pre_u, *pre_s2;        // [S*MAXD] first-round row pre-pass (lap_rect.hpp)
+    int *pre_x;
     double *out;
     int *out_counts;
 };
@@ -503,6 +505,15 @@ __global__ __launch_bounds__(256) void k_doc_final(DocArgs a) {
     }
 }
 
+// Row pre-pass of the first-round solve, chip-wide (lap_rect.hpp).
+__global__ __launch_bounds__(OC_T) void k_doc_rowpre(DocArgs a) {
+    const int s = blockIdx.y;
+    const DocCounters *c = a.cnt + s;
+    const long long db = (long long)s * a.MAXD;
+    main_lap_pre(a.mat2 + doc_mb(a, s), c->n_high, c->n_trk, a.pre_u + db, a.pre_x + db,
+                 a.pre_s2 + db);
+}
+
 __global__ __launch_bounds__(OC_T) void k_doc_assoc(DocArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     __shared__ OcShared sh;
@@ -511,6 +522,7 @@ __global__ __launch_bounds__(OC_T) void k_doc_assoc(DocArgs a) {
     const long long tb = (long long)s * a.CAP, db = (long long)s * a.MAXD, mb = doc_mb(a, s);
     const long long ub = (long long)s * (a.MAXD + a.CAP);
     unsigned char *gws = a.lap_ws + s * a.lap_ws_stride;
+    const long long lds_bytes = oc_lds_bytes(a.CAP, a.MAXD);
     const double *din = a.det_in + (long long)a.det_off[s] * 6;
     const int frame = c->frame + 1;
     int n_trk = c->n_trk;
@@ -551,7 +563,8 @@ __global__ __launch_bounds__(OC_T) void k_doc_assoc(DocArgs a) {
             block_sync();
         } else if (n_hi > 0) {
             block_sync();
-            padded_lap(LapMat{mat2, n_hi, n_trk, false}, a.rmatch + db, lds, gws, &c->err);
+            main_lap(LapMat{mat2, n_hi, n_trk, false}, a.pre_u + db, a.pre_x + db, a.pre_s2 + db,
+                     a.rmatch + db, lds, lds_bytes, gws, &c->err);
         }
         if (t == 0) { c->fast_path = fast; c->lap_calls = (fast || n_hi == 0) ? 0 : 1; }
         for (int j = t; j < n_trk; j += nt) a.cmatched[tb + j] = 0;
@@ -596,7 +609,7 @@ __global__ __launch_bounds__(OC_T) void k_doc_assoc(DocArgs a) {
         block_sync();
         mx = block_max(mx, sh);
         if (mx > a.thr) {
-            padded_lap(LapMat{mat, n_ud, n_ut, true}, a.rmatch + db, lds, gws, &c->err);
+            iou_lap(LapMat{mat, n_ud, n_ut, true}, a.rmatch + db, lds, lds_bytes, gws, &c->err);
             for (int i = t; i < n_hi; i += nt) a.tmp[ub + i] = 0;
             for (int j = t; j < n_trk; j += nt) a.nan_flag[tb + j] = 0;
             block_sync();
@@ -850,6 +863,9 @@ int doc_alloc(yta_deepocsort *e) {
     DOCALLOC(a.rw, S * MAXD);
     DOCALLOC(a.cw, S * CAP);
     DOCALLOC(a.rmatch, S * MAXD);
+    DOCALLOC(a.pre_u, S * MAXD);
+    DOCALLOC(a.pre_s2, S * MAXD);
+    DOCALLOC(a.pre_x, S * MAXD);
     DOCALLOC(a.cmatched, S * CAP);
     DOCALLOC(a.udet, S * (MAXD + CAP));
     DOCALLOC(a.utrk, S * (MAXD + CAP));
@@ -861,7 +877,7 @@ int doc_alloc(yta_deepocsort *e) {
     const long long n = std::max(CAP, MAXD);
     a.lap_ws_stride = n > OC_LDS_LAP_N ? ((dense_lap_ws_bytes(n) + 255) & ~255LL) : 256;
     DOCALLOC(a.lap_ws, S * a.lap_ws_stride);
-    e->lds = (size_t)dense_lap_ws_bytes(std::min<long long>(n, OC_LDS_LAP_N));
+    e->lds = (size_t)oc_lds_bytes(CAP, MAXD);
     DOCALLOC(e->d_off, S + 1);
     DOCALLOC(e->d_wh, 2 * S);
     DOCALLOC(e->d_warp, 6 * S);
@@ -916,6 +932,13 @@ int doc_launch(yta_deepocsort *e, const double *d_dets, const int *d_off, const 
     }
     hipLaunchKernelGGL(k_doc_final, gm, dim3(256), 0, e->stream, a);
     YTA_HIP(hipGetLastError());
+    {
+        const long long rows = (a.MAXD + OC_T / WAVE - 1) / (OC_T / WAVE);
+        const long long rcap = std::max<long long>(4, 4096 / a.S);
+        hipLaunchKernelGGL(k_doc_rowpre, dim3((unsigned)std::max<long long>(1, std::min(rows, rcap)), a.S),
+                           dim3(OC_T), 0, e->stream, a);
+        YTA_HIP(hipGetLastError());
+    }
     hipLaunchKernelGGL(k_doc_assoc, dim3(a.S), dim3(OC_T), e->lds, e->stream, a);
     YTA_HIP(hipGetLastError());
     if (!a.embedding_off) {

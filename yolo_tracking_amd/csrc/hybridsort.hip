@@ -103,6 +103,8 @@ struct HsArgs {
     int *ema_slot, *ema_row;        // [S*(CAP+MAXD)] feature jobs: slot, kept index (birth: ~p)
     unsigned char *lap_ws;
     long long lap_ws_stride;
+    double *pre_u, *pre_s2;        // [S*MAXD] first-round row pre-pass (lap_rect.hpp)
+    int *pre_x;
     double *out;
     int *out_counts;
 };
@@ -477,6 +479,15 @@ __global__ __launch_bounds__(256) void k_hs_emb(HsArgs a) {
 }
 
 // -------------------------------------------------------------------------------- k_hs_assoc
+// Row pre-pass of the first-round solve, chip-wide (lap_rect.hpp).
+__global__ __launch_bounds__(OC_T) void k_hs_rowpre(HsArgs a) {
+    const int s = blockIdx.y;
+    const HsCounters *c = a.cnt + s;
+    const long long db = (long long)s * a.MAXD;
+    main_lap_pre(a.cost + hs_mb(a, s), c->n_high, c->n_trk, a.pre_u + db, a.pre_x + db,
+                 a.pre_s2 + db);
+}
+
 __global__ __launch_bounds__(OC_T) void k_hs_assoc(HsArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     __shared__ OcShared sh;
@@ -485,6 +496,7 @@ __global__ __launch_bounds__(OC_T) void k_hs_assoc(HsArgs a) {
     const long long tb = (long long)s * a.CAP, db = (long long)s * a.MAXD, mb = hs_mb(a, s);
     const long long ub = (long long)s * (a.MAXD + a.CAP);
     unsigned char *gws = a.lap_ws + s * a.lap_ws_stride;
+    const long long lds_bytes = oc_lds_bytes(a.CAP, a.MAXD);
     const double *din = a.det_in + (long long)a.det_off[s] * 6;
     const int frame = c->frame + 1;
     int n_trk = c->n_trk;
@@ -508,7 +520,8 @@ __global__ __launch_bounds__(OC_T) void k_hs_assoc(HsArgs a) {
         block_sync();
     } else {
         block_sync();
-        padded_lap(LapMat{cost, n_hi, n_trk, false}, a.rmatch + db, lds, gws, &c->err);
+        main_lap(LapMat{cost, n_hi, n_trk, false}, a.pre_u + db, a.pre_x + db, a.pre_s2 + db,
+                 a.rmatch + db, lds, lds_bytes, gws, &c->err);
         if (t == 0) c->lap_calls = 1;
         for (int j = t; j < n_trk; j += nt) a.cmatched[tb + j] = 0;
         block_sync();
@@ -578,7 +591,7 @@ __global__ __launch_bounds__(OC_T) void k_hs_assoc(HsArgs a) {
         block_sync();
         mx = block_max(mx, sh);
         if (mx > a.thr) {
-            padded_lap(LapMat{mat, n_ud, n_ut, true}, a.rmatch + db, lds, gws, &c->err);
+            iou_lap(LapMat{mat, n_ud, n_ut, true}, a.rmatch + db, lds, lds_bytes, gws, &c->err);
             for (int i = t; i < n_hi; i += nt) a.tmp[ub + i] = 0;
             for (int j = t; j < n_trk; j += nt) a.nan_flag[tb + j] = 0;
             block_sync();
@@ -829,6 +842,9 @@ int hs_alloc(yta_hybridsort *e) {
     HSALLOC(a.cost, S * mat);
     HSALLOC(a.emat, S * mat);
     HSALLOC(a.rmatch, S * MAXD);
+    HSALLOC(a.pre_u, S * MAXD);
+    HSALLOC(a.pre_s2, S * MAXD);
+    HSALLOC(a.pre_x, S * MAXD);
     HSALLOC(a.cmatched, S * CAP);
     HSALLOC(a.udet, S * (MAXD + CAP));
     HSALLOC(a.utrk, S * (MAXD + CAP));
@@ -840,7 +856,7 @@ int hs_alloc(yta_hybridsort *e) {
     const long long n = std::max(CAP, MAXD);
     a.lap_ws_stride = n > OC_LDS_LAP_N ? ((dense_lap_ws_bytes(n) + 255) & ~255LL) : 256;
     HSALLOC(a.lap_ws, S * a.lap_ws_stride);
-    e->lds = (size_t)dense_lap_ws_bytes(std::min<long long>(n, OC_LDS_LAP_N));
+    e->lds = (size_t)oc_lds_bytes(CAP, MAXD);
     HSALLOC(e->d_off, S + 1);
     YTA_HIP(hipHostMalloc((void **)&e->h_off, sizeof(int) * (S + 1), hipHostMallocDefault));
     YTA_HIP(hipHostMalloc((void **)&e->h_cnt, sizeof(HsCounters) * S, hipHostMallocDefault));
@@ -872,6 +888,13 @@ int hs_launch(yta_hybridsort *e, const double *d_dets, const int *d_off, const f
     const dim3 ge((a.CAP + HE_TILE - 1) / HE_TILE, (a.MAXD + HE_TILE - 1) / HE_TILE, a.S);
     hipLaunchKernelGGL(k_hs_emb, ge, dim3(256), 0, e->stream, a);
     YTA_HIP(hipGetLastError());
+    {
+        const long long rows = (a.MAXD + OC_T / WAVE - 1) / (OC_T / WAVE);
+        const long long rcap = std::max<long long>(4, 4096 / a.S);
+        hipLaunchKernelGGL(k_hs_rowpre, dim3((unsigned)std::max<long long>(1, std::min(rows, rcap)), a.S),
+                           dim3(OC_T), 0, e->stream, a);
+        YTA_HIP(hipGetLastError());
+    }
     hipLaunchKernelGGL(k_hs_assoc, dim3(a.S), dim3(OC_T), e->lds, e->stream, a);
     YTA_HIP(hipGetLastError());
     const dim3 gj((a.CAP + a.MAXD + 3) / 4, a.S);

@@ -7,6 +7,7 @@
 #include "grid.hpp"
 #include "kf_xyah.hpp"
 #include "lap_dense.hpp"
+#include "lap_rect.hpp"
 
 using namespace yta;
 
@@ -127,6 +128,36 @@ __global__ __launch_bounds__(64) void k_lap_padded(const double *cost, int nr, i
     if (rc && lane_id() == 0) atomicOr(err, ERR_SOLVER);
     for (int r = lane_id(); r < nr; r += WAVE) X[r] = w.x[r] < nc ? w.x[r] : -1;
     for (int k = lane_id(); k < nc; k += WAVE) Y[k] = w.y[k] < nr ? w.y[k] : -1;
+}
+
+// Rectangular solver KAT (lap_rect.hpp): rows <= cols solved as given with the chip-wide row
+// pre-pass (k_lap_rect_pre, as the first-round association), rows > cols on the transposed view
+// with the in-block pre-pass (as the -IoU rounds).  Work arrays in global memory.
+__global__ __launch_bounds__(256) void k_lap_rect_pre(const double *cost, int nr, int nc, double *u,
+                                                      int *x, double *s2) {
+    if (nr > nc) return;
+    const RectMat M{cost, nr, nc, nc, 1, false};
+    const int nw = blockDim.x / WAVE;
+    for (int i = blockIdx.x * nw + threadIdx.x / WAVE; i < nr; i += gridDim.x * nw)
+        rect_row_pre(M, i, u, x, s2);
+}
+__global__ __launch_bounds__(256) void k_lap_rect(const double *cost, int nr, int nc,
+                                                  const double *pu, const int *px,
+                                                  const double *ps2, int *X, int *Y, int *err,
+                                                  unsigned char *ws) {
+    __shared__ RectShared sh;
+    const bool tr = nr > nc;
+    const RectMat R = tr ? RectMat{cost, nc, nr, 1, nc, false} : RectMat{cost, nr, nc, nc, 1, false};
+    const RectWs w = rect_ws(ws, R.rows, R.cols);
+    const int rc = tr ? lap_rect(R, nullptr, nullptr, nullptr, w, sh) : lap_rect(R, pu, px, ps2, w, sh);
+    if (rc && threadIdx.x == 0) atomicOr(err, 1 << (-rc));
+    block_sync();
+    if (rc) return;
+    for (int k = threadIdx.x; k < R.rows; k += blockDim.x) {
+        const int c = w.x[k];
+        if (!tr) { X[k] = c; Y[c] = k; }
+        else { Y[k] = c; X[c] = k; }
+    }
 }
 
 // One block: grid over b, then every a-box queries it; pairs with 1 - IoU < thresh are written
@@ -423,6 +454,47 @@ int yta_lap_padded(int device, int nr, int nc, const double *cost, int *x, int *
     if (nc) YTA_HIP(hipMemcpy(y, dy, sizeof(int) * nc, hipMemcpyDeviceToHost));
     YTA_HIP(hipMemcpy(&herr, derr, sizeof(int), hipMemcpyDeviceToHost));
     YTA_CHECK(herr == 0, YTA_ERR_HIP, "padded assignment solver error flags 0x%x", herr);
+    return YTA_OK;
+}
+
+int yta_lap_rect(int device, int nr, int nc, const double *cost, int *x, int *y) {
+    YTA_CHECK(nr >= 0 && nc >= 0, YTA_ERR_INVALID, "negative size");
+    YTA_CHECK((nr == 0 || x) && (nc == 0 || y), YTA_ERR_INVALID, "null buffer");
+    for (int i = 0; i < nr; ++i) x[i] = -1;
+    for (int j = 0; j < nc; ++j) y[j] = -1;
+    if (nr == 0 || nc == 0) return YTA_OK;
+    YTA_CHECK(cost, YTA_ERR_INVALID, "null buffer");
+    const int rows = nr < nc ? nr : nc, cols = nr < nc ? nc : nr;
+    YTA_CHECK(cols <= RECT_CPT_MAX * 256, YTA_ERR_INVALID, "more than %d columns", RECT_CPT_MAX * 256);
+    int rc = select_device(device);
+    if (rc) return rc;
+    DevBuf m;
+    double *dcost, *pu, *ps2;
+    int *dx, *dy, *derr, *px;
+    unsigned char *ws;
+    YTA_HIP(m.get(&dcost, (long long)nr * nc));
+    YTA_HIP(m.get(&dx, nr));
+    YTA_HIP(m.get(&dy, nc));
+    YTA_HIP(m.get(&derr, 1));
+    YTA_HIP(m.get(&pu, nr));
+    YTA_HIP(m.get(&ps2, nr));
+    YTA_HIP(m.get(&px, nr));
+    YTA_HIP(m.get(&ws, (size_t)rect_ws_bytes(rows, cols)));
+    YTA_HIP(hipMemset(derr, 0, sizeof(int)));
+    YTA_HIP(hipMemset(dx, 0xFF, sizeof(int) * nr));
+    YTA_HIP(hipMemset(dy, 0xFF, sizeof(int) * nc));
+    YTA_HIP(hipMemcpy(dcost, cost, sizeof(double) * nr * nc, hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(k_lap_rect_pre, dim3((unsigned)std::min(1024, (nr + 3) / 4)), dim3(256), 0, 0,
+                       dcost, nr, nc, pu, px, ps2);
+    YTA_HIP(hipGetLastError());
+    hipLaunchKernelGGL(k_lap_rect, dim3(1), dim3(256), 0, 0, dcost, nr, nc, pu, px, ps2, dx, dy,
+                       derr, ws);
+    YTA_HIP(hipGetLastError());
+    int herr = 0;
+    YTA_HIP(hipMemcpy(x, dx, sizeof(int) * nr, hipMemcpyDeviceToHost));
+    YTA_HIP(hipMemcpy(y, dy, sizeof(int) * nc, hipMemcpyDeviceToHost));
+    YTA_HIP(hipMemcpy(&herr, derr, sizeof(int), hipMemcpyDeviceToHost));
+    YTA_CHECK(herr == 0, YTA_ERR_HIP, "rectangular assignment solver error flags 0x%x", herr);
     return YTA_OK;
 }
 

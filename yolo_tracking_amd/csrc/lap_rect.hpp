@@ -1,0 +1,283 @@
+// Dense rectangular linear assignment on one block: the exact optimum of
+//   boxmot/utils/association.py:20-28  lap.lapjv(cost, extend_cost=True)
+// for a zero-padded problem whose real block has rows <= cols (every row is matched; the padding
+// rows take the columns left over at cost 0, so the padded optimum restricted to the real rows is
+// the rectangular optimum).  Used where the padded solve's result does not depend on how lapjv
+// breaks exact ties: the OCSORT-family first round when trackers >= detections,
+// and the -IoU rounds (BYTE / OCR), whose surviving pairs are filtered by IoU >= threshold and
+// re-sorted (np.setdiff1d).  Everything else keeps the lapjv replay of lap_dense.hpp.
+//
+// Algorithm (shortest augmenting paths with a warm start, duals u / v, v = 0 on free columns):
+//   1. row pre-pass (chip-wide kernel, or this block for small problems): u_i = min_j c_ij, its
+//      first column, and s2_i = second minimum - minimum (a lower bound of row i's reduced costs
+//      off its own column);
+//   2. every row claims its argmin column; the lowest claiming row keeps it (tight, feasible);
+//   3. every other row is augmented by Dijkstra over the columns, one block-wide step per row
+//      relaxation.  Pruning: the row of an assigned column j is only relaxed while
+//      spc_j + s2_row < B, B = the cheapest free column reached so far; any other row can only
+//      produce distances >= B and cannot change the result.  The search stops when no prunable
+//      column is left below B; every column below B gets the usual dual update.  s2 stays a valid
+//      lower bound through the dual updates (u_i += d  =>  s2_i -= d) and is reset to 0 on the
+//      augmenting path (refreshed exactly whenever the row is relaxed).
+// Each thread owns the columns j = t + q * blockDim (q < CPT): distance, price, owner row and
+// bound live in registers; a step is one coalesced row read + one block argmin (one barrier).
+#pragma once
+#include <float.h>
+#include <limits.h>
+
+#include "common.hpp"
+
+namespace yta {
+
+// The solver's view of the cost matrix: element (i, j) at m[i * rs + j * cs] (a transposed view
+// swaps the strides), negated when `neg`.
+struct RectMat {
+    const double *m;
+    int rows, cols;
+    long long rs, cs;
+    bool neg;
+    __device__ __forceinline__ double at(int i, int j) const {
+        const double v = ((const __attribute__((address_space(1))) double *)m)[i * rs + j * cs];
+        return neg ? -v : v;
+    }
+};
+
+// Work arrays (LDS or global): rect_ws_bytes(rows, cols) bytes, 8-aligned.
+struct RectWs {
+    double *u, *s2;     // rows
+    int *x, *fl;        // rows: assigned column, free-row list
+    int *path, *yw;     // cols: predecessor row, owner row (authoritative copy)
+};
+__host__ __device__ inline long long rect_ws_bytes(long long rows, long long cols) {
+    return rows * 24 + cols * 8 + 64;
+}
+__host__ __device__ inline RectWs rect_ws(unsigned char *base, int rows, int cols) {
+    RectWs w;
+    w.u = reinterpret_cast<double *>(base);
+    w.s2 = w.u + rows;
+    w.x = reinterpret_cast<int *>(w.s2 + rows);
+    w.fl = w.x + rows;
+    w.path = w.fl + rows;
+    w.yw = w.path + cols;
+    return w;
+}
+constexpr int RECT_CPT_MAX = 32;
+
+// One wave: minimum of row i (first column on ties), and second minimum - minimum.
+__device__ __forceinline__ void rect_row_pre(const RectMat M, int i, double *u, int *x, double *s2) {
+    const int lane = lane_id();
+    double m1 = INFINITY, m2 = INFINITY;
+    int k1 = INT_MAX;
+    for (int j = lane; j < M.cols; j += WAVE) {
+        const double c = M.at(i, j);
+        if (c < m1) { m2 = m1; m1 = c; k1 = j; }
+        else if (c < m2) m2 = c;
+    }
+#pragma unroll
+    for (int s = 32; s >= 1; s >>= 1) {
+        const double om1 = __shfl_xor(m1, s), om2 = __shfl_xor(m2, s);
+        const int ok1 = __shfl_xor(k1, s);
+        const bool other = om1 < m1 || (om1 == m1 && ok1 < k1);
+        const double lose = other ? m1 : om1;
+        const double m2w = other ? om2 : m2;
+        m2 = lose < m2w ? lose : m2w;
+        m1 = other ? om1 : m1;
+        k1 = other ? ok1 : k1;
+    }
+    if (lane == 0) {
+        u[i] = m1;
+        x[i] = k1 == INT_MAX ? 0 : k1;
+        s2[i] = m2 - m1;
+    }
+}
+
+struct RectRed {
+    double b, ma, mo;
+    int sink, ja, ya, pad;
+};
+struct RectShared {
+    RectRed slot[2][16];
+    int wsum[32];
+};
+
+__device__ __forceinline__ void rect_lex_min(double &v, int &k, double ov, int ok) {
+    if (ov < v || (ov == v && ok < k)) { v = ov; k = ok; }
+}
+
+// Solve.  pre_u / pre_x / pre_s2: the row pre-pass (global, or nullptr: computed here).  Returns 0,
+// or -2 if a row cannot reach a free column (rows > cols, or NaN costs).  On return w.x[i] is the
+// column of row i.  All threads of the block must call it; blockDim.x * CPT >= M.cols.
+template <int CPT>
+__device__ __noinline__ int lap_rect_block(const RectMat M, const double *pre_u, const int *pre_x,
+                                           const double *pre_s2, RectWs w, RectShared &sh) {
+    const int t = threadIdx.x, nt = blockDim.x, wid = t / WAVE, nw = nt / WAVE;
+    constexpr int CH = CPT < 8 ? CPT : 8;
+    const int rows = M.rows, cols = M.cols;
+    if (rows <= 0) return 0;
+    if (rows > cols) return -2;
+    // ---- 1. row pre-pass (when not supplied) and 2. claims
+    if (pre_u == nullptr) {
+        for (int i = wid; i < rows; i += nw) rect_row_pre(M, i, w.u, w.x, w.s2);
+        pre_u = w.u; pre_x = w.x; pre_s2 = w.s2;
+    }
+    for (int j = t; j < cols; j += nt) w.path[j] = INT_MAX;
+    block_sync();
+    for (int i = t; i < rows; i += nt) atomicMin(&w.path[pre_x[i]], i);
+    block_sync();
+    for (int i = t; i < rows; i += nt) {
+        const int xi = pre_x[i];
+        const double ui = pre_u[i], si = pre_s2[i];
+        const bool won = w.path[xi] == i;
+        w.u[i] = ui;
+        w.s2[i] = si;
+        w.x[i] = won ? xi : -1;
+    }
+    block_sync();
+    // s2c: the bound of each column's row, as a float rounded down (still a lower bound)
+    double v[CPT], spc[CPT];
+    float s2c[CPT];
+    int y[CPT];
+    unsigned rel = 0u;
+#pragma unroll
+    for (int q = 0; q < CPT; ++q) {
+        const int j = t + q * nt;
+        v[q] = 0.0;
+        y[q] = -1;
+        s2c[q] = 0.0f;
+        if (j < cols) {
+            const int r = w.path[j];
+            y[q] = r == INT_MAX ? -1 : r;
+            if (y[q] >= 0) s2c[q] = __double2float_rd(w.s2[y[q]]);
+            w.yw[j] = y[q];
+        }
+    }
+    const int nfree = block_compact(rows, sh.wsum, [&](int i) { return w.x[i] < 0; },
+                                    [&](int i, int pos) { w.fl[pos] = i; });
+    block_sync();
+    int par = 0;
+    // ---- 3. augment the free rows
+    for (int f = 0; f < nfree; ++f) {
+        const int cur = w.fl[f];
+#pragma unroll
+        for (int q = 0; q < CPT; ++q) spc[q] = INFINITY;
+        rel = 0u;
+        int i = cur, xi = -1;
+        double base = 0.0, ui = w.u[cur], bprev = INFINITY, B = INFINITY;
+        int sink = -1;
+        bool done = false;
+        for (int guard = 0; guard <= rows && !done; ++guard) {
+            double lb = INFINITY, lma = INFINITY, lmo = INFINITY;
+            int lsink = INT_MAX, lja = INT_MAX, lya = -1;
+            // row costs in chunks of 8 columns (loads of a chunk in flight together)
+#pragma unroll
+            for (int q0 = 0; q0 < CPT; q0 += CH) {
+                double c[CH];
+#pragma unroll
+                for (int k = 0; k < CH; ++k) {
+                    const int j = t + (q0 + k) * nt;
+                    c[k] = j < cols ? M.at(i, j) : 0.0;
+                }
+#pragma unroll
+                for (int k = 0; k < CH; ++k) {
+                    const int q = q0 + k;
+                    const int j = t + q * nt;
+                    if (j >= cols) continue;
+                    const double rc = c[k] - ui - v[q];
+                    if (j != xi) lmo = rc < lmo ? rc : lmo;
+                    if ((rel >> q) & 1u) continue;
+                    const double r = base + rc;
+                    if (r < spc[q]) {
+                        spc[q] = r;
+                        w.path[j] = i;
+                    }
+                    if (y[q] < 0) {
+                        if (spc[q] < lb) { lb = spc[q]; lsink = j; }
+                    } else if (spc[q] + (double)s2c[q] < bprev && spc[q] < lma) {
+                        lma = spc[q]; lja = j; lya = y[q];
+                    }
+                }
+            }
+            // wave, then block: lexicographic (B, sink), (ma, ja) carrying ya, min mo
+#pragma unroll
+            for (int s = 32; s >= 1; s >>= 1) {
+                const double ob = __shfl_xor(lb, s), oma = __shfl_xor(lma, s), omo = __shfl_xor(lmo, s);
+                const int osk = __shfl_xor(lsink, s), oja = __shfl_xor(lja, s), oya = __shfl_xor(lya, s);
+                rect_lex_min(lb, lsink, ob, osk);
+                if (oma < lma || (oma == lma && oja < lja)) { lma = oma; lja = oja; lya = oya; }
+                lmo = omo < lmo ? omo : lmo;
+            }
+            if (lane_id() == 0) sh.slot[par][wid] = RectRed{lb, lma, lmo, lsink, lja, lya, 0};
+            __syncthreads();
+            B = INFINITY;
+            sink = INT_MAX;
+            double ma = INFINITY, mo = INFINITY;
+            int ja = INT_MAX, ya = -1;
+            for (int k = 0; k < nw; ++k) {
+                const RectRed r = sh.slot[par][k];
+                rect_lex_min(B, sink, r.b, r.sink);
+                if (r.ma < ma || (r.ma == ma && r.ja < ja)) { ma = r.ma; ja = r.ja; ya = r.ya; }
+                mo = r.mo < mo ? r.mo : mo;
+            }
+            par ^= 1;
+#pragma unroll
+            for (int q = 0; q < CPT; ++q) {
+                const int j = t + q * nt;
+                if (j == xi) s2c[q] = __double2float_rd(mo);   // exact for the current duals
+                if (ma < B && j == ja) rel |= 1u << q;
+            }
+            if (!(ma < B)) { done = true; break; }
+            i = ya;
+            xi = ja;
+            base = ma;
+            bprev = B;
+            ui = w.u[ya];
+        }
+        if (!done || !(B < INFINITY) || sink == INT_MAX) return -2;
+        // dual update of every column below B (and of its row)
+#pragma unroll
+        for (int q = 0; q < CPT; ++q) {
+            const int j = t + q * nt;
+            if (j < cols && y[q] >= 0 && spc[q] < B) {
+                const double dl = B - spc[q];
+                w.u[y[q]] += dl;
+                s2c[q] = __double2float_rd((double)s2c[q] - dl);
+                v[q] -= dl;
+            }
+        }
+        if (t == 0) w.u[cur] += B;
+        block_sync();
+        if (t == 0) {   // flip the alternating path back to the source row
+            int j = sink;
+            for (int steps = 0; steps <= rows; ++steps) {
+                const int r = w.path[j];
+                w.yw[j] = r;
+                const int nx = w.x[r];
+                w.x[r] = j;
+                if (r == cur) break;
+                j = nx;
+            }
+        }
+        block_sync();
+#pragma unroll
+        for (int q = 0; q < CPT; ++q) {
+            const int j = t + q * nt;
+            if (j < cols) {
+                const int ny = w.yw[j];
+                if (ny != y[q]) { y[q] = ny; s2c[q] = 0.0f; }
+            }
+        }
+    }
+    return 0;
+}
+
+// Dispatch on the columns per thread.  Returns -3 when cols exceeds the register tiles.
+__device__ __forceinline__ int lap_rect(const RectMat M, const double *pre_u, const int *pre_x,
+                                        const double *pre_s2, RectWs w, RectShared &sh) {
+    const int nt = blockDim.x;
+    if (M.cols <= 2 * nt) return lap_rect_block<2>(M, pre_u, pre_x, pre_s2, w, sh);
+    if (M.cols <= 8 * nt) return lap_rect_block<8>(M, pre_u, pre_x, pre_s2, w, sh);
+    if (M.cols <= RECT_CPT_MAX * nt) return lap_rect_block<RECT_CPT_MAX>(M, pre_u, pre_x, pre_s2, w, sh);
+    return -3;
+}
+
+}  // namespace yta

@@ -80,6 +80,8 @@ struct OcArgs {
     int *upd;                      // [S*CAP] update source per tracker: input row, -1 none
     unsigned char *lap_ws;         // per stream (n > OC_LDS_LAP_N)
     long long lap_ws_stride;
+    double *pre_u, *pre_s2;        // [S*MAXD] first-round row pre-pass (lap_rect.hpp)
+    int *pre_x;
     double *out;                   // [S*CAP*8]
     int *out_counts;
 };
@@ -307,6 +309,16 @@ __global__ __launch_bounds__(OC_T) void k_oc_cost(OcArgs a) {
     if (giou_bad) atomicOr(&c->err, ERR_GIOU);
 }
 
+// Row pre-pass of the first-round solve (row minima, argmins, second minima of the cost matrix),
+// chip-wide, so the stream block only walks the augmenting paths.
+__global__ __launch_bounds__(OC_T) void k_oc_rowpre(OcArgs a) {
+    const int s = blockIdx.y;
+    const OcCounters *c = a.cnt + s;
+    const long long db = (long long)s * a.MAXD;
+    const long long mb = (long long)s * (a.MAXD > 4 ? a.MAXD : 4) * a.CAP;
+    main_lap_pre(a.mat2 + mb, c->n_high, c->n_trk, a.pre_u + db, a.pre_x + db, a.pre_s2 + db);
+}
+
 __global__ __launch_bounds__(OC_T) void k_oc_assoc(OcArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     __shared__ OcShared sh;
@@ -316,6 +328,7 @@ __global__ __launch_bounds__(OC_T) void k_oc_assoc(OcArgs a) {
     const long long mb = (long long)s * (a.MAXD > 4 ? a.MAXD : 4) * a.CAP;
     const long long ub = (long long)s * (a.MAXD + a.CAP);
     unsigned char *gws = a.lap_ws + s * a.lap_ws_stride;
+    const long long lds_bytes = oc_lds_bytes(a.CAP, a.MAXD);
     int nd = a.det_off[s + 1] - a.det_off[s];
     if (nd > a.MAXD || nd < 0) {
         if (t == 0) atomicOr(&c->err, ERR_DET_CAPACITY);
@@ -368,7 +381,8 @@ __global__ __launch_bounds__(OC_T) void k_oc_assoc(OcArgs a) {
             block_sync();
         } else if (n_hi > 0) {
             block_sync();
-            padded_lap(LapMat{mat2, n_hi, n_trk, false}, a.rmatch + db, lds, gws, &c->err);
+            main_lap(LapMat{mat2, n_hi, n_trk, false}, a.pre_u + db, a.pre_x + db, a.pre_s2 + db,
+                     a.rmatch + db, lds, lds_bytes, gws, &c->err);
         }
         YTA_STAMP(4);
         if (t == 0) { c->fast_path = fast; c->lap_calls = (fast || n_hi == 0) ? 0 : 1; }
@@ -417,7 +431,7 @@ __global__ __launch_bounds__(OC_T) void k_oc_assoc(OcArgs a) {
         block_sync();
         mx = block_max(mx, sh);
         if (mx > a.thr) {
-            padded_lap(LapMat{mat, n_lo, n_ut, true}, a.rmatch + db, lds, gws, &c->err);
+            iou_lap(LapMat{mat, n_lo, n_ut, true}, a.rmatch + db, lds, lds_bytes, gws, &c->err);
             for (int k = t; k < n_ut; k += nt) a.tmp[ub + k] = 0;   // taken flags
             block_sync();
             for (int p = t; p < n_lo; p += nt) {
@@ -454,7 +468,7 @@ __global__ __launch_bounds__(OC_T) void k_oc_assoc(OcArgs a) {
         block_sync();
         mx = block_max(mx, sh);
         if (mx > a.thr) {
-            padded_lap(LapMat{mat, n_ud, n_ut, true}, a.rmatch + db, lds, gws, &c->err);
+            iou_lap(LapMat{mat, n_ud, n_ut, true}, a.rmatch + db, lds, lds_bytes, gws, &c->err);
             // removed dets / trackers -> flags, then sorted set differences
             for (int i = t; i < n_hi; i += nt) a.tmp[ub + i] = 0;
             for (int j = t; j < n_trk; j += nt) a.nan_flag[tb + j] = 0;
@@ -657,6 +671,9 @@ int oc_alloc(yta_ocsort *e) {
     OCALLOC(a.mat, S * mat);                                            //  scratch of CAP boxes)
     OCALLOC(a.mat2, S * mat);
     OCALLOC(a.rmatch, S * MAXD);
+    OCALLOC(a.pre_u, S * MAXD);
+    OCALLOC(a.pre_s2, S * MAXD);
+    OCALLOC(a.pre_x, S * MAXD);
     OCALLOC(a.cmatched, S * CAP);
     OCALLOC(a.udet, S * (MAXD + CAP));
     OCALLOC(a.utrk, S * (MAXD + CAP));
@@ -666,7 +683,7 @@ int oc_alloc(yta_ocsort *e) {
     const long long n = std::max(CAP, MAXD);
     a.lap_ws_stride = n > OC_LDS_LAP_N ? ((dense_lap_ws_bytes(n) + 255) & ~255LL) : 256;
     OCALLOC(a.lap_ws, S * a.lap_ws_stride);
-    e->lds = (size_t)dense_lap_ws_bytes(std::min<long long>(n, OC_LDS_LAP_N));
+    e->lds = (size_t)oc_lds_bytes(CAP, MAXD);
     OCALLOC(e->d_off, S + 1);
     OCALLOC(e->d_wh, 2 * S);
     YTA_HIP(hipHostMalloc((void **)&e->h_off, sizeof(int) * (S + 1), hipHostMallocDefault));
@@ -700,6 +717,10 @@ int oc_launch(yta_ocsort *e, const double *d_dets, const int *d_off, const int *
     const long long per = ((long long)a.MAXD * a.CAP + OC_T - 1) / OC_T;
     const long long cap = std::max<long long>(4, 4096 / a.S);
     hipLaunchKernelGGL(k_oc_cost, dim3((unsigned)std::max<long long>(1, std::min(per, cap)), a.S),
+                       dim3(OC_T), 0, e->stream, a);
+    YTA_HIP(hipGetLastError());
+    const long long rows = (a.MAXD + OC_T / WAVE - 1) / (OC_T / WAVE);
+    hipLaunchKernelGGL(k_oc_rowpre, dim3((unsigned)std::max<long long>(1, std::min(rows, cap)), a.S),
                        dim3(OC_T), 0, e->stream, a);
     YTA_HIP(hipGetLastError());
     hipLaunchKernelGGL(k_oc_assoc, dim3(a.S), dim3(OC_T), e->lds, e->stream, a);

@@ -5,6 +5,7 @@
 #include "geometry.hpp"
 #include "lap.hpp"
 #include "lap_dense.hpp"
+#include "lap_rect.hpp"
 
 namespace yta {
 
@@ -66,6 +67,75 @@ __device__ __forceinline__ void padded_lap(const LapMat &M, int *rx, unsigned ch
         for (int r = lane_id(); r < M.na; r += WAVE) rx[r] = w.x[r] < M.nb ? w.x[r] : -1;
     }
     block_sync();
+}
+
+// Dynamic LDS of the association kernels (host launch size and device-side view of it).
+__host__ __device__ inline long long oc_lds_bytes(long long CAP, long long MAXD) {
+    const long long n = CAP > MAXD ? CAP : MAXD;
+    return dense_lap_ws_bytes(n < OC_LDS_LAP_N ? n : OC_LDS_LAP_N);
+}
+
+// Rectangular solve (lap_rect.hpp) of R; `tr`: R is the transposed view of an na-row problem, so
+// the solver's rows are the caller's columns.  rx[caller row] = caller column or -1.
+__device__ __forceinline__ void rect_solve(const RectMat &R, const double *pu, const int *px,
+                                           const double *ps2, bool tr, int na, int *rx,
+                                           unsigned char *lds, long long lds_bytes,
+                                           unsigned char *gws, int *err) {
+    __shared__ RectShared rsh;
+    const int t = threadIdx.x, nt = blockDim.x;
+    unsigned char *base = rect_ws_bytes(R.rows, R.cols) <= lds_bytes ? lds : gws;
+    const RectWs w = rect_ws(base, R.rows, R.cols);
+    const int rc = lap_rect(R, pu, px, ps2, w, rsh);
+    if (rc && t == 0) atomicOr(err, ERR_SOLVER);
+    if (!tr) {
+        for (int i = t; i < R.rows; i += nt) rx[i] = rc ? -1 : w.x[i];
+    } else {
+        for (int i = t; i < na; i += nt) rx[i] = -1;
+        block_sync();
+        if (!rc)
+            for (int k = t; k < R.rows; k += nt) rx[w.x[k]] = k;
+    }
+    block_sync();
+}
+
+// First-round solve of association.py:20-28 on the padded problem M (rows = detections, columns =
+// trackers).  With trackers >= detections every detection row is matched and the result does not
+// depend on lapjv's tie-breaking: the rectangular solver, warm-started by the
+// chip-wide row pre-pass (pu / px / ps2, main_lap_pre).  Otherwise the lapjv replay.
+__device__ __forceinline__ void main_lap(const LapMat &M, const double *pu, const int *px,
+                                         const double *ps2, int *rx, unsigned char *lds,
+                                         long long lds_bytes, unsigned char *gws, int *err) {
+    if (M.na <= M.nb && M.nb <= RECT_CPT_MAX * (int)blockDim.x)
+        rect_solve(RectMat{M.m, M.na, M.nb, M.nb, 1, M.neg}, pu, px, ps2, false, M.na, rx, lds,
+                   lds_bytes, gws, err);
+    else
+        padded_lap(M, rx, lds, gws, err);
+}
+
+// Row pre-pass of main_lap for one stream, spread over the blocks of a chip-wide launch.
+__device__ __forceinline__ void main_lap_pre(const double *mat, int na, int nb, double *u, int *x,
+                                             double *s2) {
+    if (na <= 0 || na > nb || nb > RECT_CPT_MAX * OC_T) return;
+    const RectMat M{mat, na, nb, nb, 1, false};
+    const int nw = blockDim.x / WAVE;
+    for (int i = blockIdx.x * nw + threadIdx.x / WAVE; i < na; i += gridDim.x * nw)
+        rect_row_pre(M, i, u, x, s2);
+}
+
+// The -IoU rounds (BYTE / OCR: association.py:20-28 on -iou): only pairs with IoU >= threshold
+// survive and the leftover lists are re-sorted (np.setdiff1d), so any optimal solution gives the
+// reference's result: the rectangular solver in whichever orientation has rows <= columns.
+__device__ __forceinline__ void iou_lap(const LapMat &M, int *rx, unsigned char *lds,
+                                        long long lds_bytes, unsigned char *gws, int *err) {
+    const bool tr = M.na > M.nb;
+    const int rows = tr ? M.nb : M.na, cols = tr ? M.na : M.nb;
+    if (cols > RECT_CPT_MAX * (int)blockDim.x) {
+        padded_lap(M, rx, lds, gws, err);
+        return;
+    }
+    const RectMat R = tr ? RectMat{M.m, rows, cols, 1, M.nb, M.neg}
+                         : RectMat{M.m, rows, cols, M.nb, 1, M.neg};
+    rect_solve(R, nullptr, nullptr, nullptr, tr, M.na, rx, lds, lds_bytes, gws, err);
 }
 
 }  // namespace yta
