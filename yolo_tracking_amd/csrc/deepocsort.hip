@@ -54,7 +54,8 @@ struct DocCounters {
     int lap_calls, fast_path;
     int n_ema;
     int err;
-    int pad[18];
+    int lap_done;                  // first round solved by k_doc_lap this frame
+    int pad[17];
 };
 static_assert(sizeof(DocCounters) == 128, "DocCounters layout");
 
@@ -514,6 +515,18 @@ __global__ __launch_bounds__(OC_T) void k_doc_rowpre(DocArgs a) {
                  a.pre_s2 + db);
 }
 
+// First-round solve, one LAP_T-thread block per stream (ocsort_common.hpp first_round_lap).
+__global__ __launch_bounds__(LAP_T) void k_doc_lap(DocArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    const int s = blockIdx.x;
+    DocCounters *c = a.cnt + s;
+    const long long tb = (long long)s * a.CAP, db = (long long)s * a.MAXD;
+    first_round_lap(a.mat2 + doc_mb(a, s), c->n_high, c->n_trk, a.rmatch + db, a.cmatched + tb, true,
+                    a.pre_u + db, a.pre_x + db, a.pre_s2 + db, a.rmatch + db, lds,
+                    lap_kernel_lds(a.CAP, a.MAXD), a.lap_ws + s * a.lap_ws_stride, &c->err,
+                    &c->lap_done);
+}
+
 __global__ __launch_bounds__(OC_T) void k_doc_assoc(DocArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     __shared__ OcShared sh;
@@ -533,6 +546,8 @@ __global__ __launch_bounds__(OC_T) void k_doc_assoc(DocArgs a) {
     int *udet = a.udet + ub, *utrk = a.utrk + ub;
     int n_ud = 0, n_ut = 0;
     auto hbox = [&](int i) { return box5(din + (long long)a.hi_row[db + i] * 6); };
+    YTA_STAMP_BASE(40);
+    YTA_STAMP(0);
     // ---- first round (association.py:111-201)
     if (n_trk == 0) {
         for (int i = t; i < n_hi; i += nt) udet[i] = i;
@@ -551,7 +566,8 @@ __global__ __launch_bounds__(OC_T) void k_doc_assoc(DocArgs a) {
         if (over) atomicAdd(&sh.cnt[0], over);
         if (bad) atomicOr(&sh.cnt[1], 1);
         block_sync();
-        const bool fast = sh.cnt[1] == 0 && sh.cnt[0] > 0;
+        const bool solved = c->lap_done != 0;   // by k_*_lap
+        const bool fast = !solved && sh.cnt[1] == 0 && sh.cnt[0] > 0;
         if (fast) {
             for (int i = t; i < n_hi; i += nt) {
                 int col = -1;
@@ -561,11 +577,12 @@ __global__ __launch_bounds__(OC_T) void k_doc_assoc(DocArgs a) {
                 a.rmatch[db + i] = col;
             }
             block_sync();
-        } else if (n_hi > 0) {
+        } else if (n_hi > 0 && !solved) {
             block_sync();
             main_lap(LapMat{mat2, n_hi, n_trk, false}, a.pre_u + db, a.pre_x + db, a.pre_s2 + db,
                      a.rmatch + db, lds, lds_bytes, gws, &c->err);
         }
+        YTA_STAMP(1);
         if (t == 0) { c->fast_path = fast; c->lap_calls = (fast || n_hi == 0) ? 0 : 1; }
         for (int j = t; j < n_trk; j += nt) a.cmatched[tb + j] = 0;
         block_sync();
@@ -594,6 +611,7 @@ __global__ __launch_bounds__(OC_T) void k_doc_assoc(DocArgs a) {
         n_ut += nf;
         block_sync();
     }
+    YTA_STAMP(2);
     // ---- OCR round (:470-493): asso_func(left dets, last observations), no embedding term
     if (n_ud > 0 && n_ut > 0) {
         const long long nm = (long long)n_ud * n_ut;
@@ -634,6 +652,7 @@ __global__ __launch_bounds__(OC_T) void k_doc_assoc(DocArgs a) {
             block_sync();
         }
     }
+    YTA_STAMP(3);
     // ---- tracker updates; embedding jobs for k_doc_ema
     const long long eb = (long long)s * (a.CAP + a.MAXD);
     const int n_upd = block_compact(n_trk, sh.wsum, [&](int j) { return a.upd[tb + j] >= 0; },
@@ -648,6 +667,7 @@ __global__ __launch_bounds__(OC_T) void k_doc_assoc(DocArgs a) {
         doc_update(r, row >= 0 ? din + (long long)row * 6 : nullptr, row, dt);
     }
     block_sync();
+    YTA_STAMP(4);
     // ---- births in unmatched-list order (:495-503)
     int n_free = c->n_free;
     int n_b = n_ud;
@@ -667,6 +687,7 @@ __global__ __launch_bounds__(OC_T) void k_doc_assoc(DocArgs a) {
     n_free -= n_b;
     n_trk += n_b;
     block_sync();
+    YTA_STAMP(5);
     // ---- outputs in reversed tracker order, then removal (:505-520); ids as stored (:513)
     double *out = a.out + tb * 8;
     const int n_out = block_compact(
@@ -710,6 +731,7 @@ __global__ __launch_bounds__(OC_T) void k_doc_assoc(DocArgs a) {
         c->next_id = next_id + n_b;
         if (a.out_counts) a.out_counts[s] = n_out;
     }
+    YTA_STAMP(7);
 }
 
 // update_emb (deep_ocsort.py:243-245) for every tracker updated this frame - emb = alpha emb +
@@ -885,6 +907,8 @@ int doc_alloc(yta_deepocsort *e) {
     YTA_HIP(hipHostMalloc((void **)&e->h_wh, sizeof(int) * 2 * S, hipHostMallocDefault));
     YTA_HIP(hipHostMalloc((void **)&e->h_warp, sizeof(double) * 6 * S, hipHostMallocDefault));
     YTA_HIP(hipHostMalloc((void **)&e->h_cnt, sizeof(DocCounters) * S, hipHostMallocDefault));
+    YTA_HIP(hipFuncSetAttribute((const void *)k_doc_lap, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)LAP_LDS_MAX));
     YTA_HIP(hipFuncSetAttribute((const void *)k_doc_assoc,
                                 hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)dense_lap_ws_bytes(OC_LDS_LAP_N)));
@@ -939,6 +963,9 @@ int doc_launch(yta_deepocsort *e, const double *d_dets, const int *d_off, const 
                            dim3(OC_T), 0, e->stream, a);
         YTA_HIP(hipGetLastError());
     }
+    hipLaunchKernelGGL(k_doc_lap, dim3(a.S), dim3(LAP_T), (size_t)lap_kernel_lds(a.CAP, a.MAXD),
+                       e->stream, a);
+    YTA_HIP(hipGetLastError());
     hipLaunchKernelGGL(k_doc_assoc, dim3(a.S), dim3(OC_T), e->lds, e->stream, a);
     YTA_HIP(hipGetLastError());
     if (!a.embedding_off) {
@@ -1349,5 +1376,12 @@ int yta_deepocsort_hip_stream(yta_deepocsort *e, void **stream) {
     *stream = (void *)e->stream;
     return YTA_OK;
 }
+
+#ifdef YTA_STAMPS
+int yta_deepocsort_debug_stamps(unsigned long long *out) {
+    YTA_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 128));
+    return YTA_OK;
+}
+#endif
 
 }  // extern "C"

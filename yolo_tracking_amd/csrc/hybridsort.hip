@@ -66,7 +66,8 @@ struct HsCounters {
     int lap_calls, corrections;
     int n_ema;
     int err;
-    int pad[18];
+    int lap_done;                  // first round solved by k_hs_lap this frame
+    int pad[17];
 };
 static_assert(sizeof(HsCounters) == 128, "HsCounters layout");
 
@@ -488,6 +489,18 @@ __global__ __launch_bounds__(OC_T) void k_hs_rowpre(HsArgs a) {
                  a.pre_s2 + db);
 }
 
+// First-round solve, one LAP_T-thread block per stream (ocsort_common.hpp first_round_lap).
+__global__ __launch_bounds__(LAP_T) void k_hs_lap(HsArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    const int s = blockIdx.x;
+    HsCounters *c = a.cnt + s;
+    const long long tb = (long long)s * a.CAP, db = (long long)s * a.MAXD;
+    first_round_lap(a.cost + hs_mb(a, s), c->n_high, c->n_trk, a.rmatch + db, a.cmatched + tb, false,
+                    a.pre_u + db, a.pre_x + db, a.pre_s2 + db, a.rmatch + db, lds,
+                    lap_kernel_lds(a.CAP, a.MAXD), a.lap_ws + s * a.lap_ws_stride, &c->err,
+                    &c->lap_done);
+}
+
 __global__ __launch_bounds__(OC_T) void k_hs_assoc(HsArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     __shared__ OcShared sh;
@@ -510,6 +523,8 @@ __global__ __launch_bounds__(OC_T) void k_hs_assoc(HsArgs a) {
     int n_corr = 0;
     // dets[p] (x1, y1, x2, y2, score) of kept detection p: input row hi_row[p]
     auto hrow = [&](int p) { return din + (long long)a.hi_row[db + p] * 6; };
+    YTA_STAMP_BASE(40);
+    YTA_STAMP(0);
     // ---- first round (association.py:495-581)
     if (n_trk == 0 || n_hi == 0) {
         for (int i = t; i < n_hi; i += nt) udet[i] = i;
@@ -520,8 +535,10 @@ __global__ __launch_bounds__(OC_T) void k_hs_assoc(HsArgs a) {
         block_sync();
     } else {
         block_sync();
-        main_lap(LapMat{cost, n_hi, n_trk, false}, a.pre_u + db, a.pre_x + db, a.pre_s2 + db,
+        if (!c->lap_done)   // else solved by k_hs_lap
+            main_lap(LapMat{cost, n_hi, n_trk, false}, a.pre_u + db, a.pre_x + db, a.pre_s2 + db,
                  a.rmatch + db, lds, lds_bytes, gws, &c->err);
+        YTA_STAMP(1);
         if (t == 0) c->lap_calls = 1;
         for (int j = t; j < n_trk; j += nt) a.cmatched[tb + j] = 0;
         block_sync();
@@ -559,6 +576,7 @@ __global__ __launch_bounds__(OC_T) void k_hs_assoc(HsArgs a) {
         n_ut += n_corr;
         block_sync();
     }
+    YTA_STAMP(2);
     // first-round updates with features (:462-464); feature jobs for k_hs_ema
     const long long eb = (long long)s * (a.CAP + a.MAXD);
     const int n_upd = block_compact(n_trk, sh.wsum, [&](int j) { return a.upd[tb + j] >= 0; },
@@ -575,6 +593,7 @@ __global__ __launch_bounds__(OC_T) void k_hs_assoc(HsArgs a) {
         }
     }
     block_sync();
+    YTA_STAMP(3);
     // ---- OCR round (:512-542): asso_func(left dets, last observations), no feature update
     if (n_ud > 0 && n_ut > 0) {
         const long long nm = (long long)n_ud * n_ut;
@@ -618,9 +637,11 @@ __global__ __launch_bounds__(OC_T) void k_hs_assoc(HsArgs a) {
             block_sync();
         }
     }
+    YTA_STAMP(4);
     // ---- misses (:544-545)
     for (int k = t; k < n_ut; k += nt) hs_update(a.rec[tb + list[utrk[k]]], nullptr, 0.0, 0.0, dt);
     block_sync();
+    YTA_STAMP(5);
     // ---- births in unmatched-list order (:548-550)
     int n_free = c->n_free;
     int n_b = n_ud;
@@ -641,6 +662,7 @@ __global__ __launch_bounds__(OC_T) void k_hs_assoc(HsArgs a) {
     n_free -= n_b;
     n_trk += n_b;
     block_sync();
+    YTA_STAMP(6);
     // ---- outputs in reversed tracker order, then removal (:551-570); ids + 1 (:563)
     double *out = a.out + tb * 8;
     const int n_out = block_compact(
@@ -685,6 +707,7 @@ __global__ __launch_bounds__(OC_T) void k_hs_assoc(HsArgs a) {
         c->next_id = next_id + n_b;
         if (a.out_counts) a.out_counts[s] = n_out;
     }
+    YTA_STAMP(7);
 }
 
 // ---------------------------------------------------------------------------------- k_hs_ema
@@ -860,6 +883,8 @@ int hs_alloc(yta_hybridsort *e) {
     HSALLOC(e->d_off, S + 1);
     YTA_HIP(hipHostMalloc((void **)&e->h_off, sizeof(int) * (S + 1), hipHostMallocDefault));
     YTA_HIP(hipHostMalloc((void **)&e->h_cnt, sizeof(HsCounters) * S, hipHostMallocDefault));
+    YTA_HIP(hipFuncSetAttribute((const void *)k_hs_lap, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)LAP_LDS_MAX));
     YTA_HIP(hipFuncSetAttribute((const void *)k_hs_assoc,
                                 hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)dense_lap_ws_bytes(OC_LDS_LAP_N)));
@@ -895,6 +920,9 @@ int hs_launch(yta_hybridsort *e, const double *d_dets, const int *d_off, const f
                            dim3(OC_T), 0, e->stream, a);
         YTA_HIP(hipGetLastError());
     }
+    hipLaunchKernelGGL(k_hs_lap, dim3(a.S), dim3(LAP_T), (size_t)lap_kernel_lds(a.CAP, a.MAXD),
+                       e->stream, a);
+    YTA_HIP(hipGetLastError());
     hipLaunchKernelGGL(k_hs_assoc, dim3(a.S), dim3(OC_T), e->lds, e->stream, a);
     YTA_HIP(hipGetLastError());
     const dim3 gj((a.CAP + a.MAXD + 3) / 4, a.S);
@@ -1288,5 +1316,12 @@ int yta_hybridsort_hip_stream(yta_hybridsort *e, void **stream) {
     *stream = (void *)e->stream;
     return YTA_OK;
 }
+
+#ifdef YTA_STAMPS
+int yta_hybridsort_debug_stamps(unsigned long long *out) {
+    YTA_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 128));
+    return YTA_OK;
+}
+#endif
 
 }  // extern "C"

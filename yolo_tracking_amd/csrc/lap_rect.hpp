@@ -93,7 +93,7 @@ __device__ __forceinline__ void rect_row_pre(const RectMat M, int i, double *u, 
 
 struct RectRed {
     double b, ma, mo;
-    int sink, ja, ya, pad;
+    int sink, key;   // key = ja << 16 | ya (columns, rows < 32768)
 };
 struct RectShared {
     RectRed slot[2][16];
@@ -103,15 +103,44 @@ struct RectShared {
 __device__ __forceinline__ void rect_lex_min(double &v, int &k, double ov, int ok) {
     if (ov < v || (ov == v && ok < k)) { v = ov; k = ok; }
 }
+template <int CTRL>
+__device__ __forceinline__ void dpp_lex_min(double &v, int &k) {
+    const double ov = dpp_f64<CTRL>(v);
+    const int ok = dpp_i32<CTRL>(k);
+    rect_lex_min(v, k, ov, ok);
+}
+template <int CTRL>
+__device__ __forceinline__ void dpp_fmin(double &v) {
+    const double ov = dpp_f64<CTRL>(v);
+    v = ov < v ? ov : v;
+}
+// Wave-uniform lexicographic minima of (a, ka), (b, kb) and the minimum of m: DPP within each
+// 16-lane row (quad_perm, row_ror), then the four row results by readlane.
+__device__ __forceinline__ void wave_rect_reduce(double &a, int &ka, double &b, int &kb, double &m) {
+    dpp_lex_min<0xB1>(a, ka); dpp_lex_min<0xB1>(b, kb); dpp_fmin<0xB1>(m);
+    dpp_lex_min<0x4E>(a, ka); dpp_lex_min<0x4E>(b, kb); dpp_fmin<0x4E>(m);
+    dpp_lex_min<0x124>(a, ka); dpp_lex_min<0x124>(b, kb); dpp_fmin<0x124>(m);
+    dpp_lex_min<0x128>(a, ka); dpp_lex_min<0x128>(b, kb); dpp_fmin<0x128>(m);
+    double ra = readlane_f64(a, 0), rb = readlane_f64(b, 0), rm = readlane_f64(m, 0);
+    int rka = __builtin_amdgcn_readlane(ka, 0), rkb = __builtin_amdgcn_readlane(kb, 0);
+#pragma unroll
+    for (int L = 16; L < WAVE; L += 16) {
+        rect_lex_min(ra, rka, readlane_f64(a, L), __builtin_amdgcn_readlane(ka, L));
+        rect_lex_min(rb, rkb, readlane_f64(b, L), __builtin_amdgcn_readlane(kb, L));
+        const double om = readlane_f64(m, L);
+        rm = om < rm ? om : rm;
+    }
+    a = ra; ka = rka; b = rb; kb = rkb; m = rm;
+}
 
 // Solve.  pre_u / pre_x / pre_s2: the row pre-pass (global, or nullptr: computed here).  Returns 0,
 // or -2 if a row cannot reach a free column (rows > cols, or NaN costs).  On return w.x[i] is the
 // column of row i.  All threads of the block must call it; blockDim.x * CPT >= M.cols.
 template <int CPT>
-__device__ __noinline__ int lap_rect_block(const RectMat M, const double *pre_u, const int *pre_x,
+__device__ __forceinline__ int lap_rect_body(const RectMat M, const double *pre_u, const int *pre_x,
                                            const double *pre_s2, RectWs w, RectShared &sh) {
     const int t = threadIdx.x, nt = blockDim.x, wid = t / WAVE, nw = nt / WAVE;
-    constexpr int CH = CPT < 8 ? CPT : 8;
+    constexpr int CH = CPT <= 16 ? CPT : 8;   // loads in flight per chunk
     const int rows = M.rows, cols = M.cols;
     if (rows <= 0) return 0;
     if (rows > cols) return -2;
@@ -151,6 +180,7 @@ __device__ __noinline__ int lap_rect_block(const RectMat M, const double *pre_u,
             w.yw[j] = y[q];
         }
     }
+    YTA_STAMP_ABS(104);
     const int nfree = block_compact(rows, sh.wsum, [&](int i) { return w.x[i] < 0; },
                                     [&](int i, int pos) { w.fl[pos] = i; });
     block_sync();
@@ -158,6 +188,7 @@ __device__ __noinline__ int lap_rect_block(const RectMat M, const double *pre_u,
     // ---- 3. augment the free rows
     for (int f = 0; f < nfree; ++f) {
         const int cur = w.fl[f];
+        YTA_COUNT(100);
 #pragma unroll
         for (int q = 0; q < CPT; ++q) spc[q] = INFINITY;
         rel = 0u;
@@ -166,6 +197,10 @@ __device__ __noinline__ int lap_rect_block(const RectMat M, const double *pre_u,
         int sink = -1;
         bool done = false;
         for (int guard = 0; guard <= rows && !done; ++guard) {
+            YTA_COUNT(101);
+#ifdef YTA_STAMPS
+            const unsigned long long ts0 = wall_clock64();
+#endif
             double lb = INFINITY, lma = INFINITY, lmo = INFINITY;
             int lsink = INT_MAX, lja = INT_MAX, lya = -1;
             // row costs in chunks of 8 columns (loads of a chunk in flight together)
@@ -197,28 +232,31 @@ __device__ __noinline__ int lap_rect_block(const RectMat M, const double *pre_u,
                     }
                 }
             }
-            // wave, then block: lexicographic (B, sink), (ma, ja) carrying ya, min mo
-#pragma unroll
-            for (int s = 32; s >= 1; s >>= 1) {
-                const double ob = __shfl_xor(lb, s), oma = __shfl_xor(lma, s), omo = __shfl_xor(lmo, s);
-                const int osk = __shfl_xor(lsink, s), oja = __shfl_xor(lja, s), oya = __shfl_xor(lya, s);
-                rect_lex_min(lb, lsink, ob, osk);
-                if (oma < lma || (oma == lma && oja < lja)) { lma = oma; lja = oja; lya = oya; }
-                lmo = omo < lmo ? omo : lmo;
-            }
-            if (lane_id() == 0) sh.slot[par][wid] = RectRed{lb, lma, lmo, lsink, lja, lya, 0};
+#ifdef YTA_STAMPS
+            const unsigned long long ts1 = wall_clock64();
+            if (blockIdx.x == 0 && t == 0) g_stamps[102] += ts1 - ts0;
+#endif
+            // wave (DPP), then block: lexicographic (B, sink), (ma, ja) with ya packed into the
+            // key, min mo; one barrier (the slots alternate between steps)
+            int lkey = lja == INT_MAX ? INT_MAX : ((lja << 16) | lya);
+            wave_rect_reduce(lb, lsink, lma, lkey, lmo);
+            if (lane_id() == 0) sh.slot[par][wid] = RectRed{lb, lma, lmo, lsink, lkey};
             __syncthreads();
             B = INFINITY;
             sink = INT_MAX;
             double ma = INFINITY, mo = INFINITY;
-            int ja = INT_MAX, ya = -1;
+            int key = INT_MAX;
             for (int k = 0; k < nw; ++k) {
                 const RectRed r = sh.slot[par][k];
                 rect_lex_min(B, sink, r.b, r.sink);
-                if (r.ma < ma || (r.ma == ma && r.ja < ja)) { ma = r.ma; ja = r.ja; ya = r.ya; }
+                rect_lex_min(ma, key, r.ma, r.key);
                 mo = r.mo < mo ? r.mo : mo;
             }
+            const int ja = key == INT_MAX ? INT_MAX : key >> 16, ya = key & 0xFFFF;
             par ^= 1;
+#ifdef YTA_STAMPS
+            if (blockIdx.x == 0 && t == 0) g_stamps[103] += wall_clock64() - ts1;
+#endif
 #pragma unroll
             for (int q = 0; q < CPT; ++q) {
                 const int j = t + q * nt;
@@ -267,13 +305,28 @@ __device__ __noinline__ int lap_rect_block(const RectMat M, const double *pre_u,
             }
         }
     }
+    YTA_STAMP_ABS(105);
     return 0;
 }
 
-// Dispatch on the columns per thread.  Returns -3 when cols exceeds the register tiles.
+template <int CPT>
+__device__ __noinline__ int lap_rect_block(const RectMat M, const double *pre_u, const int *pre_x,
+                                           const double *pre_s2, RectWs w, RectShared &sh) {
+    return lap_rect_body<CPT>(M, pre_u, pre_x, pre_s2, w, sh);
+}
+
+// Dispatch on the columns per thread (blockDim.x <= MAXT).  Returns -3 when cols exceeds the
+// register tiles.
+template <int MAXT = 256>
 __device__ __forceinline__ int lap_rect(const RectMat M, const double *pre_u, const int *pre_x,
                                         const double *pre_s2, RectWs w, RectShared &sh) {
     const int nt = blockDim.x;
+    if (MAXT > 256) {   // the solve kernels: inlined, registers allocated for these bodies, no calls
+        if (M.cols <= 2 * nt) return lap_rect_body<2>(M, pre_u, pre_x, pre_s2, w, sh);
+        if (M.cols <= 8 * nt) return lap_rect_body<8>(M, pre_u, pre_x, pre_s2, w, sh);
+        if (M.cols <= 16 * nt) return lap_rect_body<16>(M, pre_u, pre_x, pre_s2, w, sh);
+        return -3;
+    }
     if (M.cols <= 2 * nt) return lap_rect_block<2>(M, pre_u, pre_x, pre_s2, w, sh);
     if (M.cols <= 8 * nt) return lap_rect_block<8>(M, pre_u, pre_x, pre_s2, w, sh);
     if (M.cols <= RECT_CPT_MAX * nt) return lap_rect_block<RECT_CPT_MAX>(M, pre_u, pre_x, pre_s2, w, sh);

@@ -54,7 +54,8 @@ struct OcCounters {                // one per stream
     int n_dets, n_high, n_second, n_out, n_births;
     int lap_calls, fast_path;
     int err;
-    int pad[18];
+    int lap_done;                  // first round solved by k_oc_lap this frame
+    int pad[17];
 };
 static_assert(sizeof(OcCounters) == 128, "OcCounters layout");
 
@@ -319,6 +320,18 @@ __global__ __launch_bounds__(OC_T) void k_oc_rowpre(OcArgs a) {
     main_lap_pre(a.mat2 + mb, c->n_high, c->n_trk, a.pre_u + db, a.pre_x + db, a.pre_s2 + db);
 }
 
+// First-round solve, one LAP_T-thread block per stream (ocsort_common.hpp first_round_lap).
+__global__ __launch_bounds__(LAP_T) void k_oc_lap(OcArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    const int s = blockIdx.x;
+    OcCounters *c = a.cnt + s;
+    const long long tb = (long long)s * a.CAP, db = (long long)s * a.MAXD;
+    first_round_lap(a.mat2 + (long long)s * (a.MAXD > 4 ? a.MAXD : 4) * a.CAP, c->n_high, c->n_trk, a.rmatch + db, a.cmatched + tb, true,
+                    a.pre_u + db, a.pre_x + db, a.pre_s2 + db, a.rmatch + db, lds,
+                    lap_kernel_lds(a.CAP, a.MAXD), a.lap_ws + s * a.lap_ws_stride, &c->err,
+                    &c->lap_done);
+}
+
 __global__ __launch_bounds__(OC_T) void k_oc_assoc(OcArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     __shared__ OcShared sh;
@@ -369,7 +382,8 @@ __global__ __launch_bounds__(OC_T) void k_oc_assoc(OcArgs a) {
         if (bad) atomicOr(&sh.cnt[1], 1);
         block_sync();
         YTA_STAMP(3);
-        const bool fast = sh.cnt[1] == 0 && sh.cnt[0] > 0;
+        const bool solved = c->lap_done != 0;   // by k_*_lap
+        const bool fast = !solved && sh.cnt[1] == 0 && sh.cnt[0] > 0;
         if (fast) {
             for (int i = t; i < n_hi; i += nt) {
                 int col = -1;
@@ -379,7 +393,7 @@ __global__ __launch_bounds__(OC_T) void k_oc_assoc(OcArgs a) {
                 a.rmatch[db + i] = col;
             }
             block_sync();
-        } else if (n_hi > 0) {
+        } else if (n_hi > 0 && !solved) {
             block_sync();
             main_lap(LapMat{mat2, n_hi, n_trk, false}, a.pre_u + db, a.pre_x + db, a.pre_s2 + db,
                      a.rmatch + db, lds, lds_bytes, gws, &c->err);
@@ -689,6 +703,8 @@ int oc_alloc(yta_ocsort *e) {
     YTA_HIP(hipHostMalloc((void **)&e->h_off, sizeof(int) * (S + 1), hipHostMallocDefault));
     YTA_HIP(hipHostMalloc((void **)&e->h_wh, sizeof(int) * 2 * S, hipHostMallocDefault));
     YTA_HIP(hipHostMalloc((void **)&e->h_cnt, sizeof(OcCounters) * S, hipHostMallocDefault));
+    YTA_HIP(hipFuncSetAttribute((const void *)k_oc_lap, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)LAP_LDS_MAX));
     YTA_HIP(hipFuncSetAttribute((const void *)k_oc_assoc, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)dense_lap_ws_bytes(OC_LDS_LAP_N)));
     return YTA_OK;
@@ -722,6 +738,9 @@ int oc_launch(yta_ocsort *e, const double *d_dets, const int *d_off, const int *
     const long long rows = (a.MAXD + OC_T / WAVE - 1) / (OC_T / WAVE);
     hipLaunchKernelGGL(k_oc_rowpre, dim3((unsigned)std::max<long long>(1, std::min(rows, cap)), a.S),
                        dim3(OC_T), 0, e->stream, a);
+    YTA_HIP(hipGetLastError());
+    hipLaunchKernelGGL(k_oc_lap, dim3(a.S), dim3(LAP_T), (size_t)lap_kernel_lds(a.CAP, a.MAXD),
+                       e->stream, a);
     YTA_HIP(hipGetLastError());
     hipLaunchKernelGGL(k_oc_assoc, dim3(a.S), dim3(OC_T), e->lds, e->stream, a);
     YTA_HIP(hipGetLastError());

@@ -138,4 +138,54 @@ __device__ __forceinline__ void iou_lap(const LapMat &M, int *rx, unsigned char 
     rect_solve(R, nullptr, nullptr, nullptr, tr, M.na, rx, lds, lds_bytes, gws, err);
 }
 
+constexpr int LAP_T = 512;                      // threads of the first-round solve kernels
+constexpr long long LAP_LDS_MAX = 156 * 1024;   // their dynamic LDS cap (160 KiB - static)
+
+__host__ __device__ inline long long lap_kernel_lds(long long CAP, long long MAXD) {
+    const long long b = rect_ws_bytes(MAXD, CAP);
+    return b < LAP_LDS_MAX ? b : LAP_LDS_MAX;
+}
+
+// First-round solve in its own launch, one LAP_T-thread block per stream (up to 16 columns per
+// thread: 8192 trackers, every cost load of a step in flight at once).  When trackers >= detections and
+// the fast path (association.py:156-159, `fast_rule`) does not apply, solve with lap_rect
+// (warm-started by the row pre-pass) into rx and set *done; the association kernel then skips its
+// own first-round solve.  rcnt / ccnt: the per-row / per-column counts of asso > thr (rcnt may
+// alias rx: it is read before the solve).
+__device__ __forceinline__ void first_round_lap(const double *mat, int na, int nb, const int *rcnt,
+                                                const int *ccnt, bool fast_rule, const double *pu,
+                                                const int *px, const double *ps2, int *rx,
+                                                unsigned char *lds, long long lds_bytes,
+                                                unsigned char *gws, int *err, int *done) {
+    __shared__ RectShared rsh;
+    __shared__ int flags[2];
+    const int t = threadIdx.x, nt = blockDim.x;
+    bool solve = na > 0 && na <= nb && nb <= 16 * nt;
+    if (solve && fast_rule) {
+        if (t < 2) flags[t] = 0;
+        __syncthreads();
+        int over = 0, bad = 0;
+        for (int i = t; i < na; i += nt) {
+            const int k = rcnt[i];
+            over |= k;
+            bad |= k > 1;
+        }
+        for (int j = t; j < nb; j += nt) bad |= ccnt[j] > 1;
+        if (over) atomicOr(&flags[0], 1);
+        if (bad) atomicOr(&flags[1], 1);
+        __syncthreads();
+        if (flags[1] == 0 && flags[0]) solve = false;   // the fast path
+    }
+    if (!solve) {
+        if (t == 0) *done = 0;
+        return;
+    }
+    unsigned char *base = rect_ws_bytes(na, nb) <= lds_bytes ? lds : gws;
+    const RectWs w = rect_ws(base, na, nb);
+    const int rc = lap_rect<LAP_T>(RectMat{mat, na, nb, nb, 1, false}, pu, px, ps2, w, rsh);
+    if (rc && t == 0) atomicOr(err, ERR_SOLVER);
+    for (int i = t; i < na; i += nt) rx[i] = rc ? -1 : w.x[i];
+    if (t == 0) *done = 1;
+}
+
 }  // namespace yta
