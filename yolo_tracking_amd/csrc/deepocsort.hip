@@ -80,6 +80,7 @@ struct DocArgs {
     int *nan_flag, *cslot;          // [S*CAP]
     double *mat, *mat2, *emat;      // [S*MAXD*CAP]: asso, cost, embedding cost
     double *rw, *cw;                // [S*MAXD], [S*CAP] AW weights
+    double *cw_part;                // [S*AW_CHUNKS*CAP*2] per-row-chunk column top-2
     int *rmatch, *cmatched;
     int *udet, *utrk, *tmp;         // [S*(MAXD+CAP)]
     int *upd;                       // [S*CAP] update source per tracker (input row) or -1
@@ -263,6 +264,24 @@ __device__ void doc_birth(DocTrack &out, const double *dr, long long id, int det
     out = r;
 }
 
+// CMC (deep_ocsort.py:385-389), then predict (:269-293) of every tracker, chip-wide; k_doc_pre
+// compacts the survivors per stream.
+__global__ __launch_bounds__(256) void k_doc_predict(DocArgs a) {
+    const int s = blockIdx.y;
+    const DocCounters *c = a.cnt + s;
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= c->n_trk) return;
+    const long long tb = (long long)s * a.CAP;
+    const double *aff = a.warp ? a.warp + 6LL * s : nullptr;
+    DocTrack &r = a.rec[tb + a.list[tb + i]];
+    if (!a.cmc_off && aff) doc_apply_affine(r, aff, a.delta_t);   // identity when no warp is given
+    doc_predict(r);
+    double b[4];
+    doc_x_to_bbox(r.kf.x, b);
+    a.nan_flag[tb + i] = (b[0] != b[0]) || (b[1] != b[1]) || (b[2] != b[2]) || (b[3] != b[3]);
+    a.cbox[tb + i] = Box{b[0], b[1], b[2], b[3]};
+}
+
 __global__ __launch_bounds__(OC_T) void k_doc_pre(DocArgs a) {
     __shared__ OcShared sh;
     const int s = blockIdx.x, t = threadIdx.x, nt = blockDim.x;
@@ -278,18 +297,7 @@ __global__ __launch_bounds__(OC_T) void k_doc_pre(DocArgs a) {
     int n_trk = c->n_trk;
     const int dt = a.delta_t;
     int *list = a.list + tb;
-    // CMC (:385-389), then predict (:269-293)
-    const double *aff = a.warp ? a.warp + 6LL * s : nullptr;
-    for (int i = t; i < n_trk; i += nt) {
-        DocTrack &r = a.rec[tb + list[i]];
-        if (!a.cmc_off && aff) doc_apply_affine(r, aff, dt);   // identity when no warp is given
-        doc_predict(r);
-        double b[4];
-        doc_x_to_bbox(r.kf.x, b);
-        a.nan_flag[tb + i] = (b[0] != b[0]) || (b[1] != b[1]) || (b[2] != b[2]) || (b[3] != b[3]);
-        a.cbox[tb + i] = Box{b[0], b[1], b[2], b[3]};
-    }
-    block_sync();
+    // CMC + predict ran chip-wide in k_doc_predict
     {
         int n_free = c->n_free;
         const int n_nan = block_compact(n_trk, sh.wsum, [&](int i) { return a.nan_flag[tb + i] != 0; },
@@ -450,11 +458,16 @@ __device__ __forceinline__ double aw_weight(double m1, double m2, double bottom,
     ex = ex > 0 ? ex : 0.0;   // max(..., 0)
     return 1 - ex / (1 - bottom);
 }
+// compute_aw_max_metric (association.py:79-108) on emb (zeroed where iou <= 0).  Rows: one wave
+// per detection row.  Columns: AW_CHUNKS row chunks x 64-column tiles, 4 waves per tile (lanes =
+// columns, coalesced rows), partial top-2 merged in LDS, then k_doc_aw_cols merges the chunks
+// (top-2 selection is exact and order-free).
+constexpr int AW_CHUNKS = 8;
 __global__ __launch_bounds__(256) void k_doc_aw(DocArgs a) {
     const int s = blockIdx.y;
     const DocCounters *c = a.cnt + s;
     const int n_trk = c->n_trk, n_hi = c->n_high;
-    const long long tb = (long long)s * a.CAP, db = (long long)s * a.MAXD, mb = doc_mb(a, s);
+    const long long db = (long long)s * a.MAXD, mb = doc_mb(a, s);
     const double *E = a.emat + mb, *I = a.mat + mb;
     const int lane = lane_id(), wv = threadIdx.x / WAVE;
     const int row_blocks = (a.MAXD + 3) / 4;
@@ -474,12 +487,52 @@ __global__ __launch_bounds__(256) void k_doc_aw(DocArgs a) {
         }
         if (lane == 0) a.rw[db + r] = aw_weight(m1, m2, a.aw_param, n_trk);
     } else {
-        const int cc = ((int)blockIdx.x - row_blocks) * 256 + threadIdx.x;
-        if (cc >= n_trk) return;
+        __shared__ double part[4][WAVE][2];
+        const int q = (int)blockIdx.x - row_blocks;
+        const int tile = q / AW_CHUNKS, chunk = q % AW_CHUNKS;
+        const int cc = tile * WAVE + lane;
+        const int per = (n_hi + AW_CHUNKS - 1) / AW_CHUNKS;
+        const int r0 = chunk * per, r1 = r0 + per < n_hi ? r0 + per : n_hi;
         double m1 = -INFINITY, m2 = -INFINITY;
-        for (int r = 0; r < n_hi; ++r) top2_push(val(r, cc), m1, m2);
-        a.cw[tb + cc] = aw_weight(m1, m2, a.aw_param, n_hi);
+        if (cc < n_trk) {
+            int r = r0 + wv;
+            for (; r + 12 < r1; r += 16) {   // 4 independent rows per step
+                const double v0 = val(r, cc), v1 = val(r + 4, cc), v2 = val(r + 8, cc),
+                             v3 = val(r + 12, cc);
+                top2_push(v0, m1, m2);
+                top2_push(v1, m1, m2);
+                top2_push(v2, m1, m2);
+                top2_push(v3, m1, m2);
+            }
+            for (; r < r1; r += 4) top2_push(val(r, cc), m1, m2);
+        }
+        part[wv][lane][0] = m1;
+        part[wv][lane][1] = m2;
+        __syncthreads();
+        if (wv == 0 && cc < n_trk) {
+            for (int k = 1; k < 4; ++k) {
+                top2_push(part[k][lane][0], m1, m2);
+                top2_push(part[k][lane][1], m1, m2);
+            }
+            double *o = a.cw_part + ((long long)s * AW_CHUNKS + chunk) * a.CAP * 2 + 2LL * cc;
+            o[0] = m1;
+            o[1] = m2;
+        }
     }
+}
+__global__ __launch_bounds__(256) void k_doc_aw_cols(DocArgs a) {
+    const int s = blockIdx.y;
+    const DocCounters *c = a.cnt + s;
+    const int n_trk = c->n_trk, n_hi = c->n_high;
+    const int cc = blockIdx.x * blockDim.x + threadIdx.x;
+    if (cc >= n_trk) return;
+    double m1 = -INFINITY, m2 = -INFINITY;
+    for (int k = 0; k < AW_CHUNKS; ++k) {
+        const double *o = a.cw_part + ((long long)s * AW_CHUNKS + k) * a.CAP * 2 + 2LL * cc;
+        top2_push(o[0], m1, m2);
+        top2_push(o[1], m1, m2);
+    }
+    a.cw[(long long)s * a.CAP + cc] = aw_weight(m1, m2, a.aw_param, n_hi);
 }
 
 // final cost -(iou + angle + emb_term) (association.py:170); emb_term = ((w rw) cw) emb (AW) or
@@ -884,6 +937,7 @@ int doc_alloc(yta_deepocsort *e) {
     DOCALLOC(a.emat, S * mat);
     DOCALLOC(a.rw, S * MAXD);
     DOCALLOC(a.cw, S * CAP);
+    DOCALLOC(a.cw_part, S * AW_CHUNKS * CAP * 2);
     DOCALLOC(a.rmatch, S * MAXD);
     DOCALLOC(a.pre_u, S * MAXD);
     DOCALLOC(a.pre_s2, S * MAXD);
@@ -937,6 +991,8 @@ int doc_launch(yta_deepocsort *e, const double *d_dets, const int *d_off, const 
     a.img_wh = d_wh;
     a.out = out;
     a.out_counts = out_counts;
+    hipLaunchKernelGGL(k_doc_predict, dim3((a.CAP + 255) / 256, a.S), dim3(256), 0, e->stream, a);
+    YTA_HIP(hipGetLastError());
     hipLaunchKernelGGL(k_doc_pre, dim3(a.S), dim3(OC_T), 0, e->stream, a);
     YTA_HIP(hipGetLastError());
     const long long per = ((long long)a.MAXD * a.CAP + OC_T - 1) / OC_T;
@@ -949,8 +1005,11 @@ int doc_launch(yta_deepocsort *e, const double *d_dets, const int *d_off, const 
         hipLaunchKernelGGL(k_doc_emb, ge, dim3(256), 0, e->stream, a);
         YTA_HIP(hipGetLastError());
         if (!a.aw_off) {
-            const dim3 ga((a.MAXD + 3) / 4 + (a.CAP + 255) / 256, a.S);
+            const dim3 ga((a.MAXD + 3) / 4 + (a.CAP + WAVE - 1) / WAVE * AW_CHUNKS, a.S);
             hipLaunchKernelGGL(k_doc_aw, ga, dim3(256), 0, e->stream, a);
+            YTA_HIP(hipGetLastError());
+            hipLaunchKernelGGL(k_doc_aw_cols, dim3((a.CAP + 255) / 256, a.S), dim3(256), 0,
+                               e->stream, a);
             YTA_HIP(hipGetLastError());
         }
     }

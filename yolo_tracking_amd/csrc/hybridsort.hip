@@ -258,6 +258,30 @@ __device__ void hs_birth(HsTrack &out, const double *bbox, double cls, double de
     out = r;
 }
 
+// predict (hybridsort.py:406-413) of every tracker, chip-wide: boxes and scores into the column
+// records (by list position); k_hs_pre compacts the survivors per stream.
+__global__ __launch_bounds__(256) void k_hs_predict(HsArgs a) {
+    const int s = blockIdx.y;
+    HsCounters *c = a.cnt + s;
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= c->n_trk) return;
+    const long long tb = (long long)s * a.CAP;
+    HsTrack &r = a.rec[tb + a.list[tb + i]];
+    double b[4], ks, ss;
+    hs_predict(r, b, ks, ss);
+    const double sc = r.kf.x[3];
+    const bool nan = (b[0] != b[0]) || (b[1] != b[1]) || (b[2] != b[2]) || (b[3] != b[3]) ||
+                     (sc != sc);
+    if (!nan && !(fabs(b[0]) < INFINITY && fabs(b[1]) < INFINITY && fabs(b[2]) < INFINITY &&
+                  fabs(b[3]) < INFINITY && fabs(sc) < INFINITY))
+        atomicOr(&c->err, ERR_INF_ROW);
+    a.nan_flag[tb + i] = nan;
+    HsCol &q = a.col[tb + i];
+    for (int k = 0; k < 4; ++k) q.box[k] = b[k];
+    q.kscore = ks;
+    (void)ss;   // simple score: trks[:, 5], read only by the BYTE round (use_byte = False)
+}
+
 __global__ __launch_bounds__(OC_T) void k_hs_pre(HsArgs a) {
     __shared__ OcShared sh;
     const int s = blockIdx.x, t = threadIdx.x, nt = blockDim.x;
@@ -274,24 +298,7 @@ __global__ __launch_bounds__(OC_T) void k_hs_pre(HsArgs a) {
     const int dt = a.delta_t;
     int *list = a.list + tb;
     HsCol *col = a.col + tb;
-    // predict (:406-413): boxes and scores into the column records (by list position)
-    for (int i = t; i < n_trk; i += nt) {
-        HsTrack &r = a.rec[tb + list[i]];
-        double b[4], ks, ss;
-        hs_predict(r, b, ks, ss);
-        const double sc = r.kf.x[3];
-        const bool nan = (b[0] != b[0]) || (b[1] != b[1]) || (b[2] != b[2]) || (b[3] != b[3]) ||
-                         (sc != sc);
-        if (!nan && !(fabs(b[0]) < INFINITY && fabs(b[1]) < INFINITY && fabs(b[2]) < INFINITY &&
-                      fabs(b[3]) < INFINITY && fabs(sc) < INFINITY))
-            atomicOr(&c->err, ERR_INF_ROW);
-        a.nan_flag[tb + i] = nan;
-        HsCol &q = col[i];
-        for (int k = 0; k < 4; ++k) q.box[k] = b[k];
-        q.kscore = ks;
-        (void)ss;   // simple score: trks[:, 5], read only by the BYTE round (use_byte = False)
-    }
-    block_sync();
+    // predict ran chip-wide in k_hs_predict
     {
         int n_free = c->n_free;
         const int n_nan = block_compact(n_trk, sh.wsum, [&](int i) { return a.nan_flag[tb + i] != 0; },
@@ -908,6 +915,8 @@ int hs_launch(yta_hybridsort *e, const double *d_dets, const int *d_off, const f
     a.det_feat = d_feat;
     a.out = out;
     a.out_counts = out_counts;
+    hipLaunchKernelGGL(k_hs_predict, dim3((a.CAP + 255) / 256, a.S), dim3(256), 0, e->stream, a);
+    YTA_HIP(hipGetLastError());
     hipLaunchKernelGGL(k_hs_pre, dim3(a.S), dim3(OC_T), 0, e->stream, a);
     YTA_HIP(hipGetLastError());
     const dim3 ge((a.CAP + HE_TILE - 1) / HE_TILE, (a.MAXD + HE_TILE - 1) / HE_TILE, a.S);
