@@ -393,6 +393,7 @@ constexpr int REC_PIECES = KF_REC / 2 + 3;
 template <int V>
 __global__ __launch_bounds__(APPLY_T) void k_apply(BtArgs a) {
     __shared__ double2 rec[APPLY_T][REC_PIECES];   // 60-dword rows: no bank conflicts
+    static_assert(APPLY_T % WAVE == 0, "whole waves per block (LDS-direct load tiling)");
     __shared__ int s_slot[APPLY_T];
     __shared__ int s_wmask[APPLY_T];      // bit 0: write the Kalman record, bit 1: write the meta
     const int s = blockIdx.y, t = threadIdx.x;
@@ -407,54 +408,75 @@ __global__ __launch_bounds__(APPLY_T) void k_apply(BtArgs a) {
     // per-track decision (small loads only)
     // act: 0 predict only, 1 predict + stage-1 update, 2 predict + stage-2 update, 3 predict +
     // mark lost, 4 update (unconfirmed, stage 3), 5 remove (unconfirmed)
-    int slot = -1, det = -1, act = 0, hpos = -1;
-    if (t < nloc) {
-        if (i < n_pool) {
+    // The decision reads a short chain of small arrays; its loads are issued level by level with
+    // the record loads in flight from level 1 on.
+    // level 0 (by pool position): slot, stage-1 row result / leftover index, stage-3 result
+    const bool live = t < nloc, in_pool = i < n_pool;
+    int slot = -1, h = -1, L = -1, r3 = -1;
+    if (live) {
+        if (in_pool) {
             slot = a.pool[tb + i];
-            const int h = a.x1[tb + i];
+            h = a.x1[tb + i];
+            L = a.left_of_pool[tb + i];
+        } else {
+            slot = a.unc[tb + (i - n_pool)];
+            r3 = a.x3[tb + (i - n_pool)];
+        }
+        s_slot[t] = slot;
+    }
+    __syncthreads();
+    // level 1: flags, the stage-1 detection, the stage-2 result
+    const int flags0 = live ? a.flags[tb + slot] : 0;
+    const int det1 = h >= 0 ? a.high[db + h] : -1;
+    const int q2 = h < 0 && L >= 0 ? a.x2[tb + L] : -1;
+    // Cooperative load straight into LDS (global_load_lds_dwordx4: no VGPRs, nothing the compiler
+    // can sink behind the decision chain below): piece p = t + q * APPLY_T is piece p % 15 of
+    // record p / 15, so each wave-instruction writes 1 KiB of rec linearly and consecutive lanes
+    // read consecutive pieces of a record.  All 15 are in flight while the decision runs.
+    {
+        const double2 *kf2 = reinterpret_cast<const double2 *>(a.kf);
+        const double2 *meta2 = reinterpret_cast<const double2 *>(a.meta);
+        char *ldsb = reinterpret_cast<char *>(&rec[0][0]);
+        const int wb = __builtin_amdgcn_readfirstlane(t & ~(WAVE - 1));
+#pragma unroll
+        for (int q = 0; q < REC_PIECES; ++q) {
+            const int p = t + q * APPLY_T;
+            const int r = p / REC_PIECES, k = p - r * REC_PIECES;
+            const long long sl = tb + s_slot[r < nloc ? r : 0];   // rows past nloc: row 0 again
+            const double2 *src = k < 12 ? kf2 + sl * 12 + k : meta2 + sl * 3 + (k - 12);
+            __builtin_amdgcn_global_load_lds((glob_void *)src,
+                                             (lds_void *)(ldsb + (wb + q * APPLY_T) * 16), 16, 0, 0);
+        }
+    }
+    // level 2 (3 for stage 3): the stage-2 / stage-3 detections
+    // act: 0 predict only, 1 predict + stage-1 update, 2 predict + stage-2 update, 3 predict +
+    // mark lost, 4 update (unconfirmed, stage 3), 5 remove (unconfirmed)
+    int det = -1, act = 0, hpos = -1;
+    if (live) {
+        if (in_pool) {
             if (h >= 0) {                                            // stage 1 (:188-196)
                 act = 1;
                 hpos = h;
-                det = a.high[db + h];
-            } else {
-                const int L = a.left_of_pool[tb + i];
-                if (L >= 0) {
-                    const int q = a.x2[tb + L];
-                    if (q >= 0) {                                    // stage 2 (:212-220)
-                        act = 2;
-                        det = a.second[db + q];
-                    } else {
-                        act = 3;                                     // mark_lost (:222-226)
-                    }
+                det = det1;
+            } else if (L >= 0) {
+                if (q2 >= 0) {                                       // stage 2 (:212-220)
+                    act = 2;
+                    det = a.second[db + q2];
+                } else {
+                    act = 3;                                         // mark_lost (:222-226)
                 }
             }
+        } else if (r3 >= 0) {                                        // stage 3 (:234-236)
+            act = 4;
+            hpos = a.rest[db + r3];
+            det = a.high[db + hpos];
         } else {
-            const int j = i - n_pool;
-            slot = a.unc[tb + j];
-            const int r = a.x3[tb + j];
-            if (r >= 0) {                                            // stage 3 (:234-236)
-                act = 4;
-                hpos = a.rest[db + r];
-                det = a.high[db + hpos];
-            } else {
-                act = 5;                                             // :237-240
-            }
+            act = 5;                                                 // :237-240
         }
-        s_slot[t] = slot;
         // BoT-SORT: tracks taking a high detection also take its feature (k_ema)
         if (V == VAR_BOTSORT && a.D > 0) a.ema_job[tb + i] = hpos;
         // pieces this track rewrites: bit 0 the Kalman record, bit 1 the meta
         s_wmask[t] = act == 5 ? 0 : (act == 1 || act == 2 || act == 4 ? 3 : 1);
-    }
-    const int flags0 = t < nloc ? a.flags[tb + slot] : 0;
-    __syncthreads();
-    // cooperative load
-    const double2 *kf2 = reinterpret_cast<const double2 *>(a.kf);
-    const double2 *meta2 = reinterpret_cast<const double2 *>(a.meta);
-    for (int p = t; p < nloc * REC_PIECES; p += APPLY_T) {
-        const int r = p / REC_PIECES, k = p - r * REC_PIECES;
-        const long long sl = tb + s_slot[r];
-        rec[r][k] = k < 12 ? kf2[sl * 12 + k] : meta2[sl * 3 + (k - 12)];   // whole records
     }
     __syncthreads();
     if (t < nloc) {
@@ -912,7 +934,10 @@ struct yta_bytetrack {
 namespace {
 
 constexpr int BT_PHASES = 4;   // launches per frame, see yta_bytetrack_profile_collect
-constexpr size_t BT_LDS_BYTES = 150 * 1024;   // k_stage1 arena (one 1024-thread block per CU)
+#ifndef YTA_LDS1_KB
+#define YTA_LDS1_KB 150
+#endif
+constexpr size_t BT_LDS_BYTES = YTA_LDS1_KB * 1024;   // k_stage1 arena (one 1024-thread block per CU)
 constexpr size_t BT_LDS23_BYTES = 32 * 1024;  // k_stage23 arena (several blocks per CU)
 constexpr size_t BT_LDSF_BYTES = 20 * 1024;   // k_finish dedup arena (several blocks per CU)
 

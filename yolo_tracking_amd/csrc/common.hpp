@@ -37,6 +37,10 @@ int select_device(int device);
 // ------------------------------------------------------------------ device helpers
 constexpr int WAVE = 64;
 
+// address-space-qualified pointers for __builtin_amdgcn_global_load_lds (global -> LDS, no VGPRs)
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(1))) void glob_void;
+
 // Block barrier for kernels that hand data between threads through GLOBAL memory: every wave
 // drains its outstanding vector-memory operations before the barrier.  (__syncthreads() alone
 // lowers to a bare s_barrier on gfx950 for workgroup scope; a global store still in flight could
