@@ -28,7 +28,8 @@ STAGE1 = {2: "dets pass", 4: "tracked/lost pass",
 
 def build():
     os.makedirs(os.path.dirname(OUT), exist_ok=True)
-    srcs = [os.path.join(CSRC, f) for f in ("util.hip", "kat.hip", "bytetrack.hip")]
+    srcs = [os.path.join(CSRC, f) for f in ("util.hip", "kat.hip", "bytetrack.hip", "ocsort.hip",
+                                            "deepocsort.hip", "hybridsort.hip")]
     cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC",
            "-ffp-contract=off", "-fno-fast-math", "-munsafe-fp-atomics", "-DYTA_STAMPS",
            "-shared", "-o", OUT] + srcs
