@@ -376,6 +376,23 @@ int yta_hybridsort_hip_stream(yta_hybridsort *engine, void **stream);
 int yta_kf9_run(int device, int n, int steps, const double *b0, const double *b, double *x_out,
                 double *P_out);
 
+/* ---- GSI post-processing (boxmot/postprocessing/gsi.py; synchronous, host buffers) ----------
+ * linear_interpolation (gsi.py:12-30) of a MOT result table already sorted by (id, frame)
+ * (np.lexsort, stable): rows n x ncol float64 (frame, id, ...); for consecutive rows of one id
+ * with f_pre + 1 < f < f_pre + interval the missing frames are inserted in front of the row as
+ * row_pre + ((row - row_pre) / (f - f_pre)) * i.  virt0 = 1 when the first row's id is -1 (it then
+ * pairs with the reference's initial zero row at frame -1, gsi.py:16).  *n_out = rows of the
+ * result (YTA_ERR_CAPACITY when > out_cap; out is then untouched). */
+int yta_gsi_interpolate(int device, const double *rows, int n, int ncol, int interval, int virt0,
+                        double *out, long long out_cap, long long *n_out);
+/* gaussian_smooth (gsi.py:33-59): per track k (rows track_off[k] .. track_off[k+1]-1 of t / y),
+ * GaussianProcessRegressor(RBF(len_scale[k], 'fixed')).fit(t, y).predict(t) for the 4 columns of
+ * y (n x 4: x, y, w, h) -> out (n x 4).  band_width[k] = max(i - j) over the track's pairs with
+ * (t_i / l - t_j / l)^2 <= 120 (pairs beyond it have K < e^-60 and are dropped).  A kernel matrix
+ * that is not positive definite fails with YTA_ERR_INVALID (sklearn: LinAlgError). */
+int yta_gsi_smooth(int device, const double *t, const double *y, const int *track_off,
+                   const double *len_scale, const int *band_width, int n_tracks, double *out);
+
 #ifdef __cplusplus
 }
 #endif

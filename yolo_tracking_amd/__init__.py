@@ -15,10 +15,11 @@ from .trackers.botsort import BoTSORT, BoTSORTEngine  # noqa: E402
 from .trackers.ocsort import OCSort, OCSortEngine  # noqa: E402
 from .trackers.deepocsort import DeepOCSort, DeepOCSortEngine  # noqa: E402
 from .trackers.hybridsort import HybridSORT, HybridSortEngine  # noqa: E402
+from .postprocessing.gsi import gsi  # noqa: E402
 
 TRACKERS = ["bytetrack", "botsort", "strongsort", "ocsort", "deepocsort", "hybridsort"]
 
 __all__ = ("__version__", "BYTETracker", "ByteTrackEngine", "BoTSORT", "BoTSORTEngine", "OCSort",
            "OCSortEngine", "DeepOCSort", "DeepOCSortEngine", "HybridSORT", "HybridSortEngine",
            "create_tracker",
-           "get_tracker_config", "TRACKERS")
+           "get_tracker_config", "gsi", "TRACKERS")

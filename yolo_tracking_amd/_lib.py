@@ -147,6 +147,8 @@ _SIGS = {
     "yta_hybridsort_stats": ([_P, _P], _I),
     "yta_hybridsort_hip_stream": ([_P, _P], _I),
     "yta_kf9_run": ([_I, _I, _I, _P, _P, _P, _P], _I),
+    "yta_gsi_interpolate": ([_I, _P, _I, _I, _I, _I, _P, ctypes.c_longlong, _P], _I),
+    "yta_gsi_smooth": ([_I, _P, _P, _P, _P, _P, _I, _P], _I),
 }
 
 EXPORTED_SYMBOLS = tuple(_SIGS)
