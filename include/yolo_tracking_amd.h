@@ -193,14 +193,17 @@ int yta_botsort_create(int device, int n_streams, int track_capacity, int max_de
  * yta_bytetrack_update.  feats: for each stream in order, the rows get_features returned for its
  * detections with conf > track_high_thresh, in detection order (float32, feat_dim wide; NULL
  * when with_reid is 0).  warps: S camera-motion 2x3 affines (row-major) or NULL for identity;
- * this version accepts only identity warps (YTA_ERR_INVALID otherwise). */
+ * applied as STrack.multi_gmc (bot_sort.py:95-111) to the predicted pool and the unconfirmed
+ * tracks (:290-295). */
 int yta_botsort_update(yta_botsort *engine, const double *dets, const int *det_offsets,
                        const float *feats, const double *warps, long long *next_id, double *out,
                        int out_capacity, int *out_offsets);
-/* Device-resident update (asynchronous, identity warps): d_feats holds feat_dim floats per
- * detection row of d_dets (only the high rows are read). */
+/* Device-resident update (asynchronous): d_feats holds feat_dim floats per detection row of
+ * d_dets (only the high rows are read); d_warps S row-major 2x3 camera warps (multi_gmc,
+ * bot_sort.py:95-111, 290-295) or NULL for the identity. */
 int yta_botsort_update_device(yta_botsort *engine, const double *d_dets, const int *d_det_offsets,
-                              const float *d_feats, double *d_out, int *d_out_counts);
+                              const float *d_feats, const double *d_warps, double *d_out,
+                              int *d_out_counts);
 /* Parity introspection, in yta_bytetrack_get_state's track order: smoothed features
  * (feat_dim floats per track, may be NULL), class histograms (8 x (class, summed score) float64
  * per track, may be NULL) and their entry counts (may be NULL). */

@@ -162,7 +162,7 @@ def main():
         def step(f):
             _lib.check(fn(eng.handle, ctypes.c_void_p(d_dets.data_ptr() + f * row_bytes),
                           ctypes.c_void_p(d_off.data_ptr() + f * (S + 1) * 4),
-                          ctypes.c_void_p(d_feat.data_ptr() + f * feat_bytes),
+                          ctypes.c_void_p(d_feat.data_ptr() + f * feat_bytes), None,
                           ctypes.c_void_p(d_out.data_ptr()), None))
     for f in range(args.warmup):
         step(f)

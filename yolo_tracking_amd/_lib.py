@@ -111,7 +111,7 @@ _SIGS = {
     "yta_selftest": ([_I], _I),
     "yta_botsort_create": ([_I, _I, _I, _I, _I, _P, _P], _I),
     "yta_botsort_update": ([_P, _P, _P, _P, _P, _P, _P, _I, _P], _I),
-    "yta_botsort_update_device": ([_P, _P, _P, _P, _P, _P], _I),
+    "yta_botsort_update_device": ([_P, _P, _P, _P, _P, _P, _P], _I),
     "yta_botsort_get_features": ([_P, _I, _P, _P, _P, _P], _I),
     "yta_ocsort_create": ([_I, _I, _I, _I, _P, _P], _I),
     "yta_ocsort_destroy": ([_P], _I),

@@ -22,6 +22,7 @@
 //                             (:312-325) through a grid over the lost list, output rows (:270-281),
 //                             free-slot list
 #include <algorithm>
+#include <cmath>
 #include <cstring>
 #include <new>
 #include <vector>
@@ -173,15 +174,35 @@ __device__ __forceinline__ bool stage1_body(const BtArgs &a, int s, Arena &ar, S
     // advanced in k_apply), current for the unconfirmed (not predicted)
     const int n_tracked = c->n_tracked, n_lost = c->n_lost;
     const int *tracked = a.tracked + tb;
+    // BoT-SORT: this frame's camera warp (multi_gmc after multi_predict, bot_sort.py:290-295)
+    const double *H = V == VAR_BOTSORT ? a.warp + 6LL * s : nullptr;
+    const bool gmc = V == VAR_BOTSORT && !warp_is_identity(H);
+    auto warped = [&](double *p) {     // kron(I4, R) on (x, y), (w, h); t on (x, y) (kf_gmc)
+        const double x = p[0], y = p[1], w = p[2], h = p[3];
+        p[0] = (H[0] * x + H[1] * y) + H[2];
+        p[1] = (H[3] * x + H[4] * y) + H[5];
+        p[2] = H[0] * w + H[1] * h;
+        p[3] = H[3] * w + H[4] * h;
+    };
     auto pred_box = [&](long long slot) {
         const double *m = a.kf + slot * KF_REC;
         const bool trk = st_of(a.flags[slot]) == ST_TRACKED;
         const double vh = trk ? m[7] : 0.0;
         if (V == VAR_BOTSORT) {   // multi_predict zeroes vw and vh of non-tracked (:80-93)
-            const double p[4] = {m[0] + m[4], m[1] + m[5], m[2] + (trk ? m[6] : 0.0), m[3] + vh};
+            double p[4] = {m[0] + m[4], m[1] + m[5], m[2] + (trk ? m[6] : 0.0), m[3] + vh};
+            if (gmc) warped(p);
             return xywh_to_box(p);
         }
         return xyah_mean_to_box(m[0] + m[4], m[1] + m[5], m[2] + m[6], m[3] + vh);
+    };
+    auto unc_box_of = [&](long long slot) {   // unconfirmed: not predicted, warped (:295)
+        if (V == VAR_BOTSORT && gmc) {
+            const double *m = a.kf + slot * KF_REC;
+            double p[4] = {m[0], m[1], m[2], m[3]};
+            warped(p);
+            return xywh_to_box(p);
+        }
+        return kf_box<V>(a.kf, slot);
     };
     const int2 au = block_compact2(
         n_tracked, wsum,
@@ -193,7 +214,7 @@ __device__ __forceinline__ bool stage1_body(const BtArgs &a, int s, Arena &ar, S
                 a.pool_box[tb + pos] = pred_box(tb + slot);
             } else {
                 a.unc[tb + pos] = slot;
-                a.unc_box[tb + pos] = kf_box<V>(a.kf, tb + slot);
+                a.unc_box[tb + pos] = unc_box_of(tb + slot);
             }
         });
     const int n_act = au.x, n_unc = au.y;
@@ -372,8 +393,9 @@ __device__ __forceinline__ double vote_cls(double2 *h, int &n, double cls, doubl
 template <int V>
 __device__ __forceinline__ void take_detection(const BtArgs &a, KfState &st, TrackMeta &m,
                                                int &flags, long long det, int det_local, int fid,
-                                               long long slot, int *err) {
-    kf_update<kf_model<V>()>(st, a.det_xyah + det * 4);
+                                               long long slot, int *err, double *xc = nullptr) {
+    if (V == VAR_BOTSORT && xc) kf_update_x(st, xc, a.det_xyah + det * 4);   // warped track
+    else kf_update<kf_model<V>()>(st, a.det_xyah + det * 4);
     const bool reactivate = st_of(flags) != ST_TRACKED;
     m.tracklet_len = reactivate ? 0 : m.tracklet_len + 1;
     flags = (flags & ~FL_STATE) | ST_TRACKED | FL_ACTIVATED;
@@ -486,6 +508,21 @@ __global__ __launch_bounds__(APPLY_T) void k_apply(BtArgs a) {
         memcpy(&m, row + KF_REC, sizeof(TrackMeta));
         int flags = flags0;
         int wmask = 0;
+        // BoT-SORT camera warp (multi_gmc, bot_sort.py:293-295; kf_xyah.hpp): a warped track
+        // carries covariance cross terms in kfx from then on
+        const double *H = V == VAR_BOTSORT ? a.warp + 6LL * s : nullptr;
+        const bool gmc = V == VAR_BOTSORT && !warp_is_identity(H);
+        const bool cross = V == VAR_BOTSORT && act != 5 && (gmc || (flags0 & FL_CROSS));
+        double xc[16];
+        if (V == VAR_BOTSORT && cross) {
+            const double2 *src = reinterpret_cast<const double2 *>(a.kfx + (tb + slot) * 16);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const double2 v = (flags0 & FL_CROSS) ? src[k] : make_double2(0.0, 0.0);
+                xc[2 * k] = v.x;
+                xc[2 * k + 1] = v.y;
+            }
+        }
         if (act <= 3) {
 #pragma unroll
             for (int k = 0; k < 8; ++k) st.m[k] = row[k];
@@ -496,10 +533,16 @@ __global__ __launch_bounds__(APPLY_T) void k_apply(BtArgs a) {
                 st.m[7] = 0;
                 if (V == VAR_BOTSORT) st.m[6] = 0;
             }
-            kf_predict<kf_model<V>()>(st);
+            if (V == VAR_BOTSORT && cross) {
+                kf_predict_x(st, xc);
+                if (gmc) kf_gmc(st, xc, H);
+            } else {
+                kf_predict<kf_model<V>()>(st);
+            }
             wmask = 1;
             if (act == 1 || act == 2) {
-                take_detection<V>(a, st, m, flags, db + det, det, fid, tb + slot, &c->err);
+                take_detection<V>(a, st, m, flags, db + det, det, fid, tb + slot, &c->err,
+                                  cross ? xc : nullptr);
                 wmask = 3;
             } else if (act == 3) {
                 flags = (flags & ~FL_STATE) | ST_LOST;
@@ -511,10 +554,18 @@ __global__ __launch_bounds__(APPLY_T) void k_apply(BtArgs a) {
             for (int k = 0; k < 8; ++k) st.m[k] = row[k];
 #pragma unroll
             for (int k = 0; k < 16; ++k) st.c[k] = row[8 + k];
-            take_detection<V>(a, st, m, flags, db + det, det, fid, tb + slot, &c->err);
+            if (V == VAR_BOTSORT && gmc) kf_gmc(st, xc, H);        // unconfirmed: warped only
+            take_detection<V>(a, st, m, flags, db + det, det, fid, tb + slot, &c->err,
+                              cross ? xc : nullptr);
             wmask = 3;
         } else {
             flags = (flags & ~FL_STATE) | ST_REMOVED | FL_REMOVED_NOW;
+        }
+        if (V == VAR_BOTSORT && cross) {
+            double2 *dst = reinterpret_cast<double2 *>(a.kfx + (tb + slot) * 16);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) dst[k] = make_double2(xc[2 * k], xc[2 * k + 1]);
+            flags |= FL_CROSS;
         }
         if (flags != flags0) a.flags[tb + slot] = flags;
         if (wmask & 1) {
@@ -916,6 +967,7 @@ struct yta_bytetrack {
     float *h_feat = nullptr, *d_feat_in = nullptr;
     long long feat_cap = 0;
     hipStream_t stream = nullptr;
+    double *d_warp = nullptr, *d_warp_id = nullptr;   // BoT-SORT: staged warps / identity warps
     std::vector<void *> allocs;
     BtArgs a{};
     // host staging
@@ -988,6 +1040,18 @@ int bt_alloc(yta_bytetrack *e) {
         a.D = 0;
     }
     DALLOC(a.kf, S * CAP * KF_REC);
+    if (e->variant == VAR_BOTSORT) {
+        DALLOC(a.kfx, S * CAP * 16);
+        DALLOC(e->d_warp, S * 6);
+        DALLOC(e->d_warp_id, S * 6);
+        std::vector<double> id((size_t)S * 6);
+        for (int q = 0; q < S; ++q) {
+            const double h[6] = {1, 0, 0, 0, 1, 0};
+            std::copy(h, h + 6, id.begin() + 6 * q);
+        }
+        YTA_HIP(hipMemcpy(e->d_warp_id, id.data(), sizeof(double) * 6 * S, hipMemcpyHostToDevice));
+        a.warp = e->d_warp_id;
+    }
     DALLOC(a.meta, S * CAP);
     DALLOC(a.flags, S * CAP);
     DALLOC(a.tracked, S * CAP);
@@ -1160,6 +1224,7 @@ int reserve(yta_bytetrack *e, int cap, int maxd) {
         return YTA_OK;
     };
     if (!rc) rc = copy2d(n->a.kf, nc * KF_REC * 8, e->a.kf, oc * KF_REC * 8, oc * KF_REC * 8, S);
+    if (!rc && e->a.kfx) rc = copy2d(n->a.kfx, nc * 16 * 8, e->a.kfx, oc * 16 * 8, oc * 16 * 8, S);
     if (!rc) rc = copy2d(n->a.meta, nc * sizeof(TrackMeta), e->a.meta, oc * sizeof(TrackMeta),
                          oc * sizeof(TrackMeta), S);
     if (!rc) rc = copy2d(n->a.flags, nc * 4, e->a.flags, oc * 4, oc * 4, S);
@@ -1205,6 +1270,8 @@ int reserve(yta_bytetrack *e, int cap, int maxd) {
     n->a.lds_bytes23 = e->a.lds_bytes23;
     n->a.lds_bytes_f = e->a.lds_bytes_f;
     e->a = n->a;
+    e->d_warp = n->d_warp;
+    e->d_warp_id = n->d_warp_id;
     e->h_off = n->h_off;
     e->h_cnt = n->h_cnt;
     e->d_det_off = n->d_det_off;
@@ -1276,8 +1343,20 @@ int create_engine(int device, int n_streams, int track_capacity, int max_dets,
 // Host-buffer update shared by both trackers.  feats (BoT-SORT with ReID): per stream, the rows
 // get_features returned for that stream's high detections (conf > track_high_thresh, in
 // detection order), streams concatenated; staged here aligned with the detection rows.
+static bool identity_warps(const double *w, int S) {
+    if (!w) return true;
+    for (int s = 0; s < S; ++s) {
+        const double *h = w + 6LL * s;
+        if (!(h[0] == 1.0 && h[1] == 0.0 && h[2] == 0.0 && h[3] == 0.0 && h[4] == 1.0 &&
+              h[5] == 0.0))
+            return false;
+    }
+    return true;
+}
+
 int update_host(yta_bytetrack *e, const double *dets, const int *det_offsets, const float *feats,
-                long long *next_id, double *out, int out_capacity, int *out_offsets) {
+                long long *next_id, double *out, int out_capacity, int *out_offsets,
+                const double *warps = nullptr) {
     YTA_CHECK(e && det_offsets && out_offsets, YTA_ERR_INVALID, "null argument");
     YTA_HIP(hipSetDevice(e->device));
     const int S = e->S;
@@ -1293,6 +1372,16 @@ int update_host(yta_bytetrack *e, const double *dets, const int *det_offsets, co
         const int rc = reserve(e, need_c > e->CAP ? std::max(need_c, 2 * e->CAP) : e->CAP,
                                need_d > e->MAXD ? std::max(need_d, 2 * e->MAXD) : e->MAXD);
         if (rc) return rc;
+    }
+    if (e->variant == VAR_BOTSORT) {   // this frame's camera warps (staged after any reserve)
+        e->a.warp = e->d_warp_id;
+        if (warps && !identity_warps(warps, S)) {
+            for (long long k = 0; k < 6LL * S; ++k)
+                YTA_CHECK(std::isfinite(warps[k]), YTA_ERR_INVALID, "non-finite warp entry");
+            YTA_HIP(hipMemcpyAsync(e->d_warp, warps, sizeof(double) * 6 * S,
+                                   hipMemcpyHostToDevice, e->stream));
+            e->a.warp = e->d_warp;
+        }
     }
     const long long total = det_offsets[S];
     YTA_CHECK(total == 0 || dets, YTA_ERR_INVALID, "null dets");
@@ -1485,6 +1574,10 @@ int yta_bytetrack_get_state(yta_bytetrack *e, int stream, int *n_tracks, long lo
     YTA_HIP(hipMemcpy(meta.data(), e->a.meta + tb, sizeof(TrackMeta) * e->CAP,
                       hipMemcpyDeviceToHost));
     YTA_HIP(hipMemcpy(flags.data(), e->a.flags + tb, sizeof(int) * e->CAP, hipMemcpyDeviceToHost));
+    std::vector<double> kfx(e->a.kfx ? (size_t)e->CAP * 16 : 0);
+    if (e->a.kfx)
+        YTA_HIP(hipMemcpy(kfx.data(), e->a.kfx + tb * 16, sizeof(double) * 16 * e->CAP,
+                          hipMemcpyDeviceToHost));
     int n = 0;
     for (int which = 0; which < 2; ++which) {
         const std::vector<int> &lst = which ? lo : tr;
@@ -1502,7 +1595,15 @@ int yta_bytetrack_get_state(yta_bytetrack *e, int stream, int *n_tracks, long lo
             memcpy(st.m, kf.data() + (size_t)slot * KF_REC, sizeof(double) * 8);
             memcpy(st.c, kf.data() + (size_t)slot * KF_REC + 8, sizeof(double) * 16);
             for (int k = 0; k < 8; ++k) mean[(long long)n * 8 + k] = st.m[k];
-            kf_cov_full(st, cov + (long long)n * 64);
+            double *P = cov + (long long)n * 64;
+            kf_cov_full(st, P);
+            if (!kfx.empty() && (flags[slot] & FL_CROSS))   // BoT-SORT warped track
+                for (int g = 0; g < 2; ++g)
+                    for (int k = 0; k < 8; ++k) {
+                        int r, q;
+                        xcross(k, r, q);
+                        P[grp_global(g, r) * 8 + grp_global(g, q)] = kfx[(size_t)slot * 16 + 8 * g + k];
+                    }
             ++n;
         }
     }
@@ -1573,32 +1674,26 @@ int yta_bytetrack_hip_stream(yta_bytetrack *e, void **stream) {
     return YTA_OK;
 }
 
-static bool identity_warps(const double *w, int S) {
-    if (!w) return true;
-    for (int s = 0; s < S; ++s) {
-        const double *h = w + 6LL * s;
-        if (!(h[0] == 1.0 && h[1] == 0.0 && h[2] == 0.0 && h[3] == 0.0 && h[4] == 1.0 &&
-              h[5] == 0.0))
-            return false;
-    }
-    return true;
-}
-
 int yta_botsort_update(yta_botsort *e, const double *dets, const int *det_offsets,
                        const float *feats, const double *warps, long long *next_id, double *out,
                        int out_capacity, int *out_offsets) {
     YTA_CHECK(e && e->variant == VAR_BOTSORT, YTA_ERR_INVALID, "not a BoT-SORT engine");
-    YTA_CHECK(identity_warps(warps, e->S), YTA_ERR_INVALID,
-              "camera-motion warps other than the identity are not supported yet");
-    return update_host(e, dets, det_offsets, feats, next_id, out, out_capacity, out_offsets);
+    const int rc = update_host(e, dets, det_offsets, feats, next_id, out, out_capacity, out_offsets,
+                               warps);
+    e->a.warp = e->d_warp_id;
+    return rc;
 }
 
 int yta_botsort_update_device(yta_botsort *e, const double *d_dets, const int *d_det_offsets,
-                              const float *d_feats, double *d_out, int *d_out_counts) {
+                              const float *d_feats, const double *d_warps, double *d_out,
+                              int *d_out_counts) {
     YTA_CHECK(e && e->variant == VAR_BOTSORT && d_det_offsets && d_out, YTA_ERR_INVALID,
               "null argument / not a BoT-SORT engine");
     YTA_CHECK(e->D == 0 || d_feats, YTA_ERR_INVALID, "null feats");
-    return launch_pipeline(e, d_dets, d_det_offsets, d_out, d_out_counts, d_feats);
+    e->a.warp = d_warps ? d_warps : e->d_warp_id;
+    const int rc = launch_pipeline(e, d_dets, d_det_offsets, d_out, d_out_counts, d_feats);
+    e->a.warp = e->d_warp_id;
+    return rc;
 }
 
 int yta_botsort_get_features(yta_botsort *e, int stream, int *n_tracks, float *feats,

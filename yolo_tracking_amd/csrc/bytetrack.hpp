@@ -12,6 +12,7 @@ constexpr int FL_STATE = 3;
 constexpr int FL_ACTIVATED = 4;      // STrack.is_activated
 constexpr int FL_EVER_REMOVED = 8;   // track_id is in BYTETracker.removed_stracks
 constexpr int FL_REMOVED_NOW = 16;   // marked removed in the current frame (joins removed_stracks at its end)
+constexpr int FL_CROSS = 32;         // BoT-SORT: a camera warp coupled the axes, kfx holds the cross terms
 
 struct TrackMeta {                   // 48 B, one per slot
     double score;
@@ -67,6 +68,8 @@ struct BtArgs {
     const int *det_off;       // S+1
     // persistent state
     double *kf;               // [S*CAP][KF_REC]
+    double *kfx;              // BoT-SORT: [S*CAP][16] covariance cross terms (kf_xyah.hpp, FL_CROSS)
+    const double *warp;       // BoT-SORT: [S][6] this frame's camera warps (multi_gmc), row-major 2x3
     TrackMeta *meta;          // [S*CAP]
     int *flags;               // [S*CAP] state + FL_* bits, dense: every list scan reads these
     int *tracked, *lost, *free_list;   // [S*CAP]

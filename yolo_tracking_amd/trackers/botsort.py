@@ -9,7 +9,8 @@ from the pluggable producers and returns the (K, 8) result.
 The ReID forward pass (reid_multibackend.py) and the CMC estimator (motion/cmc/sof.py) are not part
 of the hot path: pass a `reid` object with `get_features(xyxys, img)` (or the
 frame's embeddings to `update(..., embs=...)`) and, for a moving camera, a `cmc` object with
-`apply(img, dets)` returning the 2x3 warp.  This version accepts identity warps only.
+`apply(img, dets)` returning the 2x3 warp; the engine applies it to the predicted pool and the
+unconfirmed tracks as STrack.multi_gmc does (bot_sort.py:95-111, 290-295).
 """
 import ctypes
 
