@@ -120,6 +120,7 @@ def parse():
     p.add_argument("--streams", type=int, default=1024, help="streams per GPU")
     p.add_argument("--n", type=int, default=1024, help="tracks = detections per frame")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-pcie", action="store_true", help="skip the host-buffer (PCIe) leg")
     p.add_argument("--cpu-frames", type=int, default=40)
     p.add_argument("--seed", type=int, default=1000)
     return p.parse_args()
@@ -153,6 +154,37 @@ def cpu_baseline(n, frames, seed):
     return {"value": res["frames"] / res["seconds"], "unit": "calls/s", "cores": 1, "kind": "port",
             "sample": f"oracle ByteTrack (NumPy + C lapjv), 1 stream {n}x{n}, frames 2..{frames} "
                       f"of seed {seed}, {res['seconds']:.1f} s, 1 thread"}
+
+
+def pcie_inclusive(host, off, S, N, device, frames=8):
+    """The same workload through the host-buffer ABI (yta_bytetrack_update: packed host dets in,
+    output rows back to the host every call, synchronous), on a fresh engine: rank 0's report
+    of the PCIe-inclusive rate.  Never `value`."""
+    from yolo_tracking_amd import ByteTrackEngine, _lib
+    eng = ByteTrackEngine(S, track_thresh=0.5, match_thresh=0.8, track_buffer=30, frame_rate=30,
+                          device=device, track_capacity=2 * N, max_dets=N)
+    lib, h = eng.lib, eng.handle
+    out = np.empty((S * 2 * N, 8))
+    out_off = np.zeros(S + 1, np.int32)
+    nid = np.zeros(S, np.int64)
+    frames = min(frames, len(host))
+    dets = [np.ascontiguousarray(host[f]) for f in range(frames)]
+    offs = [np.ascontiguousarray(off[f]) for f in range(frames)]
+
+    def call(f):
+        _lib.check(lib.yta_bytetrack_update(h, dets[f].ctypes.data, offs[f].ctypes.data,
+                                            nid.ctypes.data, out.ctypes.data, len(out),
+                                            out_off.ctypes.data))
+    call(0)
+    call(1)
+    t0 = time.perf_counter()
+    for f in range(2, frames):
+        call(f)
+    dt = time.perf_counter() - t0
+    return {"value": S * (frames - 2) / dt, "unit": "calls/s", "steps": frames - 2,
+            "ms_per_step": 1000 * dt / (frames - 2),
+            "note": "host-buffer ABI: packed dets host->device and output rows device->host "
+                    "inside every step (pageable numpy buffers)"}
 
 
 def main():
@@ -229,6 +261,7 @@ def main():
                           "gbs": (kernel_bytes(p, st) / (phase_ms[p] * 1e-3) / 1e9
                                   if phase_ms[p] > 0 else 0.0)} for p in PHASES}
         cpu = None if args.no_cpu_baseline else cpu_baseline(N, args.cpu_frames, args.seed)
+        pcie = None if args.no_pcie else pcie_inclusive(host, off, S, N, local_rank)
         traffic, traffic_tag = pmc_traffic(S, N)
         line = {
             "metric": "tracker.update() calls/sec @ 1024 tracks×1024 dets; 1/2/4/8 MI355X",
@@ -245,6 +278,7 @@ def main():
                                             "FETCH_SIZE x2 + WRITE_SIZE)" if traffic else None),
                          "algorithmic_bytes_per_launch": b, "avg_launch_ms": dom_ms},
             "cpu_baseline": cpu,
+            "pcie_inclusive": pcie,
             "per_kernel": per_kernel,
             "frame_counts": st,
             "busiest_kernel": busiest,

@@ -916,6 +916,17 @@ __global__ __launch_bounds__(BLKF) void k_finish(BtArgs a) {
 }
 
 // Rebuild the free-slot list of every stream from its tracked + lost lists (after a reserve).
+// Host-buffer update: every stream's output rows (a.out + s * CAP * 8) packed back to back at the
+// prefix offsets, so one copy returns them.  Block per stream, 16-B pieces.
+__global__ __launch_bounds__(256) void k_pack_out(const double *src, long long cap_rows,
+                                                   const int *off, double *dst) {
+    const int s = blockIdx.x;
+    const long long n2 = (long long)(off[s + 1] - off[s]) * 4;   // double2 pieces
+    const double2 *a = reinterpret_cast<const double2 *>(src + s * cap_rows * 8);
+    double2 *b = reinterpret_cast<double2 *>(dst + (long long)off[s] * 8);
+    for (long long k = threadIdx.x; k < n2; k += blockDim.x) b[k] = a[k];
+}
+
 __global__ __launch_bounds__(BLKF) void k_rebuild_free(BtArgs a) {
     __shared__ int wsum[32];
     extern __shared__ __attribute__((aligned(16))) unsigned int live[];
@@ -972,6 +983,10 @@ struct yta_bytetrack {
     BtArgs a{};
     // host staging
     double *h_dets = nullptr;
+    // host-buffer outputs: the streams' rows packed on the device, one copy back
+    double *d_pack = nullptr, *h_pack = nullptr;
+    int *d_pack_off = nullptr, *h_pack_off = nullptr;
+    long long pack_cap = 0;
     int *h_off = nullptr;
     BtCounters *h_cnt = nullptr;
     double *d_det_in = nullptr;
@@ -1449,14 +1464,33 @@ int update_host(yta_bytetrack *e, const double *dets, const int *det_offsets, co
     YTA_CHECK(rows <= out_capacity, YTA_ERR_CAPACITY, "output needs %lld rows > capacity %d", rows,
               out_capacity);
     YTA_CHECK(rows == 0 || out, YTA_ERR_INVALID, "null out");
-    for (int s = 0; s < S; ++s) {
-        const int n = e->h_cnt[s].n_out;
-        if (n)
-            YTA_HIP(hipMemcpyAsync(out + (long long)out_offsets[s] * 8,
-                                   e->a.out + (long long)s * e->CAP * 8, sizeof(double) * 8 * n,
-                                   hipMemcpyDeviceToHost, e->stream));
+    if (rows > 0) {   // pack on the device, one copy back through pinned staging
+        if (rows > e->pack_cap || !e->d_pack_off) {
+            if (e->d_pack) (void)hipFree(e->d_pack);
+            if (e->h_pack) (void)hipHostFree(e->h_pack);
+            if (e->d_pack_off) (void)hipFree(e->d_pack_off);
+            if (e->h_pack_off) (void)hipHostFree(e->h_pack_off);
+            e->d_pack = e->h_pack = nullptr;
+            e->d_pack_off = e->h_pack_off = nullptr;
+            e->pack_cap = 0;
+            const long long cap = std::max<long long>(2 * rows, 1024);
+            YTA_HIP(hipMalloc((void **)&e->d_pack, sizeof(double) * 8 * cap));
+            YTA_HIP(hipHostMalloc((void **)&e->h_pack, sizeof(double) * 8 * cap, hipHostMallocDefault));
+            YTA_HIP(hipMalloc((void **)&e->d_pack_off, sizeof(int) * (S + 1)));
+            YTA_HIP(hipHostMalloc((void **)&e->h_pack_off, sizeof(int) * (S + 1), hipHostMallocDefault));
+            e->pack_cap = cap;
+        }
+        memcpy(e->h_pack_off, out_offsets, sizeof(int) * (S + 1));
+        YTA_HIP(hipMemcpyAsync(e->d_pack_off, e->h_pack_off, sizeof(int) * (S + 1),
+                               hipMemcpyHostToDevice, e->stream));
+        hipLaunchKernelGGL(k_pack_out, dim3(S), dim3(256), 0, e->stream, e->a.out,
+                           (long long)e->CAP, e->d_pack_off, e->d_pack);
+        YTA_HIP(hipGetLastError());
+        YTA_HIP(hipMemcpyAsync(e->h_pack, e->d_pack, sizeof(double) * 8 * rows,
+                               hipMemcpyDeviceToHost, e->stream));
     }
     YTA_HIP(hipStreamSynchronize(e->stream));
+    if (rows > 0) memcpy(out, e->h_pack, sizeof(double) * 8 * rows);
     if (next_id)
         for (int s = 0; s < S; ++s) next_id[s] = e->h_cnt[s].next_id;
     return YTA_OK;
@@ -1500,6 +1534,10 @@ int yta_bytetrack_destroy(yta_bytetrack *e) {
     release_buffers(e);
     if (e->h_dets) (void)hipHostFree(e->h_dets);
     if (e->d_det_in) (void)hipFree(e->d_det_in);
+    if (e->d_pack) (void)hipFree(e->d_pack);
+    if (e->h_pack) (void)hipHostFree(e->h_pack);
+    if (e->d_pack_off) (void)hipFree(e->d_pack_off);
+    if (e->h_pack_off) (void)hipHostFree(e->h_pack_off);
     if (e->h_feat) (void)hipHostFree(e->h_feat);
     if (e->d_feat_in) (void)hipFree(e->d_feat_in);
     for (hipEvent_t h : e->ev) (void)hipEventDestroy(h);
