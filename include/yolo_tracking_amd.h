@@ -36,9 +36,17 @@
  *   yta_kf_xyah_update       boxmot/motion/kalman_filters/bytetrack_kf.py:194-226 (+ project :126-153)
  *   yta_lap_limited          boxmot/utils/matching.py:56-71 linear_assignment -> lap.lapjv(cost,
  *                            extend_cost=True, cost_limit=thresh)
+ *   yta_gsi_*                boxmot/postprocessing/gsi.py:12-72 linear_interpolation / gaussian_smooth
+ *   yta_reid_preprocess*     boxmot/appearance/reid_multibackend.py:189-224
+ *                            ReIDDetectMultiBackend.preprocess (crop, cv2.resize INTER_LINEAR,
+ *                            BGR -> RGB, ImageNet standardisation, NCHW batch)
+ *   yta_reid_normalize*      boxmot/appearance/reid_multibackend.py:303-311 get_features'
+ *                            `features / np.linalg.norm(features)`
  */
 #ifndef YOLO_TRACKING_AMD_H
 #define YOLO_TRACKING_AMD_H
+
+#include <stdint.h>
 
 #ifdef __cplusplus
 extern "C" {
@@ -395,6 +403,33 @@ int yta_gsi_interpolate(int device, const double *rows, int n, int ncol, int int
  * that is not positive definite fails with YTA_ERR_INVALID (sklearn: LinAlgError). */
 int yta_gsi_smooth(int device, const double *t, const double *y, const int *track_off,
                    const double *len_scale, const int *band_width, int n_tracks, double *out);
+
+/* ---- ReID crop preprocessing (boxmot/appearance/reid_multibackend.py:189-224) ----------------
+ * For each box (x1, y1, x2, y2 float64): box.astype(int) (truncation), x1 = max(0, x1),
+ * y1 = max(0, y1), x2 = min(w - 1, x2), y2 = min(h - 1, y2), crop = img[y1:y2, x1:x2] (Python
+ * slice semantics: a negative stop counts from the end); cv2.resize(crop, (out_w, out_h),
+ * INTER_LINEAR) in OpenCV's fixed-point form (INTER_AREA when both scale factors are exactly 2);
+ * BGR -> RGB; (v / 255 - mean) / std in float64 with the ImageNet mean / std of :214-215; stored as
+ * float32 (half = 0) or float16 (half = 1, the reference's fp16 .to(torch.half)) into
+ * out[n][3][out_h][out_w].  img: h x w x 3 uint8 BGR, row-major.
+ * yta_reid_preprocess: synchronous, host buffers; an empty crop fails with YTA_ERR_INVALID naming
+ * the box (cv2.resize asserts !ssize.empty()) and nothing is written. */
+int yta_reid_preprocess(int device, const uint8_t *img, int h, int w, const double *xyxys, int n,
+                        int out_h, int out_w, int half, void *out);
+/* Asynchronous device-buffer form over a batch of images (one launch for every box of every
+ * camera stream): box b reads image box_img[b] (box_img nullable = image 0) stored at
+ * d_imgs + d_img_off[i] with dims d_img_hw[2 i] (h), d_img_hw[2 i + 1] (w).  An empty crop is
+ * zero-filled and counted into *d_n_empty (nullable; the caller zeroes it).  stream: a
+ * hipStream_t (NULL = the default stream). */
+int yta_reid_preprocess_device(const uint8_t *d_imgs, const long long *d_img_off,
+                               const int *d_img_hw, const double *d_xyxys, const int *d_box_img,
+                               int n, int out_h, int out_w, int half, void *d_out, int *d_n_empty,
+                               void *stream);
+/* get_features (reid_multibackend.py:310): feats[0..count) /= ||feats||_2 over the whole batch,
+ * float32 in place (sum of squares accumulated in float64).  Synchronous, host buffer. */
+int yta_reid_normalize(int device, float *feats, long long count);
+/* Device form: d_work holds >= 256 doubles of scratch. */
+int yta_reid_normalize_device(float *d_feats, long long count, double *d_work, void *stream);
 
 #ifdef __cplusplus
 }

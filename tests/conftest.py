@@ -8,6 +8,14 @@ if REPO not in sys.path:
     sys.path.insert(0, REPO)
 GOLDEN = os.path.join(REPO, "tests", "golden")
 
+# torch bundles its own libamdhip64; importing it before libyta.so is loaded makes the library bind
+# to that same HIP runtime (one runtime per process).  Loading libyta.so first and torch later
+# leaves torch on /opt/rocm's runtime, where it finds no GPU (tests/test_gpu_reid.py needs both).
+try:
+    import torch  # noqa: F401
+except ImportError:   # pragma: no cover
+    pass
+
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs through the HIP C ABI)")

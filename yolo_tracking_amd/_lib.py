@@ -149,6 +149,10 @@ _SIGS = {
     "yta_kf9_run": ([_I, _I, _I, _P, _P, _P, _P], _I),
     "yta_gsi_interpolate": ([_I, _P, _I, _I, _I, _I, _P, ctypes.c_longlong, _P], _I),
     "yta_gsi_smooth": ([_I, _P, _P, _P, _P, _P, _I, _P], _I),
+    "yta_reid_preprocess": ([_I, _P, _I, _I, _P, _I, _I, _I, _I, _P], _I),
+    "yta_reid_preprocess_device": ([_P, _P, _P, _P, _P, _I, _I, _I, _I, _P, _P, _P], _I),
+    "yta_reid_normalize": ([_I, _P, ctypes.c_longlong], _I),
+    "yta_reid_normalize_device": ([_P, ctypes.c_longlong, _P, _P], _I),
 }
 
 EXPORTED_SYMBOLS = tuple(_SIGS)

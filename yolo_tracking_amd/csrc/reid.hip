@@ -1,0 +1,374 @@
+// ReID crop preprocessing and feature normalisation on gfx950: the work
+// boxmot/appearance/reid_multibackend.py does per crop on the CPU before and after the ReID
+// forward pass.
+//
+//   k_reid_crops   [block = (box, band of ROWS output rows), 256 threads]
+//                  preprocess (:189-224): crop rectangle with the reference's truncation / clamp /
+//                  slice semantics, cv2.resize(INTER_LINEAR) in OpenCV's fixed-point form (or the
+//                  INTER_AREA fast path when both scale factors are exactly 2), BGR -> RGB,
+//                  (v / 255 - mean) / std in float64 through a per-block LDS table, float32 or
+//                  float16 stores into out[box][c][y][x] (NCHW), 4 consecutive x per thread
+//   k_feat_sumsq   [grid]  per-block float64 partial sums of squares of the (n, D) features
+//   k_feat_scale   [grid]  every block folds the partials in the same order, norm -> float32,
+//                  features / norm (get_features :310)
+//
+// Multi-image batches: box b reads image box_img[b] (HxWx3 uint8 BGR at imgs + img_off[i], dims
+// img_hw[2i], img_hw[2i+1]).  The kernel is HBM-write bound: each 128 x 256 crop writes 393 KB of
+// float32 and reads a few KB of source pixels (which stay in L2).
+#include <hip/hip_fp16.h>
+
+#include <vector>
+
+#include "common.hpp"
+
+namespace yta {
+namespace {
+
+constexpr int RP_T = 256;       // threads per block
+constexpr int RP_ROWS = 16;     // output rows per block
+constexpr int COEF = 2048;      // INTER_RESIZE_COEF_SCALE
+constexpr int MAX_OUT_W = 1024;
+
+// reid_multibackend.py:214-215 (RGB order)
+__constant__ double c_mean[3] = {0.485, 0.456, 0.406};
+__constant__ double c_std[3] = {0.229, 0.224, 0.225};
+
+struct Rect {
+    int y0, y1, x0, x1;   // rows y0..y1-1, columns x0..x1-1; empty when y1 <= y0 or x1 <= x0
+};
+
+// Python slice stop: a negative stop counts from the end (clamped at 0); a stop past the end is
+// the end.
+__host__ __device__ inline int slice_stop(int stop, int n) {
+    if (stop < 0) stop += n;
+    if (stop < 0) stop = 0;
+    return stop > n ? n : stop;
+}
+__host__ __device__ inline int slice_start(int start, int n) { return start > n ? n : start; }
+
+// reid_multibackend.py:193-199: box.astype('int') (C truncation), max(0, x1), min(w - 1, x2),
+// img[y1:y2, x1:x2]
+__host__ __device__ inline Rect crop_rect(const double *box, int h, int w) {
+    int x1 = (int)box[0], y1 = (int)box[1], x2 = (int)box[2], y2 = (int)box[3];
+    x1 = x1 > 0 ? x1 : 0;
+    y1 = y1 > 0 ? y1 : 0;
+    x2 = x2 < w - 1 ? x2 : w - 1;
+    y2 = y2 < h - 1 ? y2 : h - 1;
+    Rect r;
+    r.x0 = slice_start(x1, w);
+    r.x1 = slice_stop(x2, w);
+    r.y0 = slice_start(y1, h);
+    r.y1 = slice_stop(y2, h);
+    return r;
+}
+
+struct RpArgs {
+    const uint8_t *imgs;
+    const long long *img_off;
+    const int *img_hw;
+    const double *boxes;
+    const int *box_img;   // nullable: every box reads image 0
+    int n, out_h, out_w, half;
+    void *out;
+    int *n_empty;         // nullable: count of empty crops (their output is zero-filled)
+};
+
+__device__ __forceinline__ void store4(void *out, long long idx, float a, float b, float c, float d,
+                                       int half) {
+    if (half) {
+        __half2 p0 = __halves2half2(__float2half_rn(a), __float2half_rn(b));
+        __half2 p1 = __halves2half2(__float2half_rn(c), __float2half_rn(d));
+        uint2 v;
+        v.x = *reinterpret_cast<unsigned *>(&p0);
+        v.y = *reinterpret_cast<unsigned *>(&p1);
+        *reinterpret_cast<uint2 *>((__half *)out + idx) = v;
+    } else {
+        *reinterpret_cast<float4 *>((float *)out + idx) = make_float4(a, b, c, d);
+    }
+}
+
+__device__ __forceinline__ void store1(void *out, long long idx, float a, int half) {
+    if (half)
+        ((__half *)out)[idx] = __float2half_rn(a);
+    else
+        ((float *)out)[idx] = a;
+}
+
+// V = consecutive output columns per thread (4 when out_w % 4 == 0, else 1)
+template <int V>
+__global__ __launch_bounds__(RP_T) void k_reid_crops(RpArgs a) {
+    __shared__ float s_lut[3][256];           // (v / 255 - mean[c]) / std[c] as float32
+    __shared__ int s_sx[MAX_OUT_W];           // source column (crop-relative)
+    __shared__ int s_a0[MAX_OUT_W], s_a1[MAX_OUT_W];
+
+    const int b = blockIdx.x;
+    const int img = a.box_img ? a.box_img[b] : 0;
+    const int h = a.img_hw[2 * img], w = a.img_hw[2 * img + 1];
+    const uint8_t *base = a.imgs + a.img_off[img];
+    const Rect r = crop_rect(a.boxes + 4 * (long long)b, h, w);
+    const int ch = r.y1 - r.y0, cw = r.x1 - r.x0;
+    const int OW = a.out_w, OH = a.out_h;
+    const long long plane = (long long)OH * OW;
+    const long long obase = (long long)b * 3 * plane;
+    const int row0 = blockIdx.y * RP_ROWS;
+    const int nrows = min(RP_ROWS, OH - row0);
+
+    if (ch <= 0 || cw <= 0) {   // cv2.resize refuses an empty source: zero crop, count it
+        for (int e = threadIdx.x; e < 3 * nrows * OW; e += RP_T) {
+            const int c = e / (nrows * OW), rem = e - c * nrows * OW;
+            store1(a.out, obase + c * plane + (long long)row0 * OW + rem, 0.f, a.half);
+        }
+        if (a.n_empty && blockIdx.y == 0 && threadIdx.x == 0) atomicAdd(a.n_empty, 1);
+        return;
+    }
+
+    for (int e = threadIdx.x; e < 768; e += RP_T) {
+        const int c = e >> 8, v = e & 255;
+        s_lut[c][v] = (float)(((double)v / 255.0 - c_mean[c]) / c_std[c]);
+    }
+    // x sampling (resize.cpp resizeGeneric_ setup, INTER_LINEAR)
+    const double scale_x = 1.0 / ((double)OW / (double)cw);
+    const double scale_y = 1.0 / ((double)OH / (double)ch);
+    const bool area2 = fabs(scale_x - 2.0) < 2.220446049250313e-16 &&
+                       fabs(scale_y - 2.0) < 2.220446049250313e-16;
+    if (!area2) {
+        for (int dx = threadIdx.x; dx < OW; dx += RP_T) {
+            float fx = (float)((dx + 0.5) * scale_x - 0.5);
+            int sx = (int)floorf(fx);
+            fx -= (float)sx;
+            int a0, a1;
+            if (sx >= cw - 1) {          // right border: D = S[W-1] * ONE
+                sx = cw - 1;
+                a0 = COEF;
+                a1 = 0;
+            } else {
+                if (sx < 0) {
+                    sx = 0;
+                    fx = 0.f;
+                }
+                a0 = (int)rintf((1.f - fx) * (float)COEF);
+                a1 = (int)rintf(fx * (float)COEF);
+            }
+            s_sx[dx] = sx;
+            s_a0[dx] = a0;
+            s_a1[dx] = a1;
+        }
+    }
+    __syncthreads();
+
+    const int groups = OW / V;                 // column groups per row
+    for (int e = threadIdx.x; e < nrows * groups; e += RP_T) {
+        const int ry = e / groups, dy = row0 + ry, dx0 = (e - ry * groups) * V;
+        float res[3][V];
+        if (area2) {
+            const uint8_t *p0 = base + ((long long)(r.y0 + 2 * dy) * w + r.x0) * 3;
+            const uint8_t *p1 = p0 + (long long)w * 3;
+#pragma unroll
+            for (int k = 0; k < V; ++k) {
+                const int sx = 2 * (dx0 + k);
+#pragma unroll
+                for (int c = 0; c < 3; ++c) {
+                    const int sc = 2 - c;   // BGR -> RGB
+                    const int s = p0[sx * 3 + sc] + p0[sx * 3 + 3 + sc] + p1[sx * 3 + sc] +
+                                  p1[sx * 3 + 3 + sc];
+                    res[c][k] = s_lut[c][(s + 2) >> 2];
+                }
+            }
+        } else {
+            float fy = (float)((dy + 0.5) * scale_y - 0.5);
+            const int sy = (int)floorf(fy);
+            fy -= (float)sy;
+            const int b0 = (int)rintf((1.f - fy) * (float)COEF), b1 = (int)rintf(fy * (float)COEF);
+            const int y0 = min(max(sy, 0), ch - 1), y1 = min(max(sy + 1, 0), ch - 1);
+            const uint8_t *q0 = base + ((long long)(r.y0 + y0) * w + r.x0) * 3;
+            const uint8_t *q1 = base + ((long long)(r.y0 + y1) * w + r.x0) * 3;
+#pragma unroll
+            for (int k = 0; k < V; ++k) {
+                const int dx = dx0 + k;
+                const int sx = s_sx[dx], a0 = s_a0[dx], a1 = s_a1[dx];
+                const int sx1 = min(sx + 1, cw - 1);
+#pragma unroll
+                for (int c = 0; c < 3; ++c) {
+                    const int sc = 2 - c;
+                    const int d0 = q0[sx * 3 + sc] * a0 + q0[sx1 * 3 + sc] * a1;
+                    const int d1 = q1[sx * 3 + sc] * a0 + q1[sx1 * 3 + sc] * a1;
+                    int v = ((((d0 >> 4) * b0) >> 16) + (((d1 >> 4) * b1) >> 16) + 2) >> 2;
+                    v = min(max(v, 0), 255);
+                    res[c][k] = s_lut[c][v];
+                }
+            }
+        }
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            const long long idx = obase + c * plane + (long long)dy * OW + dx0;
+            if (V == 4)
+                store4(a.out, idx, res[c][0], res[c][V > 1 ? 1 : 0], res[c][V > 2 ? 2 : 0],
+                       res[c][V > 3 ? 3 : 0], a.half);
+            else
+                store1(a.out, idx, res[c][0], a.half);
+        }
+    }
+}
+
+constexpr int FN_T = 256, FN_G = 256;
+
+__device__ __forceinline__ double block_sum(double v, double *sh) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
+    if (ln == 0) sh[wv] = v;
+    __syncthreads();
+    double t = 0.0;
+    if (threadIdx.x == 0)
+        for (int i = 0; i < FN_T / 64; ++i) t += sh[i];
+    __syncthreads();
+    return t;   // valid in thread 0
+}
+
+__global__ __launch_bounds__(FN_T) void k_feat_sumsq(const float *f, long long n, double *part) {
+    __shared__ double sh[FN_T / 64];
+    double s = 0.0;
+    for (long long i = blockIdx.x * (long long)FN_T + threadIdx.x; i < n;
+         i += (long long)gridDim.x * FN_T) {
+        const double v = f[i];
+        s += v * v;
+    }
+    s = block_sum(s, sh);
+    if (threadIdx.x == 0) part[blockIdx.x] = s;
+}
+
+__global__ __launch_bounds__(FN_T) void k_feat_scale(float *f, long long n, const double *part,
+                                                     int nparts) {
+    __shared__ double sh[FN_T / 64];
+    __shared__ float s_norm;
+    double s = threadIdx.x < nparts ? part[threadIdx.x] : 0.0;
+    s = block_sum(s, sh);
+    if (threadIdx.x == 0) s_norm = (float)sqrt(s);
+    __syncthreads();
+    const float nrm = s_norm;
+    for (long long i = blockIdx.x * (long long)FN_T + threadIdx.x; i < n;
+         i += (long long)gridDim.x * FN_T)
+        f[i] = f[i] / nrm;
+}
+
+int launch_crops(const RpArgs &a, hipStream_t st) {
+    YTA_CHECK(a.out_w > 0 && a.out_w <= MAX_OUT_W && a.out_h > 0, YTA_ERR_INVALID,
+              "output size %d x %d (width 1..%d)", a.out_w, a.out_h, MAX_OUT_W);
+    if (a.n == 0) return YTA_OK;
+    dim3 grid(a.n, (a.out_h + RP_ROWS - 1) / RP_ROWS);
+    if (a.out_w % 4 == 0)
+        hipLaunchKernelGGL(k_reid_crops<4>, grid, dim3(RP_T), 0, st, a);
+    else
+        hipLaunchKernelGGL(k_reid_crops<1>, grid, dim3(RP_T), 0, st, a);
+    YTA_HIP(hipGetLastError());
+    return YTA_OK;
+}
+
+int launch_normalize(float *d_f, long long n, double *d_part, hipStream_t st) {
+    if (n == 0) return YTA_OK;
+    hipLaunchKernelGGL(k_feat_sumsq, dim3(FN_G), dim3(FN_T), 0, st, d_f, n, d_part);
+    YTA_HIP(hipGetLastError());
+    const int g = (int)((n + FN_T * 4 - 1) / (FN_T * 4));
+    hipLaunchKernelGGL(k_feat_scale, dim3(g < 1024 ? g : 1024), dim3(FN_T), 0, st, d_f, n,
+                       d_part, FN_G);
+    YTA_HIP(hipGetLastError());
+    return YTA_OK;
+}
+
+struct DevBuf {
+    std::vector<void *> ptrs;
+    ~DevBuf() {
+        for (void *p : ptrs) (void)hipFree(p);
+    }
+    hipError_t get(void **p, size_t bytes) {
+        void *q = nullptr;
+        hipError_t e = hipMalloc(&q, bytes ? bytes : 1);
+        if (e == hipSuccess) ptrs.push_back(q);
+        *p = q;
+        return e;
+    }
+};
+
+}  // namespace
+}  // namespace yta
+
+using namespace yta;
+
+extern "C" {
+
+int yta_reid_preprocess(int device, const uint8_t *img, int h, int w, const double *xyxys, int n,
+                        int out_h, int out_w, int half, void *out) {
+    YTA_CHECK(n >= 0 && h > 0 && w > 0 && (half == 0 || half == 1), YTA_ERR_INVALID,
+              "bad arguments (n %d, image %d x %d, half %d)", n, h, w, half);
+    YTA_CHECK(out_w > 0 && out_w <= MAX_OUT_W && out_h > 0, YTA_ERR_INVALID,
+              "output size %d x %d (width 1..%d)", out_w, out_h, MAX_OUT_W);
+    if (n == 0) return YTA_OK;
+    YTA_CHECK(img && xyxys && out, YTA_ERR_INVALID, "null buffer");
+    for (int i = 0; i < n; ++i) {   // cv2.resize asserts !ssize.empty()
+        const Rect r = crop_rect(xyxys + 4 * i, h, w);
+        YTA_CHECK(r.y1 > r.y0 && r.x1 > r.x0, YTA_ERR_INVALID,
+                  "box %d (%g, %g, %g, %g): empty crop in a %d x %d image", i, xyxys[4 * i],
+                  xyxys[4 * i + 1], xyxys[4 * i + 2], xyxys[4 * i + 3], h, w);
+    }
+    int rc = select_device(device);
+    if (rc) return rc;
+    DevBuf m;
+    void *d_img, *d_boxes, *d_out, *d_meta;
+    const size_t img_bytes = (size_t)h * w * 3;
+    const size_t out_bytes = (size_t)n * 3 * out_h * out_w * (half ? 2 : 4);
+    YTA_HIP(m.get(&d_img, img_bytes));
+    YTA_HIP(m.get(&d_boxes, sizeof(double) * 4 * n));
+    YTA_HIP(m.get(&d_out, out_bytes));
+    YTA_HIP(m.get(&d_meta, 16));
+    const long long off0 = 0;
+    const int hw[2] = {h, w};
+    YTA_HIP(hipMemcpy(d_img, img, img_bytes, hipMemcpyHostToDevice));
+    YTA_HIP(hipMemcpy(d_boxes, xyxys, sizeof(double) * 4 * n, hipMemcpyHostToDevice));
+    YTA_HIP(hipMemcpy(d_meta, &off0, 8, hipMemcpyHostToDevice));
+    YTA_HIP(hipMemcpy((char *)d_meta + 8, hw, 8, hipMemcpyHostToDevice));
+    RpArgs a{(const uint8_t *)d_img, (const long long *)d_meta, (const int *)((char *)d_meta + 8),
+             (const double *)d_boxes, nullptr, n, out_h, out_w, half, d_out, nullptr};
+    rc = launch_crops(a, 0);
+    if (rc) return rc;
+    YTA_HIP(hipMemcpy(out, d_out, out_bytes, hipMemcpyDeviceToHost));
+    return YTA_OK;
+}
+
+int yta_reid_preprocess_device(const uint8_t *d_imgs, const long long *d_img_off,
+                               const int *d_img_hw, const double *d_xyxys, const int *d_box_img,
+                               int n, int out_h, int out_w, int half, void *d_out, int *d_n_empty,
+                               void *stream) {
+    YTA_CHECK(n >= 0 && (half == 0 || half == 1), YTA_ERR_INVALID, "bad arguments (n %d, half %d)",
+              n, half);
+    if (n == 0) return YTA_OK;
+    YTA_CHECK(d_imgs && d_img_off && d_img_hw && d_xyxys && d_out, YTA_ERR_INVALID,
+              "null buffer");
+    RpArgs a{d_imgs, d_img_off, d_img_hw, d_xyxys, d_box_img, n, out_h, out_w, half, d_out,
+             d_n_empty};
+    return launch_crops(a, (hipStream_t)stream);
+}
+
+int yta_reid_normalize(int device, float *feats, long long count) {
+    YTA_CHECK(count >= 0, YTA_ERR_INVALID, "bad count %lld", count);
+    if (count == 0) return YTA_OK;
+    YTA_CHECK(feats, YTA_ERR_INVALID, "null features");
+    int rc = select_device(device);
+    if (rc) return rc;
+    DevBuf m;
+    void *d_f, *d_part;
+    YTA_HIP(m.get(&d_f, sizeof(float) * count));
+    YTA_HIP(m.get(&d_part, sizeof(double) * FN_G));
+    YTA_HIP(hipMemcpy(d_f, feats, sizeof(float) * count, hipMemcpyHostToDevice));
+    rc = launch_normalize((float *)d_f, count, (double *)d_part, 0);
+    if (rc) return rc;
+    YTA_HIP(hipMemcpy(feats, d_f, sizeof(float) * count, hipMemcpyDeviceToHost));
+    return YTA_OK;
+}
+
+int yta_reid_normalize_device(float *d_feats, long long count, double *d_work, void *stream) {
+    YTA_CHECK(count >= 0, YTA_ERR_INVALID, "bad count %lld", count);
+    if (count == 0) return YTA_OK;
+    YTA_CHECK(d_feats && d_work, YTA_ERR_INVALID, "null buffer");
+    return launch_normalize(d_feats, count, d_work, (hipStream_t)stream);
+}
+
+}  // extern "C"
