@@ -6,11 +6,14 @@
 //                  preprocess (:189-224): crop rectangle with the reference's truncation / clamp /
 //                  slice semantics, cv2.resize(INTER_LINEAR) in OpenCV's fixed-point form (or the
 //                  INTER_AREA fast path when both scale factors are exactly 2), BGR -> RGB,
-//                  (v / 255 - mean) / std in float64 through a per-block LDS table, float32 or
+//                  (v / 255 - mean) / std through a compile-time table (IEEE float64), float32 or
 //                  float16 stores into out[box][c][y][x] (NCHW), 4 consecutive x per thread
 //   k_feat_sumsq   [grid]  per-block float64 partial sums of squares of the (n, D) features
 //   k_feat_scale   [grid]  every block folds the partials in the same order, norm -> float32,
 //                  features / norm (get_features :310)
+//
+// Output stores are nontemporal (the 393 KB per crop stream past L2; measured 1.14 -> 0.90 ms per
+// 8192-crop launch; -DYTA_REID_CACHED_STORES restores plain stores).
 //
 // Multi-image batches: box b reads image box_img[b] (HxWx3 uint8 BGR at imgs + img_off[i], dims
 // img_hw[2i], img_hw[2i+1]).  The kernel is HBM-write bound: each 128 x 256 crop writes 393 KB of
@@ -25,13 +28,28 @@ namespace yta {
 namespace {
 
 constexpr int RP_T = 256;       // threads per block
-constexpr int RP_ROWS = 16;     // output rows per block
+constexpr int RP_ROWS = 32;     // output rows per block
 constexpr int COEF = 2048;      // INTER_RESIZE_COEF_SCALE
 constexpr int MAX_OUT_W = 1024;
+constexpr int STAGE_BYTES = 24 * 1024;   // LDS for the block's source rows
+constexpr int STAGE_ROWS = 96;
 
-// reid_multibackend.py:214-215 (RGB order)
-__constant__ double c_mean[3] = {0.485, 0.456, 0.406};
-__constant__ double c_std[3] = {0.229, 0.224, 0.225};
+// (v / 255 - mean[c]) / std[c] rounded to float32, v = 0..255, c in RGB order
+// (reid_multibackend.py:211-216: crop / 255, - mean, / std in float64, then .float()).  Evaluated
+// by the compiler in IEEE double, so every entry equals NumPy's.
+struct Lut {
+    float v[3 * 256];
+};
+constexpr Lut make_lut() {
+    Lut l{};
+    constexpr double mean[3] = {0.485, 0.456, 0.406};   // :214
+    constexpr double stdv[3] = {0.229, 0.224, 0.225};   // :215
+    for (int c = 0; c < 3; ++c)
+        for (int v = 0; v < 256; ++v)
+            l.v[c * 256 + v] = (float)(((double)v / 255.0 - mean[c]) / stdv[c]);
+    return l;
+}
+__constant__ Lut c_lut = make_lut();
 
 struct Rect {
     int y0, y1, x0, x1;   // rows y0..y1-1, columns x0..x1-1; empty when y1 <= y0 or x1 <= x0
@@ -81,9 +99,19 @@ __device__ __forceinline__ void store4(void *out, long long idx, float a, float 
         uint2 v;
         v.x = *reinterpret_cast<unsigned *>(&p0);
         v.y = *reinterpret_cast<unsigned *>(&p1);
+#ifndef YTA_REID_CACHED_STORES
+        typedef unsigned u2 __attribute__((ext_vector_type(2)));
+        __builtin_nontemporal_store(u2{v.x, v.y}, reinterpret_cast<u2 *>((__half *)out + idx));
+#else
         *reinterpret_cast<uint2 *>((__half *)out + idx) = v;
+#endif
     } else {
+#ifndef YTA_REID_CACHED_STORES
+        typedef float f4 __attribute__((ext_vector_type(4)));
+        __builtin_nontemporal_store(f4{a, b, c, d}, reinterpret_cast<f4 *>((float *)out + idx));
+#else
         *reinterpret_cast<float4 *>((float *)out + idx) = make_float4(a, b, c, d);
+#endif
     }
 }
 
@@ -94,12 +122,61 @@ __device__ __forceinline__ void store1(void *out, long long idx, float a, int ha
         ((float *)out)[idx] = a;
 }
 
+// cv2 INTER_LINEAR y sampling of output row dy (no border adjustment; rows clamped on use)
+__device__ __forceinline__ void y_sample(int dy, double scale_y, int &sy, int &b0, int &b1) {
+    float fy = (float)((dy + 0.5) * scale_y - 0.5);
+    sy = (int)floorf(fy);
+    fy -= (float)sy;
+    b0 = (int)rintf((1.f - fy) * (float)COEF);
+    b1 = (int)rintf(fy * (float)COEF);
+}
+
+// One output row group (V columns from dx0) of the bilinear path; q0 / q1 address the two source
+// rows (global memory or the LDS copy), crop-relative columns.
+template <int V, typename P>
+__device__ __forceinline__ void bilinear_group(P q0, P q1, int dx0, int b0, int b1, int cw,
+                                               const int *s_sx, const int *s_a, const float *lut,
+                                               float (&res)[3][V]) {
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+        const int dx = dx0 + k;
+        const int sx = s_sx[dx], aa = s_a[dx];
+        const int a0 = aa & 0xffff, a1 = aa >> 16;
+        const int sx1 = min(sx + 1, cw - 1);
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            const int sc = 2 - c;   // BGR -> RGB
+            const int d0 = (int)q0[sx * 3 + sc] * a0 + (int)q0[sx1 * 3 + sc] * a1;
+            const int d1 = (int)q1[sx * 3 + sc] * a0 + (int)q1[sx1 * 3 + sc] * a1;
+            int v = ((((d0 >> 4) * b0) >> 16) + (((d1 >> 4) * b1) >> 16) + 2) >> 2;
+            v = min(max(v, 0), 255);
+            res[c][k] = lut[c * 256 + v];
+        }
+    }
+}
+
+template <int V>
+__device__ __forceinline__ void store_group(void *out, long long obase, long long plane, int dy,
+                                            int OW, int dx0, const float (&res)[3][V], int half) {
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        const long long idx = obase + c * plane + (long long)dy * OW + dx0;
+        if (V == 4)
+            store4(out, idx, res[c][0], res[c][V > 1 ? 1 : 0], res[c][V > 2 ? 2 : 0],
+                   res[c][V > 3 ? 3 : 0], half);
+        else
+            store1(out, idx, res[c][0], half);
+    }
+}
+
 // V = consecutive output columns per thread (4 when out_w % 4 == 0, else 1)
 template <int V>
 __global__ __launch_bounds__(RP_T) void k_reid_crops(RpArgs a) {
-    __shared__ float s_lut[3][256];           // (v / 255 - mean[c]) / std[c] as float32
+    __shared__ float s_lut[3 * 256];
     __shared__ int s_sx[MAX_OUT_W];           // source column (crop-relative)
-    __shared__ int s_a0[MAX_OUT_W], s_a1[MAX_OUT_W];
+    __shared__ int s_a[MAX_OUT_W];            // a0 | a1 << 16
+    __shared__ int s_lead[STAGE_ROWS];        // byte offset of each staged row in its dword run
+    __shared__ __attribute__((aligned(16))) uint8_t s_rows[STAGE_BYTES];
 
     const int b = blockIdx.x;
     const int img = a.box_img ? a.box_img[b] : 0;
@@ -122,45 +199,19 @@ __global__ __launch_bounds__(RP_T) void k_reid_crops(RpArgs a) {
         return;
     }
 
-    for (int e = threadIdx.x; e < 768; e += RP_T) {
-        const int c = e >> 8, v = e & 255;
-        s_lut[c][v] = (float)(((double)v / 255.0 - c_mean[c]) / c_std[c]);
-    }
-    // x sampling (resize.cpp resizeGeneric_ setup, INTER_LINEAR)
+    for (int e = threadIdx.x; e < 3 * 256; e += RP_T) s_lut[e] = c_lut.v[e];
+    // resize.cpp resizeGeneric_ setup (INTER_LINEAR); both factors exactly 2 -> INTER_AREA
     const double scale_x = 1.0 / ((double)OW / (double)cw);
     const double scale_y = 1.0 / ((double)OH / (double)ch);
     const bool area2 = fabs(scale_x - 2.0) < 2.220446049250313e-16 &&
                        fabs(scale_y - 2.0) < 2.220446049250313e-16;
-    if (!area2) {
-        for (int dx = threadIdx.x; dx < OW; dx += RP_T) {
-            float fx = (float)((dx + 0.5) * scale_x - 0.5);
-            int sx = (int)floorf(fx);
-            fx -= (float)sx;
-            int a0, a1;
-            if (sx >= cw - 1) {          // right border: D = S[W-1] * ONE
-                sx = cw - 1;
-                a0 = COEF;
-                a1 = 0;
-            } else {
-                if (sx < 0) {
-                    sx = 0;
-                    fx = 0.f;
-                }
-                a0 = (int)rintf((1.f - fx) * (float)COEF);
-                a1 = (int)rintf(fx * (float)COEF);
-            }
-            s_sx[dx] = sx;
-            s_a0[dx] = a0;
-            s_a1[dx] = a1;
-        }
-    }
-    __syncthreads();
-
     const int groups = OW / V;                 // column groups per row
-    for (int e = threadIdx.x; e < nrows * groups; e += RP_T) {
-        const int ry = e / groups, dy = row0 + ry, dx0 = (e - ry * groups) * V;
-        float res[3][V];
-        if (area2) {
+
+    if (area2) {
+        __syncthreads();
+        for (int e = threadIdx.x; e < nrows * groups; e += RP_T) {
+            const int ry = e / groups, dy = row0 + ry, dx0 = (e - ry * groups) * V;
+            float res[3][V];
             const uint8_t *p0 = base + ((long long)(r.y0 + 2 * dy) * w + r.x0) * 3;
             const uint8_t *p1 = p0 + (long long)w * 3;
 #pragma unroll
@@ -168,45 +219,74 @@ __global__ __launch_bounds__(RP_T) void k_reid_crops(RpArgs a) {
                 const int sx = 2 * (dx0 + k);
 #pragma unroll
                 for (int c = 0; c < 3; ++c) {
-                    const int sc = 2 - c;   // BGR -> RGB
-                    const int s = p0[sx * 3 + sc] + p0[sx * 3 + 3 + sc] + p1[sx * 3 + sc] +
-                                  p1[sx * 3 + 3 + sc];
-                    res[c][k] = s_lut[c][(s + 2) >> 2];
+                    const int sc = 2 - c;
+                    const int sm = p0[sx * 3 + sc] + p0[sx * 3 + 3 + sc] + p1[sx * 3 + sc] +
+                                   p1[sx * 3 + 3 + sc];
+                    res[c][k] = s_lut[c * 256 + ((sm + 2) >> 2)];
                 }
             }
+            store_group<V>(a.out, obase, plane, dy, OW, dx0, res, a.half);
+        }
+        return;
+    }
+
+    for (int dx = threadIdx.x; dx < OW; dx += RP_T) {
+        float fx = (float)((dx + 0.5) * scale_x - 0.5);
+        int sx = (int)floorf(fx);
+        fx -= (float)sx;
+        int a0, a1;
+        if (sx >= cw - 1) {          // right border: D = S[W-1] * ONE
+            sx = cw - 1;
+            a0 = COEF;
+            a1 = 0;
         } else {
-            float fy = (float)((dy + 0.5) * scale_y - 0.5);
-            const int sy = (int)floorf(fy);
-            fy -= (float)sy;
-            const int b0 = (int)rintf((1.f - fy) * (float)COEF), b1 = (int)rintf(fy * (float)COEF);
-            const int y0 = min(max(sy, 0), ch - 1), y1 = min(max(sy + 1, 0), ch - 1);
+            if (sx < 0) {
+                sx = 0;
+                fx = 0.f;
+            }
+            a0 = (int)rintf((1.f - fx) * (float)COEF);
+            a1 = (int)rintf(fx * (float)COEF);
+        }
+        s_sx[dx] = sx;
+        s_a[dx] = a0 | (a1 << 16);
+    }
+
+    // source rows this block reads: clamp(sy(row0)) .. clamp(sy(last) + 1)
+    int sy_a, sy_b, t0, t1;
+    y_sample(row0, scale_y, sy_a, t0, t1);
+    y_sample(row0 + nrows - 1, scale_y, sy_b, t0, t1);
+    const int lo = min(max(sy_a, 0), ch - 1), hi = min(max(sy_b + 1, 0), ch - 1);
+    const int R = hi - lo + 1;
+    const int rs = ((cw * 3 + 3 + 3) / 4) * 4;   // LDS stride: the row's dword run
+    const bool staged = R <= STAGE_ROWS && (long long)R * rs <= STAGE_BYTES;
+    if (staged) {   // dword-aligned runs covering each row's cw * 3 bytes, coalesced
+        const int ndw = rs / 4;
+        for (int e = threadIdx.x; e < R * ndw; e += RP_T) {
+            const int rr = e / ndw, k = e - rr * ndw;
+            const uint8_t *rp = base + ((long long)(r.y0 + lo + rr) * w + r.x0) * 3;
+            const uintptr_t al = (uintptr_t)rp & ~(uintptr_t)3;
+            if (k == 0) s_lead[rr] = (int)((uintptr_t)rp - al);
+            reinterpret_cast<unsigned *>(s_rows + rr * rs)[k] = ((const unsigned *)al)[k];
+        }
+    }
+    __syncthreads();
+
+    for (int e = threadIdx.x; e < nrows * groups; e += RP_T) {
+        const int ry = e / groups, dy = row0 + ry, dx0 = (e - ry * groups) * V;
+        int sy, b0, b1;
+        y_sample(dy, scale_y, sy, b0, b1);
+        const int y0 = min(max(sy, 0), ch - 1), y1 = min(max(sy + 1, 0), ch - 1);
+        float res[3][V];
+        if (staged) {
+            const uint8_t *q0 = s_rows + (y0 - lo) * rs + s_lead[y0 - lo];
+            const uint8_t *q1 = s_rows + (y1 - lo) * rs + s_lead[y1 - lo];
+            bilinear_group<V>(q0, q1, dx0, b0, b1, cw, s_sx, s_a, s_lut, res);
+        } else {
             const uint8_t *q0 = base + ((long long)(r.y0 + y0) * w + r.x0) * 3;
             const uint8_t *q1 = base + ((long long)(r.y0 + y1) * w + r.x0) * 3;
-#pragma unroll
-            for (int k = 0; k < V; ++k) {
-                const int dx = dx0 + k;
-                const int sx = s_sx[dx], a0 = s_a0[dx], a1 = s_a1[dx];
-                const int sx1 = min(sx + 1, cw - 1);
-#pragma unroll
-                for (int c = 0; c < 3; ++c) {
-                    const int sc = 2 - c;
-                    const int d0 = q0[sx * 3 + sc] * a0 + q0[sx1 * 3 + sc] * a1;
-                    const int d1 = q1[sx * 3 + sc] * a0 + q1[sx1 * 3 + sc] * a1;
-                    int v = ((((d0 >> 4) * b0) >> 16) + (((d1 >> 4) * b1) >> 16) + 2) >> 2;
-                    v = min(max(v, 0), 255);
-                    res[c][k] = s_lut[c][v];
-                }
-            }
+            bilinear_group<V>(q0, q1, dx0, b0, b1, cw, s_sx, s_a, s_lut, res);
         }
-#pragma unroll
-        for (int c = 0; c < 3; ++c) {
-            const long long idx = obase + c * plane + (long long)dy * OW + dx0;
-            if (V == 4)
-                store4(a.out, idx, res[c][0], res[c][V > 1 ? 1 : 0], res[c][V > 2 ? 2 : 0],
-                       res[c][V > 3 ? 3 : 0], a.half);
-            else
-                store1(a.out, idx, res[c][0], a.half);
-        }
+        store_group<V>(a.out, obase, plane, dy, OW, dx0, res, a.half);
     }
 }
 
