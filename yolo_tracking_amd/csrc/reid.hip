@@ -7,7 +7,9 @@
 //                  slice semantics, cv2.resize(INTER_LINEAR) in OpenCV's fixed-point form (or the
 //                  INTER_AREA fast path when both scale factors are exactly 2), BGR -> RGB,
 //                  (v / 255 - mean) / std through a compile-time table (IEEE float64), float32 or
-//                  float16 stores into out[box][c][y][x] (NCHW), 4 consecutive x per thread
+//                  float16 stores into out[box][c][y][x] (NCHW), 4 consecutive x per thread;
+//                  the horizontal pass runs once per source row of a band when the band's
+//                  resized rows fit in LDS (int16 D >> 4), else per output row
 //   k_feat_sumsq   [grid]  per-block float64 partial sums of squares of the (n, D) features
 //   k_feat_scale   [grid]  every block folds the partials in the same order, norm -> float32,
 //                  features / norm (get_features :310)
@@ -176,6 +178,7 @@ __global__ __launch_bounds__(RP_T) void k_reid_crops(RpArgs a) {
     __shared__ int s_sx[MAX_OUT_W];           // source column (crop-relative)
     __shared__ int s_a[MAX_OUT_W];            // a0 | a1 << 16
     __shared__ int s_lead[STAGE_ROWS];        // byte offset of each staged row in its dword run
+    // either the band's raw source rows (dword runs) or its horizontally resized rows (int16)
     __shared__ __attribute__((aligned(16))) uint8_t s_rows[STAGE_BYTES];
 
     const int b = blockIdx.x;
@@ -257,6 +260,62 @@ __global__ __launch_bounds__(RP_T) void k_reid_crops(RpArgs a) {
     y_sample(row0 + nrows - 1, scale_y, sy_b, t0, t1);
     const int lo = min(max(sy_a, 0), ch - 1), hi = min(max(sy_b + 1, 0), ch - 1);
     const int R = hi - lo + 1;
+    if (V == 4 && R <= STAGE_BYTES / (6 * OW)) {
+        // Horizontal pass once per source row of the band (HResizeLinear), kept as D >> 4 in
+        // int16 (the SIMD row kernel's v_pack input; <= 255 * 2048 >> 4 fits), then the vertical
+        // pass per output row reads two 8-byte runs per channel.
+        short *hb = reinterpret_cast<short *>(s_rows);   // [R][3][OW]
+        __syncthreads();                                  // x tables
+        for (int e = threadIdx.x; e < R * groups; e += RP_T) {
+            const int rr = e / groups, dx0 = (e - rr * groups) * V;
+            const uint8_t *q = base + ((long long)(r.y0 + lo + rr) * w + r.x0) * 3;
+            short o[3][4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int dx = dx0 + k;
+                const int sx = s_sx[dx], aa = s_a[dx];
+                const int a0 = aa & 0xffff, a1 = aa >> 16;
+                const int sx1 = min(sx + 1, cw - 1);
+#pragma unroll
+                for (int c = 0; c < 3; ++c) {
+                    const int sc = 2 - c;   // BGR -> RGB
+                    o[c][k] = (short)(((int)q[sx * 3 + sc] * a0 + (int)q[sx1 * 3 + sc] * a1) >> 4);
+                }
+            }
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                uint2 v;
+                v.x = (unsigned)(unsigned short)o[c][0] | ((unsigned)(unsigned short)o[c][1] << 16);
+                v.y = (unsigned)(unsigned short)o[c][2] | ((unsigned)(unsigned short)o[c][3] << 16);
+                *reinterpret_cast<uint2 *>(hb + ((long long)rr * 3 + c) * OW + dx0) = v;
+            }
+        }
+        __syncthreads();
+        for (int e = threadIdx.x; e < nrows * groups; e += RP_T) {
+            const int ry = e / groups, dy = row0 + ry, dx0 = (e - ry * groups) * V;
+            int sy, b0, b1;
+            y_sample(dy, scale_y, sy, b0, b1);
+            const int y0 = min(max(sy, 0), ch - 1) - lo, y1 = min(max(sy + 1, 0), ch - 1) - lo;
+            float res[3][V];
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                const uint2 u0 = *reinterpret_cast<const uint2 *>(hb + (y0 * 3 + c) * OW + dx0);
+                const uint2 u1 = *reinterpret_cast<const uint2 *>(hb + (y1 * 3 + c) * OW + dx0);
+                const int h0[4] = {(int)(short)(u0.x & 0xffff), (int)(short)(u0.x >> 16),
+                                   (int)(short)(u0.y & 0xffff), (int)(short)(u0.y >> 16)};
+                const int h1[4] = {(int)(short)(u1.x & 0xffff), (int)(short)(u1.x >> 16),
+                                   (int)(short)(u1.y & 0xffff), (int)(short)(u1.y >> 16)};
+#pragma unroll
+                for (int k = 0; k < V; ++k) {
+                    int v = (((h0[k] * b0) >> 16) + ((h1[k] * b1) >> 16) + 2) >> 2;
+                    v = min(max(v, 0), 255);
+                    res[c][k] = s_lut[c * 256 + v];
+                }
+            }
+            store_group<V>(a.out, obase, plane, dy, OW, dx0, res, a.half);
+        }
+        return;
+    }
     const int rs = ((cw * 3 + 3 + 3) / 4) * 4;   // LDS stride: the row's dword run
     const bool staged = R <= STAGE_ROWS && (long long)R * rs <= STAGE_BYTES;
     if (staged) {   // dword-aligned runs covering each row's cw * 3 bytes, coalesced
