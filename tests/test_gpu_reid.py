@@ -126,3 +126,38 @@ def test_get_features_with_a_device_network():
         raw = net(crops).cpu().numpy()
     np.testing.assert_allclose(feats, orr.global_normalize(raw), rtol=1e-5, atol=1e-7)
     assert reid.get_features(np.empty((0, 4)), img).shape == (0,)
+
+
+def test_botsort_with_device_reid_matches_oracle():
+    """End to end: BoTSORT(reid=ReIDDetectMultiBackend(model=net)) — crops, network and global
+    normalisation on the device feeding the device tracker — against the oracle tracker fed with
+    the oracle's crops through the same network.  Ids / scores / det_ind bit-exact, boxes to 1e-9
+    relative (the features differ only by the normalisation's summation order)."""
+    import torch
+    from oracle.botsort import BoTSORTOracle
+    from yolo_tracking_amd.synth import make_frames
+    from yolo_tracking_amd.trackers.botsort import BoTSORT
+    torch.manual_seed(1)
+    net = torch.nn.Sequential(torch.nn.AvgPool2d(8), torch.nn.Flatten(),
+                              torch.nn.Linear(3 * 32 * 16, 128)).to("cuda:0").eval()
+    params = dict(track_high_thresh=0.5, track_low_thresh=0.1, new_track_thresh=0.6,
+                  track_buffer=30, match_thresh=0.8, proximity_thresh=0.5,
+                  appearance_thresh=0.25, frame_rate=30)
+    n = 64
+    frames = [d for d, _ in make_frames(n, 10, seed=21)]
+    C = int(64 * np.sqrt(n))
+    rng = np.random.default_rng(4)
+    reid = ReIDDetectMultiBackend(device="cuda:0", model=net)
+    t = BoTSORT(None, "cuda:0", False, reid=reid, **params)
+    ref = BoTSORTOracle(**params)
+    for f, dets in enumerate(frames):
+        img = rng.integers(0, 256, (C + 128, C + 128, 3), dtype=np.uint8)
+        got = np.asarray(t.update(dets, img)).reshape(-1, 8)
+        hi = dets[:, 4] > params["track_high_thresh"]
+        with torch.no_grad():
+            raw = net(torch.from_numpy(orr.preprocess(dets[hi, :4], img)).to("cuda:0"))
+        feats = orr.global_normalize(raw.cpu().numpy())
+        exp = ref.update(dets, feats).reshape(-1, 8)
+        assert got.shape == exp.shape, f
+        assert np.array_equal(got[:, 4:], exp[:, 4:]), f
+        np.testing.assert_allclose(got[:, :4], exp[:, :4], rtol=1e-9, atol=1e-6)
