@@ -36,6 +36,8 @@
  *   yta_kf_xyah_update       boxmot/motion/kalman_filters/bytetrack_kf.py:194-226 (+ project :126-153)
  *   yta_lap_limited          boxmot/utils/matching.py:56-71 linear_assignment -> lap.lapjv(cost,
  *                            extend_cost=True, cost_limit=thresh)
+ *   yta_embedding_distance   boxmot/utils/matching.py:145-167 embedding_distance (max(0, cdist cosine))
+ *   yta_aw_max_metric        boxmot/utils/association.py:79-108 compute_aw_max_metric
  *   yta_gsi_*                boxmot/postprocessing/gsi.py:12-72 linear_interpolation / gaussian_smooth
  *   yta_reid_preprocess*     boxmot/appearance/reid_multibackend.py:189-224
  *                            ReIDDetectMultiBackend.preprocess (crop, cv2.resize INTER_LINEAR,
@@ -386,6 +388,16 @@ int yta_hybridsort_hip_stream(yta_hybridsort *engine, void **stream);
  * (n x 81). */
 int yta_kf9_run(int device, int n, int steps, const double *b0, const double *b, double *x_out,
                 double *P_out);
+
+/* embedding_distance (matching.py:145-167): out (n x m) = max(0, 1 - t.d / (|t| |d|)) of float32
+ * track / detection feature rows (dim wide) in float64, through the BoT-SORT engine's cosine. */
+int yta_embedding_distance(int device, const float *track_feats, int n, const float *det_feats,
+                           int m, int dim, double *out);
+/* compute_aw_max_metric (association.py:79-108): out (nr x nc) = ((w * rw_i) * cw_j) * emb_ij with
+ * the row / column weights 1 - max(second / top - bottom, 0) / (1 - bottom) (0 when top == 0, 1
+ * when the row / column has fewer than two entries) — the DeepOCSORT engine's AW code. */
+int yta_aw_max_metric(int device, const double *emb_cost, int nr, int nc, double w_association_emb,
+                      double bottom, double *out);
 
 /* ---- GSI post-processing (boxmot/postprocessing/gsi.py; synchronous, host buffers) ----------
  * linear_interpolation (gsi.py:12-30) of a MOT result table already sorted by (id, frame)

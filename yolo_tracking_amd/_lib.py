@@ -149,6 +149,8 @@ _SIGS = {
     "yta_kf9_run": ([_I, _I, _I, _P, _P, _P, _P], _I),
     "yta_gsi_interpolate": ([_I, _P, _I, _I, _I, _I, _P, ctypes.c_longlong, _P], _I),
     "yta_gsi_smooth": ([_I, _P, _P, _P, _P, _P, _I, _P], _I),
+    "yta_embedding_distance": ([_I, _P, _I, _P, _I, _I, _P], _I),
+    "yta_aw_max_metric": ([_I, _P, _I, _I, ctypes.c_double, ctypes.c_double, _P], _I),
     "yta_reid_preprocess": ([_I, _P, _I, _I, _P, _I, _I, _I, _I, _P], _I),
     "yta_reid_preprocess_device": ([_P, _P, _P, _P, _P, _I, _I, _I, _I, _P, _P, _P], _I),
     "yta_reid_normalize": ([_I, _P, ctypes.c_longlong], _I),
@@ -308,6 +310,28 @@ def kf9_run(b0, b, device=0):
     P = np.empty((n, 9, 9))
     check(load_library().yta_kf9_run(device, n, len(b), ptr(b0), ptr(b), ptr(x), ptr(P)))
     return x, P
+
+
+def embedding_distance(track_feats, det_feats, device=0):
+    """matching.py:145-167 embedding_distance on the device -> (n, m) float64."""
+    t = np.ascontiguousarray(track_feats, dtype=np.float32)
+    d = np.ascontiguousarray(det_feats, dtype=np.float32)
+    n, m = len(t), len(d)
+    out = np.zeros((n, m), dtype=np.float64)
+    if n * m:
+        assert t.shape[1] == d.shape[1]
+        check(load_library().yta_embedding_distance(device, ptr(t), n, ptr(d), m, t.shape[1],
+                                                    ptr(out)))
+    return out
+
+
+def aw_max_metric(emb_cost, w_association_emb, bottom=0.5, device=0):
+    """association.py:79-108 compute_aw_max_metric on the device."""
+    e = np.ascontiguousarray(emb_cost, dtype=np.float64)
+    out = np.empty_like(e)
+    check(load_library().yta_aw_max_metric(device, ptr(e), e.shape[0], e.shape[1],
+                                           float(w_association_emb), float(bottom), ptr(out)))
+    return out
 
 
 def lap_padded(cost, device=0):

@@ -21,6 +21,7 @@
 #include <new>
 #include <vector>
 
+#include "aw.hpp"
 #include "kf_deep.hpp"
 #include "kf_ocsort.hpp"
 #include "ocsort_common.hpp"
@@ -443,21 +444,6 @@ __global__ __launch_bounds__(256) void k_doc_emb(DocArgs a) {
 
 // compute_aw_max_metric (association.py:79-108) on emb[iou <= 0] = 0: the top two values of each
 // row (blockIdx.x < row blocks) or column; one wave per row / per 64 columns.
-__device__ __forceinline__ void top2_push(double v, double &m1, double &m2) {
-    if (v > m1) {
-        m2 = m1;
-        m1 = v;
-    } else if (v > m2) {
-        m2 = v;
-    }
-}
-__device__ __forceinline__ double aw_weight(double m1, double m2, double bottom, int n) {
-    if (n < 2) return 1.0;
-    if (m1 == 0) return 0.0;
-    double ex = (m2 / m1) - bottom;
-    ex = ex > 0 ? ex : 0.0;   // max(..., 0)
-    return 1 - ex / (1 - bottom);
-}
 // compute_aw_max_metric (association.py:79-108) on emb (zeroed where iou <= 0).  Rows: one wave
 // per detection row.  Columns: AW_CHUNKS row chunks x 64-column tiles, 4 waves per tile (lanes =
 // columns, coalesced rows), partial top-2 merged in LDS, then k_doc_aw_cols merges the chunks

@@ -4,6 +4,7 @@
 #include <vector>
 
 #include "assoc.hpp"
+#include "aw.hpp"
 #include "grid.hpp"
 #include "kf_xyah.hpp"
 #include "lap_dense.hpp"
@@ -212,6 +213,42 @@ __global__ __launch_bounds__(1024) void k_selftest(int *err) {
         if (r[0] != mn || r[1] != mx || r[2] != all || r[3] != -mx || r[4] != all || r[5] != nt)
             atomicOr(err, 2);
     }
+}
+
+// embedding_distance (matching.py:145-167): max(0, cdist(track f32, det f32, 'cosine')), one pair
+// per 16-lane row group through the engine's own cosine_dist16 (assoc.hpp)
+__global__ __launch_bounds__(256) void k_emb_dist(const float *tf, int n, const float *df, int m,
+                                                  int D, double *out) {
+    const long long pair = ((long long)blockIdx.x * 256 + threadIdx.x) >> 4;
+    const long long np = (long long)n * m;
+    const long long p = pair < np ? pair : np - 1;   // whole row groups stay for the DPP reduce
+    const int i = (int)(p / m), j = (int)(p - (long long)i * m);
+    const float *dv = df + (long long)j * D;
+    const double cd = cosine_dist16(tf + (long long)i * D, [&](int k) { return dv[k]; }, D);
+    if (pair < np && (threadIdx.x & 15) == 0) out[p] = cd > 0.0 ? cd : 0.0;
+}
+
+// compute_aw_max_metric (association.py:79-108): row and column weights from the top two values
+// (the DeepOCSORT engine's top2_push / aw_weight, aw.hpp), then ((w * rw) * cw) * emb
+__global__ void k_aw_weights(const double *e, int nr, int nc, double bottom, double *rw,
+                             double *cw) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    double m1 = -INFINITY, m2 = -INFINITY;
+    if (t < nr) {
+        for (int c = 0; c < nc; ++c) top2_push(e[(long long)t * nc + c], m1, m2);
+        rw[t] = aw_weight(m1, m2, bottom, nc);
+    } else if (t < nr + nc) {
+        const int c = t - nr;
+        for (int r = 0; r < nr; ++r) top2_push(e[(long long)r * nc + c], m1, m2);
+        cw[c] = aw_weight(m1, m2, bottom, nr);
+    }
+}
+__global__ void k_aw_apply(const double *e, int nr, int nc, double w, const double *rw,
+                           const double *cw, double *out) {
+    const long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= (long long)nr * nc) return;
+    const int r = (int)(q / nc), c = (int)(q - (long long)r * nc);
+    out[q] = ((w * rw[r]) * cw[c]) * e[q];
 }
 
 struct DevBuf {
@@ -495,6 +532,54 @@ int yta_lap_rect(int device, int nr, int nc, const double *cost, int *x, int *y)
     YTA_HIP(hipMemcpy(y, dy, sizeof(int) * nc, hipMemcpyDeviceToHost));
     YTA_HIP(hipMemcpy(&herr, derr, sizeof(int), hipMemcpyDeviceToHost));
     YTA_CHECK(herr == 0, YTA_ERR_HIP, "rectangular assignment solver error flags 0x%x", herr);
+    return YTA_OK;
+}
+
+int yta_embedding_distance(int device, const float *track_feats, int n, const float *det_feats,
+                           int m, int dim, double *out) {
+    YTA_CHECK(n >= 0 && m >= 0 && dim > 0, YTA_ERR_INVALID, "bad sizes (%d, %d, %d)", n, m, dim);
+    if ((long long)n * m == 0) return YTA_OK;
+    YTA_CHECK(track_feats && det_feats && out, YTA_ERR_INVALID, "null buffer");
+    int rc = select_device(device);
+    if (rc) return rc;
+    DevBuf mb;
+    float *dt, *dd;
+    double *dout;
+    const long long np = (long long)n * m;
+    YTA_HIP(mb.get(&dt, (size_t)n * dim));
+    YTA_HIP(mb.get(&dd, (size_t)m * dim));
+    YTA_HIP(mb.get(&dout, np));
+    YTA_HIP(hipMemcpy(dt, track_feats, sizeof(float) * n * dim, hipMemcpyHostToDevice));
+    YTA_HIP(hipMemcpy(dd, det_feats, sizeof(float) * m * dim, hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(k_emb_dist, dim3((unsigned)((np * 16 + 255) / 256)), dim3(256), 0, 0, dt, n,
+                       dd, m, dim, dout);
+    YTA_HIP(hipGetLastError());
+    YTA_HIP(hipMemcpy(out, dout, sizeof(double) * np, hipMemcpyDeviceToHost));
+    return YTA_OK;
+}
+
+int yta_aw_max_metric(int device, const double *emb_cost, int nr, int nc, double w_association_emb,
+                      double bottom, double *out) {
+    YTA_CHECK(nr >= 0 && nc >= 0, YTA_ERR_INVALID, "negative size");
+    const long long q = (long long)nr * nc;
+    if (q == 0) return YTA_OK;
+    YTA_CHECK(emb_cost && out, YTA_ERR_INVALID, "null buffer");
+    int rc = select_device(device);
+    if (rc) return rc;
+    DevBuf mb;
+    double *de, *drw, *dcw, *dout;
+    YTA_HIP(mb.get(&de, q));
+    YTA_HIP(mb.get(&drw, nr));
+    YTA_HIP(mb.get(&dcw, nc));
+    YTA_HIP(mb.get(&dout, q));
+    YTA_HIP(hipMemcpy(de, emb_cost, sizeof(double) * q, hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(k_aw_weights, dim3((nr + nc + 255) / 256), dim3(256), 0, 0, de, nr, nc,
+                       bottom, drw, dcw);
+    YTA_HIP(hipGetLastError());
+    hipLaunchKernelGGL(k_aw_apply, dim3((unsigned)((q + 255) / 256)), dim3(256), 0, 0, de, nr, nc,
+                       w_association_emb, drw, dcw, dout);
+    YTA_HIP(hipGetLastError());
+    YTA_HIP(hipMemcpy(out, dout, sizeof(double) * q, hipMemcpyDeviceToHost));
     return YTA_OK;
 }
 
