@@ -25,6 +25,7 @@
 #include <cmath>
 #include <cstring>
 #include <new>
+#include <thread>
 #include <vector>
 
 #include "bytetrack.hpp"
@@ -1008,6 +1009,35 @@ constexpr size_t BT_LDS_BYTES = YTA_LDS1_KB * 1024;   // k_stage1 arena (one 102
 constexpr size_t BT_LDS23_BYTES = 32 * 1024;  // k_stage23 arena (several blocks per CU)
 constexpr size_t BT_LDSF_BYTES = 20 * 1024;   // k_finish dedup arena (several blocks per CU)
 
+// Host-buffer ABI staging: copies between the caller's (pageable) buffers and the pinned staging
+// buffers, split over up to 8 host threads, and chunked so that each chunk's DMA overlaps the next
+// chunk's host copy.
+void par_copy(void *dst, const void *src, size_t bytes) {
+    constexpr size_t MIN_PIECE = 2u << 20;
+    const unsigned hw = std::thread::hardware_concurrency();
+    const size_t T = std::min<size_t>(std::min<unsigned>(hw ? hw : 1, 8), bytes / MIN_PIECE);
+    if (T <= 1) {
+        memcpy(dst, src, bytes);
+        return;
+    }
+    const size_t piece = (bytes + T - 1) / T;
+    std::vector<std::thread> th;
+    th.reserve(T - 1);
+    for (size_t k = 1; k < T; ++k) {
+        const size_t o = k * piece;
+        if (o >= bytes) break;
+        const size_t n = std::min(piece, bytes - o);
+        th.emplace_back([=] { memcpy((char *)dst + o, (const char *)src + o, n); });
+    }
+    memcpy(dst, src, std::min(piece, bytes));
+    for (auto &t : th) t.join();
+}
+constexpr int STAGE_CHUNKS = 4;
+inline size_t stage_chunk(size_t bytes) {
+    const int n = bytes >= (16u << 20) ? STAGE_CHUNKS : 1;
+    return ((bytes + n - 1) / n + 63) & ~(size_t)63;
+}
+
 template <typename T>
 int dalloc(yta_bytetrack *e, T **p, long long n) {
     void *q = nullptr;
@@ -1411,10 +1441,14 @@ int update_host(yta_bytetrack *e, const double *dets, const int *det_offsets, co
         YTA_HIP(hipHostMalloc((void **)&e->h_dets, sizeof(double) * 6 * cap, hipHostMallocDefault));
         e->d_det_cap = cap;
     }
-    if (total) {
-        memcpy(e->h_dets, dets, sizeof(double) * 6 * total);
-        YTA_HIP(hipMemcpyAsync(e->d_det_in, e->h_dets, sizeof(double) * 6 * total,
-                               hipMemcpyHostToDevice, e->stream));
+    if (total) {   // chunk k's DMA overlaps chunk k+1's host copy
+        const size_t bytes = sizeof(double) * 6 * total, ch = stage_chunk(bytes);
+        for (size_t o = 0; o < bytes; o += ch) {
+            const size_t n = std::min(ch, bytes - o);
+            par_copy((char *)e->h_dets + o, (const char *)dets + o, n);
+            YTA_HIP(hipMemcpyAsync((char *)e->d_det_in + o, (char *)e->h_dets + o, n,
+                                   hipMemcpyHostToDevice, e->stream));
+        }
     }
     const int D = e->a.D;
     if (D > 0 && total) {
@@ -1486,11 +1520,29 @@ int update_host(yta_bytetrack *e, const double *dets, const int *det_offsets, co
         hipLaunchKernelGGL(k_pack_out, dim3(S), dim3(256), 0, e->stream, e->a.out,
                            (long long)e->CAP, e->d_pack_off, e->d_pack);
         YTA_HIP(hipGetLastError());
-        YTA_HIP(hipMemcpyAsync(e->h_pack, e->d_pack, sizeof(double) * 8 * rows,
-                               hipMemcpyDeviceToHost, e->stream));
+        // chunked copy back: the host copies chunk k out while chunk k+1 is in flight
+        const size_t bytes = sizeof(double) * 8 * rows, ch = stage_chunk(bytes);
+        hipEvent_t ev[STAGE_CHUNKS];
+        int nev = 0;
+        hipError_t err = hipSuccess;
+        for (size_t o = 0; o < bytes && err == hipSuccess; o += ch) {
+            err = hipEventCreateWithFlags(&ev[nev], hipEventDisableTiming);
+            if (err != hipSuccess) break;
+            ++nev;
+            err = hipMemcpyAsync((char *)e->h_pack + o, (char *)e->d_pack + o,
+                                 std::min(ch, bytes - o), hipMemcpyDeviceToHost, e->stream);
+            if (err == hipSuccess) err = hipEventRecord(ev[nev - 1], e->stream);
+        }
+        size_t o = 0;
+        for (int k = 0; k < nev && err == hipSuccess; ++k, o += ch) {
+            err = hipEventSynchronize(ev[k]);
+            if (err == hipSuccess)
+                par_copy((char *)out + o, (const char *)e->h_pack + o, std::min(ch, bytes - o));
+        }
+        for (int k = 0; k < nev; ++k) (void)hipEventDestroy(ev[k]);
+        YTA_HIP(err);
     }
     YTA_HIP(hipStreamSynchronize(e->stream));
-    if (rows > 0) memcpy(out, e->h_pack, sizeof(double) * 8 * rows);
     if (next_id)
         for (int s = 0; s < S; ++s) next_id[s] = e->h_cnt[s].next_id;
     return YTA_OK;
