@@ -1012,10 +1012,17 @@ constexpr size_t BT_LDSF_BYTES = 20 * 1024;   // k_finish dedup arena (several b
 // Host-buffer ABI staging: copies between the caller's (pageable) buffers and the pinned staging
 // buffers, split over up to 8 host threads, and chunked so that each chunk's DMA overlaps the next
 // chunk's host copy.
+#ifndef YTA_STAGE_THREADS
+#define YTA_STAGE_THREADS 8
+#endif
+#ifndef YTA_STAGE_CHUNKS
+#define YTA_STAGE_CHUNKS 4
+#endif
 void par_copy(void *dst, const void *src, size_t bytes) {
     constexpr size_t MIN_PIECE = 2u << 20;
     const unsigned hw = std::thread::hardware_concurrency();
-    const size_t T = std::min<size_t>(std::min<unsigned>(hw ? hw : 1, 8), bytes / MIN_PIECE);
+    const size_t T = std::min<size_t>(std::min<unsigned>(hw ? hw : 1, YTA_STAGE_THREADS),
+                                      bytes / MIN_PIECE);
     if (T <= 1) {
         memcpy(dst, src, bytes);
         return;
@@ -1032,7 +1039,7 @@ void par_copy(void *dst, const void *src, size_t bytes) {
     memcpy(dst, src, std::min(piece, bytes));
     for (auto &t : th) t.join();
 }
-constexpr int STAGE_CHUNKS = 4;
+constexpr int STAGE_CHUNKS = YTA_STAGE_CHUNKS;
 inline size_t stage_chunk(size_t bytes) {
     const int n = bytes >= (16u << 20) ? STAGE_CHUNKS : 1;
     return ((bytes + n - 1) / n + 63) & ~(size_t)63;
