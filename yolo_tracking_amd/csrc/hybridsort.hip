@@ -388,18 +388,43 @@ __global__ __launch_bounds__(256) void k_hs_emb(HsArgs a) {
     for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[i][j] = dbl4{0.0, 0.0, 0.0, 0.0};
+    // the next chunk's 8 + 8 floats are loaded into registers while this chunk's MFMAs run
+    // (float4 pairs when D is a multiple of the chunk: rows then start 128-B aligned)
+    float pa[8], pb[8];
+    const bool vec = (D % HE_KC) == 0;
+    auto fetch = [&](int k0) {
+        if (vec) {
+            const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+            const float4 a0 = a_ok ? *reinterpret_cast<const float4 *>(arow + k0 + lk) : z;
+            const float4 a1 = a_ok ? *reinterpret_cast<const float4 *>(arow + k0 + lk + 4) : z;
+            const float4 b0 = b_ok ? *reinterpret_cast<const float4 *>(brow + k0 + lk) : z;
+            const float4 b1 = b_ok ? *reinterpret_cast<const float4 *>(brow + k0 + lk + 4) : z;
+            pa[0] = a0.x; pa[1] = a0.y; pa[2] = a0.z; pa[3] = a0.w;
+            pa[4] = a1.x; pa[5] = a1.y; pa[6] = a1.z; pa[7] = a1.w;
+            pb[0] = b0.x; pb[1] = b0.y; pb[2] = b0.z; pb[3] = b0.w;
+            pb[4] = b1.x; pb[5] = b1.y; pb[6] = b1.z; pb[7] = b1.w;
+        } else {
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int k = k0 + lk + u;
+                pa[u] = (a_ok && k < D) ? arow[k] : 0.f;
+                pb[u] = (b_ok && k < D) ? brow[k] : 0.f;
+            }
+        }
+    };
+    fetch(0);
     for (int k0 = 0; k0 < D; k0 += HE_KC) {
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
-            const int k = k0 + lk + u;
-            const double av = (a_ok && k < D) ? (double)arow[k] : 0.0;
-            const double bv = (b_ok && k < D) ? (double)brow[k] : 0.0;
+            const double av = (double)pa[u];
+            const double bv = (double)pb[u];
             qa += av * av;
             qb += bv * bv;
             As[lr * HE_LD + lk + u] = av;
             Bs[lr * HE_LD + lk + u] = bv;
         }
         __syncthreads();
+        if (k0 + HE_KC < D) fetch(k0 + HE_KC);
 #pragma unroll
         for (int ks = 0; ks < HE_KC; ks += 4) {
             const int kk = ks + (lane >> 4);
