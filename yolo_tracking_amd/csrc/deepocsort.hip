@@ -8,7 +8,7 @@
 //                                split, embedding weights alpha = af + (1 - af)(1 - trust) (:395-398)
 //   k_doc_cost   [grid]          dense asso (dets x trackers) and iou + angle (association.py:
 //                                111-170), per-row / per-column counts for the fast path
-//   k_doc_emb    [grid]          stage-1 embedding cost dets_embs @ trk_embs^T (float64 tiles)
+//   k_doc_emb    [grid]          stage-1 embedding cost dets_embs @ trk_embs^T (float64 MFMA tiles)
 //   k_doc_aw     [grid]          emb[iou <= 0] = 0, per-row / per-column top-2 weights
 //                                (compute_aw_max_metric :79-108) or the flat weight (aw_off)
 //   k_doc_final  [grid]          cost = -(iou + angle + w_r w_c w emb)
@@ -393,53 +393,78 @@ __global__ __launch_bounds__(OC_T) void k_doc_cost(DocArgs a) {
     if (giou_bad) atomicOr(&c->err, ERR_GIOU);
 }
 
-// dets_embs @ trk_embs^T (deep_ocsort.py:432): 64 x 64 output tiles, the embedding dimension
-// staged through LDS in chunks of 16; float64 accumulation.
-constexpr int EMB_TILE = 64, EMB_KC = 16;
+// dets_embs @ trk_embs^T (deep_ocsort.py:432), float64 accumulation.
+constexpr int EMB_TILE = 64;
+// 64 (detections) x 64 (trackers) tiles per block, 4 waves of 32 x 32 (2 x 2 MFMA tiles of
+// v_mfma_f64_16x16x4_f64: A[l&15][k = l>>4], B[k = l>>4][l&15], D[row (l>>4) + 4 r][col l&15]);
+// K streams through LDS in chunks of 32, the next chunk held in registers while the current
+// chunk's MFMAs run.  Detection rows are float32 (promoted exactly), tracker rows float64.
+typedef double dbl4 __attribute__((ext_vector_type(4)));
+constexpr int DE_KC = 32, DE_LD = DE_KC + 1;
 __global__ __launch_bounds__(256) void k_doc_emb(DocArgs a) {
-    __shared__ double As[EMB_KC][EMB_TILE + 1], Bs[EMB_KC][EMB_TILE + 1];
+    __shared__ double As[EMB_TILE * DE_LD], Bs[EMB_TILE * DE_LD];
     const int s = blockIdx.z;
     const DocCounters *c = a.cnt + s;
     const int n_trk = c->n_trk, n_hi = c->n_high, D = a.D;
     const int r0 = blockIdx.y * EMB_TILE, c0 = blockIdx.x * EMB_TILE;
     if (r0 >= n_hi || c0 >= n_trk) return;                   // block-uniform
     const long long tb = (long long)s * a.CAP, db = (long long)s * a.MAXD, mb = doc_mb(a, s);
-    const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
-    double acc[4][4] = {};
-    for (int k0 = 0; k0 < D; k0 += EMB_KC) {
-        for (int e = threadIdx.x; e < EMB_KC * EMB_TILE; e += 256) {
-            const int kk = e / EMB_TILE, q = e % EMB_TILE;
-            const int k = k0 + kk;
-            double av = 0.0, bv = 0.0;
-            if (k < D && r0 + q < n_hi)
-                av = (double)a.det_feat[((long long)a.det_off[s] + a.hi_row[db + r0 + q]) * D + k];
-            if (k < D && c0 + q < n_trk) bv = a.emb[(tb + a.cslot[tb + c0 + q]) * D + k];
-            As[kk][q] = av;
-            Bs[kk][q] = bv;
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int wr = (w >> 1) * 32, wc = (w & 1) * 32;
+    const int lr = t >> 2, lk = (t & 3) * 8;   // staging: 8 consecutive k of row lr
+    const bool a_ok = r0 + lr < n_hi, b_ok = c0 + lr < n_trk;
+    const float *arow = a_ok ? a.det_feat + ((long long)a.det_off[s] + a.hi_row[db + r0 + lr]) * D
+                             : nullptr;
+    const double *brow = b_ok ? a.emb + (tb + a.cslot[tb + c0 + lr]) * D : nullptr;
+    double pa[8], pb[8];
+    auto fetch = [&](int k0) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int k = k0 + lk + u;
+            pa[u] = (a_ok && k < D) ? (double)arow[k] : 0.0;
+            pb[u] = (b_ok && k < D) ? brow[k] : 0.0;
+        }
+    };
+    dbl4 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = dbl4{0.0, 0.0, 0.0, 0.0};
+    fetch(0);
+    for (int k0 = 0; k0 < D; k0 += DE_KC) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            As[lr * DE_LD + lk + u] = pa[u];
+            Bs[lr * DE_LD + lk + u] = pb[u];
         }
         __syncthreads();
+        if (k0 + DE_KC < D) fetch(k0 + DE_KC);
 #pragma unroll
-        for (int kk = 0; kk < EMB_KC; ++kk) {
-            double av[4], bv[4];
+        for (int ks = 0; ks < DE_KC; ks += 4) {
+            const int kk = ks + (lane >> 4);
+            double af[2], bf[2];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                av[u] = As[kk][ty * 4 + u];
-                bv[u] = Bs[kk][tx * 4 + u];
-            }
+            for (int i = 0; i < 2; ++i) af[i] = As[(wr + 16 * i + (lane & 15)) * DE_LD + kk];
 #pragma unroll
-            for (int u = 0; u < 4; ++u)
+            for (int j = 0; j < 2; ++j) bf[j] = Bs[(wc + 16 * j + (lane & 15)) * DE_LD + kk];
 #pragma unroll
-                for (int v = 0; v < 4; ++v) acc[u][v] = fma(av[u], bv[v], acc[u][v]);
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[i], bf[j], acc[i][j], 0, 0, 0);
         }
         __syncthreads();
     }
 #pragma unroll
-    for (int u = 0; u < 4; ++u)
+    for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int v = 0; v < 4; ++v) {
-            const int r = r0 + ty * 4 + u, cc = c0 + tx * 4 + v;
-            if (r < n_hi && cc < n_trk) a.emat[mb + (long long)r * n_trk + cc] = acc[u][v];
-        }
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr) {
+                const int p = r0 + wr + 16 * i + (lane >> 4) + 4 * rr;
+                const int q = c0 + wc + 16 * j + (lane & 15);
+                if (p < n_hi && q < n_trk) a.emat[mb + (long long)p * n_trk + q] = acc[i][j][rr];
+            }
 }
 
 // compute_aw_max_metric (association.py:79-108) on emb[iou <= 0] = 0: the top two values of each
