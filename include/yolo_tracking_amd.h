@@ -144,7 +144,13 @@ int yta_bytetrack_capacity(yta_bytetrack *engine, int *track_capacity, int *max_
  * prefix offsets (rows).  next_id: S counters (in: the last issued ID per stream, i.e. the
  * reference's BaseTrack._count; out: updated), may be NULL to use the engine's own counters.
  * out: caller buffer of out_capacity rows x 8 float64 [x1,y1,x2,y2,id,conf,cls,det_ind];
- * out_offsets: S+1 prefix offsets written by the call.  Synchronous. */
+ * out_offsets: S+1 prefix offsets written by the call.  Synchronous.
+ * out_capacity >= det_offsets[S] always suffices (every output row is a track matched to or born
+ * from one of the frame's detections) and is required: a smaller buffer fails with
+ * YTA_ERR_CAPACITY before anything is staged or launched, so the same call can be retried.  An
+ * error reported after the launch (device error flags, HIP failure) means the frame HAS been
+ * applied on the device; next_id is still written back then.  The same rules hold for every
+ * tracker's host-buffer update below. */
 int yta_bytetrack_update(yta_bytetrack *engine, const double *dets, const int *det_offsets,
                          long long *next_id, double *out, int out_capacity, int *out_offsets);
 

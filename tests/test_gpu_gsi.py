@@ -4,8 +4,9 @@ goldens (tests/golden/gsi_mot17.npz) and the oracle (oracle/gsi.py).
 Bar: linear_interpolation bit-exact (same float64 expression, row order by construction).
 gaussian_smooth: the Cholesky / substitution / K @ alpha sums run in a different order than
 LAPACK / OpenBLAS and the 1e-10 regulariser leaves K with condition numbers near 1e10, so
-predictions agree to GP_ATOL px (measured: <= 1e-4 px); the integer rows gsi() writes agree
-wherever the reference's value is more than INT_MARGIN from an integer boundary."""
+predictions agree to GP_ATOL px (the measured maximum is printed: see DESIGN.md §8); the files
+gsi() writes (integer rows, %d truncation) are identical to the reference's, including the ~27 %
+of values whose smoothed coordinate lies within INT_MARGIN of an integer."""
 import os
 
 import numpy as np
@@ -36,6 +37,7 @@ def check_smooth(got, exp):
     assert np.array_equal(got[:, [0, 1, 6, 7, 8]], exp[:, [0, 1, 6, 7, 8]])   # order, ids, conf
     err = np.abs(got[:, 2:6] - exp[:, 2:6])
     assert err.max() <= GP_ATOL, err.max()
+    print(f"gaussian_smooth: {len(got)} rows, max |err| {err.max():.3g} px")
     v = exp[:, 2:6]
     far = np.abs(v - np.round(v)) > INT_MARGIN
     assert np.array_equal(got[:, 2:6].astype(int)[far], v.astype(int)[far])
@@ -59,14 +61,19 @@ def test_gsi_files_vs_reference(g, tmp_path):
         np.savetxt(tmp_path / f"{n}.txt", g["in_" + n], fmt="%d")
     np.savetxt(tmp_path / "other.txt", g["in_" + names(g)[0]], fmt="%d")   # not MOT*FRCNN.txt
     pg.gsi(mot_results_folder=tmp_path, interval=20, tau=10)
+    n_vals = n_near = 0
     for n in names(g):
         got = np.loadtxt(tmp_path / f"{n}.txt", dtype=int)
         exp = g["out_" + n]
         v = g["gs_" + n][:, 2:6]
-        far = np.abs(v - np.round(v)) > INT_MARGIN
+        n_vals += v.size
+        n_near += int((np.abs(v - np.round(v)) <= INT_MARGIN).sum())
+        # the written files equal the reference's byte for byte, including every value whose
+        # smoothed coordinate lies within INT_MARGIN of an integer (where %d truncation could flip)
         assert got.shape == exp.shape
-        assert np.array_equal(got[:, [0, 1, 6, 7, 8]], exp[:, [0, 1, 6, 7, 8]])
-        assert np.array_equal(got[:, 2:6][far], exp[:, 2:6][far]), n
+        assert np.array_equal(got, exp), n
+    print(f"gsi files: {n_vals} box values identical to the reference, {n_near} of them within "
+          f"{INT_MARGIN} px of an integer")
     assert np.array_equal(np.loadtxt(tmp_path / "other.txt", dtype=int), g["in_" + names(g)[0]])
 
 

@@ -84,7 +84,6 @@ class ReIDDetectMultiBackend:
         self.model = model
         self.nhwc = False
         self.lib = _lib.load_library()
-        self._work = torch.empty(256, dtype=torch.float64, device=self.device)
 
     def _stream(self):
         return ctypes.c_void_p(self.torch.cuda.current_stream(self.device).cuda_stream)
@@ -156,9 +155,12 @@ class ReIDDetectMultiBackend:
     def normalize_(self, features):
         """In-place global normalisation of a float32 device tensor (get_features :310)."""
         assert features.dtype == self.torch.float32 and features.is_contiguous()
+        # partial sums: a fresh block from the caching allocator on the current stream, so calls
+        # on different streams (one per camera) never share a workspace
+        work = self.torch.empty(256, dtype=self.torch.float64, device=self.device)
         _lib.check(self.lib.yta_reid_normalize_device(
             ctypes.c_void_p(features.data_ptr()), features.numel(),
-            ctypes.c_void_p(self._work.data_ptr()), self._stream()))
+            ctypes.c_void_p(work.data_ptr()), self._stream()))
         return features
 
     def get_features(self, xyxys, img):

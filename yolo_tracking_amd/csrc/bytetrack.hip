@@ -24,11 +24,13 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <memory>
 #include <new>
 #include <thread>
 #include <vector>
 
 #include "bytetrack.hpp"
+#include "host_pool.hpp"
 
 namespace yta {
 namespace {
@@ -997,6 +999,8 @@ struct yta_bytetrack {
     bool prof = false;
     std::vector<hipEvent_t> ev;
     size_t ev_used = 0;
+    // host-buffer staging copies: persistent worker threads (created on the first large copy)
+    std::unique_ptr<CopyPool> pool;
 };
 
 namespace {
@@ -1018,7 +1022,7 @@ constexpr size_t BT_LDSF_BYTES = 20 * 1024;   // k_finish dedup arena (several b
 #ifndef YTA_STAGE_CHUNKS
 #define YTA_STAGE_CHUNKS 4
 #endif
-void par_copy(void *dst, const void *src, size_t bytes) {
+void par_copy(yta_bytetrack *e, void *dst, const void *src, size_t bytes) {
     constexpr size_t MIN_PIECE = 2u << 20;
     const unsigned hw = std::thread::hardware_concurrency();
     const size_t T = std::min<size_t>(std::min<unsigned>(hw ? hw : 1, YTA_STAGE_THREADS),
@@ -1027,17 +1031,8 @@ void par_copy(void *dst, const void *src, size_t bytes) {
         memcpy(dst, src, bytes);
         return;
     }
-    const size_t piece = (bytes + T - 1) / T;
-    std::vector<std::thread> th;
-    th.reserve(T - 1);
-    for (size_t k = 1; k < T; ++k) {
-        const size_t o = k * piece;
-        if (o >= bytes) break;
-        const size_t n = std::min(piece, bytes - o);
-        th.emplace_back([=] { memcpy((char *)dst + o, (const char *)src + o, n); });
-    }
-    memcpy(dst, src, std::min(piece, bytes));
-    for (auto &t : th) t.join();
+    if (!e->pool) e->pool.reset(new CopyPool(std::min<unsigned>(hw, YTA_STAGE_THREADS) - 1));
+    e->pool->copy(dst, src, bytes, (int)T);
 }
 constexpr int STAGE_CHUNKS = YTA_STAGE_CHUNKS;
 inline size_t stage_chunk(size_t bytes) {
@@ -1255,7 +1250,7 @@ int reserve(yta_bytetrack *e, int cap, int maxd) {
     if (cap <= e->CAP && maxd <= e->MAXD) return YTA_OK;
     cap = std::max(cap, e->CAP);
     maxd = std::max(maxd, e->MAXD);
-    YTA_HIP(hipStreamSynchronize(e->stream));
+    YTA_HIP(host_wait(e->stream));
     yta_bytetrack *n = new (std::nothrow) yta_bytetrack();
     YTA_CHECK(n, YTA_ERR_NOMEM, "out of host memory");
     n->device = e->device;
@@ -1301,7 +1296,7 @@ int reserve(yta_bytetrack *e, int cap, int maxd) {
         const size_t live_bytes = sizeof(unsigned int) * ((nc + 31) / 32);
         hipLaunchKernelGGL(k_rebuild_free, dim3(e->S), dim3(BLKF), live_bytes, e->stream, n->a);
         hipError_t he = hipGetLastError();
-        if (he == hipSuccess) he = hipStreamSynchronize(e->stream);
+        if (he == hipSuccess) he = host_wait(e->stream);
         if (he != hipSuccess) {
             set_error("reserve: %s", hipGetErrorString(he));
             rc = YTA_ERR_HIP;
@@ -1355,7 +1350,7 @@ int check_errors(yta_bytetrack *e) {
 int read_counters(yta_bytetrack *e) {
     YTA_HIP(hipMemcpyAsync(e->h_cnt, e->a.cnt, sizeof(BtCounters) * e->S, hipMemcpyDeviceToHost,
                            e->stream));
-    YTA_HIP(hipStreamSynchronize(e->stream));
+    YTA_HIP(host_wait(e->stream));
     return YTA_OK;
 }
 
@@ -1420,6 +1415,10 @@ int update_host(yta_bytetrack *e, const double *dets, const int *det_offsets, co
         need_d = std::max(need_d, m);
         need_c = std::max(need_c, e->h_cnt[s].n_tracked + e->h_cnt[s].n_lost + m);
     }
+    // every output row is a track matched to or born from one of this frame's detections, so
+    // det_offsets[S] rows always suffice; checked before anything moves (the frame is not consumed)
+    YTA_CHECK(out_capacity >= det_offsets[S], YTA_ERR_CAPACITY,
+              "out holds %d rows, the call needs det_offsets[S] = %d", out_capacity, det_offsets[S]);
     if (need_d > e->MAXD || need_c > e->CAP) {   // grow geometrically, keeping all state
         const int rc = reserve(e, need_c > e->CAP ? std::max(need_c, 2 * e->CAP) : e->CAP,
                                need_d > e->MAXD ? std::max(need_d, 2 * e->MAXD) : e->MAXD);
@@ -1452,7 +1451,7 @@ int update_host(yta_bytetrack *e, const double *dets, const int *det_offsets, co
         const size_t bytes = sizeof(double) * 6 * total, ch = stage_chunk(bytes);
         for (size_t o = 0; o < bytes; o += ch) {
             const size_t n = std::min(ch, bytes - o);
-            par_copy((char *)e->h_dets + o, (const char *)dets + o, n);
+            par_copy(e, (char *)e->h_dets + o, (const char *)dets + o, n);
             YTA_HIP(hipMemcpyAsync((char *)e->d_det_in + o, (char *)e->h_dets + o, n,
                                    hipMemcpyHostToDevice, e->stream));
         }
@@ -1494,6 +1493,8 @@ int update_host(yta_bytetrack *e, const double *dets, const int *det_offsets, co
     if (rc) return rc;
     rc = read_counters(e);
     if (rc) return rc;
+    if (next_id)   // the device counters have advanced: hand them back even on an error below
+        for (int s = 0; s < S; ++s) next_id[s] = e->h_cnt[s].next_id;
     rc = check_errors(e);
     if (rc) return rc;
     long long rows = 0;
@@ -1533,7 +1534,7 @@ int update_host(yta_bytetrack *e, const double *dets, const int *det_offsets, co
         int nev = 0;
         hipError_t err = hipSuccess;
         for (size_t o = 0; o < bytes && err == hipSuccess; o += ch) {
-            err = hipEventCreateWithFlags(&ev[nev], hipEventDisableTiming);
+            err = hipEventCreateWithFlags(&ev[nev], hipEventDisableTiming | hipEventBlockingSync);
             if (err != hipSuccess) break;
             ++nev;
             err = hipMemcpyAsync((char *)e->h_pack + o, (char *)e->d_pack + o,
@@ -1544,14 +1545,12 @@ int update_host(yta_bytetrack *e, const double *dets, const int *det_offsets, co
         for (int k = 0; k < nev && err == hipSuccess; ++k, o += ch) {
             err = hipEventSynchronize(ev[k]);
             if (err == hipSuccess)
-                par_copy((char *)out + o, (const char *)e->h_pack + o, std::min(ch, bytes - o));
+                par_copy(e, (char *)out + o, (const char *)e->h_pack + o, std::min(ch, bytes - o));
         }
         for (int k = 0; k < nev; ++k) (void)hipEventDestroy(ev[k]);
         YTA_HIP(err);
     }
-    YTA_HIP(hipStreamSynchronize(e->stream));
-    if (next_id)
-        for (int s = 0; s < S; ++s) next_id[s] = e->h_cnt[s].next_id;
+    YTA_HIP(host_wait(e->stream));
     return YTA_OK;
 }
 
@@ -1589,7 +1588,7 @@ int yta_botsort_create(int device, int n_streams, int track_capacity, int max_de
 int yta_bytetrack_destroy(yta_bytetrack *e) {
     if (!e) return YTA_OK;
     (void)hipSetDevice(e->device);
-    if (e->stream) (void)hipStreamSynchronize(e->stream);
+    if (e->stream) (void)host_wait(e->stream);
     release_buffers(e);
     if (e->h_dets) (void)hipHostFree(e->h_dets);
     if (e->d_det_in) (void)hipFree(e->d_det_in);
@@ -1612,7 +1611,7 @@ int yta_bytetrack_reset(yta_bytetrack *e) {
     YTA_HIP(hipGetLastError());
     YTA_HIP(hipMemsetAsync(e->a.meta, 0, sizeof(TrackMeta) * (size_t)e->S * e->CAP, e->stream));
     YTA_HIP(hipMemsetAsync(e->a.flags, 0, sizeof(int) * (size_t)e->S * e->CAP, e->stream));
-    YTA_HIP(hipStreamSynchronize(e->stream));
+    YTA_HIP(host_wait(e->stream));
     memset(e->h_cnt, 0, sizeof(BtCounters) * e->S);
     return YTA_OK;
 }
@@ -1710,7 +1709,7 @@ int yta_bytetrack_get_state(yta_bytetrack *e, int stream, int *n_tracks, long lo
 
 int yta_bytetrack_profile(yta_bytetrack *e, int enable) {
     YTA_CHECK(e, YTA_ERR_INVALID, "null engine");
-    YTA_HIP(hipStreamSynchronize(e->stream));
+    YTA_HIP(host_wait(e->stream));
     e->prof = enable != 0;
     e->ev_used = 0;
     return YTA_OK;
@@ -1721,7 +1720,7 @@ int yta_bytetrack_profile(yta_bytetrack *e, int enable) {
 // frames covered.
 int yta_bytetrack_profile_collect(yta_bytetrack *e, double *ms, int *frames) {
     YTA_CHECK(e && ms && frames, YTA_ERR_INVALID, "null argument");
-    YTA_HIP(hipStreamSynchronize(e->stream));
+    YTA_HIP(host_wait(e->stream));
     const size_t per = BT_PHASES + 1;
     for (int k = 0; k < BT_PHASES; ++k) ms[k] = 0.0;
     *frames = (int)(e->ev_used / per);
@@ -1758,7 +1757,7 @@ int yta_bytetrack_set_lds(yta_bytetrack *e, int bytes) {
     YTA_CHECK(e, YTA_ERR_INVALID, "null engine");
     YTA_CHECK(bytes >= 0 && bytes <= 150 * 1024, YTA_ERR_INVALID, "LDS bytes must be in [0, 150 KiB]");
     YTA_HIP(hipSetDevice(e->device));
-    YTA_HIP(hipStreamSynchronize(e->stream));
+    YTA_HIP(host_wait(e->stream));
     e->a.lds_bytes = (size_t)bytes & ~(size_t)15;
     e->a.lds_bytes23 = std::min(e->a.lds_bytes, BT_LDS23_BYTES);
     e->a.lds_bytes_f = std::min(e->a.lds_bytes, BT_LDSF_BYTES);

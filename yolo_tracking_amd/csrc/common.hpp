@@ -34,6 +34,12 @@ void set_error(const char *fmt, ...);
 
 int select_device(int device);
 
+// Wait for everything queued on `s` without spinning a host core: a blocking-sync event recorded
+// on the stream (hipStreamSynchronize may busy-wait; on a host with a CPU quota the spinning
+// threads of a synchronous update() then get the whole process throttled).  One event per host
+// thread and device.
+hipError_t host_wait(hipStream_t s);
+
 // ------------------------------------------------------------------ device helpers
 constexpr int WAVE = 64;
 

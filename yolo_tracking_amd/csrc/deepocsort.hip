@@ -1049,7 +1049,7 @@ int doc_launch(yta_deepocsort *e, const double *d_dets, const int *d_off, const 
 int doc_read_counters(yta_deepocsort *e) {
     YTA_HIP(hipMemcpyAsync(e->h_cnt, e->a.cnt, sizeof(DocCounters) * e->S, hipMemcpyDeviceToHost,
                            e->stream));
-    YTA_HIP(hipStreamSynchronize(e->stream));
+    YTA_HIP(host_wait(e->stream));
     return YTA_OK;
 }
 
@@ -1074,7 +1074,7 @@ int doc_reserve(yta_deepocsort *e, int cap, int maxd) {
     if (cap <= e->CAP && maxd <= e->MAXD) return YTA_OK;
     cap = std::max(cap, e->CAP);
     maxd = std::max(maxd, e->MAXD);
-    YTA_HIP(hipStreamSynchronize(e->stream));
+    YTA_HIP(host_wait(e->stream));
     yta_deepocsort *n = new (std::nothrow) yta_deepocsort();
     YTA_CHECK(n, YTA_ERR_NOMEM, "out of host memory");
     n->device = e->device;
@@ -1102,7 +1102,7 @@ int doc_reserve(yta_deepocsort *e, int cap, int maxd) {
         if (he == hipSuccess)
             he = hipMemcpyAsync(cnt.data(), e->a.cnt, sizeof(DocCounters) * S,
                                 hipMemcpyDeviceToHost, e->stream);
-        if (he == hipSuccess) he = hipStreamSynchronize(e->stream);
+        if (he == hipSuccess) he = host_wait(e->stream);
         if (he == hipSuccess) {
             for (size_t s = 0; s < S; ++s) {
                 int k = 0;
@@ -1195,7 +1195,7 @@ int yta_deepocsort_create(int device, int n_streams, int track_capacity, int max
 int yta_deepocsort_destroy(yta_deepocsort *e) {
     if (!e) return YTA_OK;
     (void)hipSetDevice(e->device);
-    if (e->stream) (void)hipStreamSynchronize(e->stream);
+    if (e->stream) (void)host_wait(e->stream);
     doc_release(e);
     if (e->h_dets) (void)hipHostFree(e->h_dets);
     if (e->d_det_in) (void)hipFree(e->d_det_in);
@@ -1211,7 +1211,7 @@ int yta_deepocsort_reset(yta_deepocsort *e) {
     YTA_HIP(hipSetDevice(e->device));
     hipLaunchKernelGGL(k_doc_reset, dim3(e->S), dim3(256), 0, e->stream, e->a);
     YTA_HIP(hipGetLastError());
-    YTA_HIP(hipStreamSynchronize(e->stream));
+    YTA_HIP(host_wait(e->stream));
     memset(e->h_cnt, 0, sizeof(DocCounters) * e->S);
     return YTA_OK;
 }
@@ -1238,6 +1238,10 @@ int yta_deepocsort_update(yta_deepocsort *e, const double *dets, const int *det_
         need_d = std::max(need_d, m);
         need_c = std::max(need_c, e->h_cnt[s].n_trk + m);
     }
+    // every output row is a track matched to or born from one of this frame's detections, so
+    // det_offsets[S] rows always suffice; checked before anything moves (the frame is not consumed)
+    YTA_CHECK(out_capacity >= det_offsets[S], YTA_ERR_CAPACITY,
+              "out holds %d rows, the call needs det_offsets[S] = %d", out_capacity, det_offsets[S]);
     if (need_d > e->MAXD || need_c > e->CAP) {
         const int rc = doc_reserve(e, need_c > e->CAP ? std::max(need_c, 2 * e->CAP) : e->CAP,
                                    need_d > e->MAXD ? std::max(need_d, 2 * e->MAXD) : e->MAXD);
@@ -1309,6 +1313,8 @@ int yta_deepocsort_update(yta_deepocsort *e, const double *dets, const int *det_
     if (rc) return rc;
     rc = doc_read_counters(e);
     if (rc) return rc;
+    if (next_id)   // the device counters have advanced: hand them back even on an error below
+        for (int s = 0; s < S; ++s) next_id[s] = e->h_cnt[s].next_id;
     rc = doc_check_errors(e);
     if (rc) return rc;
     long long rows = 0;
@@ -1327,9 +1333,7 @@ int yta_deepocsort_update(yta_deepocsort *e, const double *dets, const int *det_
                                    e->a.out + (long long)s * e->CAP * 8, sizeof(double) * 8 * n,
                                    hipMemcpyDeviceToHost, e->stream));
     }
-    YTA_HIP(hipStreamSynchronize(e->stream));
-    if (next_id)
-        for (int s = 0; s < S; ++s) next_id[s] = e->h_cnt[s].next_id;
+    YTA_HIP(host_wait(e->stream));
     return YTA_OK;
 }
 

@@ -750,7 +750,7 @@ int oc_launch(yta_ocsort *e, const double *d_dets, const int *d_off, const int *
 int oc_read_counters(yta_ocsort *e) {
     YTA_HIP(hipMemcpyAsync(e->h_cnt, e->a.cnt, sizeof(OcCounters) * e->S, hipMemcpyDeviceToHost,
                            e->stream));
-    YTA_HIP(hipStreamSynchronize(e->stream));
+    YTA_HIP(host_wait(e->stream));
     return YTA_OK;
 }
 
@@ -776,7 +776,7 @@ int oc_reserve(yta_ocsort *e, int cap, int maxd) {
     if (cap <= e->CAP && maxd <= e->MAXD) return YTA_OK;
     cap = std::max(cap, e->CAP);
     maxd = std::max(maxd, e->MAXD);
-    YTA_HIP(hipStreamSynchronize(e->stream));
+    YTA_HIP(host_wait(e->stream));
     yta_ocsort *n = new (std::nothrow) yta_ocsort();
     YTA_CHECK(n, YTA_ERR_NOMEM, "out of host memory");
     n->device = e->device;
@@ -805,7 +805,7 @@ int oc_reserve(yta_ocsort *e, int cap, int maxd) {
         if (he == hipSuccess)
             he = hipMemcpyAsync(cnt.data(), e->a.cnt, sizeof(OcCounters) * S,
                                 hipMemcpyDeviceToHost, e->stream);
-        if (he == hipSuccess) he = hipStreamSynchronize(e->stream);
+        if (he == hipSuccess) he = host_wait(e->stream);
         if (he != hipSuccess) {
             set_error("reserve: %s", hipGetErrorString(he));
             rc = YTA_ERR_HIP;
@@ -896,7 +896,7 @@ int yta_ocsort_create(int device, int n_streams, int track_capacity, int max_det
 int yta_ocsort_destroy(yta_ocsort *e) {
     if (!e) return YTA_OK;
     (void)hipSetDevice(e->device);
-    if (e->stream) (void)hipStreamSynchronize(e->stream);
+    if (e->stream) (void)host_wait(e->stream);
     oc_release(e);
     if (e->h_dets) (void)hipHostFree(e->h_dets);
     if (e->d_det_in) (void)hipFree(e->d_det_in);
@@ -910,7 +910,7 @@ int yta_ocsort_reset(yta_ocsort *e) {
     YTA_HIP(hipSetDevice(e->device));
     hipLaunchKernelGGL(k_oc_reset, dim3(e->S), dim3(256), 0, e->stream, e->a);
     YTA_HIP(hipGetLastError());
-    YTA_HIP(hipStreamSynchronize(e->stream));
+    YTA_HIP(host_wait(e->stream));
     memset(e->h_cnt, 0, sizeof(OcCounters) * e->S);
     return YTA_OK;
 }
@@ -937,6 +937,10 @@ int yta_ocsort_update(yta_ocsort *e, const double *dets, const int *det_offsets,
         need_d = std::max(need_d, m);
         need_c = std::max(need_c, e->h_cnt[s].n_trk + m);
     }
+    // every output row is a track matched to or born from one of this frame's detections, so
+    // det_offsets[S] rows always suffice; checked before anything moves (the frame is not consumed)
+    YTA_CHECK(out_capacity >= det_offsets[S], YTA_ERR_CAPACITY,
+              "out holds %d rows, the call needs det_offsets[S] = %d", out_capacity, det_offsets[S]);
     if (need_d > e->MAXD || need_c > e->CAP) {
         const int rc = oc_reserve(e, need_c > e->CAP ? std::max(need_c, 2 * e->CAP) : e->CAP,
                                   need_d > e->MAXD ? std::max(need_d, 2 * e->MAXD) : e->MAXD);
@@ -978,6 +982,8 @@ int yta_ocsort_update(yta_ocsort *e, const double *dets, const int *det_offsets,
     if (rc) return rc;
     rc = oc_read_counters(e);
     if (rc) return rc;
+    if (next_id)   // the device counters have advanced: hand them back even on an error below
+        for (int s = 0; s < S; ++s) next_id[s] = e->h_cnt[s].next_id;
     rc = oc_check_errors(e);
     if (rc) return rc;
     long long rows = 0;
@@ -996,9 +1002,7 @@ int yta_ocsort_update(yta_ocsort *e, const double *dets, const int *det_offsets,
                                    e->a.out + (long long)s * e->CAP * 8, sizeof(double) * 8 * n,
                                    hipMemcpyDeviceToHost, e->stream));
     }
-    YTA_HIP(hipStreamSynchronize(e->stream));
-    if (next_id)
-        for (int s = 0; s < S; ++s) next_id[s] = e->h_cnt[s].next_id;
+    YTA_HIP(host_wait(e->stream));
     return YTA_OK;
 }
 

@@ -30,6 +30,33 @@ int select_device(int device) {
     return YTA_OK;
 }
 
+hipError_t host_wait(hipStream_t s) {
+    constexpr int MAX_DEV = 64;
+    thread_local hipEvent_t ev[MAX_DEV] = {};
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    if (s) {
+        hipDevice_t sd;
+        if (hipStreamGetDevice(s, &sd) == hipSuccess) dev = (int)sd;
+    }
+    if (dev < 0 || dev >= MAX_DEV) return hipStreamSynchronize(s);
+    if (!ev[dev]) {
+        int cur = -1;
+        (void)hipGetDevice(&cur);
+        if (cur != dev) (void)hipSetDevice(dev);
+        e = hipEventCreateWithFlags(&ev[dev], hipEventBlockingSync | hipEventDisableTiming);
+        if (cur != dev) (void)hipSetDevice(cur);
+        if (e != hipSuccess) {
+            ev[dev] = nullptr;
+            return hipStreamSynchronize(s);
+        }
+    }
+    e = hipEventRecord(ev[dev], s);
+    if (e != hipSuccess) return e;
+    return hipEventSynchronize(ev[dev]);
+}
+
 }  // namespace yta
 
 extern "C" {

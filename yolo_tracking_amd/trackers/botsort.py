@@ -17,6 +17,7 @@ import ctypes
 import numpy as np
 
 from .. import _lib
+from ..motion.cmc import IdentityCMC, default_cmc
 from .bytetrack import ByteTrackEngine, STrackView
 
 
@@ -43,11 +44,6 @@ class TrackState:
     Removed = 4
 
 
-class IdentityCMC:
-    """Static-camera motion model: the identity warp every frame."""
-
-    def apply(self, img, dets):
-        return np.eye(2, 3)
 
 
 class BoTSORTEngine(ByteTrackEngine):
@@ -103,10 +99,10 @@ class BoTSORTEngine(ByteTrackEngine):
         w = None
         if warps is not None:
             w = np.ascontiguousarray(np.asarray(warps, dtype=np.float64).reshape(self.n_streams, 6))
-        cap, _ = self.capacity()
-        need = 2 * self.n_streams * cap + int(off[-1]) + 1
+        # every output row is a track matched to or born from one of this frame's detections
+        need = max(int(off[-1]), 1)
         if len(self._out) < need:
-            self._out = np.empty((need, 8), dtype=np.float64)
+            self._out = np.empty((2 * need, 8), dtype=np.float64)
         nid = None
         if next_id is not None:
             nid = np.ascontiguousarray(next_id, dtype=np.int64)
@@ -147,7 +143,8 @@ class BoTSORT:
     model_weights / fp16 name the reference's ReID model, which is outside the hot path: pass
     `reid=` (an object with get_features(xyxys, img) -> (n, D) float32, e.g. a
     ReIDDetectMultiBackend) or give `update(..., embs=...)` the frame's per-detection embeddings.
-    `cmc=` replaces the SparseOptFlow estimator (default: identity warp, static camera).
+    `cmc=` replaces the SparseOptFlow estimator (an object with apply(img, dets) -> 2x3 warp;
+    without one the identity warp is used and a one-time RuntimeWarning says so).
     """
 
     def __init__(self, model_weights=None, device=0, fp16=False, track_high_thresh=0.5,
@@ -170,7 +167,7 @@ class BoTSORT:
         self.model_weights = model_weights
         if with_reid:
             self.model = reid
-        self.cmc = cmc if cmc is not None else IdentityCMC()
+        self.cmc = cmc if cmc is not None else default_cmc("BoTSORT")
         self._kw = dict(track_high_thresh=track_high_thresh, track_low_thresh=track_low_thresh,
                         new_track_thresh=new_track_thresh, track_buffer=track_buffer,
                         match_thresh=match_thresh, proximity_thresh=proximity_thresh,

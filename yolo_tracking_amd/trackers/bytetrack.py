@@ -81,11 +81,10 @@ class ByteTrackEngine:
                 [np.asarray(d, dtype=np.float64).reshape(-1, 6) for d in dets_per_stream]))
         else:
             packed = np.zeros((0, 6))
-        cap, _ = self.capacity()
-        # rows per stream <= tracked + lost + births <= the (possibly grown) capacity <= 2*cap + M
-        need = 2 * self.n_streams * cap + int(off[-1]) + 1
+        # every output row is a track matched to or born from one of this frame's detections
+        need = max(int(off[-1]), 1)
         if len(self._out) < need:
-            self._out = np.empty((need, 8), dtype=np.float64)
+            self._out = np.empty((2 * need, 8), dtype=np.float64)
         nid = None
         if next_id is not None:
             nid = np.ascontiguousarray(next_id, dtype=np.int64)

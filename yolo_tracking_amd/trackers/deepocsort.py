@@ -10,13 +10,15 @@ features and camera warp from the pluggable producers and returns the (K, 8) res
 The ReID forward pass (:387 get_features) and the SparseOptFlow CMC estimator (:391 cmc.apply) are
 not part of the hot path: pass `reid=` (an object with get_features(xyxys, img) ->
 (n, D) float32) or give `update(..., embs=...)` the frame's per-detection embeddings, and `cmc=`
-(an object with apply(img, dets) -> 2x3 warp) for a moving camera (default: static camera).
+(an object with apply(img, dets) -> 2x3 warp) for a moving camera (without one: identity warp and
+a one-time RuntimeWarning).
 """
 import ctypes
 
 import numpy as np
 
 from .. import _lib
+from ..motion.cmc import default_cmc
 
 
 class KalmanBoxTracker:
@@ -121,8 +123,8 @@ class DeepOCSortEngine:
         if img_shapes is not None:
             wh = np.ascontiguousarray([[int(sh[1]), int(sh[0])] for sh in img_shapes],
                                       dtype=np.int32)
-        cap, _ = self.capacity()
-        need = self.n_streams * cap + int(off[-1]) + 1
+        # every output row is a track matched to or born from one of this frame's detections
+        need = max(int(off[-1]), 1)
         if len(self._out) < need:
             self._out = np.empty((2 * need, 8), dtype=np.float64)
         nid = None
@@ -161,7 +163,8 @@ class DeepOCSort:
     model_weights / fp16 name the reference's ReID model, which is outside the hot path: pass
     `reid=` (an object with get_features(xyxys, img) -> (n, D) float32) or give
     `update(..., embs=...)` the embeddings of every input detection.  `cmc=` replaces the
-    SparseOptFlow estimator (an object with apply(img, dets) -> 2x3 warp; default static camera).
+    SparseOptFlow estimator (an object with apply(img, dets) -> 2x3 warp; without one and with
+    cmc_off=False the identity warp is used and a one-time RuntimeWarning says so).
     """
 
     def __init__(self, model_weights=None, device=0, fp16=False, per_class=True, det_thresh=0.3,
@@ -191,7 +194,7 @@ class DeepOCSort:
         self.new_kf_off = new_kf_off
         KalmanBoxTracker.count = 1                                   # :347
         self.model = reid
-        self.cmc = cmc
+        self.cmc = cmc if cmc is not None or cmc_off else default_cmc("DeepOCSort")
         self._kw = dict(det_thresh=det_thresh, max_age=max_age, min_hits=min_hits,
                         iou_threshold=iou_threshold, delta_t=delta_t, asso_func=asso_func,
                         inertia=inertia, w_association_emb=w_association_emb,

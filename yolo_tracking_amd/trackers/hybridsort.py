@@ -104,8 +104,8 @@ class HybridSortEngine:
                 raise ValueError(f"stream {s}: {len(f)} embeddings for {len(d)} detections")
             rows.append(f)
         feats = np.ascontiguousarray(np.concatenate(rows)) if rows else None
-        cap, _ = self.capacity()
-        need = self.n_streams * cap + int(off[-1]) + 1
+        # every output row is a track matched to or born from one of this frame's detections
+        need = max(int(off[-1]), 1)
         if len(self._out) < need:
             self._out = np.empty((2 * need, 8), dtype=np.float64)
         nid = None

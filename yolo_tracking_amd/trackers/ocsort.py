@@ -86,8 +86,8 @@ class OCSortEngine:
         if img_shapes is not None:
             wh = np.ascontiguousarray([[int(sh[1]), int(sh[0])] for sh in img_shapes],
                                       dtype=np.int32)
-        cap, _ = self.capacity()
-        need = self.n_streams * cap + int(off[-1]) + 1
+        # every output row is a track matched to or born from one of this frame's detections
+        need = max(int(off[-1]), 1)
         if len(self._out) < need:
             self._out = np.empty((2 * need, 8), dtype=np.float64)
         nid = None
