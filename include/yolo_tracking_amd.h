@@ -449,6 +449,65 @@ int yta_reid_normalize(int device, float *feats, long long count);
 /* Device form: d_work holds >= 256 doubles of scratch. */
 int yta_reid_normalize_device(float *d_feats, long long count, double *d_work, void *stream);
 
+/* ---- Camera-motion compensation: SparseOptFlow (boxmot/motion/cmc/sof.py:15-162) -------------
+ * The estimator BoTSORT (bot_sort.py:228, :293) and DeepOCSort (deep_ocsort.py:351, :391) call once
+ * per frame: apply(img, dets) -> 2x3 float64 warp.  Per stream: gray (cvtColor BGR2GRAY), resize
+ * by `scale` (INTER_LINEAR), on the first frame goodFeaturesToTrack(maxCorners 3000, quality
+ * 0.01, minDistance 1, blockSize 3) under generate_mask (cmc_interface.py:13-24: a 2 % border and
+ * every det box x scale); afterwards calcOpticalFlowPyrLK (21x21, 3 levels) of the stored corners
+ * from the previous accepted frame, estimateAffinePartial2D(RANSAC 3 px, 2000 iters, 0.99) + LM
+ * refinement, translation / scale.  The reference's quirks are kept: the corners are detected once
+ * and only filtered (sof.py:155 stores the tracked points under another name), a failed estimate
+ * returns the identity and keeps the previous frame.  S streams per engine, every stream's frame
+ * in the same launches.  Restatement and parity: oracle/cmc_sof.py (unpinned against cv2 itself). */
+typedef struct yta_sof yta_sof;
+/* max_h / max_w: the largest input frame (pixels) any stream will pass (device-buffer form; the
+ * host-buffer form grows them). */
+int yta_sof_create(int device, int n_streams, double scale, int max_h, int max_w,
+                   yta_sof **engine);
+int yta_sof_destroy(yta_sof *engine);
+int yta_sof_reset(yta_sof *engine);
+/* Host-buffer apply (synchronous).  frames: stream s's h x w x 3 uint8 BGR frame at
+ * frames + frame_off[s] (bytes), frame_hw[2 s] = h, frame_hw[2 s + 1] = w; dets: packed float64
+ * rows of det_stride (>= 4) columns, x1 y1 x2 y2 first, stream s at rows det_off[s] ..
+ * det_off[s+1]-1 (the rows the tracker passes to cmc.apply); warps: S x 6 float64 out. */
+int yta_sof_apply(yta_sof *engine, const uint8_t *frames, const long long *frame_off,
+                  const int *frame_hw, const double *dets, int det_stride, const int *det_off,
+                  double *warps);
+/* Device-buffer apply (asynchronous on the engine stream): the same layout in device memory;
+ * d_warps (S x 6 float64) can be handed straight to yta_botsort_update_device /
+ * yta_deepocsort_update_device. */
+int yta_sof_apply_device(yta_sof *engine, const uint8_t *d_frames, const long long *d_frame_off,
+                         const int *d_frame_hw, const double *d_dets, int det_stride,
+                         const int *d_det_off, double *d_warps);
+int yta_sof_sync(yta_sof *engine);
+/* Parity introspection of stream s: the stored corners (prev_keypoints, n x 2 float32, up to
+ * cap), whether the stream has its first frame, and the stored previous gray frame (h x w uint8,
+ * may be NULL). */
+int yta_sof_get_state(yta_sof *engine, int stream, int *initialized, int *n_kp, float *kp,
+                      int cap, int *h, int *w, uint8_t *prev_img, int img_cap);
+/* Last apply's per-stream outcome (S ints): 0 first frame (corners detected or none found),
+ * 1 estimated (warp from RANSAC / 2-point model), 2 identity (no corners left / fewer than two
+ * tracked / RANSAC found no model). */
+int yta_sof_outcome(yta_sof *engine, int *outcome);
+int yta_sof_hip_stream(yta_sof *engine, void **stream);
+
+/* Known-answer entries for the estimator's stages (synchronous, host buffers, one image):
+ * gray small image (preprocess) of an h x w x 3 BGR frame -> out (round(h*scale) x round(w*scale));
+ * min-eigenvalue map (cornerMinEigenVal, blockSize 3, ksize 3) of a gray image -> float32;
+ * goodFeaturesToTrack under a mask -> corners (n x 2 float32, up to 3000). */
+int yta_sof_kat_preprocess(int device, const uint8_t *frame, int h, int w, double scale,
+                           uint8_t *out, int *out_h, int *out_w);
+int yta_sof_kat_min_eigen(int device, const uint8_t *gray, int h, int w, float *eig);
+int yta_sof_kat_corners(int device, const uint8_t *gray, const uint8_t *mask, int h, int w,
+                        float *corners, int *n);
+/* calcOpticalFlowPyrLK of n points between two gray images (same size) -> next (n x 2 float32),
+ * status (n uint8); estimateAffinePartial2D(RANSAC) + refinement of n point pairs -> M (2 x 3
+ * float64), *ok = 0 when no model (fewer than 2 points). */
+int yta_sof_kat_lk(int device, const uint8_t *prev, const uint8_t *next, int h, int w,
+                   const float *pts, int n, float *next_pts, uint8_t *status);
+int yta_sof_kat_affine(int device, const float *src, const float *dst, int n, double *M, int *ok);
+
 #ifdef __cplusplus
 }
 #endif

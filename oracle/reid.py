@@ -47,8 +47,10 @@ def crop_rect(box, h, w):
     return (ys.start, ys.stop, xs.start, xs.stop) if len(ys) and len(xs) else None
 
 
-def _axis(ssize, dsize):
-    scale = 1.0 / (np.float64(dsize) / np.float64(ssize))
+def _axis(ssize, dsize, inv_scale=None):
+    # resizeGeneric: scale = 1 / inv_scale, inv_scale = dsize / ssize unless the caller gave fx/fy
+    inv = np.float64(dsize) / np.float64(ssize) if inv_scale is None else np.float64(inv_scale)
+    scale = 1.0 / inv
     d = np.arange(dsize, dtype=np.float64)
     f = ((d + 0.5) * scale - 0.5).astype(np.float32)
     s = np.floor(f).astype(np.int64)
@@ -60,12 +62,14 @@ def _sat_short(v):
     return np.rint(v.astype(np.float32)).astype(np.int64)
 
 
-def resize_linear_u8(crop, out_w, out_h):
-    """cv2.resize(crop, (out_w, out_h), interpolation=cv2.INTER_LINEAR) for an (H, W, C) uint8."""
+def resize_linear_u8(crop, out_w, out_h, fx=None, fy=None):
+    """cv2.resize(crop, (out_w, out_h), interpolation=cv2.INTER_LINEAR) for an (H, W, C) uint8;
+    fx / fy: the scale factors of cv2.resize(crop, (0, 0), fx=, fy=) (out_w / out_h then
+    round(W * fx) / round(H * fy))."""
     crop = np.asarray(crop, dtype=np.uint8)
     H, W = crop.shape[:2]
-    sx, fx, scx = _axis(W, out_w)
-    sy, fy, scy = _axis(H, out_h)
+    sx, fx, scx = _axis(W, out_w, fx)
+    sy, fy, scy = _axis(H, out_h, fy)
     src = crop.astype(np.int64)
     if abs(scx - 2.0) < np.finfo(np.float64).eps and abs(scy - 2.0) < np.finfo(np.float64).eps:
         s = (src[0:2 * out_h:2, 0:2 * out_w:2] + src[0:2 * out_h:2, 1:2 * out_w:2]

@@ -5,7 +5,7 @@ root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc_sq"
 agg = collections.defaultdict(lambda: collections.defaultdict(list))
 for f in glob.glob(os.path.join(root, "*", "**", "*counter_collection.csv"), recursive=True):
     for r in csv.DictReader(open(f)):
-        k = r["Kernel_Name"].replace("yta::(anonymous namespace)::", "").split("(")[0]
+        k = r["Kernel_Name"].replace("yta::(anonymous namespace)::", "").replace("void ", "").split("(")[0]
         agg[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
 for k, d in agg.items():
     if not k.startswith("k_"):

@@ -155,6 +155,20 @@ _SIGS = {
     "yta_reid_preprocess_device": ([_P, _P, _P, _P, _P, _I, _I, _I, _I, _P, _P, _P], _I),
     "yta_reid_normalize": ([_I, _P, ctypes.c_longlong], _I),
     "yta_reid_normalize_device": ([_P, ctypes.c_longlong, _P, _P], _I),
+    "yta_sof_create": ([_I, _I, _D, _I, _I, _P], _I),
+    "yta_sof_destroy": ([_P], _I),
+    "yta_sof_reset": ([_P], _I),
+    "yta_sof_apply": ([_P, _P, _P, _P, _P, _I, _P, _P], _I),
+    "yta_sof_apply_device": ([_P, _P, _P, _P, _P, _I, _P, _P], _I),
+    "yta_sof_sync": ([_P], _I),
+    "yta_sof_get_state": ([_P, _I, _P, _P, _P, _I, _P, _P, _P, _I], _I),
+    "yta_sof_outcome": ([_P, _P], _I),
+    "yta_sof_hip_stream": ([_P, _P], _I),
+    "yta_sof_kat_preprocess": ([_I, _P, _I, _I, _D, _P, _P, _P], _I),
+    "yta_sof_kat_min_eigen": ([_I, _P, _I, _I, _P], _I),
+    "yta_sof_kat_corners": ([_I, _P, _P, _I, _I, _P, _P], _I),
+    "yta_sof_kat_lk": ([_I, _P, _P, _I, _I, _P, _I, _P, _P], _I),
+    "yta_sof_kat_affine": ([_I, _P, _P, _I, _P, _P], _I),
 }
 
 EXPORTED_SYMBOLS = tuple(_SIGS)
