@@ -206,3 +206,60 @@ def test_dropin_sparse_opt_flow_matches_oracle():
         H = a.apply(fr, np.hstack([dets, np.ones((len(dets), 3))]))   # 7-column dets_first rows
         assert H.shape == (2, 3) and H.dtype == np.float64
         assert np.array_equal(H, o.apply(fr, dets))
+
+
+def _moving_camera_case(n_frames=10, n=48, seed=61):
+    """Detections from the synthetic stream generator, frames from a moving textured scene."""
+    from yolo_tracking_amd.synth import make_frames
+    fr = make_frames(n, n_frames, seed, emb_dim=16, low_conf_frac=0.1)
+    C = int(64 * np.sqrt(n))
+    imgs, _ = sequence(C + 64, C + 64, n_frames, seed, step=(0.1, 1.0, 3.0, -2.0))
+    return fr, imgs
+
+
+def test_botsort_default_cmc_end_to_end():
+    """BoTSORT() with no cmc= runs the GPU SparseOptFlow (bot_sort.py:228, :293) on every frame;
+    against the oracle tracker fed the restated estimator's warps: ids / scores / det_ind
+    bit-exact, boxes to 1e-9 relative (the warped covariance's cross terms)."""
+    from oracle.botsort import BoTSORTOracle
+    from yolo_tracking_amd.trackers.botsort import BoTSORT
+    frames, imgs = _moving_camera_case()
+    params = dict(track_high_thresh=0.5, track_low_thresh=0.1, new_track_thresh=0.6,
+                  track_buffer=30, match_thresh=0.8, proximity_thresh=0.5,
+                  appearance_thresh=0.25, frame_rate=30)
+    t = BoTSORT(None, 0, False, with_reid=False, **params)
+    assert isinstance(t.cmc, SparseOptFlow)
+    ref = BoTSORTOracle(with_reid=False, **params)
+    sof = cs.SparseOptFlowOracle()
+    moved = 0
+    for f, ((dets, _), img) in enumerate(zip(frames, imgs)):
+        got = np.asarray(t.update(dets, img)).reshape(-1, 8)
+        warp = sof.apply(img, dets[dets[:, 4] > params["track_high_thresh"]])
+        moved += not np.array_equal(warp, np.eye(2, 3))
+        exp = ref.update(dets, None, warp).reshape(-1, 8)
+        assert got.shape == exp.shape, f
+        assert np.array_equal(got[:, 4:], exp[:, 4:]), f
+        np.testing.assert_allclose(got[:, :4], exp[:, :4], rtol=1e-9, atol=1e-6)
+    assert moved >= len(frames) - 1
+
+
+def test_deepocsort_default_cmc_end_to_end():
+    """DeepOCSort() with no cmc= (deep_ocsort.py:351, :391) against the oracle fed the restated
+    estimator's warps (on the kept detections' boxes): ids / scores / det_ind bit-exact, boxes to
+    1e-9 relative (the warped 2x2 blocks meet LAPACK's LU in the reference)."""
+    from oracle.deepocsort import DeepOCSortOracle
+    from yolo_tracking_amd.trackers.deepocsort import DeepOCSort
+    frames, imgs = _moving_camera_case(seed=62)
+    kw = dict(det_thresh=0.3, max_age=30, min_hits=1, iou_threshold=0.3, delta_t=3,
+              asso_func="giou", inertia=0.2)
+    t = DeepOCSort(None, 0, False, embedding_off=True, **kw)
+    assert isinstance(t.cmc, SparseOptFlow)
+    ref = DeepOCSortOracle(embedding_off=True, **kw)
+    sof = cs.SparseOptFlowOracle()
+    for f, ((dets, _), img) in enumerate(zip(frames, imgs)):
+        got = np.asarray(t.update(dets, img)).reshape(-1, 8)
+        warp = sof.apply(img, dets[dets[:, 4] > kw["det_thresh"], :4])
+        exp = np.asarray(ref.update(dets, img.shape, None, warp), dtype=np.float64).reshape(-1, 8)
+        assert got.shape == exp.shape, f
+        assert np.array_equal(got[:, 4:], exp[:, 4:]), f
+        np.testing.assert_allclose(got[:, :4], exp[:, :4], rtol=1e-9, atol=1e-6)

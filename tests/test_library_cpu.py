@@ -68,17 +68,12 @@ def test_synthetic_stream_is_deterministic():
     assert a[0][0].shape == (128, 6)
 
 
-def test_default_cmc_warns_once_and_is_identity():
-    """Without cmc= the trackers use the identity warp and say so once (the reference always
-    runs SparseOptFlow, bot_sort.py:228 / deep_ocsort.py:351)."""
-    import warnings
-
-    from yolo_tracking_amd.motion import cmc as m
-    m._warned.discard("UnitTest")
-    with warnings.catch_warnings(record=True) as w:
-        warnings.simplefilter("always")
-        c1 = m.default_cmc("UnitTest")
-        c2 = m.default_cmc("UnitTest")
-    assert sum(issubclass(x.category, RuntimeWarning) for x in w) == 1
-    assert np.array_equal(c1.apply(None, None), np.eye(2, 3))
-    assert isinstance(c2, m.IdentityCMC)
+def test_default_cmc_is_sparse_opt_flow():
+    """Without cmc= the trackers get SparseOptFlow, as in the reference (bot_sort.py:228,
+    deep_ocsort.py:351); constructing it touches no GPU (the engine starts with the first frame)."""
+    from yolo_tracking_amd.motion import IdentityCMC, SparseOptFlow, default_cmc, get_cmc_method
+    assert isinstance(default_cmc("BoTSORT"), SparseOptFlow)
+    assert get_cmc_method("sof") is SparseOptFlow
+    with pytest.raises(NotImplementedError):
+        get_cmc_method("ecc")
+    assert np.array_equal(IdentityCMC().apply(None, None), np.eye(2, 3))

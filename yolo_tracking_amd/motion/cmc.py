@@ -3,37 +3,32 @@
 Reference: BoTSORT always builds SparseOptFlow() (boxmot/trackers/botsort/bot_sort.py:228) and
 DeepOCSort builds get_cmc_method('sof')() (deep_ocsort.py:351); both call cmc.apply(img, dets)
 once per frame (bot_sort.py:293, deep_ocsort.py:391) and apply the returned 2x3 affine to every
-track (multi_gmc / apply_affine_correction), which the device engines do.
+track (multi_gmc / apply_affine_correction), which the device engines do.  The default estimator
+here is the same SparseOptFlow, on the GPU (motion/sof.py, csrc/cmc.hip).
 """
-import warnings
-
 import numpy as np
+
+from .sof import SparseOptFlow
 
 
 class IdentityCMC:
-    """Static-camera motion model: the identity warp every frame."""
+    """Static-camera motion model: the identity warp every frame (pass cmc=IdentityCMC() to
+    skip camera-motion estimation)."""
 
     def apply(self, img, dets):
         return np.eye(2, 3)
 
 
-_warned = set()
+def get_cmc_method(cmc_method):
+    """boxmot.motion.cmc.get_cmc_method (motion/cmc/__init__.py): the estimator class by name.
+    Only the sparse optical flow estimator the trackers use is on the device path."""
+    if cmc_method in ("sof", "sparseOptFlow"):
+        return SparseOptFlow
+    raise NotImplementedError(f"cmc method {cmc_method!r}: only 'sof' (SparseOptFlow, the "
+                              "estimator BoTSORT and DeepOCSort build) is on the MI355X path")
 
 
-def default_cmc(owner):
-    """The estimator a tracker gets when the caller passes no `cmc=`.
-
-    The reference estimates the warp with OpenCV's sparse optical flow; this build has no such
-    estimator on the default path, so the identity warp is used and a one-time warning says so:
-    on a moving camera the tracks then differ from the reference's.  Pass `cmc=IdentityCMC()`
-    to state a static camera explicitly (no warning), or any object with apply(img, dets) -> 2x3.
-    """
-    if owner not in _warned:
-        _warned.add(owner)
-        warnings.warn(
-            f"{owner}: no cmc= estimator given; the reference runs SparseOptFlow here "
-            "(bot_sort.py:228, deep_ocsort.py:351). Using the identity warp (static camera): on a "
-            "moving camera the tracks differ from the reference's. Pass cmc=IdentityCMC() to "
-            "silence this, or an object with apply(img, dets) -> 2x3 warp.",
-            RuntimeWarning, stacklevel=3)
-    return IdentityCMC()
+def default_cmc(owner=None, device=0):
+    """The estimator a tracker gets when the caller passes no `cmc=`: SparseOptFlow(), as in the
+    reference (bot_sort.py:228, deep_ocsort.py:351)."""
+    return SparseOptFlow(device=device)

@@ -7,11 +7,11 @@ float64 appearance embeddings) lives in HBM inside the C-ABI engine
 (yolo_tracking_amd/csrc/deepocsort.hip); this module validates inputs, gets the frame's ReID
 features and camera warp from the pluggable producers and returns the (K, 8) result.
 
-The ReID forward pass (:387 get_features) and the SparseOptFlow CMC estimator (:391 cmc.apply) are
-not part of the hot path: pass `reid=` (an object with get_features(xyxys, img) ->
-(n, D) float32) or give `update(..., embs=...)` the frame's per-detection embeddings, and `cmc=`
-(an object with apply(img, dets) -> 2x3 warp) for a moving camera (without one: identity warp and
-a one-time RuntimeWarning).
+The ReID forward pass (:387 get_features) is the caller's: pass `reid=` (an object with
+get_features(xyxys, img) -> (n, D) float32) or give `update(..., embs=...)` the frame's
+per-detection embeddings.  The camera warp (:391 cmc.apply) comes from SparseOptFlow on the GPU
+(yolo_tracking_amd/motion/sof.py, the reference's estimator, :351) unless `cmc=` (an object with
+apply(img, dets) -> 2x3 warp) replaces it.
 """
 import ctypes
 
@@ -163,8 +163,8 @@ class DeepOCSort:
     model_weights / fp16 name the reference's ReID model, which is outside the hot path: pass
     `reid=` (an object with get_features(xyxys, img) -> (n, D) float32) or give
     `update(..., embs=...)` the embeddings of every input detection.  `cmc=` replaces the
-    SparseOptFlow estimator (an object with apply(img, dets) -> 2x3 warp; without one and with
-    cmc_off=False the identity warp is used and a one-time RuntimeWarning says so).
+    SparseOptFlow estimator, which runs on the GPU by default as in the reference (deep_ocsort.py:351;
+    an object with apply(img, dets) -> 2x3 warp, e.g. IdentityCMC() for a static camera).
     """
 
     def __init__(self, model_weights=None, device=0, fp16=False, per_class=True, det_thresh=0.3,
@@ -194,7 +194,7 @@ class DeepOCSort:
         self.new_kf_off = new_kf_off
         KalmanBoxTracker.count = 1                                   # :347
         self.model = reid
-        self.cmc = cmc if cmc is not None or cmc_off else default_cmc("DeepOCSort")
+        self.cmc = cmc if cmc is not None or cmc_off else default_cmc("DeepOCSort", device)
         self._kw = dict(det_thresh=det_thresh, max_age=max_age, min_hits=min_hits,
                         iou_threshold=iou_threshold, delta_t=delta_t, asso_func=asso_func,
                         inertia=inertia, w_association_emb=w_association_emb,
