@@ -126,10 +126,15 @@ __host__ __device__ inline int sof_nlevels(int h, int w) {
     return n;
 }
 
-__host__ __device__ inline long long sof_slot_px(int h, int w) {
-    Lv lv[SOF_MAX_LEVEL + 1];
-    const int n = sof_levels(h, w, lv);
-    return lv[n - 1].off + (long long)lv[n - 1].h * lv[n - 1].w;
+__host__ __device__ inline long long sof_slot_px(int h, int w) {   // pixels of every level
+    const int n = sof_nlevels(h, w);
+    long long px = 0;
+    for (int l = 0; l < n; ++l) {
+        px += (long long)h * w;
+        h = (h + 1) / 2;
+        w = (w + 1) / 2;
+    }
+    return px;
 }
 
 // borderInterpolate(p, n, BORDER_REFLECT_101)
@@ -209,53 +214,86 @@ __global__ __launch_bounds__(256) void k_sof_small(SofArgs a) {
 }
 
 // --------------------------------------------------------------------------------- k_sof_pyr
-__device__ __forceinline__ void pyr_levels_body(uint8_t *img, short2 *der, int h0, int w0) {
+// One level's pyrDown ([1 4 6 4 1]^2, reflect-101, (sum + 128) >> 8) and Scharr derivatives
+// (calcSharrDeriv) read from `src`: the level staged in LDS, or global memory.
+template <typename Src>
+__device__ __forceinline__ void pyr_level_work(Src src, int sh, int sw, uint8_t *dst, int h, int w,
+                                               short2 *d) {
     const int t = threadIdx.x, nt = blockDim.x;
-    Lv lv[SOF_MAX_LEVEL + 1];
-    const int nl = sof_levels(h0, w0, lv);
-    for (int l = 1; l < nl; ++l) {   // pyrDown: [1 4 6 4 1]^2, reflect-101, (sum + 128) >> 8
-        const uint8_t *src = img + lv[l - 1].off;
-        uint8_t *dst = img + lv[l].off;
-        const int sh = lv[l - 1].h, sw = lv[l - 1].w, h = lv[l].h, w = lv[l].w;
+    if (dst)
         for (int i = t; i < h * w; i += nt) {
             const int y = i / w, x = i - y * w;
             const int x0 = refl(2 * x - 2, sw), x1 = refl(2 * x - 1, sw), x2 = refl(2 * x, sw),
                       x3 = refl(2 * x + 1, sw), x4 = refl(2 * x + 2, sw);
             auto row5 = [&](int r) {
-                const uint8_t *p = src + (long long)refl(2 * y + r - 2, sh) * sw;
-                return (int)p[x0] + 4 * (int)p[x1] + 6 * (int)p[x2] + 4 * (int)p[x3] + (int)p[x4];
+                const int base = refl(2 * y + r - 2, sh) * sw;
+                return (int)src[base + x0] + 4 * (int)src[base + x1] + 6 * (int)src[base + x2] +
+                       4 * (int)src[base + x3] + (int)src[base + x4];
             };
             const int sum = row5(0) + 4 * row5(1) + 6 * row5(2) + 4 * row5(3) + row5(4);
             dst[i] = (uint8_t)((sum + 128) >> 8);
         }
-        block_sync();
+    for (int i = t; i < sh * sw; i += nt) {
+        const int y = i / sw, x = i - y * sw;
+        const int ym = refl(y - 1, sh) * sw, yp = refl(y + 1, sh) * sw, yc = y * sw;
+        const int xm = refl(x - 1, sw), xp = refl(x + 1, sw);
+        auto S = [&](int row, int xx) { return (int)src[row + xx]; };
+        const int t0m = (S(ym, xm) + S(yp, xm)) * 3 + S(yc, xm) * 10;
+        const int t0p = (S(ym, xp) + S(yp, xp)) * 3 + S(yc, xp) * 10;
+        const int t1m = S(yp, xm) - S(ym, xm), t1p = S(yp, xp) - S(ym, xp);
+        const int t1c = S(yp, x) - S(ym, x);
+        d[i] = make_short2((short)(t0p - t0m), (short)((t1p + t1m) * 3 + t1c * 10));
     }
-    for (int l = 0; l < nl; ++l) {   // calcSharrDeriv
-        const uint8_t *src = img + lv[l].off;
-        short2 *d = der + lv[l].off;
-        const int h = lv[l].h, w = lv[l].w;
-        for (int i = t; i < h * w; i += nt) {
-            const int y = i / w, x = i - y * w;
-            const int ym = refl(y - 1, h), yp = refl(y + 1, h);
-            const int xm = refl(x - 1, w), xp = refl(x + 1, w);
-            auto S = [&](int yy, int xx) { return (int)src[(long long)yy * w + xx]; };
-            const int t0m = (S(ym, xm) + S(yp, xm)) * 3 + S(y, xm) * 10;
-            const int t0p = (S(ym, xp) + S(yp, xp)) * 3 + S(y, xp) * 10;
-            const int t1m = S(yp, xm) - S(ym, xm), t1p = S(yp, xp) - S(ym, xp);
-            const int t1c = S(yp, x) - S(ym, x);
-            d[i] = make_short2((short)(t0p - t0m), (short)((t1p + t1m) * 3 + t1c * 10));
-        }
-    }
-    block_sync();
 }
 
-__global__ __launch_bounds__(SOF_T) void k_sof_pyr(SofArgs a) {
+// buildOpticalFlowPyramid + calcSharrDeriv of every level: level l is staged into LDS (when it
+// fits lds_cap bytes), then level l + 1 and level l's derivatives are computed from LDS.
+__device__ void pyr_levels_body(uint8_t *img, short2 *der, int h0, int w0, uint8_t *lds,
+                                int lds_cap) {
+    const int t = threadIdx.x, nt = blockDim.x;
+    const int nl = sof_nlevels(h0, w0);
+    int sh = h0, sw = w0;
+    long long off = 0;
+    for (int l = 0; l < nl; ++l) {
+        const int h = (sh + 1) / 2, w = (sw + 1) / 2;
+        const long long noff = off + (long long)sh * sw;
+        uint8_t *dst = l + 1 < nl ? img + noff : nullptr;
+        const uint8_t *src = img + off;
+        const int n = sh * sw;
+        if (n <= lds_cap) {
+            const int nw = (n + 3) / 4;   // slot levels are not word aligned: byte copy in words
+            for (int k = t; k < nw; k += nt) {
+                unsigned v = 0;
+                for (int b = 0; b < 4; ++b) {
+                    const int q = 4 * k + b;
+                    if (q < n) v |= (unsigned)src[q] << (8 * b);
+                }
+                reinterpret_cast<unsigned *>(lds)[k] = v;
+            }
+            __syncthreads();
+            pyr_level_work(lds, sh, sw, dst, h, w, der + off);
+        } else {
+            pyr_level_work(src, sh, sw, dst, h, w, der + off);
+        }
+        block_sync();
+        off = noff;
+        sh = h;
+        sw = w;
+    }
+}
+
+constexpr int PYR_T = 1024;
+constexpr int PYR_LDS = 64 * 1024;
+
+__global__ __launch_bounds__(PYR_T) void k_sof_pyr(SofArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int s = blockIdx.x;
     const SofState &st = a.state[s];
     if (st.mode != MODE_GFTT && st.mode != MODE_LK) return;
     const int cur = 1 - st.prev;
     const long long slot = (long long)s * 2 + cur;
-    pyr_levels_body(a.img + slot * a.slot_px, a.der + slot * a.slot_px, st.h0[cur], st.w0[cur]);
+    pyr_levels_body(a.img + slot * a.slot_px, a.der + slot * a.slot_px, st.h0[cur], st.w0[cur],
+                    smem, PYR_LDS);
     if (threadIdx.x == 0) a.state[s].levels[cur] = sof_nlevels(st.h0[cur], st.w0[cur]);
 }
 
@@ -518,6 +556,7 @@ __device__ __forceinline__ void lk_point(const LkPyr &pyr, int max_level, float2
         }
         int ival[LK_SLOTS], ixv[LK_SLOTS], iyv[LK_SLOTS];
         int s11 = 0, s12 = 0, s22 = 0;
+        const bool inside = ix >= 0 && iy >= 0 && ix + SOF_WIN < L.wI && iy + SOF_WIN < L.hI;
 #pragma unroll
         for (int m = 0; m < LK_SLOTS; ++m) {
             const int k = lane + WAVE * m;
@@ -525,17 +564,31 @@ __device__ __forceinline__ void lk_point(const LkPyr &pyr, int max_level, float2
             if (k >= SOF_WIN * SOF_WIN) continue;
             const int wy = k / SOF_WIN, wx = k - wy * SOF_WIN;
             const int y = iy + wy, x = ix + wx;
-            const int ry0 = refl(y, L.hI), ry1 = refl(y + 1, L.hI);
-            const int rx0 = refl(x, L.wI), rx1 = refl(x + 1, L.wI);
-            const uint8_t *r0 = L.I + (long long)ry0 * L.wI, *r1 = L.I + (long long)ry1 * L.wI;
-            ival[m] = ((int)r0[rx0] * w00 + (int)r0[rx1] * w01 + (int)r1[rx0] * w10 +
-                       (int)r1[rx1] * w11 + (1 << 8)) >> 9;
-            auto D = [&](int yy, int xx) {
-                return (yy >= 0 && yy < L.hI && xx >= 0 && xx < L.wI)
-                           ? L.dI[(long long)yy * L.wI + xx]
-                           : make_short2(0, 0);
-            };
-            const short2 d00 = D(y, x), d01 = D(y, x + 1), d10 = D(y + 1, x), d11 = D(y + 1, x + 1);
+            short2 d00, d01, d10, d11;
+            if (inside) {   // the window and its +1 taps lie inside the level
+                const uint8_t *r0 = L.I + y * L.wI + x, *r1 = r0 + L.wI;
+                ival[m] = ((int)r0[0] * w00 + (int)r0[1] * w01 + (int)r1[0] * w10 +
+                           (int)r1[1] * w11 + (1 << 8)) >> 9;
+                const short2 *q0 = L.dI + y * L.wI + x, *q1 = q0 + L.wI;
+                d00 = q0[0];
+                d01 = q0[1];
+                d10 = q1[0];
+                d11 = q1[1];
+            } else {
+                const int ry0 = refl(y, L.hI), ry1 = refl(y + 1, L.hI);
+                const int rx0 = refl(x, L.wI), rx1 = refl(x + 1, L.wI);
+                const uint8_t *r0 = L.I + ry0 * L.wI, *r1 = L.I + ry1 * L.wI;
+                ival[m] = ((int)r0[rx0] * w00 + (int)r0[rx1] * w01 + (int)r1[rx0] * w10 +
+                           (int)r1[rx1] * w11 + (1 << 8)) >> 9;
+                auto D = [&](int yy, int xx) {
+                    return (yy >= 0 && yy < L.hI && xx >= 0 && xx < L.wI) ? L.dI[yy * L.wI + xx]
+                                                                        : make_short2(0, 0);
+                };
+                d00 = D(y, x);
+                d01 = D(y, x + 1);
+                d10 = D(y + 1, x);
+                d11 = D(y + 1, x + 1);
+            }
             ixv[m] = ((int)d00.x * w00 + (int)d01.x * w01 + (int)d10.x * w10 + (int)d11.x * w11 +
                       (1 << 13)) >> 14;
             iyv[m] = ((int)d00.y * w00 + (int)d01.y * w01 + (int)d10.y * w10 + (int)d11.y * w11 +
@@ -565,19 +618,36 @@ __device__ __forceinline__ void lk_point(const LkPyr &pyr, int max_level, float2
                 break;
             }
             int p1 = 0, p2 = 0;
+            if (jx >= 0 && jy >= 0 && jx + SOF_WIN < L.wJ && jy + SOF_WIN < L.hJ) {
+                // the window and its +1 taps lie inside the level: no border handling
+                const uint8_t *b = L.J + jy * L.wJ + jx;
 #pragma unroll
-            for (int m = 0; m < LK_SLOTS; ++m) {
-                const int k = lane + WAVE * m;
-                if (k >= SOF_WIN * SOF_WIN) continue;
-                const int wy = k / SOF_WIN, wx = k - wy * SOF_WIN;
-                const int ry0 = refl(jy + wy, L.hJ), ry1 = refl(jy + wy + 1, L.hJ);
-                const int rx0 = refl(jx + wx, L.wJ), rx1 = refl(jx + wx + 1, L.wJ);
-                const uint8_t *r0 = L.J + (long long)ry0 * L.wJ, *r1 = L.J + (long long)ry1 * L.wJ;
-                const int jv = ((int)r0[rx0] * v00 + (int)r0[rx1] * v01 + (int)r1[rx0] * v10 +
-                                (int)r1[rx1] * v11 + (1 << 8)) >> 9;
-                const int diff = jv - ival[m];
-                p1 += diff * ixv[m];
-                p2 += diff * iyv[m];
+                for (int m = 0; m < LK_SLOTS; ++m) {
+                    const int k = lane + WAVE * m;
+                    if (k >= SOF_WIN * SOF_WIN) continue;
+                    const int wy = k / SOF_WIN, wx = k - wy * SOF_WIN;
+                    const uint8_t *r0 = b + wy * L.wJ + wx, *r1 = r0 + L.wJ;
+                    const int jv = ((int)r0[0] * v00 + (int)r0[1] * v01 + (int)r1[0] * v10 +
+                                    (int)r1[1] * v11 + (1 << 8)) >> 9;
+                    const int diff = jv - ival[m];
+                    p1 += diff * ixv[m];
+                    p2 += diff * iyv[m];
+                }
+            } else {
+#pragma unroll
+                for (int m = 0; m < LK_SLOTS; ++m) {
+                    const int k = lane + WAVE * m;
+                    if (k >= SOF_WIN * SOF_WIN) continue;
+                    const int wy = k / SOF_WIN, wx = k - wy * SOF_WIN;
+                    const int ry0 = refl(jy + wy, L.hJ), ry1 = refl(jy + wy + 1, L.hJ);
+                    const int rx0 = refl(jx + wx, L.wJ), rx1 = refl(jx + wx + 1, L.wJ);
+                    const uint8_t *r0 = L.J + ry0 * L.wJ, *r1 = L.J + ry1 * L.wJ;
+                    const int jv = ((int)r0[rx0] * v00 + (int)r0[rx1] * v01 + (int)r1[rx0] * v10 +
+                                    (int)r1[rx1] * v11 + (1 << 8)) >> 9;
+                    const int diff = jv - ival[m];
+                    p1 += diff * ixv[m];
+                    p2 += diff * iyv[m];
+                }
             }
             const float b1 = (float)wave_reduce(RED_SUM, (double)p1) * FLT_SCALE;
             const float b2 = (float)wave_reduce(RED_SUM, (double)p2) * FLT_SCALE;
@@ -615,14 +685,32 @@ __device__ __forceinline__ int lk_pyr(const SofArgs &a, int s, const SofState &s
     return np_ < nc ? np_ : nc;
 }
 
-__global__ __launch_bounds__(256) void k_sof_lk(SofArgs a) {
+// 8 points per block (one wave each).  LDSJ: the current frame's pyramid (every level, the
+// image each Lucas-Kanade iteration samples) is staged in LDS first, so the iterations' bilinear
+// taps are LDS reads; the previous frame and its derivatives are read once per level from HBM.
+constexpr int LKB = 512;
+
+template <bool LDSJ>
+__global__ __launch_bounds__(LKB) void k_sof_lk(SofArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int s = blockIdx.y;
     const SofState &st = a.state[s];
     if (st.mode != MODE_LK) return;
-    const int i = blockIdx.x * (256 / WAVE) + threadIdx.x / WAVE;
-    if (i >= st.n_kp) return;
+    const int n_kp = st.n_kp;
+    const int first = blockIdx.x * (LKB / WAVE);
+    if (first >= n_kp) return;   // block-uniform
     LkPyr P;
     const int nl = lk_pyr(a, s, st, P);
+    if (LDSJ) {
+        const long long n16 = (sof_slot_px(P.hJ, P.wJ) + 15) / 16;
+        const uint4 *src = reinterpret_cast<const uint4 *>(P.J);
+        uint4 *dst = reinterpret_cast<uint4 *>(smem);
+        for (long long k = threadIdx.x; k < n16; k += LKB) dst[k] = src[k];
+        __syncthreads();
+        P.J = smem;
+    }
+    const int i = first + threadIdx.x / WAVE;
+    if (i >= n_kp) return;
     float2 out;
     int status;
     lk_point(P, nl - 1, a.kp[(long long)s * SOF_MAXKP + i], out, status);
@@ -677,8 +765,11 @@ __device__ int update_num_iters(double p, double ep, int max_iters) {   // RANSA
     return (denom >= 0 || -num >= max_iters * (-denom)) ? max_iters : (int)rint(num / denom);
 }
 
+constexpr int FIT_K = 15;   // values reduced together by lm_normal: A (10), v (4), S
+
 struct FitShared {
     double red[SOF_T];
+    double redk[FIT_K][SOF_T];
     double models[RB][6];
     int counts[RB];
     double best[6];
@@ -700,6 +791,21 @@ __device__ __forceinline__ double reduce256(double p, FitShared &sh) {
     const double r = sh.red[0];
     __syncthreads();
     return r;
+}
+
+// K independent reduce256 sums sharing each tree step's barrier (same order per value)
+template <int K>
+__device__ __forceinline__ void reduce256_k(const double *p, double *out, FitShared &sh) {
+    const int t = threadIdx.x;
+    for (int k = 0; k < K; ++k) sh.redk[k][t] = p[k];
+    __syncthreads();
+    for (int h = SOF_T / 2; h > 0; h >>= 1) {
+        if (t < h)
+            for (int k = 0; k < K; ++k) sh.redk[k][t] = sh.redk[k][t] + sh.redk[k][t + h];
+        __syncthreads();
+    }
+    for (int k = 0; k < K; ++k) out[k] = sh.redk[k][0];
+    __syncthreads();
 }
 
 // residual row e of AffinePartial2DRefineCallback::compute (x rows even, y rows odd)
@@ -768,14 +874,16 @@ __device__ void lm_normal(const double *x, const float2 *src, const float2 *dst,
         ps = ps + r * r;
         pm = fmax(pm, fabs(r));
     }
+    double vals[FIT_K], sums[FIT_K];
+    for (int k = 0; k < 10; ++k) vals[k] = pa[k];
+    for (int k = 0; k < 4; ++k) vals[10 + k] = pv[k];
+    vals[14] = ps;
+    reduce256_k<FIT_K>(vals, sums, sh);
     int q = 0;
     for (int i = 0; i < 4; ++i)
-        for (int j = i; j < 4; ++j) {
-            const double s = reduce256(pa[q++], sh);
-            A[4 * i + j] = A[4 * j + i] = s;
-        }
-    for (int i = 0; i < 4; ++i) v[i] = reduce256(pv[i], sh);
-    *S = reduce256(ps, sh);
+        for (int j = i; j < 4; ++j, ++q) A[4 * i + j] = A[4 * j + i] = sums[q];
+    for (int i = 0; i < 4; ++i) v[i] = sums[10 + i];
+    *S = sums[14];
     // max |r|: order-free
     pm = wave_reduce(RED_MAX, pm);
     if (lane_id() == 0) sh.red[t / WAVE] = pm;
@@ -975,8 +1083,9 @@ __global__ __launch_bounds__(GFTT_T) void k_kat_gftt(const uint8_t *g, const uin
     gftt_body(g, mask, h, w, cov, eig, keys, keys_cap, (unsigned long long *)smem, out, n_out, sh);
 }
 
-__global__ __launch_bounds__(SOF_T) void k_kat_pyr(uint8_t *img, short2 *der, int h, int w) {
-    pyr_levels_body(img, der, h, w);
+__global__ __launch_bounds__(PYR_T) void k_kat_pyr(uint8_t *img, short2 *der, int h, int w) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    pyr_levels_body(img, der, h, w, smem, PYR_LDS);
 }
 
 __global__ __launch_bounds__(256) void k_kat_lk(const uint8_t *pimg, const short2 *pder,
@@ -1164,11 +1273,15 @@ int sof_launch(yta_sof *e) {
     const int blocks = (int)((a.npx + 255) / 256);
     hipLaunchKernelGGL(k_sof_small, dim3(blocks, a.S), dim3(256), 0, e->stream, a);
     YTA_HIP(hipGetLastError());
-    hipLaunchKernelGGL(k_sof_pyr, dim3(a.S), dim3(SOF_T), 0, e->stream, a);
+    hipLaunchKernelGGL(k_sof_pyr, dim3(a.S), dim3(PYR_T), PYR_LDS, e->stream, a);
     YTA_HIP(hipGetLastError());
     hipLaunchKernelGGL(k_sof_gftt, dim3(a.S), dim3(GFTT_T), SORT_CAP * 8, e->stream, a);
     YTA_HIP(hipGetLastError());
-    hipLaunchKernelGGL(k_sof_lk, dim3((SOF_MAXKP + 3) / 4, a.S), dim3(256), 0, e->stream, a);
+    const dim3 glk((SOF_MAXKP + LKB / WAVE - 1) / (LKB / WAVE), a.S);
+    if (a.slot_px <= PYR_LDS)
+        hipLaunchKernelGGL(k_sof_lk<true>, glk, dim3(LKB), (size_t)a.slot_px, e->stream, a);
+    else
+        hipLaunchKernelGGL(k_sof_lk<false>, glk, dim3(LKB), 0, e->stream, a);
     YTA_HIP(hipGetLastError());
     hipLaunchKernelGGL(k_sof_fit, dim3(a.S), dim3(SOF_T), 0, e->stream, a);
     YTA_HIP(hipGetLastError());
@@ -1182,6 +1295,9 @@ int set_sof_lds() {
                                 hipFuncAttributeMaxDynamicSharedMemorySize, SORT_CAP * 8));
     YTA_HIP(hipFuncSetAttribute((const void *)k_kat_gftt,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, SORT_CAP * 8));
+    for (const void *k : {(const void *)k_sof_pyr, (const void *)k_kat_pyr,
+                          (const void *)k_sof_lk<true>})
+        YTA_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, PYR_LDS));
     done = true;
     return YTA_OK;
 }
@@ -1500,6 +1616,7 @@ int yta_sof_kat_lk(int device, const uint8_t *prev, const uint8_t *next, int h, 
     YTA_CHECK(prev && next && h > 0 && w > 0 && n >= 0 && (n == 0 || (pts && next_pts && status)),
               YTA_ERR_INVALID, "bad argument");
     KAT(select_device(device));
+    KAT(set_sof_lds());
     if (n == 0) return YTA_OK;
     KatMem m;
     const long long px = sof_slot_px(h, w);
@@ -1517,8 +1634,8 @@ int yta_sof_kat_lk(int device, const uint8_t *prev, const uint8_t *next, int h, 
     KAT(m.alloc(&dst, n));
     YTA_HIP(hipMemcpy(pi, prev, (size_t)h * w, hipMemcpyHostToDevice));
     YTA_HIP(hipMemcpy(ni, next, (size_t)h * w, hipMemcpyHostToDevice));
-    hipLaunchKernelGGL(k_kat_pyr, dim3(1), dim3(SOF_T), 0, 0, pi, pd, h, w);
-    hipLaunchKernelGGL(k_kat_pyr, dim3(1), dim3(SOF_T), 0, 0, ni, nd, h, w);
+    hipLaunchKernelGGL(k_kat_pyr, dim3(1), dim3(PYR_T), PYR_LDS, 0, pi, pd, h, w);
+    hipLaunchKernelGGL(k_kat_pyr, dim3(1), dim3(PYR_T), PYR_LDS, 0, ni, nd, h, w);
     hipLaunchKernelGGL(k_kat_lk, dim3((n + 3) / 4), dim3(256), 0, 0, pi, pd, ni, h, w, dp, n, dout,
                        dst);
     YTA_HIP(hipGetLastError());
