@@ -126,6 +126,24 @@ def test_grid_pairs_complete(seed):
         assert np.array_equal(got, _brute_pairs(a, b, thresh)), thresh
 
 
+@pytest.mark.parametrize("seed", range(4))
+def test_grid_pairs_near_threshold(seed):
+    """The corner-window query (IoU > 1 - thresh) on many jittered copies, IoUs spread across the
+    threshold, boxes of mixed sizes (incl. big ones that bypass the grid)."""
+    rng = np.random.default_rng(100 + seed)
+    n = 600
+    xy = rng.uniform(0, 1500, size=(n, 2))
+    wh = rng.uniform(8, 120, size=(n, 2)) * rng.choice([1, 1, 1, 1, 10], size=(n, 1))
+    a = np.concatenate([xy, xy + wh], 1)
+    jit = rng.uniform(0, 0.25, size=(n, 1)) * np.concatenate([wh, wh], 1)
+    b = a + rng.uniform(-1, 1, size=(n, 4)) * jit
+    b[:, 2:] = np.maximum(b[:, 2:], b[:, :2] + 1)
+    for thresh in (0.05, 0.15, 0.3, 0.6):
+        got = _lib.grid_pairs(a, b, thresh)
+        exp = _brute_pairs(a, b, thresh)
+        assert len(exp) > 50 and np.array_equal(got, exp), thresh
+
+
 def test_grid_pairs_mot17_dedup_case():
     """The lost / tracked boxes of MOT17-02 frame 316 (a duplicate at IoU distance 0.129)."""
     L = np.array([[430.97677576, 457.72682571, 460.54623113, 554.13059315],

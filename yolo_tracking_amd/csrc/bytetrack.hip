@@ -826,8 +826,10 @@ __device__ __forceinline__ void finish_body(const BtArgs &a, int s, unsigned *bi
                             atomicOr(&dropA[p >> 5], 1u << (p & 31));
                     }
                 };
-                grid_query(gv, gh, tbx, [&](int q, const Box &lb, double) { pair(q, lb); },
-                           [&](int q) { pair(q, lbox(q)); });
+                // 1 - IoU < 0.15  <=>  IoU > 0.85: only corners within 0.18 w of tbx's
+                grid_query_iou_above(gv, gh, tbx, 0.85,
+                                     [&](int q, const Box &lb, double) { pair(q, lb); },
+                                     [&](int q) { pair(q, lbox(q)); });
             });
     }
     block_sync();

@@ -242,6 +242,59 @@ __device__ __forceinline__ void grid_scan(const GridView &gv, const GridHdr &h, 
     }
 }
 
+// Binned items whose top-left corner lies in [lx, hx] x [ly, hy] (a superset: whole cells):
+// hit(k, id, box, w).  Same pipelining as grid_scan.
+template <typename Hit>
+__device__ __forceinline__ void grid_scan_corner(const GridView &gv, const GridHdr &h, double lx,
+                                                 double hx, double ly, double hy, Hit hit) {
+    if (h.n_binned == 0) return;
+    if (!(hx >= lx && hy >= ly)) return;   // also false for NaN
+    const double fx1 = floor((hx - h.ox) * h.inv_g), fy1 = floor((hy - h.oy) * h.inv_g);
+    if (fx1 < 0.0 || fy1 < 0.0) return;
+    const int cx0 = grid_cell_1d(lx, h.ox, h.inv_g, h.gx);
+    const int cy0 = grid_cell_1d(ly, h.oy, h.inv_g, h.gy);
+    const int cx1 = fx1 > (double)(h.gx - 1) ? h.gx - 1 : (int)fx1;
+    const int cy1 = fy1 > (double)(h.gy - 1) ? h.gy - 1 : (int)fy1;
+    auto wt = [&](int k) { return gv.w ? gv.w[k] : 1.0; };
+    int b = ald(gv.cell_start + cy0 * h.gx + cx0), e = ald(gv.cell_start + cy0 * h.gx + cx1 + 1);
+    for (int cy = cy0; cy <= cy1; ++cy) {
+        int nb = 0, ne = 0;
+        if (cy < cy1) {
+            const int base = (cy + 1) * h.gx;
+            nb = ald(gv.cell_start + base + cx0);
+            ne = ald(gv.cell_start + base + cx1 + 1);
+        }
+        int k = b;
+        for (; k + 1 < e; k += 2) {
+            const Box b0 = gv.boxes[k], b1 = gv.boxes[k + 1];
+            const int i0 = gv.ids[k], i1 = gv.ids[k + 1];
+            const double w0 = wt(k), w1 = wt(k + 1);
+            hit(k, i0, b0, w0);
+            hit(k + 1, i1, b1, w1);
+        }
+        if (k < e) hit(k, gv.ids[k], gv.boxes[k], wt(k));
+        b = nb;
+        e = ne;
+    }
+}
+
+// Every binned item that can have IoU(T, item) > t (0 < t < 1), plus every big item: IoU > t
+// needs the intersection width > t * max(w_T, w_item), so the corners differ by less than
+// (1 - t) / t * w_T in x (likewise in y); a relative 1e-6 plus an absolute slack covers the
+// rounding of the bound.  visit(id, box, w) then decides exactly.
+template <typename Visit, typename VisitBig>
+__device__ __forceinline__ void grid_query_iou_above(const GridView &gv, const GridHdr &h,
+                                                     const Box &T, double t, Visit visit,
+                                                     VisitBig visit_big) {
+    for (int k = 0; k < h.n_big; ++k) visit_big(gv.big[k]);
+    if (!(T.x2 > T.x1 && T.y2 > T.y1)) return;   // intersects nothing (also NaN)
+    const double r = (1.0 - t) / t * (1.0 + 1e-6);
+    const double mx = (T.x2 - T.x1) * r + (fabs(T.x1) + 1.0) * 1e-9;
+    const double my = (T.y2 - T.y1) * r + (fabs(T.y1) + 1.0) * 1e-9;
+    grid_scan_corner(gv, h, T.x1 - mx, T.x1 + mx, T.y1 - my, T.y1 + my,
+                     [&](int, int id, const Box &b, double w) { visit(id, b, w); });
+}
+
 template <typename Visit, typename VisitBig>
 __device__ __forceinline__ void grid_query(const GridView &gv, const GridHdr &h, const Box &T,
                                            Visit visit, VisitBig visit_big) {

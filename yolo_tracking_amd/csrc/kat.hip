@@ -181,8 +181,15 @@ __global__ __launch_bounds__(1024) void k_grid_pairs(const Box *a, int na, const
                 if (k < cap) { pairs[2 * k] = p; pairs[2 * k + 1] = q; }
             }
         };
-        grid_query(gv, h, T, [&](int q, const Box &lb, double) { pair(q, lb); },
-                   [&](int q) { pair(q, b[q]); });
+        // thresh < 1: 1 - IoU < thresh needs IoU > 1 - thresh, the corner-window query the
+        // duplicate removal uses; thresh >= 1: every intersecting pair (the association query)
+        if (thresh < 1.0 && thresh > 0.0)
+            grid_query_iou_above(gv, h, T, 1.0 - thresh,
+                                 [&](int q, const Box &lb, double) { pair(q, lb); },
+                                 [&](int q) { pair(q, b[q]); });
+        else
+            grid_query(gv, h, T, [&](int q, const Box &lb, double) { pair(q, lb); },
+                       [&](int q) { pair(q, b[q]); });
     }
 }
 
