@@ -508,6 +508,23 @@ int yta_sof_kat_lk(int device, const uint8_t *prev, const uint8_t *next, int h, 
                    const float *pts, int n, float *next_pts, uint8_t *status);
 int yta_sof_kat_affine(int device, const float *src, const float *dst, int n, double *M, int *ok);
 
+/* ---- OSNet omni-scale block kernels (boxmot/appearance/backbones/osnet.py LightConv3x3 /
+ * ChannelGate / OSBlock; the ReID network's forward, appearance/osnet.py).  Device pointers,
+ * asynchronous on `stream` (a hipStream_t; NULL = default), NCHW planes, float32 (half = 0) or
+ * float16 (half = 1) storage, float32 arithmetic.
+ * yta_osnet_dw3x3: per sample n and channel c (plane of H x W at x + n x_n_stride + c x_c_stride,
+ * elements): depthwise 3x3 with zero padding 1 (w: C x 9 float32, BatchNorm folded) + b[c] +
+ * ReLU; channels c < n_first go to plane c of y_first (sample stride yf_n_stride) and add their
+ * plane sum to plane_sum[n ps_n_stride + c] (float32, may be NULL), the others to plane
+ * c - n_first of y_rest.  yta_osnet_gate_sum: out[n][c] = sum_b stack[n][b][c] * gate[n][b][c]
+ * for the 4 branches (stack N x 4 x C x P, gate N x 4 x C, out N x C x P). */
+int yta_osnet_dw3x3(const void *x, long long x_n_stride, long long x_c_stride, const float *w,
+                    const float *b, int N, int C, int H, int W, int half, void *y_first,
+                    long long yf_n_stride, int n_first, void *y_rest, long long yr_n_stride,
+                    float *plane_sum, long long ps_n_stride, void *stream);
+int yta_osnet_gate_sum(const void *stack, const void *gate, int N, int C, int P, int half,
+                       void *out, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

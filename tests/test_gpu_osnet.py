@@ -1,0 +1,146 @@
+"""GPU: the OSNet ReID network (appearance/osnet.py) against the reference's module
+(tests/golden/osnet_x0_25.npz: boxmot/appearance/backbones/osnet.py with random weights and
+BatchNorm statistics, eval mode), the weight-file path of ReIDDetectMultiBackend, and the trackers
+building their ReID producer from reid_weights as the reference does.
+
+Bar: float32 features within 1e-4 of the feature scale (MIOpen's convolution algorithms sum in
+other orders than the CPU's); float16 within 2e-2 relative (the reference's half=True path is
+float16 as well)."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from yolo_tracking_amd.appearance import ReIDDetectMultiBackend
+from yolo_tracking_amd.appearance.osnet import OSNetReID
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def golden(golden_dir):
+    g = np.load(os.path.join(golden_dir, "osnet_x0_25.npz"))
+    sd = {k[4:]: g[k] for k in g.files if k.startswith("sd__")}
+    x = np.random.default_rng(int(g["input_seed"])).standard_normal((4, 3, 256, 128))
+    return sd, x.astype(np.float32), g["features"]
+
+
+def test_osnet_float32_matches_reference(golden):
+    sd, x, ref = golden
+    y = OSNetReID("osnet_x0_25", sd, device="cuda:0")(torch.from_numpy(x).cuda()).cpu().numpy()
+    assert np.abs(y - ref).max() <= 1e-4 * np.abs(ref).max()
+
+
+def test_osnet_float16(golden):
+    sd, x, ref = golden
+    y = OSNetReID("osnet_x0_25", sd, device="cuda:0", half=True)(torch.from_numpy(x).cuda())
+    assert y.dtype == torch.float16
+    y = y.float().cpu().numpy()
+    assert np.abs(y - ref).max() <= 2e-2 * np.abs(ref).max()
+
+
+def test_weight_file_and_get_features(golden, tmp_path):
+    """A reference-format checkpoint ({'state_dict': ...} with 'module.' prefixes) loads through
+    ReIDDetectMultiBackend(weights); get_features = OSNet(crops) / global norm."""
+    sd, _, _ = golden
+    w = tmp_path / "osnet_x0_25_msmt17.pt"
+    torch.save({"state_dict": {"module." + k: torch.from_numpy(v) for k, v in sd.items()}}, w)
+    reid = ReIDDetectMultiBackend(w, device=0, fp16=False)
+    rng = np.random.default_rng(3)
+    img = rng.integers(0, 256, (480, 640, 3), dtype=np.uint8)
+    boxes = np.array([[10, 20, 110, 300], [300, 50, 380, 250], [500, 100, 639, 479]], np.float64)
+    f = reid.get_features(boxes, img)
+    crops = reid.preprocess(boxes, img)
+    raw = OSNetReID("osnet_x0_25", sd, device="cuda:0")(crops).cpu().numpy()
+    np.testing.assert_allclose(f, raw / np.linalg.norm(raw), rtol=1e-5, atol=1e-7)
+    reid.warmup()
+
+
+def test_trackers_build_reid_from_weights(tmp_path):
+    """create_tracker('botsort' / 'deepocsort' / 'hybridsort', cfg, reid_weights=<path>) builds
+    the OSNet producer (bot_sort.py:217-219); a missing file runs with random weights + warning."""
+    from yolo_tracking_amd import create_tracker, get_tracker_config
+    from yolo_tracking_amd.synth import make_frames
+    rng = np.random.default_rng(0)
+    img = rng.integers(0, 256, (640, 640, 3), dtype=np.uint8)
+    dets = make_frames(24, 1, 5, canvas=600.0)[0][0]
+    for name in ("botsort", "deepocsort", "hybridsort"):
+        with pytest.warns(RuntimeWarning):
+            t = create_tracker(name, get_tracker_config(name), tmp_path / "osnet_x0_25_x.pt", "0",
+                               False, False)
+        assert isinstance(t.model, ReIDDetectMultiBackend)
+        t.model.warmup()
+        r = np.asarray(t.update(dets, img))
+        assert r.size == 0 or r.shape[1] == 8
+
+
+# ---- the block kernels (csrc/osnet.hip) against PyTorch float32 on the same inputs
+def _dw_case(n, c, h, w, n_first, half, seed):
+    import ctypes
+    from yolo_tracking_amd import _lib
+    lib = _lib.load_library()
+    dt = torch.float16 if half else torch.float32
+    g = torch.Generator().manual_seed(seed)
+    x = torch.randn((n, c + 3, h, w), generator=g).to(dt).cuda()   # strided view: 3 extra planes
+    wt = torch.randn((c, 1, 3, 3), generator=g).cuda()
+    b = torch.randn((c,), generator=g).cuda()
+    xv = x[:, 2:2 + c]
+    yf = torch.full((n, n_first + 1, h, w), 7.0, dtype=dt, device="cuda")
+    yr = torch.empty((n, c - n_first, h, w), dtype=dt, device="cuda")
+    ps = torch.zeros((n, n_first + 2), dtype=torch.float32, device="cuda")
+    _lib.check(lib.yta_osnet_dw3x3(
+        ctypes.c_void_p(xv.data_ptr()), (c + 3) * h * w, h * w,
+        ctypes.c_void_p(wt.data_ptr()), ctypes.c_void_p(b.data_ptr()), n, c, h, w, int(half),
+        ctypes.c_void_p(yf.data_ptr()), (n_first + 1) * h * w, n_first,
+        ctypes.c_void_p(yr.data_ptr()) if c > n_first else None, (c - n_first) * h * w,
+        ctypes.c_void_p(ps.data_ptr()), n_first + 2, None))
+    torch.cuda.synchronize()
+    ref = torch.relu(torch.nn.functional.conv2d(xv.float(), wt, b, padding=1, groups=c))
+    tol = 2e-3 if half else 1e-5
+    scale = ref.abs().max().item()
+    def err(a, b):
+        return (a.float() - b).abs().max().item() if a.numel() else 0.0
+    assert err(yf[:, :n_first], ref[:, :n_first]) <= tol * scale
+    assert err(yr, ref[:, n_first:]) <= tol * scale
+    assert (yf[:, n_first] == 7.0).all()                    # plane past n_first untouched
+    s = yf[:, :n_first].float().sum(dim=(2, 3))              # sums of the stored values
+    assert torch.allclose(ps[:, :n_first], s, rtol=1e-5, atol=1e-3)
+    assert (ps[:, n_first:] == 0).all()
+
+
+@pytest.mark.parametrize("half", [False, True])
+@pytest.mark.parametrize("shape", [(2, 12, 64, 32, 4), (3, 20, 16, 8, 5), (1, 6, 5, 3, 6),
+                                   (2, 9, 1, 1, 3), (1, 4, 33, 17, 0)])
+def test_dw3x3_kernel(shape, half):
+    n, c, h, w, nf = shape
+    _dw_case(n, c, h, w, nf, half, seed=sum(shape))
+
+
+@pytest.mark.parametrize("half", [False, True])
+def test_gate_sum_kernel(half):
+    import ctypes
+    from yolo_tracking_amd import _lib
+    lib = _lib.load_library()
+    dt = torch.float16 if half else torch.float32
+    g = torch.Generator().manual_seed(5)
+    n, c, p = 3, 24, 16 * 8 + 5
+    st = torch.randn((n, 4, c, p), generator=g).to(dt).cuda()
+    gate = torch.rand((n, 4, c), generator=g).to(dt).cuda()
+    out = torch.empty((n, c, p), dtype=dt, device="cuda")
+    _lib.check(lib.yta_osnet_gate_sum(ctypes.c_void_p(st.data_ptr()),
+                                      ctypes.c_void_p(gate.data_ptr()), n, c, p, int(half),
+                                      ctypes.c_void_p(out.data_ptr()), None))
+    torch.cuda.synchronize()
+    ref = (st.float() * gate.float()[..., None]).sum(1)
+    tol = 2e-3 if half else 1e-6
+    assert (out.float() - ref).abs().max().item() <= tol * ref.abs().max().item()
+
+
+def test_block_kernels_match_torch_graph(golden):
+    """The same network with hip=False (PyTorch's depthwise/pool/sum) agrees with the HIP path."""
+    sd, x, _ = golden
+    xt = torch.from_numpy(x).cuda()
+    a = OSNetReID("osnet_x0_25", sd, device="cuda:0")(xt)
+    b = OSNetReID("osnet_x0_25", sd, device="cuda:0", hip=False)(xt)
+    assert (a - b).abs().max().item() <= 1e-5 * b.abs().max().item()

@@ -71,3 +71,29 @@ def test_global_normalize():
     g = orr.global_normalize(f)
     assert g.dtype == np.float32
     assert abs(float(np.sqrt((g.astype(np.float64) ** 2).sum())) - 1) < 1e-6
+
+
+def test_osnet_graph_matches_reference_module():
+    """appearance/osnet.py (folded BatchNorms, batched branches) against the reference's OSNet
+    x0.25 module in eval mode (tests/golden/osnet_x0_25.npz, random weights + BN statistics),
+    float32 on the CPU."""
+    import os
+    import torch
+    from yolo_tracking_amd.appearance.osnet import OSNetReID
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "osnet_x0_25.npz"))
+    sd = {k[4:]: g[k] for k in g.files if k.startswith("sd__")}
+    x = np.random.default_rng(int(g["input_seed"])).standard_normal((4, 3, 256, 128))
+    y = OSNetReID("osnet_x0_25", sd, device="cpu")(torch.from_numpy(x.astype(np.float32)))
+    ref = g["features"]
+    assert np.abs(y.numpy() - ref).max() <= 1e-5 * np.abs(ref).max()
+
+
+def test_osnet_names_and_random_init():
+    import torch
+    from yolo_tracking_amd.appearance.osnet import OSNetReID, model_name, random_state_dict
+    assert model_name("weights/osnet_x0_25_msmt17.pt") == "osnet_x0_25"
+    assert model_name("osnet_x1_0_market1501.pt") == "osnet_x1_0"
+    assert model_name("resnet50_msmt17.pt") is None
+    for name in ("osnet_x0_5", "osnet_x1_0"):
+        y = OSNetReID(name, random_state_dict(name), device="cpu")(torch.zeros(2, 3, 256, 128))
+        assert y.shape == (2, 512) and torch.isfinite(y).all()

@@ -169,6 +169,10 @@ _SIGS = {
     "yta_sof_kat_corners": ([_I, _P, _P, _I, _I, _P, _P], _I),
     "yta_sof_kat_lk": ([_I, _P, _P, _I, _I, _P, _I, _P, _P], _I),
     "yta_sof_kat_affine": ([_I, _P, _P, _I, _P, _P], _I),
+    "yta_osnet_dw3x3": ([_P, ctypes.c_longlong, ctypes.c_longlong, _P, _P, _I, _I, _I, _I, _I, _P,
+                         ctypes.c_longlong, _I, _P, ctypes.c_longlong, _P, ctypes.c_longlong, _P],
+                        _I),
+    "yta_osnet_gate_sum": ([_P, _P, _I, _I, _I, _I, _P, _P], _I),
 }
 
 EXPORTED_SYMBOLS = tuple(_SIGS)

@@ -7,11 +7,17 @@ runs the ReID network (`forward`, :226-299) and divides the features by one glob
 writes every crop of every camera stream in one launch, straight into the NCHW tensor the network
 reads; `yta_reid_normalize_device` does the global normalisation before the single copy back.
 
-The network itself is the caller's: pass `model=` (a torch module on the device taking
-(N, 3, 256, 128)); loading the reference's weight files / export formats (:74-178) is outside this
-build (no weights ship with the reference).  Torch is used for device memory and
-streams only; there is no CPU fallback (a missing library raises YTAError).
+The network: OSNet (appearance/osnet.py, an eval-mode inference graph with folded BatchNorms,
+channels-last, batched branches) built from `weights` as the reference builds it from the weight
+file name (reid_multibackend.py:57-80, osnet_x0_25 .. osnet_x1_0); the reference's .pt state dicts
+load unchanged (torch.load(weights_only=True)).  A weight file that is not on disk would be
+downloaded by the reference (gdown, :61-64); there is no network here, so the network then runs
+with freshly initialised weights and a warning says so.  `model=` (any torch module on the device
+taking (N, 3, 256, 128)) replaces the network; the ONNX / OpenVINO / TensorRT / TFLite export
+backends (:82-178) are not rebuilt.  There is no CPU fallback (a missing library raises YTAError).
 """
+import warnings
+from pathlib import Path
 import ctypes
 
 import numpy as np
@@ -74,16 +80,36 @@ class ReIDDetectMultiBackend:
     """reid_multibackend.py:59 ReIDDetectMultiBackend(weights, device, fp16) with a
     caller-supplied network (`model`, a torch module on `device`)."""
 
-    def __init__(self, weights=None, device=0, fp16=False, model=None):
+    def __init__(self, weights="osnet_x0_25_msmt17.pt", device=0, fp16=False, model=None):
         import torch
         self.torch = torch
         self.weights = weights
         idx = _lib.parse_device(device)
         self.device = torch.device("cuda", idx)
         self.fp16 = bool(fp16)
-        self.model = model
         self.nhwc = False
         self.lib = _lib.load_library()
+        if model is None and weights is not None:
+            model = self._build_osnet(weights)
+        self.model = model
+
+    def _build_osnet(self, weights):
+        """reid_multibackend.py:57-80 for the OSNet family (the trackers' default weights)."""
+        from .osnet import OSNetReID, load_checkpoint, model_name
+        name = model_name(weights)
+        if name is None:
+            raise NotImplementedError(
+                f"ReID weights {str(weights)!r}: only the OSNet family (osnet_x0_25 .. osnet_x1_0) "
+                "is rebuilt on the MI355X path; pass model=<torch module> for other networks")
+        w = Path(weights)
+        if w.is_file():
+            sd = load_checkpoint(w)
+        else:
+            warnings.warn(f"ReID weights {str(w)!r} not on disk and no network to download them "
+                          f"(reid_multibackend.py:61-64): {name} runs with fresh random weights",
+                          RuntimeWarning, stacklevel=3)
+            sd = None
+        return OSNetReID(name, sd, device=self.device, half=self.fp16)
 
     def _stream(self):
         return ctypes.c_void_p(self.torch.cuda.current_stream(self.device).cuda_stream)
@@ -129,10 +155,10 @@ class ReIDDetectMultiBackend:
         return self.preprocess_batch([(xyxys, img)])
 
     def forward(self, im_batch):
-        """:226-299 for the `pt` backend: the caller's module on the batch -> NumPy."""
+        """:226-299 for the `pt` backend: the network on the batch -> NumPy."""
         if self.model is None:
-            raise RuntimeError("ReIDDetectMultiBackend: no network (pass model=<torch module>); "
-                               "loading the reference's weight files is outside this build")
+            raise RuntimeError("ReIDDetectMultiBackend(weights=None): no network (pass weights "
+                               "naming an OSNet variant or model=<torch module>)")
         if self.fp16 and im_batch.dtype != self.torch.float16:
             im_batch = im_batch.half()
         if self.nhwc:

@@ -18,6 +18,7 @@ import ctypes
 import numpy as np
 
 from .. import _lib
+from ..appearance import build_reid
 from ..motion.cmc import IdentityCMC, default_cmc
 from .bytetrack import ByteTrackEngine, STrackView
 
@@ -168,7 +169,7 @@ class BoTSORT:
         self.fuse_first_associate = fuse_first_associate
         self.model_weights = model_weights
         if with_reid:
-            self.model = reid
+            self.model = build_reid(reid, model_weights, device, fp16)
         self.cmc = cmc if cmc is not None else default_cmc("BoTSORT", device)   # :228
         self._kw = dict(track_high_thresh=track_high_thresh, track_low_thresh=track_low_thresh,
                         new_track_thresh=new_track_thresh, track_buffer=track_buffer,

@@ -18,6 +18,7 @@ import ctypes
 import numpy as np
 
 from .. import _lib
+from ..appearance import build_reid
 from ..motion.cmc import default_cmc
 
 
@@ -193,7 +194,7 @@ class DeepOCSort:
         self.aw_off = aw_off
         self.new_kf_off = new_kf_off
         KalmanBoxTracker.count = 1                                   # :347
-        self.model = reid
+        self.model = build_reid(reid, model_weights, device, fp16) if not embedding_off else reid
         self.cmc = cmc if cmc is not None or cmc_off else default_cmc("DeepOCSort", device)
         self._kw = dict(det_thresh=det_thresh, max_age=max_age, min_hits=min_hits,
                         iou_threshold=iou_threshold, delta_t=delta_t, asso_func=asso_func,

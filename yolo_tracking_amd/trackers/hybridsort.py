@@ -20,6 +20,7 @@ import ctypes
 import numpy as np
 
 from .. import _lib
+from ..appearance import build_reid
 
 
 class KalmanBoxTracker:
@@ -177,7 +178,7 @@ class HybridSORT:
         self.inertia = inertia
         self.use_byte = use_byte
         KalmanBoxTracker.count = 0                                   # :361
-        self.model = reid
+        self.model = build_reid(reid, reid_weights, device, half)
         self._kw = dict(det_thresh=det_thresh, max_age=max_age, min_hits=min_hits,
                         iou_threshold=iou_threshold, delta_t=delta_t, asso_func=asso_func,
                         inertia=inertia, device=device)
