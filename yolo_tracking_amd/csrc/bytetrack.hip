@@ -358,6 +358,450 @@ __global__ __launch_bounds__(BLK23) void k_stage23(BtArgs a) {
     if (!stage23_body<V>(a, s, ag, sh) && threadIdx.x == 0) atomicOr(&a.cnt[s].err, ERR_EDGE_OVERFLOW);
 }
 
+// ------------------------------------------------------------------ ByteTrack stage 1, split
+// k_stage1's work for ByteTrack (match_thresh <= 1) as three launches that keep several streams
+// on every CU (the fused kernel holds one 1024-thread stream per CU, its 150 KiB arena, for the
+// whole latency chain of the frame).  Under load a dependent HBM round trip costs microseconds,
+// so every pass issues all of a thread's loads before using any, and hand-offs that go through
+// LDS only do not drain global stores (lds_sync):
+//   k_s1_prep  [block/stream, 256 thr, 32 KiB static LDS] detection pass and confidence split
+//              (:149-158), tracked -> activated / unconfirmed, pool = act ++ lost with predicted
+//              boxes (:169-178, multi_predict's mean :35-48); coalesced loads, items staged in
+//              LDS per pass (holding a run of items per thread in registers measured 1.6x slower:
+//              strided rows, uncoalesced stores)
+//   k_s1_edges [block/stream, 512 thr, <= 58 KiB LDS] grid over the high detections built in
+//              LDS from two register-held detections per thread, then every pool row's candidate
+//              edges, fused IoU cost (:181-183, matching.py:117, :216-220) below match_thresh:
+//              count + the first E_SLOTS edges to HBM (the grid goes to HBM too when some row
+//              has more)
+//   k_s1_lap   [block/stream, 256 thr] CSR of the edges in LDS (rows with more edges query the
+//              grid in HBM), lap_block with cost_limit = match_thresh (:184-186) on LDS, the
+//              assignment written out; a frame that does not fit the LDS arena is redone over
+//              global memory
+// Same results as k_stage1: edges are exactly the pairs with cost < match_thresh whatever the
+// grid's cell order, and lap_block's result does not depend on the order of a row's edges.
+constexpr int PREP_T = 256;          // k_s1_prep threads
+constexpr int PREP_CH = 768;         // items staged in LDS per pass of k_s1_prep
+#ifndef YTA_BLKE
+#define YTA_BLKE 512
+#endif
+constexpr int BLKE = YTA_BLKE;       // k_s1_edges threads
+#ifndef YTA_BLKL
+#define YTA_BLKL 256
+#endif
+constexpr int BLKL = YTA_BLKL;       // k_s1_lap threads
+
+struct PrepShared {
+    union {
+        struct {
+            Box box[PREP_CH];
+            double conf[PREP_CH];
+            unsigned char cat[PREP_CH];
+        } d;                          // detections of the current pass
+        struct {
+            Box box[PREP_CH];
+            int slot[PREP_CH];
+            unsigned char cat[PREP_CH];
+        } t;                          // tracked tracks of the current pass
+    } u;
+    int wsum[32];
+};
+
+struct DetRow {
+    double v[6];
+};
+struct TrkRec {
+    int slot, flags;
+    double m[8];
+};
+
+// STrack.xyxy of multi_predict's mean (zeroed vh unless Tracked), byte_tracker.py:35-48, :100-111
+__device__ __forceinline__ Box bt_pred_box(const TrkRec &r) {
+    const double vh = st_of(r.flags) == ST_TRACKED ? r.m[7] : 0.0;
+    return xyah_mean_to_box(r.m[0] + r.m[4], r.m[1] + r.m[5], r.m[2] + r.m[6], r.m[3] + vh);
+}
+__device__ __forceinline__ TrkRec bt_trk_rec(const BtArgs &a, long long tb, int slot) {
+    TrkRec r;
+    r.slot = slot;
+    r.flags = a.flags[tb + slot];
+    const double2 *m = reinterpret_cast<const double2 *>(a.kf + (tb + slot) * KF_REC);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const double2 q = m[k];
+        r.m[2 * k] = q.x;
+        r.m[2 * k + 1] = q.y;
+    }
+    return r;
+}
+
+__global__ __launch_bounds__(PREP_T) void k_s1_prep(BtArgs a) {
+    __shared__ PrepShared sh;
+    const int s = blockIdx.x, t = threadIdx.x;
+    YTA_STAMP_BASE(60);
+    YTA_STAMP(0);
+    BtCounters *c = a.cnt + s;
+    const long long db = (long long)s * a.MAXD, tb = (long long)s * a.CAP;
+    int nd = a.det_off[s + 1] - a.det_off[s];
+    if (nd > a.MAXD || nd < 0) {
+        if (t == 0) atomicOr(&c->err, ERR_DET_CAPACITY);
+        nd = nd < 0 ? 0 : a.MAXD;
+    }
+    const double *din = a.det_in + (long long)a.det_off[s] * 6;
+    const double thr = a.track_thresh;
+    // detections, PREP_CH per pass (coalesced loads, 3 rows in flight per thread): STrack
+    // conversions (:16-18), measurement, confidence split (:149-158), boxes staged in LDS, then
+    // the order-preserving high / second lists
+    int n_high = 0, n_second = 0;
+    for (int c0 = 0; c0 < nd; c0 += PREP_CH) {
+        const int m = nd - c0 < PREP_CH ? nd - c0 : PREP_CH;
+        batched_for<3>(
+            m,
+            [&](int i) {
+                DetRow r;
+                const double *d = din + (long long)(c0 + i) * 6;
+#pragma unroll
+                for (int k = 0; k < 6; ++k) r.v[k] = d[k];
+                return r;
+            },
+            [&](int i, const DetRow &r) {
+                const long long q = db + c0 + i;
+                double xywh[4];
+                det_xyxy_to_xywh(r.v, xywh);
+                xywh_to_xyah(xywh, a.det_xyah + q * 4);
+                const double conf = r.v[4];
+                a.det_conf[q] = conf;
+                a.det_cls[q] = r.v[5];
+                sh.u.d.cat[i] = conf > thr ? 1 : (conf > a.low_thresh && conf < thr ? 2 : 0);
+                sh.u.d.box[i] = xywh_to_box(xywh);
+                sh.u.d.conf[i] = conf;
+            });
+        lds_sync();
+        const int2 hs = block_compact2<false>(
+            m, sh.wsum, [&](int i) { return (int)sh.u.d.cat[i]; },
+            [&](int i, int cat, int pos) {
+                if (cat == 1) {
+                    const long long p = db + n_high + pos;
+                    a.high[p] = c0 + i;
+                    a.high_box[p] = sh.u.d.box[i];
+                    a.high_score[p] = sh.u.d.conf[i];
+                } else {
+                    const long long p = db + n_second + pos;
+                    a.second[p] = c0 + i;
+                    a.second_box[p] = sh.u.d.box[i];
+                }
+            });
+        n_high += hs.x;
+        n_second += hs.y;
+        lds_sync();   // the staging area is reused
+    }
+    YTA_STAMP(1);
+    // tracked -> activated (pool head, predicted box) / unconfirmed (current box) (:169-178)
+    const int n_tracked = c->n_tracked, n_lost = c->n_lost;
+    int n_act = 0, n_unc = 0;
+    for (int c0 = 0; c0 < n_tracked; c0 += PREP_CH) {
+        const int m = n_tracked - c0 < PREP_CH ? n_tracked - c0 : PREP_CH;
+        batched_for<3>(
+            m, [&](int i) { return bt_trk_rec(a, tb, a.tracked[tb + c0 + i]); },
+            [&](int i, const TrkRec &r) {
+                const bool act = (r.flags & FL_ACTIVATED) != 0;
+                sh.u.t.cat[i] = act ? 1 : 2;
+                sh.u.t.slot[i] = r.slot;
+                sh.u.t.box[i] = act ? bt_pred_box(r) : xyah_mean_to_box(r.m[0], r.m[1], r.m[2], r.m[3]);
+            });
+        lds_sync();
+        const int2 au = block_compact2<false>(
+            m, sh.wsum, [&](int i) { return (int)sh.u.t.cat[i]; },
+            [&](int i, int cat, int pos) {
+                if (cat == 1) {
+                    const long long p = tb + n_act + pos;
+                    a.pool[p] = sh.u.t.slot[i];
+                    a.pool_box[p] = sh.u.t.box[i];
+                } else {
+                    const long long p = tb + n_unc + pos;
+                    a.unc[p] = sh.u.t.slot[i];
+                    a.unc_box[p] = sh.u.t.box[i];
+                }
+            });
+        n_act += au.x;
+        n_unc += au.y;
+        lds_sync();
+    }
+    YTA_STAMP(2);
+    // pool tail: the lost tracks, predicted
+    batched_for<3>(
+        n_lost, [&](int i) { return bt_trk_rec(a, tb, a.lost[tb + i]); },
+        [&](int i, const TrkRec &r) {
+            a.pool[tb + n_act + i] = r.slot;
+            a.pool_box[tb + n_act + i] = bt_pred_box(r);
+        });
+    if (t == 0) {
+        c->frame_id += 1;
+        c->n_dets = nd;
+        c->n_high = n_high;
+        c->n_second = n_second;
+        c->n_act = n_act;
+        c->n_unc = n_unc;
+        c->n_pool = n_act + n_lost;
+        c->n_left = 0;
+        c->n_rest = 0;
+        c->n_births = 0;
+    }
+    YTA_STAMP(3);
+}
+
+// Every candidate edge of pool row box rb: f(high position, fused IoU cost) for cost <
+// match_thresh.  gv: the stream's grid over its high detections (LDS or HBM); big items' boxes
+// come from the high lists.
+template <typename F>
+__device__ __forceinline__ void s1_row_edges(const BtArgs &a, int s, const GridView &gv,
+                                             const GridHdr &h, const Box &rb, F f) {
+    const long long db = (long long)s * a.MAXD;
+    const double thresh = a.match_thresh;
+    auto scored = [&](int j, const Box &cb, double w) {
+        const double dist = 1 - iou(rb, cb);                              // matching.py:117
+        const double cost = 1 - (1 - dist) * w;                           // matching.py:216-220
+        if (cost < thresh) f(j, cost);
+    };
+    grid_query(gv, h, rb, scored, [&](int j) {
+        const Box cb = a.high_box[db + j];
+        if (intersects(rb, cb)) scored(j, cb, a.high_score[db + j]);
+    });
+}
+
+__device__ __forceinline__ GridView s1_grid_hbm(const BtArgs &a, int s) {
+    const long long db = (long long)s * a.MAXD;
+    return GridView{a.g_hdr + s, a.g_cell + (long long)s * (GRID_MAX_CELLS + 1), a.g_ids + db,
+                    a.g_boxes + db, a.g_w + db, a.g_big + db};
+}
+
+// LDS bytes of a grid over C detections in k_s1_edges.
+__host__ __device__ inline long long s1_grid_bytes(long long C) {
+    return 4 * (GRID_MAX_CELLS + 1) + C * (4 + 32 + 8 + 4) + 5 * 16;
+}
+
+// k_s1_edges body over a grid whose storage (LDS or HBM) the caller fixed: inlined once per
+// storage so that every grid access compiles to ds_* or global_* instructions, not flat ones.
+template <typename HBox, typename HW>
+__device__ __forceinline__ void s1_edges_body(const BtArgs &a, int s, int nc, int nr,
+                                              const GridView &gv, HBox hbox, HW hw,
+                                              GridScratch &gs, int *wsum, int &spill) {
+    const int t = threadIdx.x, nt = blockDim.x;
+    const long long tb = (long long)s * a.CAP, SC = (long long)a.S * a.CAP;
+    grid_build(nc, hbox, hw, gv, gs, wsum);
+    const GridHdr h = gs.hdr;
+    YTA_STAMP(1);
+    // pool rows, four per thread in flight
+    for (int base = t; base < nr; base += 4 * nt) {
+        Box rb[4];
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+            if (base + b * nt < nr) rb[b] = a.pool_box[tb + base + b * nt];
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const int i = base + b * nt;
+            if (i >= nr) continue;
+            int n = 0;
+            s1_row_edges(a, s, gv, h, rb[b], [&](int j, double cost) {
+                if (n < E_SLOTS) {
+                    a.e_col[n * SC + tb + i] = j;
+                    a.e_cost[n * SC + tb + i] = cost;
+                }
+                ++n;
+            });
+            a.e_cnt[tb + i] = n;
+            if (n > E_SLOTS) spill = 1;
+        }
+    }
+}
+
+__global__ __launch_bounds__(BLKE) void k_s1_edges(BtArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    __shared__ GridScratch gs;
+    __shared__ int wsum[32];
+    __shared__ int spill;
+    const int s = blockIdx.x, t = threadIdx.x, nt = blockDim.x;
+    YTA_STAMP_BASE(66);
+    YTA_STAMP(0);
+    const BtCounters *c = a.cnt + s;
+    const long long db = (long long)s * a.MAXD;
+    const int nc = c->n_high, nr = c->n_pool;
+    // this thread's detections t and t + blockDim held in registers (nc <= 2 blockDim: every box
+    // load in flight at once; the grid build reads them three times)
+    Box hb0{0.0, 0.0, 0.0, 0.0}, hb1{0.0, 0.0, 0.0, 0.0};
+    double hw0 = 0.0, hw1 = 0.0;
+    if (t < nc) {
+        hb0 = a.high_box[db + t];
+        hw0 = a.high_score[db + t];
+    }
+    if (t + nt < nc) {
+        hb1 = a.high_box[db + t + nt];
+        hw1 = a.high_score[db + t + nt];
+    }
+    if (t == 0) spill = 0;
+    if (nc > 2 * nt || s1_grid_bytes(nc) > (long long)a.lds_bytes_e) {   // grid built in HBM
+        s1_edges_body(
+            a, s, nc, nr, s1_grid_hbm(a, s), [&](int j) { return a.high_box[db + j]; },
+            [&](int j) { return a.high_score[db + j]; }, gs, wsum, spill);
+        return;
+    }
+    // grid_build visits item j only from thread j mod blockDim: a register select, no memory
+    auto hbox = [&](int j) { return j == t ? hb0 : hb1; };
+    auto hw = [&](int j) { return j == t ? hw0 : hw1; };
+    Arena ar(smem, a.lds_bytes_e);
+    GridView gv;
+    gv.hdr = nullptr;
+    gv.cell_start = ar.alloc<int>(grid_cells_for(nc) + 1);
+    gv.ids = ar.alloc<int>(nc);
+    gv.boxes = ar.alloc<Box>(nc);
+    gv.w = ar.alloc<double>(nc);
+    gv.big = ar.alloc<int>(nc);
+    s1_edges_body(a, s, nc, nr, gv, hbox, hw, gs, wsum, spill);
+    lds_sync();
+    YTA_STAMP(2);
+    if (!spill) return;
+    // some row has more edges than slots: k_s1_lap queries the grid again, from HBM
+    const GridHdr h = gs.hdr;
+    const GridView gg = s1_grid_hbm(a, s);
+    const int ncell = h.gx * h.gy;
+    if (t == 0) *gg.hdr = h;
+    for (int q = t; q <= ncell; q += nt) gg.cell_start[q] = gv.cell_start[q];
+    for (int q = t; q < h.n_binned; q += nt) {
+        gg.ids[q] = gv.ids[q];
+        gg.boxes[q] = gv.boxes[q];
+        gg.w[q] = gv.w[q];
+    }
+    for (int q = t; q < h.n_big; q += nt) gg.big[q] = gv.big[q];
+}
+
+// Arena bytes that always suffice for s1_lap_body (the global fallback arena's size).
+__host__ __device__ inline long long s1_lap_arena_bytes(long long R, long long C, long long E) {
+    return 4 * (R + C) + 4 * (R + 1) + 4 * C + 12 * E + 4 * (R + C) * 3 + 4 * 6 * (R + C + 1) +
+           16 * 16 + 256;
+}
+
+__device__ __forceinline__ bool s1_lap_body(const BtArgs &a, int s, Arena &ar, LapShared &lsh) {
+    const int t = threadIdx.x, nt = blockDim.x;
+    BtCounters *c = a.cnt + s;
+    const long long db = (long long)s * a.MAXD, tb = (long long)s * a.CAP;
+    const long long SC = (long long)a.S * a.CAP;
+    const int nr = c->n_pool, nc = c->n_high;
+    YTA_STAMP_BASE(90);
+    YTA_STAMP(0);
+    int *X = ar.alloc<int>(nr);
+    int *Y = ar.alloc<int>(nc);
+    int *row_off = ar.alloc_top<int>(nr + 1);
+    int *col_deg = ar.alloc_top<int>(nc);
+    if (ar.fail) return false;
+    for (int j = t; j < nc; j += nt) col_deg[j] = 0;
+    // row offsets: every thread owns a contiguous run of <= 8 rows (loads in flight together)
+    int run = 0;
+    for (int base = 0; base < nr; base += 8 * nt) {
+        const int m = nr - base < 8 * nt ? nr - base : 8 * nt;
+        const int per = (m + nt - 1) / nt;
+        const int lo = base + t * per;
+        const int hi = lo + per < base + m ? lo + per : base + m;
+        int cnt[8], mine = 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            cnt[k] = lo + k < hi ? a.e_cnt[tb + lo + k] : 0;
+            mine += cnt[k];
+        }
+        int tot;
+        int pos = run + block_exclusive_scan<false>(mine, lsh.wsum, &tot);
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+            if (lo + k < hi) {
+                row_off[lo + k] = pos;
+                pos += cnt[k];
+            }
+        run += tot;
+    }
+    const int E = run;
+    if (t == 0) row_off[nr] = E;
+    int *csr_col = ar.alloc_top<int>(E);
+    double *csr_cost = ar.alloc_top<double>(E);
+    if (ar.fail) return false;
+    lds_sync();
+    YTA_STAMP(1);
+    // CSR fill from the edge slots (same row ownership, every slot load of a thread in flight);
+    // a row with more edges than slots queries the stream's grid in HBM again
+    if (E > 0) {
+        const GridView gg = s1_grid_hbm(a, s);
+        for (int base = 0; base < nr; base += 8 * nt) {
+            const int m = nr - base < 8 * nt ? nr - base : 8 * nt;
+            const int per = (m + nt - 1) / nt;
+            const int lo = base + t * per;
+            const int hi = lo + per < base + m ? lo + per : base + m;
+#pragma unroll
+          for (int half = 0; half < 8; half += 4) {   // four rows' slot loads in flight
+            int col[4][E_SLOTS];
+            double cost[4][E_SLOTS];
+            int n[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int i = lo + half + k;
+                n[k] = i < hi ? row_off[i + 1] - row_off[i] : 0;
+#pragma unroll
+                for (int q = 0; q < E_SLOTS; ++q)
+                    if (q < n[k]) {
+                        col[k][q] = a.e_col[q * SC + tb + i];
+                        cost[k][q] = a.e_cost[q * SC + tb + i];
+                    }
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                if (n[k] == 0) continue;
+                const int i = lo + half + k;
+                int e = row_off[i];
+                if (n[k] <= E_SLOTS) {
+#pragma unroll
+                    for (int q = 0; q < E_SLOTS; ++q)
+                        if (q < n[k]) {
+                            csr_col[e + q] = col[k][q];
+                            csr_cost[e + q] = cost[k][q];
+                            atomicAdd(&col_deg[col[k][q]], 1);
+                        }
+                } else {
+                    const int eend = row_off[i + 1];
+                    s1_row_edges(a, s, gg, *gg.hdr, a.pool_box[tb + i], [&](int j, double cj) {
+                        if (e >= eend) return;
+                        csr_col[e] = j;
+                        csr_cost[e] = cj;
+                        ++e;
+                        atomicAdd(&col_deg[j], 1);
+                    });
+                }
+            }
+          }
+        }
+    }
+    block_sync();
+    YTA_STAMP(2);
+    if (!lap_block(nr, nc, row_off, csr_col, csr_cost, col_deg, a.match_thresh, X, Y, &c->err, ar,
+                   slab_of(a, s), lsh))
+        return false;
+    YTA_STAMP(3);
+    for (int i = t; i < nr; i += nt) a.x1[tb + i] = X[i];
+    for (int j = t; j < nc; j += nt) a.y1[db + j] = Y[j];
+    if (t == 0) c->n_edges[0] = E;
+    YTA_STAMP(4);
+    return true;
+}
+
+__global__ __launch_bounds__(BLKL) void k_s1_lap(BtArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    __shared__ LapShared lsh;
+    const int s = blockIdx.x;
+    {
+        Arena ar(smem, a.lds_bytes_l);
+        if (s1_lap_body(a, s, ar, lsh)) return;
+    }
+    block_sync();
+    if (threadIdx.x == 0) a.cnt[s].n_fallback[0] += 1;
+    Arena ag(a.ws + s * a.ws_stride, a.ws_stride);
+    if (!s1_lap_body(a, s, ag, lsh) && threadIdx.x == 0) atomicOr(&a.cnt[s].err, ERR_EDGE_OVERFLOW);
+}
+
 // ------------------------------------------------------------------------------------ k_apply
 // BoT-SORT STrack.update_cls (bot_sort.py:50-67): per-class summed scores, the first strict
 // maximum wins; a class not seen before is appended and taken as is.
@@ -1014,6 +1458,14 @@ constexpr int BT_PHASES = 4;   // launches per frame, see yta_bytetrack_profile_
 constexpr size_t BT_LDS_BYTES = YTA_LDS1_KB * 1024;   // k_stage1 arena (one 1024-thread block per CU)
 constexpr size_t BT_LDS23_BYTES = 32 * 1024;  // k_stage23 arena (several blocks per CU)
 constexpr size_t BT_LDSF_BYTES = 20 * 1024;   // k_finish dedup arena (several blocks per CU)
+#ifndef YTA_LDSL_KB
+#define YTA_LDSL_KB 76
+#endif
+constexpr size_t BT_LDSL_BYTES = YTA_LDSL_KB * 1024;   // k_s1_lap arena (two blocks per CU)
+#ifndef YTA_LDSE_KB
+#define YTA_LDSE_KB 58
+#endif
+constexpr size_t BT_LDSE_BYTES = YTA_LDSE_KB * 1024;   // k_s1_edges grid (1024 high detections)
 
 // Host-buffer ABI staging: copies between the caller's (pageable) buffers and the pinned staging
 // buffers, split over up to 8 host threads, and chunked so that each chunk's DMA overlaps the next
@@ -1147,7 +1599,21 @@ int bt_alloc(yta_bytetrack *e) {
     a.lds_bytes = BT_LDS_BYTES;
     a.lds_bytes23 = BT_LDS23_BYTES;
     a.lds_bytes_f = BT_LDSF_BYTES;
+    a.lds_bytes_l = BT_LDSL_BYTES;
+    a.lds_bytes_e = BT_LDSE_BYTES;
     a.ws_stride = assoc_arena_bytes(CAP, MAXD, CAP * MAXD);
+    if (e->variant == VAR_BYTETRACK) {   // stage 1 as k_s1_prep / k_s1_edges / k_s1_lap
+        a.ws_stride = std::max(a.ws_stride, s1_lap_arena_bytes(CAP, MAXD, CAP * MAXD));
+        DALLOC(a.g_cell, S * (GRID_MAX_CELLS + 1));
+        DALLOC(a.g_ids, S * MAXD);
+        DALLOC(a.g_big, S * MAXD);
+        DALLOC(a.g_boxes, S * MAXD);
+        DALLOC(a.g_w, S * MAXD);
+        DALLOC(a.g_hdr, S);
+        DALLOC(a.e_cnt, S * CAP);
+        DALLOC(a.e_col, E_SLOTS * S * CAP);
+        DALLOC(a.e_cost, E_SLOTS * S * CAP);
+    }
     if (e->variant == VAR_BOTSORT && e->D > 0)
         a.ws_stride = std::max(a.ws_stride, assoc_emb_arena_bytes(CAP, MAXD));
     a.ws_stride = (a.ws_stride + 255) & ~255LL;
@@ -1185,7 +1651,8 @@ int set_lds_limits(size_t bytes) {
     const int b = (int)bytes;
     for (const void *k : {(const void *)k_stage1<VAR_BYTETRACK>, (const void *)k_stage1<VAR_BOTSORT>,
                           (const void *)k_stage23<VAR_BYTETRACK>,
-                          (const void *)k_stage23<VAR_BOTSORT>})
+                          (const void *)k_stage23<VAR_BOTSORT>, (const void *)k_s1_lap,
+                          (const void *)k_s1_edges})
         YTA_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, b));
     return YTA_OK;
 }
@@ -1203,7 +1670,15 @@ int launch_frame(yta_bytetrack *e) {
         hipLaunchKernelGGL(k_feat, gf, dim3(FEAT_T), 0, e->stream, a);
         YTA_HIP(hipGetLastError());
     }
-    hipLaunchKernelGGL(k_stage1<V>, dim3(a.S), dim3(BLK1), a.lds_bytes, e->stream, a);
+    if (V == VAR_BYTETRACK && a.match_thresh <= 1.0) {   // grid-exact candidates (assoc.hpp)
+        hipLaunchKernelGGL(k_s1_prep, dim3(a.S), dim3(PREP_T), 0, e->stream, a);
+        YTA_HIP(hipGetLastError());
+        hipLaunchKernelGGL(k_s1_edges, dim3(a.S), dim3(BLKE), a.lds_bytes_e, e->stream, a);
+        YTA_HIP(hipGetLastError());
+        hipLaunchKernelGGL(k_s1_lap, dim3(a.S), dim3(BLKL), a.lds_bytes_l, e->stream, a);
+    } else {
+        hipLaunchKernelGGL(k_stage1<V>, dim3(a.S), dim3(BLK1), a.lds_bytes, e->stream, a);
+    }
     YTA_HIP(hipGetLastError());
     MARK();
     hipLaunchKernelGGL(k_stage23<V>, dim3(a.S), dim3(BLK23), a.lds_bytes23, e->stream, a);
@@ -1318,6 +1793,8 @@ int reserve(yta_bytetrack *e, int cap, int maxd) {
     n->a.lds_bytes = e->a.lds_bytes;
     n->a.lds_bytes23 = e->a.lds_bytes23;
     n->a.lds_bytes_f = e->a.lds_bytes_f;
+    n->a.lds_bytes_l = e->a.lds_bytes_l;
+    n->a.lds_bytes_e = e->a.lds_bytes_e;
     e->a = n->a;
     e->d_warp = n->d_warp;
     e->d_warp_id = n->d_warp_id;
@@ -1763,6 +2240,8 @@ int yta_bytetrack_set_lds(yta_bytetrack *e, int bytes) {
     e->a.lds_bytes = (size_t)bytes & ~(size_t)15;
     e->a.lds_bytes23 = std::min(e->a.lds_bytes, BT_LDS23_BYTES);
     e->a.lds_bytes_f = std::min(e->a.lds_bytes, BT_LDSF_BYTES);
+    e->a.lds_bytes_l = std::min(e->a.lds_bytes, BT_LDSL_BYTES);
+    e->a.lds_bytes_e = std::min(e->a.lds_bytes, BT_LDSE_BYTES);
     return set_lds_limits(std::max<size_t>(e->a.lds_bytes, BT_LDS_BYTES));
 }
 

@@ -47,6 +47,7 @@ static_assert(sizeof(BtCounters) == 128, "BtCounters layout");
 // Tracker variants (template parameter V of the kernels).
 constexpr int VAR_BYTETRACK = 0, VAR_BOTSORT = 1;
 constexpr int CLS_K = 8;             // BoT-SORT class-histogram entries per track
+constexpr int E_SLOTS = 3;           // candidate edges kept per pool row by k_s1_edges
 
 struct BtArgs {
     int S, CAP, MAXD;
@@ -90,6 +91,18 @@ struct BtArgs {
     unsigned char *ws;
     long long ws_stride;
     LapSlab slab;             // per stream: (threads / 64) slabs
+    // ByteTrack stage 1 as three launches (k_s1_prep / k_s1_edges / k_s1_lap): the per-stream
+    // grid over the high detections and every pool row's first candidate edges, in HBM
+    int *g_cell;              // [S][GRID_MAX_CELLS + 1] cell starts
+    int *g_ids, *g_big;       // [S*MAXD] binned high positions in cell order / big items
+    Box *g_boxes;             // [S*MAXD] their boxes, cell order
+    double *g_w;              // [S*MAXD] their scores (fuse_score weights), cell order
+    GridHdr *g_hdr;           // [S]
+    int *e_cnt;               // [S*CAP] candidate edges per pool row
+    int *e_col;               // [E_SLOTS][S*CAP] the first E_SLOTS edges' high positions
+    double *e_cost;           // [E_SLOTS][S*CAP] and costs
+    size_t lds_bytes_l;       // k_s1_lap arena
+    size_t lds_bytes_e;       // k_s1_edges grid
     // outputs
     double *out;              // [S*CAP][8]
     int *out_counts;          // optional [S]

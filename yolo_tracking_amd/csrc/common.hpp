@@ -154,15 +154,25 @@ __device__ __forceinline__ double wave_reduce(int op, double v) {
                   red_op(op, readlane_f64(v, 32), readlane_f64(v, 48)));
 }
 
+// Block barrier for hand-offs through LDS only: outstanding global stores are not waited for
+// (block_sync drains them, which costs a full memory round trip under load).
+__device__ __forceinline__ void lds_sync() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __syncthreads();
+}
+
 // Exclusive prefix sum over the whole block (blockDim.x a multiple of 64, <= 1024).  `wsum` is a
 // shared scratch of >= 16 ints.  Returns the exclusive prefix; *total gets the block sum.
+// GSYNC: the barrier also drains global memory operations (block_sync), else LDS only.
+template <bool GSYNC = true>
 __device__ __forceinline__ int block_exclusive_scan(int v, int *wsum, int *total) {
     const int lane = lane_id();
     const int wid = threadIdx.x / WAVE;
     const int nw = blockDim.x / WAVE;
     const int incl = wave_inclusive_scan(v);
     if (lane == WAVE - 1) wsum[wid] = incl;
-    block_sync();
+    if (GSYNC) block_sync();
+    else lds_sync();
     int p = lane < nw ? wsum[lane] : 0;
     p = wave_inclusive_scan(p);
     const int before = wid > 0 ? __builtin_amdgcn_readlane(p, wid - 1) : 0;
@@ -175,7 +185,7 @@ __device__ __forceinline__ int block_exclusive_scan(int v, int *wsum, int *total
 // threads of the block must call it.  Returns the count.  Each thread owns a contiguous run of
 // up to 32 indices (predicate bits in a register), so one block scan covers n <= 32 * blockDim;
 // beyond that the range is processed in such super-chunks.
-template <typename Pred, typename Emit>
+template <bool GSYNC = true, typename Pred, typename Emit>
 __device__ __forceinline__ int block_compact(int n, int *wsum, Pred pred, Emit emit) {
     const int nt = blockDim.x, t = threadIdx.x;
     int count = 0;
@@ -188,7 +198,7 @@ __device__ __forceinline__ int block_compact(int n, int *wsum, Pred pred, Emit e
         for (int i = lo; i < hi; ++i)
             if (pred(i)) bits |= 1u << (i - lo);
         int tot;
-        int pos = count + block_exclusive_scan(__popc(bits), wsum, &tot);
+        int pos = count + block_exclusive_scan<GSYNC>(__popc(bits), wsum, &tot);
         while (bits) {
             const int k = __ffs(bits) - 1;
             bits &= bits - 1;
@@ -202,7 +212,7 @@ __device__ __forceinline__ int block_compact(int n, int *wsum, Pred pred, Emit e
 // Two order-preserving compactions of [0, n) in one pass (one block scan of packed counts):
 // cat(i) -> 0 (neither), 1 or 2; emit(i, cat, position within its category).  Returns the two
 // counts.  Same ownership scheme as block_compact.
-template <typename Cat, typename Emit>
+template <bool GSYNC = true, typename Cat, typename Emit>
 __device__ __forceinline__ int2 block_compact2(int n, int *wsum, Cat cat, Emit emit) {
     const int nt = blockDim.x, t = threadIdx.x;
     int c1 = 0, c2 = 0;
@@ -218,7 +228,7 @@ __device__ __forceinline__ int2 block_compact2(int n, int *wsum, Cat cat, Emit e
             else if (c == 2) b2 |= 1u << (i - lo);
         }
         int tot;   // counts <= 32 * 1024 each: 16 bits apiece
-        const int ex = block_exclusive_scan(__popc(b1) | (__popc(b2) << 16), wsum, &tot);
+        const int ex = block_exclusive_scan<GSYNC>(__popc(b1) | (__popc(b2) << 16), wsum, &tot);
         int p1 = c1 + (ex & 0xFFFF), p2 = c2 + (ex >> 16);
         while (b1 | b2) {
             const int k1 = b1 ? __ffs(b1) - 1 : 32, k2 = b2 ? __ffs(b2) - 1 : 32;

@@ -12,7 +12,9 @@
 //   P3  complex nodes and component roots listed in node order
 //   P4  components gathered by counting sort (rows then columns, ascending)
 //   P5  one-row components take their cheapest edge (lowest cost, then lowest column: what the
-//       shortest-augmenting-path solve gives); the rest are solved exactly by successive shortest
+//       shortest-augmenting-path solve gives); components of <= 3 rows and <= 3 columns with a
+//       unique optimum are enumerated by one thread (solve_small); the rest are solved exactly by
+//       successive shortest
 //       augmenting paths with one private zero-cost dummy column per row: 16-lane segments (four
 //       components per wave), one wave (<= 64 columns + dummies), or a global-memory slab.
 //
@@ -295,6 +297,88 @@ __device__ __noinline__ void solve_large(int *bi, double *bd, int R, int C, cons
     wave_mem_sync();
 }
 
+// Components with k <= 3 rows and l <= 3 columns, solved by one thread that enumerates every
+// matching (<= 64).  The objective is sum(c - thresh) over the matched edges (assoc.hpp), summed in
+// row order.  When the best matching beats every other one by more than a rounding margin it is
+// the unique optimum, which every exact solver returns (solve_seg and lapx included); on a
+// (near-)tie this returns false and the component goes to solve_seg, whose tie-breaking the
+// goldens were checked against.  Every index below is a compile-time constant after unrolling,
+// so the 3x3 cost block stays in registers.
+constexpr double SMALL_TIE_MARGIN = 1e-12;
+__device__ __forceinline__ bool solve_small(int k, int l, const int *rows, const int *cols,
+                                            const int *row_off, const int *csr_col,
+                                            const double *csr_cost, double thresh, int *X,
+                                            int *Y) {
+    double C[3][3];
+    bool has[3][3];
+    int rg[3], cg[3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        rg[a] = a < k ? rows[a] : -1;
+        cg[a] = a < l ? cols[a] : -1;
+#pragma unroll
+        for (int b = 0; b < 3; ++b) {
+            C[a][b] = 0.0;
+            has[a][b] = false;
+        }
+    }
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        if (a >= k) continue;
+        const int e0 = row_off[rg[a]], e1 = row_off[rg[a] + 1];
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {   // a row's edges all lead to the component's <= 3 columns
+            if (e0 + q >= e1) continue;
+            const int col = csr_col[e0 + q];
+            const double w = csr_cost[e0 + q] - thresh;
+#pragma unroll
+            for (int b = 0; b < 3; ++b)
+                if (col == cg[b]) {
+                    C[a][b] = w;
+                    has[a][b] = true;
+                }
+        }
+    }
+    double best = INFINITY, second = INFINITY;
+    int best_code = -1;
+#pragma unroll
+    for (int x0 = -1; x0 < 3; ++x0)
+#pragma unroll
+        for (int x1 = -1; x1 < 3; ++x1)
+#pragma unroll
+            for (int x2 = -1; x2 < 3; ++x2) {
+                if ((x1 >= 0 && x1 == x0) || (x2 >= 0 && (x2 == x0 || x2 == x1))) continue;
+                bool ok = (x0 < 0 || (k > 0 && has[0][x0 < 0 ? 0 : x0])) &&
+                          (x1 < 0 || (k > 1 && has[1][x1 < 0 ? 0 : x1])) &&
+                          (x2 < 0 || (k > 2 && has[2][x2 < 0 ? 0 : x2]));
+                if (!ok) continue;
+                double o = 0.0;
+                if (x0 >= 0) o = o + C[0][x0 < 0 ? 0 : x0];
+                if (x1 >= 0) o = o + C[1][x1 < 0 ? 0 : x1];
+                if (x2 >= 0) o = o + C[2][x2 < 0 ? 0 : x2];
+                if (o < best) {
+                    second = best;
+                    best = o;
+                    best_code = (x0 + 1) | ((x1 + 1) << 2) | ((x2 + 1) << 4);
+                } else if (o < second) {
+                    second = o;
+                }
+            }
+    if (!(second - best > SMALL_TIE_MARGIN)) return false;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        if (a >= k) continue;
+        const int x = ((best_code >> (2 * a)) & 3) - 1;
+        int colg = -1;
+#pragma unroll
+        for (int b = 0; b < 3; ++b)
+            if (x == b) colg = cg[b];
+        X[rg[a]] = colg;
+        if (colg >= 0) Y[colg] = rg[a];
+    }
+    return true;
+}
+
 // Reads of arrays that other threads modify with atomics go through ald(): on global memory they
 // bypass the CU's L1 (the atomics execute in L2); on LDS they are plain ds_read.
 __device__ __forceinline__ int uf_find(const int *parent, int a) {
@@ -495,7 +579,18 @@ __device__ __forceinline__ bool lap_block(int nr, int nc, const int *row_off, co
             }
             X[r] = bestc;
             Y[bestc] = r;
+        } else if (k <= 3 && l <= 3 &&
+                   solve_small(k, l, members + m0, members + mr, row_off, csr_col, csr_cost,
+                               thresh, X, Y)) {
+            // unique optimum of a small component
         } else if (k + l <= 16) {
+#ifdef YTA_STAMPS
+            if (blockIdx.x == 0) {   // component shapes (tools/diag_s1.py)
+                const int bkt = l == 1 ? (k == 2 ? 0 : 1)
+                                       : (k == 2 && l == 2 ? 2 : (k == 2 ? 3 : (k == 3 && l == 2 ? 4 : (k + l <= 6 ? 5 : 6))));
+                atomicAdd(&g_stamps[117 + bkt], 1ull);
+            }
+#endif
             queue[atomicAdd(&sh.cnt[0], 1)] = c;
         } else if (k + l <= 64) {
             queue[ncomp - 1 - atomicAdd(&sh.cnt[1], 1)] = c;
