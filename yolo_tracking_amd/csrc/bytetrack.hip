@@ -187,9 +187,15 @@ __device__ __forceinline__ bool stage1_body(const BtArgs &a, int s, Arena &ar, S
         p[2] = H[0] * w + H[1] * h;
         p[3] = H[3] * w + H[4] * h;
     };
-    auto pred_box = [&](long long slot) {
+    auto pred_box = [&](long long slot, bool lost_list) {
         const double *m = a.kf + slot * KF_REC;
         const bool trk = st_of(a.flags[slot]) == ST_TRACKED;
+        if (V == VAR_BYTETRACK && lost_list) {   // lazily predicted (kf_xyah.hpp)
+            double ml[8];
+            for (int k = 0; k < 8; ++k) ml[k] = m[k];
+            kf_predict_lost_mean(ml, c->frame_id - a.kf_frame[slot]);
+            return xyah_mean_to_box(ml[0] + ml[4], ml[1] + ml[5], ml[2] + ml[6], ml[3]);
+        }
         const double vh = trk ? m[7] : 0.0;
         if (V == VAR_BOTSORT) {   // multi_predict zeroes vw and vh of non-tracked (:80-93)
             double p[4] = {m[0] + m[4], m[1] + m[5], m[2] + (trk ? m[6] : 0.0), m[3] + vh};
@@ -214,7 +220,7 @@ __device__ __forceinline__ bool stage1_body(const BtArgs &a, int s, Arena &ar, S
             const int slot = tracked[i];
             if (cat == 1) {
                 a.pool[tb + pos] = slot;
-                a.pool_box[tb + pos] = pred_box(tb + slot);
+                a.pool_box[tb + pos] = pred_box(tb + slot, false);
             } else {
                 a.unc[tb + pos] = slot;
                 a.unc_box[tb + pos] = unc_box_of(tb + slot);
@@ -224,7 +230,7 @@ __device__ __forceinline__ bool stage1_body(const BtArgs &a, int s, Arena &ar, S
     for (int i = t; i < n_lost; i += nt) {
         const int slot = a.lost[tb + i];
         a.pool[tb + n_act + i] = slot;
-        a.pool_box[tb + n_act + i] = pred_box(tb + slot);
+        a.pool_box[tb + n_act + i] = pred_box(tb + slot, true);
     }
     const int n_pool = n_act + n_lost;
     block_sync();
@@ -527,10 +533,19 @@ __global__ __launch_bounds__(PREP_T) void k_s1_prep(BtArgs a) {
         lds_sync();
     }
     YTA_STAMP(2);
-    // pool tail: the lost tracks, predicted
+    // pool tail: the lost tracks, predicted (their predicts since they were lost replayed first)
+    const int fid_prev = c->frame_id;
     batched_for<3>(
-        n_lost, [&](int i) { return bt_trk_rec(a, tb, a.lost[tb + i]); },
-        [&](int i, const TrkRec &r) {
+        n_lost,
+        [&](int i) {
+            const int slot = a.lost[tb + i];
+            TrkRec r = bt_trk_rec(a, tb, slot);
+            r.flags = fid_prev - a.kf_frame[tb + slot];   // pending predicts (state is Lost)
+            return r;
+        },
+        [&](int i, TrkRec r) {
+            kf_predict_lost_mean(r.m, r.flags);
+            r.flags = ST_LOST;
             a.pool[tb + n_act + i] = r.slot;
             a.pool_box[tb + n_act + i] = bt_pred_box(r);
         });
@@ -891,11 +906,14 @@ __global__ __launch_bounds__(APPLY_T) void k_apply(BtArgs a) {
             slot = a.unc[tb + (i - n_pool)];
             r3 = a.x3[tb + (i - n_pool)];
         }
-        s_slot[t] = slot;
     }
+    // ByteTrack: a Lost track (the pool's tail) left unmatched in stage 1 (the only stage that
+    // can re-find it) is predicted lazily (kf_xyah.hpp): its record is neither read nor written
+    const bool lazy = V == VAR_BYTETRACK && live && in_pool && i >= c->n_act && h < 0;
+    if (live) s_slot[t] = lazy ? -1 : slot;
     __syncthreads();
     // level 1: flags, the stage-1 detection, the stage-2 result
-    const int flags0 = live ? a.flags[tb + slot] : 0;
+    const int flags0 = live && !lazy ? a.flags[tb + slot] : 0;
     const int det1 = h >= 0 ? a.high[db + h] : -1;
     const int q2 = h < 0 && L >= 0 ? a.x2[tb + L] : -1;
     // Cooperative load straight into LDS (global_load_lds_dwordx4: no VGPRs, nothing the compiler
@@ -911,10 +929,13 @@ __global__ __launch_bounds__(APPLY_T) void k_apply(BtArgs a) {
         for (int q = 0; q < REC_PIECES; ++q) {
             const int p = t + q * APPLY_T;
             const int r = p / REC_PIECES, k = p - r * REC_PIECES;
-            const long long sl = tb + s_slot[r < nloc ? r : 0];   // rows past nloc: row 0 again
+            const int rs = s_slot[r < nloc ? r : 0];   // rows past nloc: row 0 again
+            const long long sl = tb + (rs < 0 ? 0 : rs);
             const double2 *src = k < 12 ? kf2 + sl * 12 + k : meta2 + sl * 3 + (k - 12);
-            __builtin_amdgcn_global_load_lds((glob_void *)src,
-                                             (lds_void *)(ldsb + (wb + q * APPLY_T) * 16), 16, 0, 0);
+            if (rs >= 0)   // lazy rows: nothing loaded, their LDS row is never read
+                __builtin_amdgcn_global_load_lds((glob_void *)src,
+                                                 (lds_void *)(ldsb + (wb + q * APPLY_T) * 16), 16,
+                                                 0, 0);
         }
     }
     // level 2 (3 for stage 3): the stage-2 / stage-3 detections
@@ -947,8 +968,11 @@ __global__ __launch_bounds__(APPLY_T) void k_apply(BtArgs a) {
         // pieces this track rewrites: bit 0 the Kalman record, bit 1 the meta
         s_wmask[t] = act == 5 ? 0 : (act == 1 || act == 2 || act == 4 ? 3 : 1);
     }
+    if (lazy) s_wmask[t] = 0;
     __syncthreads();
-    if (t < nloc) {
+    if (lazy) {
+        a.kind1[tb + i] = 0;
+    } else if (t < nloc) {
         KfState st;
         double *row = reinterpret_cast<double *>(rec[t]);
         TrackMeta m;
@@ -976,6 +1000,8 @@ __global__ __launch_bounds__(APPLY_T) void k_apply(BtArgs a) {
 #pragma unroll
             for (int k = 0; k < 16; ++k) st.c[k] = row[8 + k];
             const bool tracked = st_of(flags) == ST_TRACKED;
+            if (V == VAR_BYTETRACK && in_pool && i >= c->n_act)   // re-found from the lost list:
+                kf_predict_lost(st, fid - 1 - a.kf_frame[tb + slot]);   // replay the lazy predicts
             if (!tracked) {                                          // :41-42 / bot_sort.py:85-87
                 st.m[7] = 0;
                 if (V == VAR_BOTSORT) st.m[6] = 0;
@@ -993,6 +1019,7 @@ __global__ __launch_bounds__(APPLY_T) void k_apply(BtArgs a) {
                 wmask = 3;
             } else if (act == 3) {
                 flags = (flags & ~FL_STATE) | ST_LOST;
+                if (V == VAR_BYTETRACK) a.kf_frame[tb + slot] = fid;
             }
             // stage-1 outcome for the tracked' list order: 1 tracked -> updated, 2 re-found
             a.kind1[tb + i] = act == 1 ? (tracked ? 1 : 2) : 0;
@@ -1236,7 +1263,17 @@ __device__ __forceinline__ void finish_body(const BtArgs &a, int s, unsigned *bi
         GridView gv{nullptr, ar.alloc<int>(ncell + 1), ar.alloc<int>(n_l2), ar.alloc<Box>(n_l2),
                     nullptr, ar.alloc<int>(n_l2)};
         Box *lcache = ar.try_alloc<Box>(n_l2);
-        auto lbox = [&](int q) { return kf_box<V>(a.kf, tb + a.l2[tb + q]); };
+        auto lbox = [&](int q) {
+            const long long slot = tb + a.l2[tb + q];
+            if (V == VAR_BYTETRACK) {   // every lost' track is lazily predicted (kf_xyah.hpp)
+                double m[8];
+                const double *src = a.kf + slot * KF_REC;
+                for (int k = 0; k < 8; ++k) m[k] = src[k];
+                kf_predict_lost_mean(m, fid - a.kf_frame[slot]);
+                return xyah_mean_to_box(m[0], m[1], m[2], m[3]);
+            }
+            return kf_box<V>(a.kf, slot);
+        };
         if (lcache) {
             for (int q = t; q < n_l2; q += nt) lcache[q] = lbox(q);
             block_sync();
@@ -1555,6 +1592,7 @@ int bt_alloc(yta_bytetrack *e) {
     }
     DALLOC(a.meta, S * CAP);
     DALLOC(a.flags, S * CAP);
+    DALLOC(a.kf_frame, S * CAP);
     DALLOC(a.tracked, S * CAP);
     DALLOC(a.lost, S * CAP);
     DALLOC(a.free_list, S * CAP);
@@ -1752,6 +1790,7 @@ int reserve(yta_bytetrack *e, int cap, int maxd) {
     if (!rc) rc = copy2d(n->a.meta, nc * sizeof(TrackMeta), e->a.meta, oc * sizeof(TrackMeta),
                          oc * sizeof(TrackMeta), S);
     if (!rc) rc = copy2d(n->a.flags, nc * 4, e->a.flags, oc * 4, oc * 4, S);
+    if (!rc) rc = copy2d(n->a.kf_frame, nc * 4, e->a.kf_frame, oc * 4, oc * 4, S);
     if (!rc && e->a.cls_hist)
         rc = copy2d(n->a.cls_hist, nc * CLS_K * 16, e->a.cls_hist, oc * CLS_K * 16,
                     oc * CLS_K * 16, S);
@@ -2149,6 +2188,9 @@ int yta_bytetrack_get_state(yta_bytetrack *e, int stream, int *n_tracks, long lo
     YTA_HIP(hipMemcpy(meta.data(), e->a.meta + tb, sizeof(TrackMeta) * e->CAP,
                       hipMemcpyDeviceToHost));
     YTA_HIP(hipMemcpy(flags.data(), e->a.flags + tb, sizeof(int) * e->CAP, hipMemcpyDeviceToHost));
+    std::vector<int> kf_frame(e->CAP);
+    YTA_HIP(hipMemcpy(kf_frame.data(), e->a.kf_frame + tb, sizeof(int) * e->CAP,
+                      hipMemcpyDeviceToHost));
     std::vector<double> kfx(e->a.kfx ? (size_t)e->CAP * 16 : 0);
     if (e->a.kfx)
         YTA_HIP(hipMemcpy(kfx.data(), e->a.kfx + tb * 16, sizeof(double) * 16 * e->CAP,
@@ -2169,6 +2211,8 @@ int yta_bytetrack_get_state(yta_bytetrack *e, int stream, int *n_tracks, long lo
             KfState st;
             memcpy(st.m, kf.data() + (size_t)slot * KF_REC, sizeof(double) * 8);
             memcpy(st.c, kf.data() + (size_t)slot * KF_REC + 8, sizeof(double) * 16);
+            if (e->variant == VAR_BYTETRACK && which)   // lost list: lazily predicted
+                kf_predict_lost(st, c.frame_id - kf_frame[slot]);
             for (int k = 0; k < 8; ++k) mean[(long long)n * 8 + k] = st.m[k];
             double *P = cov + (long long)n * 64;
             kf_cov_full(st, P);

@@ -73,6 +73,8 @@ struct BtArgs {
     const double *warp;       // BoT-SORT: [S][6] this frame's camera warps (multi_gmc), row-major 2x3
     TrackMeta *meta;          // [S*CAP]
     int *flags;               // [S*CAP] state + FL_* bits, dense: every list scan reads these
+    int *kf_frame;            // [S*CAP] ByteTrack, Lost tracks: the frame their stored Kalman
+                              // state belongs to (later predicts replayed lazily, kf_xyah.hpp)
     int *tracked, *lost, *free_list;   // [S*CAP]
     BtCounters *cnt;          // [S]
     // per-frame: detections [S*MAXD]

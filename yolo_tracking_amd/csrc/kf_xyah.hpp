@@ -92,6 +92,25 @@ __host__ __device__ inline void kf_predict(KfState &s) {
     }
 }
 
+// ByteTrack's lost list is predicted lazily: a track's stored state is the one of the frame it was
+// marked lost, and the k predicts of the frames since (multi_predict zeroes vh first,
+// bytetrack_kf.py:41-42; its state is Lost, or Removed for one frame after expiry, the
+// removed_stracks quirk :262-265) are replayed where the state is needed, in the same operation
+// order, so the result is bit-identical to predicting every frame.
+__host__ __device__ inline void kf_predict_lost(KfState &s, int k) {
+    for (int j = 0; j < k; ++j) {
+        s.m[7] = 0;
+        kf_predict<KF_XYAH>(s);
+    }
+}
+// The mean alone (pool / duplicate-removal boxes): kf_predict's mean update with vh = 0.
+__host__ __device__ inline void kf_predict_lost_mean(double *m, int k) {
+    m[7] = 0;
+    for (int j = 0; j < k; ++j)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) m[i] = m[i] + m[i + 4];
+}
+
 // bytetrack_kf.py:194-226 (+ project :126-153) / botsort_kf.py:192-226 (+ project :110-148).
 template <int M = KF_XYAH>
 __host__ __device__ inline void kf_update(KfState &s, const double *z) {
