@@ -263,6 +263,7 @@ __device__ __forceinline__ bool stage1_body(const BtArgs &a, int s, Arena &ar, S
         c->n_left = 0;
         c->n_rest = 0;
         c->n_births = 0;
+        c->n_lazy = 0;
     }
     return true;
 }
@@ -506,8 +507,9 @@ __global__ __launch_bounds__(PREP_T) void k_s1_prep(BtArgs a) {
     int n_act = 0, n_unc = 0;
     for (int c0 = 0; c0 < n_tracked; c0 += PREP_CH) {
         const int m = n_tracked - c0 < PREP_CH ? n_tracked - c0 : PREP_CH;
-        batched_for<3>(
-            m, [&](int i) { return bt_trk_rec(a, tb, a.tracked[tb + c0 + i]); },
+        batched_for2<3>(
+            m, [&](int i) { return a.tracked[tb + c0 + i]; },
+            [&](int, int slot) { return bt_trk_rec(a, tb, slot); },
             [&](int i, const TrkRec &r) {
                 const bool act = (r.flags & FL_ACTIVATED) != 0;
                 sh.u.t.cat[i] = act ? 1 : 2;
@@ -535,10 +537,9 @@ __global__ __launch_bounds__(PREP_T) void k_s1_prep(BtArgs a) {
     YTA_STAMP(2);
     // pool tail: the lost tracks, predicted (their predicts since they were lost replayed first)
     const int fid_prev = c->frame_id;
-    batched_for<3>(
-        n_lost,
-        [&](int i) {
-            const int slot = a.lost[tb + i];
+    batched_for2<3>(
+        n_lost, [&](int i) { return a.lost[tb + i]; },
+        [&](int, int slot) {
             TrkRec r = bt_trk_rec(a, tb, slot);
             r.flags = fid_prev - a.kf_frame[tb + slot];   // pending predicts (state is Lost)
             return r;
@@ -560,6 +561,7 @@ __global__ __launch_bounds__(PREP_T) void k_s1_prep(BtArgs a) {
         c->n_left = 0;
         c->n_rest = 0;
         c->n_births = 0;
+        c->n_lazy = 0;
     }
     YTA_STAMP(3);
 }
@@ -969,6 +971,10 @@ __global__ __launch_bounds__(APPLY_T) void k_apply(BtArgs a) {
         s_wmask[t] = act == 5 ? 0 : (act == 1 || act == 2 || act == 4 ? 3 : 1);
     }
     if (lazy) s_wmask[t] = 0;
+    if (V == VAR_BYTETRACK) {   // records left untouched (stats)
+        const unsigned long long lz = __ballot(lazy);
+        if (lane_id() == 0 && lz) atomicAdd(&c->n_lazy, __popcll(lz));
+    }
     __syncthreads();
     if (lazy) {
         a.kind1[tb + i] = 0;
@@ -1149,14 +1155,21 @@ struct FinishShared {
     int wsum[32];
 };
 
+// lost' boxes (by position) + a grid of ids over them (cell starts, ids, big list)
 __host__ __device__ inline long long dedup_arena_bytes(long long n) {
     return 4 * (grid_cells_for((int)(n < GRID_MAX_CELLS ? n : GRID_MAX_CELLS)) + 1) +
-           n * (4 + 32 + 4) + 4 * 16;
+           n * (32 + 4 + 4) + 4 * 16;
 }
 
 __device__ __forceinline__ int track_age(const BtArgs &a, long long slot) {
     return a.meta[slot].frame_id - a.meta[slot].start_frame;   // STrack.end_frame - start_frame
 }
+
+// Every pass issues all of a thread's loads before using any (block_compact_ld, batched_for):
+// the block's chain is a sequence of dependent HBM round trips, each microseconds under load.
+struct SlotFlags {
+    int slot, flags;
+};
 
 template <int V>
 __device__ __forceinline__ void finish_body(const BtArgs &a, int s, unsigned *bits, Arena &ar,
@@ -1174,39 +1187,58 @@ __device__ __forceinline__ void finish_body(const BtArgs &a, int s, unsigned *bi
     for (int w = t; w < 3 * words; w += nt) bits[w] = 0u;
     YTA_STAMP(1);
 
-    // births in ascending order of the still-unmatched high detections (:242-248)
-    int n_births = block_compact(
+    // births in ascending order of the still-unmatched high detections (:242-248), each
+    // initiated by the thread that lists it
+    struct RestItem {
+        int y3, det;
+        double score;
+    };
+    const int n_births_all = block_compact_ld<4>(
         n_rest, wsum,
-        [&](int j) { return a.y3[db + j] < 0 && a.rest_score[db + j] >= a.det_thresh; },
-        [&](int j, int pos) { a.birth[db + pos] = j; });
+        [&](int j) {
+            RestItem r;
+            r.y3 = a.y3[db + j];
+            r.score = a.rest_score[db + j];
+            r.det = a.rest[db + j];   // high position, resolved below
+            return r;
+        },
+        [&](int, RestItem r) {
+            r.det = a.high[db + r.det];
+            return r;
+        },
+        [&](int, const RestItem &r) { return r.y3 < 0 && r.score >= a.det_thresh; },
+        [&](int j, const RestItem &r, int b) {
+            a.birth[db + b] = j;
+            if (b >= n_free) return;   // capacity (flagged below)
+            const int slot = a.free_list[tb + b];
+            const int d = r.det;
+            KfState st;
+            kf_initiate<kf_model<V>()>(a.det_xyah + (db + d) * 4, st);
+            store_kf(a.kf, tb + slot, st);
+            TrackMeta m;
+            m.score = a.det_conf[db + d];
+            m.cls = a.det_cls[db + d];
+            m.id = next_id + 1 + b;
+            m.det_ind = d;
+            m.n_cls = 0;
+            if (V == VAR_BOTSORT) {   // the detection's own STrack: cls_hist [[cls, score]] (:28)
+                a.cls_hist[(tb + slot) * CLS_K] = make_double2(m.cls, m.score);
+                m.n_cls = 1;
+            }
+            a.flags[tb + slot] = ST_TRACKED | (fid == 1 ? FL_ACTIVATED : 0);
+            m.frame_id = fid;
+            m.start_frame = fid;
+            m.tracklet_len = 0;
+            m.pad = 0;
+            a.meta[tb + slot] = m;
+        });
+    int n_births = n_births_all;
     if (n_births > n_free) {
         if (t == 0) atomicOr(&c->err, ERR_TRACK_CAPACITY);
         n_births = n_free;
     }
-    for (int b = t; b < n_births; b += nt) {
-        const int slot = a.free_list[tb + b];
-        const int d = a.high[db + a.rest[db + a.birth[db + b]]];
-        KfState st;
-        kf_initiate<kf_model<V>()>(a.det_xyah + (db + d) * 4, st);
-        store_kf(a.kf, tb + slot, st);
-        TrackMeta m;
-        m.score = a.det_conf[db + d];
-        m.cls = a.det_cls[db + d];
-        m.id = next_id + 1 + b;
-        m.det_ind = d;
-        m.n_cls = 0;
-        if (V == VAR_BOTSORT) {   // the detection's own STrack: cls_hist [[cls, score]] (:28)
-            a.cls_hist[(tb + slot) * CLS_K] = make_double2(m.cls, m.score);
-            m.n_cls = 1;
-        }
-        a.flags[tb + slot] = ST_TRACKED | (fid == 1 ? FL_ACTIVATED : 0);
-        m.frame_id = fid;
-        m.start_frame = fid;
-        m.tracklet_len = 0;
-        m.pad = 0;
-        a.meta[tb + slot] = m;
-    }
     if (V == VAR_BOTSORT && a.D > 0) {   // smooth_feat of a birth = its detection's curr_feat
+        block_sync();
         const int lane = lane_id(), nw = nt / WAVE;
         for (int b = t / WAVE; b < n_births; b += nw) {
             const int slot = a.free_list[tb + b];
@@ -1217,82 +1249,114 @@ __device__ __forceinline__ void finish_body(const BtArgs &a, int s, unsigned *bi
     }
     YTA_STAMP(2);
     // lost-track expiry (:250-253); end_frame == frame_id
-    for (int i = t; i < n_lost; i += nt) {
-        const long long slot = tb + a.lost[tb + i];
-        if (fid - a.meta[slot].frame_id > a.max_time_lost)
-            a.flags[slot] = (a.flags[slot] & ~FL_STATE) | ST_REMOVED | FL_REMOVED_NOW;
-    }
+    struct LostAge {
+        long long slot;
+        int frame, flags;
+    };
+    batched_for2<4>(
+        n_lost, [&](int i) { return a.lost[tb + i]; },
+        [&](int, int sl) {
+            LostAge v;
+            v.slot = tb + sl;
+            v.frame = a.meta[v.slot].frame_id;
+            v.flags = a.flags[v.slot];
+            return v;
+        },
+        [&](int, const LostAge &v) {
+            if (fid - v.frame > a.max_time_lost)
+                a.flags[v.slot] = (v.flags & ~FL_STATE) | ST_REMOVED | FL_REMOVED_NOW;
+        });
     block_sync();
     YTA_STAMP(3);
     // tracked' = [Tracked survivors of tracked_stracks] ++ births ++ re-found (:257-261)
-    int n_t2 = block_compact(
-        n_tracked, wsum,
-        [&](int i) { return st_of(a.flags[tb + a.tracked[tb + i]]) == ST_TRACKED; },
-        [&](int i, int pos) { a.t2[tb + pos] = a.tracked[tb + i]; });
+    auto with_flags = [&](int, int slot) { return SlotFlags{slot, a.flags[tb + slot]}; };
+    int n_t2 = block_compact_ld<8>(
+        n_tracked, wsum, [&](int i) { return a.tracked[tb + i]; }, with_flags,
+        [&](int, const SlotFlags &v) { return st_of(v.flags) == ST_TRACKED; },
+        [&](int, const SlotFlags &v, int pos) { a.t2[tb + pos] = v.slot; });
     for (int b = t; b < n_births; b += nt) a.t2[tb + n_t2 + b] = a.free_list[tb + b];
     n_t2 += n_births;
-    n_t2 += block_compact(n_pool, wsum, [&](int i) { return a.kind1[tb + i] == 2; },
-                          [&](int i, int pos) { a.t2[tb + n_t2 + pos] = a.pool[tb + i]; });
-    // lost' = sub(lost, tracked') ++ newly lost, minus ids already in removed_stracks (:262-264)
-    int n_l2 = block_compact(
-        n_lost, wsum,
-        [&](int i) {
-            const int f = a.flags[tb + a.lost[tb + i]];
-            return st_of(f) != ST_TRACKED && !(f & FL_EVER_REMOVED);
+    n_t2 += block_compact_ld<8>(
+        n_pool, wsum,
+        [&](int i) { return make_int2(a.kind1[tb + i], a.pool[tb + i]); },
+        [&](int, int2 v) { return v; }, [&](int, const int2 &v) { return v.x == 2; },
+        [&](int, const int2 &v, int pos) { a.t2[tb + n_t2 + pos] = v.y; });
+    // lost' = sub(lost, tracked') ++ newly lost, minus ids already in removed_stracks (:262-264);
+    // this frame's removals join removed_stracks only now (:265)
+    int n_l2 = block_compact_ld<8>(
+        n_lost, wsum, [&](int i) { return a.lost[tb + i]; }, with_flags,
+        [&](int, const SlotFlags &v) {
+            if (v.flags & FL_REMOVED_NOW)
+                a.flags[tb + v.slot] = (v.flags & ~FL_REMOVED_NOW) | FL_EVER_REMOVED;
+            return st_of(v.flags) != ST_TRACKED && !(v.flags & FL_EVER_REMOVED);
         },
-        [&](int i, int pos) { a.l2[tb + pos] = a.lost[tb + i]; });
-    n_l2 += block_compact(
+        [&](int, const SlotFlags &v, int pos) { a.l2[tb + pos] = v.slot; });
+    struct LeftItem {
+        int x2;
+        SlotFlags sf;
+    };
+    n_l2 += block_compact_ld<4>(
         n_left, wsum,
         [&](int i) {
-            return a.x2[tb + i] < 0 &&
-                   !(a.flags[tb + a.pool[tb + a.left[tb + i]]] & FL_EVER_REMOVED);
+            LeftItem v;
+            v.x2 = a.x2[tb + i];
+            v.sf.slot = a.pool[tb + a.left[tb + i]];
+            return v;
         },
-        [&](int i, int pos) { a.l2[tb + n_l2 + pos] = a.pool[tb + a.left[tb + i]]; });
+        [&](int, LeftItem v) {
+            v.sf.flags = a.flags[tb + v.sf.slot];
+            return v;
+        },
+        [&](int, const LeftItem &v) { return v.x2 < 0 && !(v.sf.flags & FL_EVER_REMOVED); },
+        [&](int, const LeftItem &v, int pos) { a.l2[tb + n_l2 + pos] = v.sf.slot; });
     block_sync();
     YTA_STAMP(4);
-    // this frame's removals join removed_stracks only now (:265)
-    for (int i = t; i < n_lost; i += nt) {
-        const long long slot = tb + a.lost[tb + i];
-        const int f = a.flags[slot];
-        if (f & FL_REMOVED_NOW) a.flags[slot] = (f & ~FL_REMOVED_NOW) | FL_EVER_REMOVED;
-    }
     // remove_duplicate_stracks (:312-325): pairs with 1 - IoU < 0.15 drop the younger track (set
     // semantics, so pairs are visited in any order)
     if (n_t2 > 0 && n_l2 > 0) {
         const int ncell = grid_cells_for(n_l2);
-        GridView gv{nullptr, ar.alloc<int>(ncell + 1), ar.alloc<int>(n_l2), ar.alloc<Box>(n_l2),
-                    nullptr, ar.alloc<int>(n_l2)};
-        Box *lcache = ar.try_alloc<Box>(n_l2);
-        auto lbox = [&](int q) {
-            const long long slot = tb + a.l2[tb + q];
-            if (V == VAR_BYTETRACK) {   // every lost' track is lazily predicted (kf_xyah.hpp)
-                double m[8];
-                const double *src = a.kf + slot * KF_REC;
-                for (int k = 0; k < 8; ++k) m[k] = src[k];
-                kf_predict_lost_mean(m, fid - a.kf_frame[slot]);
-                return xyah_mean_to_box(m[0], m[1], m[2], m[3]);
-            }
-            return kf_box<V>(a.kf, slot);
+        Box *lcache = ar.alloc<Box>(n_l2);   // the grid reads boxes through its ids from here
+        GridView gv{nullptr, ar.alloc<int>(ncell + 1), ar.alloc<int>(n_l2), nullptr, nullptr,
+                    ar.alloc<int>(n_l2), lcache};
+        // a lost' box: ByteTrack's lost' tracks are lazily predicted (kf_xyah.hpp)
+        struct LostMean {
+            double m[8];
+            int lag;
         };
-        if (lcache) {
-            for (int q = t; q < n_l2; q += nt) lcache[q] = lbox(q);
-            block_sync();
-            grid_build(n_l2, [&](int q) { return lcache[q]; }, [](int) { return 1.0; }, gv, sh.gs,
-                       wsum);
-        } else {
-            grid_build(n_l2, lbox, [](int) { return 1.0; }, gv, sh.gs, wsum);
-        }
+        auto lmean_of = [&](int slot_local) {
+            LostMean v;
+            const long long slot = tb + slot_local;
+            const double2 *src = reinterpret_cast<const double2 *>(a.kf + slot * KF_REC);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const double2 x = src[k];
+                v.m[2 * k] = x.x;
+                v.m[2 * k + 1] = x.y;
+            }
+            v.lag = V == VAR_BYTETRACK ? fid - a.kf_frame[slot] : 0;
+            return v;
+        };
+        auto lbox_of = [&](LostMean v) {
+            if (V == VAR_BYTETRACK) kf_predict_lost_mean(v.m, v.lag);
+            return V == VAR_BOTSORT ? xywh_to_box(v.m) : xyah_mean_to_box(v.m[0], v.m[1], v.m[2], v.m[3]);
+        };
+        batched_for2<3>(
+            n_l2, [&](int q) { return a.l2[tb + q]; }, [&](int, int sl) { return lmean_of(sl); },
+            [&](int q, const LostMean &v) { lcache[q] = lbox_of(v); });
+        block_sync();   // lcache may be the global arena
+        grid_build(n_l2, [&](int q) { return lcache[q]; }, [](int) { return 1.0; }, gv, sh.gs,
+                   wsum);
         const GridHdr gh = sh.gs.hdr;
         YTA_STAMP(5);
         struct TBox {
             long long slot;
             Box b;
         };
-        batched_for<4>(
-            n_t2,
-            [&](int p) {
+        batched_for2<5>(
+            n_t2, [&](int p) { return a.t2[tb + p]; },
+            [&](int, int sl) {
                 TBox v;
-                v.slot = tb + a.t2[tb + p];
+                v.slot = tb + sl;
                 v.b = kf_box<V>(a.kf, v.slot);
                 return v;
             },
@@ -1310,37 +1374,67 @@ __device__ __forceinline__ void finish_body(const BtArgs &a, int s, unsigned *bi
                 // 1 - IoU < 0.15  <=>  IoU > 0.85: only corners within 0.18 w of tbx's
                 grid_query_iou_above(gv, gh, tbx, 0.85,
                                      [&](int q, const Box &lb, double) { pair(q, lb); },
-                                     [&](int q) { pair(q, lbox(q)); });
+                                     [&](int q) { pair(q, lcache[q]); });
             });
     }
-    block_sync();
+    lds_sync();
     YTA_STAMP(6);
-    // final lists, output rows, free slots
-    const int n_tr = block_compact(n_t2, wsum, [&](int p) { return !((dropA[p >> 5] >> (p & 31)) & 1u); },
-                                   [&](int p, int pos) {
-                                       const int slot = a.t2[tb + p];
-                                       a.tracked[tb + pos] = slot;
-                                       atomicOr(&live[slot >> 5], 1u << (slot & 31));
-                                   });
-    const int n_lo = block_compact(n_l2, wsum, [&](int q) { return !((dropB[q >> 5] >> (q & 31)) & 1u); },
-                                   [&](int q, int pos) {
-                                       const int slot = a.l2[tb + q];
-                                       a.lost[tb + pos] = slot;
-                                       atomicOr(&live[slot >> 5], 1u << (slot & 31));
-                                   });
+    // final lists (tracked, lost) and the output slots (activated tracked, in order) in one pass
+    // over tracked' (one scan of packed counts), output rows, free slots
+    ar.lo = 0;   // the dedup grid is dead: its arena holds the output slot list
+    int *outslot = reinterpret_cast<int *>(ar.base);
+    const bool os_arena = ar.hi >= (size_t)4 * (n_t2 > 0 ? n_t2 : 1);
+    int n_tr = 0, n_out = 0;
+    for (int base = 0; base < n_t2; base += 8 * nt) {
+        const int m = n_t2 - base < 8 * nt ? n_t2 - base : 8 * nt;
+        const int per = (m + nt - 1) / nt;
+        const int lo = base + t * per;
+        const int hi = lo + per < base + m ? lo + per : base + m;
+        int sl[8];
+        SlotFlags v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+            if (lo + k < hi) sl[k] = a.t2[tb + lo + k];
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+            if (lo + k < hi) v[k] = with_flags(0, sl[k]);
+        unsigned keep = 0, outb = 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int p = lo + k;
+            if (p < hi && !((dropA[p >> 5] >> (p & 31)) & 1u)) {
+                keep |= 1u << k;
+                if (v[k].flags & FL_ACTIVATED) outb |= 1u << k;
+            }
+        }
+        int tot;   // counts <= 8 * 1024 each: 16 bits apiece
+        const int ex = block_exclusive_scan(__popc(keep) | (__popc(outb) << 16), wsum, &tot);
+        int pk = n_tr + (ex & 0xFFFF), po = n_out + (ex >> 16);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            if (!((keep >> k) & 1u)) continue;
+            const int slot = v[k].slot;
+            a.tracked[tb + pk++] = slot;
+            atomicOr(&live[slot >> 5], 1u << (slot & 31));
+            if ((outb >> k) & 1u) {
+                if (os_arena) outslot[po] = slot;
+                else a.t2[tb + po] = slot;   // t2 entries < po were all read above
+                ++po;
+            }
+        }
+        n_tr += tot & 0xFFFF;
+        n_out += tot >> 16;
+    }
+    const int n_lo = block_compact_ld<8>(
+        n_l2, wsum, [&](int q) { return a.l2[tb + q]; }, [&](int, int slot) { return slot; },
+        [&](int q, int) { return !((dropB[q >> 5] >> (q & 31)) & 1u); },
+        [&](int, int slot, int pos) {
+            a.lost[tb + pos] = slot;
+            atomicOr(&live[slot >> 5], 1u << (slot & 31));
+        });
     block_sync();
     YTA_STAMP(7);
     double *out = a.out + tb * 8;
-    ar.lo = 0;   // the dedup grid is dead: its arena holds the output slot list
-    int *outslot = reinterpret_cast<int *>(ar.base);
-    const bool os_arena = ar.hi >= (size_t)4 * (n_tr > 0 ? n_tr : 1);
-    const int n_out = block_compact(
-        n_tr, wsum, [&](int i) { return (a.flags[tb + a.tracked[tb + i]] & FL_ACTIVATED) != 0; },
-        [&](int i, int pos) {
-            if (os_arena) outslot[pos] = a.tracked[tb + i];
-            else a.t2[tb + pos] = a.tracked[tb + i];   // t2 is dead: reuse as the slot list
-        });
-    block_sync();
     struct Row {
         Box b;
         TrackMeta m;
@@ -1362,9 +1456,9 @@ __device__ __forceinline__ void finish_body(const BtArgs &a, int s, unsigned *bi
             o[3] = make_double2(r.m.cls, (double)r.m.det_ind);
         });
     YTA_STAMP(8);
-    const int n_fr = block_compact(a.CAP, wsum,
-                                   [&](int slot) { return !((live[slot >> 5] >> (slot & 31)) & 1u); },
-                                   [&](int slot, int pos) { a.free_list[tb + pos] = slot; });
+    const int n_fr = block_compact<false>(
+        a.CAP, wsum, [&](int slot) { return !((live[slot >> 5] >> (slot & 31)) & 1u); },
+        [&](int slot, int pos) { a.free_list[tb + pos] = slot; });
     YTA_STAMP(9);
     if (t == 0) {
         c->n_births = n_births;
@@ -1488,13 +1582,14 @@ struct yta_bytetrack {
 
 namespace {
 
-constexpr int BT_PHASES = 4;   // launches per frame, see yta_bytetrack_profile_collect
+constexpr int BT_PHASES = 6;   // timed phases per frame, see yta_bytetrack_profile_collect
 #ifndef YTA_LDS1_KB
 #define YTA_LDS1_KB 150
 #endif
 constexpr size_t BT_LDS_BYTES = YTA_LDS1_KB * 1024;   // k_stage1 arena (one 1024-thread block per CU)
 constexpr size_t BT_LDS23_BYTES = 32 * 1024;  // k_stage23 arena (several blocks per CU)
-constexpr size_t BT_LDSF_BYTES = 20 * 1024;   // k_finish dedup arena (several blocks per CU)
+constexpr size_t BT_LDSF_BYTES = 36 * 1024;   // k_finish dedup arena (four blocks per CU; lost'
+                                              // of 720 at 1024 x 1024)
 #ifndef YTA_LDSL_KB
 #define YTA_LDSL_KB 76
 #endif
@@ -1695,9 +1790,9 @@ int set_lds_limits(size_t bytes) {
     return YTA_OK;
 }
 
-// One frame of every stream: 4 launches (ByteTrack), + k_feat and k_ema (BoT-SORT with ReID).
-// Profiling marks bracket the phases stage1 (k_feat + k_stage1), stage23, apply (k_apply +
-// k_ema), finish.
+// One frame of every stream: 6 launches (ByteTrack), 4 + k_feat and k_ema (BoT-SORT, fused stage
+// 1).  Profiling marks bracket the phases s1_prep / s1_edges / s1_lap (BoT-SORT: k_feat + k_stage1,
+// empty, empty), stage23, apply (k_apply + k_ema), finish.
 template <int V>
 int launch_frame(yta_bytetrack *e) {
     BtArgs &a = e->a;
@@ -1711,11 +1806,16 @@ int launch_frame(yta_bytetrack *e) {
     if (V == VAR_BYTETRACK && a.match_thresh <= 1.0) {   // grid-exact candidates (assoc.hpp)
         hipLaunchKernelGGL(k_s1_prep, dim3(a.S), dim3(PREP_T), 0, e->stream, a);
         YTA_HIP(hipGetLastError());
+        MARK();
         hipLaunchKernelGGL(k_s1_edges, dim3(a.S), dim3(BLKE), a.lds_bytes_e, e->stream, a);
         YTA_HIP(hipGetLastError());
+        MARK();
         hipLaunchKernelGGL(k_s1_lap, dim3(a.S), dim3(BLKL), a.lds_bytes_l, e->stream, a);
-    } else {
+    } else {   // fused stage 1: the whole stage in the first phase, the next two empty
         hipLaunchKernelGGL(k_stage1<V>, dim3(a.S), dim3(BLK1), a.lds_bytes, e->stream, a);
+        YTA_HIP(hipGetLastError());
+        MARK();
+        MARK();
     }
     YTA_HIP(hipGetLastError());
     MARK();
@@ -2262,7 +2362,7 @@ int yta_bytetrack_stats(yta_bytetrack *e, long long *stats) {
     YTA_HIP(hipSetDevice(e->device));
     const int rc = read_counters(e);
     if (rc) return rc;
-    constexpr int NS = 18;
+    constexpr int NS = 19;
     for (int k = 0; k < NS; ++k) stats[k] = 0;
     for (int s = 0; s < e->S; ++s) {
         const BtCounters &c = e->h_cnt[s];
@@ -2270,7 +2370,7 @@ int yta_bytetrack_stats(yta_bytetrack *e, long long *stats) {
                                  c.n_left, c.n_rest, c.n_births, c.n_t2, c.n_l2, c.n_tracked,
                                  c.n_lost, c.n_out, (long long)c.n_edges[0],
                                  (long long)c.n_edges[1] + c.n_edges[2], c.n_fallback[0],
-                                 c.n_fallback[1]};
+                                 c.n_fallback[1], c.n_lazy};
         for (int k = 0; k < NS; ++k) stats[k] += v[k];
     }
     return YTA_OK;

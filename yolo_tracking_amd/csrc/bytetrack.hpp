@@ -39,7 +39,8 @@ struct BtCounters {                  // one per stream, 128 B
     int err;
     int n_edges[3];
     int n_fallback[2];               // cumulative: association redone over global memory
-    int pad[7];
+    int n_lazy;                      // ByteTrack: lost-list records k_apply left untouched
+    int pad[6];
 };
 static_assert(sizeof(BtCounters) == 128, "BtCounters layout");
 

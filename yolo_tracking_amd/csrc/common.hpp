@@ -246,6 +246,70 @@ __device__ __forceinline__ int2 block_compact2(int n, int *wsum, Cat cat, Emit e
     return make_int2(c1, c2);
 }
 
+// block_compact for items whose predicate needs memory loads, as a two-level gather: a thread owns
+// a contiguous run of <= PER indices per pass, issues every first-level load of its run
+// (first(i) -> K, typically a list entry), then every second-level load (second(i, k) -> V, the
+// entry's record), and only then tests them (pred(i, v)); emit(i, v, position) gets the loaded
+// value.  A load chain written inside one per-item call would cost a round trip per item: the
+// compiler cannot issue item b + 1's index load ahead of item b's dependent load.
+// One block scan per PER * blockDim items.
+template <int PER, bool GSYNC = true, typename First, typename Second, typename Pred,
+          typename Emit>
+__device__ __forceinline__ int block_compact_ld(int n, int *wsum, First first, Second second,
+                                                Pred pred, Emit emit) {
+    const int nt = blockDim.x, t = threadIdx.x;
+    using K = decltype(first(0));
+    using V = decltype(second(0, first(0)));
+    int count = 0;
+    for (int base = 0; base < n; base += PER * nt) {
+        const int m = n - base < PER * nt ? n - base : PER * nt;
+        const int per = (m + nt - 1) / nt;
+        const int lo = base + t * per;
+        const int hi = lo + per < base + m ? lo + per : base + m;
+        K kk[PER];
+        V v[PER];
+#pragma unroll
+        for (int k = 0; k < PER; ++k)
+            if (lo + k < hi) kk[k] = first(lo + k);
+#pragma unroll
+        for (int k = 0; k < PER; ++k)
+            if (lo + k < hi) v[k] = second(lo + k, kk[k]);
+        unsigned bits = 0;
+#pragma unroll
+        for (int k = 0; k < PER; ++k)
+            if (lo + k < hi && pred(lo + k, v[k])) bits |= 1u << k;
+        int tot;
+        int pos = count + block_exclusive_scan<GSYNC>(__popc(bits), wsum, &tot);
+#pragma unroll
+        for (int k = 0; k < PER; ++k)
+            if ((bits >> k) & 1u) emit(lo + k, v[k], pos++);
+        count += tot;
+    }
+    return count;
+}
+
+// Strided loop over [0, n) as a two-level gather (see block_compact_ld): B items per thread per
+// step, first-level loads of all of them, then their second-level loads, then use(i, v).
+template <int B, typename First, typename Second, typename Use>
+__device__ __forceinline__ void batched_for2(int n, First first, Second second, Use use) {
+    const int t = threadIdx.x, nt = blockDim.x;
+    using K = decltype(first(0));
+    using V = decltype(second(0, first(0)));
+    for (int base = t; base < n; base += B * nt) {
+        K kk[B];
+        V v[B];
+#pragma unroll
+        for (int b = 0; b < B; ++b)
+            if (base + b * nt < n) kk[b] = first(base + b * nt);
+#pragma unroll
+        for (int b = 0; b < B; ++b)
+            if (base + b * nt < n) v[b] = second(base + b * nt, kk[b]);
+#pragma unroll
+        for (int b = 0; b < B; ++b)
+            if (base + b * nt < n) use(base + b * nt, v[b]);
+    }
+}
+
 // Strided loop over [0, n) that issues the loads of B iterations before using any of them, so
 // their latencies overlap: load(i) -> value, use(i, value).
 template <int B, typename Load, typename Use>

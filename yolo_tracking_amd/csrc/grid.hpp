@@ -37,10 +37,16 @@ struct GridView {
     GridHdr *hdr;      // optional copy of the header (global)
     int *cell_start;   // GRID_MAX_CELLS + 1
     int *ids;          // binned item ids, in cell order
-    Box *boxes;        // their boxes, same order
+    Box *boxes;        // their boxes, same order (nullptr: read through by_id)
     double *w;         // optional per-item weight, same order (nullptr: none)
     int *big;          // items scanned by every query
+    const Box *by_id = nullptr;   // with boxes == nullptr: every item's box, by item id
 };
+
+// Box of the binned item at cell-order position k.
+__device__ __forceinline__ Box grid_box(const GridView &gv, int k) {
+    return gv.boxes ? gv.boxes[k] : gv.by_id[gv.ids[k]];
+}
 
 
 __host__ __device__ __forceinline__ bool box_usable(const Box &b) {
@@ -191,7 +197,7 @@ __device__ __forceinline__ void grid_build(int n, BoxOf box, WOf wof, GridView g
         if (!binned(b)) continue;
         const int pos = atomicAdd(&cs[cell_of(b) + 1], 1);
         gv.ids[pos] = i;
-        gv.boxes[pos] = b;
+        if (gv.boxes) gv.boxes[pos] = b;
         if (gv.w) gv.w[pos] = wof(i);
     }
     block_sync();
@@ -227,14 +233,14 @@ __device__ __forceinline__ void grid_scan(const GridView &gv, const GridHdr &h, 
         }
         int k = b;
         for (; k + 1 < e; k += 2) {   // the cells of a grid row are contiguous
-            const Box b0 = gv.boxes[k], b1 = gv.boxes[k + 1];
+            const Box b0 = grid_box(gv, k), b1 = grid_box(gv, k + 1);
             const int i0 = gv.ids[k], i1 = gv.ids[k + 1];
             const double w0 = wt(k), w1 = wt(k + 1);
             if (intersects(T, b0)) hit(k, i0, b0, w0);
             if (intersects(T, b1)) hit(k + 1, i1, b1, w1);
         }
         if (k < e) {
-            const Box b0 = gv.boxes[k];
+            const Box b0 = grid_box(gv, k);
             if (intersects(T, b0)) hit(k, gv.ids[k], b0, wt(k));
         }
         b = nb;
@@ -266,13 +272,13 @@ __device__ __forceinline__ void grid_scan_corner(const GridView &gv, const GridH
         }
         int k = b;
         for (; k + 1 < e; k += 2) {
-            const Box b0 = gv.boxes[k], b1 = gv.boxes[k + 1];
+            const Box b0 = grid_box(gv, k), b1 = grid_box(gv, k + 1);
             const int i0 = gv.ids[k], i1 = gv.ids[k + 1];
             const double w0 = wt(k), w1 = wt(k + 1);
             hit(k, i0, b0, w0);
             hit(k + 1, i1, b1, w1);
         }
-        if (k < e) hit(k, gv.ids[k], gv.boxes[k], wt(k));
+        if (k < e) hit(k, gv.ids[k], grid_box(gv, k), wt(k));
         b = nb;
         e = ne;
     }
