@@ -26,9 +26,9 @@ import numpy as np
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
-PHASES = ["stage1", "stage23", "apply", "finish"]
+PHASES = ["s1_prep", "s1_edges", "s1_lap", "stage23", "apply", "finish"]
 STATS = ["dets", "high", "second", "pool", "act", "unc", "left", "rest", "births", "t2", "l2",
-         "tracked", "lost", "out", "edges1", "edges23", "fallback1", "fallback23"]
+         "tracked", "lost", "out", "edges1", "edges23", "fallback1", "fallback23", "lazy"]
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # Canonical algorithmic bytes per update: ByteTrack 1024 x 1024
 BYTES_PER_UPDATE_1024 = 19_259_392
@@ -41,19 +41,31 @@ def algorithmic_bytes(n, m):
 
 def kernel_bytes(phase, st):
     """Algorithmic HBM bytes one launch of `phase` must move, from the last frame's counts summed
-    over streams (DESIGN.md §Kernels).  Kalman record = 24 f64 (192 B), track meta = 48 B, box = 32 B,
-    detection row = 48 B, candidate edge = 16 B."""
+    over streams (DESIGN.md §5).  Kalman record = 24 f64 (192 B), track meta = 48 B, box = 32 B,
+    detection row = 48 B, candidate edge = 12 B (int column + f64 cost)."""
     pool, unc, high, dets = st["pool"], st["unc"], st["high"], st["dets"]
+    act, lazy = st["act"], st["lazy"]
+    lost_list = pool - act
     matched = st["tracked"]            # tracks updated this frame (upper bound: tracked list)
+    if phase == "s1_prep":
+        # dets read, measurement / conf / cls written; high and low lists with boxes (+ score);
+        # tracked list, flags and Kalman mean of every pool / unconfirmed track (+ the lazy frame
+        # of lost ones), pool / unconfirmed lists with boxes written
+        return (dets * (48 + 48) + high * (4 + 32 + 8) + st["second"] * (4 + 32)
+                + (act + unc) * (4 + 4 + 64 + 4 + 32) + lost_list * (4 + 4 + 4 + 64 + 4 + 32))
+    if phase == "s1_edges":
+        # high boxes + scores read once (grid built in LDS), every pool box read, edge count and
+        # edges written
+        return high * (32 + 8) + pool * (32 + 4) + st["edges1"] * 12
+    if phase == "s1_lap":
+        # edge counts and edges read, the assignment written (row and column results)
+        return pool * (4 + 4) + st["edges1"] * 12 + high * 4
     if phase == "apply":
-        # every pool track: KF state + meta read and written once, pool index + stage results read;
-        # every matched track: its detection's xyah / conf / cls read
-        return pool * (2 * 192 + 2 * 48 + 12) + unc * (48 + 8) + matched * 48
-    if phase == "stage1":
-        # dets read + converted rows written; high / low lists + boxes; tracked list, meta, the
-        # predicted mean of every pool track; pool / unconfirmed lists + boxes; stage-1 results
-        return (dets * (48 + 48) + high * (4 + 32 + 8 + 4) + st["second"] * (4 + 32)
-                + pool * (4 + 48 + 64 + 4 + 32 + 4) + unc * (4 + 48 + 64 + 4 + 32))
+        # every pool / unconfirmed track but the lazily predicted lost ones: Kalman record + meta
+        # read, record written; matched tracks: meta written, the detection's xyah / conf / cls
+        # read; every pool item: index + stage results read, stage-1 kind written
+        touched = pool - lazy + unc
+        return touched * (192 + 48 + 192) + matched * (48 + 48) + pool * (4 + 4 + 4 + 4) + unc * 8
     if phase == "stage23":
         return (pool * (4 + 48 + 4) + high * (4 + 8 + 8) + st["left"] * (8 + 32 + 4)
                 + st["second"] * (32 + 4) + unc * (32 + 4) + st["rest"] * (4 + 32 + 8 + 4))
@@ -253,8 +265,8 @@ def main():
     _lib.check(lib.yta_bytetrack_stats(h, stats))
     st = {STATS[k]: int(stats[k]) for k in range(len(STATS))}
     if rank == 0:
-        # roofline kernel: the Kalman predict/update pass over every live track (HBM-bound)
-        dom = "apply"
+        # roofline kernel: the longest launch of the frame (the Kalman pass k_apply, HBM-bound)
+        dom = max(phase_ms, key=lambda p: phase_ms[p])
         dom_ms = phase_ms[dom]
         b = kernel_bytes(dom, st)
         achieved = b / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0

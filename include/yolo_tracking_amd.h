@@ -167,15 +167,17 @@ int yta_bytetrack_sync(yta_bytetrack *engine);      /* waits; reports device-sid
  * (64 f64).  *n_tracks receives the count; buffers must hold track_capacity entries. */
 int yta_bytetrack_get_state(yta_bytetrack *engine, int stream, int *n_tracks, long long *ints,
                             double *mean, double *cov);
-/* Measurement: when enabled, HIP events are recorded around each of the 4 launches of a frame on
- * the engine's stream; collect returns per-launch milliseconds summed over the covered frames in
- * launch order (stage1, stage23, apply, finish). */
+/* Measurement: when enabled, HIP events are recorded around each phase of a frame on the
+ * engine's stream; collect returns per-phase milliseconds summed over the covered frames, 6 values
+ * in launch order: k_s1_prep, k_s1_edges, k_s1_lap (BoT-SORT and match_thresh > 1: the fused
+ * k_stage1 in the first, the next two 0), stage23, apply, finish. */
 int yta_bytetrack_profile(yta_bytetrack *engine, int enable);
 int yta_bytetrack_profile_collect(yta_bytetrack *engine, double *ms, int *frames);
 /* Last frame's counts summed over streams (synchronises): dets, high, second, pool, activated,
  * unconfirmed, leftovers, rest, births, tracked', lost', tracked, lost, output rows, stage-1
  * candidate edges, stage-2+3 candidate edges, then the cumulative number of stream-frames whose
- * stage-1 / stage-2+3 association did not fit in LDS and ran over global memory (18 int64). */
+ * stage-1 / stage-2+3 association did not fit in LDS and ran over global memory, then (ByteTrack)
+ * the lost-list Kalman records the last frame left untouched (lazy prediction) (19 int64). */
 int yta_bytetrack_stats(yta_bytetrack *engine, long long *stats);
 /* Tuning / testing: bytes of LDS the association kernels may use per stream (default 150 KiB,
  * at most 150 KiB); a stream-frame that does not fit runs over global memory.  0 forces the

@@ -64,7 +64,8 @@ class ByteTrackEngine:
     def stats(self):
         """Last frame's counts summed over streams (see yta_bytetrack_stats)."""
         names = ["dets", "high", "second", "pool", "act", "unc", "left", "rest", "births", "t2",
-                 "l2", "tracked", "lost", "out", "edges1", "edges23", "fallback1", "fallback23"]
+                 "l2", "tracked", "lost", "out", "edges1", "edges23", "fallback1", "fallback23",
+                 "lazy"]
         buf = (ctypes.c_longlong * len(names))()
         _lib.check(self.lib.yta_bytetrack_stats(self._h, buf))
         return {k: int(buf[i]) for i, k in enumerate(names)}
