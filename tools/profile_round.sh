@@ -1,6 +1,7 @@
 #!/bin/bash
-# rocprofv3 evidence for profiles/ (GPU box): kernel trace + stats, then FETCH_SIZE and WRITE_SIZE
-# in their own passes, all on the same bench.py command.  Usage: tools/profile_round.sh TAG STREAMS
+# rocprofv3 evidence for profiles/ (GPU box): the bench line, kernel trace + stats, then FETCH_SIZE
+# and WRITE_SIZE in their own passes, all on the same bench.py command (the driver's round-end
+# step count).  Usage: tools/profile_round.sh TAG [STREAMS]  -> gpurun_out/prof_TAG/
 set -e
 TAG=$1
 S=${2:-1024}
@@ -8,9 +9,10 @@ R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/prof_$TAG
 mkdir -p $O
 cd /tmp && export TMPDIR=/tmp
-CMD="python3 $R/bench.py --streams $S --steps 10 --warmup 3 --no-cpu-baseline"
-timeout -k 10 400 python3 $R/bench.py --streams $S --steps 10 --warmup 3 --no-cpu-baseline > $O/bench.json 2> $O/bench.err
-timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt -o run -- $CMD > $O/kt.log 2>&1
-timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/fetch -o run -- $CMD > $O/fetch.log 2>&1
-timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/write -o run -- $CMD > $O/write.log 2>&1
+ARGS="--streams $S --steps 20 --warmup 5 --no-cpu-baseline --no-pcie"
+timeout -k 10 400 python3 $R/bench.py $ARGS > $O/bench.json 2> $O/bench.err
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt -o run -- python3 $R/bench.py $ARGS > $O/kt.log 2>&1
+timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/fetch -o run -- python3 $R/bench.py $ARGS > $O/fetch.log 2>&1
+timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/write -o run -- python3 $R/bench.py $ARGS > $O/write.log 2>&1
+cd $R && python3 profiles/summarize.py $TAG $O/kt $O/fetch $O/write --streams $S --bench-json $O/bench.json > $O/summary.txt
 echo profiled

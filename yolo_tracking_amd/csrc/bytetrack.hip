@@ -52,7 +52,7 @@ constexpr int BLK_MAX = 1024;
 constexpr int SLAB_WAVES = BLK_MAX / WAVE;   // solver slabs per stream (any block size)
 
 __device__ __forceinline__ void store_kf(double *kf, long long slot, const KfState &s) {
-    double2 *dst = reinterpret_cast<double2 *>(kf + slot * KF_REC);
+    double2 *dst = reinterpret_cast<double2 *>(kf + slot * TRK_STRIDE);
 #pragma unroll
     for (int k = 0; k < 12; ++k) {
         const double *src = k < 4 ? s.m + 2 * k : s.c + 2 * (k - 4);
@@ -64,7 +64,7 @@ __device__ __forceinline__ void store_kf(double *kf, long long slot, const KfSta
 // BoT-SORT (xc, yc, w, h) (bot_sort.py:173-182)
 template <int V>
 __device__ __forceinline__ Box kf_box(const double *kf, long long slot) {
-    const double2 *m = reinterpret_cast<const double2 *>(kf + slot * KF_REC);
+    const double2 *m = reinterpret_cast<const double2 *>(kf + slot * TRK_STRIDE);
     const double2 a = m[0], b = m[1];
     if (V == VAR_BOTSORT) {
         const double xywh[4] = {a.x, a.y, b.x, b.y};
@@ -89,6 +89,10 @@ __device__ __forceinline__ DetFeat det_feat(const BtArgs &a, int s, long long db
 }
 
 __device__ __forceinline__ int st_of(int flags) { return flags & FL_STATE; }
+
+__host__ __device__ __forceinline__ TrackMeta &bt_meta(const BtArgs &a, long long slot) {
+    return *reinterpret_cast<TrackMeta *>(a.kf + slot * TRK_STRIDE + TRK_META);
+}
 
 
 // ------------------------------------------------------------------------------------ k_stage1
@@ -188,7 +192,7 @@ __device__ __forceinline__ bool stage1_body(const BtArgs &a, int s, Arena &ar, S
         p[3] = H[3] * w + H[4] * h;
     };
     auto pred_box = [&](long long slot, bool lost_list) {
-        const double *m = a.kf + slot * KF_REC;
+        const double *m = a.kf + slot * TRK_STRIDE;
         const bool trk = st_of(a.flags[slot]) == ST_TRACKED;
         if (V == VAR_BYTETRACK && lost_list) {   // lazily predicted (kf_xyah.hpp)
             double ml[8];
@@ -206,7 +210,7 @@ __device__ __forceinline__ bool stage1_body(const BtArgs &a, int s, Arena &ar, S
     };
     auto unc_box_of = [&](long long slot) {   // unconfirmed: not predicted, warped (:295)
         if (V == VAR_BOTSORT && gmc) {
-            const double *m = a.kf + slot * KF_REC;
+            const double *m = a.kf + slot * TRK_STRIDE;
             double p[4] = {m[0], m[1], m[2], m[3]};
             warped(p);
             return xywh_to_box(p);
@@ -431,7 +435,7 @@ __device__ __forceinline__ TrkRec bt_trk_rec(const BtArgs &a, long long tb, int 
     TrkRec r;
     r.slot = slot;
     r.flags = a.flags[tb + slot];
-    const double2 *m = reinterpret_cast<const double2 *>(a.kf + (tb + slot) * KF_REC);
+    const double2 *m = reinterpret_cast<const double2 *>(a.kf + (tb + slot) * TRK_STRIDE);
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         const double2 q = m[k];
@@ -874,7 +878,7 @@ __device__ __forceinline__ void take_detection(const BtArgs &a, KfState &st, Tra
 // pieces of a record (full-line reads and writes); each thread then runs the Kalman step of one
 // track out of LDS.  Pieces 0-11: the Kalman record (mean, then covariance), 12-14: the meta.
 constexpr int APPLY_T = 128;              // tracks (= threads) per block
-constexpr int REC_PIECES = KF_REC / 2 + 3;
+constexpr int REC_PIECES = KF_REC / 2 + 3;   // Kalman state + meta: the first 240 B of a record
 
 template <int V>
 __global__ __launch_bounds__(APPLY_T) void k_apply(BtArgs a) {
@@ -923,8 +927,7 @@ __global__ __launch_bounds__(APPLY_T) void k_apply(BtArgs a) {
     // record p / 15, so each wave-instruction writes 1 KiB of rec linearly and consecutive lanes
     // read consecutive pieces of a record.  All 15 are in flight while the decision runs.
     {
-        const double2 *kf2 = reinterpret_cast<const double2 *>(a.kf);
-        const double2 *meta2 = reinterpret_cast<const double2 *>(a.meta);
+        const double2 *rec2 = reinterpret_cast<const double2 *>(a.kf);
         char *ldsb = reinterpret_cast<char *>(&rec[0][0]);
         const int wb = __builtin_amdgcn_readfirstlane(t & ~(WAVE - 1));
 #pragma unroll
@@ -933,7 +936,7 @@ __global__ __launch_bounds__(APPLY_T) void k_apply(BtArgs a) {
             const int r = p / REC_PIECES, k = p - r * REC_PIECES;
             const int rs = s_slot[r < nloc ? r : 0];   // rows past nloc: row 0 again
             const long long sl = tb + (rs < 0 ? 0 : rs);
-            const double2 *src = k < 12 ? kf2 + sl * 12 + k : meta2 + sl * 3 + (k - 12);
+            const double2 *src = rec2 + sl * (TRK_STRIDE / 2) + k;
             if (rs >= 0)   // lazy rows: nothing loaded, their LDS row is never read
                 __builtin_amdgcn_global_load_lds((glob_void *)src,
                                                  (lds_void *)(ldsb + (wb + q * APPLY_T) * 16), 16,
@@ -1058,17 +1061,12 @@ __global__ __launch_bounds__(APPLY_T) void k_apply(BtArgs a) {
     }
     __syncthreads();
     // cooperative store of what changed
-    double2 *kfw = reinterpret_cast<double2 *>(a.kf);
-    double2 *metaw = reinterpret_cast<double2 *>(a.meta);
+    double2 *recw = reinterpret_cast<double2 *>(a.kf);
     for (int p = t; p < nloc * REC_PIECES; p += APPLY_T) {
         const int r = p / REC_PIECES, k = p - r * REC_PIECES;
         const int wm = s_wmask[r];
         const long long sl = tb + s_slot[r];
-        if (k < 12) {
-            if (wm & 1) kfw[sl * 12 + k] = rec[r][k];
-        } else if (wm & 2) {
-            metaw[sl * 3 + (k - 12)] = rec[r][k];
-        }
+        if (k < 12 ? (wm & 1) : (wm & 2)) recw[sl * (TRK_STRIDE / 2) + k] = rec[r][k];
     }
 }
 
@@ -1162,7 +1160,7 @@ __host__ __device__ inline long long dedup_arena_bytes(long long n) {
 }
 
 __device__ __forceinline__ int track_age(const BtArgs &a, long long slot) {
-    return a.meta[slot].frame_id - a.meta[slot].start_frame;   // STrack.end_frame - start_frame
+    return bt_meta(a, slot).frame_id - bt_meta(a, slot).start_frame;   // end_frame - start_frame
 }
 
 // Every pass issues all of a thread's loads before using any (block_compact_ld, batched_for):
@@ -1230,7 +1228,7 @@ __device__ __forceinline__ void finish_body(const BtArgs &a, int s, unsigned *bi
             m.start_frame = fid;
             m.tracklet_len = 0;
             m.pad = 0;
-            a.meta[tb + slot] = m;
+            bt_meta(a, tb + slot) = m;
         });
     int n_births = n_births_all;
     if (n_births > n_free) {
@@ -1258,7 +1256,7 @@ __device__ __forceinline__ void finish_body(const BtArgs &a, int s, unsigned *bi
         [&](int, int sl) {
             LostAge v;
             v.slot = tb + sl;
-            v.frame = a.meta[v.slot].frame_id;
+            v.frame = bt_meta(a, v.slot).frame_id;
             v.flags = a.flags[v.slot];
             return v;
         },
@@ -1326,7 +1324,7 @@ __device__ __forceinline__ void finish_body(const BtArgs &a, int s, unsigned *bi
         auto lmean_of = [&](int slot_local) {
             LostMean v;
             const long long slot = tb + slot_local;
-            const double2 *src = reinterpret_cast<const double2 *>(a.kf + slot * KF_REC);
+            const double2 *src = reinterpret_cast<const double2 *>(a.kf + slot * TRK_STRIDE);
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 const double2 x = src[k];
@@ -1445,7 +1443,7 @@ __device__ __forceinline__ void finish_body(const BtArgs &a, int s, unsigned *bi
             const long long slot = tb + (os_arena ? outslot[pos] : a.t2[tb + pos]);
             Row r;
             r.b = kf_box<V>(a.kf, slot);
-            r.m = a.meta[slot];
+            r.m = bt_meta(a, slot);
             return r;
         },
         [&](int pos, const Row &r) {
@@ -1672,7 +1670,7 @@ int bt_alloc(yta_bytetrack *e) {
         a.max_time_lost = (int)(e->prm.frame_rate / 30.0 * e->prm.track_buffer); // :128-129
         a.D = 0;
     }
-    DALLOC(a.kf, S * CAP * KF_REC);
+    DALLOC(a.kf, S * CAP * TRK_STRIDE);
     if (e->variant == VAR_BOTSORT) {
         DALLOC(a.kfx, S * CAP * 16);
         DALLOC(e->d_warp, S * 6);
@@ -1685,7 +1683,6 @@ int bt_alloc(yta_bytetrack *e) {
         YTA_HIP(hipMemcpy(e->d_warp_id, id.data(), sizeof(double) * 6 * S, hipMemcpyHostToDevice));
         a.warp = e->d_warp_id;
     }
-    DALLOC(a.meta, S * CAP);
     DALLOC(a.flags, S * CAP);
     DALLOC(a.kf_frame, S * CAP);
     DALLOC(a.tracked, S * CAP);
@@ -1885,10 +1882,10 @@ int reserve(yta_bytetrack *e, int cap, int maxd) {
                                  e->stream));
         return YTA_OK;
     };
-    if (!rc) rc = copy2d(n->a.kf, nc * KF_REC * 8, e->a.kf, oc * KF_REC * 8, oc * KF_REC * 8, S);
+    if (!rc)
+        rc = copy2d(n->a.kf, nc * TRK_STRIDE * 8, e->a.kf, oc * TRK_STRIDE * 8,
+                    oc * TRK_STRIDE * 8, S);
     if (!rc && e->a.kfx) rc = copy2d(n->a.kfx, nc * 16 * 8, e->a.kfx, oc * 16 * 8, oc * 16 * 8, S);
-    if (!rc) rc = copy2d(n->a.meta, nc * sizeof(TrackMeta), e->a.meta, oc * sizeof(TrackMeta),
-                         oc * sizeof(TrackMeta), S);
     if (!rc) rc = copy2d(n->a.flags, nc * 4, e->a.flags, oc * 4, oc * 4, S);
     if (!rc) rc = copy2d(n->a.kf_frame, nc * 4, e->a.kf_frame, oc * 4, oc * 4, S);
     if (!rc && e->a.cls_hist)
@@ -2227,7 +2224,8 @@ int yta_bytetrack_reset(yta_bytetrack *e) {
     YTA_HIP(hipSetDevice(e->device));
     hipLaunchKernelGGL(k_reset, dim3(e->S), dim3(256), 0, e->stream, e->a);
     YTA_HIP(hipGetLastError());
-    YTA_HIP(hipMemsetAsync(e->a.meta, 0, sizeof(TrackMeta) * (size_t)e->S * e->CAP, e->stream));
+    YTA_HIP(hipMemsetAsync(e->a.kf, 0, sizeof(double) * TRK_STRIDE * (size_t)e->S * e->CAP,
+                           e->stream));
     YTA_HIP(hipMemsetAsync(e->a.flags, 0, sizeof(int) * (size_t)e->S * e->CAP, e->stream));
     YTA_HIP(host_wait(e->stream));
     memset(e->h_cnt, 0, sizeof(BtCounters) * e->S);
@@ -2275,18 +2273,15 @@ int yta_bytetrack_get_state(yta_bytetrack *e, int stream, int *n_tracks, long lo
     const BtCounters c = e->h_cnt[stream];
     const long long tb = (long long)stream * e->CAP;
     std::vector<int> tr(c.n_tracked), lo(c.n_lost);
-    std::vector<double> kf((size_t)e->CAP * KF_REC);
-    std::vector<TrackMeta> meta(e->CAP);
+    std::vector<double> kf((size_t)e->CAP * TRK_STRIDE);
     std::vector<int> flags(e->CAP);
     if (c.n_tracked)
         YTA_HIP(hipMemcpy(tr.data(), e->a.tracked + tb, sizeof(int) * c.n_tracked,
                           hipMemcpyDeviceToHost));
     if (c.n_lost)
         YTA_HIP(hipMemcpy(lo.data(), e->a.lost + tb, sizeof(int) * c.n_lost, hipMemcpyDeviceToHost));
-    YTA_HIP(hipMemcpy(kf.data(), e->a.kf + tb * KF_REC, sizeof(double) * KF_REC * e->CAP,
-                      hipMemcpyDeviceToHost));
-    YTA_HIP(hipMemcpy(meta.data(), e->a.meta + tb, sizeof(TrackMeta) * e->CAP,
-                      hipMemcpyDeviceToHost));
+    YTA_HIP(hipMemcpy(kf.data(), e->a.kf + tb * TRK_STRIDE,
+                      sizeof(double) * TRK_STRIDE * e->CAP, hipMemcpyDeviceToHost));
     YTA_HIP(hipMemcpy(flags.data(), e->a.flags + tb, sizeof(int) * e->CAP, hipMemcpyDeviceToHost));
     std::vector<int> kf_frame(e->CAP);
     YTA_HIP(hipMemcpy(kf_frame.data(), e->a.kf_frame + tb, sizeof(int) * e->CAP,
@@ -2299,7 +2294,8 @@ int yta_bytetrack_get_state(yta_bytetrack *e, int stream, int *n_tracks, long lo
     for (int which = 0; which < 2; ++which) {
         const std::vector<int> &lst = which ? lo : tr;
         for (int slot : lst) {
-            const TrackMeta &m = meta[slot];
+            TrackMeta m;
+            memcpy(&m, kf.data() + (size_t)slot * TRK_STRIDE + TRK_META, sizeof(TrackMeta));
             long long *ii = ints + (long long)n * 7;
             ii[0] = which;
             ii[1] = m.id;
@@ -2309,8 +2305,8 @@ int yta_bytetrack_get_state(yta_bytetrack *e, int stream, int *n_tracks, long lo
             ii[5] = m.start_frame;
             ii[6] = m.tracklet_len;
             KfState st;
-            memcpy(st.m, kf.data() + (size_t)slot * KF_REC, sizeof(double) * 8);
-            memcpy(st.c, kf.data() + (size_t)slot * KF_REC + 8, sizeof(double) * 16);
+            memcpy(st.m, kf.data() + (size_t)slot * TRK_STRIDE, sizeof(double) * 8);
+            memcpy(st.c, kf.data() + (size_t)slot * TRK_STRIDE + 8, sizeof(double) * 16);
             if (e->variant == VAR_BYTETRACK && which)   // lost list: lazily predicted
                 kf_predict_lost(st, c.frame_id - kf_frame[slot]);
             for (int k = 0; k < 8; ++k) mean[(long long)n * 8 + k] = st.m[k];
@@ -2434,9 +2430,6 @@ int yta_botsort_get_features(yta_botsort *e, int stream, int *n_tracks, float *f
     if (c.n_lost)
         YTA_HIP(hipMemcpy(lst.data() + c.n_tracked, e->a.lost + tb, sizeof(int) * c.n_lost,
                           hipMemcpyDeviceToHost));
-    std::vector<TrackMeta> meta(e->CAP);
-    YTA_HIP(hipMemcpy(meta.data(), e->a.meta + tb, sizeof(TrackMeta) * e->CAP,
-                      hipMemcpyDeviceToHost));
     const int D = e->D;
     int n = 0;
     for (int slot : lst) {
@@ -2446,7 +2439,12 @@ int yta_botsort_get_features(yta_botsort *e, int stream, int *n_tracks, float *f
         if (cls_hist)
             YTA_HIP(hipMemcpy(cls_hist + (long long)n * CLS_K * 2, e->a.cls_hist + (tb + slot) * CLS_K,
                               sizeof(double2) * CLS_K, hipMemcpyDeviceToHost));
-        if (n_cls) n_cls[n] = meta[slot].n_cls;
+        if (n_cls) {
+            TrackMeta m;
+            YTA_HIP(hipMemcpy(&m, e->a.kf + (tb + slot) * TRK_STRIDE + TRK_META, sizeof(TrackMeta),
+                              hipMemcpyDeviceToHost));
+            n_cls[n] = m.n_cls;
+        }
         ++n;
     }
     *n_tracks = n;

@@ -28,6 +28,12 @@ struct TrackMeta {                   // 48 B, one per slot
 
 static_assert(sizeof(TrackMeta) == 48, "TrackMeta layout");
 
+// One 256-B record per slot: the Kalman state (KF_REC = 24 f64) then the meta (6 f64), padded so
+// that a record is exactly two aligned 128-B lines (a 192-B record alone straddles a third line
+// half of the time, a separate 48-B meta costs a line of its own).
+constexpr int TRK_STRIDE = 32;       // doubles per slot
+constexpr int TRK_META = KF_REC;     // offset of the meta in a record (doubles)
+
 struct BtCounters {                  // one per stream, 128 B
     long long next_id;               // last issued track id (BaseTrack._count)
     int frame_id;
@@ -69,10 +75,9 @@ struct BtArgs {
     const double *det_in;     // packed rows of 6
     const int *det_off;       // S+1
     // persistent state
-    double *kf;               // [S*CAP][KF_REC]
+    double *kf;               // [S*CAP][TRK_STRIDE]: Kalman state + TrackMeta per slot
     double *kfx;              // BoT-SORT: [S*CAP][16] covariance cross terms (kf_xyah.hpp, FL_CROSS)
     const double *warp;       // BoT-SORT: [S][6] this frame's camera warps (multi_gmc), row-major 2x3
-    TrackMeta *meta;          // [S*CAP]
     int *flags;               // [S*CAP] state + FL_* bits, dense: every list scan reads these
     int *kf_frame;            // [S*CAP] ByteTrack, Lost tracks: the frame their stored Kalman
                               // state belongs to (later predicts replayed lazily, kf_xyah.hpp)
