@@ -140,21 +140,7 @@ __device__ __forceinline__ bool stage1_body(const BtArgs &a, int s, Arena &ar, S
     const int2 hs = block_compact2(
         nd, wsum,
         [&](int i) {
-            const double *d = din + (long long)i * 6;
-            double xywh[4];
-            det_xyxy_to_xywh(d, xywh);
-            double *z = a.det_xyah + (db + i) * 4;
-            if (V == VAR_BOTSORT) {
-                z[0] = xywh[0];
-                z[1] = xywh[1];
-                z[2] = xywh[2];
-                z[3] = xywh[3];
-            } else {
-                xywh_to_xyah(xywh, z);
-            }
-            const double conf = d[4];
-            a.det_conf[db + i] = conf;
-            a.det_cls[db + i] = d[5];
+            const double conf = din[(long long)i * 6 + 4];
             // byte_tracker.py:149-158 (low bound 0.1) / bot_sort.py:263-269 (track_low_thresh)
             return conf > thr ? 1 : (conf > a.low_thresh && conf < thr ? 2 : 0);
         },
@@ -475,13 +461,9 @@ __global__ __launch_bounds__(PREP_T) void k_s1_prep(BtArgs a) {
                 return r;
             },
             [&](int i, const DetRow &r) {
-                const long long q = db + c0 + i;
                 double xywh[4];
                 det_xyxy_to_xywh(r.v, xywh);
-                xywh_to_xyah(xywh, a.det_xyah + q * 4);
                 const double conf = r.v[4];
-                a.det_conf[q] = conf;
-                a.det_cls[q] = r.v[5];
                 sh.u.d.cat[i] = conf > thr ? 1 : (conf > a.low_thresh && conf < thr ? 2 : 0);
                 sh.u.d.box[i] = xywh_to_box(xywh);
                 sh.u.d.conf[i] = conf;
@@ -856,20 +838,48 @@ __device__ __forceinline__ double vote_cls(double2 *h, int &n, double cls, doubl
     return out;
 }
 
+// A detection's Kalman measurement (ByteTrack xyah, BoT-SORT xywh: STrack's conversions,
+// ops.py:7-97), confidence and class, computed from its input row where a track takes it (one
+// 48-B row instead of three per-detection arrays written by the detection pass and gathered back).
+struct DetMeas {
+    double z[4];
+    double conf, cls;
+};
+template <int V>
+__device__ __forceinline__ DetMeas det_meas(const BtArgs &a, int s, int d) {
+    const double *r = a.det_in + ((long long)a.det_off[s] + d) * 6;
+    double v[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) v[k] = r[k];
+    DetMeas m;
+    double xywh[4];
+    det_xyxy_to_xywh(v, xywh);
+    if (V == VAR_BOTSORT) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) m.z[k] = xywh[k];
+    } else {
+        xywh_to_xyah(xywh, m.z);
+    }
+    m.conf = v[4];
+    m.cls = v[5];
+    return m;
+}
+
 // STrack.update / re_activate (byte_tracker.py:70-98; bot_sort.py:125-170) minus the feature EMA
 // (k_ema)
 template <int V>
 __device__ __forceinline__ void take_detection(const BtArgs &a, KfState &st, TrackMeta &m,
-                                               int &flags, long long det, int det_local, int fid,
-                                               long long slot, int *err, double *xc = nullptr) {
-    if (V == VAR_BOTSORT && xc) kf_update_x(st, xc, a.det_xyah + det * 4);   // warped track
-    else kf_update<kf_model<V>()>(st, a.det_xyah + det * 4);
+                                               int &flags, const DetMeas &dm, int det_local,
+                                               int fid, long long slot, int *err,
+                                               double *xc = nullptr) {
+    if (V == VAR_BOTSORT && xc) kf_update_x(st, xc, dm.z);   // warped track
+    else kf_update<kf_model<V>()>(st, dm.z);
     const bool reactivate = st_of(flags) != ST_TRACKED;
     m.tracklet_len = reactivate ? 0 : m.tracklet_len + 1;
     flags = (flags & ~FL_STATE) | ST_TRACKED | FL_ACTIVATED;
     m.frame_id = fid;
-    m.score = a.det_conf[det];
-    m.cls = a.det_cls[det];
+    m.score = dm.conf;
+    m.cls = dm.cls;
     m.det_ind = det_local;
     if (V == VAR_BOTSORT) m.cls = vote_cls(a.cls_hist + slot * CLS_K, m.n_cls, m.cls, m.score, err);
 }
@@ -947,6 +957,7 @@ __global__ __launch_bounds__(APPLY_T) void k_apply(BtArgs a) {
     // act: 0 predict only, 1 predict + stage-1 update, 2 predict + stage-2 update, 3 predict +
     // mark lost, 4 update (unconfirmed, stage 3), 5 remove (unconfirmed)
     int det = -1, act = 0, hpos = -1;
+    DetMeas dm{};
     if (live) {
         if (in_pool) {
             if (h >= 0) {                                            // stage 1 (:188-196)
@@ -970,6 +981,7 @@ __global__ __launch_bounds__(APPLY_T) void k_apply(BtArgs a) {
         }
         // BoT-SORT: tracks taking a high detection also take its feature (k_ema)
         if (V == VAR_BOTSORT && a.D > 0) a.ema_job[tb + i] = hpos;
+        if (det >= 0) dm = det_meas<V>(a, s, det);   // in flight beside the records
         // pieces this track rewrites: bit 0 the Kalman record, bit 1 the meta
         s_wmask[t] = act == 5 ? 0 : (act == 1 || act == 2 || act == 4 ? 3 : 1);
     }
@@ -1023,7 +1035,7 @@ __global__ __launch_bounds__(APPLY_T) void k_apply(BtArgs a) {
             }
             wmask = 1;
             if (act == 1 || act == 2) {
-                take_detection<V>(a, st, m, flags, db + det, det, fid, tb + slot, &c->err,
+                take_detection<V>(a, st, m, flags, dm, det, fid, tb + slot, &c->err,
                                   cross ? xc : nullptr);
                 wmask = 3;
             } else if (act == 3) {
@@ -1038,7 +1050,7 @@ __global__ __launch_bounds__(APPLY_T) void k_apply(BtArgs a) {
 #pragma unroll
             for (int k = 0; k < 16; ++k) st.c[k] = row[8 + k];
             if (V == VAR_BOTSORT && gmc) kf_gmc(st, xc, H);        // unconfirmed: warped only
-            take_detection<V>(a, st, m, flags, db + det, det, fid, tb + slot, &c->err,
+            take_detection<V>(a, st, m, flags, dm, det, fid, tb + slot, &c->err,
                               cross ? xc : nullptr);
             wmask = 3;
         } else {
@@ -1210,12 +1222,13 @@ __device__ __forceinline__ void finish_body(const BtArgs &a, int s, unsigned *bi
             if (b >= n_free) return;   // capacity (flagged below)
             const int slot = a.free_list[tb + b];
             const int d = r.det;
+            const DetMeas dm = det_meas<V>(a, s, d);
             KfState st;
-            kf_initiate<kf_model<V>()>(a.det_xyah + (db + d) * 4, st);
+            kf_initiate<kf_model<V>()>(dm.z, st);
             store_kf(a.kf, tb + slot, st);
             TrackMeta m;
-            m.score = a.det_conf[db + d];
-            m.cls = a.det_cls[db + d];
+            m.score = dm.conf;
+            m.cls = dm.cls;
             m.id = next_id + 1 + b;
             m.det_ind = d;
             m.n_cls = 0;
@@ -1689,9 +1702,6 @@ int bt_alloc(yta_bytetrack *e) {
     DALLOC(a.lost, S * CAP);
     DALLOC(a.free_list, S * CAP);
     DALLOC(a.cnt, S);
-    DALLOC(a.det_xyah, S * MAXD * 4);
-    DALLOC(a.det_conf, S * MAXD);
-    DALLOC(a.det_cls, S * MAXD);
     DALLOC(a.high, S * MAXD);
     DALLOC(a.second, S * MAXD);
     DALLOC(a.rest, S * MAXD);

@@ -84,8 +84,6 @@ struct BtArgs {
     int *tracked, *lost, *free_list;   // [S*CAP]
     BtCounters *cnt;          // [S]
     // per-frame: detections [S*MAXD]
-    double *det_xyah;         // [S*MAXD][4] Kalman measurement (ByteTrack xyah, BoT-SORT xywh)
-    double *det_conf, *det_cls;
     int *high, *second, *rest, *birth;
     Box *high_box, *second_box;
     double *high_score, *rest_score;
