@@ -62,15 +62,19 @@ def kernel_bytes(phase, st):
         return pool * (4 + 4) + st["edges1"] * 12 + high * 4
     if phase == "apply":
         # every pool / unconfirmed track but the lazily predicted lost ones: Kalman record + meta
-        # read, record written; matched tracks: meta written, the detection's xyah / conf / cls
-        # read; every pool item: index + stage results read, stage-1 kind written
+        # read, record written; matched tracks: meta written, the detection's row read; every
+        # pool item: index + stage results read, stage-1 kind written
         touched = pool - lazy + unc
         return touched * (192 + 48 + 192) + matched * (48 + 48) + pool * (4 + 4 + 4 + 4) + unc * 8
     if phase == "stage23":
         return (pool * (4 + 48 + 4) + high * (4 + 8 + 8) + st["left"] * (8 + 32 + 4)
                 + st["second"] * (32 + 4) + unc * (32 + 4) + st["rest"] * (4 + 32 + 8 + 4))
     if phase == "finish":
-        return (st["t2"] + st["l2"]) * (32 + 48 + 12) + st["out"] * 64 + st["births"] * (192 + 48)
+        # lost list expiry (slot, flags, lost frame); tracked' boxes (mean), lost' means (lazily
+        # predicted) for duplicate removal, list entries; output rows: mean + meta read, row
+        # written; births: record + meta written
+        return (lost_list * 12 + st["t2"] * (32 + 12) + st["l2"] * (64 + 4 + 12)
+                + st["out"] * (32 + 48 + 64) + st["births"] * (192 + 48))
     return 0
 
 

@@ -1269,11 +1269,13 @@ __device__ __forceinline__ void finish_body(const BtArgs &a, int s, unsigned *bi
         [&](int, int sl) {
             LostAge v;
             v.slot = tb + sl;
-            v.frame = bt_meta(a, v.slot).frame_id;
+            v.frame = V == VAR_BYTETRACK ? a.kf_frame[v.slot] - 1 : bt_meta(a, v.slot).frame_id;
             v.flags = a.flags[v.slot];
             return v;
         },
-        [&](int, const LostAge &v) {
+        [&](int, const LostAge &v0) {
+            LostAge v = v0;
+            if (V == VAR_BYTETRACK && st_of(v.flags) == ST_TRACKED) v.frame = fid;
             if (fid - v.frame > a.max_time_lost)
                 a.flags[v.slot] = (v.flags & ~FL_STATE) | ST_REMOVED | FL_REMOVED_NOW;
         });
