@@ -28,7 +28,7 @@ sys.path.insert(0, REPO)
 
 PHASES = ["s1_prep", "s1_edges", "s1_lap", "stage23", "apply", "finish"]
 STATS = ["dets", "high", "second", "pool", "act", "unc", "left", "rest", "births", "t2", "l2",
-         "tracked", "lost", "out", "edges1", "edges23", "fallback1", "fallback23", "lazy"]
+         "tracked", "lost", "out", "edges1", "edges23", "fallback1", "fallback23", "lazy", "res1"]
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # Canonical algorithmic bytes per update: ByteTrack 1024 x 1024
 BYTES_PER_UPDATE_1024 = 19_259_392
@@ -55,11 +55,12 @@ def kernel_bytes(phase, st):
                 + (act + unc) * (4 + 4 + 64 + 4 + 32) + lost_list * (4 + 4 + 4 + 64 + 4 + 32))
     if phase == "s1_edges":
         # high boxes + scores read once (grid built in LDS), every pool box read, edge count and
-        # edges written
-        return high * (32 + 8) + pool * (32 + 4) + st["edges1"] * 12
+        # edges written, single-edge matches: x1 of every pool row, y1 of every high detection
+        return high * (32 + 8 + 4) + pool * (32 + 4 + 4) + st["edges1"] * 12
     if phase == "s1_lap":
-        # edge counts and edges read, the assignment written (row and column results)
-        return pool * (4 + 4) + st["edges1"] * 12 + high * 4
+        # edge counts and the edges left after the single-edge components read, the solver's
+        # matches written
+        return pool * 4 + st["res1"] * (12 + 8)
     if phase == "apply":
         # every pool / unconfirmed track but the lazily predicted lost ones: Kalman record + meta
         # read, record written; matched tracks: meta written, the detection's row read; every

@@ -177,7 +177,8 @@ int yta_bytetrack_profile_collect(yta_bytetrack *engine, double *ms, int *frames
  * unconfirmed, leftovers, rest, births, tracked', lost', tracked, lost, output rows, stage-1
  * candidate edges, stage-2+3 candidate edges, then the cumulative number of stream-frames whose
  * stage-1 / stage-2+3 association did not fit in LDS and ran over global memory, then (ByteTrack)
- * the lost-list Kalman records the last frame left untouched (lazy prediction) (19 int64). */
+ * the lost-list Kalman records the last frame left untouched (lazy prediction), then (ByteTrack)
+ * the stage-1 candidate edges left to the solver after the single-edge components (20 int64). */
 int yta_bytetrack_stats(yta_bytetrack *engine, long long *stats);
 /* Tuning / testing: bytes of LDS the association kernels may use per stream (default 150 KiB,
  * at most 150 KiB); a stream-frame that does not fit runs over global memory.  0 forces the

@@ -26,23 +26,26 @@ STAGE1 = {2: "dets pass", 4: "tracked/lost pass",
           14: "lap solve"}
 
 
-def build():
-    os.makedirs(os.path.dirname(OUT), exist_ok=True)
+def build(out=OUT, extra=()):
+    os.makedirs(os.path.dirname(out), exist_ok=True)
     mk = open(os.path.join(CSRC, "Makefile")).read()   # every source the product builds
     names = next(l for l in mk.splitlines() if l.startswith("SRCS")).split("=", 1)[1].split()
     srcs = [os.path.join(CSRC, f) for f in names]
     cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC",
            "-ffp-contract=off", "-fno-fast-math", "-munsafe-fp-atomics", "-DYTA_STAMPS",
-           "-shared", "-o", OUT] + srcs
+           *extra, "-shared", "-o", out] + srcs
     subprocess.check_call(cmd)
-    print("built", OUT)
+    print("built", out)
 
 
 def show(st, base, names, title):
     t0 = st[base]
     print(f"-- {title} (block 0)")
     prev = t0
-    for k in sorted(names):
+    keys = names if isinstance(names, list) else sorted(names)
+    names = dict(names) if isinstance(names, list) else names
+    keys = [k for k, _ in keys] if keys and isinstance(keys[0], tuple) else keys
+    for k in keys:
         v = st[base + k]
         if v == 0 or v < prev:
             continue
@@ -55,13 +58,15 @@ def main():
     ap.add_argument("--build", action="store_true")
     ap.add_argument("--streams", type=int, default=256)
     ap.add_argument("--frames", type=int, default=6)
+    ap.add_argument("--lib", default=OUT, help="diagnostic library to build / load")
+    ap.add_argument("--flags", default="", help="extra compile flags (build)")
     args = ap.parse_args()
     if args.build:
-        build()
+        build(args.lib, args.flags.split())
         return
     from yolo_tracking_amd import _lib
     from yolo_tracking_amd.synth import make_frames
-    lib = _lib.load_library(OUT)
+    lib = _lib.load_library(args.lib)
     lib.yta_debug_stamps.argtypes = [ctypes.c_void_p]
     lib.yta_debug_stamps.restype = ctypes.c_int
     _lib._lib = lib
@@ -75,8 +80,17 @@ def main():
     _lib.check(lib.yta_debug_stamps(st.ctypes.data))
     st = st.astype(np.int64)
     print("stats", eng.stats())
-    show(st, 0, STAGE1, "k_stage1")
-    print("  stage-1 LAP: n16 %d n64 %d nbig %d edges %d complex nodes %d" % tuple(st[15:20]))
+    if st[60]:   # ByteTrack: stage 1 as k_s1_prep / k_s1_edges / k_s1_lap
+        show(st, 60, {1: "dets pass", 2: "tracked pass", 3: "lost pass"}, "k_s1_prep")
+        show(st, 66, {1: "grid build", 2: "edges"}, "k_s1_edges")
+        show(st, 90, [(1, "row offsets"), (2, "CSR fill"), (8, "lap init"), (9, "lap P1 union"),
+                      (10, "lap P2 roots"), (11, "lap P3 lists"), (12, "lap P4 gather"),
+                      (13, "lap classify"), (14, "lap solve"), (3, "lap return"),
+                      (4, "results out")], "k_s1_lap")
+        print("  stage-1 LAP: n16 %d n64 %d nbig %d edges %d complex nodes %d" % tuple(st[105:110]))
+    else:
+        show(st, 0, STAGE1, "k_stage1")
+        print("  stage-1 LAP: n16 %d n64 %d nbig %d edges %d complex nodes %d" % tuple(st[15:20]))
     show(st, 20, {4: "left/rest lists", **{k: v for k, v in STAGE1.items() if k >= 5}},
          "k_stage23 stage 2")
     show(st, 40, {k: v for k, v in STAGE1.items() if k >= 5}, "k_stage23 stage 3")
@@ -85,6 +99,24 @@ def main():
          "k_finish")
     show(st, 110, {1: "reduce", 2: "zero cells", 3: "count", 5: "cell scan", 6: "scatter"},
          "grid_build (last call)")
+    # per-block timeline of the last frame's block/stream kernels
+    blk = np.zeros(8 * 4096 * 2, dtype=np.uint64)
+    lib.yta_debug_blocks.argtypes = [ctypes.c_void_p]
+    _lib.check(lib.yta_debug_blocks(blk.ctypes.data))
+    blk = blk.reshape(8, 4096, 2).astype(np.int64)[:, :S]
+    print("-- per-block timeline (us; start relative to the kernel's first block start)")
+    for k, name in [(0, "k_s1_prep"), (1, "k_s1_edges"), (2, "k_s1_lap"), (3, "k_stage23"),
+                    (5, "k_finish")]:
+        b0, b1 = blk[k, :, 0], blk[k, :, 1]
+        if not b0.any():
+            continue
+        st0 = (b0 - b0.min()) / 100.0
+        dur = (b1 - b0) / 100.0
+        span = (b1.max() - b0.min()) / 100.0
+        q = np.percentile(dur, [50, 90, 100])
+        print(f"  {name:<11s} span {span:7.2f}  block dur p50 {q[0]:6.2f} p90 {q[1]:6.2f} max "
+              f"{q[2]:6.2f}  starts: <2us {int((st0 < 2).sum())}, p50 {np.median(st0):6.2f}, "
+              f"max {st0.max():6.2f}  slowest block {int(dur.argmax())}")
 
 
 if __name__ == "__main__":

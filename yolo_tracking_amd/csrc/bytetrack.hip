@@ -254,6 +254,7 @@ __device__ __forceinline__ bool stage1_body(const BtArgs &a, int s, Arena &ar, S
         c->n_rest = 0;
         c->n_births = 0;
         c->n_lazy = 0;
+        c->n_res1 = 0;
     }
     return true;
 }
@@ -345,9 +346,13 @@ __global__ __launch_bounds__(BLK23) void k_stage23(BtArgs a) {
     const int s = blockIdx.x;
     YTA_STAMP_BASE(20);
     YTA_STAMP(0);
+    YTA_BLK(3, 0);
     {
         Arena ar(smem, a.lds_bytes23);
-        if (stage23_body<V>(a, s, ar, sh)) return;
+        if (stage23_body<V>(a, s, ar, sh)) {
+            YTA_BLK(3, 1);
+            return;
+        }
     }
     block_sync();
     if (threadIdx.x == 0) a.cnt[s].n_fallback[1] += 1;
@@ -436,6 +441,7 @@ __global__ __launch_bounds__(PREP_T) void k_s1_prep(BtArgs a) {
     const int s = blockIdx.x, t = threadIdx.x;
     YTA_STAMP_BASE(60);
     YTA_STAMP(0);
+    YTA_BLK(0, 0);
     BtCounters *c = a.cnt + s;
     const long long db = (long long)s * a.MAXD, tb = (long long)s * a.CAP;
     int nd = a.det_off[s + 1] - a.det_off[s];
@@ -548,8 +554,10 @@ __global__ __launch_bounds__(PREP_T) void k_s1_prep(BtArgs a) {
         c->n_rest = 0;
         c->n_births = 0;
         c->n_lazy = 0;
+        c->n_res1 = 0;
     }
     YTA_STAMP(3);
+    YTA_BLK(0, 1);
 }
 
 // Every candidate edge of pool row box rb: f(high position, fused IoU cost) for cost <
@@ -584,10 +592,12 @@ __host__ __device__ inline long long s1_grid_bytes(long long C) {
 
 // k_s1_edges body over a grid whose storage (LDS or HBM) the caller fixed: inlined once per
 // storage so that every grid access compiles to ds_* or global_* instructions, not flat ones.
+// cdeg[nc]: every high detection's candidate-edge count (column degree), zeroed by the caller.
 template <typename HBox, typename HW>
 __device__ __forceinline__ void s1_edges_body(const BtArgs &a, int s, int nc, int nr,
                                               const GridView &gv, HBox hbox, HW hw,
-                                              GridScratch &gs, int *wsum, int &spill) {
+                                              GridScratch &gs, int *wsum, int &spill, int *cdeg,
+                                              int &n_edges, int (&rn)[4], int (&rc)[4]) {
     const int t = threadIdx.x, nt = blockDim.x;
     const long long tb = (long long)s * a.CAP, SC = (long long)a.S * a.CAP;
     grid_build(nc, hbox, hw, gv, gs, wsum);
@@ -603,17 +613,59 @@ __device__ __forceinline__ void s1_edges_body(const BtArgs &a, int s, int nc, in
         for (int b = 0; b < 4; ++b) {
             const int i = base + b * nt;
             if (i >= nr) continue;
-            int n = 0;
+            int n = 0, first = -1;
             s1_row_edges(a, s, gv, h, rb[b], [&](int j, double cost) {
+                if (n == 0) first = j;
                 if (n < E_SLOTS) {
                     a.e_col[n * SC + tb + i] = j;
                     a.e_cost[n * SC + tb + i] = cost;
                 }
                 ++n;
+                atomicAdd(cdeg + j, 1);
             });
             a.e_cnt[tb + i] = n;
             if (n > E_SLOTS) spill = 1;
+            if (n) atomicAdd(&n_edges, n);
+            if (base == t) {   // rows t + b * nt: kept for the single-edge pass
+                rn[b] = n;
+                rc[b] = n == 1 ? first : -1;
+            }
         }
+    }
+}
+
+// Single-edge components (a pool row whose only candidate edge goes to a high detection no other
+// row reaches) are matched outright here, as lap_block's P1 would (lapjv with cost_limit takes an
+// isolated pair with cost < thresh): x1 / y1 get them and -1 elsewhere, the row's edge count
+// becomes 0, and k_s1_lap solves what is left (about half of the edges at 1024 x 1024), with a
+// smaller LDS arena.  Removing a whole component leaves every other node's degree as it was.
+__device__ __forceinline__ void s1_single_edges(const BtArgs &a, int s, int nc, int nr, int *cdeg,
+                                                bool lds, const int (&rn)[4], const int (&rc)[4]) {
+    const int t = threadIdx.x, nt = blockDim.x;
+    const long long tb = (long long)s * a.CAP, db = (long long)s * a.MAXD;
+    if (lds) lds_sync();
+    else block_sync();
+    auto row = [&](int i, int n, int c) {   // rows i = t mod nt: this thread found their edges
+        int x = -1;
+        if (n == 1 && ald(cdeg + c) == 1) {
+            x = c;
+            cdeg[c] = ~i;   // the column's only row
+            a.e_cnt[tb + i] = 0;
+        }
+        a.x1[tb + i] = x;
+    };
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+        if (t + b * nt < nr) row(t + b * nt, rn[b], rc[b]);
+    for (int i = t + 4 * nt; i < nr; i += nt) {
+        const int n = a.e_cnt[tb + i];
+        row(i, n, n == 1 ? a.e_col[tb + i] : -1);
+    }
+    if (lds) lds_sync();
+    else block_sync();
+    for (int j = t; j < nc; j += nt) {
+        const int d = ald(cdeg + j);
+        a.y1[db + j] = d < 0 ? ~d : -1;
     }
 }
 
@@ -621,11 +673,12 @@ __global__ __launch_bounds__(BLKE) void k_s1_edges(BtArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     __shared__ GridScratch gs;
     __shared__ int wsum[32];
-    __shared__ int spill;
+    __shared__ int spill, n_edges;
     const int s = blockIdx.x, t = threadIdx.x, nt = blockDim.x;
     YTA_STAMP_BASE(66);
     YTA_STAMP(0);
-    const BtCounters *c = a.cnt + s;
+    YTA_BLK(1, 0);
+    BtCounters *c = a.cnt + s;
     const long long db = (long long)s * a.MAXD;
     const int nc = c->n_high, nr = c->n_pool;
     // this thread's detections t and t + blockDim held in registers (nc <= 2 blockDim: every box
@@ -640,11 +693,21 @@ __global__ __launch_bounds__(BLKE) void k_s1_edges(BtArgs a) {
         hb1 = a.high_box[db + t + nt];
         hw1 = a.high_score[db + t + nt];
     }
-    if (t == 0) spill = 0;
-    if (nc > 2 * nt || s1_grid_bytes(nc) > (long long)a.lds_bytes_e) {   // grid built in HBM
+    if (t == 0) {
+        spill = 0;
+        n_edges = 0;
+    }
+    int rn[4] = {0, 0, 0, 0}, rc[4] = {-1, -1, -1, -1};   // rows t + b * nt (s1_single_edges)
+    if (nc > 2 * nt || s1_grid_bytes(nc) + 4LL * nc > (long long)a.lds_bytes_e) {   // HBM grid
+        int *cdeg = a.g_deg + db;
+        for (int j = t; j < nc; j += nt) cdeg[j] = 0;
+        block_sync();
         s1_edges_body(
             a, s, nc, nr, s1_grid_hbm(a, s), [&](int j) { return a.high_box[db + j]; },
-            [&](int j) { return a.high_score[db + j]; }, gs, wsum, spill);
+            [&](int j) { return a.high_score[db + j]; }, gs, wsum, spill, cdeg, n_edges, rn, rc);
+        s1_single_edges(a, s, nc, nr, cdeg, false, rn, rc);
+        if (t == 0) c->n_edges[0] = n_edges;
+        YTA_BLK(1, 1);
         return;
     }
     // grid_build visits item j only from thread j mod blockDim: a register select, no memory
@@ -658,9 +721,13 @@ __global__ __launch_bounds__(BLKE) void k_s1_edges(BtArgs a) {
     gv.boxes = ar.alloc<Box>(nc);
     gv.w = ar.alloc<double>(nc);
     gv.big = ar.alloc<int>(nc);
-    s1_edges_body(a, s, nc, nr, gv, hbox, hw, gs, wsum, spill);
-    lds_sync();
+    int *cdeg = ar.alloc<int>(nc);
+    for (int j = t; j < nc; j += nt) cdeg[j] = 0;   // grid_build's barriers order these
+    s1_edges_body(a, s, nc, nr, gv, hbox, hw, gs, wsum, spill, cdeg, n_edges, rn, rc);
+    s1_single_edges(a, s, nc, nr, cdeg, true, rn, rc);
+    if (t == 0) c->n_edges[0] = n_edges;
     YTA_STAMP(2);
+    YTA_BLK(1, 1);
     if (!spill) return;
     // some row has more edges than slots: k_s1_lap queries the grid again, from HBM
     const GridHdr h = gs.hdr;
@@ -678,8 +745,7 @@ __global__ __launch_bounds__(BLKE) void k_s1_edges(BtArgs a) {
 
 // Arena bytes that always suffice for s1_lap_body (the global fallback arena's size).
 __host__ __device__ inline long long s1_lap_arena_bytes(long long R, long long C, long long E) {
-    return 4 * (R + C) + 4 * (R + 1) + 4 * C + 12 * E + 4 * (R + C) * 3 + 4 * 6 * (R + C + 1) +
-           16 * 16 + 256;
+    return 4 * (R + 1) + 4 * C + 12 * E + 4 * (R + C) * 3 + 4 * 6 * (R + C + 1) + 16 * 16 + 256;
 }
 
 __device__ __forceinline__ bool s1_lap_body(const BtArgs &a, int s, Arena &ar, LapShared &lsh) {
@@ -690,8 +756,10 @@ __device__ __forceinline__ bool s1_lap_body(const BtArgs &a, int s, Arena &ar, L
     const int nr = c->n_pool, nc = c->n_high;
     YTA_STAMP_BASE(90);
     YTA_STAMP(0);
-    int *X = ar.alloc<int>(nr);
-    int *Y = ar.alloc<int>(nc);
+    // the assignment goes straight to x1 / y1, which k_s1_edges filled with its single-edge
+    // matches and -1 (lap_block only writes the pairs it matches)
+    int *X = a.x1 + tb;
+    int *Y = a.y1 + db;
     int *row_off = ar.alloc_top<int>(nr + 1);
     int *col_deg = ar.alloc_top<int>(nc);
     if (ar.fail) return false;
@@ -781,28 +849,31 @@ __device__ __forceinline__ bool s1_lap_body(const BtArgs &a, int s, Arena &ar, L
     block_sync();
     YTA_STAMP(2);
     if (!lap_block(nr, nc, row_off, csr_col, csr_cost, col_deg, a.match_thresh, X, Y, &c->err, ar,
-                   slab_of(a, s), lsh))
+                   slab_of(a, s), lsh, false))
         return false;
     YTA_STAMP(3);
-    for (int i = t; i < nr; i += nt) a.x1[tb + i] = X[i];
-    for (int j = t; j < nc; j += nt) a.y1[db + j] = Y[j];
-    if (t == 0) c->n_edges[0] = E;
-    YTA_STAMP(4);
+    if (t == 0) c->n_res1 = E;   // edges left after the single-edge components
     return true;
 }
 
-__global__ __launch_bounds__(BLKL) void k_s1_lap(BtArgs a) {
+// four 256-thread blocks per CU: <= 128 VGPRs (4 waves per SIMD) and a <= 36 KiB arena
+__global__ __launch_bounds__(BLKL, 4) void k_s1_lap(BtArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     __shared__ LapShared lsh;
     const int s = blockIdx.x;
+    YTA_BLK(2, 0);
     {
         Arena ar(smem, a.lds_bytes_l);
-        if (s1_lap_body(a, s, ar, lsh)) return;
+        if (s1_lap_body(a, s, ar, lsh)) {
+            YTA_BLK(2, 1);
+            return;
+        }
     }
     block_sync();
     if (threadIdx.x == 0) a.cnt[s].n_fallback[0] += 1;
     Arena ag(a.ws + s * a.ws_stride, a.ws_stride);
     if (!s1_lap_body(a, s, ag, lsh) && threadIdx.x == 0) atomicOr(&a.cnt[s].err, ERR_EDGE_OVERFLOW);
+    YTA_BLK(2, 1);
 }
 
 // ------------------------------------------------------------------------------------ k_apply
@@ -1487,7 +1558,8 @@ __device__ __forceinline__ void finish_body(const BtArgs &a, int s, unsigned *bi
 }
 
 template <int V>
-__global__ __launch_bounds__(BLKF) void k_finish(BtArgs a) {
+// four 256-thread blocks per CU: <= 128 VGPRs (the diagnostic build's stamps would add some)
+__global__ __launch_bounds__(BLKF, 4) void k_finish(BtArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char fsmem[];
     __shared__ FinishShared sh;
     const int s = blockIdx.x;
@@ -1499,6 +1571,7 @@ __global__ __launch_bounds__(BLKF) void k_finish(BtArgs a) {
     YTA_STAMP(0);
     const BtCounters *c = a.cnt + s;
     const long long need = dedup_arena_bytes(c->n_lost + c->n_left);
+    YTA_BLK(5, 0);
     if (need <= (long long)a.lds_bytes_f) {
         Arena ar(fsmem + bits_bytes, a.lds_bytes_f);
         finish_body<V>(a, s, bits, ar, sh);
@@ -1506,6 +1579,7 @@ __global__ __launch_bounds__(BLKF) void k_finish(BtArgs a) {
         Arena ag(a.ws + s * a.ws_stride, a.ws_stride);
         finish_body<V>(a, s, bits, ag, sh);
     }
+    YTA_BLK(5, 1);
 }
 
 // Rebuild the free-slot list of every stream from its tracked + lost lists (after a reserve).
@@ -1601,14 +1675,17 @@ constexpr int BT_PHASES = 6;   // timed phases per frame, see yta_bytetrack_prof
 #endif
 constexpr size_t BT_LDS_BYTES = YTA_LDS1_KB * 1024;   // k_stage1 arena (one 1024-thread block per CU)
 constexpr size_t BT_LDS23_BYTES = 32 * 1024;  // k_stage23 arena (several blocks per CU)
-constexpr size_t BT_LDSF_BYTES = 36 * 1024;   // k_finish dedup arena (four blocks per CU; lost'
-                                              // of 720 at 1024 x 1024)
-#ifndef YTA_LDSL_KB
-#define YTA_LDSL_KB 76
+#ifndef YTA_LDSF_KB
+#define YTA_LDSF_KB 32
 #endif
-constexpr size_t BT_LDSL_BYTES = YTA_LDSL_KB * 1024;   // k_s1_lap arena (two blocks per CU)
+constexpr size_t BT_LDSF_BYTES = YTA_LDSF_KB * 1024;   // k_finish dedup arena (four blocks per
+                                                      // CU; lost' of 650 at 1024 x 1024)
+#ifndef YTA_LDSL_KB
+#define YTA_LDSL_KB 38
+#endif
+constexpr size_t BT_LDSL_BYTES = YTA_LDSL_KB * 1024;   // k_s1_lap arena (four blocks per CU)
 #ifndef YTA_LDSE_KB
-#define YTA_LDSE_KB 58
+#define YTA_LDSE_KB 62
 #endif
 constexpr size_t BT_LDSE_BYTES = YTA_LDSE_KB * 1024;   // k_s1_edges grid (1024 high detections)
 
@@ -1753,6 +1830,7 @@ int bt_alloc(yta_bytetrack *e) {
         DALLOC(a.g_w, S * MAXD);
         DALLOC(a.g_hdr, S);
         DALLOC(a.e_cnt, S * CAP);
+        DALLOC(a.g_deg, S * MAXD);
         DALLOC(a.e_col, E_SLOTS * S * CAP);
         DALLOC(a.e_cost, E_SLOTS * S * CAP);
     }
@@ -2370,7 +2448,7 @@ int yta_bytetrack_stats(yta_bytetrack *e, long long *stats) {
     YTA_HIP(hipSetDevice(e->device));
     const int rc = read_counters(e);
     if (rc) return rc;
-    constexpr int NS = 19;
+    constexpr int NS = 20;
     for (int k = 0; k < NS; ++k) stats[k] = 0;
     for (int s = 0; s < e->S; ++s) {
         const BtCounters &c = e->h_cnt[s];
@@ -2378,7 +2456,7 @@ int yta_bytetrack_stats(yta_bytetrack *e, long long *stats) {
                                  c.n_left, c.n_rest, c.n_births, c.n_t2, c.n_l2, c.n_tracked,
                                  c.n_lost, c.n_out, (long long)c.n_edges[0],
                                  (long long)c.n_edges[1] + c.n_edges[2], c.n_fallback[0],
-                                 c.n_fallback[1], c.n_lazy};
+                                 c.n_fallback[1], c.n_lazy, c.n_res1};
         for (int k = 0; k < NS; ++k) stats[k] += v[k];
     }
     return YTA_OK;
@@ -2466,6 +2544,10 @@ int yta_botsort_get_features(yta_botsort *e, int stream, int *n_tracks, float *f
 #ifdef YTA_STAMPS
 int yta_debug_stamps(unsigned long long *out) {
     YTA_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 128));
+    return YTA_OK;
+}
+int yta_debug_blocks(unsigned long long *out) {   // [8][YTA_BLK_MAX][2]
+    YTA_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_blk), sizeof(g_blk)));
     return YTA_OK;
 }
 #endif

@@ -46,7 +46,8 @@ struct BtCounters {                  // one per stream, 128 B
     int n_edges[3];
     int n_fallback[2];               // cumulative: association redone over global memory
     int n_lazy;                      // ByteTrack: lost-list records k_apply left untouched
-    int pad[6];
+    int n_res1;                      // ByteTrack: stage-1 edges left to k_s1_lap
+    int pad[5];
 };
 static_assert(sizeof(BtCounters) == 128, "BtCounters layout");
 
@@ -104,7 +105,8 @@ struct BtArgs {
     Box *g_boxes;             // [S*MAXD] their boxes, cell order
     double *g_w;              // [S*MAXD] their scores (fuse_score weights), cell order
     GridHdr *g_hdr;           // [S]
-    int *e_cnt;               // [S*CAP] candidate edges per pool row
+    int *e_cnt;               // [S*CAP] candidate edges per pool row (0 once matched outright)
+    int *g_deg;               // [S*MAXD] candidate edges per high detection (HBM-grid path)
     int *e_col;               // [E_SLOTS][S*CAP] the first E_SLOTS edges' high positions
     double *e_cost;           // [E_SLOTS][S*CAP] and costs
     size_t lds_bytes_l;       // k_s1_lap arena

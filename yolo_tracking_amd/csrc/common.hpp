@@ -77,7 +77,18 @@ static __device__ int g_stamp_off;
     do {                                                                       \
         if (blockIdx.x == 0 && threadIdx.x == 0) g_stamps[(k)] += 1;            \
     } while (0)
+// per-block timeline of the block/stream kernels: start (e = 0) and end (e = 1) of block b of
+// kernel k, read back with yta_debug_blocks
+constexpr int YTA_BLK_MAX = 4096;
+static __device__ unsigned long long g_blk[8][YTA_BLK_MAX][2];
+#define YTA_BLK(k, e)                                                                \
+    do {                                                                             \
+        if (threadIdx.x == 0 && blockIdx.x < YTA_BLK_MAX) g_blk[k][blockIdx.x][e] = wall_clock64(); \
+    } while (0)
 #else
+#define YTA_BLK(k, e) \
+    do {              \
+    } while (0)
 #define YTA_COUNT(k) \
     do {             \
     } while (0)

@@ -406,14 +406,18 @@ struct LapShared {       // static LDS of the calling kernel
 // Solve one problem.  X[nr], Y[nc] (global) receive the assignment.  Arrays come from `ar`
 // (lo end); returns false if the arena is exhausted (X / Y then hold garbage; the caller redoes
 // the frame with a larger arena or reports capacity).  Every thread of the block calls it.
+// init_xy false: the caller already set X / Y (-1, or pairs of components it matched itself and
+// left out of the graph); only matched pairs are written.
 __device__ __forceinline__ bool lap_block(int nr, int nc, const int *row_off, const int *csr_col,
                                           const double *csr_cost, const int *col_deg,
                                           double thresh, int *X, int *Y, int *err, Arena &ar,
-                                          const LapSlab &slab, LapShared &sh) {
+                                          const LapSlab &slab, LapShared &sh, bool init_xy = true) {
     const int t = threadIdx.x, nt = blockDim.x;
     const int N = nr + nc;
-    for (int i = t; i < nr; i += nt) X[i] = -1;
-    for (int j = t; j < nc; j += nt) Y[j] = -1;
+    if (init_xy) {
+        for (int i = t; i < nr; i += nt) X[i] = -1;
+        for (int j = t; j < nc; j += nt) Y[j] = -1;
+    }
     const int E = nr > 0 ? row_off[nr] : 0;
     if (E == 0) {
         block_sync();
