@@ -255,6 +255,7 @@ __device__ __forceinline__ bool stage1_body(const BtArgs &a, int s, Arena &ar, S
         c->n_births = 0;
         c->n_lazy = 0;
         c->n_res1 = 0;
+        c->n_ref = 0;
     }
     return true;
 }
@@ -270,17 +271,25 @@ __device__ __forceinline__ bool stage23_body(const BtArgs &a, int s, Arena &ar, 
     BtCounters *c = a.cnt + s;
     const long long tb = (long long)s * a.CAP, db = (long long)s * a.MAXD;
     const int n_pool = c->n_pool, n_high = c->n_high, n_second = c->n_second, n_unc = c->n_unc;
+    const int n_act = c->n_act;
     for (int i = t; i < n_pool; i += nt) a.left_of_pool[tb + i] = -1;
     block_sync();
-    const int n_left = block_compact(
-        n_pool, wsum,
-        [&](int i) {
-            return a.x1[tb + i] < 0 && st_of(a.flags[tb + a.pool[tb + i]]) == ST_TRACKED;
-        },
-        [&](int i, int pos) {
+    // leftovers: the pool's Tracked rows (its head, the activated tracks: pool = act ++ lost)
+    // left unmatched in stage 1 (:205-209)
+    const int n_left = block_compact_ld<8>(
+        n_act, wsum, [&](int i) { return a.x1[tb + i]; }, [&](int, int h) { return h; },
+        [&](int, int h) { return h < 0; },
+        [&](int i, int, int pos) {
             a.left[tb + pos] = i;
             a.left_of_pool[tb + i] = pos;
         });
+    // re-found: the pool's Lost rows matched in stage 1 (refind_stracks, :193-196), pool order,
+    // with their slot and detection (k_apply visits these and no other Lost row)
+    const int n_ref = block_compact_ld<8>(
+        n_pool - n_act, wsum,
+        [&](int k) { return make_int2(a.pool[tb + n_act + k], a.x1[tb + n_act + k]); },
+        [&](int, int2 v) { return v; }, [&](int, const int2 &v) { return v.y >= 0; },
+        [&](int, const int2 &v, int pos) { a.refound[tb + pos] = v; });
     const int n_rest = block_compact(n_high, wsum, [&](int h) { return a.y1[db + h] < 0; },
                                      [&](int h, int pos) {
                                          a.rest[db + pos] = h;
@@ -315,6 +324,9 @@ __device__ __forceinline__ bool stage23_body(const BtArgs &a, int s, Arena &ar, 
     if (t == 0) {
         c->n_left = n_left;
         c->n_rest = n_rest;
+        c->n_ref = n_ref;
+        // ByteTrack: the Lost rows k_apply leaves untouched (lazy prediction)
+        c->n_lazy = V == VAR_BYTETRACK ? n_pool - n_act - n_ref : 0;
     }
     return true;
 }
@@ -555,6 +567,7 @@ __global__ __launch_bounds__(PREP_T) void k_s1_prep(BtArgs a) {
         c->n_births = 0;
         c->n_lazy = 0;
         c->n_res1 = 0;
+        c->n_ref = 0;
     }
     YTA_STAMP(3);
     YTA_BLK(0, 1);
@@ -1057,14 +1070,8 @@ __global__ __launch_bounds__(APPLY_T) void k_apply(BtArgs a) {
         s_wmask[t] = act == 5 ? 0 : (act == 1 || act == 2 || act == 4 ? 3 : 1);
     }
     if (lazy) s_wmask[t] = 0;
-    if (V == VAR_BYTETRACK) {   // records left untouched (stats)
-        const unsigned long long lz = __ballot(lazy);
-        if (lane_id() == 0 && lz) atomicAdd(&c->n_lazy, __popcll(lz));
-    }
     __syncthreads();
-    if (lazy) {
-        a.kind1[tb + i] = 0;
-    } else if (t < nloc) {
+    if (!lazy && t < nloc) {
         KfState st;
         double *row = reinterpret_cast<double *>(rec[t]);
         TrackMeta m;
@@ -1113,8 +1120,6 @@ __global__ __launch_bounds__(APPLY_T) void k_apply(BtArgs a) {
                 flags = (flags & ~FL_STATE) | ST_LOST;
                 if (V == VAR_BYTETRACK) a.kf_frame[tb + slot] = fid;
             }
-            // stage-1 outcome for the tracked' list order: 1 tracked -> updated, 2 re-found
-            a.kind1[tb + i] = act == 1 ? (tracked ? 1 : 2) : 0;
         } else if (act == 4) {
 #pragma unroll
             for (int k = 0; k < 8; ++k) st.m[k] = row[k];
@@ -1260,7 +1265,7 @@ __device__ __forceinline__ void finish_body(const BtArgs &a, int s, unsigned *bi
     BtCounters *c = a.cnt + s;
     const long long tb = (long long)s * a.CAP, db = (long long)s * a.MAXD;
     const int fid = c->frame_id;
-    const int n_tracked = c->n_tracked, n_lost = c->n_lost, n_pool = c->n_pool;
+    const int n_tracked = c->n_tracked, n_lost = c->n_lost;
     const int n_rest = c->n_rest, n_left = c->n_left, n_free = c->n_free;
     const long long next_id = c->next_id;
     const int words = (a.CAP + 31) / 32;
@@ -1360,11 +1365,9 @@ __device__ __forceinline__ void finish_body(const BtArgs &a, int s, unsigned *bi
         [&](int, const SlotFlags &v, int pos) { a.t2[tb + pos] = v.slot; });
     for (int b = t; b < n_births; b += nt) a.t2[tb + n_t2 + b] = a.free_list[tb + b];
     n_t2 += n_births;
-    n_t2 += block_compact_ld<8>(
-        n_pool, wsum,
-        [&](int i) { return make_int2(a.kind1[tb + i], a.pool[tb + i]); },
-        [&](int, int2 v) { return v; }, [&](int, const int2 &v) { return v.x == 2; },
-        [&](int, const int2 &v, int pos) { a.t2[tb + n_t2 + pos] = v.y; });
+    const int n_ref = c->n_ref;   // re-found, pool order (k_stage23)
+    for (int k = t; k < n_ref; k += nt) a.t2[tb + n_t2 + k] = a.refound[tb + k].x;
+    n_t2 += n_ref;
     // lost' = sub(lost, tracked') ++ newly lost, minus ids already in removed_stracks (:262-264);
     // this frame's removals join removed_stracks only now (:265)
     int n_l2 = block_compact_ld<8>(
@@ -1795,7 +1798,7 @@ int bt_alloc(yta_bytetrack *e) {
     DALLOC(a.left_of_pool, S * CAP);
     DALLOC(a.t2, S * CAP);
     DALLOC(a.l2, S * CAP);
-    DALLOC(a.kind1, S * CAP);
+    DALLOC(a.refound, S * CAP);
     DALLOC(a.pool_box, S * CAP);
     DALLOC(a.unc_box, S * CAP);
     DALLOC(a.x1, S * CAP);

@@ -47,7 +47,8 @@ struct BtCounters {                  // one per stream, 128 B
     int n_fallback[2];               // cumulative: association redone over global memory
     int n_lazy;                      // ByteTrack: lost-list records k_apply left untouched
     int n_res1;                      // ByteTrack: stage-1 edges left to k_s1_lap
-    int pad[5];
+    int n_ref;                       // re-found Lost tracks (refound list)
+    int pad[4];
 };
 static_assert(sizeof(BtCounters) == 128, "BtCounters layout");
 
@@ -89,7 +90,8 @@ struct BtArgs {
     Box *high_box, *second_box;
     double *high_score, *rest_score;
     // per-frame: tracks [S*CAP]
-    int *pool, *unc, *left, *left_of_pool, *t2, *l2, *kind1;
+    int *pool, *unc, *left, *left_of_pool, *t2, *l2;
+    int2 *refound;            // [S*CAP] (slot, stage-1 high position) of each re-found Lost track
     Box *pool_box, *unc_box;
     // association results
     int *x1, *y1, *x2, *y2, *x3, *y3;   // x*: [S*CAP], y*: [S*MAXD]
