@@ -140,6 +140,8 @@ def parse():
     p.add_argument("--no-pcie", action="store_true", help="skip the host-buffer (PCIe) leg")
     p.add_argument("--cpu-frames", type=int, default=40)
     p.add_argument("--seed", type=int, default=1000)
+    p.add_argument("--queues", type=int, default=1,
+                   help="engines per GPU, each on its own HIP stream, streams split between them")
     return p.parse_args()
 
 
@@ -227,61 +229,87 @@ def main():
     host = np.stack([np.concatenate([per_stream[s][f] for s in range(S)]) for f in range(F)])
     off = np.array([[sum(len(per_stream[q][f]) for q in range(s)) for s in range(S + 1)]
                     for f in range(F)], dtype=np.int32)
-    d_dets = torch.from_numpy(host).to("cuda")
-    d_off = torch.from_numpy(off).to("cuda")
+    # Q engines (each its own HIP stream) over contiguous slices of the streams: their launches
+    # run concurrently, so one engine's latency-bound block chains overlap the other's
+    Q = max(1, args.queues)
+    assert S % Q == 0, "--streams must be a multiple of --queues"
+    Sq = S // Q
+    d_dets, d_off = [], []
+    for q in range(Q):
+        lo, hi = off[:, q * Sq], off[:, (q + 1) * Sq]
+        dq = np.stack([host[f, lo[f]:hi[f]] for f in range(F)]) if len(set(hi - lo)) == 1 else None
+        assert dq is not None, "synthetic frames have N detections per stream"
+        d_dets.append(torch.from_numpy(np.ascontiguousarray(dq)).to("cuda"))
+        d_off.append(torch.from_numpy(np.ascontiguousarray(off[:, q * Sq:(q + 1) * Sq + 1]
+                                                          - off[:, q * Sq:q * Sq + 1])).to("cuda"))
     gen_s = time.time() - t_gen
 
-    eng = ByteTrackEngine(S, track_thresh=0.5, match_thresh=0.8, track_buffer=30, frame_rate=30,
-                          device=local_rank, track_capacity=2 * N, max_dets=N)
+    engs = [ByteTrackEngine(Sq, track_thresh=0.5, match_thresh=0.8, track_buffer=30, frame_rate=30,
+                            device=local_rank, track_capacity=2 * N, max_dets=N) for _ in range(Q)]
+    eng = engs[0]
     cap, _ = eng.capacity()
-    d_out = torch.empty((S * cap, 8), dtype=torch.float64, device="cuda")
-    d_cnt = torch.zeros(S, dtype=torch.int32, device="cuda")
+    d_out = [torch.empty((Sq * cap, 8), dtype=torch.float64, device="cuda") for _ in range(Q)]
+    d_cnt = [torch.zeros(Sq, dtype=torch.int32, device="cuda") for _ in range(Q)]
     lib = eng.lib
-    h = eng.handle
-    row_bytes = N * 6 * 8 * S
+    handles = [e.handle for e in engs]
+    h = handles[0]
+    row_bytes = N * 6 * 8 * Sq
 
     def step(f):
-        _lib.check(lib.yta_bytetrack_update_device(
-            h, ctypes.c_void_p(d_dets.data_ptr() + f * row_bytes),
-            ctypes.c_void_p(d_off.data_ptr() + f * (S + 1) * 4),
-            ctypes.c_void_p(d_out.data_ptr()), ctypes.c_void_p(d_cnt.data_ptr())))
+        for q in range(Q):
+            _lib.check(lib.yta_bytetrack_update_device(
+                handles[q], ctypes.c_void_p(d_dets[q].data_ptr() + f * row_bytes),
+                ctypes.c_void_p(d_off[q].data_ptr() + f * (Sq + 1) * 4),
+                ctypes.c_void_p(d_out[q].data_ptr()), ctypes.c_void_p(d_cnt[q].data_ptr())))
+
+    def sync_all():
+        for hq in handles:
+            _lib.check(lib.yta_bytetrack_sync(hq))
 
     torch.cuda.synchronize()
     for f in range(args.warmup):
         step(f)
-    _lib.check(lib.yta_bytetrack_sync(h))
-    _lib.check(lib.yta_bytetrack_profile(h, 1))
+    sync_all()
+    for hq in handles:
+        _lib.check(lib.yta_bytetrack_profile(hq, 1))
     def run_steps():
         for f in range(args.warmup, F):
             step(f)
-        _lib.check(lib.yta_bytetrack_sync(h))
+        sync_all()
 
     elapsed = timed_region(run_steps, torch.cuda.synchronize, dist)
+    # per-launch phase times: engine 0's HIP events (with Q > 1 they overlap the other engines')
     ms = (ctypes.c_double * len(PHASES))()
     nfr = ctypes.c_int()
     _lib.check(lib.yta_bytetrack_profile_collect(h, ms, ctypes.byref(nfr)))
     phase_ms = {PHASES[k]: ms[k] / max(nfr.value, 1) for k in range(len(PHASES))}
+    for hq in handles[1:]:
+        _lib.check(lib.yta_bytetrack_profile_collect(hq, ms, ctypes.byref(nfr)))
 
     elapsed = max_over_ranks(elapsed, dist, "cuda")
     value = aggregate_rate(world, S, args.steps, elapsed)
     ms_per_step = 1000.0 * elapsed / args.steps
 
     stats = (ctypes.c_longlong * len(STATS))()
-    _lib.check(lib.yta_bytetrack_stats(h, stats))
-    st = {STATS[k]: int(stats[k]) for k in range(len(STATS))}
+    st = {k: 0 for k in STATS}
+    for hq in handles:   # summed over the engines (all S streams)
+        _lib.check(lib.yta_bytetrack_stats(hq, stats))
+        for k in range(len(STATS)):
+            st[STATS[k]] += int(stats[k])
+    st_launch = {k: v // Q for k, v in st.items()}   # one engine's launch (Q equal slices)
     if rank == 0:
         # roofline kernel: the longest launch of the frame (the Kalman pass k_apply, HBM-bound)
         dom = max(phase_ms, key=lambda p: phase_ms[p])
         dom_ms = phase_ms[dom]
-        b = kernel_bytes(dom, st)
+        b = kernel_bytes(dom, st_launch)
         achieved = b / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
         busiest = max(phase_ms, key=lambda p: phase_ms[p])
-        per_kernel = {p: {"ms": phase_ms[p], "alg_bytes": kernel_bytes(p, st),
-                          "gbs": (kernel_bytes(p, st) / (phase_ms[p] * 1e-3) / 1e9
+        per_kernel = {p: {"ms": phase_ms[p], "alg_bytes": kernel_bytes(p, st_launch),
+                          "gbs": (kernel_bytes(p, st_launch) / (phase_ms[p] * 1e-3) / 1e9
                                   if phase_ms[p] > 0 else 0.0)} for p in PHASES}
         cpu = None if args.no_cpu_baseline else cpu_baseline(N, args.cpu_frames, args.seed)
         pcie = None if args.no_pcie else pcie_inclusive(host, off, S, N, local_rank)
-        traffic, traffic_tag = pmc_traffic(S, N)
+        traffic, traffic_tag = pmc_traffic(S, N) if Q == 1 else (None, None)
         line = {
             "metric": "tracker.update() calls/sec @ 1024 tracks×1024 dets; 1/2/4/8 MI355X",
             "value": value, "unit": "calls/s", "n_gpus": world, "steps": args.steps,
@@ -289,7 +317,7 @@ def main():
             "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
             "config": {"workload": f"bytetrack {N}x{N}, {S} streams/GPU, inputs resident in HBM",
                        "tracker": "bytetrack", "tracks": N, "dets": N, "streams_per_gpu": S,
-                       "parallelism": f"stream-sharded x{world}"},
+                       "queues_per_gpu": Q, "parallelism": f"stream-sharded x{world}"},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
