@@ -117,6 +117,20 @@ def main():
         print(f"  {name:<11s} span {span:7.2f}  block dur p50 {q[0]:6.2f} p90 {q[1]:6.2f} max "
               f"{q[2]:6.2f}  starts: <2us {int((st0 < 2).sum())}, p50 {np.median(st0):6.2f}, "
               f"max {st0.max():6.2f}  slowest block {int(dur.argmax())}")
+    # k_apply phases (blocks of the first 256 streams)
+    ap = np.zeros(4096 * 5, dtype=np.uint64)
+    lib.yta_debug_apply.argtypes = [ctypes.c_void_p]
+    _lib.check(lib.yta_debug_apply(ap.ctypes.data))
+    ap = ap.reshape(4096, 5).astype(np.int64)
+    ap = ap[ap[:, 0] > 0]
+    if len(ap):
+        d = np.diff(ap, axis=1) / 100.0
+        life = (ap[:, 4] - ap[:, 0]) / 100.0
+        print(f"-- k_apply blocks sampled {len(ap)}: lifetime p50 {np.median(life):.2f} p90 "
+              f"{np.percentile(life, 90):.2f} us; span {(ap[:, 4].max() - ap[:, 0].min()) / 100.0:.2f}")
+        for k, name in enumerate(["level 0 (lists)", "records + det rows", "Kalman compute",
+                                  "store issue"]):
+            print(f"  {name:<20s} p50 {np.median(d[:, k]):6.2f}  p90 {np.percentile(d[:, k], 90):6.2f} us")
 
 
 if __name__ == "__main__":

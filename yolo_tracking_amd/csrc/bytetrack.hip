@@ -682,7 +682,8 @@ __device__ __forceinline__ void s1_single_edges(const BtArgs &a, int s, int nc, 
     }
 }
 
-__global__ __launch_bounds__(BLKE) void k_s1_edges(BtArgs a) {
+// two 512-thread blocks per CU: <= 128 VGPRs (the diagnostic build's stamps would add some)
+__global__ __launch_bounds__(BLKE, 4) void k_s1_edges(BtArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     __shared__ GridScratch gs;
     __shared__ int wsum[32];
@@ -986,6 +987,7 @@ __global__ __launch_bounds__(APPLY_T) void k_apply(BtArgs a) {
     const int i0 = blockIdx.x * APPLY_T;
     const int n_items = n_pool + n_unc;
     if (i0 >= n_items) return;                                       // block-uniform
+    YTA_APL(0);
     const int nloc = n_items - i0 < APPLY_T ? n_items - i0 : APPLY_T;
     const long long tb = (long long)s * a.CAP, db = (long long)s * a.MAXD;
     const int i = i0 + t;
@@ -1012,6 +1014,7 @@ __global__ __launch_bounds__(APPLY_T) void k_apply(BtArgs a) {
     const bool lazy = V == VAR_BYTETRACK && live && in_pool && i >= c->n_act && h < 0;
     if (live) s_slot[t] = lazy ? -1 : slot;
     __syncthreads();
+    YTA_APL(1);
     // level 1: flags, the stage-1 detection, the stage-2 result
     const int flags0 = live && !lazy ? a.flags[tb + slot] : 0;
     const int det1 = h >= 0 ? a.high[db + h] : -1;
@@ -1071,6 +1074,7 @@ __global__ __launch_bounds__(APPLY_T) void k_apply(BtArgs a) {
     }
     if (lazy) s_wmask[t] = 0;
     __syncthreads();
+    YTA_APL(2);
     if (!lazy && t < nloc) {
         KfState st;
         double *row = reinterpret_cast<double *>(rec[t]);
@@ -1148,6 +1152,7 @@ __global__ __launch_bounds__(APPLY_T) void k_apply(BtArgs a) {
         if (wmask & 2) memcpy(row + KF_REC, &m, sizeof(TrackMeta));
     }
     __syncthreads();
+    YTA_APL(3);
     // cooperative store of what changed
     double2 *recw = reinterpret_cast<double2 *>(a.kf);
     for (int p = t; p < nloc * REC_PIECES; p += APPLY_T) {
@@ -1156,6 +1161,7 @@ __global__ __launch_bounds__(APPLY_T) void k_apply(BtArgs a) {
         const long long sl = tb + s_slot[r];
         if (k < 12 ? (wm & 1) : (wm & 2)) recw[sl * (TRK_STRIDE / 2) + k] = rec[r][k];
     }
+    YTA_APL(4);
 }
 
 // ------------------------------------------------------------------------------ k_feat / k_ema
@@ -2547,6 +2553,10 @@ int yta_botsort_get_features(yta_botsort *e, int stream, int *n_tracks, float *f
 #ifdef YTA_STAMPS
 int yta_debug_stamps(unsigned long long *out) {
     YTA_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 128));
+    return YTA_OK;
+}
+int yta_debug_apply(unsigned long long *out) {   // [4096][5]
+    YTA_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_apl), sizeof(g_apl)));
     return YTA_OK;
 }
 int yta_debug_blocks(unsigned long long *out) {   // [8][YTA_BLK_MAX][2]

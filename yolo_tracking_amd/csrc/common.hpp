@@ -81,11 +81,21 @@ static __device__ int g_stamp_off;
 // kernel k, read back with yta_debug_blocks
 constexpr int YTA_BLK_MAX = 4096;
 static __device__ unsigned long long g_blk[8][YTA_BLK_MAX][2];
+// k_apply phases of blocks (x, y < 256): start, decision level 0, records in LDS, computed, stored
+static __device__ unsigned long long g_apl[4096][5];
+#define YTA_APL(k)                                                                          \
+    do {                                                                                    \
+        if (threadIdx.x == 0 && blockIdx.y < 256 && blockIdx.x < 16)                        \
+            g_apl[blockIdx.y * 16 + blockIdx.x][k] = wall_clock64();                        \
+    } while (0)
 #define YTA_BLK(k, e)                                                                \
     do {                                                                             \
         if (threadIdx.x == 0 && blockIdx.x < YTA_BLK_MAX) g_blk[k][blockIdx.x][e] = wall_clock64(); \
     } while (0)
 #else
+#define YTA_APL(k) \
+    do {           \
+    } while (0)
 #define YTA_BLK(k, e) \
     do {              \
     } while (0)
