@@ -395,7 +395,10 @@ __global__ __launch_bounds__(BLK23) void k_stage23(BtArgs a) {
 // Same results as k_stage1: edges are exactly the pairs with cost < match_thresh whatever the
 // grid's cell order, and lap_block's result does not depend on the order of a row's edges.
 constexpr int PREP_T = 256;          // k_s1_prep threads
-constexpr int PREP_CH = 768;         // items staged in LDS per pass of k_s1_prep
+#ifndef YTA_PREP_CH
+#define YTA_PREP_CH 768
+#endif
+constexpr int PREP_CH = YTA_PREP_CH;  // items staged in LDS per pass of k_s1_prep
 #ifndef YTA_BLKE
 #define YTA_BLKE 512
 #endif
@@ -409,7 +412,9 @@ struct PrepShared {
     union {
         struct {
             Box box[PREP_CH];
+#if YTA_PREP_CH <= 768
             double conf[PREP_CH];
+#endif
             unsigned char cat[PREP_CH];
         } d;                          // detections of the current pass
         struct {
@@ -484,7 +489,9 @@ __global__ __launch_bounds__(PREP_T) void k_s1_prep(BtArgs a) {
                 const double conf = r.v[4];
                 sh.u.d.cat[i] = conf > thr ? 1 : (conf > a.low_thresh && conf < thr ? 2 : 0);
                 sh.u.d.box[i] = xywh_to_box(xywh);
+#if YTA_PREP_CH <= 768
                 sh.u.d.conf[i] = conf;
+#endif
             });
         lds_sync();
         const int2 hs = block_compact2<false>(
@@ -494,7 +501,11 @@ __global__ __launch_bounds__(PREP_T) void k_s1_prep(BtArgs a) {
                     const long long p = db + n_high + pos;
                     a.high[p] = c0 + i;
                     a.high_box[p] = sh.u.d.box[i];
+#if YTA_PREP_CH <= 768
                     a.high_score[p] = sh.u.d.conf[i];
+#else
+                    a.high_score[p] = din[(long long)(c0 + i) * 6 + 4];   // L2-resident
+#endif
                 } else {
                     const long long p = db + n_second + pos;
                     a.second[p] = c0 + i;
@@ -1341,28 +1352,6 @@ __device__ __forceinline__ void finish_body(const BtArgs &a, int s, unsigned *bi
         }
     }
     YTA_STAMP(2);
-    // lost-track expiry (:250-253); end_frame == frame_id
-    struct LostAge {
-        long long slot;
-        int frame, flags;
-    };
-    batched_for2<4>(
-        n_lost, [&](int i) { return a.lost[tb + i]; },
-        [&](int, int sl) {
-            LostAge v;
-            v.slot = tb + sl;
-            v.frame = V == VAR_BYTETRACK ? a.kf_frame[v.slot] - 1 : bt_meta(a, v.slot).frame_id;
-            v.flags = a.flags[v.slot];
-            return v;
-        },
-        [&](int, const LostAge &v0) {
-            LostAge v = v0;
-            if (V == VAR_BYTETRACK && st_of(v.flags) == ST_TRACKED) v.frame = fid;
-            if (fid - v.frame > a.max_time_lost)
-                a.flags[v.slot] = (v.flags & ~FL_STATE) | ST_REMOVED | FL_REMOVED_NOW;
-        });
-    block_sync();
-    YTA_STAMP(3);
     // tracked' = [Tracked survivors of tracked_stracks] ++ births ++ re-found (:257-261)
     auto with_flags = [&](int, int slot) { return SlotFlags{slot, a.flags[tb + slot]}; };
     int n_t2 = block_compact_ld<8>(
@@ -1375,17 +1364,40 @@ __device__ __forceinline__ void finish_body(const BtArgs &a, int s, unsigned *bi
     for (int k = t; k < n_ref; k += nt) a.t2[tb + n_t2 + k] = a.refound[tb + k].x;
     n_t2 += n_ref;
     // lost' = sub(lost, tracked') ++ newly lost, minus ids already in removed_stracks (:262-264);
-    // this frame's removals join removed_stracks only now (:265)
+    // this frame's removals join removed_stracks only now (:265).  The lost-track expiry
+    // (:250-253, end_frame == frame_id) is decided in the same pass: ByteTrack: a Lost track was
+    // last updated the frame before it was marked lost (an activated Tracked track takes a
+    // detection every frame until then), so frame_id = kf_frame - 1 unless it was re-found this
+    // frame (frame_id = fid), from the dense array instead of the record's meta line.  l2pos: each
+    // lost' track's pool position (its predicted box is pool_box there).
+    const int n_act = c->n_act;
+    struct LostItem {
+        int slot, flags, frame;
+    };
     int n_l2 = block_compact_ld<8>(
-        n_lost, wsum, [&](int i) { return a.lost[tb + i]; }, with_flags,
-        [&](int, const SlotFlags &v) {
-            if (v.flags & FL_REMOVED_NOW)
-                a.flags[tb + v.slot] = (v.flags & ~FL_REMOVED_NOW) | FL_EVER_REMOVED;
-            return st_of(v.flags) != ST_TRACKED && !(v.flags & FL_EVER_REMOVED);
+        n_lost, wsum, [&](int i) { return a.lost[tb + i]; },
+        [&](int, int sl) {
+            LostItem v;
+            v.slot = sl;
+            v.flags = a.flags[tb + sl];
+            v.frame = V == VAR_BYTETRACK ? a.kf_frame[tb + sl] - 1 : bt_meta(a, tb + sl).frame_id;
+            return v;
         },
-        [&](int, const SlotFlags &v, int pos) { a.l2[tb + pos] = v.slot; });
+        [&](int, const LostItem &v) {
+            int f = v.flags;
+            const int frame = V == VAR_BYTETRACK && st_of(f) == ST_TRACKED ? fid : v.frame;
+            if (fid - frame > a.max_time_lost) f = (f & ~FL_STATE) | ST_REMOVED | FL_REMOVED_NOW;
+            const bool keep = st_of(f) != ST_TRACKED && !(f & FL_EVER_REMOVED);
+            if (f & FL_REMOVED_NOW) f = (f & ~FL_REMOVED_NOW) | FL_EVER_REMOVED;
+            if (f != v.flags) a.flags[tb + v.slot] = f;
+            return keep;
+        },
+        [&](int i, const LostItem &v, int pos) {
+            a.l2[tb + pos] = v.slot;
+            a.l2pos[tb + pos] = n_act + i;   // pool = act ++ lost, in list order
+        });
     struct LeftItem {
-        int x2;
+        int x2, pos;
         SlotFlags sf;
     };
     n_l2 += block_compact_ld<4>(
@@ -1393,7 +1405,8 @@ __device__ __forceinline__ void finish_body(const BtArgs &a, int s, unsigned *bi
         [&](int i) {
             LeftItem v;
             v.x2 = a.x2[tb + i];
-            v.sf.slot = a.pool[tb + a.left[tb + i]];
+            v.pos = a.left[tb + i];
+            v.sf.slot = a.pool[tb + v.pos];
             return v;
         },
         [&](int, LeftItem v) {
@@ -1401,7 +1414,10 @@ __device__ __forceinline__ void finish_body(const BtArgs &a, int s, unsigned *bi
             return v;
         },
         [&](int, const LeftItem &v) { return v.x2 < 0 && !(v.sf.flags & FL_EVER_REMOVED); },
-        [&](int, const LeftItem &v, int pos) { a.l2[tb + n_l2 + pos] = v.sf.slot; });
+        [&](int, const LeftItem &v, int pos) {
+            a.l2[tb + n_l2 + pos] = v.sf.slot;
+            a.l2pos[tb + n_l2 + pos] = v.pos;
+        });
     block_sync();
     YTA_STAMP(4);
     // remove_duplicate_stracks (:312-325): pairs with 1 - IoU < 0.15 drop the younger track (set
@@ -1433,9 +1449,15 @@ __device__ __forceinline__ void finish_body(const BtArgs &a, int s, unsigned *bi
             if (V == VAR_BYTETRACK) kf_predict_lost_mean(v.m, v.lag);
             return V == VAR_BOTSORT ? xywh_to_box(v.m) : xyah_mean_to_box(v.m[0], v.m[1], v.m[2], v.m[3]);
         };
-        batched_for2<3>(
-            n_l2, [&](int q) { return a.l2[tb + q]; }, [&](int, int sl) { return lmean_of(sl); },
-            [&](int q, const LostMean &v) { lcache[q] = lbox_of(v); });
+        if (V == VAR_BYTETRACK)   // the predicted box stage 1 used (k_s1_prep): same mean
+            batched_for<4>(
+                n_l2, [&](int q) { return a.pool_box[tb + a.l2pos[tb + q]]; },
+                [&](int q, const Box &b) { lcache[q] = b; });
+        else
+            batched_for2<3>(
+                n_l2, [&](int q) { return a.l2[tb + q]; },
+                [&](int, int sl) { return lmean_of(sl); },
+                [&](int q, const LostMean &v) { lcache[q] = lbox_of(v); });
         block_sync();   // lcache may be the global arena
         grid_build(n_l2, [&](int q) { return lcache[q]; }, [](int) { return 1.0; }, gv, sh.gs,
                    wsum);
@@ -1805,6 +1827,7 @@ int bt_alloc(yta_bytetrack *e) {
     DALLOC(a.t2, S * CAP);
     DALLOC(a.l2, S * CAP);
     DALLOC(a.refound, S * CAP);
+    DALLOC(a.l2pos, S * CAP);
     DALLOC(a.pool_box, S * CAP);
     DALLOC(a.unc_box, S * CAP);
     DALLOC(a.x1, S * CAP);

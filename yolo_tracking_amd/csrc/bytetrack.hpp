@@ -56,7 +56,10 @@ static_assert(sizeof(BtCounters) == 128, "BtCounters layout");
 // Tracker variants (template parameter V of the kernels).
 constexpr int VAR_BYTETRACK = 0, VAR_BOTSORT = 1;
 constexpr int CLS_K = 8;             // BoT-SORT class-histogram entries per track
-constexpr int E_SLOTS = 3;           // candidate edges kept per pool row by k_s1_edges
+#ifndef YTA_ESLOTS
+#define YTA_ESLOTS 4
+#endif
+constexpr int E_SLOTS = YTA_ESLOTS;  // candidate edges kept per pool row by k_s1_edges
 
 struct BtArgs {
     int S, CAP, MAXD;
@@ -92,6 +95,7 @@ struct BtArgs {
     // per-frame: tracks [S*CAP]
     int *pool, *unc, *left, *left_of_pool, *t2, *l2;
     int2 *refound;            // [S*CAP] (slot, stage-1 high position) of each re-found Lost track
+    int *l2pos;               // [S*CAP] per lost' entry: its pool position (k_finish)
     Box *pool_box, *unc_box;
     // association results
     int *x1, *y1, *x2, *y2, *x3, *y3;   // x*: [S*CAP], y*: [S*MAXD]
