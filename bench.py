@@ -134,7 +134,7 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=30)
     p.add_argument("--warmup", type=int, default=5)
-    p.add_argument("--streams", type=int, default=1024, help="streams per GPU")
+    p.add_argument("--streams", type=int, default=2048, help="streams per GPU")
     p.add_argument("--n", type=int, default=1024, help="tracks = detections per frame")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-pcie", action="store_true", help="skip the host-buffer (PCIe) leg")

@@ -4,7 +4,7 @@
 # step count).  Usage: tools/profile_round.sh TAG [STREAMS]  -> gpurun_out/prof_TAG/
 set -e
 TAG=$1
-S=${2:-1024}
+S=${2:-2048}
 R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/prof_$TAG
 mkdir -p $O
