@@ -54,9 +54,9 @@ constexpr int SLAB_WAVES = BLK_MAX / WAVE;   // solver slabs per stream (any blo
 __device__ __forceinline__ void store_kf(double *kf, long long slot, const KfState &s) {
     double2 *dst = reinterpret_cast<double2 *>(kf + slot * TRK_STRIDE);
 #pragma unroll
-    for (int k = 0; k < 12; ++k) {
+    for (int k = 0; k < 12; ++k) {   // mean: pieces 0-3, covariance: pieces 8-15
         const double *src = k < 4 ? s.m + 2 * k : s.c + 2 * (k - 4);
-        dst[k] = make_double2(src[0], src[1]);
+        dst[k < 4 ? k : TRK_COV / 2 + (k - 4)] = make_double2(src[0], src[1]);
     }
 }
 
@@ -982,9 +982,13 @@ __device__ __forceinline__ void take_detection(const BtArgs &a, KfState &st, Tra
 
 // Records move between HBM and LDS in whole 16-B pieces with consecutive lanes on consecutive
 // pieces of a record (full-line reads and writes); each thread then runs the Kalman step of one
-// track out of LDS.  Pieces 0-11: the Kalman record (mean, then covariance), 12-14: the meta.
+// track out of LDS.  LDS row: pieces 0-3 the mean, 4-6 the meta, 7-14 the covariance (record
+// pieces 0-6 and 8-15: the padding piece 7 is skipped).
 constexpr int APPLY_T = 128;              // tracks (= threads) per block
-constexpr int REC_PIECES = KF_REC / 2 + 3;   // Kalman state + meta: the first 240 B of a record
+constexpr int REC_PIECES = 15;            // 16-B pieces of a record that carry data
+constexpr int L_META = 8, L_COV = 14;     // doubles: meta / covariance in an LDS row
+__device__ __forceinline__ int rec_piece(int k) { return k < 7 ? k : k + 1; }   // LDS -> record
+__device__ __forceinline__ bool piece_is_meta(int k) { return k >= 4 && k < 7; }
 
 template <int V>
 __global__ __launch_bounds__(APPLY_T) void k_apply(BtArgs a) {
@@ -1044,7 +1048,7 @@ __global__ __launch_bounds__(APPLY_T) void k_apply(BtArgs a) {
             const int r = p / REC_PIECES, k = p - r * REC_PIECES;
             const int rs = s_slot[r < nloc ? r : 0];   // rows past nloc: row 0 again
             const long long sl = tb + (rs < 0 ? 0 : rs);
-            const double2 *src = rec2 + sl * (TRK_STRIDE / 2) + k;
+            const double2 *src = rec2 + sl * (TRK_STRIDE / 2) + rec_piece(k);
             if (rs >= 0)   // lazy rows: nothing loaded, their LDS row is never read
                 __builtin_amdgcn_global_load_lds((glob_void *)src,
                                                  (lds_void *)(ldsb + (wb + q * APPLY_T) * 16), 16,
@@ -1090,7 +1094,7 @@ __global__ __launch_bounds__(APPLY_T) void k_apply(BtArgs a) {
         KfState st;
         double *row = reinterpret_cast<double *>(rec[t]);
         TrackMeta m;
-        memcpy(&m, row + KF_REC, sizeof(TrackMeta));
+        memcpy(&m, row + L_META, sizeof(TrackMeta));
         int flags = flags0;
         int wmask = 0;
         // BoT-SORT camera warp (multi_gmc, bot_sort.py:293-295; kf_xyah.hpp): a warped track
@@ -1112,7 +1116,7 @@ __global__ __launch_bounds__(APPLY_T) void k_apply(BtArgs a) {
 #pragma unroll
             for (int k = 0; k < 8; ++k) st.m[k] = row[k];
 #pragma unroll
-            for (int k = 0; k < 16; ++k) st.c[k] = row[8 + k];
+            for (int k = 0; k < 16; ++k) st.c[k] = row[L_COV + k];
             const bool tracked = st_of(flags) == ST_TRACKED;
             if (V == VAR_BYTETRACK && in_pool && i >= c->n_act)   // re-found from the lost list:
                 kf_predict_lost(st, fid - 1 - a.kf_frame[tb + slot]);   // replay the lazy predicts
@@ -1139,7 +1143,7 @@ __global__ __launch_bounds__(APPLY_T) void k_apply(BtArgs a) {
 #pragma unroll
             for (int k = 0; k < 8; ++k) st.m[k] = row[k];
 #pragma unroll
-            for (int k = 0; k < 16; ++k) st.c[k] = row[8 + k];
+            for (int k = 0; k < 16; ++k) st.c[k] = row[L_COV + k];
             if (V == VAR_BOTSORT && gmc) kf_gmc(st, xc, H);        // unconfirmed: warped only
             take_detection<V>(a, st, m, flags, dm, det, fid, tb + slot, &c->err,
                               cross ? xc : nullptr);
@@ -1158,9 +1162,9 @@ __global__ __launch_bounds__(APPLY_T) void k_apply(BtArgs a) {
 #pragma unroll
             for (int k = 0; k < 8; ++k) row[k] = st.m[k];
 #pragma unroll
-            for (int k = 0; k < 16; ++k) row[8 + k] = st.c[k];
+            for (int k = 0; k < 16; ++k) row[L_COV + k] = st.c[k];
         }
-        if (wmask & 2) memcpy(row + KF_REC, &m, sizeof(TrackMeta));
+        if (wmask & 2) memcpy(row + L_META, &m, sizeof(TrackMeta));
     }
     __syncthreads();
     YTA_APL(3);
@@ -1170,7 +1174,8 @@ __global__ __launch_bounds__(APPLY_T) void k_apply(BtArgs a) {
         const int r = p / REC_PIECES, k = p - r * REC_PIECES;
         const int wm = s_wmask[r];
         const long long sl = tb + s_slot[r];
-        if (k < 12 ? (wm & 1) : (wm & 2)) recw[sl * (TRK_STRIDE / 2) + k] = rec[r][k];
+        if (piece_is_meta(k) ? (wm & 2) : (wm & 1))
+            recw[sl * (TRK_STRIDE / 2) + rec_piece(k)] = rec[r][k];
     }
     YTA_APL(4);
 }
@@ -2428,7 +2433,7 @@ int yta_bytetrack_get_state(yta_bytetrack *e, int stream, int *n_tracks, long lo
             ii[6] = m.tracklet_len;
             KfState st;
             memcpy(st.m, kf.data() + (size_t)slot * TRK_STRIDE, sizeof(double) * 8);
-            memcpy(st.c, kf.data() + (size_t)slot * TRK_STRIDE + 8, sizeof(double) * 16);
+            memcpy(st.c, kf.data() + (size_t)slot * TRK_STRIDE + TRK_COV, sizeof(double) * 16);
             if (e->variant == VAR_BYTETRACK && which)   // lost list: lazily predicted
                 kf_predict_lost(st, c.frame_id - kf_frame[slot]);
             for (int k = 0; k < 8; ++k) mean[(long long)n * 8 + k] = st.m[k];

@@ -28,11 +28,15 @@ struct TrackMeta {                   // 48 B, one per slot
 
 static_assert(sizeof(TrackMeta) == 48, "TrackMeta layout");
 
-// One 256-B record per slot: the Kalman state (KF_REC = 24 f64) then the meta (6 f64), padded so
-// that a record is exactly two aligned 128-B lines (a 192-B record alone straddles a third line
-// half of the time, a separate 48-B meta costs a line of its own).
+// One 256-B record per slot, two aligned 128-B lines: line 0 = the Kalman mean (8 f64) + the meta
+// (6 f64) + 16 B of padding, line 1 = the four 2x2 covariance blocks (16 f64).  Everything an
+// output row, a predicted box or duplicate removal needs is in line 0 (mean + score, cls, id,
+// det_ind, frames); only the Kalman pass reads line 1.  (A 192-B record alone straddles a third
+// line half of the time, a separate 48-B meta costs a line of its own.)
 constexpr int TRK_STRIDE = 32;       // doubles per slot
-constexpr int TRK_META = KF_REC;     // offset of the meta in a record (doubles)
+constexpr int TRK_META = 8;          // offset of the meta in a record (doubles)
+constexpr int TRK_COV = 16;          // offset of the covariance (doubles)
+static_assert(TRK_META + 6 <= TRK_COV && TRK_COV + 16 == TRK_STRIDE, "record layout");
 
 struct BtCounters {                  // one per stream, 128 B
     long long next_id;               // last issued track id (BaseTrack._count)
