@@ -79,18 +79,19 @@ def kernel_bytes(phase, st):
     return 0
 
 
-def pmc_traffic(streams, n):
-    """HBM bytes per launch of the roofline kernel from the committed rocprofv3 PMC summary
-    (profiles/roofline_traffic.json, FETCH_SIZE x 2 + WRITE_SIZE in separate passes), when it
-    was measured on this same workload; else None."""
+def pmc_traffic(streams, n, queues):
+    """HBM bytes per launch of the roofline kernel, and per step of the whole frame (every kernel
+    of every engine), from the committed rocprofv3 PMC summary (profiles/roofline_traffic.json,
+    FETCH_SIZE x 2 + WRITE_SIZE in separate passes), when it was measured on this same workload;
+    else None."""
     f = os.path.join(REPO, "profiles", "roofline_traffic.json")
     try:
         d = json.load(open(f))
     except (OSError, ValueError):
-        return None, None
-    if d.get("streams") == streams and d.get("n") == n:
-        return d["hbm_bytes_per_launch"], d.get("tag")
-    return None, None
+        return None, None, None
+    if d.get("streams") == streams and d.get("n") == n and d.get("queues", 1) == queues:
+        return d["hbm_bytes_per_launch"], d.get("hbm_bytes_per_step"), d.get("tag")
+    return None, None, None
 
 
 # ---------------------------------------------------------------- multi-rank harness (N > 1)
@@ -140,7 +141,7 @@ def parse():
     p.add_argument("--no-pcie", action="store_true", help="skip the host-buffer (PCIe) leg")
     p.add_argument("--cpu-frames", type=int, default=40)
     p.add_argument("--seed", type=int, default=1000)
-    p.add_argument("--queues", type=int, default=1,
+    p.add_argument("--queues", type=int, default=2,
                    help="engines per GPU, each on its own HIP stream, streams split between them")
     return p.parse_args()
 
@@ -309,7 +310,7 @@ def main():
                                   if phase_ms[p] > 0 else 0.0)} for p in PHASES}
         cpu = None if args.no_cpu_baseline else cpu_baseline(N, args.cpu_frames, args.seed)
         pcie = None if args.no_pcie else pcie_inclusive(host, off, S, N, local_rank)
-        traffic, traffic_tag = pmc_traffic(S, N) if Q == 1 else (None, None)
+        traffic, step_traffic, traffic_tag = pmc_traffic(S, N, Q)
         line = {
             "metric": "tracker.update() calls/sec @ 1024 tracks×1024 dets; 1/2/4/8 MI355X",
             "value": value, "unit": "calls/s", "n_gpus": world, "steps": args.steps,
@@ -323,7 +324,15 @@ def main():
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "traffic_source": (f"profiles/{traffic_tag}_summary.json (rocprofv3 "
                                             "FETCH_SIZE x2 + WRITE_SIZE)" if traffic else None),
-                         "algorithmic_bytes_per_launch": b, "avg_launch_ms": dom_ms},
+                         "algorithmic_bytes_per_launch": b, "avg_launch_ms": dom_ms,
+                         "launch_streams": S // Q,
+                         # every kernel of every engine: measured HBM bytes per step / step time
+                         "chip_gbs": (step_traffic / (ms_per_step * 1e-3) / 1e9
+                                      if step_traffic else None),
+                         "note": (None if Q == 1 else
+                                  f"{Q} engines of {S // Q} streams on {Q} HIP streams: each "
+                                  "launch overlaps the other engines' kernels, so its duration "
+                                  "(and this per-launch rate) includes their share of the chip")},
             "cpu_baseline": cpu,
             "pcie_inclusive": pcie,
             "per_kernel": per_kernel,

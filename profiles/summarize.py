@@ -52,6 +52,9 @@ def main():
     ap.add_argument("write")
     ap.add_argument("--streams", type=int, default=None)
     ap.add_argument("--n", type=int, default=1024)
+    ap.add_argument("--queues", type=int, default=1, help="engines (HIP streams) of the run")
+    ap.add_argument("--steps", type=int, default=None,
+                    help="frames per engine in the profiled run (for the per-step traffic)")
     ap.add_argument("--bench-json", default=None)
     args = ap.parse_args()
     here = os.path.dirname(os.path.abspath(__file__))
@@ -71,8 +74,8 @@ def main():
     json.dump(summary, open(os.path.join(here, f"{args.tag}_summary.json"), "w"), indent=1)
     os.system(f"cp '{ks_file}' '{os.path.join(here, args.tag + '_kernel_stats.csv')}'")
     lines = [f"# rocprofv3 summary `{args.tag}`", "",
-             f"Workload: bench.py --streams {args.streams}, {args.n} tracks x {args.n} dets per "
-             f"stream.  HBM bytes = 2 x FETCH_SIZE + WRITE_SIZE (KiB -> bytes), separate passes.",
+             f"Workload: bench.py --streams {args.streams} --queues {args.queues}, {args.n} tracks x "
+             f"{args.n} dets per stream.  HBM bytes = 2 x FETCH_SIZE + WRITE_SIZE (KiB -> bytes), separate passes.",
              "",
              "| kernel | calls | avg µs | % time | HBM bytes/launch | GB/s |",
              "|---|---|---|---|---|---|"]
@@ -83,8 +86,13 @@ def main():
     open(os.path.join(here, f"{args.tag}_summary.md"), "w").write("\n".join(lines) + "\n")
     ka = next((k for k in stats if k.split("<")[0] == "k_apply"), None)
     if ka and "hbm_bytes_corrected" in stats[ka]:
-        json.dump({"tag": args.tag, "streams": args.streams, "n": args.n, "kernel": "k_apply",
+        # per step: every tracker kernel once per engine (the k_* launches of a frame)
+        step = sum(v["hbm_bytes_corrected"] for k, v in stats.items()
+                   if k.startswith("k_") and k != "k_reset" and "hbm_bytes_corrected" in v)
+        json.dump({"tag": args.tag, "streams": args.streams, "n": args.n, "queues": args.queues,
+                   "kernel": "k_apply",
                    "hbm_bytes_per_launch": stats[ka]["hbm_bytes_corrected"],
+                   "hbm_bytes_per_step": step * args.queues,
                    "avg_us_rocprof": stats[ka]["avg_us"]},
                   open(os.path.join(here, "roofline_traffic.json"), "w"), indent=1)
     print("\n".join(lines))
