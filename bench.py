@@ -228,8 +228,10 @@ def main():
     t_gen = time.time()
     per_stream = [gen_stream_frames(N, F, sd) for sd in stream_seeds(args.seed, rank, S)]
     host = np.stack([np.concatenate([per_stream[s][f] for s in range(S)]) for f in range(F)])
-    off = np.array([[sum(len(per_stream[q][f]) for q in range(s)) for s in range(S + 1)]
-                    for f in range(F)], dtype=np.int32)
+    counts = np.array([[len(per_stream[s][f]) for s in range(S)] for f in range(F)])
+    off = np.zeros((F, S + 1), dtype=np.int32)
+    np.cumsum(counts, axis=1, out=off[:, 1:])
+    del per_stream, counts
     # Q engines (each its own HIP stream) over contiguous slices of the streams: their launches
     # run concurrently, so one engine's latency-bound block chains overlap the other's
     Q = max(1, args.queues)
