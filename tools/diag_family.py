@@ -24,8 +24,9 @@ PHASES = {"deepocsort": ["first round", "lists", "OCR", "updates", "births", "ou
 
 def build():
     os.makedirs(os.path.dirname(OUT), exist_ok=True)
-    srcs = [os.path.join(CSRC, f) for f in ("util.hip", "kat.hip", "bytetrack.hip", "ocsort.hip",
-                                             "deepocsort.hip", "hybridsort.hip")]
+    mk = open(os.path.join(CSRC, "Makefile")).read()   # every source the product builds
+    names = next(l for l in mk.splitlines() if l.startswith("SRCS")).split("=", 1)[1].split()
+    srcs = [os.path.join(CSRC, f) for f in names]
     cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC",
            "-ffp-contract=off", "-fno-fast-math", "-munsafe-fp-atomics", "-DYTA_STAMPS",
            "-shared", "-o", OUT] + srcs

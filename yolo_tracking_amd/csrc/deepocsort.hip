@@ -56,7 +56,8 @@ struct DocCounters {
     int n_ema;
     int err;
     int lap_done;                  // first round solved by k_doc_lap this frame
-    int pad[17];
+    int n_ud, n_upd;               // k_doc_assoc -> k_doc_finish: unmatched detections, updates
+    int pad[15];
 };
 static_assert(sizeof(DocCounters) == 128, "DocCounters layout");
 
@@ -601,10 +602,8 @@ __global__ __launch_bounds__(OC_T) void k_doc_assoc(DocArgs a) {
     unsigned char *gws = a.lap_ws + s * a.lap_ws_stride;
     const long long lds_bytes = oc_lds_bytes(a.CAP, a.MAXD);
     const double *din = a.det_in + (long long)a.det_off[s] * 6;
-    const int frame = c->frame + 1;
     int n_trk = c->n_trk;
     const int n_hi = c->n_high;
-    const int dt = a.delta_t;
     int *list = a.list + tb;
     double *mat = a.mat + mb, *mat2 = a.mat2 + mb;
     int *udet = a.udet + ub, *utrk = a.utrk + ub;
@@ -724,14 +723,44 @@ __global__ __launch_bounds__(OC_T) void k_doc_assoc(DocArgs a) {
                                         a.ema_slot[eb + pos] = list[j];
                                         a.ema_row[eb + pos] = a.upd[tb + j];
                                     });
-    for (int j = t; j < n_trk; j += nt) {
-        DocTrack &r = a.rec[tb + list[j]];
-        const int hi = a.upd[tb + j];
-        const int row = hi >= 0 ? a.hi_row[db + hi] : -1;
-        doc_update(r, row >= 0 ? din + (long long)row * 6 : nullptr, row, dt);
+    if (t == 0) {
+        c->n_ud = n_ud;
+        c->n_upd = n_upd;
     }
-    block_sync();
     YTA_STAMP(4);
+}
+
+// Every tracker's update (deep_ocsort.py:461-467, :480-493: a matched tracker takes its
+// detection, the others update(None)) chip-wide, one thread per tracker: each touches only its
+// own record.
+__global__ __launch_bounds__(256) void k_doc_upd(DocArgs a) {
+    const int s = blockIdx.y;
+    const DocCounters *c = a.cnt + s;
+    const int j = blockIdx.x * 256 + threadIdx.x;
+    if (j >= c->n_trk) return;
+    const long long tb = (long long)s * a.CAP, db = (long long)s * a.MAXD;
+    const double *din = a.det_in + (long long)a.det_off[s] * 6;
+    const int hi = a.upd[tb + j];
+    const int row = hi >= 0 ? a.hi_row[db + hi] : -1;
+    doc_update(a.rec[tb + a.list[tb + j]], row >= 0 ? din + (long long)row * 6 : nullptr, row,
+               a.delta_t);
+}
+
+// Births, outputs, removal (deep_ocsort.py:495-520), after k_doc_upd.
+__global__ __launch_bounds__(OC_T) void k_doc_finish(DocArgs a) {
+    __shared__ OcShared sh;
+    const int s = blockIdx.x, t = threadIdx.x, nt = blockDim.x;
+    DocCounters *c = a.cnt + s;
+    const long long tb = (long long)s * a.CAP, db = (long long)s * a.MAXD;
+    const long long ub = (long long)s * (a.MAXD + a.CAP);
+    const double *din = a.det_in + (long long)a.det_off[s] * 6;
+    const int frame = c->frame + 1;
+    int n_trk = c->n_trk;
+    int *list = a.list + tb;
+    const int *udet = a.udet + ub;
+    const int n_ud = c->n_ud, n_upd = c->n_upd;
+    const long long eb = (long long)s * (a.CAP + a.MAXD);
+    YTA_STAMP_BASE(40);
     // ---- births in unmatched-list order (:495-503)
     int n_free = c->n_free;
     int n_b = n_ud;
@@ -1037,6 +1066,10 @@ int doc_launch(yta_deepocsort *e, const double *d_dets, const int *d_off, const 
                        e->stream, a);
     YTA_HIP(hipGetLastError());
     hipLaunchKernelGGL(k_doc_assoc, dim3(a.S), dim3(OC_T), e->lds, e->stream, a);
+    YTA_HIP(hipGetLastError());
+    hipLaunchKernelGGL(k_doc_upd, dim3((a.CAP + 255) / 256, a.S), dim3(256), 0, e->stream, a);
+    YTA_HIP(hipGetLastError());
+    hipLaunchKernelGGL(k_doc_finish, dim3(a.S), dim3(OC_T), 0, e->stream, a);
     YTA_HIP(hipGetLastError());
     if (!a.embedding_off) {
         const dim3 gj((a.CAP + a.MAXD + 3) / 4, a.S);

@@ -533,6 +533,38 @@ __global__ __launch_bounds__(LAP_T) void k_hs_lap(HsArgs a) {
                     &c->lap_done);
 }
 
+// HybridSORT's long-term correction (hybridsort/association.py:557-567): a first-round pair (kept
+// detection i, tracker k) is undone when emb > 0.4 and iou - |kalman score - score| < thr.
+__device__ __forceinline__ bool hs_corrected(const HsArgs &a, int s, int i, int k, int n_trk) {
+    const long long tb = (long long)s * a.CAP, db = (long long)s * a.MAXD;
+    const double e = a.emat[hs_mb(a, s) + (long long)i * n_trk + k];
+    if (!(e > HS_CORR_THRESH)) return false;
+    const double *dr = a.det_in + ((long long)a.det_off[s] + a.hi_row[db + i]) * 6;
+    const HsCol &q = a.col[tb + k];
+    const double v = asso_of(a.asso, box5(dr), Box{q.box[0], q.box[1], q.box[2], q.box[3]}, 0.0,
+                             0.0);
+    const double sd = fabs(q.kscore - dr[4]);
+    return (v - sd) < a.thr;
+}
+
+// First-round Kalman updates (hybridsort.py:462-464) chip-wide, one thread per kept detection,
+// when k_hs_lap solved the first round (else k_hs_assoc updates after its own solve).  A tracker
+// is matched at most once and the updates only touch its record, so they are independent.
+__global__ __launch_bounds__(256) void k_hs_upd(HsArgs a) {
+    const int s = blockIdx.y;
+    const HsCounters *c = a.cnt + s;
+    const int n_trk = c->n_trk, n_hi = c->n_high;
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (!c->lap_done || i >= n_hi || n_trk == 0) return;
+    const long long tb = (long long)s * a.CAP, db = (long long)s * a.MAXD;
+    const int k = a.rmatch[db + i];
+    if (k < 0 || hs_corrected(a, s, i, k, n_trk)) return;
+    const double *din = a.det_in + (long long)a.det_off[s] * 6;
+    // cls / det_ind from dets0 row i of the input (filtered position, :464)
+    hs_update(a.rec[tb + a.list[tb + k]], din + (long long)a.hi_row[db + i] * 6,
+              din[(long long)i * 6 + 5], din[(long long)i * 6 + 4], a.delta_t);
+}
+
 __global__ __launch_bounds__(OC_T) void k_hs_assoc(HsArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     __shared__ OcShared sh;
@@ -548,7 +580,6 @@ __global__ __launch_bounds__(OC_T) void k_hs_assoc(HsArgs a) {
     const int n_hi = c->n_high;
     const int dt = a.delta_t;
     int *list = a.list + tb;
-    const HsCol *col = a.col + tb;
     double *cost = a.cost + mb, *emat = a.emat + mb;
     int *udet = a.udet + ub, *utrk = a.utrk + ub;
     int n_ud = 0, n_ut = 0;
@@ -586,15 +617,7 @@ __global__ __launch_bounds__(OC_T) void k_hs_assoc(HsArgs a) {
         // long-term correction (:557-567): emb > 0.4 and iou - |kalman score - score| < thr
         auto corrected = [&](int i) {
             const int k = a.rmatch[db + i];
-            if (k < 0) return false;
-            const double e = emat[(long long)i * n_trk + k];
-            if (!(e > HS_CORR_THRESH)) return false;
-            const double *dr = hrow(i);
-            const HsCol &q = col[k];
-            const double v = asso_of(a.asso, box5(dr), Box{q.box[0], q.box[1], q.box[2], q.box[3]},
-                                     0.0, 0.0);
-            const double sd = fabs(q.kscore - dr[4]);
-            return (v - sd) < a.thr;
+            return k >= 0 && hs_corrected(a, s, i, k, n_trk);
         };
         n_corr = block_compact(n_hi, sh.wsum, corrected, [&](int i, int pos) {
             udet[n_ud + pos] = i;
@@ -616,12 +639,14 @@ __global__ __launch_bounds__(OC_T) void k_hs_assoc(HsArgs a) {
                                         a.ema_slot[eb + pos] = list[j];
                                         a.ema_row[eb + pos] = a.upd[tb + j];
                                     });
-    for (int j = t; j < n_trk; j += nt) {
-        const int p = a.upd[tb + j];
-        if (p >= 0) {
-            // cls / det_ind from dets0 row p of the input (filtered position, :464)
-            hs_update(a.rec[tb + list[j]], hrow(p), din[(long long)p * 6 + 5],
-                      din[(long long)p * 6 + 4], dt);
+    if (!c->lap_done) {   // else applied chip-wide by k_hs_upd
+        for (int j = t; j < n_trk; j += nt) {
+            const int p = a.upd[tb + j];
+            if (p >= 0) {
+                // cls / det_ind from dets0 row p of the input (filtered position, :464)
+                hs_update(a.rec[tb + list[j]], hrow(p), din[(long long)p * 6 + 5],
+                          din[(long long)p * 6 + 4], dt);
+            }
         }
     }
     block_sync();
@@ -956,6 +981,8 @@ int hs_launch(yta_hybridsort *e, const double *d_dets, const int *d_off, const f
     }
     hipLaunchKernelGGL(k_hs_lap, dim3(a.S), dim3(LAP_T), (size_t)lap_kernel_lds(a.CAP, a.MAXD),
                        e->stream, a);
+    YTA_HIP(hipGetLastError());
+    hipLaunchKernelGGL(k_hs_upd, dim3((a.MAXD + 255) / 256, a.S), dim3(256), 0, e->stream, a);
     YTA_HIP(hipGetLastError());
     hipLaunchKernelGGL(k_hs_assoc, dim3(a.S), dim3(OC_T), e->lds, e->stream, a);
     YTA_HIP(hipGetLastError());
