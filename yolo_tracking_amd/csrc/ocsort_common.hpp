@@ -138,7 +138,10 @@ __device__ __forceinline__ void iou_lap(const LapMat &M, int *rx, unsigned char 
     rect_solve(R, nullptr, nullptr, nullptr, tr, M.na, rx, lds, lds_bytes, gws, err);
 }
 
-constexpr int LAP_T = 512;                      // threads of the first-round solve kernels
+#ifndef YTA_LAP_T
+#define YTA_LAP_T 512
+#endif
+constexpr int LAP_T = YTA_LAP_T;                // threads of the first-round solve kernels
 constexpr long long LAP_LDS_MAX = 156 * 1024;   // their dynamic LDS cap (160 KiB - static)
 
 __host__ __device__ inline long long lap_kernel_lds(long long CAP, long long MAXD) {
