@@ -1630,6 +1630,18 @@ __global__ __launch_bounds__(256) void k_pack_out(const double *src, long long c
     for (long long k = threadIdx.x; k < n2; k += blockDim.x) b[k] = a[k];
 }
 
+// Host-buffer update of a small engine: the packed rows' offsets from the streams' output counts
+// on the device (one thread: S is small here), so rows and counters come back in one round trip.
+__global__ void k_out_offsets(const BtCounters *cnt, int S, int cap, int *off) {
+    if (threadIdx.x != 0) return;
+    int r = 0;
+    off[0] = 0;
+    for (int s = 0; s < S; ++s) {   // clamped: a stream with error flags may hold any count
+        r += min(max(cnt[s].n_out, 0), cap);
+        off[s + 1] = r;
+    }
+}
+
 __global__ __launch_bounds__(BLKF) void k_rebuild_free(BtArgs a) {
     __shared__ int wsum[32];
     extern __shared__ __attribute__((aligned(16))) unsigned int live[];
@@ -2143,6 +2155,28 @@ static bool identity_warps(const double *w, int S) {
     return true;
 }
 
+constexpr long long SMALL_PACK_BYTES = 1LL << 20;   // single-round-trip host update below this
+
+// Device / pinned buffers for packed output rows (at least `rows`) and the S + 1 offsets.
+int ensure_pack(yta_bytetrack *e, long long rows) {
+    if (rows <= e->pack_cap && e->d_pack_off) return YTA_OK;
+    if (e->d_pack) (void)hipFree(e->d_pack);
+    if (e->h_pack) (void)hipHostFree(e->h_pack);
+    if (e->d_pack_off) (void)hipFree(e->d_pack_off);
+    if (e->h_pack_off) (void)hipHostFree(e->h_pack_off);
+    e->d_pack = e->h_pack = nullptr;
+    e->d_pack_off = e->h_pack_off = nullptr;
+    e->pack_cap = 0;
+    const long long cap = std::max<long long>(rows, 1024);
+    const int S = e->S;
+    YTA_HIP(hipMalloc((void **)&e->d_pack, sizeof(double) * 8 * cap));
+    YTA_HIP(hipHostMalloc((void **)&e->h_pack, sizeof(double) * 8 * cap, hipHostMallocDefault));
+    YTA_HIP(hipMalloc((void **)&e->d_pack_off, sizeof(int) * (S + 1)));
+    YTA_HIP(hipHostMalloc((void **)&e->h_pack_off, sizeof(int) * (S + 1), hipHostMallocDefault));
+    e->pack_cap = cap;
+    return YTA_OK;
+}
+
 int update_host(yta_bytetrack *e, const double *dets, const int *det_offsets, const float *feats,
                 long long *next_id, double *out, int out_capacity, int *out_offsets,
                 const double *warps = nullptr) {
@@ -2233,6 +2267,38 @@ int update_host(yta_bytetrack *e, const double *dets, const int *det_offsets, co
     }
     int rc = launch_pipeline(e, e->d_det_in, e->d_det_off, e->a.out, nullptr, e->d_feat_in);
     if (rc) return rc;
+    // Small engines (every stream's worst-case rows <= 1 MiB, e.g. one camera stream): rows packed
+    // at device-computed offsets and copied back with the counters, one round trip per frame
+    const long long worst = (long long)S * e->CAP;
+    if (worst * 64 <= SMALL_PACK_BYTES) {
+        rc = ensure_pack(e, worst);
+        if (rc) return rc;
+        hipLaunchKernelGGL(k_out_offsets, dim3(1), dim3(64), 0, e->stream, e->a.cnt, S,
+                           e->CAP, e->d_pack_off);
+        hipLaunchKernelGGL(k_pack_out, dim3(S), dim3(256), 0, e->stream, e->a.out,
+                           (long long)e->CAP, e->d_pack_off, e->d_pack);
+        YTA_HIP(hipGetLastError());
+        YTA_HIP(hipMemcpyAsync(e->h_cnt, e->a.cnt, sizeof(BtCounters) * S, hipMemcpyDeviceToHost,
+                               e->stream));
+        YTA_HIP(hipMemcpyAsync(e->h_pack, e->d_pack, sizeof(double) * 8 * worst,
+                               hipMemcpyDeviceToHost, e->stream));
+        YTA_HIP(host_wait(e->stream));
+        if (next_id)   // the device counters have advanced: hand them back even on an error below
+            for (int q = 0; q < S; ++q) next_id[q] = e->h_cnt[q].next_id;
+        rc = check_errors(e);
+        if (rc) return rc;
+        long long rows = 0;
+        out_offsets[0] = 0;
+        for (int q = 0; q < S; ++q) {
+            rows += e->h_cnt[q].n_out;
+            out_offsets[q + 1] = (int)rows;
+        }
+        YTA_CHECK(rows <= out_capacity, YTA_ERR_CAPACITY, "output needs %lld rows > capacity %d",
+                  rows, out_capacity);
+        YTA_CHECK(rows == 0 || out, YTA_ERR_INVALID, "null out");
+        if (rows > 0) memcpy(out, e->h_pack, sizeof(double) * 8 * rows);
+        return YTA_OK;
+    }
     rc = read_counters(e);
     if (rc) return rc;
     if (next_id)   // the device counters have advanced: hand them back even on an error below
@@ -2249,21 +2315,8 @@ int update_host(yta_bytetrack *e, const double *dets, const int *det_offsets, co
               out_capacity);
     YTA_CHECK(rows == 0 || out, YTA_ERR_INVALID, "null out");
     if (rows > 0) {   // pack on the device, one copy back through pinned staging
-        if (rows > e->pack_cap || !e->d_pack_off) {
-            if (e->d_pack) (void)hipFree(e->d_pack);
-            if (e->h_pack) (void)hipHostFree(e->h_pack);
-            if (e->d_pack_off) (void)hipFree(e->d_pack_off);
-            if (e->h_pack_off) (void)hipHostFree(e->h_pack_off);
-            e->d_pack = e->h_pack = nullptr;
-            e->d_pack_off = e->h_pack_off = nullptr;
-            e->pack_cap = 0;
-            const long long cap = std::max<long long>(2 * rows, 1024);
-            YTA_HIP(hipMalloc((void **)&e->d_pack, sizeof(double) * 8 * cap));
-            YTA_HIP(hipHostMalloc((void **)&e->h_pack, sizeof(double) * 8 * cap, hipHostMallocDefault));
-            YTA_HIP(hipMalloc((void **)&e->d_pack_off, sizeof(int) * (S + 1)));
-            YTA_HIP(hipHostMalloc((void **)&e->h_pack_off, sizeof(int) * (S + 1), hipHostMallocDefault));
-            e->pack_cap = cap;
-        }
+        rc = ensure_pack(e, 2 * rows);
+        if (rc) return rc;
         memcpy(e->h_pack_off, out_offsets, sizeof(int) * (S + 1));
         YTA_HIP(hipMemcpyAsync(e->d_pack_off, e->h_pack_off, sizeof(int) * (S + 1),
                                hipMemcpyHostToDevice, e->stream));
