@@ -181,10 +181,12 @@ def pcie_inclusive(host, off, S, N, device, frames=8):
     output rows back to the host every call, synchronous), on a fresh engine: rank 0's report
     of the PCIe-inclusive rate.  Never `value`."""
     from yolo_tracking_amd import ByteTrackEngine, _lib
+    # capacity 3N: the host path reserves ahead of need (tracked + lost + this frame's dets,
+    # ~2.2N in the steady state) and would otherwise regrow the engine on the first frames
     eng = ByteTrackEngine(S, track_thresh=0.5, match_thresh=0.8, track_buffer=30, frame_rate=30,
-                          device=device, track_capacity=2 * N, max_dets=N)
+                          device=device, track_capacity=3 * N, max_dets=N)
     lib, h = eng.lib, eng.handle
-    out = np.empty((S * 2 * N, 8))
+    out = np.empty((S * N, 8))   # <= one row per detection
     out_off = np.zeros(S + 1, np.int32)
     nid = np.zeros(S, np.int64)
     frames = min(frames, len(host))
