@@ -2157,7 +2157,8 @@ static bool identity_warps(const double *w, int S) {
 
 constexpr long long SMALL_PACK_BYTES = 1LL << 20;   // single-round-trip host update below this
 
-// Device / pinned buffers for packed output rows (at least `rows`) and the S + 1 offsets.
+// Device / pinned buffers for packed output rows (at least `rows`; grown to twice that, so a
+// slowly growing output does not reallocate every frame) and the S + 1 offsets.
 int ensure_pack(yta_bytetrack *e, long long rows) {
     if (rows <= e->pack_cap && e->d_pack_off) return YTA_OK;
     if (e->d_pack) (void)hipFree(e->d_pack);
@@ -2167,7 +2168,7 @@ int ensure_pack(yta_bytetrack *e, long long rows) {
     e->d_pack = e->h_pack = nullptr;
     e->d_pack_off = e->h_pack_off = nullptr;
     e->pack_cap = 0;
-    const long long cap = std::max<long long>(rows, 1024);
+    const long long cap = std::max<long long>(2 * rows, 1024);
     const int S = e->S;
     YTA_HIP(hipMalloc((void **)&e->d_pack, sizeof(double) * 8 * cap));
     YTA_HIP(hipHostMalloc((void **)&e->h_pack, sizeof(double) * 8 * cap, hipHostMallocDefault));
@@ -2315,7 +2316,7 @@ int update_host(yta_bytetrack *e, const double *dets, const int *det_offsets, co
               out_capacity);
     YTA_CHECK(rows == 0 || out, YTA_ERR_INVALID, "null out");
     if (rows > 0) {   // pack on the device, one copy back through pinned staging
-        rc = ensure_pack(e, 2 * rows);
+        rc = ensure_pack(e, rows);
         if (rc) return rc;
         memcpy(e->h_pack_off, out_offsets, sizeof(int) * (S + 1));
         YTA_HIP(hipMemcpyAsync(e->d_pack_off, e->h_pack_off, sizeof(int) * (S + 1),
