@@ -69,10 +69,14 @@ def test_synthetic_golden_and_kf_state(golden_dir, case):
     np.testing.assert_allclose(st["cov"], g[f"{case}__st_cov"], rtol=1e-5, atol=1e-5)
 
 
-def test_multistream_matches_independent_oracles():
+# default capacity: the host update's single round trip (worst-case rows <= 1 MiB); 4096: rows
+# packed at host-computed offsets after a counters read (worst case 5 x 4096 x 64 B > 1 MiB)
+@pytest.mark.parametrize("cap", [None, 4096])
+def test_multistream_matches_independent_oracles(cap):
     S, N, F = 5, 200, 25
     streams = [[d for d, _ in make_frames(N + 40 * s, F, seed=100 + s)] for s in range(S)]
-    eng = ByteTrackEngine(S, **KW)
+    eng = ByteTrackEngine(S, **KW) if cap is None else ByteTrackEngine(
+        S, track_capacity=cap, max_dets=512, **KW)
     refs = [ByteTrackOracle(**KW) for _ in range(S)]
     for f in range(F):
         outs = eng.update([streams[s][f] for s in range(S)])
