@@ -139,6 +139,8 @@ def parse():
     p.add_argument("--n", type=int, default=1024, help="tracks = detections per frame")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-pcie", action="store_true", help="skip the host-buffer (PCIe) leg")
+    p.add_argument("--no-isolated", action="store_true",
+                   help="skip the engine-0-alone frames after the timed region (profiling runs)")
     p.add_argument("--cpu-frames", type=int, default=40)
     p.add_argument("--seed", type=int, default=1000)
     p.add_argument("--queues", type=int, default=2,
@@ -226,23 +228,27 @@ def main():
     from yolo_tracking_amd import ByteTrackEngine, _lib
     S, N = args.streams, args.n
     F = args.warmup + args.steps
-    # synthetic frames for this rank's streams, staged in HBM: [F][S*N][6] + offsets
+    Q = max(1, args.queues)
+    # with Q > 1 engines, ISO more frames after the timed region run on engine 0 alone: the
+    # roofline kernel's rate without the other engines' overlap (reported beside, never `value`)
+    ISO = 3 if Q > 1 and not args.no_isolated else 0
+    FT = F + ISO
+    # synthetic frames for this rank's streams, staged in HBM: [FT][S*N][6] + offsets
     t_gen = time.time()
-    per_stream = [gen_stream_frames(N, F, sd) for sd in stream_seeds(args.seed, rank, S)]
-    host = np.stack([np.concatenate([per_stream[s][f] for s in range(S)]) for f in range(F)])
-    counts = np.array([[len(per_stream[s][f]) for s in range(S)] for f in range(F)])
-    off = np.zeros((F, S + 1), dtype=np.int32)
+    per_stream = [gen_stream_frames(N, FT, sd) for sd in stream_seeds(args.seed, rank, S)]
+    host = np.stack([np.concatenate([per_stream[s][f] for s in range(S)]) for f in range(FT)])
+    counts = np.array([[len(per_stream[s][f]) for s in range(S)] for f in range(FT)])
+    off = np.zeros((FT, S + 1), dtype=np.int32)
     np.cumsum(counts, axis=1, out=off[:, 1:])
     del per_stream, counts
     # Q engines (each its own HIP stream) over contiguous slices of the streams: their launches
     # run concurrently, so one engine's latency-bound block chains overlap the other's
-    Q = max(1, args.queues)
     assert S % Q == 0, "--streams must be a multiple of --queues"
     Sq = S // Q
     d_dets, d_off = [], []
     for q in range(Q):
         lo, hi = off[:, q * Sq], off[:, (q + 1) * Sq]
-        dq = np.stack([host[f, lo[f]:hi[f]] for f in range(F)]) if len(set(hi - lo)) == 1 else None
+        dq = np.stack([host[f, lo[f]:hi[f]] for f in range(FT)]) if len(set(hi - lo)) == 1 else None
         assert dq is not None, "synthetic frames have N detections per stream"
         d_dets.append(torch.from_numpy(np.ascontiguousarray(dq)).to("cuda"))
         d_off.append(torch.from_numpy(np.ascontiguousarray(off[:, q * Sq:(q + 1) * Sq + 1]
@@ -260,8 +266,8 @@ def main():
     h = handles[0]
     row_bytes = N * 6 * 8 * Sq
 
-    def step(f):
-        for q in range(Q):
+    def step(f, engines=None):
+        for q in (range(Q) if engines is None else engines):
             _lib.check(lib.yta_bytetrack_update_device(
                 handles[q], ctypes.c_void_p(d_dets[q].data_ptr() + f * row_bytes),
                 ctypes.c_void_p(d_off[q].data_ptr() + f * (Sq + 1) * 4),
@@ -290,6 +296,13 @@ def main():
     phase_ms = {PHASES[k]: ms[k] / max(nfr.value, 1) for k in range(len(PHASES))}
     for hq in handles[1:]:
         _lib.check(lib.yta_bytetrack_profile_collect(hq, ms, ctypes.byref(nfr)))
+    iso_ms = None
+    if ISO:   # after the timed region: engine 0 alone (the other engines idle) for ISO frames
+        sync_all()
+        for f in range(F, FT):
+            step(f, engines=[0])
+        _lib.check(lib.yta_bytetrack_profile_collect(h, ms, ctypes.byref(nfr)))
+        iso_ms = {PHASES[k]: ms[k] / max(nfr.value, 1) for k in range(len(PHASES))}
 
     elapsed = max_over_ranks(elapsed, dist, "cuda")
     value = aggregate_rate(world, S, args.steps, elapsed)
@@ -333,6 +346,13 @@ def main():
                          # every kernel of every engine: measured HBM bytes per step / step time
                          "chip_gbs": (step_traffic / (ms_per_step * 1e-3) / 1e9
                                       if step_traffic else None),
+                         "isolated": (None if iso_ms is None else {
+                             "avg_launch_ms": iso_ms[dom],
+                             "achieved": b / (iso_ms[dom] * 1e-3) / 1e9,
+                             "frac": b / (iso_ms[dom] * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                             "frames": ISO,
+                             "note": "engine 0 alone for the frames after the timed region, "
+                                     "same algorithmic bytes per launch"}),
                          "note": (None if Q == 1 else
                                   f"{Q} engines of {S // Q} streams on {Q} HIP streams: each "
                                   "launch overlaps the other engines' kernels, so its duration "
