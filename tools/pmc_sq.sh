@@ -8,7 +8,7 @@ R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/pmc_sq
 mkdir -p $O
 run() {
-  timeout -k 10 300 rocprofv3 --pmc $2 --output-format csv -d $O/$1 -o run -- python3 $R/bench.py --streams $S --steps 4 --warmup 2 --no-cpu-baseline > $O/$1.log 2>&1
+  timeout -k 10 300 rocprofv3 --pmc $2 --output-format csv -d $O/$1 -o run -- python3 $R/bench.py --streams $S --queues 1 --steps 4 --warmup 2 --no-cpu-baseline --no-pcie --no-isolated > $O/$1.log 2>&1
 }
 run p1 "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_VALU"
 run p2 "SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_SMEM"
