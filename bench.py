@@ -6,17 +6,28 @@
 A step = one `tracker.update()` frame for every one of the S independent streams on each GPU
 (each stream: 1024 tracks x 1024 detections per frame, SURVEY.md §8(d) synthetic generator).
 All frames are staged in HBM before the timed region; the engine's device-buffer entry point
-runs the whole update on the GPU (outputs stay in HBM).  N > 1: one process per GPU
-(torch.distributed.run), streams sharded per rank, no data-path collective, barrier + max over
-ranks around the timed region (scaling "weak": per-GPU work is fixed).
+runs the whole update on the GPU (outputs stay in HBM).  Before the W warmup frames, `--preroll`
+frames (default 35 > max_time_lost = 30, byte_tracker.py:128-129) run untimed, so the timed
+frames see the steady state: Lost tracks expire as fast as they are created.
 
-Rank 0 prints one JSON line with `roofline` (dominant kernel, HIP events on the engine stream)
-and `cpu_baseline` (the oracle's CPU restatement on this host, 1 core, bounded sample).
+N > 1: one process per GPU, streams sharded per rank with disjoint seeds, no data-path
+collective, barrier + max over ranks around the timed region (scaling "weak": per-GPU work is
+fixed).  Launched either by torch.distributed.run (RANK / LOCAL_RANK / WORLD_SIZE in the
+environment) or directly as `bench.py --gpus N`: the parent then starts N rank processes itself
+(before it touches torch or the GPU) and waits for them, the way examples/val.py:147-226 starts one
+process per sequence and device.  `--dry-cpu` runs the same harness on CPU ranks over gloo with a
+NumPy stand-in step (tests/test_bench_harness.py).
+
+Rank 0 prints one JSON line with `roofline` (dominant kernel, HIP events on the engine stream),
+`pcie_inclusive` (host buffers in and out every call) and `cpu_baseline` (the oracle's CPU
+restatement on this host: 1 core and all cores, bounded sample).
 """
 import argparse
 import ctypes
 import json
 import os
+import platform
+import socket
 import subprocess
 import sys
 import time
@@ -28,7 +39,8 @@ sys.path.insert(0, REPO)
 
 PHASES = ["s1_prep", "s1_edges", "s1_lap", "stage23", "apply", "finish"]
 STATS = ["dets", "high", "second", "pool", "act", "unc", "left", "rest", "births", "t2", "l2",
-         "tracked", "lost", "out", "edges1", "edges23", "fallback1", "fallback23", "lazy", "res1"]
+         "tracked", "lost", "out", "edges1", "edges23", "fallback1", "fallback23", "lazy", "res1",
+         "fallback_f"]
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # Canonical algorithmic bytes per update: ByteTrack 1024 x 1024
 BYTES_PER_UPDATE_1024 = 19_259_392
@@ -130,11 +142,13 @@ def aggregate_rate(world, streams, steps, elapsed):
     return world * streams * steps / elapsed
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=30)
     p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--preroll", type=int, default=35,
+                   help="untimed frames before the warmup (steady state: > max_time_lost = 30)")
     p.add_argument("--streams", type=int, default=2048, help="streams per GPU")
     p.add_argument("--n", type=int, default=1024, help="tracks = detections per frame")
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -145,7 +159,65 @@ def parse():
     p.add_argument("--seed", type=int, default=1000)
     p.add_argument("--queues", type=int, default=2,
                    help="engines per GPU, each on its own HIP stream, streams split between them")
-    return p.parse_args()
+    p.add_argument("--dry-cpu", action="store_true",
+                   help="harness rehearsal: CPU ranks over gloo, NumPy stand-in step, no GPU")
+    return p.parse_args(argv)
+
+
+# ---------------------------------------------------------------- rank launcher (--gpus N)
+def free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(argv, n):
+    """Start n rank processes of this script (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_*), wait
+    for all of them, and return the first non-zero exit status.  Runs before anything touches
+    torch or the GPU; if one rank fails the others are stopped (they would wait at a barrier)."""
+    port = free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv),
+                                      env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            r = p.poll()
+            if r is None:
+                continue
+            live.remove(p)
+            if r != 0 and rc == 0:
+                rc = r
+                for q in live:
+                    q.terminate()
+        time.sleep(0.05)
+    return rc
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or None
+
+
+def cpu_share():
+    """Host cores this job may use: the affinity mask, capped by OMP_NUM_THREADS when the
+    environment sets it (16 per GPU on the GPU box)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return max(1, n)
 
 
 def gen_stream_frames(n, frames, seed):
@@ -153,35 +225,58 @@ def gen_stream_frames(n, frames, seed):
     return [d for d, _ in make_frames(n, frames, seed)]
 
 
+_CPU_LEG = (
+    "import sys,time,json; sys.path.insert(0,%r)\n"
+    "from oracle.bytetrack import ByteTrackOracle\n"
+    "from yolo_tracking_amd.synth import make_frames\n"
+    "fr=[d for d,_ in make_frames(%d,%d,%d)]\n"
+    "t=ByteTrackOracle(0.5,0.8,30,30); t.update(fr[0])\n"
+    "t0=time.perf_counter()\n"
+    "for d in fr[1:]: t.update(d)\n"
+    "dt=time.perf_counter()-t0\n"
+    "print(json.dumps({'frames':len(fr)-1,'seconds':dt}))\n")
+
+
 def cpu_baseline(n, frames, seed):
-    """Time the oracle (CPU restatement: NumPy ByteTrack + C lapjv) on one stream, 1 thread."""
+    """Time the oracle (CPU restatement: NumPy ByteTrack + C lapjv, the cpu_baseline leg is the
+    only place bench.py runs it) on this host: one stream on 1 thread, then one stream per core
+    of this job's CPU share, all at once (1 core + all cores, CPU model)."""
     env = dict(os.environ, OMP_NUM_THREADS="1", OPENBLAS_NUM_THREADS="1", MKL_NUM_THREADS="1")
-    code = (
-        "import sys,time,json; sys.path.insert(0,%r)\n"
-        "from oracle.bytetrack import ByteTrackOracle\n"
-        "from yolo_tracking_amd.synth import make_frames\n"
-        "fr=[d for d,_ in make_frames(%d,%d,%d)]\n"
-        "t=ByteTrackOracle(0.5,0.8,30,30); t.update(fr[0])\n"
-        "t0=time.perf_counter()\n"
-        "for d in fr[1:]: t.update(d)\n"
-        "dt=time.perf_counter()-t0\n"
-        "print(json.dumps({'frames':len(fr)-1,'seconds':dt}))\n" % (REPO, n, frames, seed))
+    P = cpu_share()
+
+    def start(sd):
+        return subprocess.Popen([sys.executable, "-c", _CPU_LEG % (REPO, n, frames, sd)], env=env,
+                                stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+
+    def result(proc):
+        out, _ = proc.communicate(timeout=900)
+        return json.loads(out.strip().splitlines()[-1])
+
+    base = {"unit": "calls/s", "kind": "port", "cpu_model": cpu_model()}
     try:
-        r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
-                           timeout=900)
-        res = json.loads(r.stdout.strip().splitlines()[-1])
+        one = result(start(seed))
     except Exception as exc:  # report, never fail the bench on the baseline leg
-        return {"value": None, "unit": "calls/s", "cores": 1, "kind": "port",
-                "sample": f"failed: {exc}"}
-    return {"value": res["frames"] / res["seconds"], "unit": "calls/s", "cores": 1, "kind": "port",
-            "sample": f"oracle ByteTrack (NumPy + C lapjv), 1 stream {n}x{n}, frames 2..{frames} "
-                      f"of seed {seed}, {res['seconds']:.1f} s, 1 thread"}
+        return dict(base, value=None, cores=1, sample=f"failed: {exc}")
+    line = dict(base, value=one["frames"] / one["seconds"], cores=1,
+                sample=f"oracle ByteTrack (NumPy + C lapjv), 1 stream {n}x{n}, frames 2..{frames} "
+                       f"of seed {seed}, {one['seconds']:.1f} s, 1 thread")
+    try:
+        res = [result(p) for p in [start(seed + k) for k in range(P)]]
+        line["all_cores"] = {
+            "value": sum(r["frames"] for r in res) / max(r["seconds"] for r in res),
+            "cores": P, "processes": P,
+            "sample": f"{P} processes at once, one stream each (seeds {seed}..{seed + P - 1}), "
+                      f"frames 2..{frames}, 1 thread each; total frames / slowest process"}
+    except Exception as exc:
+        line["all_cores"] = {"value": None, "cores": P, "sample": f"failed: {exc}"}
+    return line
 
 
-def pcie_inclusive(host, off, S, N, device, frames=8):
+def pcie_inclusive(host, off, S, N, device, first, frames=8):
     """The same workload through the host-buffer ABI (yta_bytetrack_update: packed host dets in,
-    output rows back to the host every call, synchronous), on a fresh engine: rank 0's report
-    of the PCIe-inclusive rate.  Never `value`."""
+    output rows back to the host every call, synchronous) on a fresh engine, frames 0..first-1
+    untimed (steady state), then `frames` timed calls: rank 0's report of the PCIe-inclusive
+    rate.  Never `value`."""
     from yolo_tracking_amd import ByteTrackEngine, _lib
     # capacity 3N: the host path reserves ahead of need (tracked + lost + this frame's dets,
     # ~2.2N in the steady state) and would otherwise regrow the engine on the first frames
@@ -191,33 +286,81 @@ def pcie_inclusive(host, off, S, N, device, frames=8):
     out = np.empty((S * N, 8))   # <= one row per detection
     out_off = np.zeros(S + 1, np.int32)
     nid = np.zeros(S, np.int64)
-    frames = min(frames, len(host))
-    dets = [np.ascontiguousarray(host[f]) for f in range(frames)]
-    offs = [np.ascontiguousarray(off[f]) for f in range(frames)]
+    last = min(first + frames, len(host))
 
     def call(f):
-        _lib.check(lib.yta_bytetrack_update(h, dets[f].ctypes.data, offs[f].ctypes.data,
+        _lib.check(lib.yta_bytetrack_update(h, host[f].ctypes.data, off[f].ctypes.data,
                                             nid.ctypes.data, out.ctypes.data, len(out),
                                             out_off.ctypes.data))
-    call(0)
-    call(1)
+    for f in range(first):
+        call(f)
     dts = []
-    for f in range(2, frames):
+    for f in range(first, last):
         t0 = time.perf_counter()
         call(f)
         dts.append(time.perf_counter() - t0)
     dt = float(np.median(dts))
-    return {"value": S / dt, "unit": "calls/s", "steps": frames - 2,
+    return {"value": S / dt, "unit": "calls/s", "steps": len(dts), "untimed_frames": first,
             "ms_per_step": 1000 * dt, "ms_per_step_all": [round(1000 * x, 3) for x in dts],
+            "bytes_h2d_per_step": int(off[first, -1]) * 48,
             "note": "host-buffer ABI: packed dets host->device and output rows device->host "
-                    "inside every step (pageable numpy buffers); median step"}
+                    "inside every step (pageable numpy buffers, one engine of all streams); "
+                    "median step"}
+
+
+def run_dry(args, world, rank):
+    """--dry-cpu: the multi-rank harness end to end on CPU ranks (gloo): stream sharding, frame
+    staging, barrier-bracketed timed region, max over ranks, rank-0 JSON line.  The step is a
+    NumPy stand-in over the staged frames (no GPU, no tracker)."""
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo")
+    S, N = args.streams, args.n
+    seeds = stream_seeds(args.seed, rank, S)
+    F = args.preroll + args.warmup + args.steps
+    frames = [gen_stream_frames(N, F, sd) for sd in seeds]
+    acc = np.zeros(S)
+
+    def step(f):
+        for s in range(S):
+            acc[s] += frames[s][f][:, 4].sum()
+
+    for f in range(args.preroll + args.warmup):
+        step(f)
+
+    def run_steps():
+        for f in range(args.preroll + args.warmup, F):
+            step(f)
+
+    elapsed = timed_region(run_steps, lambda: None, dist)
+    elapsed = max_over_ranks(elapsed, dist, "cpu")
+    every = [seeds]
+    if dist:
+        every = [None] * world
+        dist.all_gather_object(every, seeds)
+    if rank == 0:
+        print(json.dumps({"metric": "dry-run harness", "value": aggregate_rate(world, S, args.steps,
+                                                                              elapsed),
+                          "unit": "calls/s", "n_gpus": world, "steps": args.steps,
+                          "warmup": args.warmup, "dry_run": True, "stream_seeds_by_rank": every,
+                          "checksum": float(acc.sum())}))
+    if dist:
+        dist.destroy_process_group()
 
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(sys.argv[1:], args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and rank == 0:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE {world}: using {world} ranks",
+              file=sys.stderr)
+    if args.dry_cpu:
+        return run_dry(args, world, rank)
     import torch
     torch.cuda.set_device(local_rank)
     dist = None
@@ -227,7 +370,8 @@ def main():
 
     from yolo_tracking_amd import ByteTrackEngine, _lib
     S, N = args.streams, args.n
-    F = args.warmup + args.steps
+    PRE = args.preroll + args.warmup          # untimed frames before the timed region
+    F = PRE + args.steps
     Q = max(1, args.queues)
     # with Q > 1 engines, ISO more frames after the timed region run on engine 0 alone: the
     # roofline kernel's rate without the other engines' overlap (reported beside, never `value`)
@@ -278,13 +422,14 @@ def main():
             _lib.check(lib.yta_bytetrack_sync(hq))
 
     torch.cuda.synchronize()
-    for f in range(args.warmup):
+    for f in range(PRE):
         step(f)
     sync_all()
     for hq in handles:
         _lib.check(lib.yta_bytetrack_profile(hq, 1))
+
     def run_steps():
-        for f in range(args.warmup, F):
+        for f in range(PRE, F):
             step(f)
         sync_all()
 
@@ -296,6 +441,13 @@ def main():
     phase_ms = {PHASES[k]: ms[k] / max(nfr.value, 1) for k in range(len(PHASES))}
     for hq in handles[1:]:
         _lib.check(lib.yta_bytetrack_profile_collect(hq, ms, ctypes.byref(nfr)))
+    # counters of the last timed frame (summed over the engines: all S streams)
+    stats = (ctypes.c_longlong * len(STATS))()
+    st = {k: 0 for k in STATS}
+    for hq in handles:
+        _lib.check(lib.yta_bytetrack_stats(hq, stats))
+        for k in range(len(STATS)):
+            st[STATS[k]] += int(stats[k])
     iso_ms = None
     if ISO:   # after the timed region: engine 0 alone (the other engines idle) for ISO frames
         sync_all()
@@ -308,12 +460,6 @@ def main():
     value = aggregate_rate(world, S, args.steps, elapsed)
     ms_per_step = 1000.0 * elapsed / args.steps
 
-    stats = (ctypes.c_longlong * len(STATS))()
-    st = {k: 0 for k in STATS}
-    for hq in handles:   # summed over the engines (all S streams)
-        _lib.check(lib.yta_bytetrack_stats(hq, stats))
-        for k in range(len(STATS)):
-            st[STATS[k]] += int(stats[k])
     st_launch = {k: v // Q for k, v in st.items()}   # one engine's launch (Q equal slices)
     if rank == 0:
         # roofline kernel: the longest launch of the frame (the Kalman pass k_apply, HBM-bound)
@@ -321,12 +467,16 @@ def main():
         dom_ms = phase_ms[dom]
         b = kernel_bytes(dom, st_launch)
         achieved = b / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
-        busiest = max(phase_ms, key=lambda p: phase_ms[p])
         per_kernel = {p: {"ms": phase_ms[p], "alg_bytes": kernel_bytes(p, st_launch),
                           "gbs": (kernel_bytes(p, st_launch) / (phase_ms[p] * 1e-3) / 1e9
                                   if phase_ms[p] > 0 else 0.0)} for p in PHASES}
+        # implemented minimum: what this build's six launches must move per update (the
+        # per-kernel figures above, summed, over the streams); SURVEY §8(d)'s canonical figure
+        # charges a dense N x M cost matrix and a 576-B Kalman state, neither of which exists here
+        impl_bytes = sum(kernel_bytes(p, st) for p in PHASES) / S
         cpu = None if args.no_cpu_baseline else cpu_baseline(N, args.cpu_frames, args.seed)
-        pcie = None if args.no_pcie else pcie_inclusive(host, off, S, N, local_rank)
+        pcie = (None if args.no_pcie else
+                pcie_inclusive(host, off, S, N, local_rank, first=min(PRE, FT - 8)))
         traffic, step_traffic, traffic_tag = pmc_traffic(S, N, Q)
         line = {
             "metric": "tracker.update() calls/sec @ 1024 tracks×1024 dets; 1/2/4/8 MI355X",
@@ -335,7 +485,16 @@ def main():
             "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
             "config": {"workload": f"bytetrack {N}x{N}, {S} streams/GPU, inputs resident in HBM",
                        "tracker": "bytetrack", "tracks": N, "dets": N, "streams_per_gpu": S,
-                       "queues_per_gpu": Q, "parallelism": f"stream-sharded x{world}"},
+                       "queues_per_gpu": Q, "parallelism": f"stream-sharded x{world}",
+                       "untimed_frames": PRE, "preroll": args.preroll,
+                       "timed_frames": f"{PRE + 1}..{F}",
+                       "per_stream_last_frame": {
+                           "pool": st["pool"] / S, "tracked": st["tracked"] / S,
+                           "lost": st["lost"] / S, "births": st["births"] / S,
+                           "out_rows": st["out"] / S},
+                       "value_is": "device-resident: frames staged in HBM before the timed "
+                                   "region, output rows left in HBM; the host-buffer rate "
+                                   "(dets in, rows out over PCIe every call) is pcie_inclusive"},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
@@ -357,13 +516,17 @@ def main():
                                   f"{Q} engines of {S // Q} streams on {Q} HIP streams: each "
                                   "launch overlaps the other engines' kernels, so its duration "
                                   "(and this per-launch rate) includes their share of the chip")},
-            "cpu_baseline": cpu,
             "pcie_inclusive": pcie,
+            "cpu_baseline": cpu,
             "per_kernel": per_kernel,
             "frame_counts": st,
-            "busiest_kernel": busiest,
-            "single_stream_equiv_ms": ms_per_step,
-            "algorithmic_bytes_per_update": algorithmic_bytes(N, N),
+            "busiest_kernel": dom,
+            "algorithmic_bytes_per_update": impl_bytes,
+            "algorithmic_bytes_note": "implemented minimum (sum of the six launches' algorithmic "
+                                      "bytes / streams); SURVEY §8(d)'s canonical figure "
+                                      "(dense_upper_bound) charges a dense 16*N*M cost matrix "
+                                      "and a 576-B Kalman state that this build never forms",
+            "dense_upper_bound_bytes_per_update": algorithmic_bytes(N, N),
             "stage_seconds": round(gen_s, 1),
         }
         print(json.dumps(line))

@@ -178,7 +178,9 @@ int yta_bytetrack_profile_collect(yta_bytetrack *engine, double *ms, int *frames
  * candidate edges, stage-2+3 candidate edges, then the cumulative number of stream-frames whose
  * stage-1 / stage-2+3 association did not fit in LDS and ran over global memory, then (ByteTrack)
  * the lost-list Kalman records the last frame left untouched (lazy prediction), then (ByteTrack)
- * the stage-1 candidate edges left to the solver after the single-edge components (20 int64). */
+ * the stage-1 candidate edges left to the solver after the single-edge components, then the
+ * cumulative number of stream-frames whose duplicate-removal grid (k_finish) did not fit in LDS
+ * (21 int64). */
 int yta_bytetrack_stats(yta_bytetrack *engine, long long *stats);
 /* Tuning / testing: bytes of LDS the association kernels may use per stream (default 150 KiB,
  * at most 150 KiB); a stream-frame that does not fit runs over global memory.  0 forces the

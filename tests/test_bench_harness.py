@@ -57,3 +57,23 @@ def test_two_rank_harness_gloo():
     job = jobs.pop()
     assert job >= max(r[2] for r in res) - 1e-9 and job >= 0.2
     assert res[0][4] == pytest.approx(world * 3 * 4 / job)
+
+
+def test_bench_launches_n_ranks_dry_cpu():
+    """`bench.py --gpus 2` starts two rank processes itself (no torchrun) and rank 0 reports
+    n_gpus = 2 with disjoint, contiguous stream seeds (--dry-cpu: gloo, NumPy stand-in step)."""
+    import json
+    import subprocess
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--dry-cpu",
+                        "--streams", "3", "--n", "32", "--steps", "3", "--warmup", "1",
+                        "--preroll", "2"], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout               # rank 0 alone prints
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["steps"] == 3 and d["dry_run"]
+    seeds = d["stream_seeds_by_rank"]
+    assert seeds == [[1000, 1001, 1002], [1003, 1004, 1005]]
+    assert d["value"] > 0

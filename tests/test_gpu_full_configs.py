@@ -1,0 +1,168 @@
+"""GPU: every BASELINE.json configuration at its stated size against the reference's full-size
+goldens (tests/golden/make_goldens_full.py: the reference imported and run at 1024 / 2048 / 4096).
+
+Bar: every frame's output rows (ids, order, boxes, conf, cls, det_ind) bit-exact (SHA-256 of
+the reference's rows, the last frame compared in full); final tracker states: ids exact,
+Kalman means bit-exact where the engine's arithmetic is the reference's operation for operation
+(ByteTrack, BoT-SORT, HybridSORT) and within the documented tolerances elsewhere (DeepOCSORT under
+a camera warp: 1e-9 relative, tests/test_gpu_deepocsort.py).  Multi-stream configs run all of
+their streams through one engine launch, each stream checked against its own golden.
+"""
+import numpy as np
+import pytest
+
+import full_configs as fc
+from test_oracle_golden import reid_features
+from yolo_tracking_amd.trackers.botsort import BoTSORTEngine
+from yolo_tracking_amd.trackers.bytetrack import ByteTrackEngine
+
+pytestmark = pytest.mark.gpu
+
+KW = dict(track_thresh=0.5, match_thresh=0.8, track_buffer=30, frame_rate=30)
+
+
+@pytest.fixture(scope="module")
+def g():
+    return fc.load()
+
+
+def test_bytetrack_1024_45_frames(g):
+    """The headline config past Lost-track expiry (max_time_lost 30, byte_tracker.py:250-253), as
+    bench.py runs it (capacity 2N, N detections per frame): every frame bit-exact, the final
+    tracked + lost lists and Kalman means bit-exact, and no stream-frame left the LDS arenas."""
+    name = "bt_n1024_f45"
+    frames = fc.bytetrack_frames(g, name)
+    eng = ByteTrackEngine(1, track_capacity=2048, max_dets=1024, **KW)
+    for f, d in enumerate(frames):
+        fc.check_frame(g, name, f, eng.update([d])[0])
+    st = eng.state(0)
+    assert np.array_equal(st["list"], g[f"{name}__st_list"])
+    assert np.array_equal(st["id"], g[f"{name}__st_id"])
+    assert np.array_equal(st["state"], g[f"{name}__st_state"])
+    assert np.array_equal(st["frame_id"], g[f"{name}__st_frame"])
+    assert np.array_equal(st["mean"], g[f"{name}__st_mean"])
+    assert np.array_equal(st["cov"][::64], g[f"{name}__st_cov_sample"])
+    s = eng.stats()
+    assert s["fallback1"] == 0 and s["fallback23"] == 0 and s["fallback_f"] == 0, s
+
+
+def test_bytetrack_1024_batched_streams(g):
+    """The same stream three times in one engine (and the headline's capacity): identical rows in
+    every copy, every frame."""
+    name = "bt_n1024_f45"
+    frames = fc.bytetrack_frames(g, name)
+    eng = ByteTrackEngine(3, track_capacity=2048, max_dets=1024, **KW)
+    for f, d in enumerate(frames):
+        outs = eng.update([d, d, d])
+        for o in outs:
+            fc.check_frame(g, name, f, o)
+
+
+def test_botsort_1024_d512(g):
+    """C3: BoT-SORT 1024 x 1024 with 512-d embeddings (fused IoU-gated cosine cost)."""
+    name = "bs_n1024_d512"
+    frames, params, D = fc.botsort_frames(g, name)
+    eng = BoTSORTEngine(1, feat_dim=D, **params)
+    for f, (dets, embs) in enumerate(frames):
+        feats = reid_features(dets, embs, params["track_high_thresh"])
+        fc.check_frame(g, name, f, eng.update([dets], [feats])[0])
+    st = eng.state(0)
+    assert np.array_equal(st["list"], g[f"{name}__st_list"])
+    assert np.array_equal(st["id"], g[f"{name}__st_id"])
+    assert np.array_equal(st["mean"], g[f"{name}__st_mean"])
+    assert np.array_equal(st["cov"][::64], g[f"{name}__st_cov_sample"])
+    feats, _, _ = eng.features(0)
+    np.testing.assert_allclose(feats[::64], g[f"{name}__st_feat_sample"], rtol=1e-5, atol=1e-6)
+
+
+# ------------------------------------------------------------------ C4 DeepOCSORT 2048 + CMC
+def test_deepocsort_2048_d512_cmc_four_streams(g):
+    """C4: four DeepOCSORT streams of 2048 x 2048 with 512-d embeddings and the fixed CMC warp,
+    one engine launch per frame, every stream against its own golden."""
+    from yolo_tracking_amd.trackers.deepocsort import DeepOCSortEngine
+    cases = [fc.deepocsort_frames(g, n) for n in fc.DOS_CMC]
+    kw, D = cases[0][2], cases[0][4]
+    assert all(c[2] == kw for c in cases)
+    S = len(cases)
+    eng = DeepOCSortEngine(S, feat_dim=D, **kw)
+    warps = np.stack([c[3] for c in cases])
+    nf = len(cases[0][0])
+    for f in range(nf):
+        outs = eng.update([c[0][f][0] for c in cases], [c[0][f][1] for c in cases], warps=warps,
+                          img_shapes=[c[1] for c in cases])
+        for s, name in enumerate(fc.DOS_CMC):
+            fc.check_frame(g, name, f, outs[s])
+    for s, name in enumerate(fc.DOS_CMC):
+        st = eng.state(s)
+        assert np.array_equal(st["id"], g[f"{name}__st_id"])
+        np.testing.assert_allclose(st["x"], g[f"{name}__st_x"], rtol=1e-9, atol=1e-9)
+        np.testing.assert_allclose(st["P"][::64], g[f"{name}__st_P_sample"], rtol=1e-9, atol=1e-9)
+        np.testing.assert_allclose(st["emb"][::64], g[f"{name}__st_emb_sample"], rtol=0,
+                                   atol=1e-12)
+
+
+def test_deepocsort_2048_detection_surge(g):
+    """A crowd entering: 2048 trackers meet ~3900 detections (more detections than trackers,
+    deep_ocsort.py:430-450 -> association.py:111-201 with dummy columns).  Against the reference
+    up to the numbering of same-frame births (lapx's tie-breaking among exactly-zero costs is
+    unpinned), and bit-exact against the oracle, which restates lapx's tie-breaking."""
+    from oracle.deepocsort import DeepOCSortOracle
+    from test_oracle_golden import canonical_equal
+    from yolo_tracking_amd.trackers.deepocsort import DeepOCSortEngine
+    name = "dos_n2048_surge"
+    frames, img_shape, kw, warp, D = fc.deepocsort_frames(g, name)
+    assert warp is None
+    eng = DeepOCSortEngine(1, feat_dim=D, **kw)
+    o = DeepOCSortOracle(**kw)
+    got = []
+    for f, (d, feats) in enumerate(frames):
+        out = eng.update([d], [feats], img_shapes=[img_shape])[0]
+        ref = np.asarray(o.update(d, img_shape, feats, None), dtype=np.float64).reshape(-1, 8)
+        assert np.array_equal(out, ref), f
+        got.append(out)
+    counts = g[f"{name}__out_counts"]
+    offs = np.concatenate([[0], np.cumsum(counts)])
+    exp = [g[f"{name}__out"][offs[f]:offs[f + 1]] for f in range(len(counts))]
+    assert canonical_equal(got, exp)
+
+
+# ------------------------------------------------------------------ C5 HybridSORT 4096
+def test_hybridsort_4096_d512_two_streams(g):
+    """C5: two HybridSORT streams of 4096 x 4096 with 512-d embeddings in one engine launch."""
+    from yolo_tracking_amd.trackers.hybridsort import HybridSortEngine
+    cases = [fc.hybridsort_frames(g, n) for n in fc.HS_4096]
+    kw, D = cases[0][1], cases[0][2]
+    S = len(cases)
+    eng = HybridSortEngine(S, feat_dim=D, **kw)
+    nid = np.zeros(S, dtype=np.int64)
+    nf = len(cases[0][0])
+    for f in range(nf):
+        dets = [c[0][f][0] for c in cases]
+        feats = [c[0][f][1] / np.linalg.norm(c[0][f][1]) for c in cases]
+        outs = eng.update(dets, feats, next_id=nid)
+        for s, name in enumerate(fc.HS_4096):
+            fc.check_frame(g, name, f, outs[s])
+    for s, name in enumerate(fc.HS_4096):
+        st = eng.state(s)
+        assert np.array_equal(st["id"], g[f"{name}__st_id"])
+        assert np.array_equal(st["x"], g[f"{name}__st_x"])
+        assert np.array_equal(st["P"][::64], g[f"{name}__st_P_sample"])
+        np.testing.assert_allclose(st["feat"][::64], g[f"{name}__st_feat_sample"], rtol=0,
+                                   atol=2e-7)
+        assert nid[s] == int(g[f"{name}__count"])
+
+
+def test_hybridsort_4096_python_surface(g):
+    """C5 through the HybridSORT class (the reference's PerClassDecorator replayed call by call,
+    ReID features from a get_features producer), stream a."""
+    from test_gpu_hybridsort import FrameReID
+    from yolo_tracking_amd.trackers.hybridsort import HybridSORT, KalmanBoxTracker
+    name = fc.HS_4096[0]
+    frames, kw, D = fc.hybridsort_frames(g, name)
+    reid = FrameReID()
+    trk = HybridSORT(None, 0, False, reid=reid, **kw)
+    img = np.zeros((8, 8, 3), np.uint8)
+    for f, (d, raw) in enumerate(frames):
+        reid.set(d, raw)
+        fc.check_frame(g, name, f, trk.update(d, img))
+    assert KalmanBoxTracker.count == int(g[f"{name}__count"])

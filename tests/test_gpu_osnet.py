@@ -59,16 +59,22 @@ def test_weight_file_and_get_features(golden, tmp_path):
 
 def test_trackers_build_reid_from_weights(tmp_path):
     """create_tracker('botsort' / 'deepocsort' / 'hybridsort', cfg, reid_weights=<path>) builds
-    the OSNet producer (bot_sort.py:217-219); a missing file runs with random weights + warning."""
+    the OSNet producer (bot_sort.py:217-219); a missing file raises FileNotFoundError, random
+    weights only on request (random_init=True)."""
     from yolo_tracking_amd import create_tracker, get_tracker_config
     from yolo_tracking_amd.synth import make_frames
     rng = np.random.default_rng(0)
     img = rng.integers(0, 256, (640, 640, 3), dtype=np.uint8)
     dets = make_frames(24, 1, 5, canvas=600.0)[0][0]
+    from yolo_tracking_amd.appearance.osnet import random_state_dict
+    w = tmp_path / "osnet_x0_25_x.pt"
+    torch.save({"state_dict": {k: torch.from_numpy(np.asarray(v))
+                               for k, v in random_state_dict("osnet_x0_25", 1).items()}}, w)
     for name in ("botsort", "deepocsort", "hybridsort"):
-        with pytest.warns(RuntimeWarning):
-            t = create_tracker(name, get_tracker_config(name), tmp_path / "osnet_x0_25_x.pt", "0",
-                               False, False)
+        with pytest.raises(FileNotFoundError):
+            create_tracker(name, get_tracker_config(name), tmp_path / "missing_osnet_x0_25.pt",
+                           "0", False, False)
+        t = create_tracker(name, get_tracker_config(name), w, "0", False, False)
         assert isinstance(t.model, ReIDDetectMultiBackend)
         t.model.warmup()
         r = np.asarray(t.update(dets, img))

@@ -76,7 +76,7 @@ def test_device_batch_over_images_and_empty_count():
     per = [boxes_for(rng, im.shape[0], im.shape[1], 20) for im in imgs]
     per = [b[[orr.crop_rect(x, im.shape[0], im.shape[1]) is not None for x in b]]
            for b, im in zip(per, imgs)]
-    reid = ReIDDetectMultiBackend(device=0)
+    reid = ReIDDetectMultiBackend(device=0, random_init=True)
     got = reid.preprocess_batch(list(zip(per, imgs))).cpu().numpy()
     exp = np.concatenate([orr.preprocess(b, im) for b, im in zip(per, imgs)])
     assert np.array_equal(got, exp)

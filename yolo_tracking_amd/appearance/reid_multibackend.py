@@ -11,8 +11,9 @@ The network: OSNet (appearance/osnet.py, an eval-mode inference graph with folde
 channels-last, batched branches) built from `weights` as the reference builds it from the weight
 file name (reid_multibackend.py:57-80, osnet_x0_25 .. osnet_x1_0); the reference's .pt state dicts
 load unchanged (torch.load(weights_only=True)).  A weight file that is not on disk would be
-downloaded by the reference (gdown, :61-64); there is no network here, so the network then runs
-with freshly initialised weights and a warning says so.  `model=` (any torch module on the device
+downloaded by the reference (gdown, :61-64) or end the program (:67-72); there is no network here,
+so a missing file raises FileNotFoundError.  Freshly initialised weights (benchmarks, plumbing
+tests) are an explicit opt-in: `random_init=True`.  `model=` (any torch module on the device
 taking (N, 3, 256, 128)) replaces the network; the ONNX / OpenVINO / TensorRT / TFLite export
 backends (:82-178) are not rebuilt.  There is no CPU fallback (a missing library raises YTAError).
 """
@@ -80,7 +81,8 @@ class ReIDDetectMultiBackend:
     """reid_multibackend.py:59 ReIDDetectMultiBackend(weights, device, fp16) with a
     caller-supplied network (`model`, a torch module on `device`)."""
 
-    def __init__(self, weights="osnet_x0_25_msmt17.pt", device=0, fp16=False, model=None):
+    def __init__(self, weights="osnet_x0_25_msmt17.pt", device=0, fp16=False, model=None,
+                 random_init=False):
         import torch
         self.torch = torch
         self.weights = weights
@@ -89,6 +91,7 @@ class ReIDDetectMultiBackend:
         self.fp16 = bool(fp16)
         self.nhwc = False
         self.lib = _lib.load_library()
+        self.random_init = bool(random_init)
         if model is None and weights is not None:
             model = self._build_osnet(weights)
         self.model = model
@@ -104,11 +107,15 @@ class ReIDDetectMultiBackend:
         w = Path(weights)
         if w.is_file():
             sd = load_checkpoint(w)
-        else:
-            warnings.warn(f"ReID weights {str(w)!r} not on disk and no network to download them "
-                          f"(reid_multibackend.py:61-64): {name} runs with fresh random weights",
-                          RuntimeWarning, stacklevel=3)
+        elif self.random_init:
+            warnings.warn(f"ReID weights {str(w)!r} not on disk: {name} runs with fresh random "
+                          "weights (random_init=True)", RuntimeWarning, stacklevel=3)
             sd = None
+        else:
+            raise FileNotFoundError(
+                f"ReID weights {str(w)!r} not found and there is no network to download them "
+                f"(reid_multibackend.py:61-72); pass an existing {name} checkpoint, model=<torch "
+                "module>, or random_init=True for untrained weights")
         return OSNetReID(name, sd, device=self.device, half=self.fp16)
 
     def _stream(self):

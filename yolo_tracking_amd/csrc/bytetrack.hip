@@ -768,11 +768,20 @@ __global__ __launch_bounds__(BLKE, 4) void k_s1_edges(BtArgs a) {
     for (int q = t; q < h.n_big; q += nt) gg.big[q] = gv.big[q];
 }
 
-// Arena bytes that always suffice for s1_lap_body (the global fallback arena's size).
+// Arena bytes that always suffice for s1_lap_body (the global fallback arena's size): compact
+// rows (ids, offsets, matches), column bitmap + word prefix, compact columns (ids, degrees,
+// matches), the CSR, lap_block's work arrays.
 __host__ __device__ inline long long s1_lap_arena_bytes(long long R, long long C, long long E) {
-    return 4 * (R + 1) + 4 * C + 12 * E + 4 * (R + C) * 3 + 4 * 6 * (R + C + 1) + 16 * 16 + 256;
+    return 4 * (R + 1) + 8 * R + 8 * ((C + 31) / 32 + 1) + 12 * C + 12 * E + 4 * (R + C) * 3 +
+           4 * 6 * (R + C + 1) + 16 * 16 + 512;
 }
 
+// The residual problem (pool rows with edges left after k_s1_edges' single-edge components,
+// high detections they reach) is solved on compact, order-preserving renumberings of its rows and
+// columns: lap_block's results depend on node ids only through their order, so the assignment is
+// the one it finds on the full index ranges, while its arrays (union-find over rows + columns, the
+// CSR offsets) cover the ~30 % of pool rows and ~40 % of detections that are in play instead of all
+// of them (the steady state's 1600-row pools otherwise overflow the 38 KiB arena).
 __device__ __forceinline__ bool s1_lap_body(const BtArgs &a, int s, Arena &ar, LapShared &lsh) {
     const int t = threadIdx.x, nt = blockDim.x;
     BtCounters *c = a.cnt + s;
@@ -781,90 +790,111 @@ __device__ __forceinline__ bool s1_lap_body(const BtArgs &a, int s, Arena &ar, L
     const int nr = c->n_pool, nc = c->n_high;
     YTA_STAMP_BASE(90);
     YTA_STAMP(0);
-    // the assignment goes straight to x1 / y1, which k_s1_edges filled with its single-edge
-    // matches and -1 (lap_block only writes the pairs it matches)
+    // k_s1_edges filled x1 / y1 with its single-edge matches and -1; only the residual problem's
+    // matches are written below
     int *X = a.x1 + tb;
     int *Y = a.y1 + db;
-    int *row_off = ar.alloc_top<int>(nr + 1);
-    int *col_deg = ar.alloc_top<int>(nc);
+    // rows in play and their edge total
+    int myr = 0, mye = 0;
+    for (int i = t; i < nr; i += nt) {
+        const int n = a.e_cnt[tb + i];
+        myr += n > 0;
+        mye += n;
+    }
+    int R, E;
+    block_exclusive_scan<false>(myr, lsh.wsum, &R);
+    block_exclusive_scan<false>(mye, lsh.wsum, &E);
+    if (E == 0) {
+        if (t == 0) c->n_res1 = 0;
+        return true;
+    }
+    const int words = (nc + 31) >> 5;
+    int *rid = ar.alloc_top<int>(R);
+    int *row_off = ar.alloc_top<int>(R + 1);
+    unsigned *cbits = ar.alloc_top<unsigned>(words);
+    int *cpre = ar.alloc_top<int>(words + 1);
+    int *csr_col = ar.alloc_top<int>(E);
+    double *csr_cost = ar.alloc_top<double>(E);
     if (ar.fail) return false;
-    for (int j = t; j < nc; j += nt) col_deg[j] = 0;
-    // row offsets: every thread owns a contiguous run of <= 8 rows (loads in flight together)
-    int run = 0;
+    for (int w = t; w < words; w += nt) cbits[w] = 0u;
+    // compact rows in pool order (each thread a contiguous run of <= 8 rows) and their offsets
+    int runR = 0, runE = 0;
     for (int base = 0; base < nr; base += 8 * nt) {
         const int m = nr - base < 8 * nt ? nr - base : 8 * nt;
         const int per = (m + nt - 1) / nt;
         const int lo = base + t * per;
         const int hi = lo + per < base + m ? lo + per : base + m;
-        int cnt[8], mine = 0;
+        int cnt[8], mr = 0, me = 0;
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
             cnt[k] = lo + k < hi ? a.e_cnt[tb + lo + k] : 0;
-            mine += cnt[k];
+            mr += cnt[k] > 0;
+            me += cnt[k];
         }
-        int tot;
-        int pos = run + block_exclusive_scan<false>(mine, lsh.wsum, &tot);
+        int totR, totE;
+        int pr = runR + block_exclusive_scan<false>(mr, lsh.wsum, &totR);
+        int pe = runE + block_exclusive_scan<false>(me, lsh.wsum, &totE);
 #pragma unroll
         for (int k = 0; k < 8; ++k)
-            if (lo + k < hi) {
-                row_off[lo + k] = pos;
-                pos += cnt[k];
+            if (cnt[k] > 0) {
+                rid[pr] = lo + k;
+                row_off[pr] = pe;
+                ++pr;
+                pe += cnt[k];
             }
-        run += tot;
+        runR += totR;
+        runE += totE;
     }
-    const int E = run;
-    if (t == 0) row_off[nr] = E;
-    int *csr_col = ar.alloc_top<int>(E);
-    double *csr_cost = ar.alloc_top<double>(E);
-    if (ar.fail) return false;
-    lds_sync();
+    if (t == 0) row_off[R] = E;
+    block_sync();
     YTA_STAMP(1);
-    // CSR fill from the edge slots (same row ownership, every slot load of a thread in flight);
-    // a row with more edges than slots queries the stream's grid in HBM again
-    if (E > 0) {
+    // CSR fill from the edge slots (runs of compact rows, four rows' slot loads in flight); a row
+    // with more edges than slots queries the stream's grid in HBM again.  Columns in play: bitmap.
+    {
         const GridView gg = s1_grid_hbm(a, s);
-        for (int base = 0; base < nr; base += 8 * nt) {
-            const int m = nr - base < 8 * nt ? nr - base : 8 * nt;
+        for (int base = 0; base < R; base += 8 * nt) {
+            const int m = R - base < 8 * nt ? R - base : 8 * nt;
             const int per = (m + nt - 1) / nt;
             const int lo = base + t * per;
             const int hi = lo + per < base + m ? lo + per : base + m;
 #pragma unroll
-          for (int half = 0; half < 8; half += 4) {   // four rows' slot loads in flight
+          for (int half = 0; half < 8; half += 4) {
             int col[4][E_SLOTS];
             double cost[4][E_SLOTS];
-            int n[4];
+            int n[4], gi[4];
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
-                const int i = lo + half + k;
-                n[k] = i < hi ? row_off[i + 1] - row_off[i] : 0;
+                const int r = lo + half + k;
+                n[k] = r < hi ? row_off[r + 1] - row_off[r] : 0;
+                gi[k] = r < hi ? rid[r] : 0;
 #pragma unroll
                 for (int q = 0; q < E_SLOTS; ++q)
                     if (q < n[k]) {
-                        col[k][q] = a.e_col[q * SC + tb + i];
-                        cost[k][q] = a.e_cost[q * SC + tb + i];
+                        col[k][q] = a.e_col[q * SC + tb + gi[k]];
+                        cost[k][q] = a.e_cost[q * SC + tb + gi[k]];
                     }
             }
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 if (n[k] == 0) continue;
-                const int i = lo + half + k;
-                int e = row_off[i];
+                const int r = lo + half + k;
+                int e = row_off[r];
                 if (n[k] <= E_SLOTS) {
 #pragma unroll
                     for (int q = 0; q < E_SLOTS; ++q)
                         if (q < n[k]) {
                             csr_col[e + q] = col[k][q];
                             csr_cost[e + q] = cost[k][q];
-                            atomicAdd(&col_deg[col[k][q]], 1);
+                            atomicOr(&cbits[col[k][q] >> 5], 1u << (col[k][q] & 31));
                         }
                 } else {
-                    const int eend = row_off[i + 1];
-                    s1_row_edges(a, s, gg, *gg.hdr, a.pool_box[tb + i], [&](int j, double cj) {
+                    const int eend = row_off[r + 1];
+                    s1_row_edges(a, s, gg, *gg.hdr, a.pool_box[tb + gi[k]], [&](int j, double cj) {
                         if (e >= eend) return;
                         csr_col[e] = j;
                         csr_cost[e] = cj;
                         ++e;
-                        atomicAdd(&col_deg[j], 1);
+                        atomicOr(&cbits[j >> 5], 1u << (j & 31));
                     });
                 }
             }
@@ -873,10 +903,56 @@ __device__ __forceinline__ bool s1_lap_body(const BtArgs &a, int s, Arena &ar, L
     }
     block_sync();
     YTA_STAMP(2);
-    if (!lap_block(nr, nc, row_off, csr_col, csr_cost, col_deg, a.match_thresh, X, Y, &c->err, ar,
-                   slab_of(a, s), lsh, false))
+    // compact columns in detection order: prefix over the bitmap words (written by atomics: read
+    // around the L1 when the arena is global)
+    auto cword = [&](int w) { return (unsigned)ald(reinterpret_cast<const int *>(cbits + w)); };
+    int C = 0;
+    for (int base = 0; base < words; base += nt) {
+        const int w = base + t;
+        const int pc = w < words ? __popc(cword(w)) : 0;
+        int tot;
+        const int ex = block_exclusive_scan<false>(pc, lsh.wsum, &tot);
+        if (w < words) cpre[w] = C + ex;
+        C += tot;
+    }
+    int *cols = ar.alloc_top<int>(C);
+    int *cdeg = ar.alloc_top<int>(C);
+    int *Xc = ar.alloc_top<int>(R);
+    int *Yc = ar.alloc_top<int>(C);
+    if (ar.fail) return false;
+    block_sync();
+    for (int w = t; w < words; w += nt) {
+        unsigned b = cword(w);
+        int p = cpre[w];
+        while (b) {
+            const int k = __ffs(b) - 1;
+            b &= b - 1;
+            cols[p] = w * 32 + k;
+            cdeg[p] = 0;
+            ++p;
+        }
+    }
+    block_sync();
+    for (int e = t; e < E; e += nt) {
+        const int j = csr_col[e];
+        const int w = j >> 5;
+        const int cc = cpre[w] + __popc(cword(w) & ((1u << (j & 31)) - 1u));
+        csr_col[e] = cc;
+        atomicAdd(&cdeg[cc], 1);
+    }
+    block_sync();
+    if (!lap_block(R, C, row_off, csr_col, csr_cost, cdeg, a.match_thresh, Xc, Yc, &c->err, ar,
+                   slab_of(a, s), lsh, true))
         return false;
     YTA_STAMP(3);
+    // the residual matches, in the original numbering
+    for (int r = t; r < R; r += nt) {
+        const int x = Xc[r];
+        if (x >= 0) {
+            X[rid[r]] = cols[x];
+            Y[cols[x]] = rid[r];
+        }
+    }
     if (t == 0) c->n_res1 = E;   // edges left after the single-edge components
     return true;
 }
@@ -1263,10 +1339,10 @@ struct FinishShared {
     int wsum[32];
 };
 
-// lost' boxes (by position) + a grid of ids over them (cell starts, ids, big list)
+// lost' float boxes (by position) + a grid of ids over them (cell starts, ids, big list)
 __host__ __device__ inline long long dedup_arena_bytes(long long n) {
     return 4 * (grid_cells_for((int)(n < GRID_MAX_CELLS ? n : GRID_MAX_CELLS)) + 1) +
-           n * (32 + 4 + 4) + 4 * 16;
+           n * (16 + 4 + 4) + 4 * 16;
 }
 
 __device__ __forceinline__ int track_age(const BtArgs &a, long long slot) {
@@ -1426,12 +1502,14 @@ __device__ __forceinline__ void finish_body(const BtArgs &a, int s, unsigned *bi
     block_sync();
     YTA_STAMP(4);
     // remove_duplicate_stracks (:312-325): pairs with 1 - IoU < 0.15 drop the younger track (set
-    // semantics, so pairs are visited in any order)
+    // semantics, so pairs are visited in any order).  The grid over lost' keeps outward-rounded
+    // float boxes (16 B each: a steady-state lost' list of ~800 fits the LDS arena); a candidate
+    // passing the conservative float pre-test is decided on its exact box, read again.
     if (n_t2 > 0 && n_l2 > 0) {
         const int ncell = grid_cells_for(n_l2);
-        Box *lcache = ar.alloc<Box>(n_l2);   // the grid reads boxes through its ids from here
+        float4 *lcache = ar.alloc<float4>(n_l2);   // the grid reads boxes through its ids here
         GridView gv{nullptr, ar.alloc<int>(ncell + 1), ar.alloc<int>(n_l2), nullptr, nullptr,
-                    ar.alloc<int>(n_l2), lcache};
+                    ar.alloc<int>(n_l2), nullptr};
         // a lost' box: ByteTrack's lost' tracks are lazily predicted (kf_xyah.hpp)
         struct LostMean {
             double m[8];
@@ -1454,18 +1532,22 @@ __device__ __forceinline__ void finish_body(const BtArgs &a, int s, unsigned *bi
             if (V == VAR_BYTETRACK) kf_predict_lost_mean(v.m, v.lag);
             return V == VAR_BOTSORT ? xywh_to_box(v.m) : xyah_mean_to_box(v.m[0], v.m[1], v.m[2], v.m[3]);
         };
+        auto exact_lbox = [&](int q) {
+            if (V == VAR_BYTETRACK) return a.pool_box[tb + a.l2pos[tb + q]];
+            return lbox_of(lmean_of(a.l2[tb + q]));
+        };
         if (V == VAR_BYTETRACK)   // the predicted box stage 1 used (k_s1_prep): same mean
             batched_for<4>(
                 n_l2, [&](int q) { return a.pool_box[tb + a.l2pos[tb + q]]; },
-                [&](int q, const Box &b) { lcache[q] = b; });
+                [&](int q, const Box &b) { lcache[q] = box_outer_f32(b); });
         else
             batched_for2<3>(
                 n_l2, [&](int q) { return a.l2[tb + q]; },
                 [&](int, int sl) { return lmean_of(sl); },
-                [&](int q, const LostMean &v) { lcache[q] = lbox_of(v); });
+                [&](int q, const LostMean &v) { lcache[q] = box_outer_f32(lbox_of(v)); });
         block_sync();   // lcache may be the global arena
-        grid_build(n_l2, [&](int q) { return lcache[q]; }, [](int) { return 1.0; }, gv, sh.gs,
-                   wsum);
+        grid_build(n_l2, [&](int q) { return box_of_f4(lcache[q]); }, [](int) { return 1.0; }, gv,
+                   sh.gs, wsum);
         const GridHdr gh = sh.gs.hdr;
         YTA_STAMP(5);
         struct TBox {
@@ -1482,7 +1564,9 @@ __device__ __forceinline__ void finish_body(const BtArgs &a, int s, unsigned *bi
             },
             [&](int p, const TBox &v) {
                 const Box &tbx = v.b;
-                auto pair = [&](int q, const Box &lb) {
+                auto pair = [&](int q, const float4 &lf) {
+                    if (!iou_may_exceed(tbx, lf, 0.85)) return;
+                    const Box lb = exact_lbox(q);
                     if (!intersects(tbx, lb)) return;
                     if (1 - iou(tbx, lb) < 0.15) {
                         if (track_age(a, v.slot) > track_age(a, tb + a.l2[tb + q]))
@@ -1492,9 +1576,8 @@ __device__ __forceinline__ void finish_body(const BtArgs &a, int s, unsigned *bi
                     }
                 };
                 // 1 - IoU < 0.15  <=>  IoU > 0.85: only corners within 0.18 w of tbx's
-                grid_query_iou_above(gv, gh, tbx, 0.85,
-                                     [&](int q, const Box &lb, double) { pair(q, lb); },
-                                     [&](int q) { pair(q, lcache[q]); });
+                grid_query_iou_above_f4(gv, gh, lcache, tbx, 0.85, pair,
+                                        [&](int q) { pair(q, lcache[q]); });
             });
     }
     lds_sync();
@@ -1612,6 +1695,7 @@ __global__ __launch_bounds__(BLKF, 4) void k_finish(BtArgs a) {
         Arena ar(fsmem + bits_bytes, a.lds_bytes_f);
         finish_body<V>(a, s, bits, ar, sh);
     } else {
+        if (threadIdx.x == 0) a.cnt[s].n_fallback_f += 1;
         Arena ag(a.ws + s * a.ws_stride, a.ws_stride);
         finish_body<V>(a, s, bits, ag, sh);
     }
@@ -2539,7 +2623,7 @@ int yta_bytetrack_stats(yta_bytetrack *e, long long *stats) {
     YTA_HIP(hipSetDevice(e->device));
     const int rc = read_counters(e);
     if (rc) return rc;
-    constexpr int NS = 20;
+    constexpr int NS = 21;
     for (int k = 0; k < NS; ++k) stats[k] = 0;
     for (int s = 0; s < e->S; ++s) {
         const BtCounters &c = e->h_cnt[s];
@@ -2547,7 +2631,7 @@ int yta_bytetrack_stats(yta_bytetrack *e, long long *stats) {
                                  c.n_left, c.n_rest, c.n_births, c.n_t2, c.n_l2, c.n_tracked,
                                  c.n_lost, c.n_out, (long long)c.n_edges[0],
                                  (long long)c.n_edges[1] + c.n_edges[2], c.n_fallback[0],
-                                 c.n_fallback[1], c.n_lazy, c.n_res1};
+                                 c.n_fallback[1], c.n_lazy, c.n_res1, c.n_fallback_f};
         for (int k = 0; k < NS; ++k) stats[k] += v[k];
     }
     return YTA_OK;

@@ -52,7 +52,8 @@ struct BtCounters {                  // one per stream, 128 B
     int n_lazy;                      // ByteTrack: lost-list records k_apply left untouched
     int n_res1;                      // ByteTrack: stage-1 edges left to k_s1_lap
     int n_ref;                       // re-found Lost tracks (refound list)
-    int pad[4];
+    int n_fallback_f;                // cumulative: k_finish's duplicate-removal grid over global
+    int pad[3];
 };
 static_assert(sizeof(BtCounters) == 128, "BtCounters layout");
 

@@ -301,6 +301,82 @@ __device__ __forceinline__ void grid_query_iou_above(const GridView &gv, const G
                      [&](int, int id, const Box &b, double w) { visit(id, b, w); });
 }
 
+// ---- float boxes with exact pre-tests (the duplicate-removal grid, k_finish)
+// A box rounded outward to float: the float box contains the double one (x1 / y1 rounded down,
+// x2 / y2 up; NaN stays NaN).  16 B instead of 32 in LDS.
+__device__ __forceinline__ float4 box_outer_f32(const Box &b) {
+    auto dn = [](double x) {
+        const float f = (float)x;
+        return (double)f > x ? nextafterf(f, -INFINITY) : f;
+    };
+    auto up = [](double x) {
+        const float f = (float)x;
+        return (double)f < x ? nextafterf(f, INFINITY) : f;
+    };
+    return make_float4(dn(b.x1), dn(b.y1), up(b.x2), up(b.y2));
+}
+
+__device__ __forceinline__ Box box_of_f4(const float4 &f) {
+    return Box{(double)f.x, (double)f.y, (double)f.z, (double)f.w};
+}
+
+// Conservative pre-test of IoU(T, L) > t for a box L known only by its outward-rounded float box
+// Lo: the exact L lies between Lo and the inner box one float step inside it, so
+// IoU(T, L) <= I(T, Lo) / (A(T) + A(inner) - I(T, Lo)) (IoU grows with the intersection, falls
+// with the other area).  Float values and their products are exact in double; the remaining
+// double roundings (~1e-16 relative) are covered by the 1e-6 slack.  false => IoU(T, L) <= t
+// (1 - 1e-6): the pair can be skipped; NaN boxes intersect nothing.
+__device__ __forceinline__ bool iou_may_exceed(const Box &T, const float4 &Lo, double t) {
+    const double iw = fmin(T.x2, (double)Lo.z) - fmax(T.x1, (double)Lo.x);
+    const double ih = fmin(T.y2, (double)Lo.w) - fmax(T.y1, (double)Lo.y);
+    if (!(iw > 0.0 && ih > 0.0)) return false;   // the outer boxes do not meet: neither do L, T
+    const double I = iw * ih;
+    const double bw = (double)nextafterf(Lo.z, -INFINITY) - (double)nextafterf(Lo.x, INFINITY);
+    const double bh = (double)nextafterf(Lo.w, -INFINITY) - (double)nextafterf(Lo.y, INFINITY);
+    const double B = fmax(bw, 0.0) * fmax(bh, 0.0);
+    const double den = (T.x2 - T.x1) * (T.y2 - T.y1) + B - I;
+    return !(den > 0.0) || I > t * (1.0 - 1e-6) * den;
+}
+
+// grid_query_iou_above over a grid whose items' boxes are outward-rounded float boxes lc[id]
+// (grid built on box_of_f4(lc[id])): the corner window is widened by the float rounding of the
+// corners (<= 2^-23 relative); visit(id, lc[id]) / visit_big(id) then decide.
+template <typename Visit, typename VisitBig>
+__device__ __forceinline__ void grid_query_iou_above_f4(const GridView &gv, const GridHdr &h,
+                                                        const float4 *lc, const Box &T, double t,
+                                                        Visit visit, VisitBig visit_big) {
+    for (int k = 0; k < h.n_big; ++k) visit_big(gv.big[k]);
+    if (!(T.x2 > T.x1 && T.y2 > T.y1)) return;   // intersects nothing (also NaN)
+    if (h.n_binned == 0) return;
+    const double r = (1.0 - t) / t * (1.0 + 1e-6);
+    double mx = (T.x2 - T.x1) * r + (fabs(T.x1) + 1.0) * 1e-9;
+    double my = (T.y2 - T.y1) * r + (fabs(T.y1) + 1.0) * 1e-9;
+    mx += (fabs(T.x1) + mx + 1.0) * 2.5e-7;
+    my += (fabs(T.y1) + my + 1.0) * 2.5e-7;
+    const double lx = T.x1 - mx, hx = T.x1 + mx, ly = T.y1 - my, hy = T.y1 + my;
+    const double fx1 = floor((hx - h.ox) * h.inv_g), fy1 = floor((hy - h.oy) * h.inv_g);
+    if (fx1 < 0.0 || fy1 < 0.0) return;
+    const int cx0 = grid_cell_1d(lx, h.ox, h.inv_g, h.gx);
+    const int cy0 = grid_cell_1d(ly, h.oy, h.inv_g, h.gy);
+    const int cx1 = fx1 > (double)(h.gx - 1) ? h.gx - 1 : (int)fx1;
+    const int cy1 = fy1 > (double)(h.gy - 1) ? h.gy - 1 : (int)fy1;
+    for (int cy = cy0; cy <= cy1; ++cy) {
+        const int b = ald(gv.cell_start + cy * h.gx + cx0);
+        const int e = ald(gv.cell_start + cy * h.gx + cx1 + 1);
+        int k = b;
+        for (; k + 1 < e; k += 2) {
+            const int i0 = gv.ids[k], i1 = gv.ids[k + 1];
+            const float4 b0 = lc[i0], b1 = lc[i1];
+            visit(i0, b0);
+            visit(i1, b1);
+        }
+        if (k < e) {
+            const int i0 = gv.ids[k];
+            visit(i0, lc[i0]);
+        }
+    }
+}
+
 template <typename Visit, typename VisitBig>
 __device__ __forceinline__ void grid_query(const GridView &gv, const GridHdr &h, const Box &T,
                                            Visit visit, VisitBig visit_big) {

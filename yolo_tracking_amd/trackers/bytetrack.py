@@ -65,7 +65,7 @@ class ByteTrackEngine:
         """Last frame's counts summed over streams (see yta_bytetrack_stats)."""
         names = ["dets", "high", "second", "pool", "act", "unc", "left", "rest", "births", "t2",
                  "l2", "tracked", "lost", "out", "edges1", "edges23", "fallback1", "fallback23",
-                 "lazy", "res1"]
+                 "lazy", "res1", "fallback_f"]
         buf = (ctypes.c_longlong * len(names))()
         _lib.check(self.lib.yta_bytetrack_stats(self._h, buf))
         return {k: int(buf[i]) for i, k in enumerate(names)}
