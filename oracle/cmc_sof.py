@@ -626,6 +626,8 @@ class SparseOptFlowOracle:
             return H
         if len(self.prev_keypoints) == 0:       # calcOpticalFlowPyrLK returns None outputs
             return H
+        if img.shape != self.prev_img.shape:    # calcOpticalFlowPyrLK asserts equal level sizes;
+            return H                            # sof.py:105-110 catches it: identity, state kept
         pyr = build_pyramid(img)
         nxt, status = lk_track(self.prev_pyr, pyr, self.prev_keypoints)
         self.prev_keypoints = self.prev_keypoints[status == 1]

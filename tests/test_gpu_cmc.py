@@ -197,6 +197,28 @@ def test_engine_first_frame_without_corners_and_point_loss():
         assert np.array_equal(eng.state(0)["keypoints"], _kp(o))
 
 
+def test_engine_resolution_switch_mid_sequence():
+    """A stream whose frame size changes after the first frame: calcOpticalFlowPyrLK asserts on
+    the level sizes and sof.py:105-110 returns the identity with the stored frame and corners
+    kept -- for a smaller frame, a larger one that fits the buffers, and one larger than the
+    engine was built for (the host path grows the buffers keeping the state).  Frames of the
+    stored size then track again."""
+    big, _ = sequence(480, 640, 6, 52, step=(0.1, 1.0, 2.0, -1.0))
+    small, _ = sequence(240, 320, 2, 53)
+    huge, _ = sequence(600, 800, 1, 54)
+    seq = [big[0], big[1], small[0], big[2], huge[0], small[1], big[3], big[4], big[5]]
+    eng = SofEngine(1, 0.1, 0, 480, 640)
+    o = cs.SparseOptFlowOracle(0.1)
+    for f, fr in enumerate(seq):
+        got = eng.apply([fr], [np.zeros((0, 4))])[0]
+        exp = o.apply(fr, None)
+        assert np.array_equal(got, exp), (f, got - exp)
+        st = eng.state(0, with_image=True)
+        assert np.array_equal(st["keypoints"], _kp(o)), f
+        assert np.array_equal(st["prev_img"], o.prev_img), f
+    assert not np.array_equal(got, np.eye(2, 3))
+
+
 def test_dropin_sparse_opt_flow_matches_oracle():
     frames, _ = sequence(720, 1280, 4, 44)
     dets = boxes(720, 1280, 10, 4)

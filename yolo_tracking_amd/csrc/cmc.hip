@@ -198,12 +198,20 @@ __global__ __launch_bounds__(256) void k_sof_small(SofArgs a) {
     const int H = a.frame_hw[2 * s], W = a.frame_hw[2 * s + 1];
     const int h0 = (int)rint(H * a.scale), w0 = (int)rint(W * a.scale);
     const int cur = 1 - st.prev;
-    const bool ok = H >= 1 && W >= 1 && h0 >= 1 && w0 >= 1 && h0 <= a.h0max && w0 <= a.w0max;
+    const bool fits = H >= 1 && W >= 1 && h0 >= 1 && w0 >= 1 && h0 <= a.h0max && w0 <= a.w0max;
+    // After the first frame a frame of another size makes calcOpticalFlowPyrLK assert on the
+    // level sizes; sof.py:105-110 catches it and returns the identity with prev_img and the
+    // corners kept (also when the frame exceeds the buffers: that is a size change too).  Only a
+    // first frame that does not fit is an error, and it belongs to this frame alone.
+    const bool resized = st.init && (!fits || h0 != st.h0[st.prev] || w0 != st.w0[st.prev]);
+    const bool ok = fits && !resized;
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         st.mode = !ok ? MODE_SKIP : (!st.init ? MODE_GFTT : (st.n_kp > 0 ? MODE_LK : MODE_NOKP));
-        if (!ok) st.err |= SOF_ERR_SIZE;
-        st.h0[cur] = h0;
-        st.w0[cur] = w0;
+        st.err = !fits && !st.init ? SOF_ERR_SIZE : 0;
+        if (ok) {
+            st.h0[cur] = h0;
+            st.w0[cur] = w0;
+        }
     }
     if (!ok) return;
     const int i = blockIdx.x * 256 + threadIdx.x;
@@ -1458,20 +1466,34 @@ int yta_sof_apply(yta_sof *e, const uint8_t *frames, const long long *frame_off,
         mw = std::max(mw, frame_hw[2 * s + 1]);
         YTA_CHECK(det_off[s + 1] >= det_off[s], YTA_ERR_INVALID, "det_off must be non-decreasing");
     }
-    if (mh > e->max_h || mw > e->max_w) {   // grow: the stored state is dropped with the buffers
-        int fresh = 1;
-        YTA_HIP(hipMemcpyAsync(e->h_state, e->a.state, sizeof(SofState) * S, hipMemcpyDeviceToHost,
-                               e->stream));
+    if (mh > e->max_h || mw > e->max_w) {
+        // grow, keeping every stream's state: the stored frame's pyramid and derivatives (packed
+        // from the slot start at the stored frame's own size), the corners and SofState
         YTA_HIP(host_wait(e->stream));
-        for (int s = 0; s < S; ++s) fresh &= e->h_state[s].init == 0;
-        YTA_CHECK(fresh, YTA_ERR_CAPACITY,
-                  "frame %d x %d exceeds the engine's %d x %d after the first frame", mh, mw,
-                  e->max_h, e->max_w);
-        sof_free(e);
+        const SofArgs old = e->a;
+        std::vector<void *> old_allocs;
+        old_allocs.swap(e->allocs);
+        if (e->h_state) (void)hipHostFree(e->h_state);
+        e->h_state = nullptr;
         e->max_h = mh;
         e->max_w = mw;
         rc = sof_buffers(e);
         if (!rc) rc = yta_sof_reset(e);
+        if (!rc) {
+            SofArgs &a = e->a;
+            const size_t rows = (size_t)S * 2;
+            YTA_HIP(hipMemcpy2DAsync(a.img, a.slot_px, old.img, old.slot_px, old.slot_px, rows,
+                                     hipMemcpyDeviceToDevice, e->stream));
+            YTA_HIP(hipMemcpy2DAsync(a.der, a.slot_px * sizeof(short2), old.der,
+                                     old.slot_px * sizeof(short2), old.slot_px * sizeof(short2),
+                                     rows, hipMemcpyDeviceToDevice, e->stream));
+            YTA_HIP(hipMemcpyAsync(a.kp, old.kp, sizeof(float2) * S * SOF_MAXKP,
+                                   hipMemcpyDeviceToDevice, e->stream));
+            YTA_HIP(hipMemcpyAsync(a.state, old.state, sizeof(SofState) * S,
+                                   hipMemcpyDeviceToDevice, e->stream));
+            rc = host_wait(e->stream) == hipSuccess ? YTA_OK : YTA_ERR_HIP;
+        }
+        for (void *p : old_allocs) (void)hipFree(p);
         if (rc) return rc;
     }
     if (bytes > e->frames_cap) {
