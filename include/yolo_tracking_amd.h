@@ -114,6 +114,14 @@ int yta_lap_padded(int device, int nr, int nc, const double *cost, int *x, int *
  * smaller side is matched; equal to yta_lap_padded whenever the optimum is unique.  At most 8192
  * entries on the larger side. */
 int yta_lap_rect(int device, int nr, int nc, const double *cost, int *x, int *y);
+/* The OCSORT-family first-round solve (ocsort_common.hpp first_round_lap, association.py:20-28)
+ * exactly as the engines launch it (chip-wide row pre-pass + one LAP_T-thread block), no fast
+ * path: na x nb cost (rows = detections).  rx (na): tracker of each detection or -1; *done: 1 =
+ * solved, 0 = the engine would replay lapjv (more detections than trackers and the optimum not
+ * certified unique); *n_tight: tight non-matching edges the certificate examined (-1 unless
+ * na > nb). */
+int yta_lap_first_round(int device, int na, int nb, const double *cost, int *rx, int *done,
+                        int *n_tight);
 
 /* ---- ByteTrack engine: S independent streams, state resident in HBM -----------------------
  * One engine = S trackers with identical parameters (BYTETracker(track_thresh, match_thresh,
@@ -275,6 +283,11 @@ int yta_ocsort_get_state(yta_ocsort *engine, int stream, int *n_tracks, long lon
 /* Last frame's counts summed over streams: dets, first-round dets, BYTE dets, live trackers,
  * output rows, births, LAP calls, fast-path frames (8 int64). */
 int yta_ocsort_stats(yta_ocsort *engine, long long *stats);
+/* Solver counters since create / reset, summed over streams (3 int64): first-round solves of the
+ * transposed problem (more detections than trackers, association.py:20-28 with dummy columns),
+ * those of them whose optimum was not certified unique (exact ties: lapjv replayed instead), and
+ * lapjv replays in any round (the single-wavefront restatement of lapx's tie-breaking). */
+int yta_ocsort_lap_stats(yta_ocsort *engine, long long *stats);
 int yta_ocsort_hip_stream(yta_ocsort *engine, void **stream);
 /* OCSORT Kalman KAT: n tracks initialised from z0 (n x 4, [u, v, s, r]) run `steps` steps of
  * predict + update(z[step] (n x 4 per step); a NaN first value = update(None)), freeze /
@@ -335,6 +348,11 @@ int yta_deepocsort_get_state(yta_deepocsort *engine, int stream, int *n_tracks, 
 /* Last frame's counts summed over streams: dets, kept dets, 0, live trackers, output rows,
  * births, LAP calls, fast-path frames (8 int64). */
 int yta_deepocsort_stats(yta_deepocsort *engine, long long *stats);
+/* Solver counters since create / reset, summed over streams (3 int64): first-round solves of the
+ * transposed problem (more detections than trackers, association.py:20-28 with dummy columns),
+ * those of them whose optimum was not certified unique (exact ties: lapjv replayed instead), and
+ * lapjv replays in any round (the single-wavefront restatement of lapx's tie-breaking). */
+int yta_deepocsort_lap_stats(yta_deepocsort *engine, long long *stats);
 int yta_deepocsort_hip_stream(yta_deepocsort *engine, void **stream);
 /* DeepOCSORT Kalman KAT (deep_ocsort.py:103-136, 198-293 new-KF branch): n tracks initialised
  * from boxes b0 (n x 4, x1 y1 x2 y2) run `steps` steps of [affine (warps: steps x n x 6, NULL =
@@ -392,6 +410,11 @@ int yta_hybridsort_classes(yta_hybridsort *engine, int stream, double *cls, int 
 /* Last frame's counts summed over streams: dets, kept dets, live trackers, output rows, births,
  * LAP calls, long-term corrections, feature jobs (8 int64). */
 int yta_hybridsort_stats(yta_hybridsort *engine, long long *stats);
+/* Solver counters since create / reset, summed over streams (3 int64): first-round solves of the
+ * transposed problem (more detections than trackers, association.py:20-28 with dummy columns),
+ * those of them whose optimum was not certified unique (exact ties: lapjv replayed instead), and
+ * lapjv replays in any round (the single-wavefront restatement of lapx's tie-breaking). */
+int yta_hybridsort_lap_stats(yta_hybridsort *engine, long long *stats);
 int yta_hybridsort_hip_stream(yta_hybridsort *engine, void **stream);
 /* HybridSORT Kalman KAT (hybridsort.py:112-320): n tracks initialised from rows b0 (n x 5:
  * x1 y1 x2 y2 score) run `steps` steps of predict (velocity clamp) + update(b[step] (n x 5); a

@@ -94,6 +94,7 @@ _SIGS = {
     "yta_lap_limited": ([_I, _I, _I, _P, _D, _P, _P], _I),
     "yta_lap_padded": ([_I, _I, _I, _P, _P, _P], _I),
     "yta_lap_rect": ([_I, _I, _I, _P, _P, _P], _I),
+    "yta_lap_first_round": ([_I, _I, _I, _P, _P, _P, _P], _I),
     "yta_bytetrack_create": ([_I, _I, _I, _I, _P, _P], _I),
     "yta_bytetrack_destroy": ([_P], _I),
     "yta_bytetrack_reset": ([_P], _I),
@@ -122,6 +123,7 @@ _SIGS = {
     "yta_ocsort_sync": ([_P], _I),
     "yta_ocsort_get_state": ([_P, _I, _P, _P, _P, _P], _I),
     "yta_ocsort_stats": ([_P, _P], _I),
+    "yta_ocsort_lap_stats": ([_P, _P], _I),
     "yta_ocsort_hip_stream": ([_P, _P], _I),
     "yta_kf7_run": ([_I, _I, _I, _P, _P, _P, _P], _I),
     "yta_deepocsort_create": ([_I, _I, _I, _I, _I, _P, _P], _I),
@@ -133,6 +135,7 @@ _SIGS = {
     "yta_deepocsort_sync": ([_P], _I),
     "yta_deepocsort_get_state": ([_P, _I, _P, _P, _P, _P, _P], _I),
     "yta_deepocsort_stats": ([_P, _P], _I),
+    "yta_deepocsort_lap_stats": ([_P, _P], _I),
     "yta_deepocsort_hip_stream": ([_P, _P], _I),
     "yta_kf8_run": ([_I, _I, _I, _P, _P, _P, _P, _P], _I),
     "yta_hybridsort_create": ([_I, _I, _I, _I, _I, _P, _P], _I),
@@ -145,6 +148,7 @@ _SIGS = {
     "yta_hybridsort_get_state": ([_P, _I, _P, _P, _P, _P, _P, _P], _I),
     "yta_hybridsort_classes": ([_P, _I, _P, _I, _P], _I),
     "yta_hybridsort_stats": ([_P, _P], _I),
+    "yta_hybridsort_lap_stats": ([_P, _P], _I),
     "yta_hybridsort_hip_stream": ([_P, _P], _I),
     "yta_kf9_run": ([_I, _I, _I, _P, _P, _P, _P], _I),
     "yta_gsi_interpolate": ([_I, _P, _I, _I, _I, _I, _P, ctypes.c_longlong, _P], _I),
@@ -370,6 +374,21 @@ def lap_rect(cost, device=0):
     y = np.empty(nc, dtype=np.int32)
     check(load_library().yta_lap_rect(device, nr, nc, ptr(c), ptr(x), ptr(y)))
     return x, y
+
+
+def lap_first_round(cost, device=0):
+    """The OCSORT-family first-round solve as the engines run it -> (rx, done, n_tight): rx[i] =
+    column of row i or -1; done = False when the engine would replay lapjv (rows > columns and
+    the optimum not certified unique); n_tight = tight non-matching edges the uniqueness
+    certificate examined (-1 unless rows > columns)."""
+    c = np.ascontiguousarray(cost, dtype=np.float64)
+    na, nb = c.shape
+    rx = np.empty(na, dtype=np.int32)
+    done = ctypes.c_int(0)
+    nt = ctypes.c_int(0)
+    check(load_library().yta_lap_first_round(device, na, nb, ptr(c), ptr(rx), ctypes.byref(done),
+                                             ctypes.byref(nt)))
+    return rx, bool(done.value), nt.value
 
 
 def lap_limited(cost, cost_limit, device=0):

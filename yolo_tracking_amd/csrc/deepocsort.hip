@@ -57,7 +57,8 @@ struct DocCounters {
     int err;
     int lap_done;                  // first round solved by k_doc_lap this frame
     int n_ud, n_upd;               // k_doc_assoc -> k_doc_finish: unmatched detections, updates
-    int pad[15];
+    LapStats ls;                   // cumulative solver counters
+    int pad[12];
 };
 static_assert(sizeof(DocCounters) == 128, "DocCounters layout");
 
@@ -589,7 +590,7 @@ __global__ __launch_bounds__(LAP_T) void k_doc_lap(DocArgs a) {
     first_round_lap(a.mat2 + doc_mb(a, s), c->n_high, c->n_trk, a.rmatch + db, a.cmatched + tb, true,
                     a.pre_u + db, a.pre_x + db, a.pre_s2 + db, a.rmatch + db, lds,
                     lap_kernel_lds(a.CAP, a.MAXD), a.lap_ws + s * a.lap_ws_stride, &c->err,
-                    &c->lap_done);
+                    &c->lap_done, &c->ls, a.lap_ws + (s + 1) * a.lap_ws_stride - tight_ws_bytes());
 }
 
 __global__ __launch_bounds__(OC_T) void k_doc_assoc(DocArgs a) {
@@ -643,7 +644,7 @@ __global__ __launch_bounds__(OC_T) void k_doc_assoc(DocArgs a) {
         } else if (n_hi > 0 && !solved) {
             block_sync();
             main_lap(LapMat{mat2, n_hi, n_trk, false}, a.pre_u + db, a.pre_x + db, a.pre_s2 + db,
-                     a.rmatch + db, lds, lds_bytes, gws, &c->err);
+                     a.rmatch + db, lds, lds_bytes, gws, &c->err, &c->ls);
         }
         YTA_STAMP(1);
         if (t == 0) { c->fast_path = fast; c->lap_calls = (fast || n_hi == 0) ? 0 : 1; }
@@ -690,7 +691,7 @@ __global__ __launch_bounds__(OC_T) void k_doc_assoc(DocArgs a) {
         block_sync();
         mx = block_max(mx, sh);
         if (mx > a.thr) {
-            iou_lap(LapMat{mat, n_ud, n_ut, true}, a.rmatch + db, lds, lds_bytes, gws, &c->err);
+            iou_lap(LapMat{mat, n_ud, n_ut, true}, a.rmatch + db, lds, lds_bytes, gws, &c->err, &c->ls);
             for (int i = t; i < n_hi; i += nt) a.tmp[ub + i] = 0;
             for (int j = t; j < n_trk; j += nt) a.nan_flag[tb + j] = 0;
             block_sync();
@@ -991,7 +992,7 @@ int doc_alloc(yta_deepocsort *e) {
     DOCALLOC(a.ema_row, S * (MAXD + CAP));
     DOCALLOC(a.out, S * CAP * 8);
     const long long n = std::max(CAP, MAXD);
-    a.lap_ws_stride = n > OC_LDS_LAP_N ? ((dense_lap_ws_bytes(n) + 255) & ~255LL) : 256;
+    a.lap_ws_stride = (n > OC_LDS_LAP_N ? ((dense_lap_ws_bytes(n) + 255) & ~255LL) : 256) + tight_ws_bytes();
     DOCALLOC(a.lap_ws, S * a.lap_ws_stride);
     e->lds = (size_t)oc_lds_bytes(CAP, MAXD);
     DOCALLOC(e->d_off, S + 1);
@@ -1474,6 +1475,20 @@ int yta_kf8_run(int device, int n, int steps, const double *b0, const double *b,
     if (he != hipSuccess) {
         set_error("yta_kf8_run: %s", hipGetErrorString(he));
         return YTA_ERR_HIP;
+    }
+    return YTA_OK;
+}
+
+int yta_deepocsort_lap_stats(yta_deepocsort *e, long long *stats) {
+    YTA_CHECK(e && stats, YTA_ERR_INVALID, "null argument");
+    const int rc = doc_read_counters(e);
+    if (rc) return rc;
+    for (int k = 0; k < 3; ++k) stats[k] = 0;
+    for (int s = 0; s < e->S; ++s) {
+        const LapStats &l = e->h_cnt[s].ls;
+        stats[0] += l.transposed;
+        stats[1] += l.uncertified;
+        stats[2] += l.replays;
     }
     return YTA_OK;
 }

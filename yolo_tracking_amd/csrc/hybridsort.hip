@@ -67,7 +67,8 @@ struct HsCounters {
     int n_ema;
     int err;
     int lap_done;                  // first round solved by k_hs_lap this frame
-    int pad[17];
+    LapStats ls;                   // cumulative solver counters
+    int pad[14];
 };
 static_assert(sizeof(HsCounters) == 128, "HsCounters layout");
 
@@ -530,7 +531,7 @@ __global__ __launch_bounds__(LAP_T) void k_hs_lap(HsArgs a) {
     first_round_lap(a.cost + hs_mb(a, s), c->n_high, c->n_trk, a.rmatch + db, a.cmatched + tb, false,
                     a.pre_u + db, a.pre_x + db, a.pre_s2 + db, a.rmatch + db, lds,
                     lap_kernel_lds(a.CAP, a.MAXD), a.lap_ws + s * a.lap_ws_stride, &c->err,
-                    &c->lap_done);
+                    &c->lap_done, &c->ls, a.lap_ws + (s + 1) * a.lap_ws_stride - tight_ws_bytes());
 }
 
 // HybridSORT's long-term correction (hybridsort/association.py:557-567): a first-round pair (kept
@@ -600,7 +601,7 @@ __global__ __launch_bounds__(OC_T) void k_hs_assoc(HsArgs a) {
         block_sync();
         if (!c->lap_done)   // else solved by k_hs_lap
             main_lap(LapMat{cost, n_hi, n_trk, false}, a.pre_u + db, a.pre_x + db, a.pre_s2 + db,
-                 a.rmatch + db, lds, lds_bytes, gws, &c->err);
+                 a.rmatch + db, lds, lds_bytes, gws, &c->err, &c->ls);
         YTA_STAMP(1);
         if (t == 0) c->lap_calls = 1;
         for (int j = t; j < n_trk; j += nt) a.cmatched[tb + j] = 0;
@@ -667,7 +668,7 @@ __global__ __launch_bounds__(OC_T) void k_hs_assoc(HsArgs a) {
         block_sync();
         mx = block_max(mx, sh);
         if (mx > a.thr) {
-            iou_lap(LapMat{mat, n_ud, n_ut, true}, a.rmatch + db, lds, lds_bytes, gws, &c->err);
+            iou_lap(LapMat{mat, n_ud, n_ut, true}, a.rmatch + db, lds, lds_bytes, gws, &c->err, &c->ls);
             for (int i = t; i < n_hi; i += nt) a.tmp[ub + i] = 0;
             for (int j = t; j < n_trk; j += nt) a.nan_flag[tb + j] = 0;
             block_sync();
@@ -934,7 +935,7 @@ int hs_alloc(yta_hybridsort *e) {
     HSALLOC(a.ema_row, S * (MAXD + CAP));
     HSALLOC(a.out, S * CAP * 8);
     const long long n = std::max(CAP, MAXD);
-    a.lap_ws_stride = n > OC_LDS_LAP_N ? ((dense_lap_ws_bytes(n) + 255) & ~255LL) : 256;
+    a.lap_ws_stride = (n > OC_LDS_LAP_N ? ((dense_lap_ws_bytes(n) + 255) & ~255LL) : 256) + tight_ws_bytes();
     HSALLOC(a.lap_ws, S * a.lap_ws_stride);
     e->lds = (size_t)oc_lds_bytes(CAP, MAXD);
     HSALLOC(e->d_off, S + 1);
@@ -1372,6 +1373,20 @@ int yta_kf9_run(int device, int n, int steps, const double *b0, const double *b,
     if (he != hipSuccess) {
         set_error("yta_kf9_run: %s", hipGetErrorString(he));
         return YTA_ERR_HIP;
+    }
+    return YTA_OK;
+}
+
+int yta_hybridsort_lap_stats(yta_hybridsort *e, long long *stats) {
+    YTA_CHECK(e && stats, YTA_ERR_INVALID, "null argument");
+    const int rc = hs_read_counters(e);
+    if (rc) return rc;
+    for (int k = 0; k < 3; ++k) stats[k] = 0;
+    for (int s = 0; s < e->S; ++s) {
+        const LapStats &l = e->h_cnt[s].ls;
+        stats[0] += l.transposed;
+        stats[1] += l.uncertified;
+        stats[2] += l.replays;
     }
     return YTA_OK;
 }

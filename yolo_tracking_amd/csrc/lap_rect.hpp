@@ -45,17 +45,19 @@ struct RectMat {
 // Work arrays (LDS or global): rect_ws_bytes(rows, cols) bytes, 8-aligned.
 struct RectWs {
     double *u, *s2;     // rows
+    double *v;          // cols: the column duals on return (<= 0, 0 on free columns)
     int *x, *fl;        // rows: assigned column, free-row list
     int *path, *yw;     // cols: predecessor row, owner row (authoritative copy)
 };
 __host__ __device__ inline long long rect_ws_bytes(long long rows, long long cols) {
-    return rows * 24 + cols * 8 + 64;
+    return rows * 24 + cols * 16 + 64;
 }
 __host__ __device__ inline RectWs rect_ws(unsigned char *base, int rows, int cols) {
     RectWs w;
     w.u = reinterpret_cast<double *>(base);
     w.s2 = w.u + rows;
-    w.x = reinterpret_cast<int *>(w.s2 + rows);
+    w.v = w.s2 + rows;
+    w.x = reinterpret_cast<int *>(w.v + cols);
     w.fl = w.x + rows;
     w.path = w.fl + rows;
     w.yw = w.path + cols;
@@ -306,6 +308,11 @@ __device__ __forceinline__ int lap_rect_body(const RectMat M, const double *pre_
         }
     }
     YTA_STAMP_ABS(105);
+#pragma unroll
+    for (int q = 0; q < CPT; ++q) {
+        const int j = t + q * nt;
+        if (j < cols) w.v[j] = v[q];
+    }
     return 0;
 }
 
@@ -325,6 +332,8 @@ __device__ __forceinline__ int lap_rect(const RectMat M, const double *pre_u, co
         if (M.cols <= 2 * nt) return lap_rect_body<2>(M, pre_u, pre_x, pre_s2, w, sh);
         if (M.cols <= 8 * nt) return lap_rect_body<8>(M, pre_u, pre_x, pre_s2, w, sh);
         if (M.cols <= 16 * nt) return lap_rect_body<16>(M, pre_u, pre_x, pre_s2, w, sh);
+        // > 8192 columns (rare): not inlined, so its spills do not touch the common bodies
+        if (M.cols <= RECT_CPT_MAX * nt) return lap_rect_block<RECT_CPT_MAX>(M, pre_u, pre_x, pre_s2, w, sh);
         return -3;
     }
     if (M.cols <= 2 * nt) return lap_rect_block<2>(M, pre_u, pre_x, pre_s2, w, sh);

@@ -55,7 +55,8 @@ struct OcCounters {                // one per stream
     int lap_calls, fast_path;
     int err;
     int lap_done;                  // first round solved by k_oc_lap this frame
-    int pad[17];
+    LapStats ls;                   // cumulative solver counters
+    int pad[14];
 };
 static_assert(sizeof(OcCounters) == 128, "OcCounters layout");
 
@@ -329,7 +330,7 @@ __global__ __launch_bounds__(LAP_T) void k_oc_lap(OcArgs a) {
     first_round_lap(a.mat2 + (long long)s * (a.MAXD > 4 ? a.MAXD : 4) * a.CAP, c->n_high, c->n_trk, a.rmatch + db, a.cmatched + tb, true,
                     a.pre_u + db, a.pre_x + db, a.pre_s2 + db, a.rmatch + db, lds,
                     lap_kernel_lds(a.CAP, a.MAXD), a.lap_ws + s * a.lap_ws_stride, &c->err,
-                    &c->lap_done);
+                    &c->lap_done, &c->ls, a.lap_ws + (s + 1) * a.lap_ws_stride - tight_ws_bytes());
 }
 
 __global__ __launch_bounds__(OC_T) void k_oc_assoc(OcArgs a) {
@@ -396,7 +397,7 @@ __global__ __launch_bounds__(OC_T) void k_oc_assoc(OcArgs a) {
         } else if (n_hi > 0 && !solved) {
             block_sync();
             main_lap(LapMat{mat2, n_hi, n_trk, false}, a.pre_u + db, a.pre_x + db, a.pre_s2 + db,
-                     a.rmatch + db, lds, lds_bytes, gws, &c->err);
+                     a.rmatch + db, lds, lds_bytes, gws, &c->err, &c->ls);
         }
         YTA_STAMP(4);
         if (t == 0) { c->fast_path = fast; c->lap_calls = (fast || n_hi == 0) ? 0 : 1; }
@@ -445,7 +446,7 @@ __global__ __launch_bounds__(OC_T) void k_oc_assoc(OcArgs a) {
         block_sync();
         mx = block_max(mx, sh);
         if (mx > a.thr) {
-            iou_lap(LapMat{mat, n_lo, n_ut, true}, a.rmatch + db, lds, lds_bytes, gws, &c->err);
+            iou_lap(LapMat{mat, n_lo, n_ut, true}, a.rmatch + db, lds, lds_bytes, gws, &c->err, &c->ls);
             for (int k = t; k < n_ut; k += nt) a.tmp[ub + k] = 0;   // taken flags
             block_sync();
             for (int p = t; p < n_lo; p += nt) {
@@ -482,7 +483,7 @@ __global__ __launch_bounds__(OC_T) void k_oc_assoc(OcArgs a) {
         block_sync();
         mx = block_max(mx, sh);
         if (mx > a.thr) {
-            iou_lap(LapMat{mat, n_ud, n_ut, true}, a.rmatch + db, lds, lds_bytes, gws, &c->err);
+            iou_lap(LapMat{mat, n_ud, n_ut, true}, a.rmatch + db, lds, lds_bytes, gws, &c->err, &c->ls);
             // removed dets / trackers -> flags, then sorted set differences
             for (int i = t; i < n_hi; i += nt) a.tmp[ub + i] = 0;
             for (int j = t; j < n_trk; j += nt) a.nan_flag[tb + j] = 0;
@@ -695,7 +696,7 @@ int oc_alloc(yta_ocsort *e) {
     OCALLOC(a.upd, S * CAP);
     OCALLOC(a.out, S * CAP * 8);
     const long long n = std::max(CAP, MAXD);
-    a.lap_ws_stride = n > OC_LDS_LAP_N ? ((dense_lap_ws_bytes(n) + 255) & ~255LL) : 256;
+    a.lap_ws_stride = (n > OC_LDS_LAP_N ? ((dense_lap_ws_bytes(n) + 255) & ~255LL) : 256) + tight_ws_bytes();
     OCALLOC(a.lap_ws, S * a.lap_ws_stride);
     e->lds = (size_t)oc_lds_bytes(CAP, MAXD);
     OCALLOC(e->d_off, S + 1);
@@ -1076,6 +1077,20 @@ int yta_ocsort_stats(yta_ocsort *e, long long *stats) {
     return YTA_OK;
 }
 
+int yta_ocsort_lap_stats(yta_ocsort *e, long long *stats) {
+    YTA_CHECK(e && stats, YTA_ERR_INVALID, "null argument");
+    const int rc = oc_read_counters(e);
+    if (rc) return rc;
+    for (int k = 0; k < 3; ++k) stats[k] = 0;
+    for (int s = 0; s < e->S; ++s) {
+        const LapStats &l = e->h_cnt[s].ls;
+        stats[0] += l.transposed;
+        stats[1] += l.uncertified;
+        stats[2] += l.replays;
+    }
+    return YTA_OK;
+}
+
 int yta_ocsort_hip_stream(yta_ocsort *e, void **stream) {
     YTA_CHECK(e && stream, YTA_ERR_INVALID, "null argument");
     *stream = (void *)e->stream;
@@ -1171,5 +1186,87 @@ extern "C" int yta_kf7_run(int device, int n, int steps, const double *z0, const
     if (he == hipSuccess) he = hipMemcpy(P_out, d_P, sizeof(double) * 49 * n, hipMemcpyDeviceToHost);
     cleanup();
     YTA_CHECK(he == hipSuccess, YTA_ERR_HIP, "kf7 KAT: %s", hipGetErrorString(he));
+    return YTA_OK;
+}
+
+// ----------------------------------------------------------------------------------------------
+// First-round solve KAT (ocsort_common.hpp): the chip-wide row pre-pass and the LAP_T-thread
+// solve exactly as the engines launch them, on one na x nb cost matrix (rows = detections,
+// columns = trackers; no fast path).  rx[i] = tracker of detection i or -1 when solved; *done = 0
+// when the association kernel would replay lapjv instead; *gap = the uniqueness certificate of a
+// transposed solve (na > nb; +inf otherwise).
+namespace {
+__global__ __launch_bounds__(OC_T) void k_kat_fr_pre(const double *m, int na, int nb, double *u,
+                                                     int *x, double *s2) {
+    main_lap_pre(m, na, nb, u, x, s2);
+}
+__global__ __launch_bounds__(LAP_T) void k_kat_fr(const double *m, int na, int nb, const double *u,
+                                                  const int *x, const double *s2, int *rx,
+                                                  long long lds_bytes, unsigned char *gws, int *st,
+                                                  int *n_tight) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    LapStats ls{0, 0, 0};
+    if (threadIdx.x == 0) *n_tight = -1;
+    __syncthreads();
+    first_round_lap(m, na, nb, rx, rx, false, u, x, s2, rx, lds, lds_bytes, gws, st, st + 1, &ls,
+                    gws + dense_lap_ws_bytes(na > nb ? na : nb), n_tight);
+}
+struct KatBuf {
+    std::vector<void *> ptrs;
+    ~KatBuf() {
+        for (void *p : ptrs) (void)hipFree(p);
+    }
+    template <typename T>
+    hipError_t get(T **p, size_t n) {
+        void *q = nullptr;
+        const hipError_t e = hipMalloc(&q, sizeof(T) * (n ? n : 1));
+        if (e == hipSuccess) ptrs.push_back(q);
+        *p = (T *)q;
+        return e;
+    }
+};
+}  // namespace
+
+extern "C" int yta_lap_first_round(int device, int na, int nb, const double *cost, int *rx,
+                                   int *done, int *n_tight) {
+    YTA_CHECK(na > 0 && nb > 0 && cost && rx && done && n_tight, YTA_ERR_INVALID, "bad arguments");
+    const int n = std::max(na, nb);
+    YTA_CHECK(n <= RECT_CPT_MAX * LAP_T, YTA_ERR_INVALID, "more than %d rows or columns",
+              RECT_CPT_MAX * LAP_T);
+    int rc = select_device(device);
+    if (rc) return rc;
+    KatBuf m;
+    double *dc, *u, *s2;
+    int *x, *drx, *st, *dg;
+    unsigned char *gws;
+    YTA_HIP(m.get(&dc, (long long)na * nb));
+    YTA_HIP(m.get(&u, n));
+    YTA_HIP(m.get(&s2, n));
+    YTA_HIP(m.get(&x, n));
+    YTA_HIP(m.get(&drx, na));
+    YTA_HIP(m.get(&st, 2));
+    YTA_HIP(m.get(&dg, 1));
+    YTA_HIP(m.get(&gws, (size_t)(dense_lap_ws_bytes(n) + tight_ws_bytes())));
+    YTA_HIP(hipMemcpy(dc, cost, sizeof(double) * na * nb, hipMemcpyHostToDevice));
+    YTA_HIP(hipMemset(drx, 0, sizeof(int) * na));   // rcnt = 0: no fast path
+    YTA_HIP(hipMemset(st, 0, sizeof(int) * 2));
+    static bool attr = false;
+    if (!attr) {
+        YTA_HIP(hipFuncSetAttribute((const void *)k_kat_fr,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)LAP_LDS_MAX));
+        attr = true;
+    }
+    const long long lds = lap_kernel_lds(nb, na);
+    hipLaunchKernelGGL(k_kat_fr_pre, dim3(256), dim3(OC_T), 0, 0, dc, na, nb, u, x, s2);
+    YTA_HIP(hipGetLastError());
+    hipLaunchKernelGGL(k_kat_fr, dim3(1), dim3(LAP_T), (size_t)lds, 0, dc, na, nb, u, x, s2, drx,
+                       lds, gws, st, dg);
+    YTA_HIP(hipGetLastError());
+    int hst[2];
+    YTA_HIP(hipMemcpy(hst, st, sizeof(hst), hipMemcpyDeviceToHost));
+    YTA_HIP(hipMemcpy(rx, drx, sizeof(int) * na, hipMemcpyDeviceToHost));
+    YTA_HIP(hipMemcpy(n_tight, dg, sizeof(int), hipMemcpyDeviceToHost));
+    YTA_CHECK(hst[0] == 0, YTA_ERR_HIP, "solver error flags 0x%x", hst[0]);
+    *done = hst[1];
     return YTA_OK;
 }

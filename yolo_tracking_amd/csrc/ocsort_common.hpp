@@ -47,12 +47,20 @@ __device__ __forceinline__ double block_max(double v, OcShared &sh) {
     return m;
 }
 
+// Solver counters of a stream, cumulative over frames (yta_*_lap_stats): first-round solves of the
+// transposed problem (more detections than trackers), those whose optimum was not certified
+// unique, and lapjv replays (padded_lap, any round).
+struct LapStats {
+    int transposed, uncertified, replays;
+};
+
 // association.py:20-28 on the padded problem M: wave 0 solves, x[r] = column or -1 -> rx.
 // The solver is one dependent chain of row reads; the matrix was written by k_oc_cost on every
 // XCD, so the whole block first streams it once (coalesced) into this XCD's L2.
 __device__ __forceinline__ void padded_lap(const LapMat &M, int *rx, unsigned char *lds,
-                                           unsigned char *gws, int *err) {
+                                           unsigned char *gws, int *err, LapStats *ls) {
     const int n = M.na > M.nb ? M.na : M.nb;
+    if (threadIdx.x == 0 && n > 0) ls->replays += 1;
     {
         const long long cnt = (long long)M.na * M.nb;
         double acc = 0.0;
@@ -67,6 +75,20 @@ __device__ __forceinline__ void padded_lap(const LapMat &M, int *rx, unsigned ch
         for (int r = lane_id(); r < M.na; r += WAVE) rx[r] = w.x[r] < M.nb ? w.x[r] : -1;
     }
     block_sync();
+}
+
+#ifndef YTA_LAP_T
+#define YTA_LAP_T 512
+#endif
+constexpr int LAP_T = YTA_LAP_T;                // threads of the first-round solve kernels
+constexpr long long LAP_LDS_MAX = 156 * 1024;   // their dynamic LDS cap (160 KiB - static)
+
+// The first-round solve's work arrays, either orientation (first_round_lap transposes the
+// problem when detections outnumber trackers).
+__host__ __device__ inline long long lap_kernel_lds(long long CAP, long long MAXD) {
+    const long long b1 = rect_ws_bytes(MAXD, CAP), b2 = rect_ws_bytes(CAP, MAXD);
+    const long long b = b1 > b2 ? b1 : b2;
+    return b < LAP_LDS_MAX ? b : LAP_LDS_MAX;
 }
 
 // Dynamic LDS of the association kernels (host launch size and device-side view of it).
@@ -99,38 +121,81 @@ __device__ __forceinline__ void rect_solve(const RectMat &R, const double *pu, c
 }
 
 // First-round solve of association.py:20-28 on the padded problem M (rows = detections, columns =
-// trackers).  With trackers >= detections every detection row is matched and the result does not
-// depend on lapjv's tie-breaking: the rectangular solver, warm-started by the
-// chip-wide row pre-pass (pu / px / ps2, main_lap_pre).  Otherwise the lapjv replay.
+// trackers) when k_*_lap left it (more than 16384 trackers): the rectangular solver with
+// trackers >= detections, otherwise the lapjv replay.
 __device__ __forceinline__ void main_lap(const LapMat &M, const double *pu, const int *px,
                                          const double *ps2, int *rx, unsigned char *lds,
-                                         long long lds_bytes, unsigned char *gws, int *err) {
+                                         long long lds_bytes, unsigned char *gws, int *err,
+                                         LapStats *ls) {
     if (M.na <= M.nb && M.nb <= RECT_CPT_MAX * (int)blockDim.x)
         rect_solve(RectMat{M.m, M.na, M.nb, M.nb, 1, M.neg}, pu, px, ps2, false, M.na, rx, lds,
                    lds_bytes, gws, err);
     else
-        padded_lap(M, rx, lds, gws, err);
+        padded_lap(M, rx, lds, gws, err, ls);
 }
 
-// Row pre-pass of main_lap for one stream, spread over the blocks of a chip-wide launch.
+// Row pre-pass of the first-round solve for one stream, spread over the blocks of a chip-wide
+// launch.  na <= nb: the rows of mat (one wave a row).  na > nb: the rows of the transposed
+// problem (first_round_lap), i.e. the columns of mat: a block takes 64 tracker columns, lane =
+// column (coalesced across the wave), its waves split the detection rows, partials merged in LDS.
 __device__ __forceinline__ void main_lap_pre(const double *mat, int na, int nb, double *u, int *x,
                                              double *s2) {
-    if (na <= 0 || na > nb || nb > RECT_CPT_MAX * OC_T) return;
-    const RectMat M{mat, na, nb, nb, 1, false};
+    if (na <= 0 || nb <= 0) return;
     const int nw = blockDim.x / WAVE;
-    for (int i = blockIdx.x * nw + threadIdx.x / WAVE; i < na; i += gridDim.x * nw)
-        rect_row_pre(M, i, u, x, s2);
+    if (na <= nb) {
+        if (nb > RECT_CPT_MAX * LAP_T) return;
+        const RectMat M{mat, na, nb, nb, 1, false};
+        for (int i = blockIdx.x * nw + threadIdx.x / WAVE; i < na; i += gridDim.x * nw)
+            rect_row_pre(M, i, u, x, s2);
+        return;
+    }
+    if (na > RECT_CPT_MAX * LAP_T) return;
+    __shared__ double pm1[OC_T], pm2[OC_T];
+    __shared__ int pk1[OC_T];
+    const int lane = lane_id(), wid = threadIdx.x / WAVE;
+    for (int g = blockIdx.x; g * WAVE < nb; g += gridDim.x) {
+        const int j = g * WAVE + lane;
+        double m1 = INFINITY, m2 = INFINITY;
+        int k1 = INT_MAX;
+        if (j < nb)
+            for (int i = wid; i < na; i += nw) {   // ascending rows: strict < keeps the first
+                const double c = mat[(long long)i * nb + j];
+                if (c < m1) { m2 = m1; m1 = c; k1 = i; }
+                else if (c < m2) m2 = c;
+            }
+        pm1[threadIdx.x] = m1;
+        pm2[threadIdx.x] = m2;
+        pk1[threadIdx.x] = k1;
+        __syncthreads();
+        if (wid == 0 && j < nb) {
+            for (int w = 1; w < nw; ++w) {
+                const double om1 = pm1[w * WAVE + lane], om2 = pm2[w * WAVE + lane];
+                const int ok1 = pk1[w * WAVE + lane];
+                const bool other = om1 < m1 || (om1 == m1 && ok1 < k1);
+                const double lose = other ? m1 : om1;
+                const double m2w = other ? om2 : m2;
+                m2 = lose < m2w ? lose : m2w;
+                m1 = other ? om1 : m1;
+                k1 = other ? ok1 : k1;
+            }
+            u[j] = m1;
+            x[j] = k1 == INT_MAX ? 0 : k1;
+            s2[j] = m2 - m1;
+        }
+        __syncthreads();
+    }
 }
 
 // The -IoU rounds (BYTE / OCR: association.py:20-28 on -iou): only pairs with IoU >= threshold
 // survive and the leftover lists are re-sorted (np.setdiff1d), so any optimal solution gives the
 // reference's result: the rectangular solver in whichever orientation has rows <= columns.
 __device__ __forceinline__ void iou_lap(const LapMat &M, int *rx, unsigned char *lds,
-                                        long long lds_bytes, unsigned char *gws, int *err) {
+                                        long long lds_bytes, unsigned char *gws, int *err,
+                                        LapStats *ls) {
     const bool tr = M.na > M.nb;
     const int rows = tr ? M.nb : M.na, cols = tr ? M.na : M.nb;
     if (cols > RECT_CPT_MAX * (int)blockDim.x) {
-        padded_lap(M, rx, lds, gws, err);
+        padded_lap(M, rx, lds, gws, err, ls);
         return;
     }
     const RectMat R = tr ? RectMat{M.m, rows, cols, 1, M.nb, M.neg}
@@ -138,32 +203,111 @@ __device__ __forceinline__ void iou_lap(const LapMat &M, int *rx, unsigned char 
     rect_solve(R, nullptr, nullptr, nullptr, tr, M.na, rx, lds, lds_bytes, gws, err);
 }
 
-#ifndef YTA_LAP_T
-#define YTA_LAP_T 512
-#endif
-constexpr int LAP_T = YTA_LAP_T;                // threads of the first-round solve kernels
-constexpr long long LAP_LDS_MAX = 156 * 1024;   // their dynamic LDS cap (160 KiB - static)
-
-__host__ __device__ inline long long lap_kernel_lds(long long CAP, long long MAXD) {
-    const long long b = rect_ws_bytes(MAXD, CAP);
-    return b < LAP_LDS_MAX ? b : LAP_LDS_MAX;
+// Is x, the solution of the transposed first-round problem (rows = trackers, all matched;
+// columns = detections), its UNIQUE optimum?  With the solver's column duals v (v <= 0, v = 0 on
+// unmatched columns) and u_i = c(i, x_i) - v(x_i), (u, v) is dual feasible and tight on x, so by
+// complementary slackness every optimum uses tight edges only and matches every column with
+// v < 0.  Another optimum differs from x by an alternating cycle of tight edges, or by an
+// alternating path of tight edges ending at an unmatched column.  The shortest-path trees of the
+// augmentations leave tight non-matching edges behind (a row stays tight to the column it left),
+// so the test is structural: collect the tight non-matching edges (reduced cost <= UNIQ_TOL, a
+// margin over either solver's rounding: |c| <~ 3, a few hundred dual updates), fail on one into
+// an unmatched column, and look for a cycle in the column digraph (x_i -> k for a tight (i, k)),
+// by peeling columns without out-edges.  Unique => lapjv (any exact solver) returns x too,
+// whatever its tie-breaking.  Block-wide; the edges go to `tws` (TIGHT_CAP), out-degrees to the
+// solver's path array (dead after the solve).  Returns 1 = unique; *n_tight = edges found.
+constexpr double UNIQ_TOL = 1e-9;
+constexpr int TIGHT_CAP = 16384;
+__host__ __device__ inline long long tight_ws_bytes() { return 8LL * TIGHT_CAP; }
+__device__ __forceinline__ int unique_optimum_tr(const double *mat, int na, int nb, const RectWs &w,
+                                                 int2 *tws, int *n_tight) {
+    __shared__ int ne, bad, changed[2];
+    const int t = threadIdx.x, nt = blockDim.x;
+    if (t == 0) { ne = 0; bad = 0; changed[0] = changed[1] = 0; }
+    block_sync();
+    for (int j0 = 0; j0 < nb; j0 += nt) {
+        const int j = j0 + t;
+        if (j >= nb) break;
+        const int xj = w.x[j];
+        const double own = mat[(long long)xj * nb + j] - w.v[xj];
+        auto visit = [&](int i, double c) {
+            const double r = (c - w.v[i]) - own;
+            if (r != r) { bad = 1; return; }
+            if (i == xj || r > UNIQ_TOL) return;
+            if (w.yw[i] < 0) { bad = 1; return; }   // tight into an unmatched column
+            const int k = atomicAdd(&ne, 1);
+            if (k < TIGHT_CAP) tws[k] = make_int2(xj, i);
+            else bad = 1;
+        };
+        int i = 0;
+        for (; i + 4 <= na; i += 4) {
+            double c[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) c[k] = mat[(long long)(i + k) * nb + j];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) visit(i + k, c[k]);
+        }
+        for (; i < na; ++i) visit(i, mat[(long long)i * nb + j]);
+    }
+    block_sync();
+    const int m = ne < TIGHT_CAP ? ne : TIGHT_CAP;
+    if (n_tight && t == 0) *n_tight = ne;
+    if (bad) return 0;
+    if (m == 0) return 1;
+    int *deg = w.path;
+    for (int i = t; i < na; i += nt) deg[i] = 0;
+    block_sync();
+    for (int e = t; e < m; e += nt) atomicAdd(&deg[tws[e].x], 1);
+    block_sync();
+    for (int par = 0;; par ^= 1) {   // peel: an edge into a column without out-edges goes
+        for (int e = t; e < m; e += nt) {
+            const int2 ed = tws[e];
+            if (ed.x >= 0 && atomicAdd(&deg[ed.y], 0) == 0) {
+                atomicSub(&deg[ed.x], 1);
+                tws[e].x = -1;
+                changed[par] = 1;
+            }
+        }
+        block_sync();
+        const int ch = changed[par];
+        if (t == 0) changed[par ^ 1] = 0;
+        block_sync();
+        if (!ch) break;
+    }
+    int left = 0;
+    for (int e = t; e < m; e += nt) left |= tws[e].x >= 0;
+    if (left) bad = 1;   // a cycle of tight edges
+    block_sync();
+    return bad == 0;
 }
 
-// First-round solve in its own launch, one LAP_T-thread block per stream (up to 16 columns per
-// thread: 8192 trackers, every cost load of a step in flight at once).  When trackers >= detections and
-// the fast path (association.py:156-159, `fast_rule`) does not apply, solve with lap_rect
-// (warm-started by the row pre-pass) into rx and set *done; the association kernel then skips its
-// own first-round solve.  rcnt / ccnt: the per-row / per-column counts of asso > thr (rcnt may
-// alias rx: it is read before the solve).
+// First-round solve in its own launch, one LAP_T-thread block per stream (up to 32 columns per
+// thread: 16384 columns, every cost load of a step in flight at once), when the fast path
+// (association.py:156-159, `fast_rule`) does not apply; rx and *done = 1 on success, else the
+// association kernel solves.  rcnt / ccnt: the per-row / per-column counts of asso > thr (rcnt
+// may alias rx: it is read before the solve).
+//  * trackers >= detections: lap_rect warm-started by the row pre-pass; every detection row is
+//    matched and the outputs do not depend on which optimum is returned.
+//  * more detections than trackers (a crowd entering): which detections stay on lapjv's dummy
+//    columns sets the order of the unmatched list (association.py:179-199) and so the birth ids;
+//    the transposed problem (trackers as rows, every one matched; dummy columns cost 0, so the
+//    padded optimum is the rectangular one) is solved, and kept when its optimum is certified
+//    unique (unique_optimum_tr).  Otherwise (exact ties: e.g. a tracker without velocity and
+//    without overlap has a whole row of exact zeros under IoU) *done = 0 and the association
+//    kernel replays lapjv.
 __device__ __forceinline__ void first_round_lap(const double *mat, int na, int nb, const int *rcnt,
                                                 const int *ccnt, bool fast_rule, const double *pu,
                                                 const int *px, const double *ps2, int *rx,
                                                 unsigned char *lds, long long lds_bytes,
-                                                unsigned char *gws, int *err, int *done) {
+                                                unsigned char *gws, int *err, int *done,
+                                                LapStats *ls, unsigned char *tws,
+                                                int *n_tight = nullptr) {
     __shared__ RectShared rsh;
     __shared__ int flags[2];
     const int t = threadIdx.x, nt = blockDim.x;
-    bool solve = na > 0 && na <= nb && nb <= 16 * nt;
+    const bool tr = na > nb;
+    const int rows = tr ? nb : na, cols = tr ? na : nb;
+    bool solve = rows > 0 && cols <= RECT_CPT_MAX * nt;
     if (solve && fast_rule) {
         if (t < 2) flags[t] = 0;
         __syncthreads();
@@ -183,11 +327,30 @@ __device__ __forceinline__ void first_round_lap(const double *mat, int na, int n
         if (t == 0) *done = 0;
         return;
     }
-    unsigned char *base = rect_ws_bytes(na, nb) <= lds_bytes ? lds : gws;
-    const RectWs w = rect_ws(base, na, nb);
-    const int rc = lap_rect<LAP_T>(RectMat{mat, na, nb, nb, 1, false}, pu, px, ps2, w, rsh);
+    unsigned char *base = rect_ws_bytes(rows, cols) <= lds_bytes ? lds : gws;
+    const RectWs w = rect_ws(base, rows, cols);
+    const RectMat R = tr ? RectMat{mat, rows, cols, 1, nb, false} : RectMat{mat, rows, cols, nb, 1, false};
+    const int rc = lap_rect<LAP_T>(R, pu, px, ps2, w, rsh);
     if (rc && t == 0) atomicOr(err, ERR_SOLVER);
-    for (int i = t; i < na; i += nt) rx[i] = rc ? -1 : w.x[i];
+    if (!tr) {
+        for (int i = t; i < na; i += nt) rx[i] = rc ? -1 : w.x[i];
+        if (t == 0) *done = 1;
+        return;
+    }
+    if (t == 0) ls->transposed += 1;
+    block_sync();
+    const bool uniq = rc == 0 &&
+        unique_optimum_tr(mat, na, nb, w, reinterpret_cast<int2 *>(tws), n_tight);
+    if (!uniq) {
+        if (t == 0) {
+            if (rc == 0) ls->uncertified += 1;
+            *done = 0;
+        }
+        return;
+    }
+    for (int i = t; i < na; i += nt) rx[i] = -1;
+    block_sync();
+    for (int k = t; k < nb; k += nt) rx[w.x[k]] = k;
     if (t == 0) *done = 1;
 }
 

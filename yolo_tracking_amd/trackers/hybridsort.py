@@ -77,6 +77,15 @@ class HybridSortEngine:
         _lib.check(self.lib.yta_hybridsort_capacity(self._h, ctypes.byref(c), ctypes.byref(d)))
         return c.value, d.value
 
+    def lap_stats(self):
+        """Solver counters since create / reset (yta_hybridsort_lap_stats): first-round solves of the
+        transposed problem (more detections than trackers), those not certified unique, and
+        lapjv replays."""
+        names = ["transposed", "uncertified", "replays"]
+        buf = (ctypes.c_longlong * len(names))()
+        _lib.check(self.lib.yta_hybridsort_lap_stats(self._h, buf))
+        return {k: int(buf[i]) for i, k in enumerate(names)}
+
     def stats(self):
         names = ["dets", "high", "trackers", "out", "births", "lap_calls", "corrections",
                  "feature_jobs"]

@@ -64,6 +64,15 @@ class OCSortEngine:
         _lib.check(self.lib.yta_ocsort_capacity(self._h, ctypes.byref(c), ctypes.byref(d)))
         return c.value, d.value
 
+    def lap_stats(self):
+        """Solver counters since create / reset (yta_ocsort_lap_stats): first-round solves of the
+        transposed problem (more detections than trackers), those not certified unique, and
+        lapjv replays."""
+        names = ["transposed", "uncertified", "replays"]
+        buf = (ctypes.c_longlong * len(names))()
+        _lib.check(self.lib.yta_ocsort_lap_stats(self._h, buf))
+        return {k: int(buf[i]) for i, k in enumerate(names)}
+
     def stats(self):
         names = ["dets", "high", "second", "trackers", "out", "births", "lap_calls", "fast_path"]
         buf = (ctypes.c_longlong * len(names))()
