@@ -1,0 +1,111 @@
+#!/usr/bin/env python3
+"""Roofline lines for BASELINE.json configs 2-5 from a tools/bench_tracker.py
+line and the rocprofv3 kernel stats of the same command.
+
+    python tools/config_roofline.py BENCH.json KERNEL_STATS.csv > line.json
+
+Two views, both printed:
+  * canonical: §8(d)'s per-update algorithmic bytes B and FLOPs F (dense formulation: a 16*N*M
+    cost matrix, the full Kalman state, the D=512 cosine GEMMs), bound = max(B / 8 TB/s,
+    F / f64 peak) per update, and the fraction of it the measured update time reaches;
+  * per kernel: every kernel's share of the step, with its own bound where it has one (the f64
+    embedding GEMMs: FLOPs / duration vs the f64 peak; the dense cost passes: bytes / duration vs
+    HBM); the first-round solves (k_*_lap) and the one-block association kernels are dependent
+    chains (Dijkstra steps, list scans) and carry no roofline ("latency").
+Peaks: HBM 8.0 TB/s (MI355X_MICROARCH.md); f64 78.6 TFLOP/s (vector = matrix on MI355X, vendor
+spec, SURVEY.md §8(d) -- not in the microarchitecture guide's measured table).
+"""
+import csv
+import json
+import sys
+
+HBM = 8.0e12
+F64 = 78.6e12
+STATE = {"ocsort": 448, "botsort": 576, "deepocsort": 576, "hybridsort": 720}
+GEMMS = {"ocsort": 0, "botsort": 1, "deepocsort": 1, "hybridsort": 2}
+
+
+def canonical(tracker, N, M, D):
+    """SURVEY.md §8(d) 'Algorithmic bytes per update' and FLOPs, one stream."""
+    S = STATE[tracker]
+    b = 4 * S * N + 56 * M + 16 * N * M + 64 * N
+    if tracker == "ocsort":
+        b += 136 * N
+    elif tracker == "botsort":
+        b += 4 * D * (N + M) + 8 * D * N
+    elif tracker == "deepocsort":
+        b += 2 * S * N + 16 * N * M + 136 * N + 8 * D * N + 4 * D * M + 16 * D * N
+    elif tracker == "hybridsort":
+        b += 208 * N + 8 * D * N + 4 * D * 30 * N + 4 * D * M + 16 * D * N + 4 * D * N
+    return b, 2 * N * M * D * GEMMS[tracker]
+
+
+def kernel_model(tracker, name, trk, det, D, S):
+    """Work of one launch summed over the streams (trk / det: live trackers / kept detections of
+    the last frame, summed over streams): ('flop', F) for the embedding GEMMs, ('hbm', B) for the
+    dense cost passes (each f64 matrix entry read / written once), None for latency chains."""
+    nm = trk * det / S   # matrix entries over all streams (the streams are alike: S * (trk/S) * (det/S))
+    if "_emb" in name and tracker in ("deepocsort", "hybridsort"):
+        return ("flop", 2.0 * nm * D)
+    if tracker == "ocsort" and "k_oc_cost" in name:
+        return ("hbm", 2 * 8 * nm)            # asso + asso+angle written
+    if tracker == "deepocsort":
+        if "k_doc_cost" in name:
+            return ("hbm", 2 * 8 * nm)
+        if "k_doc_final" in name:
+            return ("hbm", 4 * 8 * nm)        # asso, emb, cost read; cost written
+        if "k_doc_aw" in name and "cols" not in name:
+            return ("hbm", 2 * 8 * nm)        # emb read by rows and by column chunks
+    if "rowpre" in name:
+        return ("hbm", 8 * nm)
+    return None
+
+
+def main():
+    bench = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
+    rows = list(csv.DictReader(open(sys.argv[2])))
+    tracker = bench["metric"].split()[0]
+    N = int(bench["metric"].split("@")[1].split()[0])
+    D = int(bench["config"]["workload"].split("D=")[1].split(",")[0]) if "D=" in bench["config"]["workload"] else 0
+    S = int(bench["config"]["streams"])
+    fc = bench.get("frame_counts", {})
+    trk = fc.get("trackers", N * S)
+    det = fc.get("high", N * S)
+    B, F = canonical(tracker, N, N, D)
+    t_upd = bench["ms_per_step"] * 1e-3 / S
+    tb, tf = B / HBM, F / F64
+    bound = max(tb, tf)
+    kernels = []
+    steps = bench["steps"] + bench["warmup"]
+    for r in rows:
+        name = r["Name"]
+        if "yta::" not in name:
+            continue
+        avg = float(r["AverageNs"]) * 1e-9
+        calls = int(r["Calls"])
+        k = {"kernel": name.replace("(anonymous namespace)::", "").split("(")[0].split("::")[-1],
+             "avg_us": round(avg * 1e6, 2), "calls": calls,
+             "share_of_step": round(avg * calls / steps / (bench["ms_per_step"] * 1e-3), 4)}
+        m = kernel_model(tracker, name, trk, det, D, S)
+        if m is None:
+            k["bound"] = "latency"
+        elif m[0] == "flop":
+            k.update(bound="f64", achieved_tflops=round(m[1] / avg / 1e12, 2),
+                     peak_tflops=F64 / 1e12, frac=round(m[1] / avg / F64, 4))
+        else:
+            k.update(bound="hbm", achieved_gbs=round(m[1] / avg / 1e9, 1), peak_gbs=HBM / 1e9,
+                     frac=round(m[1] / avg / HBM, 4))
+        kernels.append(k)
+    kernels.sort(key=lambda k: -k["share_of_step"])
+    out = {"tracker": tracker, "config": bench["config"], "calls_per_s": bench["value"],
+           "ms_per_update": t_upd * 1e3,
+           "canonical": {"bytes_per_update": B, "flops_per_update": F,
+                         "t_bytes_us": tb * 1e6, "t_flops_us": tf * 1e6,
+                         "binding": "f64" if tf > tb else "hbm",
+                         "bound_us": bound * 1e6, "frac": bound / t_upd},
+           "dominant": kernels[0] if kernels else None, "kernels": kernels}
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
