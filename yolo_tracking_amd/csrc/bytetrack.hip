@@ -1659,9 +1659,20 @@ __device__ __forceinline__ void finish_body(const BtArgs &a, int s, unsigned *bi
             o[3] = make_double2(r.m.cls, (double)r.m.det_ind);
         });
     YTA_STAMP(8);
+    // free slots in cyclic order from the slot after this frame's last birth: births then take
+    // ascending slots across frames, so the tracked list (survivors in order, births appended)
+    // stays sorted by slot up to a rotation, and the record gathers of k_s1_prep / k_apply /
+    // k_finish walk memory in (gapped) ascending order instead of at random
+    const int cur0 = c->slot_cursor;
+    const int cur = n_births > 0 ? (a.free_list[tb + n_births - 1] + 1) % a.CAP : cur0;
+    block_sync();   // every thread read the old free list above
     const int n_fr = block_compact<false>(
-        a.CAP, wsum, [&](int slot) { return !((live[slot >> 5] >> (slot & 31)) & 1u); },
-        [&](int slot, int pos) { a.free_list[tb + pos] = slot; });
+        a.CAP, wsum,
+        [&](int i) {
+            const int slot = i + cur < a.CAP ? i + cur : i + cur - a.CAP;
+            return !((live[slot >> 5] >> (slot & 31)) & 1u);
+        },
+        [&](int i, int pos) { a.free_list[tb + pos] = i + cur < a.CAP ? i + cur : i + cur - a.CAP; });
     YTA_STAMP(9);
     if (t == 0) {
         c->n_births = n_births;
@@ -1671,6 +1682,7 @@ __device__ __forceinline__ void finish_body(const BtArgs &a, int s, unsigned *bi
         c->n_tracked = n_tr;
         c->n_lost = n_lo;
         c->n_free = n_fr;
+        c->slot_cursor = cur;
         c->n_out = n_out;
         if (a.out_counts) a.out_counts[s] = n_out;
     }
@@ -1744,9 +1756,14 @@ __global__ __launch_bounds__(BLKF) void k_rebuild_free(BtArgs a) {
         atomicOr(&live[slot >> 5], 1u << (slot & 31));
     }
     block_sync();
-    const int n_free = block_compact(a.CAP, wsum,
-                                     [&](int slot) { return !((live[slot >> 5] >> (slot & 31)) & 1u); },
-                                     [&](int slot, int pos) { a.free_list[tb + pos] = slot; });
+    const int cur = c->slot_cursor < a.CAP ? c->slot_cursor : 0;   // cyclic order, as k_finish
+    const int n_free = block_compact(
+        a.CAP, wsum,
+        [&](int i) {
+            const int slot = i + cur < a.CAP ? i + cur : i + cur - a.CAP;
+            return !((live[slot >> 5] >> (slot & 31)) & 1u);
+        },
+        [&](int i, int pos) { a.free_list[tb + pos] = i + cur < a.CAP ? i + cur : i + cur - a.CAP; });
     if (t == 0) c->n_free = n_free;
 }
 

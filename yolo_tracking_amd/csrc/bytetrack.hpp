@@ -53,7 +53,8 @@ struct BtCounters {                  // one per stream, 128 B
     int n_res1;                      // ByteTrack: stage-1 edges left to k_s1_lap
     int n_ref;                       // re-found Lost tracks (refound list)
     int n_fallback_f;                // cumulative: k_finish's duplicate-removal grid over global
-    int pad[3];
+    int slot_cursor;                 // births take free slots from here on, cyclically
+    int pad[2];
 };
 static_assert(sizeof(BtCounters) == 128, "BtCounters layout");
 
