@@ -5,7 +5,7 @@ set -e
 S=${1:-256}
 cd /tmp && export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
-O=$R/gpurun_out/pmc_sq
+O=$R/gpurun_out/${PMC_TAG:-pmc_sq}
 mkdir -p $O
 run() {
   timeout -k 10 300 rocprofv3 --pmc $2 --output-format csv -d $O/$1 -o run -- python3 $R/bench.py --streams $S --queues 1 --steps 4 --warmup 2 --no-cpu-baseline --no-pcie --no-isolated > $O/$1.log 2>&1

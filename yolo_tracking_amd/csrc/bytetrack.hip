@@ -658,6 +658,143 @@ __device__ __forceinline__ void s1_edges_body(const BtArgs &a, int s, int nc, in
     }
 }
 
+// The row phase of k_s1_edges over an LDS grid, one wave at a time on 64 pool rows (lane = row,
+// rows t + m * blockDim as in s1_edges_body): each lane lists its row's grid candidates (the
+// positions of the cells its window covers, contiguous per cell row) into the wave's queue at its
+// prefix offset, then the wave scores the queue 64 candidates at a time, so a wave's trip count is
+// its candidate total / 64 instead of its longest row, and consecutive lanes read consecutive
+// grid positions (no LDS bank conflicts from 64 scattered 32-B boxes).  A row's box reaches the
+// lane scoring its candidate by ds_bpermute.  Edges land in per-row LDS counters; their order
+// within a row does not matter (lap_block, the single-edge pass and k_s1_lap's re-query are
+// order-free).  Queues hold WQ_CAP entries; a larger candidate total is listed and scored in
+// windows.  Big items (larger than 4 x the mean box) are visited per lane, as grid_query does.
+constexpr int WQ_CAP = 384;
+struct EdgeWaveQ {
+    unsigned q[WQ_CAP];   // lane << 24 | grid position
+    int cnt[WAVE];        // edges of the wave's row `lane`
+    int first[WAVE];      // its first edge's detection
+};
+
+__device__ __forceinline__ double bperm_f64(double v, int src_lane) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_ds_bpermute(src_lane << 2, (int)b);
+    const int hi = __builtin_amdgcn_ds_bpermute(src_lane << 2, (int)(b >> 32));
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
+__device__ __forceinline__ void s1_edges_rows_wave(const BtArgs &a, int s, int nr,
+                                                   const GridView &gv, const GridHdr &h,
+                                                   EdgeWaveQ &wq, int &spill, int *cdeg,
+                                                   int &n_edges, int (&rn)[4], int (&rc)[4]) {
+    const int t = threadIdx.x, nt = blockDim.x, lane = lane_id();
+    const long long tb = (long long)s * a.CAP, db = (long long)s * a.MAXD;
+    const long long SC = (long long)a.S * a.CAP;
+    const double thresh = a.match_thresh;
+    int m = 0;
+    for (int base = t - lane; base < nr; base += nt, ++m) {   // wave-uniform loop
+        const int i = base + lane;
+        const bool on = i < nr;
+        Box rb{0.0, 0.0, 0.0, 0.0};
+        if (on) rb = a.pool_box[tb + i];
+        int cx0 = 0, cx1 = -1, cy0 = 0, cy1 = -1;
+        if (!on || !grid_scan_window(h, rb, cx0, cx1, cy0, cy1)) cy1 = cy0 - 1;
+        // this row's candidate count (cells of a grid row are contiguous)
+        int cnt = 0;
+        for (int cy = cy0; cy <= cy1; ++cy)
+            cnt += gv.cell_start[cy * h.gx + cx1 + 1] - gv.cell_start[cy * h.gx + cx0];
+        const int incl = wave_inclusive_scan(cnt);
+        const int off = incl - cnt;
+        const int total = __builtin_amdgcn_readlane(incl, WAVE - 1);
+        wq.cnt[lane] = 0;
+        wq.first[lane] = -1;
+        for (int lo = 0; lo < total; lo += WQ_CAP) {
+            const int hi = lo + WQ_CAP;
+            // list this row's candidates whose wave index falls in [lo, hi)
+            if (off < hi && off + cnt > lo) {
+                int idx = off;
+                for (int cy = cy0; cy <= cy1 && idx < hi; ++cy) {
+                    const int b = gv.cell_start[cy * h.gx + cx0], e = gv.cell_start[cy * h.gx + cx1 + 1];
+                    const int k0 = idx < lo ? lo - idx : 0;
+                    const int k1 = idx + (e - b) < hi ? e - b : hi - idx;
+                    for (int k = k0; k < k1; ++k) wq.q[idx + k - lo] = ((unsigned)lane << 24) | (unsigned)(b + k);
+                    idx += e - b;
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            const int n = total - lo < WQ_CAP ? total - lo : WQ_CAP;
+            // pass 1: keep the intersecting candidates (compacted in place: a survivor's new index
+            // is at most its old one, and a chunk is read before any of it is overwritten)
+            int ns = 0;
+            for (int k0 = 0; k0 < n; k0 += WAVE) {   // wave-uniform trip count
+                const int k = k0 + lane;
+                const unsigned ent = k < n ? wq.q[k] : 0u;
+                const int r = (int)(ent >> 24), pos = (int)(ent & 0xFFFFFFu);
+                const Box tb_{bperm_f64(rb.x1, r), bperm_f64(rb.y1, r), bperm_f64(rb.x2, r),
+                              bperm_f64(rb.y2, r)};
+                const bool hit = k < n && intersects(tb_, gv.boxes[pos]);
+                const unsigned long long bal = __ballot(hit);
+                if (hit) wq.q[ns + __popcll(bal & ((1ull << lane) - 1ull))] = ent;
+                ns += __popcll(bal);
+            }
+            __builtin_amdgcn_wave_barrier();
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            // pass 2: score the survivors (full lanes for the float64 IoU)
+            for (int k0 = 0; k0 < ns; k0 += WAVE) {
+                const int k = k0 + lane;
+                const unsigned ent = k < ns ? wq.q[k] : 0u;
+                const int r = (int)(ent >> 24), pos = (int)(ent & 0xFFFFFFu);
+                const Box tb_{bperm_f64(rb.x1, r), bperm_f64(rb.y1, r), bperm_f64(rb.x2, r),
+                              bperm_f64(rb.y2, r)};
+                if (k >= ns) continue;
+                const Box cb = gv.boxes[pos];
+                const double dist = 1 - iou(tb_, cb);                   // matching.py:117
+                const double cost = 1 - (1 - dist) * gv.w[pos];         // matching.py:216-220
+                if (!(cost < thresh)) continue;
+                const int j = gv.ids[pos];
+                const int c = atomicAdd(&wq.cnt[r], 1);
+                if (c < E_SLOTS) {
+                    a.e_col[c * SC + tb + base + r] = j;
+                    a.e_cost[c * SC + tb + base + r] = cost;
+                }
+                if (c == 0) wq.first[r] = j;
+                atomicAdd(cdeg + j, 1);
+            }
+            __builtin_amdgcn_wave_barrier();
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        }
+        int nn = wq.cnt[lane];
+        int first = wq.first[lane];
+        // big items: every query visits them (grid_query), boxes from the high lists
+        if (on)
+            for (int k = 0; k < h.n_big; ++k) {
+                const int j = gv.big[k];
+                const Box cb = a.high_box[db + j];
+                if (!intersects(rb, cb)) continue;
+                const double dist = 1 - iou(rb, cb);
+                const double cost = 1 - (1 - dist) * a.high_score[db + j];
+                if (!(cost < thresh)) continue;
+                if (nn < E_SLOTS) {
+                    a.e_col[nn * SC + tb + i] = j;
+                    a.e_cost[nn * SC + tb + i] = cost;
+                }
+                if (nn == 0) first = j;
+                ++nn;
+                atomicAdd(cdeg + j, 1);
+            }
+        if (on) {
+            a.e_cnt[tb + i] = nn;
+            if (nn > E_SLOTS) spill = 1;
+            if (nn) atomicAdd(&n_edges, nn);
+            if (m < 4) {   // rows t + m * nt: kept for the single-edge pass
+                rn[m] = nn;
+                rc[m] = nn == 1 ? first : -1;
+            }
+        }
+        __builtin_amdgcn_wave_barrier();   // wq.cnt / first are reset by the next pass
+    }
+}
+
 // Single-edge components (a pool row whose only candidate edge goes to a high detection no other
 // row reaches) are matched outright here, as lap_block's P1 would (lapjv with cost_limit takes an
 // isolated pair with cost < thresh): x1 / y1 get them and -1 elsewhere, the row's edge count
@@ -699,6 +836,7 @@ __global__ __launch_bounds__(BLKE, 4) void k_s1_edges(BtArgs a) {
     __shared__ GridScratch gs;
     __shared__ int wsum[32];
     __shared__ int spill, n_edges;
+    __shared__ EdgeWaveQ ewq[BLKE / WAVE];
     const int s = blockIdx.x, t = threadIdx.x, nt = blockDim.x;
     YTA_STAMP_BASE(66);
     YTA_STAMP(0);
@@ -748,7 +886,9 @@ __global__ __launch_bounds__(BLKE, 4) void k_s1_edges(BtArgs a) {
     gv.big = ar.alloc<int>(nc);
     int *cdeg = ar.alloc<int>(nc);
     for (int j = t; j < nc; j += nt) cdeg[j] = 0;   // grid_build's barriers order these
-    s1_edges_body(a, s, nc, nr, gv, hbox, hw, gs, wsum, spill, cdeg, n_edges, rn, rc);
+    grid_build(nc, hbox, hw, gv, gs, wsum);
+    YTA_STAMP(1);
+    s1_edges_rows_wave(a, s, nr, gv, gs.hdr, ewq[t / WAVE], spill, cdeg, n_edges, rn, rc);
     s1_single_edges(a, s, nc, nr, cdeg, true, rn, rc);
     if (t == 0) c->n_edges[0] = n_edges;
     YTA_STAMP(2);
@@ -2021,9 +2161,11 @@ int set_lds_limits(size_t bytes) {
     const int b = (int)bytes;
     for (const void *k : {(const void *)k_stage1<VAR_BYTETRACK>, (const void *)k_stage1<VAR_BOTSORT>,
                           (const void *)k_stage23<VAR_BYTETRACK>,
-                          (const void *)k_stage23<VAR_BOTSORT>, (const void *)k_s1_lap,
-                          (const void *)k_s1_edges})
+                          (const void *)k_stage23<VAR_BOTSORT>, (const void *)k_s1_lap})
         YTA_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, b));
+    // k_s1_edges never launches with more than BT_LDSE_BYTES (its wave queues are static LDS)
+    YTA_HIP(hipFuncSetAttribute((const void *)k_s1_edges, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)std::min(bytes, BT_LDSE_BYTES)));
     return YTA_OK;
 }
 

@@ -248,6 +248,22 @@ __device__ __forceinline__ void grid_scan(const GridView &gv, const GridHdr &h, 
     }
 }
 
+// The cell window grid_scan visits for query box T: false when it visits nothing.
+__device__ __forceinline__ bool grid_scan_window(const GridHdr &h, const Box &T, int &cx0, int &cx1,
+                                                 int &cy0, int &cy1) {
+    if (h.n_binned == 0) return false;
+    if (!(T.x2 > T.x1 && T.y2 > T.y1)) return false;   // also false for NaN: intersects nothing
+    const double lx = (T.x1 - h.maxw * (1.0 + 1e-12)) - (fabs(T.x1) + h.maxw) * 1e-12;
+    const double ly = (T.y1 - h.maxh * (1.0 + 1e-12)) - (fabs(T.y1) + h.maxh) * 1e-12;
+    const double fx1 = floor((T.x2 - h.ox) * h.inv_g), fy1 = floor((T.y2 - h.oy) * h.inv_g);
+    if (fx1 < 0.0 || fy1 < 0.0) return false;
+    cx0 = grid_cell_1d(lx, h.ox, h.inv_g, h.gx);
+    cy0 = grid_cell_1d(ly, h.oy, h.inv_g, h.gy);
+    cx1 = fx1 > (double)(h.gx - 1) ? h.gx - 1 : (int)fx1;
+    cy1 = fy1 > (double)(h.gy - 1) ? h.gy - 1 : (int)fy1;
+    return true;
+}
+
 // Binned items whose top-left corner lies in [lx, hx] x [ly, hy] (a superset: whole cells):
 // hit(k, id, box, w).  Same pipelining as grid_scan.
 template <typename Hit>
