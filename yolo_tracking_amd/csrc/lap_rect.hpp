@@ -42,25 +42,30 @@ struct RectMat {
     }
 };
 
-// Work arrays (LDS or global): rect_ws_bytes(rows, cols) bytes, 8-aligned.
+// Work arrays (LDS or global): rect_ws_bytes(rows, cols, duals) bytes, 8-aligned.  `duals`: keep
+// the column duals on return (the transposed first round's uniqueness certificate); they cost 8 B
+// a column, which would push a 4096 x 4096 problem's arrays out of LDS.
 struct RectWs {
     double *u, *s2;     // rows
-    double *v;          // cols: the column duals on return (<= 0, 0 on free columns)
+    double *v;          // cols: the column duals on return (<= 0, 0 on free columns), or nullptr
     int *x, *fl;        // rows: assigned column, free-row list
     int *path, *yw;     // cols: predecessor row, owner row (authoritative copy)
 };
-__host__ __device__ inline long long rect_ws_bytes(long long rows, long long cols) {
-    return rows * 24 + cols * 16 + 64;
+__host__ __device__ inline long long rect_ws_bytes(long long rows, long long cols,
+                                                   bool duals = false) {
+    return rows * 24 + cols * (duals ? 16 : 8) + 64;
 }
-__host__ __device__ inline RectWs rect_ws(unsigned char *base, int rows, int cols) {
+__host__ __device__ inline RectWs rect_ws(unsigned char *base, int rows, int cols,
+                                          bool duals = false) {
     RectWs w;
     w.u = reinterpret_cast<double *>(base);
     w.s2 = w.u + rows;
-    w.v = w.s2 + rows;
-    w.x = reinterpret_cast<int *>(w.v + cols);
+    w.x = reinterpret_cast<int *>(w.s2 + rows);
     w.fl = w.x + rows;
     w.path = w.fl + rows;
     w.yw = w.path + cols;
+    // 8-aligned: 24 * rows + 8 * cols bytes precede it
+    w.v = duals ? reinterpret_cast<double *>(w.yw + cols) : nullptr;
     return w;
 }
 constexpr int RECT_CPT_MAX = 32;
@@ -308,11 +313,12 @@ __device__ __forceinline__ int lap_rect_body(const RectMat M, const double *pre_
         }
     }
     YTA_STAMP_ABS(105);
+    if (w.v)
 #pragma unroll
-    for (int q = 0; q < CPT; ++q) {
-        const int j = t + q * nt;
-        if (j < cols) w.v[j] = v[q];
-    }
+        for (int q = 0; q < CPT; ++q) {
+            const int j = t + q * nt;
+            if (j < cols) w.v[j] = v[q];
+        }
     return 0;
 }
 

@@ -86,7 +86,7 @@ constexpr long long LAP_LDS_MAX = 156 * 1024;   // their dynamic LDS cap (160 Ki
 // The first-round solve's work arrays, either orientation (first_round_lap transposes the
 // problem when detections outnumber trackers).
 __host__ __device__ inline long long lap_kernel_lds(long long CAP, long long MAXD) {
-    const long long b1 = rect_ws_bytes(MAXD, CAP), b2 = rect_ws_bytes(CAP, MAXD);
+    const long long b1 = rect_ws_bytes(MAXD, CAP), b2 = rect_ws_bytes(CAP, MAXD, true);
     const long long b = b1 > b2 ? b1 : b2;
     return b < LAP_LDS_MAX ? b : LAP_LDS_MAX;
 }
@@ -327,8 +327,8 @@ __device__ __forceinline__ void first_round_lap(const double *mat, int na, int n
         if (t == 0) *done = 0;
         return;
     }
-    unsigned char *base = rect_ws_bytes(rows, cols) <= lds_bytes ? lds : gws;
-    const RectWs w = rect_ws(base, rows, cols);
+    unsigned char *base = rect_ws_bytes(rows, cols, tr) <= lds_bytes ? lds : gws;
+    const RectWs w = rect_ws(base, rows, cols, tr);
     const RectMat R = tr ? RectMat{mat, rows, cols, 1, nb, false} : RectMat{mat, rows, cols, nb, 1, false};
     const int rc = lap_rect<LAP_T>(R, pu, px, ps2, w, rsh);
     if (rc && t == 0) atomicOr(err, ERR_SOLVER);
