@@ -1384,14 +1384,18 @@ __global__ __launch_bounds__(APPLY_T) void k_apply(BtArgs a) {
     }
     __syncthreads();
     YTA_APL(3);
-    // cooperative store of what changed
+    // cooperative store of what changed, in whole lines or aligned half lines: a written Kalman
+    // record takes its (maybe unchanged) meta and the zero padding piece with it, a meta-only
+    // change the padding (a partially written line costs a read-modify-write: 3-5 % on the
+    // record pass, profiles/r03q_rmwbench.txt)
     double2 *recw = reinterpret_cast<double2 *>(a.kf);
-    for (int p = t; p < nloc * REC_PIECES; p += APPLY_T) {
-        const int r = p / REC_PIECES, k = p - r * REC_PIECES;
+    for (int p = t; p < nloc * 16; p += APPLY_T) {
+        const int r = p >> 4, k = p & 15;   // record piece
         const int wm = s_wmask[r];
+        const bool meta_half = k >= 4 && k < 8;
+        if (!(meta_half ? (wm & 3) : (wm & 1))) continue;
         const long long sl = tb + s_slot[r];
-        if (piece_is_meta(k) ? (wm & 2) : (wm & 1))
-            recw[sl * (TRK_STRIDE / 2) + rec_piece(k)] = rec[r][k];
+        recw[sl * (TRK_STRIDE / 2) + k] = k == 7 ? make_double2(0.0, 0.0) : rec[r][k < 7 ? k : k - 1];
     }
     YTA_APL(4);
 }
