@@ -552,6 +552,41 @@ int yta_osnet_dw3x3(const void *x, long long x_n_stride, long long x_c_stride, c
                     float *plane_sum, long long ps_n_stride, void *stream);
 int yta_osnet_gate_sum(const void *stack, const void *gate, int N, int C, int P, int half,
                        void *out, void *stream);
+/* yta_osnet_pointwise: every 1x1 convolution of the network (osnet.py Conv1x1 / Conv1x1Linear /
+ * LightConv3x3.conv1 / the ChannelGate-free layers, the fc) as an MFMA GEMM over strided tensors
+ * (elements; sample n, channel c, pixel p of a tensor at base + n * sn + c * sc + p * sp):
+ *   y[n][g cout_g + co][p] = relu?( sum_{k < k1} w[g][k][co] x1[n][g k1 + k][p]
+ *                                 + sum_{k < k2} w[g][k1 + k][co] x2[n][k][p]
+ *                                 + bias[g cout_g + co] + res[n][g cout_g + co][p] )
+ * w: float32 [G][k1 + k2][cout_g] (k-major: BatchNorm folded, transposed); bias, x2 (k2 = 0),
+ * res may be NULL. */
+typedef struct yta_pw_args {
+    const void *x1;
+    long long x1n, x1c, x1p;
+    const void *x2;
+    long long x2n, x2c, x2p;
+    const float *w;
+    const float *bias;
+    const void *res;
+    long long rn, rc, rp;
+    void *y;
+    long long yn, yc, yp;
+    int k1, k2, G, cout_g, P, N, relu, pad;
+} yta_pw_args;
+int yta_osnet_pointwise(const yta_pw_args *args, int half, void *stream);
+/* yta_osnet_stem: conv1 (7x7, stride 2, padding 3, 3 -> C0 <= 128; w: float32 C0 x 3 x 7 x 7,
+ * BatchNorm folded) + b + ReLU: x N x 3 x H x W -> y N x C0 x ((H-1)/2+1) x ((W-1)/2+1).
+ * yta_osnet_pool: kind 0 max 3x3 stride 2 padding 1, 1 average 2x2 stride 2, 2 global mean
+ * (y N x C).  yta_osnet_gate: the ChannelGate's fc1 + ReLU, fc2 + sigmoid on the four branches'
+ * pooled planes (plane_sum N x 4 x mid float32 sums over P pixels; w1 hid x mid, b1 hid, w2
+ * mid x hid, b2 mid in the storage type) -> gate N x 4 x mid. */
+int yta_osnet_stem(const void *x, int N, int H, int W, const float *w, const float *b, int C0,
+                   int half, void *y, void *stream);
+int yta_osnet_pool(const void *x, int N, int C, int H, int W, int kind, int half, void *y,
+                   void *stream);
+int yta_osnet_gate(const float *plane_sum, int N, int mid, int hid, int P, const void *w1,
+                   const void *b1, const void *w2, const void *b2, int half, void *gate,
+                   void *stream);
 
 #ifdef __cplusplus
 }

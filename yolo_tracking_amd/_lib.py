@@ -13,6 +13,20 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # YTA_LIBRARY: an alternative build of the same library (tuning experiments, tools/)
 LIB_PATH = os.environ.get("YTA_LIBRARY") or os.path.join(_HERE, "libyta.so")
 
+
+class PwArgs(ctypes.Structure):
+    """yta_pw_args (include/yolo_tracking_amd.h): one 1x1 convolution / linear layer."""
+    _fields_ = [("x1", ctypes.c_void_p), ("x1n", ctypes.c_longlong), ("x1c", ctypes.c_longlong),
+                ("x1p", ctypes.c_longlong), ("x2", ctypes.c_void_p), ("x2n", ctypes.c_longlong),
+                ("x2c", ctypes.c_longlong), ("x2p", ctypes.c_longlong), ("w", ctypes.c_void_p),
+                ("bias", ctypes.c_void_p), ("res", ctypes.c_void_p), ("rn", ctypes.c_longlong),
+                ("rc", ctypes.c_longlong), ("rp", ctypes.c_longlong), ("y", ctypes.c_void_p),
+                ("yn", ctypes.c_longlong), ("yc", ctypes.c_longlong), ("yp", ctypes.c_longlong),
+                ("k1", ctypes.c_int), ("k2", ctypes.c_int), ("G", ctypes.c_int),
+                ("cout_g", ctypes.c_int), ("P", ctypes.c_int), ("N", ctypes.c_int),
+                ("relu", ctypes.c_int), ("pad", ctypes.c_int)]
+
+
 YTA_OK = 0
 YTA_ERR_INVALID = -1
 YTA_ERR_HIP = -2
@@ -177,6 +191,10 @@ _SIGS = {
                          ctypes.c_longlong, _I, _P, ctypes.c_longlong, _P, ctypes.c_longlong, _P],
                         _I),
     "yta_osnet_gate_sum": ([_P, _P, _I, _I, _I, _I, _P, _P], _I),
+    "yta_osnet_pointwise": ([_P, _I, _P], _I),
+    "yta_osnet_stem": ([_P, _I, _I, _I, _P, _P, _I, _I, _P, _P], _I),
+    "yta_osnet_pool": ([_P, _I, _I, _I, _I, _I, _I, _P, _P], _I),
+    "yta_osnet_gate": ([_P, _I, _I, _I, _I, _P, _P, _P, _P, _I, _P, _P], _I),
 }
 
 EXPORTED_SYMBOLS = tuple(_SIGS)

@@ -110,9 +110,11 @@ class OSNetReID:
     """Eval-mode OSNet feature extractor: crops (N, 3, H, W) -> (N, 512) in the crops' dtype
     (float32 or float16), on the crops' device.
 
-    On a GPU the omni-scale blocks' depthwise convolutions, channel-gate pools and gated branch
-    sums run in csrc/osnet.hip (NCHW; `hip=False` keeps PyTorch's kernels, for comparison); the
-    1x1 convolutions and the stem are MIOpen's.  On the CPU the whole graph is PyTorch's."""
+    On a GPU every layer runs in csrc/osnet.hip (NCHW): the stem (7x7 conv), the pools, every
+    1x1 convolution and the fc as MFMA GEMMs with bias / residual / ReLU epilogues, the depthwise
+    3x3s, the channel gates and the gated branch sums; PyTorch only allocates the activations.
+    `hip=False` runs the same folded graph on PyTorch's kernels (MIOpen), for comparison, and is
+    what a CPU device gets."""
 
     def __init__(self, name="osnet_x0_25", state_dict=None, device="cuda:0", half=False,
                  chunk=CHUNK, channels_last=None, hip=True):
@@ -146,10 +148,19 @@ class OSNetReID:
         shape = (-1,) + (1,) * (w.dim() - 1)
         return w * scale.reshape(shape), sd[bn + ".bias"] - sd[bn + ".running_mean"] * scale
 
+    def _f32(self, x, shape=None):
+        """float32 on the device; with `shape` = (G, cout_g, K) a 1x1 weight in the k-major
+        [G][K][cout_g] layout yta_osnet_pointwise reads (lanes along the output channels)."""
+        x = x.to(self.device, self.torch.float32)
+        if shape is None:
+            return x.contiguous()
+        return x.reshape(shape).transpose(1, 2).contiguous()
+
     def _build(self, sd):
         P = {}
         w, b = self._fold(sd["conv1.conv.weight"], sd, "conv1.bn")
         P["stem"] = (self._t(w), self._t(b))
+        H = {"stem": (self._f32(w), self._f32(b))}      # the HIP kernels' float32 operands
         self.blocks = []
         for stage in (2, 3, 4):
             for i in (0, 1):
@@ -157,13 +168,17 @@ class OSNetReID:
             red = f"conv{stage}.2.0"
             if red + ".conv.weight" in sd:
                 w, b = self._fold(sd[red + ".conv.weight"], sd, red + ".bn")
-                self.blocks.append(("reduce", self._t(w), self._t(b)))
+                self.blocks.append(("reduce", self._t(w), self._t(b),
+                                    self._f32(w, (1, w.shape[0], w.shape[1])), self._f32(b)))
         w, b = self._fold(sd["conv5.conv.weight"], sd, "conv5.bn")
         P["conv5"] = (self._t(w), self._t(b))
+        H["conv5"] = (self._f32(w, (1, w.shape[0], w.shape[1])), self._f32(b))
         w, b = self._fold(sd["fc.0.weight"], sd, "fc.1")
         b = b + sd["fc.0.bias"] * (sd["fc.1.weight"] / (sd["fc.1.running_var"] + BN_EPS).sqrt())
         P["fc"] = (self._t(w), self._t(b))
+        H["fc"] = (self._f32(w, (1,) + tuple(w.shape)), self._f32(b))
         self.P = P
+        self.H = H
 
     def _block(self, sd, key):
         torch = self.torch
@@ -173,9 +188,11 @@ class OSNetReID:
                                           for br, depth in (("conv2b", 2), ("conv2c", 3),
                                                             ("conv2d", 4))]
         layers = []   # depth d: the branches still running, 1x1 weights stacked, dw folded
+        pw32 = []     # the same 1x1 weights as the HIP GEMM's float32 [groups][cout_g][k]
         for d in range(4):
             live = [br[d] for br in branches if len(br) > d]
             pw = torch.cat([sd[k + ".conv1.weight"] for k in live], 0)
+            pw32.append(self._f32(pw, (1 if d == 0 else len(live), -1, mid)))
             dws, dbs = zip(*[self._fold(sd[k + ".conv2.weight"], sd, k + ".bn") for k in live])
             dw, db = torch.cat(dws, 0), torch.cat(dbs, 0)
             layers.append((len(live), self._t(pw), self._t(dw), self._t(db),
@@ -187,18 +204,25 @@ class OSNetReID:
              self._t(sd[key + ".gate.fc2.bias"]))
         w3, b3 = self._fold(sd[key + ".conv3.conv.weight"], sd, key + ".conv3.bn")
         ds = None
+        cout, cin = w3.shape[0], w1.shape[1]
+        w3k, b3k = w3.reshape(cout, mid), b3
         if key + ".downsample.conv.weight" in sd:
             wd, bd = self._fold(sd[key + ".downsample.conv.weight"], sd, key + ".downsample.bn")
             ds = (self._t(wd), self._t(bd))
-        return ("os", mid, (self._t(w1), self._t(b1)), layers, g, (self._t(w3), self._t(b3)), ds)
+            # conv3(x2) + downsample(x): one GEMM over the concatenated inputs [x2; x]
+            w3k, b3k = torch.cat([w3k, wd.reshape(cout, cin)], 1), b3 + bd
+        hip = {"conv1": (self._f32(w1, (1, mid, cin)), self._f32(b1)),
+               "layers": pw32,
+               "conv3": (self._f32(w3k, (1,) + tuple(w3k.shape)), self._f32(b3k)),
+               "cin": cin, "cout": cout, "hid": g[0].shape[0]}
+        return ("os", mid, (self._t(w1), self._t(b1)), layers, g, (self._t(w3), self._t(b3)), ds,
+                hip)
 
     # ---- forward
     def _os_block(self, x, blk):
-        if self.hip:
-            return self._os_block_hip(x, blk)
         F = self.torch.nn.functional
         torch = self.torch
-        _, mid, (w1, b1), layers, (g1w, g1b, g2w, g2b), (w3, b3), ds = blk
+        _, mid, (w1, b1), layers, (g1w, g1b, g2w, g2b), (w3, b3), ds, _ = blk
         x1 = F.relu(F.conv2d(x, w1, b1))
         outs = []                       # branch outputs, finished at depths 1, 2, 3, 4
         y = None
@@ -219,45 +243,137 @@ class OSNetReID:
         idt = F.conv2d(x, ds[0], ds[1]) if ds is not None else x
         return F.relu(x3 + idt)
 
-    def _os_block_hip(self, x, blk):
-        """The block with csrc/osnet.hip: each depth's depthwise 3x3 + bias + ReLU writes the
-        branch ending there straight into the (N, 4, mid, H, W) stack (plus its plane sums for
-        the gate) and the others into the next depth's input; the gated branch sum is one pass."""
-        import ctypes
+    # ---- the HIP forward (csrc/osnet.hip): every layer a kernel of ours
+    def _pw(self, x1, w, bias=None, *, k1, G=1, cout_g, P, N, relu, x2=None, k2=0, res=None,
+            out=None, x1s=None, x2s=None, ys=None):
+        """1x1 convolution / linear layer through yta_osnet_pointwise.  x1s / x2s / ys: (sample,
+        channel, pixel) element strides, default NCHW-contiguous."""
         from .. import _lib
         torch = self.torch
-        F = torch.nn.functional
+        if out is None:
+            out = torch.empty((N, G * cout_g, P), dtype=self.dtype, device=self.device)
+        a = _lib.PwArgs()
+        a.x1 = x1.data_ptr()
+        a.x1n, a.x1c, a.x1p = x1s or (G * k1 * P, P, 1)
+        if x2 is not None:
+            a.x2 = x2.data_ptr()
+            a.x2n, a.x2c, a.x2p = x2s or (k2 * P, P, 1)
+        a.w = w.data_ptr()
+        a.bias = bias.data_ptr() if bias is not None else None
+        if res is not None:
+            a.res = res.data_ptr()
+            a.rn, a.rc, a.rp = (G * cout_g * P, P, 1)
+        a.y = out.data_ptr()
+        a.yn, a.yc, a.yp = ys or (G * cout_g * P, P, 1)
+        a.k1, a.k2, a.G, a.cout_g, a.P, a.N, a.relu = k1, k2, G, cout_g, P, N, int(relu)
+        _lib.check(_lib.load_library().yta_osnet_pointwise(self._ctypes.byref(a), self._half,
+                                                           self._stream()))
+        return out
+
+    def _stream(self):
+        return self._ctypes.c_void_p(self.torch.cuda.current_stream(self.device).cuda_stream)
+
+    def _os_block_hip(self, x, blk):
+        """One OSBlock: conv1 (GEMM + bias + ReLU); per depth the branches' 1x1s (one GEMM, grouped
+        by branch after depth 0) and the depthwise 3x3 + bias + ReLU, which routes the branch
+        ending at that depth into the (N, 4, mid, H, W) stack with its plane sums; the channel gate
+        on those sums; the gated branch sum; conv3 and the downsample 1x1 as one GEMM over [x2; x]
+        (or + x) with ReLU."""
+        ctypes = self._ctypes
+        from .. import _lib
+        torch = self.torch
         lib = _lib.load_library()
-        _, mid, (w1, b1), layers, (g1w, g1b, g2w, g2b), (w3, b3), ds = blk
-        n, _, h, w = x.shape
+        _, mid, _, layers, (g1w, g1b, g2w, g2b), _, ds, hp = blk
+        n, cin, h, w = x.shape
         hw = h * w
-        half = int(self.dtype == torch.float16)
-        es = 2 if half else 4
-        st = ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
-        z = F.relu(F.conv2d(x, w1, b1)).contiguous()
+        es = 2 if self._half else 4
+        st = self._stream()
+        w1, b1 = hp["conv1"]
+        z = self._pw(x, w1, b1, k1=cin, cout_g=mid, P=hw, N=n, relu=True)
         stack = torch.empty((n, 4, mid, h, w), dtype=self.dtype, device=self.device)
         psum = torch.empty((n, 4, mid), dtype=torch.float32, device=self.device)
-        for d, (nlive, pw, _, _, dwf, dbf) in enumerate(layers):
-            y = (F.conv2d(z, pw) if d == 0 else F.conv2d(z, pw, groups=nlive)).contiguous()
+        for d, (nlive, _, _, _, dwf, dbf) in enumerate(layers):
+            wd = hp["layers"][d]
+            y = (self._pw(z, wd, k1=mid, cout_g=4 * mid, P=hw, N=n, relu=False) if d == 0 else
+                 self._pw(z, wd, k1=mid, G=nlive, cout_g=mid, P=hw, N=n, relu=False))
             rest = (torch.empty((n, (nlive - 1) * mid, h, w), dtype=self.dtype, device=self.device)
                     if nlive > 1 else None)
             _lib.check(lib.yta_osnet_dw3x3(
                 ctypes.c_void_p(y.data_ptr()), nlive * mid * hw, hw,
                 ctypes.c_void_p(dwf.data_ptr()), ctypes.c_void_p(dbf.data_ptr()), n, nlive * mid,
-                h, w, half, ctypes.c_void_p(stack.data_ptr() + d * mid * hw * es), 4 * mid * hw,
-                mid, ctypes.c_void_p(rest.data_ptr()) if rest is not None else None,
+                h, w, self._half, ctypes.c_void_p(stack.data_ptr() + d * mid * hw * es),
+                4 * mid * hw, mid, ctypes.c_void_p(rest.data_ptr()) if rest is not None else None,
                 (nlive - 1) * mid * hw, ctypes.c_void_p(psum.data_ptr() + d * mid * 4), 4 * mid,
                 st))
             z = rest
-        pooled = (psum / hw).to(self.dtype)
-        gate = torch.sigmoid(F.linear(F.relu(F.linear(pooled, g1w, g1b)), g2w, g2b)).contiguous()
+        gate = torch.empty((n, 4, mid), dtype=self.dtype, device=self.device)
+        _lib.check(lib.yta_osnet_gate(ctypes.c_void_p(psum.data_ptr()), n, mid, hp["hid"], hw,
+                                      ctypes.c_void_p(g1w.data_ptr()), ctypes.c_void_p(g1b.data_ptr()),
+                                      ctypes.c_void_p(g2w.data_ptr()), ctypes.c_void_p(g2b.data_ptr()),
+                                      self._half, ctypes.c_void_p(gate.data_ptr()), st))
         x2 = torch.empty((n, mid, h, w), dtype=self.dtype, device=self.device)
         _lib.check(lib.yta_osnet_gate_sum(ctypes.c_void_p(stack.data_ptr()),
-                                          ctypes.c_void_p(gate.data_ptr()), n, mid, hw, half,
+                                          ctypes.c_void_p(gate.data_ptr()), n, mid, hw, self._half,
                                           ctypes.c_void_p(x2.data_ptr()), st))
-        out = F.conv2d(x2, w3, b3)
-        out += F.conv2d(x, ds[0], ds[1]) if ds is not None else x
-        return out.relu_()
+        w3, b3 = hp["conv3"]
+        cout = hp["cout"]
+        if ds is not None:
+            out = self._pw(x2, w3, b3, k1=mid, cout_g=cout, P=hw, N=n, relu=True, x2=x, k2=cin)
+        else:
+            out = self._pw(x2, w3, b3, k1=mid, cout_g=cout, P=hw, N=n, relu=True, res=x)
+        return out.view(n, cout, h, w)
+
+    def _pool(self, x, kind):
+        from .. import _lib
+        torch = self.torch
+        n, c, h, w = x.shape
+        if kind == 0:
+            out = torch.empty((n, c, (h - 1) // 2 + 1, (w - 1) // 2 + 1), dtype=self.dtype,
+                              device=self.device)
+        elif kind == 1:
+            out = torch.empty((n, c, h // 2, w // 2), dtype=self.dtype, device=self.device)
+        else:
+            out = torch.empty((n, c), dtype=self.dtype, device=self.device)
+        _lib.check(_lib.load_library().yta_osnet_pool(
+            self._ctypes.c_void_p(x.data_ptr()), n, c, h, w, kind, self._half,
+            self._ctypes.c_void_p(out.data_ptr()), self._stream()))
+        return out
+
+    def _forward_hip(self, crops):
+        import ctypes
+        from .. import _lib
+        torch = self.torch
+        self._ctypes = ctypes
+        self._half = int(self.dtype == torch.float16)
+        x = crops.to(self.device, self.dtype).contiguous()
+        n, _, H, W = x.shape
+        ws, bs = self.H["stem"]
+        c0 = ws.shape[0]
+        stem = torch.empty((n, c0, (H - 1) // 2 + 1, (W - 1) // 2 + 1), dtype=self.dtype,
+                           device=self.device)
+        _lib.check(_lib.load_library().yta_osnet_stem(
+            ctypes.c_void_p(x.data_ptr()), n, H, W, ctypes.c_void_p(ws.data_ptr()),
+            ctypes.c_void_p(bs.data_ptr()), c0, self._half, ctypes.c_void_p(stem.data_ptr()),
+            self._stream()))
+        x = self._pool(stem, 0)
+        for blk in self.blocks:
+            if blk[0] == "reduce":
+                _, _, _, wr, br = blk
+                c, h, w = x.shape[1], x.shape[2], x.shape[3]
+                y = self._pw(x, wr, br, k1=c, cout_g=wr.shape[2], P=h * w, N=n, relu=True)
+                x = self._pool(y.view(n, wr.shape[2], h, w), 1)
+            else:
+                x = self._os_block_hip(x, blk)
+        w5, b5 = self.H["conv5"]
+        c, h, w = x.shape[1], x.shape[2], x.shape[3]
+        y = self._pw(x, w5, b5, k1=c, cout_g=w5.shape[2], P=h * w, N=n, relu=True)
+        v = self._pool(y.view(n, w5.shape[2], h, w), 2)                 # (n, C) means
+        wf, bf = self.H["fc"]
+        feat = torch.empty((n, wf.shape[2]), dtype=self.dtype, device=self.device)
+        # the fc as a GEMM over the crops: one "sample", the crops on the pixel axis
+        self._pw(v, wf, bf, k1=c, cout_g=wf.shape[2], P=n, N=1, relu=True, x1s=(0, 1, c),
+                 ys=(0, 1, wf.shape[2]), out=feat)
+        return feat
 
     def __call__(self, crops):
         torch = self.torch
@@ -269,6 +385,8 @@ class OSNetReID:
                               for i in range(0, n, self.chunk)])
 
     def _forward(self, crops):
+        if self.hip:
+            return self._forward_hip(crops)
         torch = self.torch
         F = torch.nn.functional
         x = crops.to(self.device, self.dtype).contiguous(memory_format=self.fmt)
