@@ -83,10 +83,11 @@ __global__ __launch_bounds__(DW_T) void k_dw3x3(const T *x, long long xn, long l
     }
 }
 
-// The same for planes that fit LDS: a block takes ppb consecutive planes of a sample (about 2048
+// The same for planes that fit LDS: a block takes ppb consecutive planes of a sample (about 4096
 // pixels together, so small late-stage planes do not leave most of a block idle), stages them in
-// LDS with coalesced loads, computes every output from LDS, and sums each first-branch plane's
-// stored outputs in a fixed order (one wave a plane: deterministic gate inputs).
+// LDS with coalesced loads and computes every output from LDS; a first-branch plane's sum of its
+// stored outputs is reduced in a fixed order (thread partials, waves, then wave 0: deterministic
+// gate inputs).
 constexpr int DW_LDS_PX = 4096;
 template <typename T>
 __global__ __launch_bounds__(DW_T) void k_dw3x3_lds(const T *x, long long xn, long long xc,
@@ -94,7 +95,8 @@ __global__ __launch_bounds__(DW_T) void k_dw3x3_lds(const T *x, long long xn, lo
                                                      int W, int ppb, T *yf, long long yfn,
                                                      int n_first, T *yr, long long yrn,
                                                      float *psum, long long psn) {
-    __shared__ float in[DW_LDS_PX], ob[DW_LDS_PX];
+    __shared__ float in[DW_LDS_PX];
+    __shared__ float red[DW_T / WAVE];
     const int n = blockIdx.y, c0 = blockIdx.x * ppb;
     const int np = C - c0 < ppb ? C - c0 : ppb;
     const int HW = H * W;
@@ -111,8 +113,9 @@ __global__ __launch_bounds__(DW_T) void k_dw3x3_lds(const T *x, long long xn, lo
 #pragma unroll
         for (int u = 0; u < 9; ++u) k[u] = w[c * 9 + u];
         const float bias = b[c];
-        T *dst = c < n_first ? yf + n * yfn + (long long)c * HW
-                             : yr + n * yrn + (long long)(c - n_first) * HW;
+        const bool first = c < n_first;
+        T *dst = first ? yf + n * yfn + (long long)c * HW : yr + n * yrn + (long long)(c - n_first) * HW;
+        float acc = 0.f;
         for (int q = threadIdx.x; q < HW; q += DW_T) {
             const int y = (int)(((float)q + 0.5f) * invW), xx = q - y * W;
             float s = 0.f;
@@ -129,18 +132,19 @@ __global__ __launch_bounds__(DW_T) void k_dw3x3_lds(const T *x, long long xn, lo
             }
             const T o = (T)fmaxf(s + bias, 0.f);
             dst[q] = o;
-            ob[j * HW + q] = (float)o;
+            acc += (float)o;
         }
-    }
-    if (!psum) return;
-    __syncthreads();
-    const int lane = lane_id();
-    for (int j = threadIdx.x / WAVE; j < np; j += DW_T / WAVE) {
-        if (c0 + j >= n_first) break;
-        float a = 0.f;
-        for (int q = lane; q < HW; q += WAVE) a += ob[j * HW + q];
-        a = (float)wave_reduce(RED_SUM, (double)a);
-        if (lane == 0) psum[n * psn + c0 + j] = a;
+        if (first && psum) {   // block-uniform
+            acc = (float)wave_reduce(RED_SUM, (double)acc);
+            if (lane_id() == 0) red[threadIdx.x / WAVE] = acc;
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                float t = 0.f;
+                for (int u = 0; u < DW_T / WAVE; ++u) t += red[u];
+                psum[n * psn + c] = t;
+            }
+            __syncthreads();
+        }
     }
 }
 
@@ -386,7 +390,7 @@ int yta_osnet_dw3x3(const void *x, long long x_n_stride, long long x_c_stride, c
     YTA_CHECK((n_first == 0 || y_first) && (n_first == C || y_rest), YTA_ERR_INVALID,
               "null output");
     if (H * W <= DW_LDS_PX) {
-        const int ppb = std::max(1, std::min(C, 2048 / (H * W)));
+        const int ppb = std::max(1, std::min(C, DW_LDS_PX / (H * W)));
         const dim3 gl((C + ppb - 1) / ppb, N);
         if (half)
             hipLaunchKernelGGL(k_dw3x3_lds<_Float16>, gl, dim3(DW_T), 0, (hipStream_t)stream,
