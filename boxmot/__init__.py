@@ -55,6 +55,7 @@ ALIASES = {
     "boxmot.motion": "yolo_tracking_amd.motion",
     "boxmot.motion.cmc": "yolo_tracking_amd.motion.cmc",
     "boxmot.motion.cmc.sof": "yolo_tracking_amd.motion.sof",
+    "boxmot.motion.cmc.ecc": "yolo_tracking_amd.motion.ecc",
 }
 
 

@@ -536,6 +536,36 @@ int yta_sof_kat_lk(int device, const uint8_t *prev, const uint8_t *next, int h, 
                    const float *pts, int n, float *next_pts, uint8_t *status);
 int yta_sof_kat_affine(int device, const float *src, const float *dst, int n, double *M, int *ok);
 
+/* ---- Camera-motion compensation: ECC (boxmot/motion/cmc/ecc.py:13-104) -------------------------
+ * get_cmc_method('ecc') (motion/cmc/__init__.py:9-11, built by hybridsort.py:366): apply(img, dets)
+ * -> 2x3 float32 warp = cv2.findTransformECC(prev, curr, eye(2, 3), warp_mode, (COUNT | EPS,
+ * max_iter, eps), None, 1) (ecc.py:73-81) on the gray frames resized by `scale`, translation divided
+ * by `scale` (ecc.py:87-89); the identity on the first frame (ecc.py:66-68) and when OpenCV raises
+ * (NaN correlation, or a step that would minimise it; ecc.py:82-84: prev_img kept).  warp_mode:
+ * MOTION_TRANSLATION 0, MOTION_EUCLIDEAN 1 (the reference's default), MOTION_AFFINE 2
+ * (MOTION_HOMOGRAPHY is refused).  S streams per engine, one 1024-thread block runs a stream's
+ * whole Gauss-Newton loop.  Restatement and parity: oracle/cmc_ecc.py (unpinned against cv2). */
+typedef struct yta_ecc yta_ecc;
+int yta_ecc_create(int device, int n_streams, int warp_mode, double eps, int max_iter,
+                   double scale, int max_h, int max_w, yta_ecc **engine);
+int yta_ecc_destroy(yta_ecc *engine);
+int yta_ecc_reset(yta_ecc *engine);
+/* Host-buffer apply (synchronous): frames as yta_sof_apply; warps: S x 6 float32 out. */
+int yta_ecc_apply(yta_ecc *engine, const uint8_t *frames, const long long *frame_off,
+                  const int *frame_hw, float *warps);
+/* Device-buffer apply (asynchronous on the engine stream), then yta_ecc_sync. */
+int yta_ecc_apply_device(yta_ecc *engine, const uint8_t *d_frames, const long long *d_frame_off,
+                         const int *d_frame_hw, float *d_warps);
+int yta_ecc_sync(yta_ecc *engine);
+/* Last apply per stream (each array S entries, may be NULL): outcome 0 first frame, 1 estimated,
+ * 2 identity (OpenCV would have raised); Gauss-Newton iterations run; the final correlation rho. */
+int yta_ecc_outcome(yta_ecc *engine, int *outcome, int *iters, double *rho);
+/* Whether stream s has its first frame, and its stored previous gray frame (h x w uint8, may be
+ * NULL). */
+int yta_ecc_get_state(yta_ecc *engine, int stream, int *initialized, int *h, int *w,
+                      uint8_t *prev_img, int img_cap);
+int yta_ecc_hip_stream(yta_ecc *engine, void **stream);
+
 /* ---- OSNet omni-scale block kernels (boxmot/appearance/backbones/osnet.py LightConv3x3 /
  * ChannelGate / OSBlock; the ReID network's forward, appearance/osnet.py).  Device pointers,
  * asynchronous on `stream` (a hipStream_t; NULL = default), NCHW planes, float32 (half = 0) or

@@ -71,9 +71,11 @@ def test_synthetic_stream_is_deterministic():
 def test_default_cmc_is_sparse_opt_flow():
     """Without cmc= the trackers get SparseOptFlow, as in the reference (bot_sort.py:228,
     deep_ocsort.py:351); constructing it touches no GPU (the engine starts with the first frame)."""
-    from yolo_tracking_amd.motion import IdentityCMC, SparseOptFlow, default_cmc, get_cmc_method
+    from yolo_tracking_amd.motion import (ECC, IdentityCMC, SparseOptFlow, default_cmc,
+                                          get_cmc_method)
     assert isinstance(default_cmc("BoTSORT"), SparseOptFlow)
     assert get_cmc_method("sof") is SparseOptFlow
+    assert get_cmc_method("ecc") is ECC and isinstance(ECC(), ECC)
     with pytest.raises(NotImplementedError):
-        get_cmc_method("ecc")
+        get_cmc_method("orb")
     assert np.array_equal(IdentityCMC().apply(None, None), np.eye(2, 3))

@@ -187,6 +187,15 @@ _SIGS = {
     "yta_sof_kat_corners": ([_I, _P, _P, _I, _I, _P, _P], _I),
     "yta_sof_kat_lk": ([_I, _P, _P, _I, _I, _P, _I, _P, _P], _I),
     "yta_sof_kat_affine": ([_I, _P, _P, _I, _P, _P], _I),
+    "yta_ecc_create": ([_I, _I, _I, _D, _I, _D, _I, _I, _P], _I),
+    "yta_ecc_destroy": ([_P], _I),
+    "yta_ecc_reset": ([_P], _I),
+    "yta_ecc_apply": ([_P, _P, _P, _P, _P], _I),
+    "yta_ecc_apply_device": ([_P, _P, _P, _P, _P], _I),
+    "yta_ecc_sync": ([_P], _I),
+    "yta_ecc_outcome": ([_P, _P, _P, _P], _I),
+    "yta_ecc_get_state": ([_P, _I, _P, _P, _P, _P, _I], _I),
+    "yta_ecc_hip_stream": ([_P, _P], _I),
     "yta_osnet_dw3x3": ([_P, ctypes.c_longlong, ctypes.c_longlong, _P, _P, _I, _I, _I, _I, _I, _P,
                          ctypes.c_longlong, _I, _P, ctypes.c_longlong, _P, ctypes.c_longlong, _P],
                         _I),

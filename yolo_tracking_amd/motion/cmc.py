@@ -8,6 +8,7 @@ here is the same SparseOptFlow, on the GPU (motion/sof.py, csrc/cmc.hip).
 """
 import numpy as np
 
+from .ecc import ECC
 from .sof import SparseOptFlow
 
 
@@ -20,12 +21,15 @@ class IdentityCMC:
 
 
 def get_cmc_method(cmc_method):
-    """boxmot.motion.cmc.get_cmc_method (motion/cmc/__init__.py): the estimator class by name.
-    Only the sparse optical flow estimator the trackers use is on the device path."""
+    """boxmot.motion.cmc.get_cmc_method (motion/cmc/__init__.py:9-19): the estimator class by
+    name.  SparseOptFlow (what BoTSORT and DeepOCSort build) and ECC (what HybridSORT builds) run on
+    the device; ORB / SIFT (OpenCV feature matchers no in-scope tracker uses) are refused."""
     if cmc_method in ("sof", "sparseOptFlow"):
         return SparseOptFlow
-    raise NotImplementedError(f"cmc method {cmc_method!r}: only 'sof' (SparseOptFlow, the "
-                              "estimator BoTSORT and DeepOCSort build) is on the MI355X path")
+    if cmc_method == "ecc":
+        return ECC
+    raise NotImplementedError(f"cmc method {cmc_method!r}: 'sof' (SparseOptFlow) and 'ecc' (ECC) "
+                              "are on the MI355X path")
 
 
 def default_cmc(owner=None, device=0):
