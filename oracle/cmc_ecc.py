@@ -23,7 +23,7 @@ fixes one order that csrc/ecc.hip reproduces:
   * every image sum (meanStdDev's, the Hessian's, the three projections, the correlation) is a
     float64 sum of float32 operands in the fixed order of block_sum(): pixel p belongs to thread
     p % T (T = 1024, 512 for the affine model) which adds its pixels in order, then a halving
-    tree over the 64 lanes of each wave and one over the waves;
+    tree over each group of 16 threads and one over the T / 16 group partials;
   * float32 per-pixel arithmetic (zero-mean subtraction, jacobians, the error image) in the order
     written below, no fused multiply-adds;
   * cv::invert (DECOMP_LU) closed forms for 2 x 2 / 3 x 3 (float64 cofactors, stored as float32)
@@ -58,7 +58,9 @@ class ECCError(Exception):
 
 # ------------------------------------------------------------------------------ reductions
 def block_sum(v, n_threads=ECC_T):
-    """Sum of the last axis of v (float64) in the device's fixed order (module docstring)."""
+    """Sum of the last axis of v (float64) in the device's fixed order: thread t accumulates the
+    pixels t, t + T, ... in order; a halving tree inside each group of 16 threads; a halving tree
+    over the T / 16 group partials (csrc/ecc.hip block_sum)."""
     v = np.asarray(v, dtype=np.float64)
     lead = v.shape[:-1]
     n = v.shape[-1]
@@ -69,7 +71,7 @@ def block_sum(v, n_threads=ECC_T):
     acc = np.zeros(lead + (n_threads,))
     for r in range(k):
         acc = acc + rows[..., r, :]
-    a = acc.reshape(lead + (n_threads // WAVE, WAVE))
+    a = acc.reshape(lead + (n_threads // 16, 16))
     while a.shape[-1] > 1:
         h = a.shape[-1] // 2
         a = a[..., :h] + a[..., h:]

@@ -40,7 +40,8 @@ def test_block_sum_order():
     for n in (1, 63, 1024, 1500, 20736):
         v = rng.normal(0, 1, n)
         assert abs(ce.block_sum(v) - v.sum()) <= 1e-12 * max(1.0, np.abs(v).sum())
-    # the documented order: thread t adds pixels t, t + 1024, ... then halving trees
+    # the documented order: thread t adds pixels t, t + 1024, ... then halving trees over groups
+    # of 16 threads and over the 64 group partials
     v = rng.normal(0, 1, (2, 3000))
     acc = np.zeros((2, 1024))
     for r in range(3):
@@ -48,7 +49,7 @@ def test_block_sum_order():
         seg = v[:, r * 1024:(r + 1) * 1024]
         blk[:, :seg.shape[1]] = seg
         acc = acc + blk
-    lanes = acc.reshape(2, 16, 64)
+    lanes = acc.reshape(2, 64, 16)
     while lanes.shape[-1] > 1:
         lanes = lanes[..., :lanes.shape[-1] // 2] + lanes[..., lanes.shape[-1] // 2:]
     waves = lanes[..., 0]

@@ -5,7 +5,9 @@ streams' frames in the same 5 launches), warps left on the device.  Frame 0 is t
 path (goodFeaturesToTrack); the timed steps are the steady state (pyramids, Lucas-Kanade of the
 stored corners, RANSAC + LM).  Frames: a textured scene per stream seen through a moving crop
 window (integer shifts of a few px per frame).  CPU leg: oracle/cmc_sof.py (NumPy restatement) on
-one stream, 1 thread, a bounded sample of the same frames.  Prints one JSON line."""
+one stream, 1 thread, a bounded sample of the same frames.  Prints one JSON line.
+--estimator ecc: the ECC estimator instead (ecc.py, csrc/ecc.hip: one yta_ecc_apply_device call
+per step, warp_mode --warp-mode, default euclidean), its CPU leg oracle/cmc_ecc.py."""
 import argparse
 import ctypes
 import json
@@ -43,6 +45,8 @@ def main():
     ap.add_argument("--scale", type=float, default=0.1)
     ap.add_argument("--cpu-frames", type=int, default=4)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--estimator", choices=["sof", "ecc"], default="sof")
+    ap.add_argument("--warp-mode", type=int, default=1, help="ECC: 0 translation, 1 euclidean, 2 affine")
     args = ap.parse_args()
     import torch
     from yolo_tracking_amd import _lib
@@ -61,14 +65,28 @@ def main():
     d_hw = torch.tensor([H, W] * S, dtype=torch.int32, device=d)
     d_dets = torch.from_numpy(dets).to(d)
     d_doff = torch.arange(S + 1, dtype=torch.int32, device=d) * args.dets
-    d_warps = torch.zeros((S, 6), dtype=torch.float64, device=d)
-    eng = SofEngine(S, args.scale, 0, H, W)
-    lib = eng.lib
+    ecc = args.estimator == "ecc"
+    d_warps = torch.zeros((S, 6), dtype=torch.float32 if ecc else torch.float64, device=d)
     hs = ctypes.c_void_p()
-    _lib.check(lib.yta_sof_hip_stream(eng.handle, ctypes.byref(hs)))
+    if ecc:
+        from yolo_tracking_amd.motion.ecc import EccEngine
+        eng = EccEngine(S, args.warp_mode, 1e-5, 100, args.scale, 0, H, W)
+        lib = eng.lib
+        _lib.check(lib.yta_ecc_hip_stream(eng.handle, ctypes.byref(hs)))
+    else:
+        eng = SofEngine(S, args.scale, 0, H, W)
+        lib = eng.lib
+        _lib.check(lib.yta_sof_hip_stream(eng.handle, ctypes.byref(hs)))
     stream = torch.cuda.ExternalStream(hs.value, device=d)
+    sync = (lambda: _lib.check(lib.yta_ecc_sync(eng.handle))) if ecc else \
+        (lambda: _lib.check(lib.yta_sof_sync(eng.handle)))
 
     def step(f):
+        if ecc:
+            _lib.check(lib.yta_ecc_apply_device(
+                eng.handle, ctypes.c_void_p(d_fr[f].data_ptr()), ctypes.c_void_p(d_off.data_ptr()),
+                ctypes.c_void_p(d_hw.data_ptr()), ctypes.c_void_p(d_warps.data_ptr())))
+            return
         _lib.check(lib.yta_sof_apply_device(
             eng.handle, ctypes.c_void_p(d_fr[f].data_ptr()), ctypes.c_void_p(d_off.data_ptr()),
             ctypes.c_void_p(d_hw.data_ptr()), ctypes.c_void_p(d_dets.data_ptr()), 4,
@@ -80,27 +98,47 @@ def main():
     step(0)                            # first frame: corners
     e[1].record(stream)
     step(1)                            # warm-up of the steady-state path
-    _lib.check(lib.yta_sof_sync(eng.handle))
+    sync()
     t1 = time.perf_counter()
     e[2].record(stream)
     for f in range(2, F):
         step(f)
     e_end = torch.cuda.Event(enable_timing=True)
     e_end.record(stream)
-    _lib.check(lib.yta_sof_sync(eng.handle))
+    sync()
     wall = time.perf_counter() - t1
     torch.cuda.synchronize()
     first_ms = e[0].elapsed_time(e[1])
     steady_ms = e[2].elapsed_time(e_end) / (F - 2)
-    oc = eng.outcome()
-    n_kp = [len(eng.state(s)["keypoints"]) for s in range(min(S, 4))]
-    line = {"metric": "SparseOptFlow.apply() frames/s", "value": S / (steady_ms * 1e-3),
+    if ecc:
+        oc, iters, _ = eng.outcome()
+        extra = {"iters_mean": float(np.mean(iters)), "iters_max": int(np.max(iters)),
+                 "warp_mode": args.warp_mode}
+    else:
+        oc = eng.outcome()
+        extra = {"corners_stream0_3": [len(eng.state(s)["keypoints"]) for s in range(min(S, 4))]}
+    name = "ECC.apply()" if ecc else "SparseOptFlow.apply()"
+    line = {"metric": f"{name} frames/s", "value": S / (steady_ms * 1e-3),
             "unit": "frames/s", "streams": S, "frame": f"{W}x{H}", "scale": args.scale,
             "steps": F - 2, "ms_per_step": steady_ms, "first_frame_ms": first_ms,
             "wall_ms_per_step": 1000 * wall / (F - 2), "outcomes": np.bincount(oc, minlength=3).tolist(),
-            "corners_stream0_3": n_kp, "dets_per_stream": args.dets, "gen_s": round(gen_s, 1),
-            "data": "synthetic textured scene, moving crop window"}
-    if not args.no_cpu:
+            "dets_per_stream": args.dets, "gen_s": round(gen_s, 1),
+            "data": "synthetic textured scene, moving crop window", **extra}
+    if not args.no_cpu and ecc:
+        from oracle import cmc_ecc as ce
+        o = ce.ECCOracle(warp_mode=args.warp_mode, scale=args.scale)
+        o.apply(fr[0, 0])
+        o.apply(fr[1, 0])
+        n = min(args.cpu_frames, F - 2)
+        c0 = time.perf_counter()
+        for f in range(2, 2 + n):
+            o.apply(fr[f, 0])
+        cpu_s = (time.perf_counter() - c0) / n
+        line["cpu_baseline"] = {"value": 1.0 / cpu_s, "unit": "frames/s", "cores": 1,
+                                "kind": "port",
+                                "sample": f"oracle/cmc_ecc.py, stream 0, frames 2..{1 + n}, "
+                                          f"{cpu_s * 1000:.1f} ms/frame, 1 thread"}
+    elif not args.no_cpu:
         from oracle import cmc_sof as cs
         o = cs.SparseOptFlowOracle(args.scale)
         dd = dets[:args.dets]

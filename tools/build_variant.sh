@@ -9,7 +9,7 @@ out=../../tools/variants/build_$name
 mkdir -p $out
 FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -Wall -Wno-unused-function -munsafe-fp-atomics $*"
 objs=""
-for s in util kat bytetrack ocsort deepocsort hybridsort gsi reid cmc osnet; do
+for s in util kat bytetrack ocsort deepocsort hybridsort gsi reid cmc ecc osnet; do
   /opt/rocm/bin/hipcc $FLAGS -c $s.hip -o $out/$s.o 2>/dev/null &
   objs="$objs $out/$s.o"
 done

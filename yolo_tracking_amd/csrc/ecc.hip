@@ -26,6 +26,7 @@
 // HBM layout per stream: two u8 slots (previous accepted frame / current frame) of
 // round(max_h * scale) x round(max_w * scale) bytes, EccState, the 2x3 float32 warp.
 #include <algorithm>
+#include <type_traits>
 #include <cfloat>
 #include <cmath>
 #include <new>
@@ -38,7 +39,7 @@ namespace yta {
 namespace {
 using namespace cmc;
 
-constexpr int ECC_LDS = 144 * 1024;         // current frame bytes staged in LDS
+constexpr int ECC_LDS = 144 * 1024;         // k_ecc's dynamic LDS (warp tables + packed frame)
 
 enum { ECC_TRANSLATION = 0, ECC_EUCLIDEAN = 1, ECC_AFFINE = 2 };
 enum { ECC_OUT_FIRST = 0, ECC_OUT_EST = 1, ECC_OUT_FAIL = 2 };
@@ -71,7 +72,24 @@ __host__ __device__ constexpr int ecc_nparams(int mode) {
 }
 
 // k_ecc's block: 1024 threads, 512 for the affine model (34 float64 sums per thread in pass B)
-__host__ __device__ constexpr int ecc_threads(int mode) { return mode == ECC_AFFINE ? 512 : 1024; }
+#ifndef ECC_T1
+#define ECC_T1 1024
+#endif
+__host__ __device__ constexpr int ecc_threads(int mode) {
+    return mode == ECC_AFFINE ? 512 : mode == ECC_EUCLIDEAN ? ECC_T1 : 1024;
+}
+// unrolling of the three pixel loops (moments; Hessian + projections; error projection)
+#ifndef ECC_UA
+#define ECC_UA 4
+#endif
+#ifndef ECC_UB
+#define ECC_UB 1
+#endif
+#ifndef ECC_UC
+#define ECC_UC 2
+#endif
+#define ECC_PRAGMA(x) _Pragma(#x)
+#define ECC_UNROLL(n) ECC_PRAGMA(unroll n)
 
 // ------------------------------------------------------------------------------- k_ecc_small
 __global__ __launch_bounds__(256) void k_ecc_small(EccArgs a) {
@@ -124,48 +142,116 @@ struct Warped {
     bool m;             // nearest sample of the all-ones premask
 };
 
-// One template pixel (x, y) warped into the current frame `img` (hd x wd).  Every bilinear
-// sample is exact in float32 (u8 or half-integer values times k / 1024 weights), the sum order
-// is remapBilinear's ((v00 w0 + v01 w1) + v10 w2) + v11 w3.
-template <bool GRAD, typename P>
-__device__ __forceinline__ Warped warp_px(P img, int hd, int wd, const double (&M)[6], int x,
-                                          int y) {
-    const int xr = cv_round((M[1] * y + M[2]) * 1024.0), yr = cv_round((M[4] * y + M[5]) * 1024.0);
-    const int ad = cv_round(M[0] * x * 1024.0), bd = cv_round(M[3] * x * 1024.0);
+// The current frame in LDS, one word per pixel: the byte, and 2 x the x / y gradients (the
+// filter2D (-0.5, 0, 0.5) responses with reflect-101 borders are half-integers in
+// [-127.5, 127.5]) biased by 255 in 9 bits each.  One LDS read per bilinear tap.
+struct PackedSrc {
+    const unsigned *p;
+    int hd, wd;
+    // pixel q: the byte and 2 x the gradients (integers)
+    __device__ __forceinline__ void tap(int q, int &v, int &g2x, int &g2y) const {
+        const unsigned w = p[q];
+        v = (int)(w & 255u);
+        g2x = (int)__builtin_amdgcn_ubfe(w, 8, 9) - 255;
+        g2y = (int)__builtin_amdgcn_ubfe(w, 17, 9) - 255;
+    }
+};
+
+__device__ __forceinline__ unsigned pack_px(const uint8_t *img, int hd, int wd, int q) {
+    const int r = q / wd, u = q - r * wd, row = r * wd;
+    const int gx2 = (int)img[row + refl(u + 1, wd)] - (int)img[row + refl(u - 1, wd)];
+    const int gy2 = (int)img[refl(r + 1, hd) * wd + u] - (int)img[refl(r - 1, hd) * wd + u];
+    return (unsigned)img[q] | ((unsigned)(gx2 + 255) << 8) | ((unsigned)(gy2 + 255) << 17);
+}
+
+// The current frame's bytes in HBM (frames too large for the LDS stage): gradients formed from
+// the neighbouring bytes at every tap.
+struct RawSrc {
+    const uint8_t *p;
+    int hd, wd;
+    __device__ __forceinline__ void tap(int q, int &v, int &g2x, int &g2y) const {
+        const int r = q / wd, u = q - r * wd, row = r * wd;
+        v = p[q];
+        g2x = (int)p[row + refl(u + 1, wd)] - (int)p[row + refl(u - 1, wd)];
+        g2y = (int)p[refl(r + 1, hd) * wd + u] - (int)p[refl(r - 1, hd) * wd + u];
+    }
+};
+
+// warpAffine's per-row and per-column fixed-point terms of one iteration's map (LDS):
+// xr / yr[y] = cvRound((M1 y + M2) 1024) / cvRound((M4 y + M5) 1024),
+// ad / bd[x] = cvRound(M0 x 1024) / cvRound(M3 x 1024) (WarpAffineInvoker's adelta / bdelta).
+struct WarpTabs {
+    int *xr, *yr, *ad, *bd;
+};
+
+// One template pixel (x, y) warped into the current frame.  remapBilinear's float32 sum
+// ((v00 w0 + v01 w1) + v10 w2) + v11 w3 with the table's weights (32 - f)(32 - g) / 1024 ... is
+// exact here (u8 or half-integer values, 11-bit weights, < 2^24 in every partial sum), so it is
+// formed as the integer sum of weight numerators x values, scaled by 2^-10 (2^-11 for the
+// gradients, which are stored doubled): the same float32 bits in any order.
+template <bool GRAD, typename Src>
+__device__ __forceinline__ Warped warp_px(const Src &src, const WarpTabs &tb, int x, int y) {
+    const int xr = tb.xr[y], yr = tb.yr[y], ad = tb.ad[x], bd = tb.bd[x];
     const int X = (xr + 16 + ad) >> 5, Y = (yr + 16 + bd) >> 5;
     const int sx = sat16(X >> 5), sy = sat16(Y >> 5);
     const int nx = sat16((xr + 512 + ad) >> 10), ny = sat16((yr + 512 + bd) >> 10);
-    const float tx = (float)(X & 31) * (1.f / 32), ty = (float)(Y & 31) * (1.f / 32);
-    const float vx0 = 1.f - tx, vy0 = 1.f - ty;
-    const float w[4] = {vy0 * vx0, vy0 * tx, ty * vx0, ty * tx};
-    Warped o;
-    o.iw = o.gx = o.gy = 0.f;
+    const int fx = X & 31, fy = Y & 31;
+    const int wn[4] = {(32 - fx) * (32 - fy), fx * (32 - fy), (32 - fx) * fy, fx * fy};
+    const int wd = src.wd, hd = src.hd;
+    int si = 0, sgx = 0, sgy = 0;
+    const int q0 = sy * wd + sx;
+    if ((unsigned)sx < (unsigned)(wd - 1) && (unsigned)sy < (unsigned)(hd - 1)) {   // interior
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {   // taps accumulated in remapBilinear's order
-        const int u = sx + (k & 1), r = sy + (k >> 1);
-        const bool in = (unsigned)u < (unsigned)wd && (unsigned)r < (unsigned)hd;
-        float v = 0.f, gx = 0.f, gy = 0.f;
-        if (in) {
-            const int row = r * wd;
-            v = (float)img[row + u];
+        for (int k = 0; k < 4; ++k) {
+            int v, g2x, g2y;
+            src.tap(q0 + (k & 1) + (k >> 1) * wd, v, g2x, g2y);
+            si += wn[k] * v;
             if (GRAD) {
-                gx = 0.5f * ((float)img[row + refl(u + 1, wd)] - (float)img[row + refl(u - 1, wd)]);
-                gy = 0.5f * ((float)img[refl(r + 1, hd) * wd + u] - (float)img[refl(r - 1, hd) * wd + u]);
+                sgx += wn[k] * g2x;
+                sgy += wn[k] * g2y;
             }
         }
-        if (k == 0) {
-            o.iw = v * w[0];
-            o.gx = gx * w[0];
-            o.gy = gy * w[0];
-        } else {
-            o.iw = o.iw + v * w[k];
-            o.gx = o.gx + gx * w[k];
-            o.gy = o.gy + gy * w[k];
+    } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int u = sx + (k & 1), r = sy + (k >> 1);
+            if ((unsigned)u < (unsigned)wd && (unsigned)r < (unsigned)hd) {
+                int v, g2x, g2y;
+                src.tap(r * wd + u, v, g2x, g2y);
+                si += wn[k] * v;
+                if (GRAD) {
+                    sgx += wn[k] * g2x;
+                    sgy += wn[k] * g2y;
+                }
+            }
         }
     }
+    Warped o;
+    o.iw = (float)si * (1.f / 1024);
+    o.gx = GRAD ? (float)sgx * (1.f / 2048) : 0.f;
+    o.gy = GRAD ? (float)sgy * (1.f / 2048) : 0.f;
     o.m = (unsigned)nx < (unsigned)wd && (unsigned)ny < (unsigned)hd;
     return o;
 }
+
+// pixels t, t + T, ... of a w-wide grid in raster order, (x, y) stepped without divisions
+struct PixIter {
+    int x, y, dx, dy, w;
+    __device__ __forceinline__ PixIter(int p0, int step, int w_) : w(w_) {
+        y = p0 / w_;
+        x = p0 - y * w_;
+        dy = step / w_;
+        dx = step - dy * w_;
+    }
+    __device__ __forceinline__ void next() {
+        x += dx;
+        y += dy;
+        if (x >= w) {
+            x -= w;
+            ++y;
+        }
+    }
+};
 
 // image_jacobian_{translation, euclidean, affine}_ECC (ecc.cpp) at one pixel, float32
 template <int MODE>
@@ -189,30 +275,34 @@ __device__ __forceinline__ void jac(float gx, float gy, float X, float Y, float 
     }
 }
 
-// Block sum of K float64 values over T threads, identical in every thread: halving tree over each
-// wave's lanes, then thread k < K runs the halving tree over the waves of value k
-// (oracle/cmc_ecc.py block_sum); red holds K x T/64 wave sums, tot the K totals.
+// Block sum of K float64 values over T threads, identical in every thread: a halving tree inside
+// each 16-lane row (DPP row shifts), the T / 16 row partials through LDS, then for each value one
+// wave runs the halving tree over its row partials (lane i holds partial i; bpermute for the
+// cross-row strides, DPP within rows) - oracle/cmc_ecc.py block_sum.  red: K x T/16 doubles.
 template <int T, int K>
 __device__ __forceinline__ void block_sum(double (&v)[K], double *red, double *tot) {
-    constexpr int NW = T / WAVE;
+    constexpr int NR = T / 16, NW = T / WAVE;
     const int t = threadIdx.x, lane = t & (WAVE - 1), wave = t / WAVE;
 #pragma unroll
-    for (int k = 0; k < K; ++k)
+    for (int k = 0; k < K; ++k) {
+        v[k] = v[k] + dpp_f64<0x108>(v[k]);   // row_shl:8
+        v[k] = v[k] + dpp_f64<0x104>(v[k]);
+        v[k] = v[k] + dpp_f64<0x102>(v[k]);
+        v[k] = v[k] + dpp_f64<0x101>(v[k]);
+    }
+    if ((t & 15) == 0)
 #pragma unroll
-        for (int off = WAVE / 2; off >= 1; off >>= 1) v[k] = v[k] + __shfl_down(v[k], off, WAVE);
-    if (lane == 0)
-#pragma unroll
-        for (int k = 0; k < K; ++k) red[k * NW + wave] = v[k];
+        for (int k = 0; k < K; ++k) red[k * NR + (t >> 4)] = v[k];
     __syncthreads();
-    if (t < K) {
-        double w[NW];
-#pragma unroll
-        for (int i = 0; i < NW; ++i) w[i] = red[t * NW + i];
-#pragma unroll
-        for (int h = NW / 2; h >= 1; h >>= 1)
-#pragma unroll
-            for (int i = 0; i < h; ++i) w[i] = w[i] + w[i + h];
-        tot[t] = w[0];
+    for (int k = wave; k < K; k += NW) {   // wave-uniform
+        double x = lane < NR ? red[k * NR + lane] : 0.0;
+        if (NR > 32) x = x + __shfl_down(x, 32, WAVE);
+        if (NR > 16) x = x + __shfl_down(x, 16, WAVE);
+        x = x + dpp_f64<0x108>(x);
+        x = x + dpp_f64<0x104>(x);
+        x = x + dpp_f64<0x102>(x);
+        x = x + dpp_f64<0x101>(x);
+        if (lane == 0) tot[k] = x;
     }
     __syncthreads();
 #pragma unroll
@@ -315,6 +405,22 @@ __device__ __forceinline__ double dot64(const float *a, const float *b) {
 // The whole findTransformECC loop of stream blockIdx.x (oracle/cmc_ecc.py find_transform_ecc).
 // Thread 0 does the small solves in LDS between the passes; the loop's control values are read
 // back by every thread after a barrier, so its exit is block-uniform.
+#ifdef YTA_STAMPS
+// diagnostic build: block 0's time per phase of the loop, summed over iterations (100 MHz ticks)
+#define ECC_PH(k)                                                 \
+    do {                                                          \
+        if (blockIdx.x == 0 && threadIdx.x == 0) {                \
+            const unsigned long long now = wall_clock64();        \
+            ph[k] += now - ph_t;                                  \
+            ph_t = now;                                           \
+        }                                                         \
+    } while (0)
+#else
+#define ECC_PH(k) \
+    do {          \
+    } while (0)
+#endif
+
 struct EccSolve {
     float H[6][6], Hi[6][6], A[6][6];
     float P[6], Q[6], iph[6], E[6], dp[6];
@@ -323,13 +429,13 @@ struct EccSolve {
     int fail;
 };
 
-template <bool LDS, int MODE>
+template <bool PACKED, int MODE>
 __global__ __launch_bounds__(ecc_threads(MODE)) void k_ecc(EccArgs a) {
     constexpr int T = ecc_threads(MODE);
     constexpr int N = ecc_nparams(MODE);
     constexpr int NB = N * (N + 1) / 2 + 2 * N + 1;   // pass B sums
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    __shared__ double red[NB * (T / WAVE)], tot[NB];
+    __shared__ double red[NB * (T / 16)], tot[NB];
     __shared__ EccSolve sv;
     const int s = blockIdx.x, t = threadIdx.x;
     EccState &st = a.state[s];
@@ -352,41 +458,78 @@ __global__ __launch_bounds__(ecc_threads(MODE)) void k_ecc(EccArgs a) {
         }
         return;
     }
-    const int hs = st0.h[st0.prev], ws = st0.w[st0.prev], hd = st0.h[cur], wd = st0.w[cur];
-    const uint8_t *tmpl = a.img + ((long long)s * 2 + st0.prev) * a.slot_px;
+    // (selects, not indexing: a dynamically indexed local array would live in scratch)
+    const int hs = st0.prev ? st0.h[1] : st0.h[0], ws = st0.prev ? st0.w[1] : st0.w[0];
+    const int hd = cur ? st0.h[1] : st0.h[0], wd = cur ? st0.w[1] : st0.w[0];
+    const uint8_t *gtmpl = a.img + ((long long)s * 2 + st0.prev) * a.slot_px;
     const uint8_t *gimg = a.img + ((long long)s * 2 + cur) * a.slot_px;
     const int npx = hs * ws, nd = hd * wd;
-    if (LDS) {
-        const uint4 *src = reinterpret_cast<const uint4 *>(gimg);
-        uint4 *dst = reinterpret_cast<uint4 *>(smem);
-        for (int k = t; k < (nd + 15) / 16; k += T) dst[k] = src[k];
+    // LDS: the warp tables, then (PACKED) the current frame's words and the template's bytes
+    WarpTabs tb;
+    tb.xr = reinterpret_cast<int *>(smem);
+    tb.yr = tb.xr + hs;
+    tb.ad = tb.yr + hs;
+    tb.bd = tb.ad + ws;
+    const long long tab_bytes = ((2LL * (hs + ws) * 4) + 15) & ~15LL;
+    unsigned *words = reinterpret_cast<unsigned *>(smem + tab_bytes);
+    uint8_t *ltmpl = reinterpret_cast<uint8_t *>(words + nd);
+    if (PACKED) {
+        for (int q = t; q < nd; q += T) words[q] = pack_px(gimg, hd, wd, q);
+        for (int q = t; q < npx; q += T) ltmpl[q] = gtmpl[q];
     }
     if (t < 6) sv.m[t] = (t == 0 || t == 4) ? 1.f : 0.f;
-    __syncthreads();
-    const uint8_t *img = LDS ? (const uint8_t *)smem : gimg;
+    const uint8_t *tmpl = PACKED ? (const uint8_t *)ltmpl : gtmpl;
+    using Src = typename std::conditional<PACKED, PackedSrc, RawSrc>::type;
+    Src src;
+    if constexpr (PACKED) src.p = words;
+    else src.p = gimg;
+    src.hd = hd;
+    src.wd = wd;
     float m[6] = {1.f, 0.f, 0.f, 0.f, 1.f, 0.f};
     double rho = -1.0, last_rho = -a.eps;
     int it = 0;
     bool fail = false;
+#ifdef YTA_STAMPS
+    unsigned long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0}, ph_t = wall_clock64();
+    const unsigned long long clk0 = clock64();
+#endif
+    __syncthreads();
+    ECC_PH(0);
     while (it < a.max_iter && fabs(rho - last_rho) >= a.eps) {
         ++it;
-        const double M[6] = {uni((double)m[0]), uni((double)m[1]), uni((double)m[2]),
-                             uni((double)m[3]), uni((double)m[4]), uni((double)m[5])};
+        {   // this iteration's warp tables
+            const double M[6] = {uni((double)m[0]), uni((double)m[1]), uni((double)m[2]),
+                                 uni((double)m[3]), uni((double)m[4]), uni((double)m[5])};
+            for (int k = t; k < hs; k += T) {
+                tb.xr[k] = cv_round((M[1] * k + M[2]) * 1024.0);
+                tb.yr[k] = cv_round((M[4] * k + M[5]) * 1024.0);
+            }
+            for (int k = t; k < ws; k += T) {
+                tb.ad[k] = cv_round(M[0] * k * 1024.0);
+                tb.bd[k] = cv_round(M[3] * k * 1024.0);
+            }
+            __syncthreads();
+        }
+        ECC_PH(1);
         // pass A: meanStdDev of the warped image and of the template over the warped mask
         double va[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
-        for (int p = t; p < npx; p += T) {
-            const int y = p / ws, x = p - y * ws;
-            const Warped q = warp_px<false>(img, hd, wd, M, x, y);
+        PixIter pa(t, T, ws);
+        ECC_UNROLL(ECC_UA)
+        for (int p = t; p < npx; p += T, pa.next()) {
+            const int x = pa.x, y = pa.y;
+            const Warped q = warp_px<false>(src, tb, x, y);
             if (q.m) {
                 const double iw = q.iw, tv = (double)tmpl[p];
                 va[0] = va[0] + iw;
-                va[1] = va[1] + iw * iw;
+                va[1] = fma(iw, iw, va[1]);   // products of float32 values are exact in float64
                 va[2] = va[2] + tv;
-                va[3] = va[3] + tv * tv;
+                va[3] = fma(tv, tv, va[3]);
                 va[4] = va[4] + 1.0;
             }
         }
+        ECC_PH(2);
         block_sum<T>(va, red, tot);
+        ECC_PH(3);
 #pragma unroll
         for (int k = 0; k < 5; ++k) va[k] = uni(va[k]);
         const double cnt = va[4];
@@ -402,9 +545,11 @@ __global__ __launch_bounds__(ecc_threads(MODE)) void k_ecc(EccArgs a) {
         double vb[NB];
 #pragma unroll
         for (int k = 0; k < NB; ++k) vb[k] = 0.0;
-        for (int p = t; p < npx; p += T) {
-            const int y = p / ws, x = p - y * ws;
-            const Warped q = warp_px<true>(img, hd, wd, M, x, y);
+        PixIter pb(t, T, ws);
+        ECC_UNROLL(ECC_UB)
+        for (int p = t; p < npx; p += T, pb.next()) {
+            const int x = pb.x, y = pb.y;
+            const Warped q = warp_px<true>(src, tb, x, y);
             const float tv = (float)tmpl[p];
             const float iwz = q.m ? q.iw - img_mean_f : q.iw;
             const float tz = q.m ? tv - tmp_mean_f : 0.f;
@@ -414,14 +559,16 @@ __global__ __launch_bounds__(ecc_threads(MODE)) void k_ecc(EccArgs a) {
 #pragma unroll
             for (int i = 0; i < N; ++i)
 #pragma unroll
-                for (int j = i; j < N; ++j, ++k) vb[k] = vb[k] + (double)J[i] * (double)J[j];
+                for (int j = i; j < N; ++j, ++k) vb[k] = fma((double)J[i], (double)J[j], vb[k]);
 #pragma unroll
-            for (int i = 0; i < N; ++i) vb[k + i] = vb[k + i] + (double)J[i] * (double)iwz;
+            for (int i = 0; i < N; ++i) vb[k + i] = fma((double)J[i], (double)iwz, vb[k + i]);
 #pragma unroll
-            for (int i = 0; i < N; ++i) vb[k + N + i] = vb[k + N + i] + (double)J[i] * (double)tz;
-            vb[k + 2 * N] = vb[k + 2 * N] + (double)tz * (double)iwz;
+            for (int i = 0; i < N; ++i) vb[k + N + i] = fma((double)J[i], (double)tz, vb[k + N + i]);
+            vb[k + 2 * N] = fma((double)tz, (double)iwz, vb[k + 2 * N]);
         }
+        ECC_PH(4);
         block_sum<T>(vb, red, tot);
+        ECC_PH(3);
         if (t == 0) {
             int k = 0;
             for (int i = 0; i < N; ++i)
@@ -453,6 +600,7 @@ __global__ __launch_bounds__(ecc_threads(MODE)) void k_ecc(EccArgs a) {
             }
         }
         __syncthreads();
+        ECC_PH(5);
         last_rho = rho;
         rho = sv.rho;
         if (sv.fail) {
@@ -464,9 +612,11 @@ __global__ __launch_bounds__(ecc_threads(MODE)) void k_ecc(EccArgs a) {
         double vc[N];
 #pragma unroll
         for (int k = 0; k < N; ++k) vc[k] = 0.0;
-        for (int p = t; p < npx; p += T) {
-            const int y = p / ws, x = p - y * ws;
-            const Warped q = warp_px<true>(img, hd, wd, M, x, y);
+        PixIter pc(t, T, ws);
+        ECC_UNROLL(ECC_UC)
+        for (int p = t; p < npx; p += T, pc.next()) {
+            const int x = pc.x, y = pc.y;
+            const Warped q = warp_px<true>(src, tb, x, y);
             const float tv = (float)tmpl[p];
             const float iwz = q.m ? q.iw - img_mean_f : q.iw;
             const float tz = q.m ? tv - tmp_mean_f : 0.f;
@@ -474,9 +624,11 @@ __global__ __launch_bounds__(ecc_threads(MODE)) void k_ecc(EccArgs a) {
             float J[N];
             jac<MODE>(q.gx, q.gy, (float)x, (float)y, c, sn, J);
 #pragma unroll
-            for (int i = 0; i < N; ++i) vc[i] = vc[i] + (double)J[i] * (double)e;
+            for (int i = 0; i < N; ++i) vc[i] = fma((double)J[i], (double)e, vc[i]);
         }
+        ECC_PH(6);
         block_sum<T>(vc, red, tot);
+        ECC_PH(3);
         if (t == 0) {   // update_warping_matrix_ECC
             for (int i = 0; i < N; ++i) sv.E[i] = (float)tot[i];
             gemv<N>(sv.Hi, sv.E, sv.dp);
@@ -502,9 +654,15 @@ __global__ __launch_bounds__(ecc_threads(MODE)) void k_ecc(EccArgs a) {
             }
         }
         __syncthreads();
+        ECC_PH(5);
 #pragma unroll
         for (int k = 0; k < 6; ++k) m[k] = uni(sv.m[k]);
     }
+#ifdef YTA_STAMPS
+    if (blockIdx.x == 0 && threadIdx.x == 0)
+        for (int k = 0; k < 9; ++k)
+            g_stamps[k] = k == 7 ? (unsigned long long)it : k == 8 ? clock64() - clk0 : ph[k];
+#endif
     if (fail) {   // ecc.py:82-84: the identity, prev_img kept
         if (t < 6) W[t] = (t == 0 || t == 4) ? 1.f : 0.f;
         if (t == 0) {
@@ -514,11 +672,12 @@ __global__ __launch_bounds__(ecc_threads(MODE)) void k_ecc(EccArgs a) {
         }
         return;
     }
-    if (a.scale < 1.0) {   // ecc.py:87-89 (float32 division, NumPy's float32 scalar rules)
-        m[2] = m[2] / (float)a.scale;
-        m[5] = m[5] / (float)a.scale;
+    if (t == 0 && a.scale < 1.0) {   // ecc.py:87-89 (float32 division, NumPy's float32 scalars)
+        sv.m[2] = sv.m[2] / (float)a.scale;
+        sv.m[5] = sv.m[5] / (float)a.scale;
     }
-    if (t < 6) W[t] = m[t];
+    __syncthreads();
+    if (t < 6) W[t] = sv.m[t];
     if (t == 0) {
         st.prev = cur;   // ecc.py:102
         st.outcome = ECC_OUT_EST;
@@ -561,6 +720,8 @@ int ecc_slots(yta_ecc *e) {
     a.hmax = (int)std::rint(e->max_h * e->scale);
     a.wmax = (int)std::rint(e->max_w * e->scale);
     YTA_CHECK(a.hmax >= 1 && a.wmax >= 1, YTA_ERR_INVALID, "frames scale to an empty image");
+    YTA_CHECK(8LL * (a.hmax + a.wmax) + 16 <= ECC_LDS, YTA_ERR_CAPACITY,
+              "scaled frames of %d x %d: the warp tables exceed the LDS stage", a.hmax, a.wmax);
     a.slot_px = ((long long)a.hmax * a.wmax + 15) & ~15LL;
     YTA_HIP(hipMalloc((void **)&e->img, (size_t)(2LL * e->S * a.slot_px)));
     a.img = e->img;
@@ -578,8 +739,8 @@ int set_ecc_lds() {
     static bool done = false;
     if (done) return YTA_OK;
     for (int mode = 0; mode < 3; ++mode)
-        YTA_HIP(hipFuncSetAttribute(ecc_kernel<true>(mode),
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, ECC_LDS));
+        for (const void *k : {ecc_kernel<true>(mode), ecc_kernel<false>(mode)})
+            YTA_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, ECC_LDS));
     done = true;
     return YTA_OK;
 }
@@ -595,10 +756,13 @@ int ecc_launch(yta_ecc *e) {
     const int blocks = (int)((a.slot_px + 255) / 256);
     hipLaunchKernelGGL(k_ecc_small, dim3(blocks, a.S), dim3(256), 0, e->stream, a);
     YTA_HIP(hipGetLastError());
-    const bool lds = a.slot_px <= ECC_LDS;
+    // dynamic LDS: the warp tables, then (packed path) 4 B per current-frame pixel + the template
+    const long long tab = ((2LL * (a.hmax + a.wmax) * 4) + 15) & ~15LL;
+    const bool packed = tab + 5 * a.slot_px <= ECC_LDS;
+    const size_t lds = (size_t)(packed ? tab + 5 * a.slot_px : tab);
     void *args[] = {&a};
-    YTA_HIP(hipLaunchKernel(lds ? ecc_kernel<true>(e->mode) : ecc_kernel<false>(e->mode),
-                            dim3(a.S), dim3(ecc_threads(e->mode)), args, lds ? (size_t)a.slot_px : 0, e->stream));
+    YTA_HIP(hipLaunchKernel(packed ? ecc_kernel<true>(e->mode) : ecc_kernel<false>(e->mode),
+                            dim3(a.S), dim3(ecc_threads(e->mode)), args, lds, e->stream));
     return YTA_OK;
 }
 
@@ -786,6 +950,16 @@ int yta_ecc_get_state(yta_ecc *e, int stream, int *initialized, int *h, int *w,
     }
     return YTA_OK;
 }
+
+#ifdef YTA_STAMPS
+// diagnostic build only: block 0's phase ticks of the last k_ecc (setup, tables, pass A, the
+// three block sums, pass B, the solves, pass C, iterations)
+int yta_ecc_debug_stamps(yta_ecc *e, unsigned long long *out) {
+    YTA_HIP(host_wait(e->stream));
+    YTA_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), 9 * sizeof(unsigned long long)));
+    return YTA_OK;
+}
+#endif
 
 int yta_ecc_hip_stream(yta_ecc *e, void **stream) {
     YTA_CHECK(e && stream, YTA_ERR_INVALID, "null argument");
