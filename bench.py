@@ -159,6 +159,10 @@ def parse(argv=None):
     p.add_argument("--seed", type=int, default=1000)
     p.add_argument("--queues", type=int, default=2,
                    help="engines per GPU, each on its own HIP stream, streams split between them")
+    p.add_argument("--shared-gpu", action="store_true",
+                   help="rehearsal on a box with fewer GPUs than ranks: rank r uses device "
+                        "r mod device_count and the ranks synchronise over gloo (not a scaling "
+                        "measurement: the ranks share the card)")
     p.add_argument("--dry-cpu", action="store_true",
                    help="harness rehearsal: CPU ranks over gloo, NumPy stand-in step, no GPU")
     return p.parse_args(argv)
@@ -362,11 +366,16 @@ def main():
     if args.dry_cpu:
         return run_dry(args, world, rank)
     import torch
+    if args.shared_gpu:
+        local_rank = local_rank % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local_rank)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if args.shared_gpu:   # RCCL refuses two ranks on one device
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
 
     from yolo_tracking_amd import ByteTrackEngine, _lib
     S, N = args.streams, args.n
@@ -456,7 +465,7 @@ def main():
         _lib.check(lib.yta_bytetrack_profile_collect(h, ms, ctypes.byref(nfr)))
         iso_ms = {PHASES[k]: ms[k] / max(nfr.value, 1) for k in range(len(PHASES))}
 
-    elapsed = max_over_ranks(elapsed, dist, "cuda")
+    elapsed = max_over_ranks(elapsed, dist, "cpu" if args.shared_gpu else "cuda")
     value = aggregate_rate(world, S, args.steps, elapsed)
     ms_per_step = 1000.0 * elapsed / args.steps
 
