@@ -1,0 +1,41 @@
+"""Time the lapjv replay (lap_dense.hpp, one wave; yta_lap_padded KAT) on a GIoU-surge-shaped
+cost matrix: more detections than trackers, every pair that does not overlap costs exactly 0 (the
+reference's giou_batch gives non-overlapping pairs -1 -> 0 after the shift), a few overlapping
+pairs per tracker cost -(iou-like) < 0.  Checks the assignment against oracle/lapjv.c and prints
+both times.  GPU box: python tools/time_replay.py [--na 3874 --nb 1934]"""
+import argparse
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+from oracle import lap as olap  # noqa: E402
+from yolo_tracking_amd import _lib  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--na", type=int, default=3874)
+ap.add_argument("--nb", type=int, default=1934)
+ap.add_argument("--per-col", type=int, default=4)
+ap.add_argument("--seed", type=int, default=5)
+args = ap.parse_args()
+rng = np.random.default_rng(args.seed)
+c = np.zeros((args.na, args.nb))
+for j in range(args.nb):
+    rows = rng.choice(args.na, size=args.per_col, replace=False)
+    c[rows, j] = -rng.random(args.per_col) * 0.8 - 0.05
+print(f"{args.na} x {args.nb}, {np.count_nonzero(c)} nonzero entries", flush=True)
+t0 = time.perf_counter()
+_, x_ref, _ = olap.lapjv(c, extend_cost=True)
+t_cpu = time.perf_counter() - t0
+x, _ = _lib.lap_padded(c)   # warm-up (module load, allocation)
+t0 = time.perf_counter()
+x, _ = _lib.lap_padded(c)
+t_gpu = time.perf_counter() - t0
+same = np.array_equal(np.where(np.asarray(x) < args.nb, x, -1), np.where(x_ref < args.nb, x_ref, -1))
+print(f"replay {t_gpu * 1e3:.1f} ms on the device, oracle/lapjv.c {t_cpu * 1e3:.1f} ms on one core, "
+      f"assignments equal: {same}", flush=True)
+sys.exit(0 if same else 1)

@@ -115,17 +115,17 @@ __global__ __launch_bounds__(1024) void k_lap_dense(const double *cost, int nr, 
         atomicOr(err, ERR_EDGE_OVERFLOW);
 }
 
-// One wave: the padded dense solve of association.py:20-28 (lapjv(cost, extend_cost=True)).
-// Work arrays in LDS (n <= LAP_PADDED_LDS_N) or in the global buffer `gws`.
-constexpr int LAP_PADDED_LDS_N = 1536;
+// One wave: the padded dense solve of association.py:20-28 (lapjv(cost, extend_cost=True)),
+// work arrays placed as the engines place them (lap_dense_placed) within `lds_bytes` of LDS.
+constexpr long long LAP_PADDED_LDS = 156 * 1024;   // the first-round kernels' LDS cap
 __global__ __launch_bounds__(64) void k_lap_padded(const double *cost, int nr, int nc, int *X,
-                                                   int *Y, int *err, unsigned char *gws) {
+                                                   int *Y, int *err, unsigned char *gws,
+                                                   long long lds_bytes) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int n = nr > nc ? nr : nc;
-    unsigned char *base = n <= LAP_PADDED_LDS_N ? smem : gws;
-    const DenseLapWs w = dense_lap_ws(base, n);
     const LapMat M{cost, nr, nc, false};
-    const int rc = n <= LAP_PADDED_LDS_N ? lap_dense_wave<true>(n, M, w) : lap_dense_wave<false>(n, M, w);
+    DenseLapWs w;
+    const int rc = lap_dense_placed(n, M, smem, lds_bytes, gws, w);
     if (rc && lane_id() == 0) atomicOr(err, ERR_SOLVER);
     for (int r = lane_id(); r < nr; r += WAVE) X[r] = w.x[r] < nc ? w.x[r] : -1;
     for (int k = lane_id(); k < nc; k += WAVE) Y[k] = w.y[k] < nr ? w.y[k] : -1;
@@ -487,11 +487,13 @@ int yta_lap_padded(int device, int nr, int nc, const double *cost, int *x, int *
     YTA_HIP(hipMemset(derr, 0, sizeof(int)));
     if (dcost)
         YTA_HIP(hipMemcpy(dcost, cost, sizeof(double) * nr * nc, hipMemcpyHostToDevice));
-    const size_t lds = n <= LAP_PADDED_LDS_N ? ws : 0;
+    const long long lds = dense_lap_ws_bytes(n) <= LAP_PADDED_LDS ? dense_lap_ws_bytes(n)
+                          : dense_lap_ws_bytes_norow(n) <= LAP_PADDED_LDS ? dense_lap_ws_bytes_norow(n)
+                                                                           : 0;
     YTA_HIP(hipFuncSetAttribute((const void *)k_lap_padded,
-                                hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)dense_lap_ws_bytes(LAP_PADDED_LDS_N)));
-    hipLaunchKernelGGL(k_lap_padded, dim3(1), dim3(64), lds, 0, dcost, nr, nc, dx, dy, derr, gws);
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)LAP_PADDED_LDS));
+    hipLaunchKernelGGL(k_lap_padded, dim3(1), dim3(64), (size_t)lds, 0, dcost, nr, nc, dx, dy, derr,
+                       gws, lds);
     YTA_HIP(hipGetLastError());
     int herr = 0;
     if (nr) YTA_HIP(hipMemcpy(x, dx, sizeof(int) * nr, hipMemcpyDeviceToHost));

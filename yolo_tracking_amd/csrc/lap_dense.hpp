@@ -58,6 +58,11 @@ __host__ __device__ inline long long dense_lap_ws_bytes(long long n) {
     return n * (6 * 4 + 4 * 8) + 64;
 }
 
+// the work arrays without the two row buffers (those then live in global memory)
+__host__ __device__ inline long long dense_lap_ws_bytes_norow(long long n) {
+    return n * (6 * 4 + 2 * 8) + 64;
+}
+
 // carve a DenseLapWs out of `base` (dense_lap_ws_bytes(n) bytes, 8-aligned)
 __host__ __device__ inline DenseLapWs dense_lap_ws(unsigned char *base, int n) {
     DenseLapWs w;
@@ -70,6 +75,22 @@ __host__ __device__ inline DenseLapWs dense_lap_ws(unsigned char *base, int n) {
     w.cols = w.free_rows + n;
     w.pred = w.cols + n;
     w.aux = w.pred + n;
+    return w;
+}
+
+// the same with the row buffers (2 n doubles) at `rows` instead (LDS arrays, global rows)
+__host__ __device__ inline DenseLapWs dense_lap_ws_split(unsigned char *base, unsigned char *rows,
+                                                        int n) {
+    DenseLapWs w;
+    w.v = reinterpret_cast<double *>(base);
+    w.d = w.v + n;
+    w.x = reinterpret_cast<int *>(w.d + n);
+    w.y = w.x + n;
+    w.free_rows = w.y + n;
+    w.cols = w.free_rows + n;
+    w.pred = w.cols + n;
+    w.aux = w.pred + n;
+    w.row = reinterpret_cast<double *>(rows);
     return w;
 }
 
@@ -239,9 +260,9 @@ __device__ __forceinline__ int gather_min_reg(int n, int lo, DP d, IP cols) {
 // distance is computed at once; the first position that reaches a free column at the current
 // minimum ends the sweep (positions after it are not visited); lane 0 replays the swaps of the
 // other minimum-distance positions before it.  Returns that free column or -1; `shi` advances.
-template <bool LDS_WS, int LAP_PF, typename DP, typename IP>
+template <bool LDS_WS, int LAP_PF, typename RP, typename DP, typename IP>
 __device__ __forceinline__ int relax_reg(int n, int &shi, int r, double h, double dk, bool real_row,
-                                         DP rowbuf, DP d, DP v, IP pred, IP cols, IP y) {
+                                         RP rowbuf, DP d, DP v, IP pred, IP cols, IP y) {
     const int lane = lane_id();
     const int b0 = shi;
     int kk[LAP_PF];
@@ -323,7 +344,9 @@ __device__ __forceinline__ int relax_reg(int n, int &shi, int r, double h, doubl
 // Square dense solve of the padded n x n problem M by the calling wave (all 64 lanes).  x[row] =
 // col, y[col] = row.  Returns 0, or -2 if an augmenting path could not be traced (corrupt input).
 // LDS_WS: the work arrays of `w` are in LDS.
-template <bool LDS_WS, int LAP_PF>
+// ROW_LDS: the two row buffers are in LDS too (else in global memory, the other arrays in LDS
+// when LDS_WS).
+template <bool LDS_WS, bool ROW_LDS, int LAP_PF>
 __device__ __noinline__ int lap_dense_wave_pf(int n, const LapMat M, const DenseLapWs w) {
     const int lane = lane_id();
     auto x = ws_ptr<LDS_WS>(w.x), y = ws_ptr<LDS_WS>(w.y), fr = ws_ptr<LDS_WS>(w.free_rows);
@@ -490,7 +513,8 @@ __device__ __noinline__ int lap_dense_wave_pf(int n, const LapMat M, const Dense
 #ifdef YTA_STAMPS
     unsigned long long acc_store = 0, acc_relax = 0, acc_gather = 0, acc_init = 0;
 #endif
-    auto rowA = ws_ptr<LDS_WS>(w.row), rowB = ws_ptr<LDS_WS>(w.row + n);
+    auto rowA = ws_ptr<ROW_LDS>(w.row), rowB = ws_ptr<ROW_LDS>(w.row + n);
+    constexpr bool ROW_SYNC_LDS = LDS_WS && ROW_LDS;   // a staged row is visible after an LDS wait
     for (int f = 0; f < nfree; ++f) {
         const int src = fr[f];
         YTA_COUNT(121);
@@ -596,7 +620,7 @@ __device__ __noinline__ int lap_dense_wave_pf(int n, const LapMat M, const Dense
                     if (real_row) row_store(M, r, n, nxt, rowbuf);
                     r_next = slo < shi ? y[cols[slo]] : -1;
                     if (r_next >= 0) row_issue(M, r_next, n, nxt);
-                    lap_sync<LDS_WS>();
+                    lap_sync<ROW_SYNC_LDS>();
                     const double dk = d[k];
                     const double h = (real_row ? rowbuf[k] : 0.0) - v[k] - dk;
 #ifdef YTA_STAMPS
@@ -695,10 +719,31 @@ __device__ __noinline__ int lap_dense_wave_pf(int n, const LapMat M, const Dense
 }
 
 // Dispatch on the problem size: 8 registers per lane up to n = 512, 24 beyond.
-template <bool LDS_WS>
+template <bool LDS_WS, bool ROW_LDS = LDS_WS>
 __device__ __forceinline__ int lap_dense_wave(int n, const LapMat M, const DenseLapWs w) {
-    if (n <= WAVE * 8) return lap_dense_wave_pf<LDS_WS, 8>(n, M, w);
-    return lap_dense_wave_pf<LDS_WS, LAP_PF_MAX>(n, M, w);
+    if (n <= WAVE * 8) return lap_dense_wave_pf<LDS_WS, ROW_LDS, 8>(n, M, w);
+    return lap_dense_wave_pf<LDS_WS, ROW_LDS, LAP_PF_MAX>(n, M, w);
 }
 
+}  // namespace yta
+
+namespace yta {
+// The padded solve with its work arrays placed by size: all in LDS (dense_lap_ws_bytes(n) <=
+// lds_bytes); else the arrays in LDS and the two row buffers in `gws`
+// (dense_lap_ws_bytes_norow(n) <= lds_bytes: n <= ~3900 in 156 KiB); else all in `gws`.  `w`
+// receives the layout used (the caller reads w.x / w.y).
+__device__ __forceinline__ int lap_dense_placed(int n, const LapMat M, unsigned char *lds,
+                                                long long lds_bytes, unsigned char *gws,
+                                                DenseLapWs &w) {
+    if (dense_lap_ws_bytes(n) <= lds_bytes) {
+        w = dense_lap_ws(lds, n);
+        return lap_dense_wave<true>(n, M, w);
+    }
+    if (dense_lap_ws_bytes_norow(n) <= lds_bytes) {
+        w = dense_lap_ws_split(lds, gws, n);
+        return lap_dense_wave<true, false>(n, M, w);
+    }
+    w = dense_lap_ws(gws, n);
+    return lap_dense_wave<false>(n, M, w);
+}
 }  // namespace yta

@@ -57,8 +57,11 @@ struct LapStats {
 // association.py:20-28 on the padded problem M: wave 0 solves, x[r] = column or -1 -> rx.
 // The solver is one dependent chain of row reads; the matrix was written by k_oc_cost on every
 // XCD, so the whole block first streams it once (coalesced) into this XCD's L2.
+// Work arrays: all in LDS when they fit `lds_bytes`; else the arrays in LDS and the two row buffers
+// in `gws` when those fit (n <= ~3900 in the 156 KiB of the first-round kernels); else all in gws.
 __device__ __forceinline__ void padded_lap(const LapMat &M, int *rx, unsigned char *lds,
-                                           unsigned char *gws, int *err, LapStats *ls) {
+                                           long long lds_bytes, unsigned char *gws, int *err,
+                                           LapStats *ls) {
     const int n = M.na > M.nb ? M.na : M.nb;
     if (threadIdx.x == 0 && n > 0) ls->replays += 1;
     {
@@ -69,8 +72,8 @@ __device__ __forceinline__ void padded_lap(const LapMat &M, int *rx, unsigned ch
         block_sync();
     }
     if (threadIdx.x < WAVE && n > 0) {
-        const DenseLapWs w = dense_lap_ws(n <= OC_LDS_LAP_N ? lds : gws, n);
-        const int rc = n <= OC_LDS_LAP_N ? lap_dense_wave<true>(n, M, w) : lap_dense_wave<false>(n, M, w);
+        DenseLapWs w;
+        const int rc = lap_dense_placed(n, M, lds, lds_bytes, gws, w);
         if (rc && lane_id() == 0) atomicOr(err, ERR_SOLVER);
         for (int r = lane_id(); r < M.na; r += WAVE) rx[r] = w.x[r] < M.nb ? w.x[r] : -1;
     }
@@ -131,7 +134,7 @@ __device__ __forceinline__ void main_lap(const LapMat &M, const double *pu, cons
         rect_solve(RectMat{M.m, M.na, M.nb, M.nb, 1, M.neg}, pu, px, ps2, false, M.na, rx, lds,
                    lds_bytes, gws, err);
     else
-        padded_lap(M, rx, lds, gws, err, ls);
+        padded_lap(M, rx, lds, lds_bytes, gws, err, ls);
 }
 
 // Row pre-pass of the first-round solve for one stream, spread over the blocks of a chip-wide
@@ -195,7 +198,7 @@ __device__ __forceinline__ void iou_lap(const LapMat &M, int *rx, unsigned char 
     const bool tr = M.na > M.nb;
     const int rows = tr ? M.nb : M.na, cols = tr ? M.na : M.nb;
     if (cols > RECT_CPT_MAX * (int)blockDim.x) {
-        padded_lap(M, rx, lds, gws, err, ls);
+        padded_lap(M, rx, lds, lds_bytes, gws, err, ls);
         return;
     }
     const RectMat R = tr ? RectMat{M.m, rows, cols, 1, M.nb, M.neg}
