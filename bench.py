@@ -153,6 +153,10 @@ def parse(argv=None):
     p.add_argument("--n", type=int, default=1024, help="tracks = detections per frame")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-pcie", action="store_true", help="skip the host-buffer (PCIe) leg")
+    p.add_argument("--pcie-engines", type=int, default=1,
+                   help="engines (host threads) of the host-buffer leg")
+    p.add_argument("--no-pcie-pinned", action="store_true",
+                   help="skip the host-buffer leg's page-locked variant")
     p.add_argument("--no-isolated", action="store_true",
                    help="skip the engine-0-alone frames after the timed region (profiling runs)")
     p.add_argument("--cpu-frames", type=int, default=40)
@@ -276,40 +280,81 @@ def cpu_baseline(n, frames, seed):
     return line
 
 
-def pcie_inclusive(host, off, S, N, device, first, frames=8):
+def pcie_inclusive(host, off, S, N, device, first, frames=8, engines=1, pinned=False):
     """The same workload through the host-buffer ABI (yta_bytetrack_update: packed host dets in,
-    output rows back to the host every call, synchronous) on a fresh engine, frames 0..first-1
-    untimed (steady state), then `frames` timed calls: rank 0's report of the PCIe-inclusive
-    rate.  Never `value`."""
+    output rows back to the host every call, synchronous) on fresh engines, frames 0..first-1
+    untimed (steady state), then `frames` timed steps: rank 0's report of the PCIe-inclusive
+    rate.  With engines > 1 the streams are split over that many engines whose calls run on as
+    many host threads at once (ctypes releases the GIL), so one engine's copies overlap another's
+    kernels, as a multi-camera host would run them; a step ends when every engine's call has
+    returned.  pinned: the caller's buffers are page-locked (as a detector writing its boxes into
+    pinned memory would leave them): each frame's dets are placed in them before its timed call,
+    and the library DMAs straight from / into them (no staging copy).  Never `value`
+    (DESIGN.md §5)."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    import torch
+
     from yolo_tracking_amd import ByteTrackEngine, _lib
-    # capacity 3N: the host path reserves ahead of need (tracked + lost + this frame's dets,
-    # ~2.2N in the steady state) and would otherwise regrow the engine on the first frames
-    eng = ByteTrackEngine(S, track_thresh=0.5, match_thresh=0.8, track_buffer=30, frame_rate=30,
-                          device=device, track_capacity=3 * N, max_dets=N)
-    lib, h = eng.lib, eng.handle
-    out = np.empty((S * N, 8))   # <= one row per detection
-    out_off = np.zeros(S + 1, np.int32)
-    nid = np.zeros(S, np.int64)
+    E = max(1, min(engines, S))
+    bounds = [S * q // E for q in range(E + 1)]
+    engs, jobs = [], []
+    for q in range(E):
+        a, b = bounds[q], bounds[q + 1]
+        # capacity 3N: the host path reserves ahead of need (tracked + lost + this frame's dets,
+        # ~2.2N in the steady state) and would otherwise regrow the engine on the first frames
+        eng = ByteTrackEngine(b - a, track_thresh=0.5, match_thresh=0.8, track_buffer=30,
+                              frame_rate=30, device=device, track_capacity=3 * N, max_dets=N)
+        engs.append(eng)
+        dets = [np.ascontiguousarray(host[f][off[f][a]:off[f][b]]) for f in range(len(host))]
+        offs = [np.ascontiguousarray(off[f][a:b + 1] - off[f][a]) for f in range(len(host))]
+        def buf(shape):
+            if not pinned:
+                return np.empty(shape)
+            return torch.empty(shape, dtype=torch.float64, pin_memory=True).numpy()
+        jobs.append({"h": eng.handle, "lib": eng.lib, "dets": dets, "offs": offs,
+                     "out": buf(((b - a) * N, 8)), "out_off": np.zeros(b - a + 1, np.int32),
+                     "nid": np.zeros(b - a, np.int64),
+                     "pin": buf((max(len(d) for d in dets), 6)) if pinned else None})
     last = min(first + frames, len(host))
 
-    def call(f):
-        _lib.check(lib.yta_bytetrack_update(h, host[f].ctypes.data, off[f].ctypes.data,
-                                            nid.ctypes.data, out.ctypes.data, len(out),
-                                            out_off.ctypes.data))
+    def place(f):   # pinned: this frame's dets into the page-locked buffers (untimed)
+        for j in jobs:
+            if j["pin"] is not None:
+                j["pin"][:len(j["dets"][f])] = j["dets"][f]
+
+    def call(j, f):
+        src = j["dets"][f] if j["pin"] is None else j["pin"]
+        _lib.check(j["lib"].yta_bytetrack_update(j["h"], src.ctypes.data,
+                                                 j["offs"][f].ctypes.data, j["nid"].ctypes.data,
+                                                 j["out"].ctypes.data, len(j["out"]),
+                                                 j["out_off"].ctypes.data))
+    pool = ThreadPoolExecutor(max_workers=E)
+
+    def step(f):
+        if E == 1:
+            call(jobs[0], f)
+        else:
+            for r in [pool.submit(call, j, f) for j in jobs]:
+                r.result()
     for f in range(first):
-        call(f)
+        place(f)
+        step(f)
     dts = []
     for f in range(first, last):
+        place(f)
         t0 = time.perf_counter()
-        call(f)
+        step(f)
         dts.append(time.perf_counter() - t0)
+    pool.shutdown()
     dt = float(np.median(dts))
     return {"value": S / dt, "unit": "calls/s", "steps": len(dts), "untimed_frames": first,
-            "ms_per_step": 1000 * dt, "ms_per_step_all": [round(1000 * x, 3) for x in dts],
+            "engines": E, "ms_per_step": 1000 * dt,
+            "ms_per_step_all": [round(1000 * x, 3) for x in dts],
             "bytes_h2d_per_step": int(off[first, -1]) * 48,
             "note": "host-buffer ABI: packed dets host->device and output rows device->host "
-                    "inside every step (pageable numpy buffers, one engine of all streams); "
-                    "median step"}
+                    f"inside every step ({'page-locked' if pinned else 'pageable numpy'} buffers, "
+                    f"{E} engine(s) on as many host threads); median step"}
 
 
 def run_dry(args, world, rank):
@@ -485,7 +530,13 @@ def main():
         impl_bytes = sum(kernel_bytes(p, st) for p in PHASES) / S
         cpu = None if args.no_cpu_baseline else cpu_baseline(N, args.cpu_frames, args.seed)
         pcie = (None if args.no_pcie else
-                pcie_inclusive(host, off, S, N, local_rank, first=min(PRE, FT - 8)))
+                pcie_inclusive(host, off, S, N, local_rank, first=min(PRE, FT - 8),
+                               engines=args.pcie_engines))
+        if pcie is not None and not args.no_pcie_pinned:
+            pp = pcie_inclusive(host, off, S, N, local_rank, first=min(PRE, FT - 8),
+                                engines=args.pcie_engines, pinned=True)
+            pcie["pinned"] = {k: pp[k] for k in ("value", "ms_per_step", "ms_per_step_all")}
+            pcie["pinned"]["note"] = pp["note"]
         traffic, step_traffic, traffic_tag = pmc_traffic(S, N, Q)
         line = {
             "metric": "tracker.update() calls/sec @ 1024 tracks×1024 dets; 1/2/4/8 MI355X",

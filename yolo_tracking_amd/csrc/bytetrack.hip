@@ -2004,6 +2004,23 @@ void par_copy(yta_bytetrack *e, void *dst, const void *src, size_t bytes) {
     e->pool->copy(dst, src, bytes, (int)T);
 }
 constexpr int STAGE_CHUNKS = YTA_STAGE_CHUNKS;
+
+// True when the caller's buffer [p, p + bytes) is page-locked host memory (hipHostMalloc'd or
+// hipHostRegister'ed, e.g. a pinned torch tensor's numpy view): the DMA engines then read / write
+// it directly and the staging copy is skipped.  Pageable memory makes the query fail; its error
+// is cleared.
+bool host_pinned(const void *p, size_t bytes) {
+    if (!p || !bytes) return false;
+    for (const char *q : {(const char *)p, (const char *)p + bytes - 1}) {
+        hipPointerAttribute_t at;
+        if (hipPointerGetAttributes(&at, q) != hipSuccess) {
+            (void)hipGetLastError();
+            return false;
+        }
+        if (at.type != hipMemoryTypeHost) return false;
+    }
+    return true;
+}
 inline size_t stage_chunk(size_t bytes) {
     const int n = bytes >= (16u << 20) ? STAGE_CHUNKS : 1;
     return ((bytes + n - 1) / n + 63) & ~(size_t)63;
@@ -2471,7 +2488,10 @@ int update_host(yta_bytetrack *e, const double *dets, const int *det_offsets, co
         YTA_HIP(hipHostMalloc((void **)&e->h_dets, sizeof(double) * 6 * cap, hipHostMallocDefault));
         e->d_det_cap = cap;
     }
-    if (total) {   // chunk k's DMA overlaps chunk k+1's host copy
+    if (total && host_pinned(dets, sizeof(double) * 6 * total)) {   // straight from the caller
+        YTA_HIP(hipMemcpyAsync(e->d_det_in, dets, sizeof(double) * 6 * total,
+                               hipMemcpyHostToDevice, e->stream));
+    } else if (total) {   // chunk k's DMA overlaps chunk k+1's host copy
         const size_t bytes = sizeof(double) * 6 * total, ch = stage_chunk(bytes);
         for (size_t o = 0; o < bytes; o += ch) {
             const size_t n = std::min(ch, bytes - o);
@@ -2571,8 +2591,13 @@ int update_host(yta_bytetrack *e, const double *dets, const int *det_offsets, co
         hipLaunchKernelGGL(k_pack_out, dim3(S), dim3(256), 0, e->stream, e->a.out,
                            (long long)e->CAP, e->d_pack_off, e->d_pack);
         YTA_HIP(hipGetLastError());
-        // chunked copy back: the host copies chunk k out while chunk k+1 is in flight
         const size_t bytes = sizeof(double) * 8 * rows, ch = stage_chunk(bytes);
+        if (host_pinned(out, bytes)) {   // straight into the caller's buffer
+            YTA_HIP(hipMemcpyAsync(out, e->d_pack, bytes, hipMemcpyDeviceToHost, e->stream));
+            YTA_HIP(host_wait(e->stream));
+            return YTA_OK;
+        }
+        // chunked copy back: the host copies chunk k out while chunk k+1 is in flight
         hipEvent_t ev[STAGE_CHUNKS];
         int nev = 0;
         hipError_t err = hipSuccess;
