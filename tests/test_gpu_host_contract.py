@@ -132,3 +132,34 @@ def test_short_output_buffer_leaves_the_frame_unapplied(name):
             assert len(got[s]) <= len(fr[s][0])      # the bound the contract rests on
         assert np.array_equal(nid_a, nid_b), (name, f)
     assert nid_a.sum() > 0
+
+
+def test_pinned_caller_buffers_match_pageable():
+    """Page-locked caller buffers (a pinned tensor's NumPy view) are DMA'd directly, without the
+    staging copy (bytetrack.hip host_pinned): frame by frame the rows, offsets and IDs equal those
+    of the same frames passed in pageable buffers."""
+    import torch
+    S, N = 5, 300
+    streams = [make_frames(N, 8, 700 + s) for s in range(S)]
+    a = ByteTrackEngine(S, track_thresh=0.5, match_thresh=0.8, track_buffer=30, frame_rate=30,
+                        track_capacity=3 * N, max_dets=N)
+    b = ByteTrackEngine(S, track_thresh=0.5, match_thresh=0.8, track_buffer=30, frame_rate=30,
+                        track_capacity=3 * N, max_dets=N)
+    most = max(sum(len(streams[s][f][0]) for s in range(S)) for f in range(8))
+    pin_in = torch.empty((most, 6), dtype=torch.float64, pin_memory=True).numpy()
+    pin_out = torch.empty((most, 8), dtype=torch.float64, pin_memory=True).numpy()
+    off = np.zeros(S + 1, np.int32)
+    out_off = np.zeros(S + 1, np.int32)
+    nid_a, nid_b = np.zeros(S, np.int64), np.zeros(S, np.int64)
+    for f in range(8):
+        dets = [streams[s][f][0] for s in range(S)]
+        ref = a.update(dets, next_id=nid_a)
+        np.cumsum([len(d) for d in dets], out=off[1:])
+        pin_in[:off[-1]] = np.concatenate(dets)
+        _lib.check(b.lib.yta_bytetrack_update(b.handle, _lib.ptr(pin_in), _lib.ptr(off),
+                                              _lib.ptr(nid_b), _lib.ptr(pin_out), len(pin_out),
+                                              _lib.ptr(out_off)))
+        got = [pin_out[out_off[s]:out_off[s + 1]] for s in range(S)]
+        assert np.array_equal(nid_a, nid_b), f
+        for s in range(S):
+            assert np.array_equal(got[s], ref[s]), (f, s)
