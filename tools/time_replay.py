@@ -35,6 +35,14 @@ x, _ = _lib.lap_padded(c)   # warm-up (module load, allocation)
 t0 = time.perf_counter()
 x, _ = _lib.lap_padded(c)
 t_gpu = time.perf_counter() - t0
+if os.environ.get("YTA_STAMPS_READ"):   # diagnostic library: phase split of the last solve
+    import ctypes
+    st = np.zeros(128, np.uint64)
+    fn = _lib.load_library().yta_kat_debug_stamps
+    fn.argtypes = [ctypes.c_void_p]
+    _lib.check(fn(st.ctypes.data))
+    print(f"phases 1-2 {(int(st[61]) - int(st[60])) / 100:.0f} us, phase 3 "
+          f"{(int(st[62]) - int(st[61])) / 100:.0f} us (100 MHz stamps)", flush=True)
 same = np.array_equal(np.where(np.asarray(x) < args.nb, x, -1), np.where(x_ref < args.nb, x_ref, -1))
 print(f"replay {t_gpu * 1e3:.1f} ms on the device, oracle/lapjv.c {t_cpu * 1e3:.1f} ms on one core, "
       f"assignments equal: {same}", flush=True)

@@ -8,6 +8,7 @@
 #include "grid.hpp"
 #include "kf_xyah.hpp"
 #include "lap_dense.hpp"
+#include "lap_dense_block.hpp"
 #include "lap_rect.hpp"
 
 using namespace yta;
@@ -115,20 +116,23 @@ __global__ __launch_bounds__(1024) void k_lap_dense(const double *cost, int nr, 
         atomicOr(err, ERR_EDGE_OVERFLOW);
 }
 
-// One wave: the padded dense solve of association.py:20-28 (lapjv(cost, extend_cost=True)),
-// work arrays placed as the engines place them (lap_dense_placed) within `lds_bytes` of LDS.
-constexpr long long LAP_PADDED_LDS = 156 * 1024;   // the first-round kernels' LDS cap
-__global__ __launch_bounds__(64) void k_lap_padded(const double *cost, int nr, int nc, int *X,
-                                                   int *Y, int *err, unsigned char *gws,
-                                                   long long lds_bytes) {
+// The padded dense solve of association.py:20-28 (lapjv(cost, extend_cost=True)) as the engines
+// run it (padded_lap: one 512-thread block, phases 1-2 on wave 0, phase 3 block-wide for large n,
+// work arrays placed within `lds_bytes` of LDS).
+constexpr long long LAP_PADDED_LDS = 152 * 1024;   // the first-round kernels' LDS cap (LAP_LDS_MAX)
+constexpr int LAP_PADDED_T = 512;
+__global__ __launch_bounds__(LAP_PADDED_T) void k_lap_padded(const double *cost, int nr, int nc,
+                                                             int *X, int *Y, int *err,
+                                                             unsigned char *gws,
+                                                             long long lds_bytes) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int n = nr > nc ? nr : nc;
     const LapMat M{cost, nr, nc, false};
     DenseLapWs w;
-    const int rc = lap_dense_placed(n, M, smem, lds_bytes, gws, w);
-    if (rc && lane_id() == 0) atomicOr(err, ERR_SOLVER);
-    for (int r = lane_id(); r < nr; r += WAVE) X[r] = w.x[r] < nc ? w.x[r] : -1;
-    for (int k = lane_id(); k < nc; k += WAVE) Y[k] = w.y[k] < nr ? w.y[k] : -1;
+    const int rc = lap_dense_block(n, M, smem, lds_bytes, gws, w);
+    if (rc && threadIdx.x == 0) atomicOr(err, ERR_SOLVER);
+    for (int r = threadIdx.x; r < nr; r += blockDim.x) X[r] = w.x[r] < nc ? w.x[r] : -1;
+    for (int k = threadIdx.x; k < nc; k += blockDim.x) Y[k] = w.y[k] < nr ? w.y[k] : -1;
 }
 
 // Rectangular solver KAT (lap_rect.hpp): rows <= cols solved as given with the chip-wide row
@@ -492,8 +496,8 @@ int yta_lap_padded(int device, int nr, int nc, const double *cost, int *x, int *
                                                                            : 0;
     YTA_HIP(hipFuncSetAttribute((const void *)k_lap_padded,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)LAP_PADDED_LDS));
-    hipLaunchKernelGGL(k_lap_padded, dim3(1), dim3(64), (size_t)lds, 0, dcost, nr, nc, dx, dy, derr,
-                       gws, lds);
+    hipLaunchKernelGGL(k_lap_padded, dim3(1), dim3(LAP_PADDED_T), (size_t)lds, 0, dcost, nr, nc, dx,
+                       dy, derr, gws, lds);
     YTA_HIP(hipGetLastError());
     int herr = 0;
     if (nr) YTA_HIP(hipMemcpy(x, dx, sizeof(int) * nr, hipMemcpyDeviceToHost));
@@ -593,3 +597,12 @@ int yta_aw_max_metric(int device, const double *emb_cost, int nr, int nc, double
 }
 
 }  // extern "C"
+
+#ifdef YTA_STAMPS
+// diagnostic build only: this file's stamps (the KATs' solver phases)
+extern "C" int yta_kat_debug_stamps(unsigned long long *out) {
+    YTA_HIP(hipDeviceSynchronize());
+    YTA_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), 128 * sizeof(unsigned long long)));
+    return YTA_OK;
+}
+#endif

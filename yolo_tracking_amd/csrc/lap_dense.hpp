@@ -346,7 +346,9 @@ __device__ __forceinline__ int relax_reg(int n, int &shi, int r, double h, doubl
 // LDS_WS: the work arrays of `w` are in LDS.
 // ROW_LDS: the two row buffers are in LDS too (else in global memory, the other arrays in LDS
 // when LDS_WS).
-template <bool LDS_WS, bool ROW_LDS, int LAP_PF>
+// P3 = false: stop after phase 2 and return the number of free rows left (w.free_rows), for a
+// block-wide phase 3 (lap_dense_block.hpp).
+template <bool LDS_WS, bool ROW_LDS, int LAP_PF, bool P3 = true>
 __device__ __noinline__ int lap_dense_wave_pf(int n, const LapMat M, const DenseLapWs w) {
     const int lane = lane_id();
     auto x = ws_ptr<LDS_WS>(w.x), y = ws_ptr<LDS_WS>(w.y), fr = ws_ptr<LDS_WS>(w.free_rows);
@@ -509,6 +511,7 @@ __device__ __noinline__ int lap_dense_wave_pf(int n, const LapMat M, const Dense
         nfree = out;
     }
     YTA_STAMP(22);
+    if (!P3) return nfree;
     // ---------------- phase 3: shortest augmenting paths ----------------
 #ifdef YTA_STAMPS
     unsigned long long acc_store = 0, acc_relax = 0, acc_gather = 0, acc_init = 0;
@@ -719,10 +722,10 @@ __device__ __noinline__ int lap_dense_wave_pf(int n, const LapMat M, const Dense
 }
 
 // Dispatch on the problem size: 8 registers per lane up to n = 512, 24 beyond.
-template <bool LDS_WS, bool ROW_LDS = LDS_WS>
+template <bool LDS_WS, bool ROW_LDS = LDS_WS, bool P3 = true>
 __device__ __forceinline__ int lap_dense_wave(int n, const LapMat M, const DenseLapWs w) {
-    if (n <= WAVE * 8) return lap_dense_wave_pf<LDS_WS, ROW_LDS, 8>(n, M, w);
-    return lap_dense_wave_pf<LDS_WS, ROW_LDS, LAP_PF_MAX>(n, M, w);
+    if (n <= WAVE * 8) return lap_dense_wave_pf<LDS_WS, ROW_LDS, 8, P3>(n, M, w);
+    return lap_dense_wave_pf<LDS_WS, ROW_LDS, LAP_PF_MAX, P3>(n, M, w);
 }
 
 }  // namespace yta

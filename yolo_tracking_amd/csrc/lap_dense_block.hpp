@@ -1,0 +1,324 @@
+// Phase 3 of the lapjv replay (shortest augmenting paths, oracle/lapjv.c shortest_path /
+// gather_min / relax_scan) run by a whole block instead of one wave, with the same operation and
+// tie-breaking sequence.  Phases 1-2 (column reduction, reduction transfer, augmenting row
+// reduction) stay on wave 0 (lap_dense.hpp, P3 = false); a large replay (a crowd surge under
+// GIoU) spends its time here, in row scans over every remaining column.
+//
+// relax_scan: a row's sweep over the positions [hi, n) visits each position once in position
+// order and stops at the first free column reached at the current minimum; its distance updates
+// touch distinct columns, and its hits (columns reached at the minimum) are swapped to the front
+// in position order.  So the block evaluates every position at once: the first free hit is a
+// block minimum of positions, the updates up to it are independent, and thread 0 replays the
+// hits' swaps from a position bitmap in order.  gather_min: a position qualifies when its
+// distance is <= the running minimum of the earlier ones; a block prefix-minimum over contiguous
+// position ranges marks them, and thread 0 replays their swaps (with the resets) in order.
+#pragma once
+#include "lap_dense.hpp"
+
+namespace yta {
+
+constexpr int LAPB_MAX_N = 8192;    // positions covered by the sweep bitmap (1 KiB of LDS)
+constexpr int LAPB_MIN_N = 768;     // below this the one-wave replay is as fast
+
+struct LapBShared {
+    unsigned bits[LAPB_MAX_N / 32];
+    int wrank[LAPB_MAX_N / 32];   // exclusive prefix of the bitmap words' popcounts
+    int wsum[32];
+    double red[32];
+    int lo, hi, end, ready;
+};
+
+// lapjv.c's swap-to-front (for each marked position p, ascending: swap(cols[p], cols[h]); ++h,
+// from h = h0) done by the block.  The result in closed form: the marked elements land at h0,
+// h0 + 1, ... in position order; the unmarked elements of the window [h0, h0 + m) move, in
+// position order, to the marked positions beyond the window (in order); nothing else moves.
+// bits: the marks over positions [h0, h0 + 32 nwords) (nwords <= blockDim.x).  hitpos (n ints)
+// and tmp (2 n ints) are scratch.  Returns m.
+template <typename IP, typename HP, typename TP>
+__device__ int lapb_swap_front(int h0, int nwords, IP cols, HP hitpos, TP tmp, LapBShared &sh) {
+    const int t = threadIdx.x, nt = blockDim.x;
+    const unsigned wbits = t < nwords ? sh.bits[t] : 0u;
+    int m = 0;
+    const int wr = block_exclusive_scan(__popc(wbits), sh.wsum, &m);
+    if (t < nwords) sh.wrank[t] = wr;
+    {
+        unsigned b = wbits;
+        int r = wr;
+        while (b) {
+            hitpos[r++] = h0 + t * 32 + __builtin_ctz(b);
+            b &= b - 1u;
+        }
+    }
+    block_sync();
+    if (m == 0) return 0;
+    auto rank_before = [&](int q) -> int {   // marked positions in [h0, q)
+        const int o = q - h0, wi = o >> 5;
+        if (wi >= nwords) return m;
+        return sh.wrank[wi] + (int)__popc(sh.bits[wi] & ((1u << (o & 31)) - 1u));
+    };
+    const int k = rank_before(h0 + m);   // marked positions inside the window
+    for (int i = t; i < m; i += nt) tmp[i] = cols[hitpos[i]];
+    for (int q = h0 + t; q < h0 + m; q += nt) {
+        const int o = q - h0;
+        const bool marked = (o >> 5) < nwords && ((sh.bits[o >> 5] >> (o & 31)) & 1u);
+        if (!marked) tmp[m + (o - rank_before(q))] = cols[q];
+    }
+    block_sync();
+    for (int i = t; i < m; i += nt) cols[h0 + i] = tmp[i];
+    for (int r = t; r < m - k; r += nt) cols[hitpos[k + r]] = tmp[m + r];
+    block_sync();
+    return m;
+}
+
+// block-uniform minimum / maximum of a double (all threads get it); `red` holds one slot per wave
+__device__ __forceinline__ double lapb_reduce(bool is_min, double v, double *red) {
+    v = wave_reduce(is_min ? RED_MIN : RED_MAX, v);
+    const int nw = blockDim.x / WAVE, wv = threadIdx.x / WAVE;
+    if (lane_id() == 0) red[wv] = v;
+    block_sync();
+    double r = red[0];
+    for (int k = 1; k < nw; ++k) r = is_min ? (red[k] < r ? red[k] : r) : (red[k] > r ? red[k] : r);
+    block_sync();
+    return r;
+}
+
+// relax_scan (lapjv.c) by the block.  Returns a free column reached at the minimum distance
+// (lo / hi left as they were, as the C code's early return leaves *plo / *phi), or -1 with
+// lo / hi advanced.
+template <typename DP, typename IP, typename HP, typename TP>
+__device__ int lapb_relax_scan(int n, const LapMat &M, int &lo, int &hi, DP d, DP v, IP cols,
+                               IP pred, IP y, HP hitpos, TP tmp, LapBShared &sh) {
+    const int t = threadIdx.x, nt = blockDim.x;
+    int l = lo, h = hi;
+    while (l != h) {
+        const int k = cols[l++];
+        const int r = y[k];
+        const double dk = d[k];
+        const double hh = M.at(r, k) - v[k] - dk;
+        const int base = h, cnt = n - h;
+        for (int q = t; q < (cnt + 31) / 32; q += nt) sh.bits[q] = 0u;
+        // the first free column reached at the minimum (in position order)
+        int my_fin = INT_MAX;
+        for (int p = base + t; p < n; p += nt) {
+            const int kk = cols[p];
+            const double nd = M.at(r, kk) - v[kk] - hh;
+            if (nd < d[kk] && nd == dk && y[kk] < 0) {
+                my_fin = p;
+                break;
+            }
+        }
+        const double ff = lapb_reduce(true, my_fin == INT_MAX ? 1e300 : (double)my_fin, sh.red);
+        const int ffin = ff >= 1e300 ? INT_MAX : (int)ff;
+        // every position up to it is visited: distance updates, hits into the bitmap
+        for (int p = base + t; p < n && p <= ffin; p += nt) {
+            const int kk = cols[p];
+            const double nd = M.at(r, kk) - v[kk] - hh;
+            if (nd < d[kk]) {
+                d[kk] = nd;
+                pred[kk] = r;
+                if (nd == dk && p < ffin)
+                    atomicOr(&sh.bits[(p - base) >> 5], 1u << ((p - base) & 31));
+            }
+        }
+        block_sync();
+        const int last = ffin < n ? ffin - base : cnt;
+        h += lapb_swap_front(base, (last + 31) / 32, cols, hitpos, tmp, sh);
+        const int end = ffin < n ? cols[ffin] : -1;   // ffin is beyond every moved position
+        if (end >= 0) return end;
+    }
+    lo = l;
+    hi = h;
+    return -1;
+}
+
+// gather_min (lapjv.c) by the block: returns the new hi.  A position qualifies when its distance
+// is <= the running minimum of the earlier ones (starting from m0 = d[cols[lo]]); a strictly
+// smaller one resets the front.  With m* the minimum over [lo, n): if m0 == m*, the qualifying
+// positions are exactly the ties to m0 and the whole gather is one swap-to-front from lo + 1;
+// otherwise the qualifying positions before the first occurrence q* of m* are replayed in order
+// by thread 0 (with their resets), then q* and the later ties to m* are one swap-to-front from lo.
+template <typename DP, typename IP, typename HP, typename TP>
+__device__ int lapb_gather_min(int n, int lo, DP d, IP cols, HP hitpos, TP tmp, LapBShared &sh) {
+    const int t = threadIdx.x, nt = blockDim.x, lane = lane_id(), wv = t / WAVE;
+    const double m0 = d[cols[lo]];
+    const int first = lo + 1, cnt = n - first;
+    double lmin = LAP_BIG;
+    for (int q = first + t; q < n; q += nt) {
+        const double e = d[cols[q]];
+        lmin = e < lmin ? e : lmin;
+    }
+    const double gmin = lapb_reduce(true, lmin, sh.red);
+    if (!(gmin < m0)) {   // no reset: the ties to m0, one swap-to-front from lo + 1
+        for (int q = t; q < (cnt + 31) / 32; q += nt) sh.bits[q] = 0u;
+        block_sync();
+        for (int q = first + t; q < n; q += nt)
+            if (d[cols[q]] == m0) atomicOr(&sh.bits[(q - first) >> 5], 1u << ((q - first) & 31));
+        block_sync();
+        return first + lapb_swap_front(first, (cnt + 31) / 32, cols, hitpos, tmp, sh);
+    }
+    // q*: the first position holding the minimum
+    double fq = 1e300;
+    for (int q = first + t; q < n; q += nt)
+        if (d[cols[q]] == gmin) {
+            fq = (double)q;
+            break;
+        }
+    const int qs = (int)lapb_reduce(true, fq, sh.red);
+    // the qualifying positions in (lo, q*): prefix minima over contiguous ranges
+    const int pc = qs - first;
+    const int per = (pc + nt - 1) / nt;
+    const int a = first + t * per, b = min(qs, a + per);
+    double rmin = LAP_BIG;
+    for (int q = a; q < b; ++q) {
+        const double e = d[cols[q]];
+        rmin = e < rmin ? e : rmin;
+    }
+    for (int q = t; q < (cnt + 31) / 32; q += nt) sh.bits[q] = 0u;
+    const double incl = wave_incl_min(rmin);
+    double excl = __shfl_up(incl, 1);
+    if (lane == 0) excl = LAP_BIG;
+    if (lane == WAVE - 1) sh.red[wv] = incl;
+    block_sync();
+    for (int k = 0; k < wv; ++k) excl = sh.red[k] < excl ? sh.red[k] : excl;
+    double run = m0 < excl ? m0 : excl;
+    for (int q = a; q < b; ++q) {
+        const double e = d[cols[q]];
+        if (e <= run) {
+            atomicOr(&sh.bits[(q - first) >> 5], 1u << ((q - first) & 31));
+            run = e < run ? e : run;
+        }
+    }
+    block_sync();
+    if (t == 0) {   // their swaps (and resets) in position order
+        int hi = lo + 1;
+        double m = m0;
+        for (int q = 0; q < (pc + 31) / 32; ++q) {
+            unsigned bb = sh.bits[q];
+            while (bb) {
+                const int p = first + q * 32 + __builtin_ctz(bb);
+                bb &= bb - 1u;
+                const int k = cols[p];
+                const double e = d[k];
+                if (e < m) {
+                    hi = lo;
+                    m = e;
+                }
+                cols[p] = cols[hi];
+                cols[hi] = k;
+                ++hi;
+            }
+        }
+    }
+    block_sync();
+    // the reset at q* and the ties after it: one swap-to-front from lo
+    const int cnt2 = n - lo;
+    for (int q = t; q < (cnt2 + 31) / 32; q += nt) sh.bits[q] = 0u;
+    block_sync();
+    for (int q = qs + t; q < n; q += nt)
+        if (d[cols[q]] == gmin) atomicOr(&sh.bits[(q - lo) >> 5], 1u << ((q - lo) & 31));
+    block_sync();
+    return lo + lapb_swap_front(lo, (cnt2 + 31) / 32, cols, hitpos, tmp, sh);
+}
+
+// Phase 3 for the free rows w.free_rows[0 .. nfree) left by phases 1-2 (all threads of the block).
+// Returns 0, or -2 when an augmenting path does not close.
+template <bool LDS_WS>
+__device__ int lap_dense_block_p3(int n, const LapMat M, const DenseLapWs w, int nfree) {
+    __shared__ LapBShared sh;
+    const int t = threadIdx.x, nt = blockDim.x;
+    auto x = ws_ptr<LDS_WS>(w.x), y = ws_ptr<LDS_WS>(w.y), fr = ws_ptr<LDS_WS>(w.free_rows);
+    auto cols = ws_ptr<LDS_WS>(w.cols), pred = ws_ptr<LDS_WS>(w.pred);
+    auto v = ws_ptr<LDS_WS>(w.v), d = ws_ptr<LDS_WS>(w.d);
+    // scratch of the swap-to-front: aux (n ints) and the unused row buffers (2 n doubles)
+    auto hitpos = ws_ptr<LDS_WS>(w.aux);
+    int *tmp = reinterpret_cast<int *>(w.row);
+    for (int f = 0; f < nfree; ++f) {
+        const int src = fr[f];
+        for (int k = t; k < n; k += nt) {
+            cols[k] = k;
+            pred[k] = src;
+            d[k] = M.at(src, k) - v[k];
+        }
+        block_sync();
+        int lo = 0, hi = 0, ready = 0, end = -1;
+        while (end < 0) {
+            if (lo == hi) {
+                ready = lo;
+                hi = lapb_gather_min(n, lo, d, cols, hitpos, tmp, sh);
+                // the last free column of the gathered set
+                double e = -1.0;
+                for (int q = lo + t; q < hi; q += nt)
+                    if (y[cols[q]] < 0) e = (double)q;
+                e = lapb_reduce(false, e, sh.red);
+                if (e >= 0.0) end = cols[(int)e];
+            }
+            if (end < 0) end = lapb_relax_scan(n, M, lo, hi, d, v, cols, pred, y, hitpos, tmp, sh);
+        }
+        const double m = d[cols[lo]];
+        for (int q = t; q < ready; q += nt) {
+            const int k = cols[q];
+            v[k] += d[k] - m;
+        }
+        block_sync();
+        if (t == 0) {   // flip the alternating path back to the source row
+            int k = end, r = -1, steps = 0;
+            sh.end = 0;
+            while (r != src) {
+                r = pred[k];
+                y[k] = r;
+                const int prev = x[r];
+                x[r] = k;
+                k = prev;
+                if (++steps > n) {
+                    sh.end = -2;
+                    break;
+                }
+            }
+        }
+        block_sync();
+        if (sh.end == -2) return -2;
+        block_sync();
+    }
+    return 0;
+}
+
+// The whole replay on a block: phases 1-2 on wave 0, phase 3 block-wide when n is large enough,
+// work arrays in LDS (without the row buffers, which phase 3 does not use) when they fit.  Every
+// thread of the block calls it; `w` receives the layout (w.x: the assignment).  Returns the
+// solver's rc (0 on success).
+__device__ __forceinline__ int lap_dense_block(int n, const LapMat M, unsigned char *lds,
+                                               long long lds_bytes, unsigned char *gws,
+                                               DenseLapWs &w) {
+    __shared__ int s_rc;
+    if (n < LAPB_MIN_N || n > LAPB_MAX_N || blockDim.x < 256) {
+        if (threadIdx.x < WAVE) {
+            const int rc = lap_dense_placed(n, M, lds, lds_bytes, gws, w);
+            if (lane_id() == 0) s_rc = rc;
+        } else {   // the layout lap_dense_placed picks, for the other threads' reads of w.x
+            w = dense_lap_ws_bytes(n) <= lds_bytes ? dense_lap_ws(lds, n)
+                : dense_lap_ws_bytes_norow(n) <= lds_bytes ? dense_lap_ws_split(lds, gws, n)
+                                                           : dense_lap_ws(gws, n);
+        }
+        block_sync();
+        return s_rc;
+    }
+    const bool in_lds = dense_lap_ws_bytes_norow(n) <= lds_bytes;
+    w = in_lds ? dense_lap_ws_split(lds, gws, n) : dense_lap_ws(gws, n);
+    YTA_STAMP_ABS(60);
+    if (threadIdx.x < WAVE) {
+        const int nf = in_lds ? lap_dense_wave<true, false, false>(n, M, w)
+                              : lap_dense_wave<false, false, false>(n, M, w);
+        if (lane_id() == 0) s_rc = nf;
+    }
+    block_sync();
+    const int nfree = s_rc;
+    block_sync();
+    YTA_STAMP_ABS(61);
+    if (nfree < 0) return nfree;
+    const int rc = in_lds ? lap_dense_block_p3<true>(n, M, w, nfree)
+                          : lap_dense_block_p3<false>(n, M, w, nfree);
+    YTA_STAMP_ABS(62);
+    return rc;
+}
+
+}  // namespace yta

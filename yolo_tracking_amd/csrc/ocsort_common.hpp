@@ -5,6 +5,7 @@
 #include "geometry.hpp"
 #include "lap.hpp"
 #include "lap_dense.hpp"
+#include "lap_dense_block.hpp"
 #include "lap_rect.hpp"
 
 namespace yta {
@@ -71,11 +72,11 @@ __device__ __forceinline__ void padded_lap(const LapMat &M, int *rx, unsigned ch
         if (acc == 1.2345e300) rx[0] = -7;   // keeps the loads; never true for cost matrices
         block_sync();
     }
-    if (threadIdx.x < WAVE && n > 0) {
+    if (n > 0) {   // the whole block (phase 3 block-wide for large n, lap_dense_block.hpp)
         DenseLapWs w;
-        const int rc = lap_dense_placed(n, M, lds, lds_bytes, gws, w);
-        if (rc && lane_id() == 0) atomicOr(err, ERR_SOLVER);
-        for (int r = lane_id(); r < M.na; r += WAVE) rx[r] = w.x[r] < M.nb ? w.x[r] : -1;
+        const int rc = lap_dense_block(n, M, lds, lds_bytes, gws, w);
+        if (rc && threadIdx.x == 0) atomicOr(err, ERR_SOLVER);
+        for (int r = threadIdx.x; r < M.na; r += blockDim.x) rx[r] = w.x[r] < M.nb ? w.x[r] : -1;
     }
     block_sync();
 }
@@ -84,7 +85,7 @@ __device__ __forceinline__ void padded_lap(const LapMat &M, int *rx, unsigned ch
 #define YTA_LAP_T 512
 #endif
 constexpr int LAP_T = YTA_LAP_T;                // threads of the first-round solve kernels
-constexpr long long LAP_LDS_MAX = 156 * 1024;   // their dynamic LDS cap (160 KiB - static)
+constexpr long long LAP_LDS_MAX = 152 * 1024;   // their dynamic LDS cap (160 KiB - static)
 
 // The first-round solve's work arrays, either orientation (first_round_lap transposes the
 // problem when detections outnumber trackers).
