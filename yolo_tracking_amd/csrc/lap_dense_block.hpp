@@ -20,11 +20,26 @@ namespace yta {
 constexpr int LAPB_MAX_N = 8192;    // positions covered by the sweep bitmap (1 KiB of LDS)
 constexpr int LAPB_MIN_N = 768;     // below this the one-wave replay is as fast
 
+#ifdef YTA_STAMPS
+// diagnostic build: block 0 thread 0 accumulates ticks / counts into g_stamps[k]
+#define LAPB_ADD(k, v)                                                         \
+    do {                                                                       \
+        if (blockIdx.x == 0 && threadIdx.x == 0) g_stamps[(k)] += (v);          \
+    } while (0)
+#define LAPB_T0() const unsigned long long lapb_t0 = wall_clock64()
+#define LAPB_DT(k) LAPB_ADD(k, wall_clock64() - lapb_t0)
+#else
+#define LAPB_ADD(k, v) do { } while (0)
+#define LAPB_T0() do { } while (0)
+#define LAPB_DT(k) do { } while (0)
+#endif
+
 struct LapBShared {
     unsigned bits[LAPB_MAX_N / 32];
     int wrank[LAPB_MAX_N / 32];   // exclusive prefix of the bitmap words' popcounts
     int wsum[32];
-    double red[32];
+    double red[2][32];            // alternating reduction slots (one barrier per reduction)
+    double pre[32];               // gather_min's per-wave prefix minima
     int lo, hi, end, ready;
 };
 
@@ -37,9 +52,11 @@ struct LapBShared {
 template <typename IP, typename HP, typename TP>
 __device__ int lapb_swap_front(int h0, int nwords, IP cols, HP hitpos, TP tmp, LapBShared &sh) {
     const int t = threadIdx.x, nt = blockDim.x;
+    LAPB_T0();
     const unsigned wbits = t < nwords ? sh.bits[t] : 0u;
     int m = 0;
     const int wr = block_exclusive_scan(__popc(wbits), sh.wsum, &m);
+    if (m == 0) return 0;   // (every thread read its bitmap word before the scan's barriers)
     if (t < nwords) sh.wrank[t] = wr;
     {
         unsigned b = wbits;
@@ -50,7 +67,6 @@ __device__ int lapb_swap_front(int h0, int nwords, IP cols, HP hitpos, TP tmp, L
         }
     }
     block_sync();
-    if (m == 0) return 0;
     auto rank_before = [&](int q) -> int {   // marked positions in [h0, q)
         const int o = q - h0, wi = o >> 5;
         if (wi >= nwords) return m;
@@ -67,18 +83,23 @@ __device__ int lapb_swap_front(int h0, int nwords, IP cols, HP hitpos, TP tmp, L
     for (int i = t; i < m; i += nt) cols[h0 + i] = tmp[i];
     for (int r = t; r < m - k; r += nt) cols[hitpos[k + r]] = tmp[m + r];
     block_sync();
+    LAPB_DT(66);
+    LAPB_ADD(67, m);
     return m;
 }
 
-// block-uniform minimum / maximum of a double (all threads get it); `red` holds one slot per wave
-__device__ __forceinline__ double lapb_reduce(bool is_min, double v, double *red) {
+// block-uniform minimum / maximum of a double (all threads get it).  The slots alternate between
+// calls (par: block-uniform, a register of every thread), so one barrier suffices: a slot is
+// rewritten two reductions later, after the other reduction's barrier.
+__device__ __forceinline__ double lapb_reduce(bool is_min, double v, LapBShared &sh, int &par) {
     v = wave_reduce(is_min ? RED_MIN : RED_MAX, v);
     const int nw = blockDim.x / WAVE, wv = threadIdx.x / WAVE;
+    double *red = sh.red[par];
+    par ^= 1;
     if (lane_id() == 0) red[wv] = v;
     block_sync();
     double r = red[0];
     for (int k = 1; k < nw; ++k) r = is_min ? (red[k] < r ? red[k] : r) : (red[k] > r ? red[k] : r);
-    block_sync();
     return r;
 }
 
@@ -87,10 +108,12 @@ __device__ __forceinline__ double lapb_reduce(bool is_min, double v, double *red
 // lo / hi advanced.
 template <typename DP, typename IP, typename HP, typename TP>
 __device__ int lapb_relax_scan(int n, const LapMat &M, int &lo, int &hi, DP d, DP v, IP cols,
-                               IP pred, IP y, HP hitpos, TP tmp, LapBShared &sh) {
+                               IP pred, IP y, HP hitpos, TP tmp, LapBShared &sh, int &par) {
     const int t = threadIdx.x, nt = blockDim.x;
     int l = lo, h = hi;
     while (l != h) {
+        LAPB_ADD(63, 1);
+        LAPB_T0();
         const int k = cols[l++];
         const int r = y[k];
         const double dk = d[k];
@@ -107,7 +130,7 @@ __device__ int lapb_relax_scan(int n, const LapMat &M, int &lo, int &hi, DP d, D
                 break;
             }
         }
-        const double ff = lapb_reduce(true, my_fin == INT_MAX ? 1e300 : (double)my_fin, sh.red);
+        const double ff = lapb_reduce(true, my_fin == INT_MAX ? 1e300 : (double)my_fin, sh, par);
         const int ffin = ff >= 1e300 ? INT_MAX : (int)ff;
         // every position up to it is visited: distance updates, hits into the bitmap
         for (int p = base + t; p < n && p <= ffin; p += nt) {
@@ -124,6 +147,7 @@ __device__ int lapb_relax_scan(int n, const LapMat &M, int &lo, int &hi, DP d, D
         const int last = ffin < n ? ffin - base : cnt;
         h += lapb_swap_front(base, (last + 31) / 32, cols, hitpos, tmp, sh);
         const int end = ffin < n ? cols[ffin] : -1;   // ffin is beyond every moved position
+        LAPB_DT(64);
         if (end >= 0) return end;
     }
     lo = l;
@@ -138,8 +162,10 @@ __device__ int lapb_relax_scan(int n, const LapMat &M, int &lo, int &hi, DP d, D
 // otherwise the qualifying positions before the first occurrence q* of m* are replayed in order
 // by thread 0 (with their resets), then q* and the later ties to m* are one swap-to-front from lo.
 template <typename DP, typename IP, typename HP, typename TP>
-__device__ int lapb_gather_min(int n, int lo, DP d, IP cols, HP hitpos, TP tmp, LapBShared &sh) {
+__device__ int lapb_gather_min(int n, int lo, DP d, IP cols, HP hitpos, TP tmp, LapBShared &sh,
+                               int &par) {
     const int t = threadIdx.x, nt = blockDim.x, lane = lane_id(), wv = t / WAVE;
+    LAPB_ADD(65, 1);
     const double m0 = d[cols[lo]];
     const int first = lo + 1, cnt = n - first;
     double lmin = LAP_BIG;
@@ -147,7 +173,7 @@ __device__ int lapb_gather_min(int n, int lo, DP d, IP cols, HP hitpos, TP tmp, 
         const double e = d[cols[q]];
         lmin = e < lmin ? e : lmin;
     }
-    const double gmin = lapb_reduce(true, lmin, sh.red);
+    const double gmin = lapb_reduce(true, lmin, sh, par);
     if (!(gmin < m0)) {   // no reset: the ties to m0, one swap-to-front from lo + 1
         for (int q = t; q < (cnt + 31) / 32; q += nt) sh.bits[q] = 0u;
         block_sync();
@@ -163,7 +189,7 @@ __device__ int lapb_gather_min(int n, int lo, DP d, IP cols, HP hitpos, TP tmp, 
             fq = (double)q;
             break;
         }
-    const int qs = (int)lapb_reduce(true, fq, sh.red);
+    const int qs = (int)lapb_reduce(true, fq, sh, par);
     // the qualifying positions in (lo, q*): prefix minima over contiguous ranges
     const int pc = qs - first;
     const int per = (pc + nt - 1) / nt;
@@ -177,9 +203,9 @@ __device__ int lapb_gather_min(int n, int lo, DP d, IP cols, HP hitpos, TP tmp, 
     const double incl = wave_incl_min(rmin);
     double excl = __shfl_up(incl, 1);
     if (lane == 0) excl = LAP_BIG;
-    if (lane == WAVE - 1) sh.red[wv] = incl;
+    if (lane == WAVE - 1) sh.pre[wv] = incl;
     block_sync();
-    for (int k = 0; k < wv; ++k) excl = sh.red[k] < excl ? sh.red[k] : excl;
+    for (int k = 0; k < wv; ++k) excl = sh.pre[k] < excl ? sh.pre[k] : excl;
     double run = m0 < excl ? m0 : excl;
     for (int q = a; q < b; ++q) {
         const double e = d[cols[q]];
@@ -232,6 +258,7 @@ __device__ int lap_dense_block_p3(int n, const LapMat M, const DenseLapWs w, int
     // scratch of the swap-to-front: aux (n ints) and the unused row buffers (2 n doubles)
     auto hitpos = ws_ptr<LDS_WS>(w.aux);
     int *tmp = reinterpret_cast<int *>(w.row);
+    int par = 0;
     for (int f = 0; f < nfree; ++f) {
         const int src = fr[f];
         for (int k = t; k < n; k += nt) {
@@ -244,15 +271,15 @@ __device__ int lap_dense_block_p3(int n, const LapMat M, const DenseLapWs w, int
         while (end < 0) {
             if (lo == hi) {
                 ready = lo;
-                hi = lapb_gather_min(n, lo, d, cols, hitpos, tmp, sh);
+                hi = lapb_gather_min(n, lo, d, cols, hitpos, tmp, sh, par);
                 // the last free column of the gathered set
                 double e = -1.0;
                 for (int q = lo + t; q < hi; q += nt)
                     if (y[cols[q]] < 0) e = (double)q;
-                e = lapb_reduce(false, e, sh.red);
+                e = lapb_reduce(false, e, sh, par);
                 if (e >= 0.0) end = cols[(int)e];
             }
-            if (end < 0) end = lapb_relax_scan(n, M, lo, hi, d, v, cols, pred, y, hitpos, tmp, sh);
+            if (end < 0) end = lapb_relax_scan(n, M, lo, hi, d, v, cols, pred, y, hitpos, tmp, sh, par);
         }
         const double m = d[cols[lo]];
         for (int q = t; q < ready; q += nt) {
