@@ -165,3 +165,12 @@ def test_ecc_class_first_frame_scale_and_errors():
     assert np.array_equal(o.prev_img, prev)
     with pytest.raises(NotImplementedError):
         ce.ECCOracle(warp_mode=ce.MOTION_HOMOGRAPHY).apply(frame)
+
+
+def test_uncorrelated_frames_raise():
+    rng = np.random.default_rng(0)
+    a = rng.integers(0, 256, (60, 80), dtype=np.uint8)
+    b = rng.integers(0, 256, (60, 80), dtype=np.uint8)
+    for mode in (0, 1, 2):
+        with pytest.raises(ce.ECCError):
+            ce.find_transform_ecc(a, b, np.eye(2, 3, dtype=np.float32), mode, 100, 1e-5)

@@ -107,3 +107,13 @@ def test_dropin_class_and_growth():
     assert np.array_equal(ecc.apply(big, None), o.apply(big))
     with pytest.raises(NotImplementedError):
         ECC(warp_mode=3)
+
+
+def test_uncorrelated_frames_error_path():
+    """Independent noise frames: the step would minimise the correlation (lambda_d <= 0), where
+    OpenCV raises; identity, prev_img kept - bit-exact with the restatement for every model."""
+    rng = np.random.default_rng(4)
+    fr = [gray_bgr(rng.integers(0, 256, (60, 80), dtype=np.uint8)) for _ in range(4)]
+    inv = gray_bgr(255 - fr[1][..., 0])
+    for mode in (0, 1, 2):
+        run_pair([fr, [fr[0], fr[1], inv, fr[3]]], mode=mode, scale=1.0)
