@@ -168,6 +168,9 @@ def main():
         step(f)
     _lib.check(sync(eng.handle))
     torch.cuda.synchronize()
+    stamps = os.environ.get("YTA_HS_STAMPS") and args.tracker == "hybridsort"
+    if stamps:   # diagnostic library: k_hs_lap's solver phases over the timed frames
+        eng.lib.yta_hs_debug_stamps_reset()
     t0 = time.perf_counter()
     for f in range(args.warmup, F):
         step(f)
@@ -175,6 +178,14 @@ def main():
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     value = S * args.steps / el
+    if stamps:
+        st = np.zeros(128, np.uint64)
+        fnst = eng.lib.yta_hs_debug_stamps
+        fnst.argtypes = [ctypes.c_void_p]
+        _lib.check(fnst(st.ctypes.data))
+        print(f"k_hs_lap (block 0, {args.steps} frames): free rows {int(st[100])}, steps "
+              f"{int(st[101])}, scan {int(st[102]) / 100:.0f} us, reduce {int(st[103]) / 100:.0f} us",
+              file=sys.stderr)
     stats = eng.stats()
     # CPU leg: the oracle on stream 0, 1 thread, bounded sample
     cf = args.cpu_frames if args.cpu_frames is not None else (30 if oc else (2 if fam else 6))

@@ -1404,4 +1404,18 @@ int yta_hybridsort_debug_stamps(unsigned long long *out) {
 }
 #endif
 
+#ifdef YTA_STAMPS
+// diagnostic build only: this file's stamps (k_hs_lap's rectangular solver phases)
+int yta_hs_debug_stamps(unsigned long long *out) {
+    YTA_HIP(hipDeviceSynchronize());
+    YTA_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), 128 * sizeof(unsigned long long)));
+    return YTA_OK;
+}
+int yta_hs_debug_stamps_reset() {
+    unsigned long long z[128] = {};
+    YTA_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), z, sizeof(z)));
+    return YTA_OK;
+}
+#endif
+
 }  // extern "C"
