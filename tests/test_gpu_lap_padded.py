@@ -1,4 +1,4 @@
-"""GPU: the one-wave dense solver (lap_dense.hpp) against the restated lapjv (oracle/lapjv.c) on
+"""GPU: the dense replay solver (lap_dense.hpp, phase 3 block-wide from n = 768 in lap_dense_block.hpp) against the restated lapjv (oracle/lapjv.c) on
 the padded calls of association.py:20-28 — identical x / y (the same operation and tie-breaking
 sequence), including tie-heavy integer matrices where many optima exist."""
 import numpy as np
@@ -46,3 +46,29 @@ def test_lap_padded_large_global_workspace():
     _, xo, yo = lapjv(c, extend_cost=True)
     x, y = _lib.lap_padded(c)
     assert np.array_equal(x, xo) and np.array_equal(y, yo)
+
+
+def _surge(rng, na, nb, per_col):
+    """GIoU-surge-shaped: every pair that does not overlap costs exactly 0."""
+    c = np.zeros((na, nb))
+    for j in range(nb):
+        rows = rng.choice(na, size=per_col, replace=False)
+        c[rows, j] = -rng.random(per_col) * 0.8 - 0.05
+    return c
+
+
+@pytest.mark.parametrize("case", ["ints_900x700", "zeros_1200", "ties_800x1500", "surge_2000x800",
+                                  "surge_4000x500"])
+def test_lap_padded_block_replay_tie_heavy(case):
+    """n >= 768: phase 3 runs block-wide (lap_dense_block.hpp); tie-heavy matrices exercise its
+    swap-to-front and gather resets; 4000 x 500 also puts the work arrays in global memory."""
+    rng = np.random.default_rng(sum(map(ord, case)))
+    c = {"ints_900x700": lambda: rng.integers(0, 4, size=(900, 700)).astype(np.float64),
+         "zeros_1200": lambda: np.zeros((1200, 1200)),
+         "ties_800x1500": lambda: -rng.integers(0, 3, size=(800, 1500)).astype(np.float64),
+         "surge_2000x800": lambda: _surge(rng, 2000, 800, 3),
+         "surge_4000x500": lambda: _surge(rng, 4000, 500, 2)}[case]()
+    _, xo, yo = lapjv(c, extend_cost=True)
+    x, y = _lib.lap_padded(c)
+    assert np.array_equal(x, xo), (case, np.nonzero(x != xo)[0][:10])
+    assert np.array_equal(y, yo), case
