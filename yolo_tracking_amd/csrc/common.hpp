@@ -56,6 +56,23 @@ __device__ __forceinline__ void block_sync() {
     __syncthreads();
 }
 
+// XCD-aware placement of a (gx x gy) tile grid (blockIdx.x: column tiles, blockIdx.y: row tiles,
+// one grid slice per blockIdx.z).  Workgroups are dispatched round-robin over the 8 XCDs, each
+// with its own L2, so launch-order neighbours share nothing.  Instead XCD x (linear id mod 8)
+// takes row band x (gy / 8 row tiles) and walks it column by column: the band's row operands
+// stay in its L2 and each column operand is fetched once per XCD and reused band-rows times.
+// A bijection whenever gy is a multiple of 8; otherwise the launch order is kept.
+__device__ __forceinline__ void xcd_tile(int &bx, int &by) {
+    bx = blockIdx.x;
+    by = blockIdx.y;
+    const int gx = gridDim.x, gy = gridDim.y;
+    if ((gy & 7) == 0) {
+        const int lin = bx + gx * by, xcd = lin & 7, k = lin >> 3, band = gy >> 3;
+        by = xcd * band + k % band;
+        bx = k / band;
+    }
+}
+
 // Diagnostic build only (-DYTA_STAMPS, tools/diag_stamps.py): wall-clock stamps (100 MHz) of
 // block 0's phases, read back with yta_debug_stamps.
 #ifdef YTA_STAMPS

@@ -408,7 +408,9 @@ __global__ __launch_bounds__(256) void k_doc_emb(DocArgs a) {
     const int s = blockIdx.z;
     const DocCounters *c = a.cnt + s;
     const int n_trk = c->n_trk, n_hi = c->n_high, D = a.D;
-    const int r0 = blockIdx.y * EMB_TILE, c0 = blockIdx.x * EMB_TILE;
+    int bx, by;
+    xcd_tile(bx, by);                                         // row bands per XCD (common.hpp)
+    const int r0 = by * EMB_TILE, c0 = bx * EMB_TILE;
     if (r0 >= n_hi || c0 >= n_trk) return;                   // block-uniform
     const long long tb = (long long)s * a.CAP, db = (long long)s * a.MAXD, mb = doc_mb(a, s);
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;

@@ -355,24 +355,40 @@ __global__ __launch_bounds__(OC_T) void k_hs_pre(HsArgs a) {
 // ---------------------------------------------------------------------------------- k_hs_emb
 // 64 (detections) x 64 (trackers) cost tiles per block, 4 waves of 32 x 32 (2 x 2 MFMA tiles of
 // v_mfma_f64_16x16x4_f64: A[l&15][k = l>>4], B[k = l>>4][l&15], D[row (l>>4) + 4 r][col l&15]).
-// The embedding dimension streams through LDS in chunks of 32 (float32 -> float64 on the way),
-// with the row norms accumulated from the same chunks.
+// The embedding dimension streams through LDS in chunks of 32 floats, double-buffered (one
+// barrier per chunk: a chunk is stored into the other buffer while this one's MFMAs run) and
+// widened to float64 as the MFMA operands are read (exact); the row norms accumulate from the
+// same chunks.  Rows are 36 floats apart, so the 16 rows x 4 k of one operand read hit 64
+// distinct banks.  The epilogue's column records reuse the GEMM buffers (LDS 47.6 -> 38 KiB:
+// four blocks per CU), and the association function is a template argument.  Tiles are placed
+// by XCD row bands (xcd_tile): C5 1049 -> 861 us per 4096^2 launch, 7.16 -> 5.65 ms at 8 streams.
 typedef double dbl4 __attribute__((ext_vector_type(4)));
-constexpr int HE_TILE = 64, HE_KC = 32, HE_LD = HE_KC + 1;
+constexpr int HE_TILE = 64, HE_KC = 32, HE_LDF = 36;
 
 struct HsDetCol {                   // per detection row of the tile
     double box[4], score;
 };
 
-__global__ __launch_bounds__(256) void k_hs_emb(HsArgs a) {
-    __shared__ double As[HE_TILE * HE_LD], Bs[HE_TILE * HE_LD];
+union HeLds {
+    struct {
+        float A[2][HE_TILE * HE_LDF], B[2][HE_TILE * HE_LDF];
+    } g;
+    struct {
+        HsDetCol d[HE_TILE];
+        HsCol t[HE_TILE];
+    } c;
+};
+
+template <int ASSO>
+__global__ __launch_bounds__(256, 4) void k_hs_emb(HsArgs a) {
+    __shared__ __attribute__((aligned(16))) HeLds L;
     __shared__ double nA[HE_TILE], nB[HE_TILE];
-    __shared__ HsDetCol dcol[HE_TILE];
-    __shared__ HsCol tcol[HE_TILE];
     const int s = blockIdx.z;
     const HsCounters *c = a.cnt + s;
     const int n_trk = c->n_trk, n_hi = c->n_high, D = a.D;
-    const int r0 = blockIdx.y * HE_TILE, c0 = blockIdx.x * HE_TILE;
+    int bx, by;
+    xcd_tile(bx, by);                                         // row bands per XCD (common.hpp)
+    const int r0 = by * HE_TILE, c0 = bx * HE_TILE;
     if (r0 >= n_hi || c0 >= n_trk) return;                   // block-uniform
     const long long tb = (long long)s * a.CAP, db = (long long)s * a.MAXD, mb = hs_mb(a, s);
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
@@ -391,56 +407,72 @@ __global__ __launch_bounds__(256) void k_hs_emb(HsArgs a) {
         for (int j = 0; j < 2; ++j) acc[i][j] = dbl4{0.0, 0.0, 0.0, 0.0};
     // the next chunk's 8 + 8 floats are loaded into registers while this chunk's MFMAs run
     // (float4 pairs when D is a multiple of the chunk: rows then start 128-B aligned)
-    float pa[8], pb[8];
+    float4 pa[2], pb[2];
     const bool vec = (D % HE_KC) == 0;
     auto fetch = [&](int k0) {
+        const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
         if (vec) {
-            const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
-            const float4 a0 = a_ok ? *reinterpret_cast<const float4 *>(arow + k0 + lk) : z;
-            const float4 a1 = a_ok ? *reinterpret_cast<const float4 *>(arow + k0 + lk + 4) : z;
-            const float4 b0 = b_ok ? *reinterpret_cast<const float4 *>(brow + k0 + lk) : z;
-            const float4 b1 = b_ok ? *reinterpret_cast<const float4 *>(brow + k0 + lk + 4) : z;
-            pa[0] = a0.x; pa[1] = a0.y; pa[2] = a0.z; pa[3] = a0.w;
-            pa[4] = a1.x; pa[5] = a1.y; pa[6] = a1.z; pa[7] = a1.w;
-            pb[0] = b0.x; pb[1] = b0.y; pb[2] = b0.z; pb[3] = b0.w;
-            pb[4] = b1.x; pb[5] = b1.y; pb[6] = b1.z; pb[7] = b1.w;
+            pa[0] = a_ok ? *reinterpret_cast<const float4 *>(arow + k0 + lk) : z;
+            pa[1] = a_ok ? *reinterpret_cast<const float4 *>(arow + k0 + lk + 4) : z;
+            pb[0] = b_ok ? *reinterpret_cast<const float4 *>(brow + k0 + lk) : z;
+            pb[1] = b_ok ? *reinterpret_cast<const float4 *>(brow + k0 + lk + 4) : z;
         } else {
+            float ta[8], tb8[8];
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
                 const int k = k0 + lk + u;
-                pa[u] = (a_ok && k < D) ? arow[k] : 0.f;
-                pb[u] = (b_ok && k < D) ? brow[k] : 0.f;
+                ta[u] = (a_ok && k < D) ? arow[k] : 0.f;
+                tb8[u] = (b_ok && k < D) ? brow[k] : 0.f;
             }
+            pa[0] = make_float4(ta[0], ta[1], ta[2], ta[3]);
+            pa[1] = make_float4(ta[4], ta[5], ta[6], ta[7]);
+            pb[0] = make_float4(tb8[0], tb8[1], tb8[2], tb8[3]);
+            pb[1] = make_float4(tb8[4], tb8[5], tb8[6], tb8[7]);
         }
     };
-    fetch(0);
-    for (int k0 = 0; k0 < D; k0 += HE_KC) {
+    // norms in k order (u = 0..7 of this thread's 8), then the chunk into LDS buffer b
+    auto stash = [&](int b) {
+        const float va[8] = {pa[0].x, pa[0].y, pa[0].z, pa[0].w, pa[1].x, pa[1].y, pa[1].z, pa[1].w};
+        const float vb[8] = {pb[0].x, pb[0].y, pb[0].z, pb[0].w, pb[1].x, pb[1].y, pb[1].z, pb[1].w};
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
-            const double av = (double)pa[u];
-            const double bv = (double)pb[u];
+            const double av = (double)va[u], bv = (double)vb[u];
             qa += av * av;
             qb += bv * bv;
-            As[lr * HE_LD + lk + u] = av;
-            Bs[lr * HE_LD + lk + u] = bv;
         }
-        __syncthreads();
-        if (k0 + HE_KC < D) fetch(k0 + HE_KC);
+        float4 *da = reinterpret_cast<float4 *>(&L.g.A[b][lr * HE_LDF + lk]);
+        float4 *dbp = reinterpret_cast<float4 *>(&L.g.B[b][lr * HE_LDF + lk]);
+        da[0] = pa[0];
+        da[1] = pa[1];
+        dbp[0] = pb[0];
+        dbp[1] = pb[1];
+    };
+    fetch(0);
+    stash(0);
+    __syncthreads();
+    int buf = 0;
+    for (int k0 = 0; k0 < D; k0 += HE_KC) {
+        const bool more = k0 + HE_KC < D;
+        if (more) fetch(k0 + HE_KC);
+        const float *As = L.g.A[buf], *Bs = L.g.B[buf];
 #pragma unroll
         for (int ks = 0; ks < HE_KC; ks += 4) {
             const int kk = ks + (lane >> 4);
             double af[2], bf[2];
 #pragma unroll
-            for (int i = 0; i < 2; ++i) af[i] = As[(wr + 16 * i + (lane & 15)) * HE_LD + kk];
+            for (int i = 0; i < 2; ++i) af[i] = (double)As[(wr + 16 * i + (lane & 15)) * HE_LDF + kk];
 #pragma unroll
-            for (int j = 0; j < 2; ++j) bf[j] = Bs[(wc + 16 * j + (lane & 15)) * HE_LD + kk];
+            for (int j = 0; j < 2; ++j) bf[j] = (double)Bs[(wc + 16 * j + (lane & 15)) * HE_LDF + kk];
 #pragma unroll
             for (int i = 0; i < 2; ++i)
 #pragma unroll
                 for (int j = 0; j < 2; ++j)
                     acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[i], bf[j], acc[i][j], 0, 0, 0);
         }
+        // the other buffer was last read before the previous barrier
+        if (more) stash(buf ^ 1);
         __syncthreads();
+        buf ^= 1;
     }
     // row norms (4 threads per row)
     qa += __shfl_xor(qa, 1);
@@ -451,11 +483,15 @@ __global__ __launch_bounds__(256) void k_hs_emb(HsArgs a) {
         nA[lr] = qa;
         nB[lr] = qb;
     }
+    // column records over the GEMM buffers (every MFMA read is behind the loop's last barrier)
+    HsDetCol *dcol = L.c.d;
+    HsCol *tcol = L.c.t;
     if (t < HE_TILE) {
         const int p = r0 + t;
         if (p < n_hi) {
             const double *dr = a.det_in + ((long long)a.det_off[s] + a.hi_row[db + p]) * 6;
             HsDetCol dc;
+#pragma unroll
             for (int k = 0; k < 4; ++k) dc.box[k] = dr[k];
             dc.score = dr[4];
             dcol[t] = dc;
@@ -488,9 +524,10 @@ __global__ __launch_bounds__(256) void k_hs_emb(HsArgs a) {
                 const HsCol &tc = tcol[lcol];
                 const Box db_{dc.box[0], dc.box[1], dc.box[2], dc.box[3]};
                 const Box tb_{tc.box[0], tc.box[1], tc.box[2], tc.box[3]};
-                const double v = asso_of(a.asso, db_, tb_, 0.0, 0.0);
-                if (a.asso == 1 && v != v) giou_bad = true;
+                const double v = asso_of(ASSO, db_, tb_, 0.0, 0.0);
+                if (ASSO == 1 && v != v) giou_bad = true;
                 double angle = 0.0;
+#pragma unroll
                 for (int cc = 0; cc < 4; ++cc) {
                     const double dx = dc.box[hs_cx(cc)] - tc.kobs[hs_cx(cc)];
                     const double dy = dc.box[hs_cy(cc)] - tc.kobs[hs_cy(cc)];
@@ -971,7 +1008,13 @@ int hs_launch(yta_hybridsort *e, const double *d_dets, const int *d_off, const f
     hipLaunchKernelGGL(k_hs_pre, dim3(a.S), dim3(OC_T), 0, e->stream, a);
     YTA_HIP(hipGetLastError());
     const dim3 ge((a.CAP + HE_TILE - 1) / HE_TILE, (a.MAXD + HE_TILE - 1) / HE_TILE, a.S);
-    hipLaunchKernelGGL(k_hs_emb, ge, dim3(256), 0, e->stream, a);
+    switch (a.asso) {
+        case 0: hipLaunchKernelGGL(k_hs_emb<0>, ge, dim3(256), 0, e->stream, a); break;
+        case 1: hipLaunchKernelGGL(k_hs_emb<1>, ge, dim3(256), 0, e->stream, a); break;
+        case 2: hipLaunchKernelGGL(k_hs_emb<2>, ge, dim3(256), 0, e->stream, a); break;
+        case 3: hipLaunchKernelGGL(k_hs_emb<3>, ge, dim3(256), 0, e->stream, a); break;
+        default: hipLaunchKernelGGL(k_hs_emb<4>, ge, dim3(256), 0, e->stream, a); break;
+    }
     YTA_HIP(hipGetLastError());
     {
         const long long rows = (a.MAXD + OC_T / WAVE - 1) / (OC_T / WAVE);
