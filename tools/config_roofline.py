@@ -13,7 +13,9 @@ Two views, both printed:
     HBM); the first-round solves (k_*_lap) and the one-block association kernels are dependent
     chains (Dijkstra steps, list scans) and carry no roofline ("latency").
 Peaks: HBM 8.0 TB/s (MI355X_MICROARCH.md); f64 78.6 TFLOP/s (vector = matrix on MI355X, vendor
-spec, SURVEY.md §8(d) -- not in the microarchitecture guide's measured table).
+spec, SURVEY.md §8(d) -- not in the microarchitecture guide's measured table); the GEMM lines
+also carry the fraction of the f64 MFMA rate measured on the box (49.6 TFLOP/s, 8 independent
+v_mfma_f64_16x16x4_f64 chains per wave, tools/mfma_f64_peak.hip).
 """
 import csv
 import json
@@ -21,6 +23,7 @@ import sys
 
 HBM = 8.0e12
 F64 = 78.6e12
+F64_MEASURED = 49.6e12    # tools/mfma_f64_peak.hip on the box: profiles/r03ze_mfma_f64_peak.jsonl
 STATE = {"ocsort": 448, "botsort": 576, "deepocsort": 576, "hybridsort": 720}
 GEMMS = {"ocsort": 0, "botsort": 1, "deepocsort": 1, "hybridsort": 2}
 
@@ -91,7 +94,9 @@ def main():
             k["bound"] = "latency"
         elif m[0] == "flop":
             k.update(bound="f64", achieved_tflops=round(m[1] / avg / 1e12, 2),
-                     peak_tflops=F64 / 1e12, frac=round(m[1] / avg / F64, 4))
+                     peak_tflops=F64 / 1e12, frac=round(m[1] / avg / F64, 4),
+                     measured_peak_tflops=F64_MEASURED / 1e12,
+                     frac_of_measured_peak=round(m[1] / avg / F64_MEASURED, 4))
         else:
             k.update(bound="hbm", achieved_gbs=round(m[1] / avg / 1e9, 1), peak_gbs=HBM / 1e9,
                      frac=round(m[1] / avg / HBM, 4))
