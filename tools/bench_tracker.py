@@ -62,6 +62,11 @@ def main():
     p.add_argument("--n", type=int, default=None)
     p.add_argument("--dim", type=int, default=512)
     p.add_argument("--streams", type=int, default=1)
+    p.add_argument("--queues", type=int, default=None,
+                   help="deepocsort / hybridsort: Q engines of streams/Q streams, each on its own "
+                        "HIP stream, so one engine's one-block-per-stream solve overlaps another's "
+                        "chip-wide GEMM (default 2 for an even stream count, else 1; "
+                        "profiles/r03zf_queues_sweep.txt)")
     p.add_argument("--steps", type=int, default=50)
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--cpu-frames", type=int, default=None)
@@ -71,6 +76,8 @@ def main():
     from yolo_tracking_amd import _lib
     from yolo_tracking_amd.synth import SyntheticStream, make_frames
     S = args.streams
+    if args.queues is None:
+        args.queues = 2 if S >= 2 and S % 2 == 0 else 1
     F = args.warmup + args.steps
     oc = args.tracker == "ocsort"
     fam = args.tracker in ("deepocsort", "hybridsort")
@@ -113,32 +120,58 @@ def main():
         d_feat = torch.from_numpy(feats).cuda()
         del feats
         feat_bytes = dets.shape[1] * D * 4
+        Q = max(1, args.queues)
+        assert S % Q == 0, "--streams must be a multiple of --queues"
+        Sq = S // Q
+        engines, calls = [], []
         if args.tracker == "deepocsort":
             from yolo_tracking_amd.trackers.deepocsort import DeepOCSortEngine
-            eng = DeepOCSortEngine(S, feat_dim=D, **DEEPOCSORT_YAML, track_capacity=2 * N,
-                                   max_dets=N)
-            d_warp = torch.tensor([CMC_AFFINE] * S, dtype=torch.float64).cuda()
             shape = SyntheticStream(N, args.seed, **kw_stream).img_shape
+            d_warp = torch.tensor([CMC_AFFINE] * S, dtype=torch.float64).cuda()
             d_wh = torch.tensor([[shape[1], shape[0]]] * S, dtype=torch.int32).cuda()
-            fn, sync = eng.lib.yta_deepocsort_update_device, eng.lib.yta_deepocsort_sync
         else:
             from yolo_tracking_amd.trackers.hybridsort import HybridSortEngine
-            eng = HybridSortEngine(S, feat_dim=D, **HYBRIDSORT_YAML, track_capacity=2 * N,
-                                   max_dets=N)
-            fn, sync = eng.lib.yta_hybridsort_update_device, eng.lib.yta_hybridsort_sync
-        cap, _ = eng.capacity()
-        d_out = torch.empty((S * cap, 8), dtype=torch.float64, device="cuda")
+        for q in range(Q):
+            # engine q: streams q*Sq .. (q+1)*Sq - 1, detection offsets rebased to its first row
+            base = off[:, q * Sq].astype(np.int64)
+            d_offq = torch.from_numpy(
+                np.ascontiguousarray(off[:, q * Sq:(q + 1) * Sq + 1] - base[:, None]).astype(np.int32)).cuda()
+            if args.tracker == "deepocsort":
+                e = DeepOCSortEngine(Sq, feat_dim=D, **DEEPOCSORT_YAML, track_capacity=2 * N,
+                                     max_dets=N)
+                fn, sync1 = e.lib.yta_deepocsort_update_device, e.lib.yta_deepocsort_sync
+            else:
+                e = HybridSortEngine(Sq, feat_dim=D, **HYBRIDSORT_YAML, track_capacity=2 * N,
+                                     max_dets=N)
+                fn, sync1 = e.lib.yta_hybridsort_update_device, e.lib.yta_hybridsort_sync
+            cap, _ = e.capacity()
+            d_out = torch.empty((Sq * cap, 8), dtype=torch.float64, device="cuda")
+            engines.append(e)
+            calls.append((fn, d_offq, base, q, d_out))
+        eng = engines[0]
+
+        class _AllSync:   # sync(handle) over every engine (the handle argument is ignored)
+            def __call__(self, _handle):
+                for e_ in engines:
+                    rc = sync1(e_.handle)
+                    if rc:
+                        return rc
+                return 0
+        sync = _AllSync()
 
         def step(f):
-            pd = ctypes.c_void_p(d_dets.data_ptr() + f * row_bytes)
-            po = ctypes.c_void_p(d_off.data_ptr() + f * (S + 1) * 4)
-            pf = ctypes.c_void_p(d_feat.data_ptr() + f * feat_bytes)
-            if args.tracker == "deepocsort":
-                _lib.check(fn(eng.handle, pd, po, pf, ctypes.c_void_p(d_warp.data_ptr()),
-                              ctypes.c_void_p(d_wh.data_ptr()), ctypes.c_void_p(d_out.data_ptr()),
-                              None))
-            else:
-                _lib.check(fn(eng.handle, pd, po, pf, ctypes.c_void_p(d_out.data_ptr()), None))
+            for (fn_, d_offq, base, q, d_out), e_ in zip(calls, engines):
+                r0 = int(base[f])
+                pd = ctypes.c_void_p(d_dets.data_ptr() + f * row_bytes + r0 * 48)
+                po = ctypes.c_void_p(d_offq.data_ptr() + f * (Sq + 1) * 4)
+                pf = ctypes.c_void_p(d_feat.data_ptr() + f * feat_bytes + r0 * D * 4)
+                if args.tracker == "deepocsort":
+                    _lib.check(fn_(e_.handle, pd, po, pf,
+                                   ctypes.c_void_p(d_warp.data_ptr() + q * Sq * 6 * 8),
+                                   ctypes.c_void_p(d_wh.data_ptr() + q * Sq * 2 * 4),
+                                   ctypes.c_void_p(d_out.data_ptr()), None))
+                else:
+                    _lib.check(fn_(e_.handle, pd, po, pf, ctypes.c_void_p(d_out.data_ptr()), None))
     else:
         from yolo_tracking_amd.trackers.botsort import BoTSORTEngine
         eng = BoTSORTEngine(S, feat_dim=D, **BOTSORT_YAML, track_capacity=2 * N, max_dets=N)
@@ -187,6 +220,11 @@ def main():
               f"{int(st[101])}, scan {int(st[102]) / 100:.0f} us, reduce {int(st[103]) / 100:.0f} us",
               file=sys.stderr)
     stats = eng.stats()
+    if fam and len(engines) > 1:   # summed over the engines: the same totals as one engine of S
+        for e_ in engines[1:]:
+            for k, v in e_.stats().items():
+                if isinstance(v, (int, float)) and isinstance(stats.get(k), (int, float)):
+                    stats[k] += v
     # CPU leg: the oracle on stream 0, 1 thread, bounded sample
     cf = args.cpu_frames if args.cpu_frames is not None else (30 if oc else (2 if fam else 6))
     if cf == 0:
@@ -251,7 +289,7 @@ def main():
             "higher_is_better": True, "dtype": "f64", "data": "synthetic",
             "config": {"workload": f"{args.tracker} {N}x{N}" + (f" D={D}" if D else "")
                                    + f", {S} streams, inputs resident in HBM",
-                       "streams": S},
+                       "streams": S, "queues": max(1, args.queues) if fam else 1},
             "cpu_baseline": cpu, "frame_counts": stats}
     print(json.dumps(line))
 
