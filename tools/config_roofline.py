@@ -71,6 +71,7 @@ def main():
     N = int(bench["metric"].split("@")[1].split()[0])
     D = int(bench["config"]["workload"].split("D=")[1].split(",")[0]) if "D=" in bench["config"]["workload"] else 0
     S = int(bench["config"]["streams"])
+    Q = int(bench["config"].get("queues", 1))
     fc = bench.get("frame_counts", {})
     trk = fc.get("trackers", N * S)
     det = fc.get("high", N * S)
@@ -90,6 +91,8 @@ def main():
              "avg_us": round(avg * 1e6, 2), "calls": calls,
              "share_of_step": round(avg * calls / steps / (bench["ms_per_step"] * 1e-3), 4)}
         m = kernel_model(tracker, name, trk, det, D, S)
+        if m is not None and Q > 1:       # Q engines: one launch covers S / Q of the streams
+            m = (m[0], m[1] / Q)
         if m is None:
             k["bound"] = "latency"
         elif m[0] == "flop":
