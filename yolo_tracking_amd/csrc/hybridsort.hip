@@ -588,11 +588,14 @@ __device__ __forceinline__ bool hs_corrected(const HsArgs &a, int s, int i, int 
 // First-round Kalman updates (hybridsort.py:462-464) chip-wide, one thread per kept detection,
 // when k_hs_lap solved the first round (else k_hs_assoc updates after its own solve).  A tracker
 // is matched at most once and the updates only touch its record, so they are independent.
-__global__ __launch_bounds__(256) void k_hs_upd(HsArgs a) {
+// One wave per block: a 4096-detection frame spreads over 64 CUs instead of 16, so the record
+// gathers of each update (one record per lane) go through 4x as many CUs' memory pipes.
+constexpr int HS_UPD_T = 64;
+__global__ __launch_bounds__(HS_UPD_T) void k_hs_upd(HsArgs a) {
     const int s = blockIdx.y;
     const HsCounters *c = a.cnt + s;
     const int n_trk = c->n_trk, n_hi = c->n_high;
-    const int i = blockIdx.x * 256 + threadIdx.x;
+    const int i = blockIdx.x * HS_UPD_T + threadIdx.x;
     if (!c->lap_done || i >= n_hi || n_trk == 0) return;
     const long long tb = (long long)s * a.CAP, db = (long long)s * a.MAXD;
     const int k = a.rmatch[db + i];
@@ -1026,7 +1029,8 @@ int hs_launch(yta_hybridsort *e, const double *d_dets, const int *d_off, const f
     hipLaunchKernelGGL(k_hs_lap, dim3(a.S), dim3(LAP_T), (size_t)lap_kernel_lds(a.CAP, a.MAXD),
                        e->stream, a);
     YTA_HIP(hipGetLastError());
-    hipLaunchKernelGGL(k_hs_upd, dim3((a.MAXD + 255) / 256, a.S), dim3(256), 0, e->stream, a);
+    hipLaunchKernelGGL(k_hs_upd, dim3((a.MAXD + HS_UPD_T - 1) / HS_UPD_T, a.S), dim3(HS_UPD_T), 0,
+                       e->stream, a);
     YTA_HIP(hipGetLastError());
     hipLaunchKernelGGL(k_hs_assoc, dim3(a.S), dim3(OC_T), e->lds, e->stream, a);
     YTA_HIP(hipGetLastError());
