@@ -269,7 +269,10 @@ __device__ void doc_birth(DocTrack &out, const double *dr, long long id, int det
 
 // CMC (deep_ocsort.py:385-389), then predict (:269-293) of every tracker, chip-wide; k_doc_pre
 // compacts the survivors per stream.
-__global__ __launch_bounds__(256) void k_doc_predict(DocArgs a) {
+// Per-tracker kernels (predict, Kalman updates) run one wave per block: a frame's trackers spread
+// over 4x the CUs of 256-thread blocks (k_hs_upd's A/B: profiles/r03zi_ab_hs_upd_wave_blocks.txt).
+constexpr int DOC_TRK_T = 64;
+__global__ __launch_bounds__(DOC_TRK_T) void k_doc_predict(DocArgs a) {
     const int s = blockIdx.y;
     const DocCounters *c = a.cnt + s;
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -736,10 +739,10 @@ __global__ __launch_bounds__(OC_T) void k_doc_assoc(DocArgs a) {
 // Every tracker's update (deep_ocsort.py:461-467, :480-493: a matched tracker takes its
 // detection, the others update(None)) chip-wide, one thread per tracker: each touches only its
 // own record.
-__global__ __launch_bounds__(256) void k_doc_upd(DocArgs a) {
+__global__ __launch_bounds__(DOC_TRK_T) void k_doc_upd(DocArgs a) {
     const int s = blockIdx.y;
     const DocCounters *c = a.cnt + s;
-    const int j = blockIdx.x * 256 + threadIdx.x;
+    const int j = blockIdx.x * DOC_TRK_T + threadIdx.x;
     if (j >= c->n_trk) return;
     const long long tb = (long long)s * a.CAP, db = (long long)s * a.MAXD;
     const double *din = a.det_in + (long long)a.det_off[s] * 6;
@@ -1034,7 +1037,8 @@ int doc_launch(yta_deepocsort *e, const double *d_dets, const int *d_off, const 
     a.img_wh = d_wh;
     a.out = out;
     a.out_counts = out_counts;
-    hipLaunchKernelGGL(k_doc_predict, dim3((a.CAP + 255) / 256, a.S), dim3(256), 0, e->stream, a);
+    hipLaunchKernelGGL(k_doc_predict, dim3((a.CAP + DOC_TRK_T - 1) / DOC_TRK_T, a.S), dim3(DOC_TRK_T), 0,
+                       e->stream, a);
     YTA_HIP(hipGetLastError());
     hipLaunchKernelGGL(k_doc_pre, dim3(a.S), dim3(OC_T), 0, e->stream, a);
     YTA_HIP(hipGetLastError());
@@ -1070,7 +1074,8 @@ int doc_launch(yta_deepocsort *e, const double *d_dets, const int *d_off, const 
     YTA_HIP(hipGetLastError());
     hipLaunchKernelGGL(k_doc_assoc, dim3(a.S), dim3(OC_T), e->lds, e->stream, a);
     YTA_HIP(hipGetLastError());
-    hipLaunchKernelGGL(k_doc_upd, dim3((a.CAP + 255) / 256, a.S), dim3(256), 0, e->stream, a);
+    hipLaunchKernelGGL(k_doc_upd, dim3((a.CAP + DOC_TRK_T - 1) / DOC_TRK_T, a.S), dim3(DOC_TRK_T), 0,
+                       e->stream, a);
     YTA_HIP(hipGetLastError());
     hipLaunchKernelGGL(k_doc_finish, dim3(a.S), dim3(OC_T), 0, e->stream, a);
     YTA_HIP(hipGetLastError());

@@ -261,7 +261,8 @@ __device__ void hs_birth(HsTrack &out, const double *bbox, double cls, double de
 
 // predict (hybridsort.py:406-413) of every tracker, chip-wide: boxes and scores into the column
 // records (by list position); k_hs_pre compacts the survivors per stream.
-__global__ __launch_bounds__(256) void k_hs_predict(HsArgs a) {
+// One wave per block, as k_hs_upd (HS_UPD_T): the trackers spread over 4x the CUs.
+__global__ __launch_bounds__(64) void k_hs_predict(HsArgs a) {
     const int s = blockIdx.y;
     HsCounters *c = a.cnt + s;
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1006,7 +1007,7 @@ int hs_launch(yta_hybridsort *e, const double *d_dets, const int *d_off, const f
     a.det_feat = d_feat;
     a.out = out;
     a.out_counts = out_counts;
-    hipLaunchKernelGGL(k_hs_predict, dim3((a.CAP + 255) / 256, a.S), dim3(256), 0, e->stream, a);
+    hipLaunchKernelGGL(k_hs_predict, dim3((a.CAP + 63) / 64, a.S), dim3(64), 0, e->stream, a);
     YTA_HIP(hipGetLastError());
     hipLaunchKernelGGL(k_hs_pre, dim3(a.S), dim3(OC_T), 0, e->stream, a);
     YTA_HIP(hipGetLastError());
