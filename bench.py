@@ -18,7 +18,9 @@ environment) or directly as `bench.py --gpus N`: the parent then starts N rank p
 process per sequence and device.  `--dry-cpu` runs the same harness on CPU ranks over gloo with a
 NumPy stand-in step (tests/test_bench_harness.py).
 
-Rank 0 prints one JSON line with `roofline` (dominant kernel, HIP events on the engine stream),
+Rank 0 prints one JSON line with `roofline` (the longest launch of the isolated leg - engine 0
+alone after the timed region - by HIP events on its stream, with its measured HBM bytes from the
+committed rocprofv3 PMC summary, per kernel),
 `pcie_inclusive` (host buffers in and out every call) and `cpu_baseline` (the oracle's CPU
 restatement on this host: 1 core and all cores, bounded sample).
 """
@@ -91,19 +93,25 @@ def kernel_bytes(phase, st):
     return 0
 
 
+PHASE_KERNEL = {"s1_prep": "k_s1_prep", "s1_edges": "k_s1_edges", "s1_lap": "k_s1_lap",
+                "stage23": "k_stage23", "apply": "k_apply", "finish": "k_finish"}
+
+
 def pmc_traffic(streams, n, queues):
-    """HBM bytes per launch of the roofline kernel, and per step of the whole frame (every kernel
-    of every engine), from the committed rocprofv3 PMC summary (profiles/roofline_traffic.json,
-    FETCH_SIZE x 2 + WRITE_SIZE in separate passes), when it was measured on this same workload;
-    else None."""
+    """Measured HBM bytes per launch of every kernel of the frame, and per step of the whole frame
+    (every kernel of every engine), from the committed rocprofv3 PMC summary
+    (profiles/roofline_traffic.json, written by profiles/summarize.py: FETCH_SIZE x 2 +
+    WRITE_SIZE in separate passes, keyed by kernel), when it was measured on this same workload;
+    else ({}, None, None)."""
     f = os.path.join(REPO, "profiles", "roofline_traffic.json")
     try:
         d = json.load(open(f))
     except (OSError, ValueError):
-        return None, None, None
-    if d.get("streams") == streams and d.get("n") == n and d.get("queues", 1) == queues:
-        return d["hbm_bytes_per_launch"], d.get("hbm_bytes_per_step"), d.get("tag")
-    return None, None, None
+        return {}, None, None
+    if (d.get("streams") == streams and d.get("n") == n and d.get("queues", 1) == queues
+            and isinstance(d.get("kernels"), dict)):
+        return d["kernels"], d.get("hbm_bytes_per_step"), d.get("tag")
+    return {}, None, None
 
 
 # ---------------------------------------------------------------- multi-rank harness (N > 1)
@@ -233,6 +241,35 @@ def gen_stream_frames(n, frames, seed):
     return [d for d, _ in make_frames(n, frames, seed)]
 
 
+def stage_frames(n, frames, seeds, Q, device):
+    """Synthetic frames of this rank's streams straight into HBM, one frame at a time: every
+    stream's generator advances one frame into a page-locked [S*N][6] buffer, which is copied into
+    each engine's [frames][S/Q*N][6] device tensor.  Host memory stays at one frame of every
+    stream (no per-stream frame lists, no stacked copy), whatever the step count or rank count.
+    Returns (per-engine device tensors, per-engine device offset tensors [frames][S/Q + 1])."""
+    import torch
+
+    from yolo_tracking_amd.synth import SyntheticStream
+    S = len(seeds)
+    Sq = S // Q
+    gens = [SyntheticStream(n, sd) for sd in seeds]
+    buf = torch.empty((S * n, 6), dtype=torch.float64, pin_memory=True)
+    host = buf.numpy()
+    d_dets = [torch.empty((frames, Sq * n, 6), dtype=torch.float64, device=device)
+              for _ in range(Q)]
+    for f in range(frames):
+        for s, g in enumerate(gens):
+            d, _ = g.next_frame()
+            assert len(d) == n, "synthetic frames have N detections per stream"
+            host[s * n:(s + 1) * n] = d
+        for q in range(Q):
+            d_dets[q][f].copy_(buf[q * Sq * n:(q + 1) * Sq * n])
+    torch.cuda.synchronize()
+    off = torch.arange(Sq + 1, dtype=torch.int32) * n
+    d_off = [off.repeat(frames, 1).contiguous().to(device) for _ in range(Q)]
+    return d_dets, d_off
+
+
 _CPU_LEG = (
     "import sys,time,json; sys.path.insert(0,%r)\n"
     "from oracle.bytetrack import ByteTrackOracle\n"
@@ -280,16 +317,17 @@ def cpu_baseline(n, frames, seed):
     return line
 
 
-def pcie_inclusive(host, off, S, N, device, first, frames=8, engines=1, pinned=False):
+def pcie_inclusive(frame_of, S, N, device, first, frames=8, engines=1, pinned=False):
     """The same workload through the host-buffer ABI (yta_bytetrack_update: packed host dets in,
     output rows back to the host every call, synchronous) on fresh engines, frames 0..first-1
     untimed (steady state), then `frames` timed steps: rank 0's report of the PCIe-inclusive
-    rate.  With engines > 1 the streams are split over that many engines whose calls run on as
-    many host threads at once (ctypes releases the GIL), so one engine's copies overlap another's
-    kernels, as a multi-camera host would run them; a step ends when every engine's call has
-    returned.  pinned: the caller's buffers are page-locked (as a detector writing its boxes into
-    pinned memory would leave them): each frame's dets are placed in them before its timed call,
-    and the library DMAs straight from / into them (no staging copy).  Never `value`
+    rate.  frame_of(f) -> the (S*N, 6) host array of frame f (read back from the staged device
+    frames, untimed).  With engines > 1 the streams are split over that many engines whose calls
+    run on as many host threads at once (ctypes releases the GIL), so one engine's copies overlap
+    another's kernels, as a multi-camera host would run them; a step ends when every engine's call
+    has returned.  pinned: the caller's buffers are page-locked (as a detector writing its boxes
+    into pinned memory would leave them): each frame's dets are placed in them before its timed
+    call, and the library DMAs straight from / into them (no staging copy).  Never `value`
     (DESIGN.md §5)."""
     from concurrent.futures import ThreadPoolExecutor
 
@@ -299,6 +337,11 @@ def pcie_inclusive(host, off, S, N, device, first, frames=8, engines=1, pinned=F
     E = max(1, min(engines, S))
     bounds = [S * q // E for q in range(E + 1)]
     engs, jobs = [], []
+
+    def buf(shape):
+        if not pinned:
+            return np.empty(shape)
+        return torch.empty(shape, dtype=torch.float64, pin_memory=True).numpy()
     for q in range(E):
         a, b = bounds[q], bounds[q + 1]
         # capacity 3N: the host path reserves ahead of need (tracked + lost + this frame's dets,
@@ -306,52 +349,45 @@ def pcie_inclusive(host, off, S, N, device, first, frames=8, engines=1, pinned=F
         eng = ByteTrackEngine(b - a, track_thresh=0.5, match_thresh=0.8, track_buffer=30,
                               frame_rate=30, device=device, track_capacity=3 * N, max_dets=N)
         engs.append(eng)
-        dets = [np.ascontiguousarray(host[f][off[f][a]:off[f][b]]) for f in range(len(host))]
-        offs = [np.ascontiguousarray(off[f][a:b + 1] - off[f][a]) for f in range(len(host))]
-        def buf(shape):
-            if not pinned:
-                return np.empty(shape)
-            return torch.empty(shape, dtype=torch.float64, pin_memory=True).numpy()
-        jobs.append({"h": eng.handle, "lib": eng.lib, "dets": dets, "offs": offs,
+        jobs.append({"h": eng.handle, "lib": eng.lib, "a": a, "b": b,
+                     "offs": np.ascontiguousarray(np.arange(b - a + 1, dtype=np.int32) * N),
                      "out": buf(((b - a) * N, 8)), "out_off": np.zeros(b - a + 1, np.int32),
-                     "nid": np.zeros(b - a, np.int64),
-                     "pin": buf((max(len(d) for d in dets), 6)) if pinned else None})
-    last = min(first + frames, len(host))
+                     "nid": np.zeros(b - a, np.int64), "in": buf(((b - a) * N, 6))})
+    last = first + frames
 
-    def place(f):   # pinned: this frame's dets into the page-locked buffers (untimed)
+    def place(f):   # this frame's dets into the callers' buffers (untimed)
+        fr = frame_of(f)
         for j in jobs:
-            if j["pin"] is not None:
-                j["pin"][:len(j["dets"][f])] = j["dets"][f]
+            j["in"][:] = fr[j["a"] * N:j["b"] * N]
 
-    def call(j, f):
-        src = j["dets"][f] if j["pin"] is None else j["pin"]
-        _lib.check(j["lib"].yta_bytetrack_update(j["h"], src.ctypes.data,
-                                                 j["offs"][f].ctypes.data, j["nid"].ctypes.data,
+    def call(j):
+        _lib.check(j["lib"].yta_bytetrack_update(j["h"], j["in"].ctypes.data,
+                                                 j["offs"].ctypes.data, j["nid"].ctypes.data,
                                                  j["out"].ctypes.data, len(j["out"]),
                                                  j["out_off"].ctypes.data))
     pool = ThreadPoolExecutor(max_workers=E)
 
-    def step(f):
+    def step():
         if E == 1:
-            call(jobs[0], f)
+            call(jobs[0])
         else:
-            for r in [pool.submit(call, j, f) for j in jobs]:
+            for r in [pool.submit(call, j) for j in jobs]:
                 r.result()
     for f in range(first):
         place(f)
-        step(f)
+        step()
     dts = []
     for f in range(first, last):
         place(f)
         t0 = time.perf_counter()
-        step(f)
+        step()
         dts.append(time.perf_counter() - t0)
     pool.shutdown()
     dt = float(np.median(dts))
     return {"value": S / dt, "unit": "calls/s", "steps": len(dts), "untimed_frames": first,
             "engines": E, "ms_per_step": 1000 * dt,
             "ms_per_step_all": [round(1000 * x, 3) for x in dts],
-            "bytes_h2d_per_step": int(off[first, -1]) * 48,
+            "bytes_h2d_per_step": S * N * 48,
             "note": "host-buffer ABI: packed dets host->device and output rows device->host "
                     f"inside every step ({'page-locked' if pinned else 'pageable numpy'} buffers, "
                     f"{E} engine(s) on as many host threads); median step"}
@@ -428,30 +464,19 @@ def main():
     F = PRE + args.steps
     Q = max(1, args.queues)
     # with Q > 1 engines, ISO more frames after the timed region run on engine 0 alone: the
-    # roofline kernel's rate without the other engines' overlap (reported beside, never `value`)
+    # roofline kernel's launch with the chip to itself (never part of `value`)
     ISO = 3 if Q > 1 and not args.no_isolated else 0
     FT = F + ISO
-    # synthetic frames for this rank's streams, staged in HBM: [FT][S*N][6] + offsets
-    t_gen = time.time()
-    per_stream = [gen_stream_frames(N, FT, sd) for sd in stream_seeds(args.seed, rank, S)]
-    host = np.stack([np.concatenate([per_stream[s][f] for s in range(S)]) for f in range(FT)])
-    counts = np.array([[len(per_stream[s][f]) for s in range(S)] for f in range(FT)])
-    off = np.zeros((FT, S + 1), dtype=np.int32)
-    np.cumsum(counts, axis=1, out=off[:, 1:])
-    del per_stream, counts
-    # Q engines (each its own HIP stream) over contiguous slices of the streams: their launches
-    # run concurrently, so one engine's latency-bound block chains overlap the other's
+    # synthetic frames for this rank's streams, staged in HBM one frame at a time:
+    # Q x [FT][S/Q*N][6] + offsets
     assert S % Q == 0, "--streams must be a multiple of --queues"
     Sq = S // Q
-    d_dets, d_off = [], []
-    for q in range(Q):
-        lo, hi = off[:, q * Sq], off[:, (q + 1) * Sq]
-        dq = np.stack([host[f, lo[f]:hi[f]] for f in range(FT)]) if len(set(hi - lo)) == 1 else None
-        assert dq is not None, "synthetic frames have N detections per stream"
-        d_dets.append(torch.from_numpy(np.ascontiguousarray(dq)).to("cuda"))
-        d_off.append(torch.from_numpy(np.ascontiguousarray(off[:, q * Sq:(q + 1) * Sq + 1]
-                                                          - off[:, q * Sq:q * Sq + 1])).to("cuda"))
+    t_gen = time.time()
+    d_dets, d_off = stage_frames(N, FT, stream_seeds(args.seed, rank, S), Q, "cuda")
     gen_s = time.time() - t_gen
+
+    def frame_of(f):   # the host copy of frame f (pcie leg only; untimed)
+        return torch.cat([d[f] for d in d_dets]).cpu().numpy()
 
     engs = [ByteTrackEngine(Sq, track_thresh=0.5, match_thresh=0.8, track_buffer=30, frame_rate=30,
                             device=local_rank, track_capacity=2 * N, max_dets=N) for _ in range(Q)]
@@ -502,13 +527,15 @@ def main():
         _lib.check(lib.yta_bytetrack_stats(hq, stats))
         for k in range(len(STATS)):
             st[STATS[k]] += int(stats[k])
-    iso_ms = None
+    iso_ms, st_iso = None, None
     if ISO:   # after the timed region: engine 0 alone (the other engines idle) for ISO frames
         sync_all()
         for f in range(F, FT):
             step(f, engines=[0])
         _lib.check(lib.yta_bytetrack_profile_collect(h, ms, ctypes.byref(nfr)))
         iso_ms = {PHASES[k]: ms[k] / max(nfr.value, 1) for k in range(len(PHASES))}
+        _lib.check(lib.yta_bytetrack_stats(h, stats))   # engine 0's last isolated frame
+        st_iso = {STATS[k]: int(stats[k]) for k in range(len(STATS))}
 
     elapsed = max_over_ranks(elapsed, dist, "cpu" if args.shared_gpu else "cuda")
     value = aggregate_rate(world, S, args.steps, elapsed)
@@ -516,12 +543,30 @@ def main():
 
     st_launch = {k: v // Q for k, v in st.items()}   # one engine's launch (Q equal slices)
     if rank == 0:
-        # roofline kernel: the longest launch of the frame (the Kalman pass k_apply, HBM-bound)
-        dom = max(phase_ms, key=lambda p: phase_ms[p])
-        dom_ms = phase_ms[dom]
-        b = kernel_bytes(dom, st_launch)
+        traffic, step_traffic, traffic_tag = pmc_traffic(S, N, Q)
+        # Roofline kernel: the longest launch of a frame with the chip to itself (the isolated
+        # leg: engine 0 alone, HIP events on its stream; with Q = 1 the timed region is that
+        # already).  The overlapped launches of the timed region (two engines interleaving on the
+        # chip) are reported beside it: their events include the other engine's share.
+        ref_ms, ref_st = (iso_ms, st_iso) if iso_ms else (phase_ms, st_launch)
+        dom = max(ref_ms, key=lambda p: ref_ms[p])
+        dom_ms = ref_ms[dom]
+        b = kernel_bytes(dom, ref_st)
         achieved = b / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
-        per_kernel = {p: {"ms": phase_ms[p], "alg_bytes": kernel_bytes(p, st_launch),
+
+        def kline(p, t_ms, stc):
+            alg = kernel_bytes(p, stc)
+            k = traffic.get(PHASE_KERNEL[p], {})
+            hbm = k.get("hbm_bytes_per_launch")
+            return {"ms": t_ms, "alg_bytes": alg,
+                    "gbs": alg / (t_ms * 1e-3) / 1e9 if t_ms > 0 else 0.0,
+                    "frac": alg / (t_ms * 1e-3) / 1e9 / HBM_PEAK_GBS if t_ms > 0 else 0.0,
+                    "pmc_bytes": hbm,
+                    "pmc_over_alg": (hbm / alg) if hbm and alg else None,
+                    "rocprof_avg_us": k.get("avg_us_isolated" if ref_ms is iso_ms
+                                            else "avg_us_timed")}
+        per_kernel = {p: kline(p, ref_ms[p], ref_st) for p in PHASES}
+        overlapped = {p: {"ms": phase_ms[p],
                           "gbs": (kernel_bytes(p, st_launch) / (phase_ms[p] * 1e-3) / 1e9
                                   if phase_ms[p] > 0 else 0.0)} for p in PHASES}
         # implemented minimum: what this build's six launches must move per update (the
@@ -530,14 +575,14 @@ def main():
         impl_bytes = sum(kernel_bytes(p, st) for p in PHASES) / S
         cpu = None if args.no_cpu_baseline else cpu_baseline(N, args.cpu_frames, args.seed)
         pcie = (None if args.no_pcie else
-                pcie_inclusive(host, off, S, N, local_rank, first=min(PRE, FT - 8),
+                pcie_inclusive(frame_of, S, N, local_rank, first=min(PRE, FT - 8),
                                engines=args.pcie_engines))
         if pcie is not None and not args.no_pcie_pinned:
-            pp = pcie_inclusive(host, off, S, N, local_rank, first=min(PRE, FT - 8),
+            pp = pcie_inclusive(frame_of, S, N, local_rank, first=min(PRE, FT - 8),
                                 engines=args.pcie_engines, pinned=True)
             pcie["pinned"] = {k: pp[k] for k in ("value", "ms_per_step", "ms_per_step_all")}
             pcie["pinned"]["note"] = pp["note"]
-        traffic, step_traffic, traffic_tag = pmc_traffic(S, N, Q)
+        dk = traffic.get(PHASE_KERNEL[dom], {})
         line = {
             "metric": "tracker.update() calls/sec @ 1024 tracks×1024 dets; 1/2/4/8 MI355X",
             "value": value, "unit": "calls/s", "n_gpus": world, "steps": args.steps,
@@ -555,30 +600,39 @@ def main():
                        "value_is": "device-resident: frames staged in HBM before the timed "
                                    "region, output rows left in HBM; the host-buffer rate "
                                    "(dets in, rows out over PCIe every call) is pcie_inclusive"},
-            "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved,
+            "roofline": {"bound": "hbm", "kernel": PHASE_KERNEL[dom], "achieved": achieved,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "frac": achieved / HBM_PEAK_GBS,
+                         "traffic": dk.get("hbm_bytes_per_launch"),
+                         "traffic_over_alg": (dk["hbm_bytes_per_launch"] / b
+                                              if dk.get("hbm_bytes_per_launch") else None),
                          "traffic_source": (f"profiles/{traffic_tag}_summary.json (rocprofv3 "
-                                            "FETCH_SIZE x2 + WRITE_SIZE)" if traffic else None),
+                                            f"{PHASE_KERNEL[dom]}: FETCH_SIZE x2 + WRITE_SIZE, "
+                                            "isolated launches)" if dk else None),
                          "algorithmic_bytes_per_launch": b, "avg_launch_ms": dom_ms,
+                         "rocprof_avg_launch_ms": (dk.get("avg_us_isolated") / 1e3
+                                                   if dk.get("avg_us_isolated") else None),
                          "launch_streams": S // Q,
+                         "timing": ("isolated leg: engine 0 alone for the frames after the timed "
+                                    "region, HIP events on its stream" if iso_ms else
+                                    "timed region, HIP events on the engine stream"),
+                         "isolated_frames": ISO,
                          # every kernel of every engine: measured HBM bytes per step / step time
                          "chip_gbs": (step_traffic / (ms_per_step * 1e-3) / 1e9
                                       if step_traffic else None),
-                         "isolated": (None if iso_ms is None else {
-                             "avg_launch_ms": iso_ms[dom],
-                             "achieved": b / (iso_ms[dom] * 1e-3) / 1e9,
-                             "frac": b / (iso_ms[dom] * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                             "frames": ISO,
-                             "note": "engine 0 alone for the frames after the timed region, "
-                                     "same algorithmic bytes per launch"}),
-                         "note": (None if Q == 1 else
-                                  f"{Q} engines of {S // Q} streams on {Q} HIP streams: each "
-                                  "launch overlaps the other engines' kernels, so its duration "
-                                  "(and this per-launch rate) includes their share of the chip")},
+                         "beside": {p: per_kernel[p] for p in ("s1_edges", "finish")
+                                    if p != dom},
+                         "overlapped": (None if Q == 1 else {
+                             "avg_launch_ms": phase_ms[dom],
+                             "frac": (kernel_bytes(dom, st_launch) / (phase_ms[dom] * 1e-3) / 1e9
+                                      / HBM_PEAK_GBS if phase_ms[dom] > 0 else None),
+                             "note": f"{Q} engines of {S // Q} streams on {Q} HIP streams in the "
+                                     "timed region: each launch overlaps the other engines' "
+                                     "kernels, so its event duration includes their share"})},
             "pcie_inclusive": pcie,
             "cpu_baseline": cpu,
             "per_kernel": per_kernel,
+            "per_kernel_overlapped": overlapped,
             "frame_counts": st,
             "busiest_kernel": dom,
             "algorithmic_bytes_per_update": impl_bytes,

@@ -2,8 +2,9 @@
 
 The reference's package (boxmot/__init__.py:5-18) and the module paths its users and
 `examples/track.py:9-12` import resolve here to the modules of `yolo_tracking_amd` — the same
-module objects, so the classes, the process-global ID counters and the loaded C-ABI library are
-shared — and the tracker YAMLs live at `ROOT/'boxmot'/'configs'` exactly where
+module objects for every leaf module (a package path that also has alias children is a
+forwarding node over the real package), so the classes, the process-global ID counters and the
+loaded C-ABI library are shared — and the tracker YAMLs live at `ROOT/'boxmot'/'configs'` exactly where
 `examples/track.py:37-41` builds their paths (ROOT = boxmot.utils.ROOT = the repository root).
 
     import boxmot                                  # registers every alias below
@@ -59,10 +60,28 @@ ALIASES = {
 }
 
 
+class _Forward(types.ModuleType):
+    """A reference package path whose module of this build also has alias-only children (e.g.
+    boxmot.trackers -> yolo_tracking_amd.trackers, with boxmot.trackers.bytetrack below it):
+    attribute lookups fall through to the real module, while the alias children are attached
+    here, never onto the real module (whose own submodule attributes stay untouched)."""
+
+    def __init__(self, name, target):
+        super().__init__(name, target.__doc__)
+        self.__path__ = []
+        self.__wrapped__ = target
+
+    def __getattr__(self, attr):
+        return getattr(self.__wrapped__, attr)
+
+
 def _register():
     me = sys.modules[__name__]
+    parents = {a.rsplit(".", 1)[0] for a in ALIASES}
     for alias in sorted(ALIASES, key=lambda a: a.count(".")):
         mod = importlib.import_module(ALIASES[alias])
+        if any(p == alias or p.startswith(alias + ".") for p in parents):
+            mod = _Forward(alias, mod)          # has alias children: a boxmot-owned node
         parts = alias.split(".")
         parent = me
         for depth in range(1, len(parts) - 1):   # reference-only intermediate packages
@@ -74,6 +93,9 @@ def _register():
                 setattr(parent, parts[depth], pkg)
             parent = sys.modules[name]
         sys.modules[alias] = mod
+        # only boxmot-owned modules (this package, alias namespaces, _Forward nodes) get
+        # attributes: a yolo_tracking_amd module is never modified
+        assert parent.__name__.startswith("boxmot"), parent.__name__
         setattr(parent, parts[-1], mod)
 
 

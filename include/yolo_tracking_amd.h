@@ -169,6 +169,26 @@ int yta_bytetrack_update_device(yta_bytetrack *engine, const double *d_dets,
                                 const int *d_det_offsets, double *d_out, int *d_out_counts);
 int yta_bytetrack_sync(yta_bytetrack *engine);      /* waits; reports device-side errors */
 
+/* Host-buffer update of a SUBSET of the streams (update(ctx, n_streams,
+ * stream_ids, ...)).  In the reference every camera stream is its own tracker
+ * (examples/track.py:43-57) and a stream without a new frame is simply not called
+ * (examples/val.py:184-226 runs sequences of different lengths side by side).  stream_ids:
+ * n_streams ascending ids in 0..S-1; dets / det_offsets (n_streams + 1) / next_id (n_streams) /
+ * out / out_offsets (n_streams + 1) as yta_bytetrack_update, over those streams in id order.
+ * Every other stream is left exactly as it was: tracks, Kalman state, frame counter, ID counter. */
+int yta_bytetrack_update_streams(yta_bytetrack *engine, int n_streams, const int *stream_ids,
+                                 const double *dets, const int *det_offsets, long long *next_id,
+                                 double *out, int out_capacity, int *out_offsets);
+/* Device form of the subset update: d_active = S ints on the device, nonzero = update that stream
+ * this call (NULL = every stream); skipped streams report 0 rows in d_out_counts. */
+int yta_bytetrack_update_device_masked(yta_bytetrack *engine, const int *d_active,
+                                       const double *d_dets, const int *d_det_offsets,
+                                       double *d_out, int *d_out_counts);
+/* Reset ONE stream to a freshly created tracker (no tracks, frame and ID counters 0), as
+ * constructing a new BYTETracker for that camera would (byte_tracker.py:115-130); the other
+ * streams are untouched.  Also for BoT-SORT engines. */
+int yta_bytetrack_reset_stream(yta_bytetrack *engine, int stream);
+
 /* Parity introspection: copy stream s's live tracks, tracked list first then lost list, in list
  * order.  Per track: list (0 tracked / 1 lost), id, state (0 New 1 Tracked 2 Lost 3 Removed),
  * activated, frame_id, start_frame, tracklet_len (ints: 7 x int64 per track), mean (8 f64), cov
@@ -233,6 +253,12 @@ int yta_botsort_update(yta_botsort *engine, const double *dets, const int *det_o
 int yta_botsort_update_device(yta_botsort *engine, const double *d_dets, const int *d_det_offsets,
                               const float *d_feats, const double *d_warps, double *d_out,
                               int *d_out_counts);
+/* Subset update (see yta_bytetrack_update_streams): feats cover the listed streams' high
+ * detections in id order, warps n_streams 2x3 affines (or NULL). */
+int yta_botsort_update_streams(yta_botsort *engine, int n_streams, const int *stream_ids,
+                               const double *dets, const int *det_offsets, const float *feats,
+                               const double *warps, long long *next_id, double *out,
+                               int out_capacity, int *out_offsets);
 /* Parity introspection, in yta_bytetrack_get_state's track order: smoothed features
  * (feat_dim floats per track, may be NULL), class histograms (8 x (class, summed score) float64
  * per track, may be NULL) and their entry counts (may be NULL). */

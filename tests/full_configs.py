@@ -14,10 +14,18 @@ PATH = os.path.join(HERE, "golden", "full_configs.npz")
 DOS_CMC = ["dos_n2048_d512_cmc_a", "dos_n2048_d512_cmc_b", "dos_n2048_d512_cmc_c",
            "dos_n2048_d512_cmc_d"]
 HS_4096 = ["hs_n4096_d512_a", "hs_n4096_d512_b"]
+# long cases (tests/golden/make_goldens_deep.py -> full_deep.npz)
+DEEP_PATH = os.path.join(HERE, "golden", "full_deep.npz")
+DOS_F40 = ["dos_n2048_cmc_f40_a", "dos_n2048_cmc_f40_b"]
+HS_S8 = [f"hs_n4096_s8_{k}" for k in "abcdefgh"]
 
 
 def load():
     return np.load(PATH)
+
+
+def load_deep():
+    return np.load(DEEP_PATH)
 
 
 def digest(rows):
@@ -60,7 +68,11 @@ def bytetrack_frames(g, name):
 def botsort_frames(g, name):
     """(frames [(dets, embs)], params dict, D) of the full-size BoT-SORT case."""
     n, nf, seed, D = (int(x) for x in g[f"{name}__gen"])
-    frames = make_frames(n, nf, seed, emb_dim=D)
+    skw = {}
+    if f"{name}__stream" in g.files:
+        low, drop = (float(x) for x in g[f"{name}__stream"])
+        skw = dict(low_conf_frac=low, drop_frac=drop)
+    frames = make_frames(n, nf, seed, emb_dim=D, **skw)
     sums = g[f"{name}__in_sum"]
     assert float(np.sum([d.sum() for d, _ in frames])) == sums[0]
     assert float(np.sum([e.astype(np.float64).sum() for _, e in frames])) == sums[1]

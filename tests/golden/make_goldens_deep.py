@@ -1,0 +1,122 @@
+#!/usr/bin/env python3
+"""Long full-size goldens: the BASELINE.json configs at their stated sizes, run long enough to
+reach the lifecycle paths (container-only: imports the reference through refshim).
+
+    python tests/golden/make_goldens_deep.py all [-j 6]   # every case in parallel, then merge
+    python tests/golden/make_goldens_deep.py part CASE    # one case -> tests/golden/_parts/CASE.npz
+    python tests/golden/make_goldens_deep.py merge        # _parts/*.npz -> tests/golden/full_deep.npz
+
+Cases (stored exactly as make_goldens_full.py stores its cases: per-frame SHA-256 digests of the
+reference's (K, 8) rows, row counts, every frame's ids and det_ind, the last frame in full, final
+tracker states with covariances / embeddings sampled every 64th tracker):
+  bs_n1024_d512_f65       C3 BoT-SORT 1024 x 1024, D 512, 65 frames, 5 % missed detections: Lost
+                          tracks re-found (bot_sort.py:339-346) and expired after max_time_lost =
+                          60 (botsort.yaml track_buffer 60, bot_sort.py:386-390).
+  dos_n2048_cmc_f40_{a,b} C4 DeepOCSORT 2048 x 2048, D 512, CMC affine, 40 frames, 2 streams (one
+                          engine launch per frame in the GPU test), 5 % missed detections: ORU
+                          re-acquisitions (deep_ocsort.py:220-232 -> deepocsort_kf.py:unfreeze)
+                          and deaths after max_age = 30 (deep_ocsort.py:514-517).
+  hs_n4096_f35            C5 HybridSORT 4096 x 4096, D 512, 35 frames: deaths after max_age = 30
+                          (hybridsort.py:562-567), feature banks up to 30 deep
+                          (hybridsort.py:190, :438-439).
+  hs_n4096_s8_{a..h}      C5 at its per-GPU concurrency: 8 streams x 12 frames, one engine launch
+                          per frame in the GPU test; banks 12 deep, delta_t history full.
+Every LAP call is tie-checked and every threshold comparison margin-checked as in
+make_goldens.py; DeepOCSORT / HybridSORT seeds are advanced (seed0, seed0 + 100, ...) until the
+oracle reproduces the reference exactly in lock-step (birth numbering included).
+"""
+import os
+import subprocess
+import sys
+import time
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+PARTS = os.path.join(HERE, "_parts")
+OUTFILE = os.path.join(HERE, "full_deep.npz")
+
+CASES = {}
+CASES["bs_n1024_d512_f65"] = ("bs", dict(n=1024, nf=65, seed=1146, D=512,
+                                         skw=dict(low_conf_frac=0.1, drop_frac=0.05)))
+for k, s in zip("ab", (2161, 2162)):
+    CASES[f"dos_n2048_cmc_f40_{k}"] = ("dos", dict(n=2048, nf=40, seed=s, D=512))
+CASES["hs_n4096_f35"] = ("hs", dict(n=4096, nf=35, seed=4191, D=512))
+for k, s in zip("abcdefgh", range(4201, 4209)):
+    CASES[f"hs_n4096_s8_{k}"] = ("hs", dict(n=4096, nf=12, seed=s, D=512))
+
+
+def run_part(case):
+    sys.path.insert(0, HERE)
+    import make_goldens_full as mgf
+    from yolo_tracking_amd.synth import SyntheticStream, make_frames
+    kind, p = CASES[case]
+    mgf.OUT.clear()
+    t0 = time.time()
+    if kind == "bs":
+        for seed in range(p["seed"], p["seed"] + 1000, 100):
+            if mgf.bs_case(case, p["n"], p["nf"], seed, p["D"], p["skw"]):
+                break
+        else:
+            raise RuntimeError(f"{case}: no tie-free seed")
+    elif kind == "dos":
+        skw = dict(low_conf_frac=0.0, drop_frac=0.05)
+        n, nf, D = p["n"], p["nf"], p["D"]
+        for seed in range(p["seed"], p["seed"] + 1000, 100):
+            frames = make_frames(n, nf, seed, emb_dim=D, **skw)
+            img_shape = SyntheticStream(n, seed, emb_dim=D, **skw).img_shape
+            if mgf.run_deepocsort_case(case, frames, img_shape, mgf.mg.CMC_AFFINE, D, nf, n,
+                                       seed, skw):
+                break
+        else:
+            raise RuntimeError(f"{case}: no tie-free seed")
+    else:
+        mgf.hs_case(case, p["n"], p["nf"], p["seed"], p["D"])
+    os.makedirs(PARTS, exist_ok=True)
+    np.savez_compressed(os.path.join(PARTS, case + ".npz"), **mgf.OUT)
+    print(f"{case}: done in {time.time() - t0:.0f}s", flush=True)
+
+
+def merge():
+    out = {}
+    for case in CASES:
+        with np.load(os.path.join(PARTS, case + ".npz")) as z:
+            out.update({k: z[k] for k in z.files})
+    out["cases"] = np.array(sorted(CASES))
+    np.savez_compressed(OUTFILE, **out)
+    print(f"wrote {OUTFILE}: {os.path.getsize(OUTFILE) / 1e6:.2f} MB")
+
+
+def run_all(jobs):
+    env = dict(os.environ, OMP_NUM_THREADS="1", OPENBLAS_NUM_THREADS="1", MKL_NUM_THREADS="1")
+    todo = [c for c in CASES if not os.path.exists(os.path.join(PARTS, c + ".npz"))]
+    # longest first
+    todo.sort(key=lambda c: -CASES[c][1]["nf"] * CASES[c][1]["n"] ** 2)
+    running = []
+    os.makedirs(PARTS, exist_ok=True)
+    while todo or running:
+        while todo and len(running) < jobs:
+            c = todo.pop(0)
+            log = open(os.path.join(PARTS, c + ".log"), "w")
+            running.append((c, subprocess.Popen([sys.executable, __file__, "part", c],
+                                                stdout=log, stderr=subprocess.STDOUT, env=env)))
+        time.sleep(5)
+        for c, pr in list(running):
+            if pr.poll() is not None:
+                running.remove((c, pr))
+                print(f"{c}: rc {pr.returncode}", flush=True)
+                if pr.returncode:
+                    raise SystemExit(f"{c} failed, see {PARTS}/{c}.log")
+    merge()
+
+
+if __name__ == "__main__":
+    sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+    cmd = sys.argv[1] if len(sys.argv) > 1 else "all"
+    if cmd == "part":
+        run_part(sys.argv[2])
+    elif cmd == "merge":
+        merge()
+    else:
+        jobs = int(sys.argv[sys.argv.index("-j") + 1]) if "-j" in sys.argv else 6
+        run_all(jobs)

@@ -45,3 +45,27 @@ def test_track_py_imports_and_config_paths():
         for k in keys[m]:
             assert k in cfg, (m, k)
     assert ns["WEIGHTS"] == ns["ROOT"] / "examples" / "weights"
+
+
+def test_alias_leaves_native_package_untouched():
+    """Importing boxmot must not replace yolo_tracking_amd's own submodule attributes with the
+    alias-only namespaces (boxmot.trackers.bytetrack etc.)."""
+    import importlib
+
+    import boxmot  # noqa: F401
+    import yolo_tracking_amd.motion
+    import yolo_tracking_amd.trackers
+    from yolo_tracking_amd.trackers import bytetrack, ocsort
+    assert yolo_tracking_amd.trackers.bytetrack is bytetrack
+    assert hasattr(yolo_tracking_amd.trackers.bytetrack, "ByteTrackEngine")
+    m = importlib.import_module("yolo_tracking_amd.trackers.ocsort")
+    assert m is ocsort and hasattr(m, "OCSort")
+    assert not hasattr(yolo_tracking_amd.motion.cmc, "sof")
+    # the reference paths still resolve, attribute access included
+    import boxmot.trackers.bytetrack.byte_tracker as bt
+    assert bt is bytetrack
+    assert boxmot.trackers.bytetrack.byte_tracker.BYTETracker is bytetrack.BYTETracker
+    assert boxmot.trackers.ocsort.ocsort.OCSort is ocsort.OCSort
+    assert boxmot.motion.cmc.sof.SparseOptFlow is importlib.import_module(
+        "yolo_tracking_amd.motion.sof").SparseOptFlow
+    from boxmot.utils import ROOT  # noqa: F401

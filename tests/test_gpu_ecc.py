@@ -117,3 +117,22 @@ def test_uncorrelated_frames_error_path():
     inv = gray_bgr(255 - fr[1][..., 0])
     for mode in (0, 1, 2):
         run_pair([fr, [fr[0], fr[1], inv, fr[3]]], mode=mode, scale=1.0)
+
+
+def test_capacity_error_leaves_engine_intact():
+    """A frame whose scaled size overflows the LDS warp tables is refused (YTA_ERR_CAPACITY) and
+    leaves the engine exactly as it was: the next normal frame matches the oracle that never saw
+    the refused one (the slots are grown transactionally, csrc/ecc.hip ecc_slots)."""
+    from yolo_tracking_amd._lib import YTAError
+    frames = moving_frames(120, 160, 3, seed=5)
+    eng = EccEngine(1, 1, 1e-5, 100, 0.1, 0, 120, 160)
+    o = ce.ECCOracle(warp_mode=1, eps=1e-5, max_iter=100, scale=0.1)
+    for k in range(2):
+        assert np.array_equal(eng.apply([frames[k]])[0], o.apply(frames[k]))
+    huge = np.zeros((1, 190000, 3), np.uint8)
+    with pytest.raises(YTAError):
+        eng.apply([huge])
+    assert np.array_equal(eng.apply([frames[2]])[0], o.apply(frames[2]))
+    st = eng.state(0, with_image=True)
+    assert np.array_equal(st["prev_img"], o.prev_img)
+    eng.close()

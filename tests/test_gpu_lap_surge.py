@@ -160,3 +160,26 @@ def test_first_round_normal_orientation_unchanged():
     rx, done, n_tight = _lib.lap_first_round(c)
     assert done and n_tight == -1
     assert np.array_equal(rx, xo)
+
+
+@pytest.mark.parametrize("gap", [1e-10, 1e-9, 3e-9, 1e-8])
+@pytest.mark.parametrize("scale", [1.0, 50.0])
+def test_first_round_near_ties_uncertified_or_lapjv(gap, scale):
+    """Near-tied alternative optima (an unmatched detection row given a matched pair's cost plus a
+    reduced-cost gap of 1e-10 .. 1e-8, at unit scale and at 50x, as embedding- or long-term-
+    weighted costs can be): the transposed solve is either left uncertified (the engine replays
+    lapjv) or equals lapjv's solution row for row (the tolerance scales with the costs)."""
+    from oracle.lap import lapjv
+    from yolo_tracking_amd import _lib
+    rng = np.random.default_rng(int(gap * 1e12) + int(scale))
+    c = _surge_like(rng, 600, 200) * scale
+    _, xo, _ = lapjv(c, extend_cost=True)
+    free = np.nonzero(xo < 0)[0]
+    used = np.nonzero(xo >= 0)[0]
+    for k in range(8):   # eight near-tied swaps
+        r, r2 = free[k], used[rng.integers(len(used))]
+        c[r, xo[r2]] = c[r2, xo[r2]] + gap * scale
+    _, xo, _ = lapjv(c, extend_cost=True)
+    rx, done, n_tight = _lib.lap_first_round(c)
+    print(gap, scale, "done", done, "tight", n_tight)
+    assert (not done) or np.array_equal(rx, xo), np.nonzero(rx != xo)[0][:10]

@@ -3,8 +3,8 @@
 BatchNorm statistics, eval mode), the weight-file path of ReIDDetectMultiBackend, and the trackers
 building their ReID producer from reid_weights as the reference does.
 
-Bar: float32 features within 1e-4 of the feature scale (MIOpen's convolution algorithms sum in
-other orders than the CPU's); float16 within 2e-2 relative (the reference's half=True path is
+Bar: float32 features within 1e-4 of the feature scale (the HIP forward, csrc/osnet.hip, sums its
+convolutions and MFMA GEMM tiles in other orders than the CPU's); float16 within 2e-2 relative (the reference's half=True path is
 float16 as well)."""
 import os
 

@@ -31,3 +31,15 @@ def test_oracle_botsort_1024_d512():
     for f, (dets, embs) in enumerate(frames):
         fc.check_frame_close(g, name, f, t.update(
             dets, reid_features(dets, embs, params["track_high_thresh"])))
+
+
+def test_oracle_botsort_1024_d512_65_frames():
+    """The long C3 golden (tests/golden/full_deep.npz): Lost tracks re-found and expired after
+    max_time_lost = 60 (bot_sort.py:339-346, :386-390), every frame's ids and det_ind exact."""
+    g = fc.load_deep()
+    name = "bs_n1024_d512_f65"
+    frames, params, D = fc.botsort_frames(g, name)
+    t = BoTSORTOracle(**params)
+    for f, (dets, embs) in enumerate(frames):
+        fc.check_frame_close(g, name, f, t.update(
+            dets, reid_features(dets, embs, params["track_high_thresh"])))

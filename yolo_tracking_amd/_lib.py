@@ -117,6 +117,9 @@ _SIGS = {
     "yta_bytetrack_update": ([_P, _P, _P, _P, _P, _I, _P], _I),
     "yta_bytetrack_update_device": ([_P, _P, _P, _P, _P], _I),
     "yta_bytetrack_sync": ([_P], _I),
+    "yta_bytetrack_update_streams": ([_P, _I, _P, _P, _P, _P, _P, _I, _P], _I),
+    "yta_bytetrack_update_device_masked": ([_P, _P, _P, _P, _P, _P], _I),
+    "yta_bytetrack_reset_stream": ([_P, _I], _I),
     "yta_bytetrack_get_state": ([_P, _I, _P, _P, _P, _P], _I),
     "yta_bytetrack_profile": ([_P, _I], _I),
     "yta_bytetrack_profile_collect": ([_P, _P, _P], _I),
@@ -128,6 +131,7 @@ _SIGS = {
     "yta_botsort_update": ([_P, _P, _P, _P, _P, _P, _P, _I, _P], _I),
     "yta_botsort_update_device": ([_P, _P, _P, _P, _P, _P, _P], _I),
     "yta_botsort_get_features": ([_P, _I, _P, _P, _P, _P], _I),
+    "yta_botsort_update_streams": ([_P, _I, _P, _P, _P, _P, _P, _P, _P, _I, _P], _I),
     "yta_ocsort_create": ([_I, _I, _I, _I, _P, _P], _I),
     "yta_ocsort_destroy": ([_P], _I),
     "yta_ocsort_reset": ([_P], _I),

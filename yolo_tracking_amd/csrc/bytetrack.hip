@@ -339,6 +339,7 @@ __global__ __launch_bounds__(BLK1) void k_stage1(BtArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     __shared__ StageShared sh;
     const int s = blockIdx.x;
+    if (stream_skipped(a, s)) return;
     YTA_STAMP_BASE(0);
     YTA_STAMP(0);
     {
@@ -356,6 +357,7 @@ __global__ __launch_bounds__(BLK23) void k_stage23(BtArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     __shared__ StageShared sh;
     const int s = blockIdx.x;
+    if (stream_skipped(a, s)) return;
     YTA_STAMP_BASE(20);
     YTA_STAMP(0);
     YTA_BLK(3, 0);
@@ -456,6 +458,7 @@ __device__ __forceinline__ TrkRec bt_trk_rec(const BtArgs &a, long long tb, int 
 __global__ __launch_bounds__(PREP_T) void k_s1_prep(BtArgs a) {
     __shared__ PrepShared sh;
     const int s = blockIdx.x, t = threadIdx.x;
+    if (stream_skipped(a, s)) return;
     YTA_STAMP_BASE(60);
     YTA_STAMP(0);
     YTA_BLK(0, 0);
@@ -838,6 +841,7 @@ __global__ __launch_bounds__(BLKE, 4) void k_s1_edges(BtArgs a) {
     __shared__ int spill, n_edges;
     __shared__ EdgeWaveQ ewq[BLKE / WAVE];
     const int s = blockIdx.x, t = threadIdx.x, nt = blockDim.x;
+    if (stream_skipped(a, s)) return;
     YTA_STAMP_BASE(66);
     YTA_STAMP(0);
     YTA_BLK(1, 0);
@@ -1102,6 +1106,7 @@ __global__ __launch_bounds__(BLKL, 4) void k_s1_lap(BtArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     __shared__ LapShared lsh;
     const int s = blockIdx.x;
+    if (stream_skipped(a, s)) return;
     YTA_BLK(2, 0);
     {
         Arena ar(smem, a.lds_bytes_l);
@@ -1213,6 +1218,7 @@ __global__ __launch_bounds__(APPLY_T) void k_apply(BtArgs a) {
     __shared__ int s_slot[APPLY_T];
     __shared__ int s_wmask[APPLY_T];      // bit 0: write the Kalman record, bit 1: write the meta
     const int s = blockIdx.y, t = threadIdx.x;
+    if (stream_skipped(a, s)) return;
     BtCounters *c = a.cnt + s;
     const int n_pool = c->n_pool, n_unc = c->n_unc, fid = c->frame_id;
     const int i0 = blockIdx.x * APPLY_T;
@@ -1413,6 +1419,7 @@ __device__ __forceinline__ float f32_norm(double sumsq) { return sqrtf((float)su
 constexpr int FEAT_T = 256;
 __global__ __launch_bounds__(FEAT_T) void k_feat(BtArgs a) {
     const int s = blockIdx.y, lane = lane_id();
+    if (stream_skipped(a, s)) return;
     const int d = blockIdx.x * (FEAT_T / WAVE) + threadIdx.x / WAVE;
     const int nd = min(a.det_off[s + 1] - a.det_off[s], a.MAXD);
     if (d >= nd) return;
@@ -1449,6 +1456,7 @@ __global__ __launch_bounds__(FEAT_T) void k_feat(BtArgs a) {
 constexpr int EMA_T = 256;
 __global__ __launch_bounds__(EMA_T) void k_ema(BtArgs a) {
     const int s = blockIdx.y, lane = lane_id();
+    if (stream_skipped(a, s)) return;
     const BtCounters *c = a.cnt + s;
     const int n_pool = c->n_pool, n_items = n_pool + c->n_unc;
     const int item = blockIdx.x * (EMA_T / WAVE) + threadIdx.x / WAVE;
@@ -1838,6 +1846,13 @@ __global__ __launch_bounds__(BLKF, 4) void k_finish(BtArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char fsmem[];
     __shared__ FinishShared sh;
     const int s = blockIdx.x;
+    if (stream_skipped(a, s)) {   // not updated this frame: no output rows
+        if (threadIdx.x == 0) {
+            a.cnt[s].n_out = 0;
+            if (a.out_counts) a.out_counts[s] = 0;
+        }
+        return;
+    }
     const int words = (a.CAP + 31) / 32;
     const size_t bits_bytes = ((size_t)12 * words + 15) & ~(size_t)15;
     unsigned *bits = reinterpret_cast<unsigned *>(fsmem);
@@ -1911,8 +1926,8 @@ __global__ __launch_bounds__(BLKF) void k_rebuild_free(BtArgs a) {
     if (t == 0) c->n_free = n_free;
 }
 
-__global__ void k_reset(BtArgs a) {
-    const int s = blockIdx.x;
+__global__ void k_reset(BtArgs a, int s0) {
+    const int s = s0 + blockIdx.x;
     const long long tb = (long long)s * a.CAP;
     for (int i = threadIdx.x; i < a.CAP; i += blockDim.x) a.free_list[tb + i] = i;
     if (threadIdx.x == 0) {
@@ -1952,6 +1967,8 @@ struct yta_bytetrack {
     double *d_det_in = nullptr;
     long long d_det_cap = 0;
     int *d_det_off = nullptr;
+    // stream-subset updates: the [S] mask on the device and its pinned staging
+    int *d_active = nullptr, *h_active = nullptr;
     // optional per-kernel timing with HIP events on the engine stream
     bool prof = false;
     std::vector<hipEvent_t> ev;
@@ -2009,17 +2026,28 @@ constexpr int STAGE_CHUNKS = YTA_STAGE_CHUNKS;
 // hipHostRegister'ed, e.g. a pinned torch tensor's numpy view): the DMA engines then read / write
 // it directly and the staging copy is skipped.  Pageable memory makes the query fail; its error
 // is cleared.
+// Is [p, p + bytes) one page-locked host allocation?  Both ends page-locked is not enough (a
+// view spanning two pinned allocations with pageable pages between them): the whole range must
+// lie inside the allocation that holds p.  Anything the runtime cannot vouch for is staged.
 bool host_pinned(const void *p, size_t bytes) {
     if (!p || !bytes) return false;
-    for (const char *q : {(const char *)p, (const char *)p + bytes - 1}) {
-        hipPointerAttribute_t at;
-        if (hipPointerGetAttributes(&at, q) != hipSuccess) {
-            (void)hipGetLastError();
-            return false;
-        }
-        if (at.type != hipMemoryTypeHost) return false;
+    hipPointerAttribute_t at;
+    if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
     }
-    return true;
+    if (at.type != hipMemoryTypeHost) return false;
+    hipDeviceptr_t base = nullptr;
+    size_t size = 0;
+    if (hipPointerGetAttribute(&base, HIP_POINTER_ATTRIBUTE_RANGE_START_ADDR,
+                               (hipDeviceptr_t)p) != hipSuccess ||
+        hipPointerGetAttribute(&size, HIP_POINTER_ATTRIBUTE_RANGE_SIZE, (hipDeviceptr_t)p) !=
+            hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    const char *b = (const char *)base, *q = (const char *)p;
+    return b && q >= b && bytes <= size && (size_t)(q - b) <= size - bytes;
 }
 inline size_t stage_chunk(size_t bytes) {
     const int n = bytes >= (16u << 20) ? STAGE_CHUNKS : 1;
@@ -2156,6 +2184,7 @@ int bt_alloc(yta_bytetrack *e) {
     DALLOC(a.slab.i, S * SLAB_WAVES * a.slab.i_stride);
     DALLOC(a.slab.d, S * SLAB_WAVES * a.slab.d_stride);
     DALLOC(e->d_det_off, S + 1);
+    DALLOC(e->d_active, S);
     YTA_HIP(hipHostMalloc((void **)&e->h_off, sizeof(int) * (S + 1), hipHostMallocDefault));
     YTA_HIP(hipHostMalloc((void **)&e->h_cnt, sizeof(BtCounters) * S, hipHostMallocDefault));
     return YTA_OK;
@@ -2340,6 +2369,7 @@ int reserve(yta_bytetrack *e, int cap, int maxd) {
     e->h_off = n->h_off;
     e->h_cnt = n->h_cnt;
     e->d_det_off = n->d_det_off;
+    e->d_active = n->d_active;
     n->h_off = nullptr;
     n->h_cnt = nullptr;
     n->stream = nullptr;
@@ -2444,7 +2474,7 @@ int ensure_pack(yta_bytetrack *e, long long rows) {
 
 int update_host(yta_bytetrack *e, const double *dets, const int *det_offsets, const float *feats,
                 long long *next_id, double *out, int out_capacity, int *out_offsets,
-                const double *warps = nullptr) {
+                const double *warps = nullptr, const int *active = nullptr) {
     YTA_CHECK(e && det_offsets && out_offsets, YTA_ERR_INVALID, "null argument");
     YTA_HIP(hipSetDevice(e->device));
     const int S = e->S;
@@ -2533,7 +2563,17 @@ int update_host(yta_bytetrack *e, const double *dets, const int *det_offsets, co
                                  sizeof(BtCounters), sizeof(long long), S, hipMemcpyHostToDevice,
                                  e->stream));
     }
+    if (active) {   // stream subset: the others' kernels return at once (BtArgs::active)
+        if (!e->h_active) {
+            YTA_HIP(hipHostMalloc((void **)&e->h_active, sizeof(int) * S, hipHostMallocDefault));
+        }
+        memcpy(e->h_active, active, sizeof(int) * S);
+        YTA_HIP(hipMemcpyAsync(e->d_active, e->h_active, sizeof(int) * S, hipMemcpyHostToDevice,
+                               e->stream));
+        e->a.active = e->d_active;
+    }
     int rc = launch_pipeline(e, e->d_det_in, e->d_det_off, e->a.out, nullptr, e->d_feat_in);
+    e->a.active = nullptr;
     if (rc) return rc;
     // Small engines (every stream's worst-case rows <= 1 MiB, e.g. one camera stream): rows packed
     // at device-computed offsets and copied back with the counters, one round trip per frame
@@ -2622,6 +2662,62 @@ int update_host(yta_bytetrack *e, const double *dets, const int *det_offsets, co
     return YTA_OK;
 }
 
+// Host-buffer update of a subset of the streams: n ascending stream ids; dets / det_offsets (n+1)
+// / feats / warps (n x 6) / next_id (n) / out_offsets (n+1) cover those streams only, in id
+// order.  Expanded to the engine's S streams (zero detections, identity warp and the engine's
+// own counter for the others, which the stream mask leaves untouched), run, and compacted.
+int update_host_subset(yta_bytetrack *e, int n, const int *ids, const double *dets,
+                       const int *det_offsets, const float *feats, long long *next_id,
+                       double *out, int out_capacity, int *out_offsets, const double *warps) {
+    YTA_CHECK(e && ids && det_offsets && out_offsets, YTA_ERR_INVALID, "null argument");
+    const int S = e->S;
+    YTA_CHECK(n >= 1 && n <= S, YTA_ERR_INVALID, "n_streams %d outside 1..%d", n, S);
+    for (int k = 0; k < n; ++k)
+        YTA_CHECK(ids[k] >= 0 && ids[k] < S && (k == 0 || ids[k] > ids[k - 1]), YTA_ERR_INVALID,
+                  "stream_ids must be ascending and within 0..%d", S - 1);
+    YTA_CHECK(det_offsets[0] == 0, YTA_ERR_INVALID, "det_offsets[0] must be 0");
+    std::vector<int> active(S, 0), off(S + 1, 0), full_oo(S + 1, 0);
+    std::vector<long long> nid(S);
+    std::vector<double> w;
+    if (next_id) {   // the skipped streams keep their device counters: read them first (a device
+                     // update since the last host call may have advanced them)
+        YTA_HIP(hipSetDevice(e->device));
+        const int rc = read_counters(e);
+        if (rc) return rc;
+    }
+    for (int s = 0; s < S; ++s) nid[s] = e->h_cnt[s].next_id;
+    if (warps && e->variant == VAR_BOTSORT) {
+        w.assign((size_t)6 * S, 0.0);
+        for (int s = 0; s < S; ++s) w[6 * s] = w[6 * s + 4] = 1.0;
+    }
+    for (int k = 0; k < n; ++k) {
+        active[ids[k]] = 1;
+        if (next_id) nid[ids[k]] = next_id[k];
+        if (!w.empty()) std::copy(warps + 6LL * k, warps + 6LL * k + 6, w.begin() + 6LL * ids[k]);
+    }
+    for (int s = 0, k = 0; s < S; ++s) {
+        int m = 0;
+        if (active[s]) {
+            m = det_offsets[k + 1] - det_offsets[k];
+            YTA_CHECK(m >= 0, YTA_ERR_INVALID, "det_offsets must be non-decreasing");
+            ++k;
+        }
+        off[s + 1] = off[s] + m;
+    }
+    const int rc = update_host(e, dets, off.data(), feats, next_id ? nid.data() : nullptr, out,
+                               out_capacity, full_oo.data(), w.empty() ? nullptr : w.data(),
+                               active.data());
+    if (e->variant == VAR_BOTSORT) e->a.warp = e->d_warp_id;
+    // the device counters have advanced for the active streams: hand them back even on an error
+    if (next_id)
+        for (int k = 0; k < n; ++k) next_id[k] = nid[ids[k]];
+    if (rc) return rc;
+    out_offsets[0] = 0;
+    for (int k = 0; k < n; ++k)   // skipped streams have 0 rows: the packing is the subset's
+        out_offsets[k + 1] = out_offsets[k] + (full_oo[ids[k] + 1] - full_oo[ids[k]]);
+    return YTA_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -2666,6 +2762,7 @@ int yta_bytetrack_destroy(yta_bytetrack *e) {
     if (e->h_pack_off) (void)hipHostFree(e->h_pack_off);
     if (e->h_feat) (void)hipHostFree(e->h_feat);
     if (e->d_feat_in) (void)hipFree(e->d_feat_in);
+    if (e->h_active) (void)hipHostFree(e->h_active);
     for (hipEvent_t h : e->ev) (void)hipEventDestroy(h);
     if (e->stream) (void)hipStreamDestroy(e->stream);
     delete e;
@@ -2675,13 +2772,29 @@ int yta_bytetrack_destroy(yta_bytetrack *e) {
 int yta_bytetrack_reset(yta_bytetrack *e) {
     YTA_CHECK(e, YTA_ERR_INVALID, "null engine");
     YTA_HIP(hipSetDevice(e->device));
-    hipLaunchKernelGGL(k_reset, dim3(e->S), dim3(256), 0, e->stream, e->a);
+    hipLaunchKernelGGL(k_reset, dim3(e->S), dim3(256), 0, e->stream, e->a, 0);
     YTA_HIP(hipGetLastError());
     YTA_HIP(hipMemsetAsync(e->a.kf, 0, sizeof(double) * TRK_STRIDE * (size_t)e->S * e->CAP,
                            e->stream));
     YTA_HIP(hipMemsetAsync(e->a.flags, 0, sizeof(int) * (size_t)e->S * e->CAP, e->stream));
     YTA_HIP(host_wait(e->stream));
     memset(e->h_cnt, 0, sizeof(BtCounters) * e->S);
+    return YTA_OK;
+}
+
+int yta_bytetrack_reset_stream(yta_bytetrack *e, int stream) {
+    YTA_CHECK(e, YTA_ERR_INVALID, "null engine");
+    YTA_CHECK(stream >= 0 && stream < e->S, YTA_ERR_INVALID, "stream %d outside 0..%d", stream,
+              e->S - 1);
+    YTA_HIP(hipSetDevice(e->device));
+    hipLaunchKernelGGL(k_reset, dim3(1), dim3(256), 0, e->stream, e->a, stream);
+    YTA_HIP(hipGetLastError());
+    const size_t tb = (size_t)stream * e->CAP;
+    YTA_HIP(hipMemsetAsync(e->a.kf + tb * TRK_STRIDE, 0, sizeof(double) * TRK_STRIDE * e->CAP,
+                           e->stream));
+    YTA_HIP(hipMemsetAsync(e->a.flags + tb, 0, sizeof(int) * e->CAP, e->stream));
+    YTA_HIP(host_wait(e->stream));
+    memset(&e->h_cnt[stream], 0, sizeof(BtCounters));
     return YTA_OK;
 }
 
@@ -2707,6 +2820,23 @@ int yta_bytetrack_update_device(yta_bytetrack *e, const double *d_dets, const in
                                 double *d_out, int *d_out_counts) {
     YTA_CHECK(e && d_det_offsets && d_out, YTA_ERR_INVALID, "null argument");
     return launch_pipeline(e, d_dets, d_det_offsets, d_out, d_out_counts);
+}
+
+int yta_bytetrack_update_streams(yta_bytetrack *e, int n_streams, const int *stream_ids,
+                                 const double *dets, const int *det_offsets, long long *next_id,
+                                 double *out, int out_capacity, int *out_offsets) {
+    return update_host_subset(e, n_streams, stream_ids, dets, det_offsets, nullptr, next_id, out,
+                              out_capacity, out_offsets, nullptr);
+}
+
+int yta_bytetrack_update_device_masked(yta_bytetrack *e, const int *d_active,
+                                       const double *d_dets, const int *d_det_offsets,
+                                       double *d_out, int *d_out_counts) {
+    YTA_CHECK(e && d_det_offsets && d_out, YTA_ERR_INVALID, "null argument");
+    e->a.active = d_active;
+    const int rc = launch_pipeline(e, d_dets, d_det_offsets, d_out, d_out_counts);
+    e->a.active = nullptr;
+    return rc;
 }
 
 int yta_bytetrack_sync(yta_bytetrack *e) {
@@ -2864,6 +2994,15 @@ int yta_botsort_update_device(yta_botsort *e, const double *d_dets, const int *d
     const int rc = launch_pipeline(e, d_dets, d_det_offsets, d_out, d_out_counts, d_feats);
     e->a.warp = e->d_warp_id;
     return rc;
+}
+
+int yta_botsort_update_streams(yta_botsort *e, int n_streams, const int *stream_ids,
+                               const double *dets, const int *det_offsets, const float *feats,
+                               const double *warps, long long *next_id, double *out,
+                               int out_capacity, int *out_offsets) {
+    YTA_CHECK(e && e->variant == VAR_BOTSORT, YTA_ERR_INVALID, "not a BoT-SORT engine");
+    return update_host_subset(e, n_streams, stream_ids, dets, det_offsets, feats, next_id, out,
+                              out_capacity, out_offsets, warps);
 }
 
 int yta_botsort_get_features(yta_botsort *e, int stream, int *n_tracks, float *feats,

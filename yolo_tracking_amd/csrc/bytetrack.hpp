@@ -126,6 +126,14 @@ struct BtArgs {
     // outputs
     double *out;              // [S*CAP][8]
     int *out_counts;          // optional [S]
+    // stream subset: [S] nonzero = update this stream this frame; nullptr = every stream.  A
+    // skipped stream's kernels return at once (its state, frame counter and ID counter are not
+    // touched); k_finish reports 0 output rows for it.
+    const int *active;
 };
+
+__device__ __forceinline__ bool stream_skipped(const BtArgs &a, int s) {
+    return a.active != nullptr && a.active[s] == 0;
+}
 
 }  // namespace yta

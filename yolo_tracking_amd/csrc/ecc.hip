@@ -715,16 +715,27 @@ void ecc_free_slots(yta_ecc *e) {
     e->img = nullptr;
 }
 
-int ecc_slots(yta_ecc *e) {
+// Allocate the two image slots per stream for frames up to mh x mw.  Transactional: the engine
+// (max_h / max_w, the slot geometry in e->a, e->img) changes only on success; the caller frees
+// the previous slots (returned in *old) after copying what it keeps out of them.
+int ecc_slots(yta_ecc *e, int mh, int mw, uint8_t **old, long long *old_px) {
     EccArgs &a = e->a;
-    a.hmax = (int)std::rint(e->max_h * e->scale);
-    a.wmax = (int)std::rint(e->max_w * e->scale);
-    YTA_CHECK(a.hmax >= 1 && a.wmax >= 1, YTA_ERR_INVALID, "frames scale to an empty image");
-    YTA_CHECK(8LL * (a.hmax + a.wmax) + 16 <= ECC_LDS, YTA_ERR_CAPACITY,
-              "scaled frames of %d x %d: the warp tables exceed the LDS stage", a.hmax, a.wmax);
-    a.slot_px = ((long long)a.hmax * a.wmax + 15) & ~15LL;
-    YTA_HIP(hipMalloc((void **)&e->img, (size_t)(2LL * e->S * a.slot_px)));
-    a.img = e->img;
+    const int hmax = (int)std::rint(mh * e->scale);
+    const int wmax = (int)std::rint(mw * e->scale);
+    YTA_CHECK(hmax >= 1 && wmax >= 1, YTA_ERR_INVALID, "frames scale to an empty image");
+    YTA_CHECK(8LL * (hmax + wmax) + 16 <= ECC_LDS, YTA_ERR_CAPACITY,
+              "scaled frames of %d x %d: the warp tables exceed the LDS stage", hmax, wmax);
+    const long long slot_px = ((long long)hmax * wmax + 15) & ~15LL;
+    uint8_t *img = nullptr;
+    YTA_HIP(hipMalloc((void **)&img, (size_t)(2LL * e->S * slot_px)));
+    if (old) *old = e->img;
+    if (old_px) *old_px = a.slot_px;
+    e->max_h = mh;
+    e->max_w = mw;
+    a.hmax = hmax;
+    a.wmax = wmax;
+    a.slot_px = slot_px;
+    a.img = e->img = img;
     return YTA_OK;
 }
 
@@ -792,8 +803,8 @@ int yta_ecc_create(int device, int n_streams, int warp_mode, double eps, int max
     e->eps = eps;
     e->max_iter = max_iter;
     e->scale = scale;
-    e->max_h = max_h;
-    e->max_w = max_w;
+    e->max_h = 0;
+    e->max_w = 0;
     hipError_t he = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
     if (he != hipSuccess) {
         set_error("hipStreamCreate: %s", hipGetErrorString(he));
@@ -804,7 +815,7 @@ int yta_ecc_create(int device, int n_streams, int warp_mode, double eps, int max
         yta_ecc_destroy(e);
         return code;
     };
-    rc = ecc_slots(e);
+    rc = ecc_slots(e, max_h, max_w, nullptr, nullptr);
     if (rc) return fail(rc);
     if (hipMalloc((void **)&e->state, sizeof(EccState) * n_streams) != hipSuccess ||
         hipMalloc((void **)&e->d_warps, sizeof(float) * 6 * n_streams) != hipSuccess ||
@@ -884,20 +895,20 @@ int yta_ecc_apply(yta_ecc *e, const uint8_t *frames, const long long *frame_off,
         mw = std::max(mw, w);
     }
     if (mh > e->max_h || mw > e->max_w) {
-        // grow the slots, keeping every stream's previous frame (packed from the slot start)
+        // grow the slots, keeping every stream's previous frame (packed from the slot start);
+        // on failure the engine keeps its previous slots and size untouched
         YTA_HIP(host_wait(e->stream));
-        uint8_t *old = e->img;
-        const long long old_px = e->a.slot_px;
-        e->img = nullptr;
-        e->max_h = mh;
-        e->max_w = mw;
-        int rc = ecc_slots(e);
-        if (!rc) {
-            YTA_HIP(hipMemcpy2DAsync(e->img, e->a.slot_px, old, old_px, old_px, (size_t)S * 2,
-                                     hipMemcpyDeviceToDevice, e->stream));
-            rc = host_wait(e->stream) == hipSuccess ? YTA_OK : YTA_ERR_HIP;
+        uint8_t *old = nullptr;
+        long long old_px = 0;
+        int rc = ecc_slots(e, mh, mw, &old, &old_px);
+        if (rc) return rc;
+        if (old) {
+            if (hipMemcpy2DAsync(e->img, e->a.slot_px, old, old_px, old_px, (size_t)S * 2,
+                                 hipMemcpyDeviceToDevice, e->stream) != hipSuccess ||
+                host_wait(e->stream) != hipSuccess)
+                rc = YTA_ERR_HIP;
+            (void)hipFree(old);
         }
-        (void)hipFree(old);
         if (rc) return rc;
     }
     if (bytes > e->frames_cap) {

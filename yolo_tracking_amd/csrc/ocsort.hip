@@ -1193,8 +1193,9 @@ extern "C" int yta_kf7_run(int device, int n, int steps, const double *z0, const
 // First-round solve KAT (ocsort_common.hpp): the chip-wide row pre-pass and the LAP_T-thread
 // solve exactly as the engines launch them, on one na x nb cost matrix (rows = detections,
 // columns = trackers; no fast path).  rx[i] = tracker of detection i or -1 when solved; *done = 0
-// when the association kernel would replay lapjv instead; *gap = the uniqueness certificate of a
-// transposed solve (na > nb; +inf otherwise).
+// when the association kernel would replay lapjv instead; *n_tight = the number of tight
+// non-matching edges the uniqueness certificate of a transposed solve examined (na > nb), -1
+// when the problem was solved in its normal orientation (no certificate).
 namespace {
 __global__ __launch_bounds__(OC_T) void k_kat_fr_pre(const double *m, int na, int nb, double *u,
                                                      int *x, double *s2) {

@@ -214,8 +214,11 @@ __device__ __forceinline__ void iou_lap(const LapMat &M, int *rx, unsigned char 
 // v < 0.  Another optimum differs from x by an alternating cycle of tight edges, or by an
 // alternating path of tight edges ending at an unmatched column.  The shortest-path trees of the
 // augmentations leave tight non-matching edges behind (a row stays tight to the column it left),
-// so the test is structural: collect the tight non-matching edges (reduced cost <= UNIQ_TOL, a
-// margin over either solver's rounding: |c| <~ 3, a few hundred dual updates), fail on one into
+// so the test is structural: collect the tight non-matching edges (reduced cost <= UNIQ_TOL times
+// the magnitude of the entry and duals involved, at least 1: a margin over either solver's
+// rounding that scales with the costs, so an embedding- or long-term-weighted matrix with larger
+// entries is judged as conservatively as a unit-scale one; a looser test only certifies less
+// and sends more frames to the exact replay), fail on one into
 // an unmatched column, and look for a cycle in the column digraph (x_i -> k for a tight (i, k)),
 // by peeling columns without out-edges.  Unique => lapjv (any exact solver) returns x too,
 // whatever its tie-breaking.  Block-wide; the edges go to `tws` (TIGHT_CAP), out-degrees to the
@@ -237,7 +240,8 @@ __device__ __forceinline__ int unique_optimum_tr(const double *mat, int na, int 
         auto visit = [&](int i, double c) {
             const double r = (c - w.v[i]) - own;
             if (r != r) { bad = 1; return; }
-            if (i == xj || r > UNIQ_TOL) return;
+            const double mag = fmax(1.0, fmax(fabs(c), fmax(fabs(w.v[i]), fabs(own))));
+            if (i == xj || r > UNIQ_TOL * mag) return;
             if (w.yw[i] < 0) { bad = 1; return; }   // tight into an unmatched column
             const int k = atomicAdd(&ne, 1);
             if (k < TIGHT_CAP) tws[k] = make_int2(xj, i);

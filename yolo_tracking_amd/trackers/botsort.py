@@ -72,14 +72,29 @@ class BoTSORTEngine(ByteTrackEngine):
         self._out = np.empty((0, 8), dtype=np.float64)
         self._out_off = np.zeros(self.n_streams + 1, dtype=np.int32)
 
-    def update(self, dets_per_stream, feats_per_stream=None, warps=None, next_id=None):
+    def update(self, dets_per_stream, feats_per_stream=None, warps=None, next_id=None,
+               streams=None):
         """dets_per_stream: S float64 (M_s, 6) arrays; feats_per_stream: S float32 (H_s, D)
         arrays, the ReID rows of each stream's high detections (conf > track_high_thresh) in
         detection order; warps: optional S 2x3 affines; next_id: optional int64 (S,) counters,
-        updated in place.  Returns S (K_s, 8) arrays."""
-        assert len(dets_per_stream) == self.n_streams
+        updated in place.  Returns S (K_s, 8) arrays.  streams: update only these stream ids
+        (every per-stream argument and the result then follow the listed streams)."""
+        ids = None
+        if streams is not None:
+            ids, order = self._subset(streams, len(dets_per_stream))
+            dets_per_stream = [dets_per_stream[k] for k in order]
+            if feats_per_stream is not None:
+                feats_per_stream = [feats_per_stream[k] for k in order]
+            if warps is not None:
+                warps = np.asarray(warps, dtype=np.float64).reshape(-1, 6)[order]
+            nid_user = next_id
+            if next_id is not None:
+                next_id = np.ascontiguousarray(np.asarray(next_id, np.int64)[order])
+        else:
+            assert len(dets_per_stream) == self.n_streams
+        n = len(dets_per_stream)
         counts = [len(d) for d in dets_per_stream]
-        off = np.zeros(self.n_streams + 1, dtype=np.int32)
+        off = np.zeros(n + 1, dtype=np.int32)
         np.cumsum(counts, out=off[1:])
         if off[-1]:
             packed = np.ascontiguousarray(np.concatenate(
@@ -89,7 +104,7 @@ class BoTSORTEngine(ByteTrackEngine):
         feats = None
         if self.feat_dim:
             rows = []
-            for d, f in zip(dets_per_stream, feats_per_stream or [None] * self.n_streams):
+            for d, f in zip(dets_per_stream, feats_per_stream or [None] * n):
                 nh = int(np.count_nonzero(np.asarray(d, np.float64).reshape(-1, 6)[:, 4]
                                           > self.track_high_thresh))
                 f = np.zeros((0, self.feat_dim), np.float32) if f is None or nh == 0 else f
@@ -100,7 +115,7 @@ class BoTSORTEngine(ByteTrackEngine):
             feats = np.ascontiguousarray(np.concatenate(rows)) if rows else None
         w = None
         if warps is not None:
-            w = np.ascontiguousarray(np.asarray(warps, dtype=np.float64).reshape(self.n_streams, 6))
+            w = np.ascontiguousarray(np.asarray(warps, dtype=np.float64).reshape(n, 6))
         # every output row is a track matched to or born from one of this frame's detections
         need = max(int(off[-1]), 1)
         if len(self._out) < need:
@@ -108,14 +123,20 @@ class BoTSORTEngine(ByteTrackEngine):
         nid = None
         if next_id is not None:
             nid = np.ascontiguousarray(next_id, dtype=np.int64)
-        _lib.check(self.lib.yta_botsort_update(self._h, _lib.ptr(packed), _lib.ptr(off),
-                                               _lib.ptr(feats), _lib.ptr(w), _lib.ptr(nid),
-                                               _lib.ptr(self._out), len(self._out),
-                                               _lib.ptr(self._out_off)))
-        if next_id is not None:
-            next_id[...] = nid
-        o = self._out_off
-        return [self._out[o[s]:o[s + 1]].copy() for s in range(self.n_streams)]
+        if ids is None:
+            _lib.check(self.lib.yta_botsort_update(self._h, _lib.ptr(packed), _lib.ptr(off),
+                                                   _lib.ptr(feats), _lib.ptr(w), _lib.ptr(nid),
+                                                   _lib.ptr(self._out), len(self._out),
+                                                   _lib.ptr(self._out_off)))
+            if next_id is not None:
+                next_id[...] = nid
+            o = self._out_off
+            return [self._out[o[s]:o[s + 1]].copy() for s in range(self.n_streams)]
+        o = np.zeros(n + 1, dtype=np.int32)
+        _lib.check(self.lib.yta_botsort_update_streams(
+            self._h, n, _lib.ptr(ids), _lib.ptr(packed), _lib.ptr(off), _lib.ptr(feats),
+            _lib.ptr(w), _lib.ptr(nid), _lib.ptr(self._out), len(self._out), _lib.ptr(o)))
+        return self._subset_result(o, order, nid, nid_user)
 
     def features(self, stream=0):
         """Smoothed features, class histograms (n, 8, 2) and their entry counts of the live

@@ -49,6 +49,22 @@ class ByteTrackEngine:
     def reset(self):
         _lib.check(self.lib.yta_bytetrack_reset(self._h))
 
+    def reset_stream(self, stream):
+        """Reset one stream to a fresh tracker; the others are untouched."""
+        _lib.check(self.lib.yta_bytetrack_reset_stream(self._h, int(stream)))
+
+    def _subset(self, streams, n_items):
+        """Validated stream ids of a subset update as an ascending int32 array + the order that
+        sorts the caller's lists (outputs are handed back in the caller's order)."""
+        ids = np.asarray(streams, dtype=np.int64).reshape(-1)
+        if len(ids) != n_items or len(ids) == 0:
+            raise ValueError("one entry per listed stream")
+        order = np.argsort(ids, kind="stable")
+        ids = ids[order]
+        if ids[0] < 0 or ids[-1] >= self.n_streams or np.any(np.diff(ids) == 0):
+            raise ValueError(f"stream ids must be distinct and in 0..{self.n_streams - 1}")
+        return np.ascontiguousarray(ids, dtype=np.int32), order
+
     def capacity(self):
         c, d = ctypes.c_int(), ctypes.c_int()
         _lib.check(self.lib.yta_bytetrack_capacity(self._h, ctypes.byref(c), ctypes.byref(d)))
@@ -70,12 +86,24 @@ class ByteTrackEngine:
         _lib.check(self.lib.yta_bytetrack_stats(self._h, buf))
         return {k: int(buf[i]) for i, k in enumerate(names)}
 
-    def update(self, dets_per_stream, next_id=None):
+    def update(self, dets_per_stream, next_id=None, streams=None):
         """dets_per_stream: list of S float64 (M_s, 6) arrays.  next_id: optional int64 (S,) array
-        of last-issued IDs, updated in place.  Returns a list of S (K_s, 8) arrays."""
-        assert len(dets_per_stream) == self.n_streams
+        of last-issued IDs, updated in place.  Returns a list of S (K_s, 8) arrays.
+        streams: update only these stream ids (dets_per_stream / next_id / the result then have
+        one entry per listed stream, in the listed order); every other stream is left as it was
+        (yta_bytetrack_update_streams)."""
+        ids = None
+        if streams is not None:
+            ids, order = self._subset(streams, len(dets_per_stream))
+            dets_per_stream = [dets_per_stream[k] for k in order]
+            nid_user = next_id
+            if next_id is not None:
+                next_id = np.ascontiguousarray(np.asarray(next_id, np.int64)[order])
+        else:
+            assert len(dets_per_stream) == self.n_streams
+        n = len(dets_per_stream)
         counts = [len(d) for d in dets_per_stream]
-        off = np.zeros(self.n_streams + 1, dtype=np.int32)
+        off = np.zeros(n + 1, dtype=np.int32)
         np.cumsum(counts, out=off[1:])
         if off[-1]:
             packed = np.ascontiguousarray(np.concatenate(
@@ -89,13 +117,27 @@ class ByteTrackEngine:
         nid = None
         if next_id is not None:
             nid = np.ascontiguousarray(next_id, dtype=np.int64)
-        _lib.check(self.lib.yta_bytetrack_update(self._h, _lib.ptr(packed), _lib.ptr(off),
-                                                 _lib.ptr(nid), _lib.ptr(self._out),
-                                                 len(self._out), _lib.ptr(self._out_off)))
-        if next_id is not None:
-            next_id[...] = nid
-        o = self._out_off
-        return [self._out[o[s]:o[s + 1]].copy() for s in range(self.n_streams)]
+        if ids is None:
+            _lib.check(self.lib.yta_bytetrack_update(self._h, _lib.ptr(packed), _lib.ptr(off),
+                                                     _lib.ptr(nid), _lib.ptr(self._out),
+                                                     len(self._out), _lib.ptr(self._out_off)))
+            if next_id is not None:
+                next_id[...] = nid
+            o = self._out_off
+            return [self._out[o[s]:o[s + 1]].copy() for s in range(self.n_streams)]
+        o = np.zeros(n + 1, dtype=np.int32)
+        _lib.check(self.lib.yta_bytetrack_update_streams(
+            self._h, n, _lib.ptr(ids), _lib.ptr(packed), _lib.ptr(off), _lib.ptr(nid),
+            _lib.ptr(self._out), len(self._out), _lib.ptr(o)))
+        return self._subset_result(o, order, nid, nid_user)
+
+    def _subset_result(self, o, order, nid, nid_user):
+        res = [None] * len(order)
+        for k, pos in enumerate(order):
+            res[pos] = self._out[o[k]:o[k + 1]].copy()
+        if nid_user is not None:
+            nid_user[order] = nid
+        return res
 
     def state(self, stream=0):
         """Live tracks of one stream (tracked list then lost list) for parity checks."""
