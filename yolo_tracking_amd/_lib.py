@@ -120,6 +120,8 @@ _SIGS = {
     "yta_bytetrack_update_streams": ([_P, _I, _P, _P, _P, _P, _P, _I, _P], _I),
     "yta_bytetrack_update_device_masked": ([_P, _P, _P, _P, _P, _P], _I),
     "yta_bytetrack_reset_stream": ([_P, _I], _I),
+    "yta_bytetrack_submit": ([_P, _P, _P, _P, _P, _I], _I),
+    "yta_bytetrack_collect": ([_P, _P, _P], _I),
     "yta_bytetrack_get_state": ([_P, _I, _P, _P, _P, _P], _I),
     "yta_bytetrack_profile": ([_P, _I], _I),
     "yta_bytetrack_profile_collect": ([_P, _P, _P], _I),

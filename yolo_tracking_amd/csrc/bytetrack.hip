@@ -1897,6 +1897,32 @@ __global__ void k_out_offsets(const BtCounters *cnt, int S, int cap, int *off) {
     }
 }
 
+// Pipelined host-buffer update (any S): the same prefix offsets from one 1024-thread block, each
+// thread summing a run of streams, then a block scan.
+constexpr int OFFS_T = 1024;
+__global__ __launch_bounds__(OFFS_T) void k_out_offsets_scan(const BtCounters *cnt, int S, int cap,
+                                                              int *off) {
+    __shared__ int part[OFFS_T];
+    const int t = threadIdx.x;
+    const int per = (S + OFFS_T - 1) / OFFS_T, s0 = min(S, t * per), s1 = min(S, s0 + per);
+    int sum = 0;
+    for (int s = s0; s < s1; ++s) sum += min(max(cnt[s].n_out, 0), cap);
+    part[t] = sum;
+    __syncthreads();
+    for (int d = 1; d < OFFS_T; d <<= 1) {   // inclusive Hillis-Steele scan
+        const int v = t >= d ? part[t - d] : 0;
+        __syncthreads();
+        part[t] += v;
+        __syncthreads();
+    }
+    int r = part[t] - sum;   // exclusive prefix of this thread's run
+    if (t == 0) off[0] = 0;
+    for (int s = s0; s < s1; ++s) {
+        r += min(max(cnt[s].n_out, 0), cap);
+        off[s + 1] = r;
+    }
+}
+
 __global__ __launch_bounds__(BLKF) void k_rebuild_free(BtArgs a) {
     __shared__ int wsum[32];
     extern __shared__ __attribute__((aligned(16))) unsigned int live[];
@@ -1969,6 +1995,25 @@ struct yta_bytetrack {
     int *d_det_off = nullptr;
     // stream-subset updates: the [S] mask on the device and its pinned staging
     int *d_active = nullptr, *h_active = nullptr;
+    // pipelined host-buffer updates (yta_bytetrack_submit / _collect): two frame slots, a copy-in
+    // and a copy-out stream beside the compute stream
+    struct PipeSlot {
+        double *d_in = nullptr, *h_in = nullptr;     // detections (pinned staging for pageable)
+        long long in_cap = 0;
+        int *d_off = nullptr, *h_off = nullptr;      // S + 1 detection offsets
+        double *d_pack = nullptr, *h_pack = nullptr; // packed output rows
+        long long pack_cap = 0;
+        int *d_pack_off = nullptr, *h_pack_off = nullptr;   // S + 1 row offsets
+        BtCounters *d_cnt = nullptr, *h_cnt = nullptr;      // counters after this frame
+        long long *h_nid = nullptr;                  // next_id staging
+        hipEvent_t in_done = nullptr, kern_done = nullptr, out_done = nullptr;
+        double *user_out = nullptr;                  // the caller's buffer
+        long long rows_bound = 0;                    // det_offsets[S] of the frame
+        bool direct_out = false;                     // DMA straight into user_out
+    };
+    PipeSlot pipe[2];
+    int pipe_head = 0, pipe_count = 0;
+    hipStream_t s_in = nullptr, s_out = nullptr;
     // optional per-kernel timing with HIP events on the engine stream
     bool prof = false;
     std::vector<hipEvent_t> ev;
@@ -2476,6 +2521,7 @@ int update_host(yta_bytetrack *e, const double *dets, const int *det_offsets, co
                 long long *next_id, double *out, int out_capacity, int *out_offsets,
                 const double *warps = nullptr, const int *active = nullptr) {
     YTA_CHECK(e && det_offsets && out_offsets, YTA_ERR_INVALID, "null argument");
+    YTA_CHECK(e->pipe_count == 0, YTA_ERR_INVALID, "pipelined frames in flight: collect them first");
     YTA_HIP(hipSetDevice(e->device));
     const int S = e->S;
     YTA_CHECK(det_offsets[0] == 0, YTA_ERR_INVALID, "det_offsets[0] must be 0");
@@ -2718,6 +2764,187 @@ int update_host_subset(yta_bytetrack *e, int n, const int *ids, const double *de
     return YTA_OK;
 }
 
+// ---- pipelined host-buffer update --------------------------------------------------------------
+// Frame f's detections go host -> device on s_in while frame f-1's kernels run on the compute
+// stream and frame f-2's rows come back on s_out (both PCIe directions and the kernels at once).
+// The compute stream snapshots every frame's rows (k_pack_out into the slot) and counters before
+// the next frame's kernels can touch them, so the copy-out of frame f never races frame f+1.
+void pipe_free(yta_bytetrack *e) {
+    for (auto &p : e->pipe) {
+        for (void *d : {(void *)p.d_in, (void *)p.d_off, (void *)p.d_pack, (void *)p.d_pack_off,
+                        (void *)p.d_cnt})
+            if (d) (void)hipFree(d);
+        for (void *h : {(void *)p.h_in, (void *)p.h_off, (void *)p.h_pack, (void *)p.h_pack_off,
+                        (void *)p.h_cnt, (void *)p.h_nid})
+            if (h) (void)hipHostFree(h);
+        for (hipEvent_t ev : {p.in_done, p.kern_done, p.out_done})
+            if (ev) (void)hipEventDestroy(ev);
+        p = yta_bytetrack::PipeSlot{};
+    }
+    for (hipStream_t st : {e->s_in, e->s_out})
+        if (st) (void)hipStreamDestroy(st);
+    e->s_in = e->s_out = nullptr;
+    e->pipe_count = 0;
+    e->pipe_head = 0;
+}
+
+int pipe_slot_ready(yta_bytetrack *e, yta_bytetrack::PipeSlot &p, long long dets) {
+    const int S = e->S;
+    if (!e->s_in) {
+        YTA_HIP(hipStreamCreateWithFlags(&e->s_in, hipStreamNonBlocking));
+        YTA_HIP(hipStreamCreateWithFlags(&e->s_out, hipStreamNonBlocking));
+    }
+    if (!p.in_done) {
+        for (hipEvent_t *ev : {&p.in_done, &p.kern_done, &p.out_done})
+            YTA_HIP(hipEventCreateWithFlags(ev, hipEventDisableTiming));
+        YTA_HIP(hipMalloc((void **)&p.d_off, sizeof(int) * (S + 1)));
+        YTA_HIP(hipHostMalloc((void **)&p.h_off, sizeof(int) * (S + 1), hipHostMallocDefault));
+        YTA_HIP(hipMalloc((void **)&p.d_pack_off, sizeof(int) * (S + 1)));
+        YTA_HIP(hipHostMalloc((void **)&p.h_pack_off, sizeof(int) * (S + 1),
+                              hipHostMallocDefault));
+        YTA_HIP(hipMalloc((void **)&p.d_cnt, sizeof(BtCounters) * S));
+        YTA_HIP(hipHostMalloc((void **)&p.h_cnt, sizeof(BtCounters) * S, hipHostMallocDefault));
+        YTA_HIP(hipHostMalloc((void **)&p.h_nid, sizeof(long long) * S, hipHostMallocDefault));
+    }
+    if (dets > p.in_cap) {   // detections and packed rows: both bounded by the frame's dets
+        for (void *d : {(void *)p.d_in, (void *)p.d_pack})
+            if (d) (void)hipFree(d);
+        for (void *h : {(void *)p.h_in, (void *)p.h_pack})
+            if (h) (void)hipHostFree(h);
+        p.d_in = p.h_in = p.d_pack = p.h_pack = nullptr;
+        p.in_cap = p.pack_cap = 0;
+        const long long cap = std::max<long long>(dets + dets / 8, 1024);
+        YTA_HIP(hipMalloc((void **)&p.d_in, sizeof(double) * 6 * cap));
+        YTA_HIP(hipHostMalloc((void **)&p.h_in, sizeof(double) * 6 * cap, hipHostMallocDefault));
+        YTA_HIP(hipMalloc((void **)&p.d_pack, sizeof(double) * 8 * cap));
+        YTA_HIP(hipHostMalloc((void **)&p.h_pack, sizeof(double) * 8 * cap,
+                              hipHostMallocDefault));
+        p.in_cap = p.pack_cap = cap;
+    }
+    return YTA_OK;
+}
+
+int pipe_submit(yta_bytetrack *e, const double *dets, const int *det_offsets,
+                const long long *next_id, double *out, long long out_capacity) {
+    YTA_CHECK(e && det_offsets, YTA_ERR_INVALID, "null argument");
+    YTA_CHECK(e->variant == VAR_BYTETRACK, YTA_ERR_INVALID, "pipelined updates: ByteTrack engines");
+    YTA_HIP(hipSetDevice(e->device));
+    YTA_CHECK(e->pipe_count < 2, YTA_ERR_INVALID, "two frames in flight: collect one first");
+    const int S = e->S;
+    YTA_CHECK(det_offsets[0] == 0, YTA_ERR_INVALID, "det_offsets[0] must be 0");
+    const long long total = det_offsets[S];
+    YTA_CHECK(total == 0 || dets, YTA_ERR_INVALID, "null dets");
+    YTA_CHECK(out_capacity >= total && (total == 0 || out), YTA_ERR_CAPACITY,
+              "out holds %lld rows, the frame needs det_offsets[S] = %lld", out_capacity, total);
+    // capacity: the live tracks of the last collected frame plus every detection of the frames in
+    // flight and of this one bound each stream's tracked + lost lists
+    int need_d = e->MAXD, need_c = e->CAP;
+    bool grow = false;
+    for (int s = 0; s < S; ++s) {
+        const int m = det_offsets[s + 1] - det_offsets[s];
+        YTA_CHECK(m >= 0, YTA_ERR_INVALID, "det_offsets must be non-decreasing");
+        need_d = std::max(need_d, m);
+        long long bound = (long long)e->h_cnt[s].n_tracked + e->h_cnt[s].n_lost + m;
+        for (int k = 0; k < e->pipe_count; ++k) {
+            const auto &q = e->pipe[(e->pipe_head + k) % 2];
+            bound += q.h_off[s + 1] - q.h_off[s];
+        }
+        if (bound > e->CAP) grow = true;
+    }
+    if (grow || need_d > e->MAXD) {   // drain the kernels in flight, then the exact need
+        YTA_HIP(host_wait(e->stream));   // every frame in flight has run: a.cnt is current
+        std::vector<BtCounters> c(S);
+        YTA_HIP(hipMemcpy(c.data(), e->a.cnt, sizeof(BtCounters) * S, hipMemcpyDeviceToHost));
+        for (int s = 0; s < S; ++s)
+            need_c = std::max(need_c, c[s].n_tracked + c[s].n_lost +
+                                          (det_offsets[s + 1] - det_offsets[s]));
+        if (need_d > e->MAXD || need_c > e->CAP) {
+            const int rc = reserve(e, need_c > e->CAP ? std::max(need_c, 2 * e->CAP) : e->CAP,
+                                   need_d > e->MAXD ? std::max(need_d, 2 * e->MAXD) : e->MAXD);
+            if (rc) return rc;
+        }
+    }
+    auto &p = e->pipe[(e->pipe_head + e->pipe_count) % 2];
+    int rc = pipe_slot_ready(e, p, total);
+    if (rc) return rc;
+    // this slot's last frame was collected (its events completed): its buffers are free
+    memcpy(p.h_off, det_offsets, sizeof(int) * (S + 1));
+    YTA_HIP(hipMemcpyAsync(p.d_off, p.h_off, sizeof(int) * (S + 1), hipMemcpyHostToDevice,
+                           e->s_in));
+    if (total) {
+        const size_t bytes = sizeof(double) * 6 * total;
+        if (host_pinned(dets, bytes)) {   // straight from the caller (kept until collected)
+            YTA_HIP(hipMemcpyAsync(p.d_in, dets, bytes, hipMemcpyHostToDevice, e->s_in));
+        } else {   // staged: chunk k's DMA overlaps chunk k+1's host copy
+            const size_t ch = stage_chunk(bytes);
+            for (size_t o = 0; o < bytes; o += ch) {
+                const size_t n = std::min(ch, bytes - o);
+                par_copy(e, (char *)p.h_in + o, (const char *)dets + o, n);
+                YTA_HIP(hipMemcpyAsync((char *)p.d_in + o, (char *)p.h_in + o, n,
+                                       hipMemcpyHostToDevice, e->s_in));
+            }
+        }
+    }
+    YTA_HIP(hipEventRecord(p.in_done, e->s_in));
+    // compute stream: the frame, then its rows and counters snapshotted into the slot
+    YTA_HIP(hipStreamWaitEvent(e->stream, p.in_done, 0));
+    if (next_id) {
+        memcpy(p.h_nid, next_id, sizeof(long long) * S);
+        YTA_HIP(hipMemcpy2DAsync(&e->a.cnt[0].next_id, sizeof(BtCounters), p.h_nid,
+                                 sizeof(long long), sizeof(long long), S, hipMemcpyHostToDevice,
+                                 e->stream));
+    }
+    rc = launch_pipeline(e, p.d_in, p.d_off, e->a.out, nullptr);
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_out_offsets_scan, dim3(1), dim3(OFFS_T), 0, e->stream, e->a.cnt, S,
+                       e->CAP, p.d_pack_off);
+    hipLaunchKernelGGL(k_pack_out, dim3(S), dim3(256), 0, e->stream, e->a.out, (long long)e->CAP,
+                       p.d_pack_off, p.d_pack);
+    YTA_HIP(hipGetLastError());
+    YTA_HIP(hipMemcpyAsync(p.d_cnt, e->a.cnt, sizeof(BtCounters) * S, hipMemcpyDeviceToDevice,
+                           e->stream));
+    YTA_HIP(hipEventRecord(p.kern_done, e->stream));
+    // copy-out stream: counters, offsets and at most det_offsets[S] rows (every output row is a
+    // track matched to or born from one of the frame's detections)
+    YTA_HIP(hipStreamWaitEvent(e->s_out, p.kern_done, 0));
+    YTA_HIP(hipMemcpyAsync(p.h_cnt, p.d_cnt, sizeof(BtCounters) * S, hipMemcpyDeviceToHost,
+                           e->s_out));
+    YTA_HIP(hipMemcpyAsync(p.h_pack_off, p.d_pack_off, sizeof(int) * (S + 1),
+                           hipMemcpyDeviceToHost, e->s_out));
+    p.user_out = out;
+    p.rows_bound = total;
+    p.direct_out = total > 0 && host_pinned(out, sizeof(double) * 8 * total);
+    if (total)
+        YTA_HIP(hipMemcpyAsync(p.direct_out ? out : p.h_pack, p.d_pack, sizeof(double) * 8 * total,
+                               hipMemcpyDeviceToHost, e->s_out));
+    YTA_HIP(hipEventRecord(p.out_done, e->s_out));
+    ++e->pipe_count;
+    return YTA_OK;
+}
+
+int pipe_collect(yta_bytetrack *e, long long *next_id, int *out_offsets) {
+    YTA_CHECK(e && out_offsets, YTA_ERR_INVALID, "null argument");
+    YTA_CHECK(e->pipe_count > 0, YTA_ERR_INVALID, "no frame in flight");
+    YTA_HIP(hipSetDevice(e->device));
+    auto &p = e->pipe[e->pipe_head];
+    e->pipe_head = (e->pipe_head + 1) % 2;
+    --e->pipe_count;
+    YTA_HIP(hipEventSynchronize(p.out_done));
+    const int S = e->S;
+    memcpy(e->h_cnt, p.h_cnt, sizeof(BtCounters) * S);   // the latest known counters
+    if (next_id)
+        for (int s = 0; s < S; ++s) next_id[s] = p.h_cnt[s].next_id;
+    const int rc = check_errors(e);
+    if (rc) return rc;
+    memcpy(out_offsets, p.h_pack_off, sizeof(int) * (S + 1));
+    const long long rows = out_offsets[S];
+    YTA_CHECK(rows <= p.rows_bound, YTA_ERR_HIP, "%lld output rows > %lld detections", rows,
+              p.rows_bound);
+    if (rows > 0 && !p.direct_out)
+        par_copy(e, p.user_out, p.h_pack, sizeof(double) * 8 * rows);
+    return YTA_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -2763,6 +2990,7 @@ int yta_bytetrack_destroy(yta_bytetrack *e) {
     if (e->h_feat) (void)hipHostFree(e->h_feat);
     if (e->d_feat_in) (void)hipFree(e->d_feat_in);
     if (e->h_active) (void)hipHostFree(e->h_active);
+    pipe_free(e);
     for (hipEvent_t h : e->ev) (void)hipEventDestroy(h);
     if (e->stream) (void)hipStreamDestroy(e->stream);
     delete e;
@@ -2771,6 +2999,7 @@ int yta_bytetrack_destroy(yta_bytetrack *e) {
 
 int yta_bytetrack_reset(yta_bytetrack *e) {
     YTA_CHECK(e, YTA_ERR_INVALID, "null engine");
+    YTA_CHECK(e->pipe_count == 0, YTA_ERR_INVALID, "pipelined frames in flight: collect them first");
     YTA_HIP(hipSetDevice(e->device));
     hipLaunchKernelGGL(k_reset, dim3(e->S), dim3(256), 0, e->stream, e->a, 0);
     YTA_HIP(hipGetLastError());
@@ -2784,6 +3013,7 @@ int yta_bytetrack_reset(yta_bytetrack *e) {
 
 int yta_bytetrack_reset_stream(yta_bytetrack *e, int stream) {
     YTA_CHECK(e, YTA_ERR_INVALID, "null engine");
+    YTA_CHECK(e->pipe_count == 0, YTA_ERR_INVALID, "pipelined frames in flight: collect them first");
     YTA_CHECK(stream >= 0 && stream < e->S, YTA_ERR_INVALID, "stream %d outside 0..%d", stream,
               e->S - 1);
     YTA_HIP(hipSetDevice(e->device));
@@ -2800,6 +3030,7 @@ int yta_bytetrack_reset_stream(yta_bytetrack *e, int stream) {
 
 int yta_bytetrack_reserve(yta_bytetrack *e, int track_capacity, int max_dets) {
     YTA_CHECK(e, YTA_ERR_INVALID, "null engine");
+    YTA_CHECK(e->pipe_count == 0, YTA_ERR_INVALID, "pipelined frames in flight: collect them first");
     YTA_HIP(hipSetDevice(e->device));
     return reserve(e, track_capacity, max_dets);
 }
@@ -2837,6 +3068,15 @@ int yta_bytetrack_update_device_masked(yta_bytetrack *e, const int *d_active,
     const int rc = launch_pipeline(e, d_dets, d_det_offsets, d_out, d_out_counts);
     e->a.active = nullptr;
     return rc;
+}
+
+int yta_bytetrack_submit(yta_bytetrack *e, const double *dets, const int *det_offsets,
+                         const long long *next_id, double *out, int out_capacity) {
+    return pipe_submit(e, dets, det_offsets, next_id, out, out_capacity);
+}
+
+int yta_bytetrack_collect(yta_bytetrack *e, long long *next_id, int *out_offsets) {
+    return pipe_collect(e, next_id, out_offsets);
 }
 
 int yta_bytetrack_sync(yta_bytetrack *e) {

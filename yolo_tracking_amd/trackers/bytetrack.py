@@ -139,6 +139,41 @@ class ByteTrackEngine:
             nid_user[order] = nid
         return res
 
+    def submit(self, dets_per_stream, out=None):
+        """Pipelined update, first half (yta_bytetrack_submit): enqueue one frame of every stream
+        and return at once; at most two frames in flight.  The engine's own ID counters are used.
+        out: optional float64 (>= total dets, 8) buffer the matching collect() fills (kept alive
+        here until then).  Returns nothing; collect() returns the oldest submitted frame."""
+        assert len(dets_per_stream) == self.n_streams
+        off = np.zeros(self.n_streams + 1, dtype=np.int32)
+        np.cumsum([len(d) for d in dets_per_stream], out=off[1:])
+        packed = (np.ascontiguousarray(np.concatenate(
+            [np.asarray(d, dtype=np.float64).reshape(-1, 6) for d in dets_per_stream]))
+            if off[-1] else np.zeros((0, 6)))
+        need = max(int(off[-1]), 1)
+        if out is None or len(out) < need:
+            out = np.empty((need, 8), dtype=np.float64)
+        _lib.check(self.lib.yta_bytetrack_submit(self._h, _lib.ptr(packed), _lib.ptr(off), None,
+                                                 _lib.ptr(out), len(out)))
+        if not hasattr(self, "_inflight"):
+            self._inflight = []
+        self._inflight.append((packed, out))   # the buffers must outlive the DMA
+
+    def collect(self, next_id=None):
+        """Pipelined update, second half: the oldest submitted frame's S (K_s, 8) arrays.
+        next_id: optional int64 (S,) array receiving the counters after that frame."""
+        if not getattr(self, "_inflight", None):
+            raise _lib.YTAError("collect(): no frame in flight")
+        o = np.zeros(self.n_streams + 1, dtype=np.int32)
+        nid = None if next_id is None else np.zeros(self.n_streams, np.int64)
+        try:
+            _lib.check(self.lib.yta_bytetrack_collect(self._h, _lib.ptr(nid), _lib.ptr(o)))
+        finally:
+            _, out = self._inflight.pop(0)
+        if next_id is not None:
+            next_id[...] = nid
+        return [out[o[s]:o[s + 1]].copy() for s in range(self.n_streams)]
+
     def state(self, stream=0):
         """Live tracks of one stream (tracked list then lost list) for parity checks."""
         cap, _ = self.capacity()
