@@ -321,6 +321,21 @@ int yta_ocsort_update(yta_ocsort *engine, const double *dets, const int *det_off
 int yta_ocsort_update_device(yta_ocsort *engine, const double *d_dets, const int *d_det_offsets,
                              const int *d_img_wh, double *d_out, int *d_out_counts);
 int yta_ocsort_sync(yta_ocsort *engine);
+/* Stream subsets (see yta_bytetrack_update_streams): the listed streams (ascending ids) updated,
+ * every other stream left exactly as it was; per-stream arguments (dets, img_wh n x 2, next_id,
+ * out_offsets n + 1) cover the listed streams in id order.  The device form takes an [S] mask on
+ * the device (nonzero = update; skipped streams report 0 rows).  reset_stream: one stream back to
+ * a freshly constructed tracker (ocsort.py:188-216), the others untouched.  The same three calls
+ * exist for DeepOCSORT (feats of the listed streams' kept detections, warps n x 6) and
+ * HybridSORT (feats of the listed streams' rows). */
+int yta_ocsort_update_streams(yta_ocsort *engine, int n_streams, const int *stream_ids,
+                              const double *dets, const int *det_offsets, const int *img_wh,
+                              long long *next_id, double *out, int out_capacity,
+                              int *out_offsets);
+int yta_ocsort_update_device_masked(yta_ocsort *engine, const int *d_active, const double *d_dets,
+                                    const int *d_det_offsets, const int *d_img_wh, double *d_out,
+                                    int *d_out_counts);
+int yta_ocsort_reset_stream(yta_ocsort *engine, int stream);
 /* Parity introspection, tracker-list order: ints 7 x int64 per tracker (id, age, hits,
  * hit_streak, time_since_update, kf.observed, kf.attr_saved is not None), x (7 f64), P (49 f64). */
 int yta_ocsort_get_state(yta_ocsort *engine, int stream, int *n_tracks, long long *ints,
@@ -385,6 +400,17 @@ int yta_deepocsort_update_device(yta_deepocsort *engine, const double *d_dets,
                                  const double *d_warps, const int *d_img_wh, double *d_out,
                                  int *d_out_counts);
 int yta_deepocsort_sync(yta_deepocsort *engine);
+/* Stream subsets and per-stream reset: as yta_ocsort_update_streams / _update_device_masked /
+ * _reset_stream (deep_ocsort.py:308-347 for a fresh tracker). */
+int yta_deepocsort_update_streams(yta_deepocsort *engine, int n_streams, const int *stream_ids,
+                                  const double *dets, const int *det_offsets, const float *feats,
+                                  const double *warps, const int *img_wh, long long *next_id,
+                                  double *out, int out_capacity, int *out_offsets);
+int yta_deepocsort_update_device_masked(yta_deepocsort *engine, const int *d_active,
+                                        const double *d_dets, const int *d_det_offsets,
+                                        const float *d_feats, const double *d_warps,
+                                        const int *d_img_wh, double *d_out, int *d_out_counts);
+int yta_deepocsort_reset_stream(yta_deepocsort *engine, int stream);
 /* Parity introspection, tracker-list order: ints 7 x int64 per tracker (id, age, hits,
  * hit_streak, time_since_update, kf.observed, frozen), x (8 f64), P (64 f64), emb (feat_dim f64
  * per tracker; may be NULL). */
@@ -444,6 +470,16 @@ int yta_hybridsort_update_device(yta_hybridsort *engine, const double *d_dets,
                                  const int *d_det_offsets, const float *d_feats, double *d_out,
                                  int *d_out_counts);
 int yta_hybridsort_sync(yta_hybridsort *engine);
+/* Stream subsets and per-stream reset: as yta_ocsort_update_streams / _update_device_masked /
+ * _reset_stream (hybridsort.py:329-361 for a fresh tracker). */
+int yta_hybridsort_update_streams(yta_hybridsort *engine, int n_streams, const int *stream_ids,
+                                  const double *dets, const int *det_offsets, const float *feats,
+                                  long long *next_id, double *out, int out_capacity,
+                                  int *out_offsets);
+int yta_hybridsort_update_device_masked(yta_hybridsort *engine, const int *d_active,
+                                        const double *d_dets, const int *d_det_offsets,
+                                        const float *d_feats, double *d_out, int *d_out_counts);
+int yta_hybridsort_reset_stream(yta_hybridsort *engine, int stream);
 /* Parity introspection, tracker-list order: ints 6 x int64 per tracker (id, age, hits,
  * hit_streak, time_since_update, kf.observed), dbl 3 x f64 (conf, cls, det_ind), x (9 f64),
  * P (81 f64), feat (feat_dim float32 smooth_feat per tracker; may be NULL). */

@@ -174,3 +174,89 @@ def test_subset_rejects_bad_stream_ids():
         eng.update([d], streams=[3])
     with pytest.raises(_lib.YTAError):
         eng.reset_stream(5)
+
+
+# ------------------------------------------------------------------ OCSORT family
+OC_KW = dict(det_thresh=0.0, max_age=30, min_hits=1, asso_threshold=0.3, delta_t=3,
+             asso_func="giou", inertia=0.2, use_byte=False)
+DOC_KW = dict(det_thresh=0.0, max_age=30, min_hits=1, iou_threshold=0.3, delta_t=3,
+              asso_func="giou", inertia=0.2, w_association_emb=0.75, alpha_fixed_emb=0.95,
+              aw_param=0.5, embedding_off=False, cmc_off=False, aw_off=False)
+HS_KW = dict(det_thresh=0.0, max_age=30, min_hits=1, iou_threshold=0.3, delta_t=3,
+             asso_func="giou", inertia=0.2)
+
+
+def _family(kind, S, D=32):
+    if kind == "ocsort":
+        from yolo_tracking_amd.trackers.ocsort import OCSortEngine
+        return lambda n: OCSortEngine(n, **OC_KW)
+    if kind == "deepocsort":
+        from yolo_tracking_amd.trackers.deepocsort import DeepOCSortEngine
+        return lambda n: DeepOCSortEngine(n, feat_dim=D, **DOC_KW)
+    from yolo_tracking_amd.trackers.hybridsort import HybridSortEngine
+    return lambda n: HybridSortEngine(n, feat_dim=D, **HS_KW)
+
+
+def _family_inputs(kind, frame):
+    d, e = frame
+    if kind == "ocsort":
+        return d, None
+    f = e if kind == "hybridsort" else e[d[:, 4] > 0.0]
+    return d, f / np.linalg.norm(f)
+
+
+def _family_call(kind, eng, dets, feats, warps, shapes, nid, streams=None):
+    if kind == "ocsort":
+        return eng.update(dets, shapes, next_id=nid, streams=streams)
+    if kind == "deepocsort":
+        return eng.update(dets, feats, warps=warps, img_shapes=shapes, next_id=nid,
+                          streams=streams)
+    return eng.update(dets, feats, next_id=nid, streams=streams)
+
+
+@pytest.mark.parametrize("kind", ["ocsort", "deepocsort", "hybridsort"])
+def test_ocsort_family_subset_and_reset(kind):
+    """Random stream subsets (and one reset_stream) against one-stream engines fed each stream's
+    own frames: rows and ID counters bit-identical, skipped streams' states untouched."""
+    S, F, D = 3, 16, 32
+    shape = (1400, 1400, 3)
+    frames = [make_frames(100 + 20 * s, F, seed=900 + s, emb_dim=D, low_conf_frac=0.0,
+                          drop_frac=0.05, canvas=1400.0) for s in range(S)]
+    warp = np.array([[1.0, 1e-3, 0.5], [-1e-3, 1.0, -0.3]])
+    make = _family(kind, S, D)
+    eng = make(S)
+    solo = [make(1) for _ in range(S)]
+    nid_solo = [np.zeros(1, np.int64) + (1 if kind == "deepocsort" else 0) for _ in range(S)]
+    nid = np.array([int(v[0]) for v in nid_solo])
+    rng = np.random.default_rng(21)
+    pos = [0] * S
+    reset_done = False
+    for step in range(3 * F):
+        ids = [int(i) for i in rng.permutation(S)[:int(rng.integers(1, S + 1))] if pos[i] < F]
+        if not ids:
+            continue
+        if not reset_done and min(pos) >= 6:   # stream 1 restarts as a fresh tracker
+            eng.reset_stream(1)
+            solo[1] = make(1)
+            nid_solo[1][:] = 1 if kind == "deepocsort" else 0
+            nid[1] = nid_solo[1][0]
+            reset_done = True
+        skipped = [s for s in range(S) if s not in ids]
+        before = {s: eng.state(s) for s in skipped}
+        ins = [_family_inputs(kind, frames[s][pos[s]]) for s in ids]
+        dets = [x[0] for x in ins]
+        feats = [x[1] for x in ins]
+        warps = np.stack([warp if (s + pos[s]) % 2 else np.eye(2, 3) for s in ids])
+        sub_nid = nid[ids].copy()
+        outs = _family_call(kind, eng, dets, feats, warps, [shape] * len(ids), sub_nid, ids)
+        nid[ids] = sub_nid
+        for k, s in enumerate(ids):
+            exp = _family_call(kind, solo[s], [dets[k]], [feats[k]], warps[k:k + 1], [shape],
+                               nid_solo[s])[0]
+            assert np.array_equal(outs[k], exp), (kind, step, s, pos[s])
+            assert nid[s] == nid_solo[s][0], (kind, step, s)
+            pos[s] += 1
+        for s in skipped:
+            after = eng.state(s)
+            assert all(np.array_equal(before[s][k], after[k]) for k in after), (kind, step, s)
+    assert reset_done and min(pos) > 8

@@ -140,6 +140,9 @@ _SIGS = {
     "yta_ocsort_capacity": ([_P, _P, _P], _I),
     "yta_ocsort_update": ([_P, _P, _P, _P, _P, _P, _I, _P], _I),
     "yta_ocsort_update_device": ([_P, _P, _P, _P, _P, _P], _I),
+    "yta_ocsort_update_streams": ([_P, _I, _P, _P, _P, _P, _P, _P, _I, _P], _I),
+    "yta_ocsort_update_device_masked": ([_P, _P, _P, _P, _P, _P, _P], _I),
+    "yta_ocsort_reset_stream": ([_P, _I], _I),
     "yta_ocsort_sync": ([_P], _I),
     "yta_ocsort_get_state": ([_P, _I, _P, _P, _P, _P], _I),
     "yta_ocsort_stats": ([_P, _P], _I),
@@ -152,6 +155,9 @@ _SIGS = {
     "yta_deepocsort_capacity": ([_P, _P, _P], _I),
     "yta_deepocsort_update": ([_P, _P, _P, _P, _P, _P, _P, _P, _I, _P], _I),
     "yta_deepocsort_update_device": ([_P, _P, _P, _P, _P, _P, _P, _P], _I),
+    "yta_deepocsort_update_streams": ([_P, _I, _P, _P, _P, _P, _P, _P, _P, _P, _I, _P], _I),
+    "yta_deepocsort_update_device_masked": ([_P, _P, _P, _P, _P, _P, _P, _P, _P], _I),
+    "yta_deepocsort_reset_stream": ([_P, _I], _I),
     "yta_deepocsort_sync": ([_P], _I),
     "yta_deepocsort_get_state": ([_P, _I, _P, _P, _P, _P, _P], _I),
     "yta_deepocsort_stats": ([_P, _P], _I),
@@ -164,6 +170,9 @@ _SIGS = {
     "yta_hybridsort_capacity": ([_P, _P, _P], _I),
     "yta_hybridsort_update": ([_P, _P, _P, _P, _P, _P, _I, _P], _I),
     "yta_hybridsort_update_device": ([_P, _P, _P, _P, _P, _P], _I),
+    "yta_hybridsort_update_streams": ([_P, _I, _P, _P, _P, _P, _P, _P, _I, _P], _I),
+    "yta_hybridsort_update_device_masked": ([_P, _P, _P, _P, _P, _P, _P], _I),
+    "yta_hybridsort_reset_stream": ([_P, _I], _I),
     "yta_hybridsort_sync": ([_P], _I),
     "yta_hybridsort_get_state": ([_P, _I, _P, _P, _P, _P, _P, _P], _I),
     "yta_hybridsort_classes": ([_P, _I, _P, _I, _P], _I),

@@ -25,6 +25,7 @@
 #include "kf_deep.hpp"
 #include "kf_ocsort.hpp"
 #include "ocsort_common.hpp"
+#include "subset.hpp"
 
 namespace yta {
 namespace {
@@ -94,6 +95,7 @@ struct DocArgs {
     int *pre_x;
     double *out;
     int *out_counts;
+    const int *active;             // [S] nonzero = update the stream this frame; null = all
 };
 
 __device__ __forceinline__ long long doc_mb(const DocArgs &a, int s) {
@@ -274,6 +276,7 @@ __device__ void doc_birth(DocTrack &out, const double *dr, long long id, int det
 constexpr int DOC_TRK_T = 64;
 __global__ __launch_bounds__(DOC_TRK_T) void k_doc_predict(DocArgs a) {
     const int s = blockIdx.y;
+    if (a.active && !a.active[s]) return;   // stream not updated this frame
     const DocCounters *c = a.cnt + s;
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= c->n_trk) return;
@@ -291,6 +294,7 @@ __global__ __launch_bounds__(DOC_TRK_T) void k_doc_predict(DocArgs a) {
 __global__ __launch_bounds__(OC_T) void k_doc_pre(DocArgs a) {
     __shared__ OcShared sh;
     const int s = blockIdx.x, t = threadIdx.x, nt = blockDim.x;
+    if (a.active && !a.active[s]) return;   // stream not updated this frame
     DocCounters *c = a.cnt + s;
     const long long tb = (long long)s * a.CAP, db = (long long)s * a.MAXD;
     const long long ub = (long long)s * (a.MAXD + a.CAP);
@@ -362,6 +366,7 @@ __global__ __launch_bounds__(OC_T) void k_doc_pre(DocArgs a) {
 
 __global__ __launch_bounds__(OC_T) void k_doc_cost(DocArgs a) {
     const int s = blockIdx.y;
+    if (a.active && !a.active[s]) return;   // stream not updated this frame
     DocCounters *c = a.cnt + s;
     const int n_trk = c->n_trk, n_hi = c->n_high;
     const long long nm = (long long)n_hi * n_trk;
@@ -409,6 +414,7 @@ constexpr int DE_KC = 32, DE_LD = DE_KC + 1;
 __global__ __launch_bounds__(256) void k_doc_emb(DocArgs a) {
     __shared__ double As[EMB_TILE * DE_LD], Bs[EMB_TILE * DE_LD];
     const int s = blockIdx.z;
+    if (a.active && !a.active[s]) return;   // stream not updated this frame
     const DocCounters *c = a.cnt + s;
     const int n_trk = c->n_trk, n_hi = c->n_high, D = a.D;
     int bx, by;
@@ -483,6 +489,7 @@ __global__ __launch_bounds__(256) void k_doc_emb(DocArgs a) {
 constexpr int AW_CHUNKS = 8;
 __global__ __launch_bounds__(256) void k_doc_aw(DocArgs a) {
     const int s = blockIdx.y;
+    if (a.active && !a.active[s]) return;   // stream not updated this frame
     const DocCounters *c = a.cnt + s;
     const int n_trk = c->n_trk, n_hi = c->n_high;
     const long long db = (long long)s * a.MAXD, mb = doc_mb(a, s);
@@ -540,6 +547,7 @@ __global__ __launch_bounds__(256) void k_doc_aw(DocArgs a) {
 }
 __global__ __launch_bounds__(256) void k_doc_aw_cols(DocArgs a) {
     const int s = blockIdx.y;
+    if (a.active && !a.active[s]) return;   // stream not updated this frame
     const DocCounters *c = a.cnt + s;
     const int n_trk = c->n_trk, n_hi = c->n_high;
     const int cc = blockIdx.x * blockDim.x + threadIdx.x;
@@ -557,6 +565,7 @@ __global__ __launch_bounds__(256) void k_doc_aw_cols(DocArgs a) {
 // emb * w (aw_off), emb zeroed where iou <= 0.
 __global__ __launch_bounds__(256) void k_doc_final(DocArgs a) {
     const int s = blockIdx.y;
+    if (a.active && !a.active[s]) return;   // stream not updated this frame
     const DocCounters *c = a.cnt + s;
     const int n_trk = c->n_trk, n_hi = c->n_high;
     const long long nm = (long long)n_hi * n_trk;
@@ -580,6 +589,7 @@ __global__ __launch_bounds__(256) void k_doc_final(DocArgs a) {
 // Row pre-pass of the first-round solve, chip-wide (lap_rect.hpp).
 __global__ __launch_bounds__(OC_T) void k_doc_rowpre(DocArgs a) {
     const int s = blockIdx.y;
+    if (a.active && !a.active[s]) return;   // stream not updated this frame
     const DocCounters *c = a.cnt + s;
     const long long db = (long long)s * a.MAXD;
     main_lap_pre(a.mat2 + doc_mb(a, s), c->n_high, c->n_trk, a.pre_u + db, a.pre_x + db,
@@ -590,6 +600,7 @@ __global__ __launch_bounds__(OC_T) void k_doc_rowpre(DocArgs a) {
 __global__ __launch_bounds__(LAP_T) void k_doc_lap(DocArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const int s = blockIdx.x;
+    if (a.active && !a.active[s]) return;   // stream not updated this frame
     DocCounters *c = a.cnt + s;
     const long long tb = (long long)s * a.CAP, db = (long long)s * a.MAXD;
     first_round_lap(a.mat2 + doc_mb(a, s), c->n_high, c->n_trk, a.rmatch + db, a.cmatched + tb, true,
@@ -602,6 +613,7 @@ __global__ __launch_bounds__(OC_T) void k_doc_assoc(DocArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     __shared__ OcShared sh;
     const int s = blockIdx.x, t = threadIdx.x, nt = blockDim.x;
+    if (a.active && !a.active[s]) return;   // stream not updated this frame
     DocCounters *c = a.cnt + s;
     const long long tb = (long long)s * a.CAP, db = (long long)s * a.MAXD, mb = doc_mb(a, s);
     const long long ub = (long long)s * (a.MAXD + a.CAP);
@@ -741,6 +753,7 @@ __global__ __launch_bounds__(OC_T) void k_doc_assoc(DocArgs a) {
 // own record.
 __global__ __launch_bounds__(DOC_TRK_T) void k_doc_upd(DocArgs a) {
     const int s = blockIdx.y;
+    if (a.active && !a.active[s]) return;   // stream not updated this frame
     const DocCounters *c = a.cnt + s;
     const int j = blockIdx.x * DOC_TRK_T + threadIdx.x;
     if (j >= c->n_trk) return;
@@ -756,6 +769,13 @@ __global__ __launch_bounds__(DOC_TRK_T) void k_doc_upd(DocArgs a) {
 __global__ __launch_bounds__(OC_T) void k_doc_finish(DocArgs a) {
     __shared__ OcShared sh;
     const int s = blockIdx.x, t = threadIdx.x, nt = blockDim.x;
+    if (a.active && !a.active[s]) {   // not updated this frame: no output rows
+        if (threadIdx.x == 0) {
+            a.cnt[s].n_out = 0;
+            if (a.out_counts) a.out_counts[s] = 0;
+        }
+        return;
+    }
     DocCounters *c = a.cnt + s;
     const long long tb = (long long)s * a.CAP, db = (long long)s * a.MAXD;
     const long long ub = (long long)s * (a.MAXD + a.CAP);
@@ -838,6 +858,7 @@ __global__ __launch_bounds__(OC_T) void k_doc_finish(DocArgs a) {
 // detection's row).  One wave per job.
 __global__ __launch_bounds__(256) void k_doc_ema(DocArgs a) {
     const int s = blockIdx.y, lane = lane_id();
+    if (a.active && !a.active[s]) return;   // stream not updated this frame
     const DocCounters *c = a.cnt + s;
     const int job = blockIdx.x * 4 + threadIdx.x / WAVE;
     if (job >= c->n_ema) return;
@@ -885,8 +906,8 @@ __global__ void k_kf8_run(int n, int steps, int dt, const double *b0, const doub
             for (int b1 = 0; b1 < 4; ++b1) M[dk_glob(g, a0) * 8 + dk_glob(g, b1)] = r.kf.p[g][4 * a0 + b1];
 }
 
-__global__ void k_doc_reset(DocArgs a) {
-    const int s = blockIdx.x;
+__global__ void k_doc_reset(DocArgs a, int s0) {
+    const int s = s0 + blockIdx.x;
     const long long tb = (long long)s * a.CAP;
     for (int i = threadIdx.x; i < a.CAP; i += blockDim.x) a.free_list[tb + i] = a.CAP - 1 - i;
     if (threadIdx.x == 0) {
@@ -918,6 +939,7 @@ struct yta_deepocsort {
     double *h_warp = nullptr, *d_warp = nullptr;
     DocCounters *h_cnt = nullptr;
     size_t lds = 0;
+    StreamMask mask;   // stream-subset updates (subset.hpp)
 };
 
 namespace {
@@ -1037,6 +1059,10 @@ int doc_launch(yta_deepocsort *e, const double *d_dets, const int *d_off, const 
     a.img_wh = d_wh;
     a.out = out;
     a.out_counts = out_counts;
+    {
+        const int mrc = e->mask.stage(a.S, e->stream, &a.active);
+        if (mrc) return mrc;
+    }
     hipLaunchKernelGGL(k_doc_predict, dim3((a.CAP + DOC_TRK_T - 1) / DOC_TRK_T, a.S), dim3(DOC_TRK_T), 0,
                        e->stream, a);
     YTA_HIP(hipGetLastError());
@@ -1238,6 +1264,7 @@ int yta_deepocsort_destroy(yta_deepocsort *e) {
     (void)hipSetDevice(e->device);
     if (e->stream) (void)host_wait(e->stream);
     doc_release(e);
+    e->mask.release();
     if (e->h_dets) (void)hipHostFree(e->h_dets);
     if (e->d_det_in) (void)hipFree(e->d_det_in);
     if (e->h_feat) (void)hipHostFree(e->h_feat);
@@ -1250,7 +1277,7 @@ int yta_deepocsort_destroy(yta_deepocsort *e) {
 int yta_deepocsort_reset(yta_deepocsort *e) {
     YTA_CHECK(e, YTA_ERR_INVALID, "null engine");
     YTA_HIP(hipSetDevice(e->device));
-    hipLaunchKernelGGL(k_doc_reset, dim3(e->S), dim3(256), 0, e->stream, e->a);
+    hipLaunchKernelGGL(k_doc_reset, dim3(e->S), dim3(256), 0, e->stream, e->a, 0);
     YTA_HIP(hipGetLastError());
     YTA_HIP(host_wait(e->stream));
     memset(e->h_cnt, 0, sizeof(DocCounters) * e->S);
@@ -1512,5 +1539,60 @@ int yta_deepocsort_debug_stamps(unsigned long long *out) {
     return YTA_OK;
 }
 #endif
+
+
+// ---- stream subsets (subset.hpp): the listed streams updated, every other stream untouched
+int yta_deepocsort_reset_stream(yta_deepocsort *e, int stream) {
+    YTA_CHECK(e, YTA_ERR_INVALID, "null engine");
+    YTA_CHECK(stream >= 0 && stream < e->S, YTA_ERR_INVALID, "stream %d outside 0..%d", stream,
+              e->S - 1);
+    YTA_HIP(hipSetDevice(e->device));
+    hipLaunchKernelGGL(k_doc_reset, dim3(1), dim3(256), 0, e->stream, e->a, stream);
+    YTA_HIP(hipGetLastError());
+    YTA_HIP(host_wait(e->stream));
+    return doc_read_counters(e);
+}
+
+int yta_deepocsort_update_device_masked(yta_deepocsort *e, const int *d_active, const double *d_dets, const int *d_det_offsets, const float *d_feats, const double *d_warps, const int *d_img_wh, double *d_out, int *d_out_counts) {
+    YTA_CHECK(e, YTA_ERR_INVALID, "null engine");
+    e->mask.req_dev = d_active;
+    const int rc = yta_deepocsort_update_device(e, d_dets, d_det_offsets, d_feats, d_warps, d_img_wh, d_out, d_out_counts);
+    e->mask.req_dev = nullptr;
+    return rc;
+}
+
+int yta_deepocsort_update_streams(yta_deepocsort *e, int n_streams, const int *stream_ids, const double *dets, const int *det_offsets, const float *feats, const double *warps, const int *img_wh,
+                           long long *next_id, double *out, int out_capacity, int *out_offsets) {
+    YTA_CHECK(e && out_offsets, YTA_ERR_INVALID, "null argument");
+    YTA_HIP(hipSetDevice(e->device));
+    const int S = e->S;
+    std::vector<int> mask, off, full_oo(S + 1, 0);
+    int rc = subset_expand(S, n_streams, stream_ids, det_offsets, mask, off);
+    if (rc) return rc;
+    std::vector<long long> nid(S);
+    if (next_id) {   // the skipped streams keep their device counters: read them first
+        rc = doc_read_counters(e);
+        if (rc) return rc;
+        for (int s = 0; s < S; ++s) nid[s] = e->h_cnt[s].next_id;
+        for (int k = 0; k < n_streams; ++k) nid[stream_ids[k]] = next_id[k];
+    }
+    std::vector<int> wh;
+    if (img_wh) wh = subset_spread<int>(S, n_streams, stream_ids, img_wh, 2, 1);
+    std::vector<double> w;
+    if (warps) {
+        w = subset_spread<double>(S, n_streams, stream_ids, warps, 6, 0.0);
+        for (int s = 0; s < S; ++s)
+            if (!mask[s]) w[6 * s] = w[6 * s + 4] = 1.0;   // identity for the skipped streams
+    }
+    e->mask.req_host = mask.data();
+    rc = yta_deepocsort_update(e, dets, off.data(), feats, warps ? w.data() : nullptr, img_wh ? wh.data() : nullptr, next_id ? nid.data() : nullptr, out,
+                        out_capacity, full_oo.data());
+    e->mask.req_host = nullptr;
+    if (next_id)
+        for (int k = 0; k < n_streams; ++k) next_id[k] = nid[stream_ids[k]];
+    if (rc) return rc;
+    subset_compact(n_streams, stream_ids, full_oo, out_offsets);
+    return YTA_OK;
+}
 
 }  // extern "C"

@@ -31,6 +31,7 @@
 #include "kf_hybrid.hpp"
 #include "kf_ocsort.hpp"   // np_sum5
 #include "ocsort_common.hpp"
+#include "subset.hpp"
 
 namespace yta {
 namespace {
@@ -109,6 +110,7 @@ struct HsArgs {
     int *pre_x;
     double *out;
     int *out_counts;
+    const int *active;             // [S] nonzero = update the stream this frame; null = all
 };
 
 __device__ __forceinline__ long long hs_mb(const HsArgs &a, int s) {
@@ -264,6 +266,7 @@ __device__ void hs_birth(HsTrack &out, const double *bbox, double cls, double de
 // One wave per block, as k_hs_upd (HS_UPD_T): the trackers spread over 4x the CUs.
 __global__ __launch_bounds__(64) void k_hs_predict(HsArgs a) {
     const int s = blockIdx.y;
+    if (a.active && !a.active[s]) return;   // stream not updated this frame
     HsCounters *c = a.cnt + s;
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= c->n_trk) return;
@@ -287,6 +290,7 @@ __global__ __launch_bounds__(64) void k_hs_predict(HsArgs a) {
 __global__ __launch_bounds__(OC_T) void k_hs_pre(HsArgs a) {
     __shared__ OcShared sh;
     const int s = blockIdx.x, t = threadIdx.x, nt = blockDim.x;
+    if (a.active && !a.active[s]) return;   // stream not updated this frame
     HsCounters *c = a.cnt + s;
     const long long tb = (long long)s * a.CAP, db = (long long)s * a.MAXD;
     const long long ub = (long long)s * (a.MAXD + a.CAP);
@@ -385,6 +389,7 @@ __global__ __launch_bounds__(256, 4) void k_hs_emb(HsArgs a) {
     __shared__ __attribute__((aligned(16))) HeLds L;
     __shared__ double nA[HE_TILE], nB[HE_TILE];
     const int s = blockIdx.z;
+    if (a.active && !a.active[s]) return;   // stream not updated this frame
     const HsCounters *c = a.cnt + s;
     const int n_trk = c->n_trk, n_hi = c->n_high, D = a.D;
     int bx, by;
@@ -554,6 +559,7 @@ __global__ __launch_bounds__(256, 4) void k_hs_emb(HsArgs a) {
 // Row pre-pass of the first-round solve, chip-wide (lap_rect.hpp).
 __global__ __launch_bounds__(OC_T) void k_hs_rowpre(HsArgs a) {
     const int s = blockIdx.y;
+    if (a.active && !a.active[s]) return;   // stream not updated this frame
     const HsCounters *c = a.cnt + s;
     const long long db = (long long)s * a.MAXD;
     main_lap_pre(a.cost + hs_mb(a, s), c->n_high, c->n_trk, a.pre_u + db, a.pre_x + db,
@@ -564,6 +570,7 @@ __global__ __launch_bounds__(OC_T) void k_hs_rowpre(HsArgs a) {
 __global__ __launch_bounds__(LAP_T) void k_hs_lap(HsArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const int s = blockIdx.x;
+    if (a.active && !a.active[s]) return;   // stream not updated this frame
     HsCounters *c = a.cnt + s;
     const long long tb = (long long)s * a.CAP, db = (long long)s * a.MAXD;
     first_round_lap(a.cost + hs_mb(a, s), c->n_high, c->n_trk, a.rmatch + db, a.cmatched + tb, false,
@@ -594,6 +601,7 @@ __device__ __forceinline__ bool hs_corrected(const HsArgs &a, int s, int i, int 
 constexpr int HS_UPD_T = 64;
 __global__ __launch_bounds__(HS_UPD_T) void k_hs_upd(HsArgs a) {
     const int s = blockIdx.y;
+    if (a.active && !a.active[s]) return;   // stream not updated this frame
     const HsCounters *c = a.cnt + s;
     const int n_trk = c->n_trk, n_hi = c->n_high;
     const int i = blockIdx.x * HS_UPD_T + threadIdx.x;
@@ -611,6 +619,13 @@ __global__ __launch_bounds__(OC_T) void k_hs_assoc(HsArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     __shared__ OcShared sh;
     const int s = blockIdx.x, t = threadIdx.x, nt = blockDim.x;
+    if (a.active && !a.active[s]) {   // not updated this frame: no output rows
+        if (threadIdx.x == 0) {
+            a.cnt[s].n_out = 0;
+            if (a.out_counts) a.out_counts[s] = 0;
+        }
+        return;
+    }
     HsCounters *c = a.cnt + s;
     const long long tb = (long long)s * a.CAP, db = (long long)s * a.MAXD, mb = hs_mb(a, s);
     const long long ub = (long long)s * (a.MAXD + a.CAP);
@@ -820,6 +835,7 @@ __device__ __forceinline__ float hs_f32_norm(double sumsq) { return sqrtf((float
 
 __global__ __launch_bounds__(256) void k_hs_ema(HsArgs a) {
     const int s = blockIdx.y, lane = lane_id();
+    if (a.active && !a.active[s]) return;   // stream not updated this frame
     const HsCounters *c = a.cnt + s;
     const int job = blockIdx.x * 4 + threadIdx.x / WAVE;
     if (job >= c->n_ema) return;
@@ -877,8 +893,8 @@ __global__ void k_kf9_run(int n, int steps, const double *b0, const double *b, d
     M[4 * 9 + 4] = r.kf.p[16];
 }
 
-__global__ void k_hs_reset(HsArgs a) {
-    const int s = blockIdx.x;
+__global__ void k_hs_reset(HsArgs a, int s0) {
+    const int s = s0 + blockIdx.x;
     const long long tb = (long long)s * a.CAP;
     for (int i = threadIdx.x; i < a.CAP; i += blockDim.x) a.free_list[tb + i] = a.CAP - 1 - i;
     if (threadIdx.x == 0) {
@@ -909,6 +925,7 @@ struct yta_hybridsort {
     int *h_off = nullptr, *d_off = nullptr;
     HsCounters *h_cnt = nullptr;
     size_t lds = 0;
+    StreamMask mask;   // stream-subset updates (subset.hpp)
 };
 
 namespace {
@@ -1007,6 +1024,10 @@ int hs_launch(yta_hybridsort *e, const double *d_dets, const int *d_off, const f
     a.det_feat = d_feat;
     a.out = out;
     a.out_counts = out_counts;
+    {
+        const int mrc = e->mask.stage(a.S, e->stream, &a.active);
+        if (mrc) return mrc;
+    }
     hipLaunchKernelGGL(k_hs_predict, dim3((a.CAP + 63) / 64, a.S), dim3(64), 0, e->stream, a);
     YTA_HIP(hipGetLastError());
     hipLaunchKernelGGL(k_hs_pre, dim3(a.S), dim3(OC_T), 0, e->stream, a);
@@ -1187,6 +1208,7 @@ int yta_hybridsort_destroy(yta_hybridsort *e) {
     (void)hipSetDevice(e->device);
     if (e->stream) (void)host_wait(e->stream);
     hs_release(e);
+    e->mask.release();
     if (e->h_dets) (void)hipHostFree(e->h_dets);
     if (e->d_det_in) (void)hipFree(e->d_det_in);
     if (e->h_feat) (void)hipHostFree(e->h_feat);
@@ -1199,7 +1221,7 @@ int yta_hybridsort_destroy(yta_hybridsort *e) {
 int yta_hybridsort_reset(yta_hybridsort *e) {
     YTA_CHECK(e, YTA_ERR_INVALID, "null engine");
     YTA_HIP(hipSetDevice(e->device));
-    hipLaunchKernelGGL(k_hs_reset, dim3(e->S), dim3(256), 0, e->stream, e->a);
+    hipLaunchKernelGGL(k_hs_reset, dim3(e->S), dim3(256), 0, e->stream, e->a, 0);
     YTA_HIP(hipGetLastError());
     YTA_HIP(host_wait(e->stream));
     memset(e->h_cnt, 0, sizeof(HsCounters) * e->S);
@@ -1465,5 +1487,53 @@ int yta_hs_debug_stamps_reset() {
     return YTA_OK;
 }
 #endif
+
+
+// ---- stream subsets (subset.hpp): the listed streams updated, every other stream untouched
+int yta_hybridsort_reset_stream(yta_hybridsort *e, int stream) {
+    YTA_CHECK(e, YTA_ERR_INVALID, "null engine");
+    YTA_CHECK(stream >= 0 && stream < e->S, YTA_ERR_INVALID, "stream %d outside 0..%d", stream,
+              e->S - 1);
+    YTA_HIP(hipSetDevice(e->device));
+    hipLaunchKernelGGL(k_hs_reset, dim3(1), dim3(256), 0, e->stream, e->a, stream);
+    YTA_HIP(hipGetLastError());
+    YTA_HIP(host_wait(e->stream));
+    return hs_read_counters(e);
+}
+
+int yta_hybridsort_update_device_masked(yta_hybridsort *e, const int *d_active, const double *d_dets, const int *d_det_offsets, const float *d_feats, double *d_out, int *d_out_counts) {
+    YTA_CHECK(e, YTA_ERR_INVALID, "null engine");
+    e->mask.req_dev = d_active;
+    const int rc = yta_hybridsort_update_device(e, d_dets, d_det_offsets, d_feats, d_out, d_out_counts);
+    e->mask.req_dev = nullptr;
+    return rc;
+}
+
+int yta_hybridsort_update_streams(yta_hybridsort *e, int n_streams, const int *stream_ids, const double *dets, const int *det_offsets, const float *feats,
+                           long long *next_id, double *out, int out_capacity, int *out_offsets) {
+    YTA_CHECK(e && out_offsets, YTA_ERR_INVALID, "null argument");
+    YTA_HIP(hipSetDevice(e->device));
+    const int S = e->S;
+    std::vector<int> mask, off, full_oo(S + 1, 0);
+    int rc = subset_expand(S, n_streams, stream_ids, det_offsets, mask, off);
+    if (rc) return rc;
+    std::vector<long long> nid(S);
+    if (next_id) {   // the skipped streams keep their device counters: read them first
+        rc = hs_read_counters(e);
+        if (rc) return rc;
+        for (int s = 0; s < S; ++s) nid[s] = e->h_cnt[s].next_id;
+        for (int k = 0; k < n_streams; ++k) nid[stream_ids[k]] = next_id[k];
+    }
+
+    e->mask.req_host = mask.data();
+    rc = yta_hybridsort_update(e, dets, off.data(), feats, next_id ? nid.data() : nullptr, out,
+                        out_capacity, full_oo.data());
+    e->mask.req_host = nullptr;
+    if (next_id)
+        for (int k = 0; k < n_streams; ++k) next_id[k] = nid[stream_ids[k]];
+    if (rc) return rc;
+    subset_compact(n_streams, stream_ids, full_oo, out_offsets);
+    return YTA_OK;
+}
 
 }  // extern "C"

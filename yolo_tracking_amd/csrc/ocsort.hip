@@ -29,6 +29,7 @@
 
 #include "kf_ocsort.hpp"
 #include "ocsort_common.hpp"
+#include "subset.hpp"
 
 namespace yta {
 namespace {
@@ -86,6 +87,7 @@ struct OcArgs {
     int *pre_x;
     double *out;                   // [S*CAP*8]
     int *out_counts;
+    const int *active;             // [S] nonzero = update the stream this frame; null = all
 };
 
 // k_previous_obs (ocsort.py:14-22) from the ring
@@ -171,6 +173,7 @@ __global__ __launch_bounds__(OC_T) void k_oc_pre(OcArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     __shared__ OcShared sh;
     const int s = blockIdx.x, t = threadIdx.x, nt = blockDim.x;
+    if (a.active && !a.active[s]) return;   // stream not updated this frame
     OcCounters *c = a.cnt + s;
     const long long tb = (long long)s * a.CAP, db = (long long)s * a.MAXD;
     const long long mb = (long long)s * (a.MAXD > 4 ? a.MAXD : 4) * a.CAP;
@@ -273,6 +276,7 @@ __global__ __launch_bounds__(OC_T) void k_oc_pre(OcArgs a) {
 // of asso > thr that decide the fast path (:156-159).
 __global__ __launch_bounds__(OC_T) void k_oc_cost(OcArgs a) {
     const int s = blockIdx.y;
+    if (a.active && !a.active[s]) return;   // stream not updated this frame
     OcCounters *c = a.cnt + s;
     const int n_trk = c->n_trk, n_hi = c->n_high;
     const long long nm = (long long)n_hi * n_trk;
@@ -315,6 +319,7 @@ __global__ __launch_bounds__(OC_T) void k_oc_cost(OcArgs a) {
 // chip-wide, so the stream block only walks the augmenting paths.
 __global__ __launch_bounds__(OC_T) void k_oc_rowpre(OcArgs a) {
     const int s = blockIdx.y;
+    if (a.active && !a.active[s]) return;   // stream not updated this frame
     const OcCounters *c = a.cnt + s;
     const long long db = (long long)s * a.MAXD;
     const long long mb = (long long)s * (a.MAXD > 4 ? a.MAXD : 4) * a.CAP;
@@ -325,6 +330,7 @@ __global__ __launch_bounds__(OC_T) void k_oc_rowpre(OcArgs a) {
 __global__ __launch_bounds__(LAP_T) void k_oc_lap(OcArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const int s = blockIdx.x;
+    if (a.active && !a.active[s]) return;   // stream not updated this frame
     OcCounters *c = a.cnt + s;
     const long long tb = (long long)s * a.CAP, db = (long long)s * a.MAXD;
     first_round_lap(a.mat2 + (long long)s * (a.MAXD > 4 ? a.MAXD : 4) * a.CAP, c->n_high, c->n_trk, a.rmatch + db, a.cmatched + tb, true,
@@ -337,6 +343,13 @@ __global__ __launch_bounds__(OC_T) void k_oc_assoc(OcArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     __shared__ OcShared sh;
     const int s = blockIdx.x, t = threadIdx.x, nt = blockDim.x;
+    if (a.active && !a.active[s]) {   // not updated this frame: no output rows
+        if (threadIdx.x == 0) {
+            a.cnt[s].n_out = 0;
+            if (a.out_counts) a.out_counts[s] = 0;
+        }
+        return;
+    }
     OcCounters *c = a.cnt + s;
     const long long tb = (long long)s * a.CAP, db = (long long)s * a.MAXD;
     const long long mb = (long long)s * (a.MAXD > 4 ? a.MAXD : 4) * a.CAP;
@@ -601,8 +614,8 @@ __global__ __launch_bounds__(OC_T) void k_oc_assoc(OcArgs a) {
     }
 }
 
-__global__ void k_oc_reset(OcArgs a) {
-    const int s = blockIdx.x;
+__global__ void k_oc_reset(OcArgs a, int s0) {
+    const int s = s0 + blockIdx.x;
     const long long tb = (long long)s * a.CAP;
     // births pop from the end of the free list: store it descending so slots fill from 0
     for (int i = threadIdx.x; i < a.CAP; i += blockDim.x) a.free_list[tb + i] = a.CAP - 1 - i;
@@ -631,6 +644,7 @@ struct yta_ocsort {
     int *h_off = nullptr, *d_off = nullptr, *h_wh = nullptr, *d_wh = nullptr;
     OcCounters *h_cnt = nullptr;
     size_t lds = 0;
+    StreamMask mask;   // stream-subset updates (subset.hpp)
 };
 
 namespace {
@@ -729,6 +743,10 @@ int oc_launch(yta_ocsort *e, const double *d_dets, const int *d_off, const int *
     a.img_wh = d_wh;
     a.out = out;
     a.out_counts = out_counts;
+    {
+        const int mrc = e->mask.stage(a.S, e->stream, &a.active);
+        if (mrc) return mrc;
+    }
     hipLaunchKernelGGL(k_oc_pre, dim3(a.S), dim3(OC_T), 0, e->stream, a);
     YTA_HIP(hipGetLastError());
     const long long per = ((long long)a.MAXD * a.CAP + OC_T - 1) / OC_T;
@@ -899,6 +917,7 @@ int yta_ocsort_destroy(yta_ocsort *e) {
     (void)hipSetDevice(e->device);
     if (e->stream) (void)host_wait(e->stream);
     oc_release(e);
+    e->mask.release();
     if (e->h_dets) (void)hipHostFree(e->h_dets);
     if (e->d_det_in) (void)hipFree(e->d_det_in);
     if (e->stream) (void)hipStreamDestroy(e->stream);
@@ -909,7 +928,7 @@ int yta_ocsort_destroy(yta_ocsort *e) {
 int yta_ocsort_reset(yta_ocsort *e) {
     YTA_CHECK(e, YTA_ERR_INVALID, "null engine");
     YTA_HIP(hipSetDevice(e->device));
-    hipLaunchKernelGGL(k_oc_reset, dim3(e->S), dim3(256), 0, e->stream, e->a);
+    hipLaunchKernelGGL(k_oc_reset, dim3(e->S), dim3(256), 0, e->stream, e->a, 0);
     YTA_HIP(hipGetLastError());
     YTA_HIP(host_wait(e->stream));
     memset(e->h_cnt, 0, sizeof(OcCounters) * e->S);
@@ -1109,6 +1128,55 @@ int yta_ocsort_debug_stamps(unsigned long long *out) {
 // and full P (49) per track.
 int yta_kf7_run(int device, int n, int steps, const double *z0, const double *z, double *x_out,
                 double *P_out);
+
+
+// ---- stream subsets (subset.hpp): the listed streams updated, every other stream untouched
+int yta_ocsort_reset_stream(yta_ocsort *e, int stream) {
+    YTA_CHECK(e, YTA_ERR_INVALID, "null engine");
+    YTA_CHECK(stream >= 0 && stream < e->S, YTA_ERR_INVALID, "stream %d outside 0..%d", stream,
+              e->S - 1);
+    YTA_HIP(hipSetDevice(e->device));
+    hipLaunchKernelGGL(k_oc_reset, dim3(1), dim3(256), 0, e->stream, e->a, stream);
+    YTA_HIP(hipGetLastError());
+    YTA_HIP(host_wait(e->stream));
+    return oc_read_counters(e);
+}
+
+int yta_ocsort_update_device_masked(yta_ocsort *e, const int *d_active, const double *d_dets, const int *d_det_offsets, const int *d_img_wh, double *d_out, int *d_out_counts) {
+    YTA_CHECK(e, YTA_ERR_INVALID, "null engine");
+    e->mask.req_dev = d_active;
+    const int rc = yta_ocsort_update_device(e, d_dets, d_det_offsets, d_img_wh, d_out, d_out_counts);
+    e->mask.req_dev = nullptr;
+    return rc;
+}
+
+int yta_ocsort_update_streams(yta_ocsort *e, int n_streams, const int *stream_ids, const double *dets, const int *det_offsets, const int *img_wh,
+                           long long *next_id, double *out, int out_capacity, int *out_offsets) {
+    YTA_CHECK(e && out_offsets, YTA_ERR_INVALID, "null argument");
+    YTA_HIP(hipSetDevice(e->device));
+    const int S = e->S;
+    std::vector<int> mask, off, full_oo(S + 1, 0);
+    int rc = subset_expand(S, n_streams, stream_ids, det_offsets, mask, off);
+    if (rc) return rc;
+    std::vector<long long> nid(S);
+    if (next_id) {   // the skipped streams keep their device counters: read them first
+        rc = oc_read_counters(e);
+        if (rc) return rc;
+        for (int s = 0; s < S; ++s) nid[s] = e->h_cnt[s].next_id;
+        for (int k = 0; k < n_streams; ++k) nid[stream_ids[k]] = next_id[k];
+    }
+    std::vector<int> wh;
+    if (img_wh) wh = subset_spread<int>(S, n_streams, stream_ids, img_wh, 2, 1);
+    e->mask.req_host = mask.data();
+    rc = yta_ocsort_update(e, dets, off.data(), img_wh ? wh.data() : nullptr, next_id ? nid.data() : nullptr, out,
+                        out_capacity, full_oo.data());
+    e->mask.req_host = nullptr;
+    if (next_id)
+        for (int k = 0; k < n_streams; ++k) next_id[k] = nid[stream_ids[k]];
+    if (rc) return rc;
+    subset_compact(n_streams, stream_ids, full_oo, out_offsets);
+    return YTA_OK;
+}
 
 }  // extern "C"
 

@@ -10,10 +10,11 @@ import ctypes
 import numpy as np
 
 from .. import _lib
+from ._streams import StreamSubset
 from .basetrack import BaseTrack, TrackState
 
 
-class ByteTrackEngine:
+class ByteTrackEngine(StreamSubset):
     """S independent ByteTrack streams sharing one device engine (one launch per kernel covers
     every stream).  Stream s has its own tracks and ID counter."""
 
@@ -52,18 +53,6 @@ class ByteTrackEngine:
     def reset_stream(self, stream):
         """Reset one stream to a fresh tracker; the others are untouched."""
         _lib.check(self.lib.yta_bytetrack_reset_stream(self._h, int(stream)))
-
-    def _subset(self, streams, n_items):
-        """Validated stream ids of a subset update as an ascending int32 array + the order that
-        sorts the caller's lists (outputs are handed back in the caller's order)."""
-        ids = np.asarray(streams, dtype=np.int64).reshape(-1)
-        if len(ids) != n_items or len(ids) == 0:
-            raise ValueError("one entry per listed stream")
-        order = np.argsort(ids, kind="stable")
-        ids = ids[order]
-        if ids[0] < 0 or ids[-1] >= self.n_streams or np.any(np.diff(ids) == 0):
-            raise ValueError(f"stream ids must be distinct and in 0..{self.n_streams - 1}")
-        return np.ascontiguousarray(ids, dtype=np.int32), order
 
     def capacity(self):
         c, d = ctypes.c_int(), ctypes.c_int()
@@ -131,14 +120,6 @@ class ByteTrackEngine:
             _lib.ptr(self._out), len(self._out), _lib.ptr(o)))
         return self._subset_result(o, order, nid, nid_user)
 
-    def _subset_result(self, o, order, nid, nid_user):
-        res = [None] * len(order)
-        for k, pos in enumerate(order):
-            res[pos] = self._out[o[k]:o[k + 1]].copy()
-        if nid_user is not None:
-            nid_user[order] = nid
-        return res
-
     def submit(self, dets_per_stream, out=None):
         """Pipelined update, first half (yta_bytetrack_submit): enqueue one frame of every stream
         and return at once; at most two frames in flight.  The engine's own ID counters are used.
@@ -163,7 +144,7 @@ class ByteTrackEngine:
         """Pipelined update, second half: the oldest submitted frame's S (K_s, 8) arrays.
         next_id: optional int64 (S,) array receiving the counters after that frame."""
         if not getattr(self, "_inflight", None):
-            raise _lib.YTAError("collect(): no frame in flight")
+            raise _lib.YTAError(-1, "collect(): no frame in flight")
         o = np.zeros(self.n_streams + 1, dtype=np.int32)
         nid = None if next_id is None else np.zeros(self.n_streams, np.int64)
         try:

@@ -18,6 +18,7 @@ import ctypes
 import numpy as np
 
 from .. import _lib
+from ._streams import StreamSubset
 from ..appearance import build_reid
 from ..motion.cmc import default_cmc
 
@@ -28,7 +29,7 @@ class KalmanBoxTracker:
     count = 1
 
 
-class DeepOCSortEngine:
+class DeepOCSortEngine(StreamSubset):
     """S independent DeepOCSORT streams sharing one device engine."""
 
     def __init__(self, n_streams=1, feat_dim=512, det_thresh=0.3, max_age=30, min_hits=3,
@@ -73,6 +74,10 @@ class DeepOCSortEngine:
     def reset(self):
         _lib.check(self.lib.yta_deepocsort_reset(self._h))
 
+    def reset_stream(self, stream):
+        """Reset one stream to a freshly constructed tracker; the others are untouched."""
+        _lib.check(self.lib.yta_deepocsort_reset_stream(self._h, int(stream)))
+
     def capacity(self):
         c, d = ctypes.c_int(), ctypes.c_int()
         _lib.check(self.lib.yta_deepocsort_capacity(self._h, ctypes.byref(c), ctypes.byref(d)))
@@ -94,15 +99,30 @@ class DeepOCSortEngine:
         return {k: int(buf[i]) for i, k in enumerate(names)}
 
     def update(self, dets_per_stream, feats_per_stream=None, warps=None, img_shapes=None,
-               next_id=None):
-        """dets_per_stream: S float64 (M_s, 6); feats_per_stream: S float32 (K_s, D), the
+               next_id=None, streams=None):
+        """streams: update only these stream ids (every per-stream argument and the result then
+        follow the listed streams; the others are left as they were).
+        dets_per_stream: S float64 (M_s, 6); feats_per_stream: S float32 (K_s, D), the
         embeddings of the detections with conf > det_thresh in input order (None when there are
         none or embeddings are off); warps: (S, 2, 3) float64 camera warps or None (identity);
         img_shapes: S image shapes (h, w, ...) or None; next_id: optional int64 (S,) counters
         (KalmanBoxTracker.count), updated in place."""
-        assert len(dets_per_stream) == self.n_streams
+        ids = None
+        if streams is not None:
+            ids, order = self._subset(streams, len(dets_per_stream))
+            dets_per_stream = self._reorder(dets_per_stream, order)
+            feats_per_stream = self._reorder(feats_per_stream, order)
+            img_shapes = self._reorder(img_shapes, order)
+            if warps is not None:
+                warps = np.asarray(warps, dtype=np.float64).reshape(-1, 6)[order]
+            nid_user = next_id
+            if next_id is not None:
+                next_id = np.ascontiguousarray(np.asarray(next_id, np.int64)[order])
+        else:
+            assert len(dets_per_stream) == self.n_streams
+        n = len(dets_per_stream)
         counts = [len(d) for d in dets_per_stream]
-        off = np.zeros(self.n_streams + 1, dtype=np.int32)
+        off = np.zeros(n + 1, dtype=np.int32)
         np.cumsum(counts, out=off[1:])
         if off[-1]:
             packed = np.ascontiguousarray(np.concatenate(
@@ -128,7 +148,7 @@ class DeepOCSortEngine:
                 feats = np.ascontiguousarray(np.concatenate(rows))
         wp = None
         if warps is not None:
-            wp = np.ascontiguousarray(warps, dtype=np.float64).reshape(self.n_streams, 6)
+            wp = np.ascontiguousarray(warps, dtype=np.float64).reshape(n, 6)
         wh = None
         if img_shapes is not None:
             wh = np.ascontiguousarray([[int(sh[1]), int(sh[0])] for sh in img_shapes],
@@ -140,6 +160,13 @@ class DeepOCSortEngine:
         nid = None
         if next_id is not None:
             nid = np.ascontiguousarray(next_id, dtype=np.int64)
+        if ids is not None:
+            o = np.zeros(n + 1, dtype=np.int32)
+            _lib.check(self.lib.yta_deepocsort_update_streams(
+                self._h, n, _lib.ptr(ids), _lib.ptr(packed), _lib.ptr(off), _lib.ptr(feats),
+                _lib.ptr(wp), _lib.ptr(wh), _lib.ptr(nid), _lib.ptr(self._out), len(self._out),
+                _lib.ptr(o)))
+            return self._subset_result(o, order, nid, nid_user)
         _lib.check(self.lib.yta_deepocsort_update(
             self._h, _lib.ptr(packed), _lib.ptr(off), _lib.ptr(feats), _lib.ptr(wp),
             _lib.ptr(wh), _lib.ptr(nid), _lib.ptr(self._out), len(self._out),

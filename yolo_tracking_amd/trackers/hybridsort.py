@@ -20,6 +20,7 @@ import ctypes
 import numpy as np
 
 from .. import _lib
+from ._streams import StreamSubset
 from ..appearance import build_reid
 
 
@@ -29,7 +30,7 @@ class KalmanBoxTracker:
     count = 0
 
 
-class HybridSortEngine:
+class HybridSortEngine(StreamSubset):
     """S independent HybridSORT streams sharing one device engine; one update() = one
     undecorated HybridSORT.update call per stream."""
 
@@ -72,6 +73,10 @@ class HybridSortEngine:
     def reset(self):
         _lib.check(self.lib.yta_hybridsort_reset(self._h))
 
+    def reset_stream(self, stream):
+        """Reset one stream to a freshly constructed tracker; the others are untouched."""
+        _lib.check(self.lib.yta_hybridsort_reset_stream(self._h, int(stream)))
+
     def capacity(self):
         c, d = ctypes.c_int(), ctypes.c_int()
         _lib.check(self.lib.yta_hybridsort_capacity(self._h, ctypes.byref(c), ctypes.byref(d)))
@@ -93,13 +98,25 @@ class HybridSortEngine:
         _lib.check(self.lib.yta_hybridsort_stats(self._h, buf))
         return {k: int(buf[i]) for i, k in enumerate(names)}
 
-    def update(self, dets_per_stream, feats_per_stream, next_id=None):
+    def update(self, dets_per_stream, feats_per_stream, next_id=None, streams=None):
         """dets_per_stream: S float64 (M_s, 6); feats_per_stream: S float32 (M_s, D), the
         get_features rows of every detection; next_id: optional int64 (S,) counters
-        (KalmanBoxTracker.count), updated in place."""
-        assert len(dets_per_stream) == self.n_streams
+        (KalmanBoxTracker.count), updated in place.  streams: update only these stream ids
+        (every per-stream argument and the result then follow the listed streams; the others
+        are left as they were)."""
+        ids = None
+        if streams is not None:
+            ids, order = self._subset(streams, len(dets_per_stream))
+            dets_per_stream = self._reorder(dets_per_stream, order)
+            feats_per_stream = self._reorder(feats_per_stream, order)
+            nid_user = next_id
+            if next_id is not None:
+                next_id = np.ascontiguousarray(np.asarray(next_id, np.int64)[order])
+        else:
+            assert len(dets_per_stream) == self.n_streams
+        n = len(dets_per_stream)
         dets = [np.asarray(d, dtype=np.float64).reshape(-1, 6) for d in dets_per_stream]
-        off = np.zeros(self.n_streams + 1, dtype=np.int32)
+        off = np.zeros(n + 1, dtype=np.int32)
         np.cumsum([len(d) for d in dets], out=off[1:])
         packed = np.ascontiguousarray(np.concatenate(dets)) if off[-1] else np.zeros((0, 6))
         rows = []
@@ -121,6 +138,12 @@ class HybridSortEngine:
         nid = None
         if next_id is not None:
             nid = np.ascontiguousarray(next_id, dtype=np.int64)
+        if ids is not None:
+            o = np.zeros(n + 1, dtype=np.int32)
+            _lib.check(self.lib.yta_hybridsort_update_streams(
+                self._h, n, _lib.ptr(ids), _lib.ptr(packed), _lib.ptr(off), _lib.ptr(feats),
+                _lib.ptr(nid), _lib.ptr(self._out), len(self._out), _lib.ptr(o)))
+            return self._subset_result(o, order, nid, nid_user)
         _lib.check(self.lib.yta_hybridsort_update(
             self._h, _lib.ptr(packed), _lib.ptr(off), _lib.ptr(feats), _lib.ptr(nid),
             _lib.ptr(self._out), len(self._out), _lib.ptr(self._out_off)))

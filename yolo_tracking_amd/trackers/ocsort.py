@@ -11,6 +11,7 @@ import ctypes
 import numpy as np
 
 from .. import _lib
+from ._streams import StreamSubset
 
 
 class KalmanBoxTracker:
@@ -19,7 +20,7 @@ class KalmanBoxTracker:
     count = 0
 
 
-class OCSortEngine:
+class OCSortEngine(StreamSubset):
     """S independent OCSORT streams sharing one device engine."""
 
     def __init__(self, n_streams=1, det_thresh=0.2, max_age=30, min_hits=3, asso_threshold=0.3,
@@ -59,6 +60,10 @@ class OCSortEngine:
     def reset(self):
         _lib.check(self.lib.yta_ocsort_reset(self._h))
 
+    def reset_stream(self, stream):
+        """Reset one stream to a freshly constructed tracker; the others are untouched."""
+        _lib.check(self.lib.yta_ocsort_reset_stream(self._h, int(stream)))
+
     def capacity(self):
         c, d = ctypes.c_int(), ctypes.c_int()
         _lib.check(self.lib.yta_ocsort_capacity(self._h, ctypes.byref(c), ctypes.byref(d)))
@@ -79,12 +84,24 @@ class OCSortEngine:
         _lib.check(self.lib.yta_ocsort_stats(self._h, buf))
         return {k: int(buf[i]) for i, k in enumerate(names)}
 
-    def update(self, dets_per_stream, img_shapes=None, next_id=None):
+    def update(self, dets_per_stream, img_shapes=None, next_id=None, streams=None):
         """dets_per_stream: S float64 (M_s, 6); img_shapes: S image shapes (h, w, ...) or None;
-        next_id: optional int64 (S,) counters (KalmanBoxTracker.count), updated in place."""
-        assert len(dets_per_stream) == self.n_streams
+        next_id: optional int64 (S,) counters (KalmanBoxTracker.count), updated in place.
+        streams: update only these stream ids (every per-stream argument and the result then
+        follow the listed streams; the others are left as they were)."""
+        ids = None
+        if streams is not None:
+            ids, order = self._subset(streams, len(dets_per_stream))
+            dets_per_stream = self._reorder(dets_per_stream, order)
+            img_shapes = self._reorder(img_shapes, order)
+            nid_user = next_id
+            if next_id is not None:
+                next_id = np.ascontiguousarray(np.asarray(next_id, np.int64)[order])
+        else:
+            assert len(dets_per_stream) == self.n_streams
+        n = len(dets_per_stream)
         counts = [len(d) for d in dets_per_stream]
-        off = np.zeros(self.n_streams + 1, dtype=np.int32)
+        off = np.zeros(n + 1, dtype=np.int32)
         np.cumsum(counts, out=off[1:])
         if off[-1]:
             packed = np.ascontiguousarray(np.concatenate(
@@ -102,6 +119,12 @@ class OCSortEngine:
         nid = None
         if next_id is not None:
             nid = np.ascontiguousarray(next_id, dtype=np.int64)
+        if ids is not None:
+            o = np.zeros(n + 1, dtype=np.int32)
+            _lib.check(self.lib.yta_ocsort_update_streams(
+                self._h, n, _lib.ptr(ids), _lib.ptr(packed), _lib.ptr(off), _lib.ptr(wh),
+                _lib.ptr(nid), _lib.ptr(self._out), len(self._out), _lib.ptr(o)))
+            return self._subset_result(o, order, nid, nid_user)
         _lib.check(self.lib.yta_ocsort_update(self._h, _lib.ptr(packed), _lib.ptr(off),
                                               _lib.ptr(wh), _lib.ptr(nid), _lib.ptr(self._out),
                                               len(self._out), _lib.ptr(self._out_off)))
