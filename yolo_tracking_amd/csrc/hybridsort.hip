@@ -309,6 +309,7 @@ __global__ __launch_bounds__(OC_T) void k_hs_pre(HsArgs a) {
         int n_free = c->n_free;
         const int n_nan = block_compact(n_trk, sh.wsum, [&](int i) { return a.nan_flag[tb + i] != 0; },
                                         [&](int i, int pos) { a.tmp[ub + pos] = list[i]; });
+        block_sync();   // the compaction's tmp stores (other threads' runs) before their reads
         for (int k = t; k < n_nan; k += nt) a.free_list[tb + n_free + k] = a.tmp[ub + k];
         n_free += n_nan;
         block_sync();
@@ -803,6 +804,7 @@ __global__ __launch_bounds__(OC_T) void k_hs_assoc(HsArgs a) {
     const int n_dead = block_compact(n_trk, sh.wsum,
                                      [&](int j) { return a.rec[tb + list[j]].tsu > a.max_age; },
                                      [&](int j, int pos) { a.tmp[ub + pos] = list[j]; });
+    block_sync();   // the compaction's tmp stores (other threads' runs) before their reads
     for (int k = t; k < n_dead; k += nt) a.free_list[tb + n_free + k] = a.tmp[ub + k];
     block_sync();
     const int n_live = block_compact(n_trk, sh.wsum,
