@@ -393,13 +393,13 @@ def pcie_inclusive(frame_of, S, N, device, first, frames=8, engines=1, pinned=Fa
                     f"{E} engine(s) on as many host threads); median step"}
 
 
-def pcie_pipelined(frame_of, S, N, device, first, frames=8, pinned=False):
+def pcie_pipelined(frame_of, S, N, device, first, frames=8, pinned=False, f32=False):
     """The host-buffer path pipelined (yta_bytetrack_submit / _collect, one engine): frame f's
-    detections go host -> device while frame f-1's kernels run and frame f-2's rows come back, so
-    both PCIe directions and the kernels overlap.  Every timed frame's packed dets sit in their
+    detections go host -> device while frame f-1's kernels run and frame f-2's rows come back (up
+    to three frames in flight), so both PCIe directions and the kernels overlap.  Every timed frame's packed dets sit in their
     own caller buffer before the timed region (page-locked: written there by the detector, DMA'd
-    directly; pageable: staged by the library during submit); output rows land in two
-    alternating caller buffers (page-locked: DMA'd directly).  value = frames / wall time of the
+    directly; pageable: staged by the library during submit); output rows land in three
+    rotating caller buffers (page-locked: DMA'd directly).  value = frames / wall time of the
     timed submit/collect loop.  Never `value` of the bench line."""
     import torch
 
@@ -408,18 +408,22 @@ def pcie_pipelined(frame_of, S, N, device, first, frames=8, pinned=False):
                           device=device, track_capacity=3 * N, max_dets=N)
     lib, h = eng.lib, eng.handle
 
-    def buf(shape):
+    def buf(shape, dt=np.float64):
         if not pinned:
-            return np.empty(shape)
-        return torch.empty(shape, dtype=torch.float64, pin_memory=True).numpy()
+            return np.empty(shape, dtype=dt)
+        return torch.empty(shape, dtype=torch.float32 if dt == np.float32 else torch.float64,
+                           pin_memory=True).numpy()
     offs = np.ascontiguousarray(np.arange(S + 1, dtype=np.int32) * N)
-    outs = [buf((S * N, 8)) for _ in range(2)]
+    in_dt = np.float32 if f32 else np.float64
+    submit_fn = lib.yta_bytetrack_submit_f32 if f32 else lib.yta_bytetrack_submit
+    DEPTH = 3   # frames in flight (csrc/bytetrack.hip PIPE_DEPTH)
+    outs = [buf((S * N, 8)) for _ in range(DEPTH)]
     out_off = np.zeros(S + 1, np.int32)
-    stage = buf((S * N, 6))
+    stage = buf((S * N, 6), in_dt)
 
     def submit(src, f):
-        _lib.check(lib.yta_bytetrack_submit(h, src.ctypes.data, offs.ctypes.data, None,
-                                            outs[f % 2].ctypes.data, S * N))
+        _lib.check(submit_fn(h, src.ctypes.data, offs.ctypes.data, None,
+                             outs[f % DEPTH].ctypes.data, S * N))
 
     def collect():
         _lib.check(lib.yta_bytetrack_collect(h, None, out_off.ctypes.data))
@@ -429,20 +433,22 @@ def pcie_pipelined(frame_of, S, N, device, first, frames=8, pinned=False):
         collect()
     timed = []
     for f in range(first, first + frames):
-        b = buf((S * N, 6))
+        b = buf((S * N, 6), in_dt)
         b[:] = frame_of(f)
         timed.append(b)
     t0 = time.perf_counter()
     for k, src in enumerate(timed):
         submit(src, first + k)
-        if k:
+        if k >= DEPTH - 1:
             collect()
-    collect()
+    for _ in range(min(DEPTH - 1, len(timed))):
+        collect()
     dt = (time.perf_counter() - t0) / frames
     eng.close()
     return {"value": S / dt, "unit": "calls/s", "steps": frames, "ms_per_step": 1000 * dt,
-            "note": "pipelined host-buffer ABI (submit/collect, two frames in flight), "
-                    f"{'page-locked' if pinned else 'pageable numpy'} caller buffers; "
+            "note": "pipelined host-buffer ABI (submit/collect, up to three frames in flight), "
+                    f"{'page-locked' if pinned else 'pageable numpy'} caller buffers"
+                    f"{', float32 detection rows' if f32 else ''}; "
                     "wall time of the timed loop / frames"}
 
 
@@ -641,6 +647,8 @@ def main():
             if not args.no_pcie_pinned:
                 pcie["pipelined"]["pinned"] = pcie_pipelined(frame_of, S, N, local_rank,
                                                              first=min(PRE, FT - 8), pinned=True)
+                pcie["pipelined"]["pinned_f32"] = pcie_pipelined(
+                    frame_of, S, N, local_rank, first=min(PRE, FT - 8), pinned=True, f32=True)
         dk = traffic.get(PHASE_KERNEL[dom], {})
         line = {
             "metric": "tracker.update() calls/sec @ 1024 tracks×1024 dets; 1/2/4/8 MI355X",

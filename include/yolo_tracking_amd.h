@@ -170,9 +170,9 @@ int yta_bytetrack_update_device(yta_bytetrack *engine, const double *d_dets,
 int yta_bytetrack_sync(yta_bytetrack *engine);      /* waits; reports device-side errors */
 
 /* Pipelined host-buffer update (ByteTrack engines): submit enqueues one frame of every stream and
- * returns at once; collect waits for the OLDEST submitted frame and reports it.  Up to two frames
- * are in flight, so frame f's detections travel host -> device while frame f-1's kernels run and
- * frame f-2's rows travel back: both PCIe directions and the kernels overlap (the synchronous
+ * returns at once; collect waits for the OLDEST submitted frame and reports it.  Up to three
+ * frames are in flight, so frame f's detections travel host -> device while frame f-1's kernels
+ * run and frame f-2's rows travel back: both PCIe directions and the kernels overlap (the synchronous
  * yta_bytetrack_update does them one after the other).  Results are identical to
  * yta_bytetrack_update frame by frame.
  *   submit: dets / det_offsets as yta_bytetrack_update; next_id: S counters written to the device
@@ -180,13 +180,22 @@ int yta_bytetrack_sync(yta_bytetrack *engine);      /* waits; reports device-sid
  *     the host copies are a frame behind); out: out_capacity >= det_offsets[S] rows x 8, filled
  *     by the matching collect (rows beyond out_offsets[S] unspecified).  Page-locked dets / out
  *     are DMA'd directly and must stay untouched until the frame is collected; pageable dets are
- *     staged during the call (reusable at once).  A third submit before a collect fails with
+ *     staged during the call (reusable at once).  A fourth submit before a collect fails with
  *     YTA_ERR_INVALID; so do the synchronous update / reset / reserve while frames are in flight.
  *   collect: next_id (S, may be NULL) receives the counters after that frame; out_offsets S + 1
  *     row offsets into that frame's out; device error flags are reported here. */
 int yta_bytetrack_submit(yta_bytetrack *engine, const double *dets, const int *det_offsets,
                          const long long *next_id, double *out, int out_capacity);
 int yta_bytetrack_collect(yta_bytetrack *engine, long long *next_id, int *out_offsets);
+/* float32 detections (ultralytics hands BoxMOT float32 boxes; the reference promotes them to
+ * float64 exactly, byte_tracker.py:143): packed rows of 6 float32 cross PCIe at half the bytes and
+ * are widened on the device, so every result equals the float64 call on the promoted rows.  Same
+ * contracts as yta_bytetrack_submit / yta_bytetrack_update otherwise. */
+int yta_bytetrack_submit_f32(yta_bytetrack *engine, const float *dets, const int *det_offsets,
+                             const long long *next_id, double *out, int out_capacity);
+int yta_bytetrack_update_f32(yta_bytetrack *engine, const float *dets, const int *det_offsets,
+                             long long *next_id, double *out, int out_capacity,
+                             int *out_offsets);
 
 /* Host-buffer update of a SUBSET of the streams (update(ctx, n_streams,
  * stream_ids, ...)).  In the reference every camera stream is its own tracker

@@ -1897,6 +1897,21 @@ __global__ void k_out_offsets(const BtCounters *cnt, int S, int cap, int *off) {
     }
 }
 
+// float32 detection rows (what a float32 detector hands over; the reference promotes them to
+// float64 exactly, byte_tracker.py:143) widened to the float64 rows the kernels read: n values,
+// two per thread (8-B loads, 16-B stores).
+__global__ __launch_bounds__(256) void k_widen_f32(const float *src, double *dst, long long n) {
+    const long long stride = (long long)gridDim.x * blockDim.x;
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; 2 * i < n; i += stride) {
+        if (2 * i + 1 < n) {
+            const float2 v = reinterpret_cast<const float2 *>(src)[i];
+            reinterpret_cast<double2 *>(dst)[i] = make_double2((double)v.x, (double)v.y);
+        } else {
+            dst[2 * i] = (double)src[2 * i];
+        }
+    }
+}
+
 // Pipelined host-buffer update (any S): the same prefix offsets from one 1024-thread block, each
 // thread summing a run of streams, then a block scan.
 constexpr int OFFS_T = 1024;
@@ -1970,6 +1985,8 @@ __global__ void k_reset(BtArgs a, int s0) {
 // ================================================================================== host engine
 using namespace yta;
 
+constexpr int PIPE_DEPTH = 3;   // frames in flight of the pipelined host-buffer update
+
 struct yta_bytetrack {
     int device = 0, S = 0, CAP = 0, MAXD = 0;
     int variant = VAR_BYTETRACK, D = 0;
@@ -1993,13 +2010,17 @@ struct yta_bytetrack {
     double *d_det_in = nullptr;
     long long d_det_cap = 0;
     int *d_det_off = nullptr;
+    float *d_det32 = nullptr, *h_det32 = nullptr;   // float32 detection rows (before widening)
+    long long det32_cap = 0;
     // stream-subset updates: the [S] mask on the device and its pinned staging
     int *d_active = nullptr, *h_active = nullptr;
-    // pipelined host-buffer updates (yta_bytetrack_submit / _collect): two frame slots, a copy-in
-    // and a copy-out stream beside the compute stream
+    // pipelined host-buffer updates (yta_bytetrack_submit / _collect): PIPE_DEPTH frame slots, a
+    // copy-in and a copy-out stream beside the compute stream
     struct PipeSlot {
         double *d_in = nullptr, *h_in = nullptr;     // detections (pinned staging for pageable)
         long long in_cap = 0;
+        float *d_in32 = nullptr, *h_in32 = nullptr;  // float32 detections (before widening)
+        long long in32_cap = 0;
         int *d_off = nullptr, *h_off = nullptr;      // S + 1 detection offsets
         double *d_pack = nullptr, *h_pack = nullptr; // packed output rows
         long long pack_cap = 0;
@@ -2011,7 +2032,7 @@ struct yta_bytetrack {
         long long rows_bound = 0;                    // det_offsets[S] of the frame
         bool direct_out = false;                     // DMA straight into user_out
     };
-    PipeSlot pipe[2];
+    PipeSlot pipe[PIPE_DEPTH];
     int pipe_head = 0, pipe_count = 0;
     hipStream_t s_in = nullptr, s_out = nullptr;
     // optional per-kernel timing with HIP events on the engine stream
@@ -2517,10 +2538,49 @@ int ensure_pack(yta_bytetrack *e, long long rows) {
     return YTA_OK;
 }
 
+// float32 detection rows into a device buffer of `cap` floats (grown, contents dropped), through
+// page-locked staging when the caller's buffer is pageable; enqueued on `st`.
+int stage_f32(yta_bytetrack *e, const float *src, long long n, float **dbuf, float **hbuf,
+              long long *cap, hipStream_t st) {
+    if (n > *cap) {
+        if (*dbuf) (void)hipFree(*dbuf);
+        if (*hbuf) (void)hipHostFree(*hbuf);
+        *dbuf = *hbuf = nullptr;
+        *cap = 0;
+        const long long c = std::max<long long>(n + n / 8, 6144);
+        YTA_HIP(hipMalloc((void **)dbuf, sizeof(float) * c));
+        YTA_HIP(hipHostMalloc((void **)hbuf, sizeof(float) * c, hipHostMallocDefault));
+        *cap = c;
+    }
+    const size_t bytes = sizeof(float) * n;
+    if (host_pinned(src, bytes)) {
+        YTA_HIP(hipMemcpyAsync(*dbuf, src, bytes, hipMemcpyHostToDevice, st));
+        return YTA_OK;
+    }
+    const size_t ch = stage_chunk(bytes);
+    for (size_t o = 0; o < bytes; o += ch) {
+        const size_t m = std::min(ch, bytes - o);
+        par_copy(e, (char *)*hbuf + o, (const char *)src + o, m);
+        YTA_HIP(hipMemcpyAsync((char *)*dbuf + o, (char *)*hbuf + o, m, hipMemcpyHostToDevice, st));
+    }
+    return YTA_OK;
+}
+
+int widen_f32(const float *src, double *dst, long long n, hipStream_t st) {
+    const long long pairs = (n + 1) / 2;
+    const unsigned blocks = (unsigned)std::min<long long>(4096, (pairs + 255) / 256);
+    hipLaunchKernelGGL(k_widen_f32, dim3(std::max(1u, blocks)), dim3(256), 0, st, src, dst, n);
+    YTA_HIP(hipGetLastError());
+    return YTA_OK;
+}
+
 int update_host(yta_bytetrack *e, const double *dets, const int *det_offsets, const float *feats,
                 long long *next_id, double *out, int out_capacity, int *out_offsets,
-                const double *warps = nullptr, const int *active = nullptr) {
+                const double *warps = nullptr, const int *active = nullptr,
+                const float *dets32 = nullptr) {
     YTA_CHECK(e && det_offsets && out_offsets, YTA_ERR_INVALID, "null argument");
+    YTA_CHECK(!dets32 || (e->variant == VAR_BYTETRACK && !dets), YTA_ERR_INVALID,
+              "float32 detections: ByteTrack engines, instead of the float64 rows");
     YTA_CHECK(e->pipe_count == 0, YTA_ERR_INVALID, "pipelined frames in flight: collect them first");
     YTA_HIP(hipSetDevice(e->device));
     const int S = e->S;
@@ -2552,7 +2612,7 @@ int update_host(yta_bytetrack *e, const double *dets, const int *det_offsets, co
         }
     }
     const long long total = det_offsets[S];
-    YTA_CHECK(total == 0 || dets, YTA_ERR_INVALID, "null dets");
+    YTA_CHECK(total == 0 || dets || dets32, YTA_ERR_INVALID, "null dets");
     if (total > e->d_det_cap) {
         if (e->d_det_in) (void)hipFree(e->d_det_in);
         if (e->h_dets) (void)hipHostFree(e->h_dets);
@@ -2564,7 +2624,12 @@ int update_host(yta_bytetrack *e, const double *dets, const int *det_offsets, co
         YTA_HIP(hipHostMalloc((void **)&e->h_dets, sizeof(double) * 6 * cap, hipHostMallocDefault));
         e->d_det_cap = cap;
     }
-    if (total && host_pinned(dets, sizeof(double) * 6 * total)) {   // straight from the caller
+    if (total && dets32) {   // float32 rows: half the bytes over the link, widened on the device
+        int src = stage_f32(e, dets32, 6 * total, &e->d_det32, &e->h_det32, &e->det32_cap,
+                            e->stream);
+        if (!src) src = widen_f32(e->d_det32, e->d_det_in, 6 * total, e->stream);
+        if (src) return src;
+    } else if (total && host_pinned(dets, sizeof(double) * 6 * total)) {   // straight from the caller
         YTA_HIP(hipMemcpyAsync(e->d_det_in, dets, sizeof(double) * 6 * total,
                                hipMemcpyHostToDevice, e->stream));
     } else if (total) {   // chunk k's DMA overlaps chunk k+1's host copy
@@ -2766,16 +2831,16 @@ int update_host_subset(yta_bytetrack *e, int n, const int *ids, const double *de
 
 // ---- pipelined host-buffer update --------------------------------------------------------------
 // Frame f's detections go host -> device on s_in while frame f-1's kernels run on the compute
-// stream and frame f-2's rows come back on s_out (both PCIe directions and the kernels at once).
+// stream and frame f-2's rows come back on s_out (PIPE_DEPTH frames in flight) (both PCIe directions and the kernels at once).
 // The compute stream snapshots every frame's rows (k_pack_out into the slot) and counters before
 // the next frame's kernels can touch them, so the copy-out of frame f never races frame f+1.
 void pipe_free(yta_bytetrack *e) {
     for (auto &p : e->pipe) {
         for (void *d : {(void *)p.d_in, (void *)p.d_off, (void *)p.d_pack, (void *)p.d_pack_off,
-                        (void *)p.d_cnt})
+                        (void *)p.d_cnt, (void *)p.d_in32})
             if (d) (void)hipFree(d);
         for (void *h : {(void *)p.h_in, (void *)p.h_off, (void *)p.h_pack, (void *)p.h_pack_off,
-                        (void *)p.h_cnt, (void *)p.h_nid})
+                        (void *)p.h_cnt, (void *)p.h_nid, (void *)p.h_in32})
             if (h) (void)hipHostFree(h);
         for (hipEvent_t ev : {p.in_done, p.kern_done, p.out_done})
             if (ev) (void)hipEventDestroy(ev);
@@ -2825,15 +2890,17 @@ int pipe_slot_ready(yta_bytetrack *e, yta_bytetrack::PipeSlot &p, long long dets
 }
 
 int pipe_submit(yta_bytetrack *e, const double *dets, const int *det_offsets,
-                const long long *next_id, double *out, long long out_capacity) {
+                const long long *next_id, double *out, long long out_capacity,
+                const float *dets32 = nullptr) {
     YTA_CHECK(e && det_offsets, YTA_ERR_INVALID, "null argument");
     YTA_CHECK(e->variant == VAR_BYTETRACK, YTA_ERR_INVALID, "pipelined updates: ByteTrack engines");
     YTA_HIP(hipSetDevice(e->device));
-    YTA_CHECK(e->pipe_count < 2, YTA_ERR_INVALID, "two frames in flight: collect one first");
+    YTA_CHECK(e->pipe_count < PIPE_DEPTH, YTA_ERR_INVALID, "%d frames in flight: collect one first",
+              PIPE_DEPTH);
     const int S = e->S;
     YTA_CHECK(det_offsets[0] == 0, YTA_ERR_INVALID, "det_offsets[0] must be 0");
     const long long total = det_offsets[S];
-    YTA_CHECK(total == 0 || dets, YTA_ERR_INVALID, "null dets");
+    YTA_CHECK(total == 0 || dets || dets32, YTA_ERR_INVALID, "null dets");
     YTA_CHECK(out_capacity >= total && (total == 0 || out), YTA_ERR_CAPACITY,
               "out holds %lld rows, the frame needs det_offsets[S] = %lld", out_capacity, total);
     // capacity: the live tracks of the last collected frame plus every detection of the frames in
@@ -2846,7 +2913,7 @@ int pipe_submit(yta_bytetrack *e, const double *dets, const int *det_offsets,
         need_d = std::max(need_d, m);
         long long bound = (long long)e->h_cnt[s].n_tracked + e->h_cnt[s].n_lost + m;
         for (int k = 0; k < e->pipe_count; ++k) {
-            const auto &q = e->pipe[(e->pipe_head + k) % 2];
+            const auto &q = e->pipe[(e->pipe_head + k) % PIPE_DEPTH];
             bound += q.h_off[s + 1] - q.h_off[s];
         }
         if (bound > e->CAP) grow = true;
@@ -2864,14 +2931,17 @@ int pipe_submit(yta_bytetrack *e, const double *dets, const int *det_offsets,
             if (rc) return rc;
         }
     }
-    auto &p = e->pipe[(e->pipe_head + e->pipe_count) % 2];
+    auto &p = e->pipe[(e->pipe_head + e->pipe_count) % PIPE_DEPTH];
     int rc = pipe_slot_ready(e, p, total);
     if (rc) return rc;
     // this slot's last frame was collected (its events completed): its buffers are free
     memcpy(p.h_off, det_offsets, sizeof(int) * (S + 1));
     YTA_HIP(hipMemcpyAsync(p.d_off, p.h_off, sizeof(int) * (S + 1), hipMemcpyHostToDevice,
                            e->s_in));
-    if (total) {
+    if (total && dets32) {   // float32 rows: half the bytes over the link, widened on the device
+        rc = stage_f32(e, dets32, 6 * total, &p.d_in32, &p.h_in32, &p.in32_cap, e->s_in);
+        if (rc) return rc;
+    } else if (total) {
         const size_t bytes = sizeof(double) * 6 * total;
         if (host_pinned(dets, bytes)) {   // straight from the caller (kept until collected)
             YTA_HIP(hipMemcpyAsync(p.d_in, dets, bytes, hipMemcpyHostToDevice, e->s_in));
@@ -2893,6 +2963,10 @@ int pipe_submit(yta_bytetrack *e, const double *dets, const int *det_offsets,
         YTA_HIP(hipMemcpy2DAsync(&e->a.cnt[0].next_id, sizeof(BtCounters), p.h_nid,
                                  sizeof(long long), sizeof(long long), S, hipMemcpyHostToDevice,
                                  e->stream));
+    }
+    if (total && dets32) {
+        rc = widen_f32(p.d_in32, p.d_in, 6 * total, e->stream);
+        if (rc) return rc;
     }
     rc = launch_pipeline(e, p.d_in, p.d_off, e->a.out, nullptr);
     if (rc) return rc;
@@ -2927,7 +3001,7 @@ int pipe_collect(yta_bytetrack *e, long long *next_id, int *out_offsets) {
     YTA_CHECK(e->pipe_count > 0, YTA_ERR_INVALID, "no frame in flight");
     YTA_HIP(hipSetDevice(e->device));
     auto &p = e->pipe[e->pipe_head];
-    e->pipe_head = (e->pipe_head + 1) % 2;
+    e->pipe_head = (e->pipe_head + 1) % PIPE_DEPTH;
     --e->pipe_count;
     YTA_HIP(hipEventSynchronize(p.out_done));
     const int S = e->S;
@@ -2990,6 +3064,8 @@ int yta_bytetrack_destroy(yta_bytetrack *e) {
     if (e->h_feat) (void)hipHostFree(e->h_feat);
     if (e->d_feat_in) (void)hipFree(e->d_feat_in);
     if (e->h_active) (void)hipHostFree(e->h_active);
+    if (e->d_det32) (void)hipFree(e->d_det32);
+    if (e->h_det32) (void)hipHostFree(e->h_det32);
     pipe_free(e);
     for (hipEvent_t h : e->ev) (void)hipEventDestroy(h);
     if (e->stream) (void)hipStreamDestroy(e->stream);
@@ -3073,6 +3149,18 @@ int yta_bytetrack_update_device_masked(yta_bytetrack *e, const int *d_active,
 int yta_bytetrack_submit(yta_bytetrack *e, const double *dets, const int *det_offsets,
                          const long long *next_id, double *out, int out_capacity) {
     return pipe_submit(e, dets, det_offsets, next_id, out, out_capacity);
+}
+
+int yta_bytetrack_submit_f32(yta_bytetrack *e, const float *dets, const int *det_offsets,
+                             const long long *next_id, double *out, int out_capacity) {
+    return pipe_submit(e, nullptr, det_offsets, next_id, out, out_capacity, dets);
+}
+
+int yta_bytetrack_update_f32(yta_bytetrack *e, const float *dets, const int *det_offsets,
+                             long long *next_id, double *out, int out_capacity,
+                             int *out_offsets) {
+    return update_host(e, nullptr, det_offsets, nullptr, next_id, out, out_capacity, out_offsets,
+                       nullptr, nullptr, dets);
 }
 
 int yta_bytetrack_collect(yta_bytetrack *e, long long *next_id, int *out_offsets) {

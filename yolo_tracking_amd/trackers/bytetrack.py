@@ -94,11 +94,15 @@ class ByteTrackEngine(StreamSubset):
         counts = [len(d) for d in dets_per_stream]
         off = np.zeros(n + 1, dtype=np.int32)
         np.cumsum(counts, out=off[1:])
+        # float32 detections (what a float32 detector hands over) cross the link as float32 and
+        # are widened on the device, exactly as the reference's promotion (yta_bytetrack_update_f32)
+        f32 = ids is None and all(np.asarray(d).dtype == np.float32 for d in dets_per_stream)
+        dt = np.float32 if f32 else np.float64
         if off[-1]:
             packed = np.ascontiguousarray(np.concatenate(
-                [np.asarray(d, dtype=np.float64).reshape(-1, 6) for d in dets_per_stream]))
+                [np.asarray(d, dtype=dt).reshape(-1, 6) for d in dets_per_stream]))
         else:
-            packed = np.zeros((0, 6))
+            packed = np.zeros((0, 6), dtype=dt)
         # every output row is a track matched to or born from one of this frame's detections
         need = max(int(off[-1]), 1)
         if len(self._out) < need:
@@ -107,7 +111,8 @@ class ByteTrackEngine(StreamSubset):
         if next_id is not None:
             nid = np.ascontiguousarray(next_id, dtype=np.int64)
         if ids is None:
-            _lib.check(self.lib.yta_bytetrack_update(self._h, _lib.ptr(packed), _lib.ptr(off),
+            fn = self.lib.yta_bytetrack_update_f32 if f32 else self.lib.yta_bytetrack_update
+            _lib.check(fn(self._h, _lib.ptr(packed), _lib.ptr(off),
                                                      _lib.ptr(nid), _lib.ptr(self._out),
                                                      len(self._out), _lib.ptr(self._out_off)))
             if next_id is not None:
@@ -122,20 +127,22 @@ class ByteTrackEngine(StreamSubset):
 
     def submit(self, dets_per_stream, out=None):
         """Pipelined update, first half (yta_bytetrack_submit): enqueue one frame of every stream
-        and return at once; at most two frames in flight.  The engine's own ID counters are used.
+        and return at once; at most three frames in flight.  The engine's own ID counters are used.
         out: optional float64 (>= total dets, 8) buffer the matching collect() fills (kept alive
         here until then).  Returns nothing; collect() returns the oldest submitted frame."""
         assert len(dets_per_stream) == self.n_streams
         off = np.zeros(self.n_streams + 1, dtype=np.int32)
         np.cumsum([len(d) for d in dets_per_stream], out=off[1:])
+        f32 = all(np.asarray(d).dtype == np.float32 for d in dets_per_stream)
+        dt = np.float32 if f32 else np.float64
         packed = (np.ascontiguousarray(np.concatenate(
-            [np.asarray(d, dtype=np.float64).reshape(-1, 6) for d in dets_per_stream]))
-            if off[-1] else np.zeros((0, 6)))
+            [np.asarray(d, dtype=dt).reshape(-1, 6) for d in dets_per_stream]))
+            if off[-1] else np.zeros((0, 6), dtype=dt))
         need = max(int(off[-1]), 1)
         if out is None or len(out) < need:
             out = np.empty((need, 8), dtype=np.float64)
-        _lib.check(self.lib.yta_bytetrack_submit(self._h, _lib.ptr(packed), _lib.ptr(off), None,
-                                                 _lib.ptr(out), len(out)))
+        fn = self.lib.yta_bytetrack_submit_f32 if f32 else self.lib.yta_bytetrack_submit
+        _lib.check(fn(self._h, _lib.ptr(packed), _lib.ptr(off), None, _lib.ptr(out), len(out)))
         if not hasattr(self, "_inflight"):
             self._inflight = []
         self._inflight.append((packed, out))   # the buffers must outlive the DMA
