@@ -21,6 +21,11 @@ tracker states with covariances / embeddings sampled every 64th tracker):
                           (hybridsort.py:190, :438-439).
   hs_n4096_s8_{a..h}      C5 at its per-GPU concurrency: 8 streams x 12 frames, one engine launch
                           per frame in the GPU test; banks 12 deep, delta_t history full.
+  oc_n256_f45             C2 OCSORT 256 x 256 (GIoU), 45 frames, 5 % missed detections: ORU
+                          re-acquisitions and deaths after max_age = 30 (ocsort.py:374-377).
+  bs_n1024_d512_cmc_f30   C3 BoT-SORT at size under the CMC camera warp of §8(d) every frame
+                          (multi_gmc, bot_sort.py:290-295): the warped Kalman path (states within
+                          1e-9 relative, every IoU comparison margin-checked), rows kept in full.
 Every LAP call is tie-checked and every threshold comparison margin-checked as in
 make_goldens.py; DeepOCSORT / HybridSORT seeds are advanced (seed0, seed0 + 100, ...) until the
 oracle reproduces the reference exactly in lock-step (birth numbering included).
@@ -42,6 +47,11 @@ CASES["bs_n1024_d512_f65"] = ("bs", dict(n=1024, nf=65, seed=1146, D=512,
 for k, s in zip("ab", (2161, 2162)):
     CASES[f"dos_n2048_cmc_f40_{k}"] = ("dos", dict(n=2048, nf=40, seed=s, D=512))
 CASES["hs_n4096_f35"] = ("hs", dict(n=4096, nf=35, seed=4191, D=512))
+CASES["oc_n256_f45"] = ("oc", dict(n=256, nf=45, seed=2561,
+                                   skw=dict(low_conf_frac=0.0, drop_frac=0.05)))
+CASES["bs_n1024_d512_cmc_f30"] = ("bs", dict(n=1024, nf=30, seed=1147, D=512,
+                                             skw=dict(low_conf_frac=0.1, drop_frac=0.05),
+                                             warp=True))
 for k, s in zip("abcdefgh", range(4201, 4209)):
     CASES[f"hs_n4096_s8_{k}"] = ("hs", dict(n=4096, nf=12, seed=s, D=512))
 
@@ -54,8 +64,9 @@ def run_part(case):
     mgf.OUT.clear()
     t0 = time.time()
     if kind == "bs":
+        warp = mgf.mg.CMC_AFFINE if p.get("warp") else None
         for seed in range(p["seed"], p["seed"] + 1000, 100):
-            if mgf.bs_case(case, p["n"], p["nf"], seed, p["D"], p["skw"]):
+            if mgf.bs_case(case, p["n"], p["nf"], seed, p["D"], p["skw"], warp=warp):
                 break
         else:
             raise RuntimeError(f"{case}: no tie-free seed")
@@ -70,6 +81,8 @@ def run_part(case):
                 break
         else:
             raise RuntimeError(f"{case}: no tie-free seed")
+    elif kind == "oc":
+        mgf.oc_case(case, p["n"], p["nf"], p["seed"], p["skw"])
     else:
         mgf.hs_case(case, p["n"], p["nf"], p["seed"], p["D"])
     os.makedirs(PARTS, exist_ok=True)

@@ -100,3 +100,55 @@ def test_hybridsort_4096_35_frames_deaths(g):
 
 def test_hybridsort_4096_eight_streams_one_launch(g):
     _hybridsort_run(g, fc.HS_S8)
+
+
+def test_ocsort_256_45_frames_deaths(g):
+    """C2 OCSORT 256 x 256 (GIoU) past max_age = 30 with ORU re-acquisitions: every frame
+    bit-exact, final Kalman states bit-exact, the ID counter."""
+    from yolo_tracking_amd.trackers.ocsort import OCSortEngine
+    name = "oc_n256_f45"
+    n, nf, seed = (int(x) for x in g[f"{name}__gen"])
+    low, drop = (float(x) for x in g[f"{name}__stream"])
+    frames = [d for d, _ in fc.make_frames(n, nf, seed, low_conf_frac=low, drop_frac=drop)]
+    assert float(np.sum([d.sum() for d in frames])) == g[f"{name}__in_sum"][0]
+    p = g[f"{name}__params"]
+    kw = dict(det_thresh=float(p[0]), max_age=int(p[1]), min_hits=int(p[2]),
+              asso_threshold=float(p[3]), delta_t=int(p[4]), inertia=float(p[5]),
+              use_byte=bool(p[6]), asso_func=str(g[f"{name}__asso"]))
+    shape = tuple(int(v) for v in g[f"{name}__img"]) + (3,)
+    eng = OCSortEngine(1, **kw)
+    nid = np.zeros(1, np.int64)
+    for f, d in enumerate(frames):
+        fc.check_frame(g, name, f, eng.update([d], [shape], next_id=nid)[0])
+    st = eng.state(0)
+    assert np.array_equal(st["id"], g[f"{name}__st_id"])
+    assert np.array_equal(st["x"], g[f"{name}__st_x"])
+    assert np.array_equal(st["P"][::64], g[f"{name}__st_P_sample"])
+    assert nid[0] == int(g[f"{name}__count"])
+
+
+def test_botsort_1024_d512_cmc_warp_30_frames(g):
+    """C3 BoT-SORT at size under the §8(d) CMC warp every frame (multi_gmc): ids, order,
+    det_ind, scores and classes exact every frame, boxes and final states within 1e-9 relative
+    (the warped covariance path is not the reference's operation order)."""
+    from yolo_tracking_amd.trackers.botsort import BoTSORTEngine
+    name = "bs_n1024_d512_cmc_f30"
+    frames, params, D = fc.botsort_frames(g, name)
+    warp = g[f"{name}__warp"]
+    eng = BoTSORTEngine(1, feat_dim=D, **params)
+    counts = g[f"{name}__out_counts"]
+    offs = np.concatenate([[0], np.cumsum(counts)])
+    rows = g[f"{name}__out"]
+    for f, (dets, embs) in enumerate(frames):
+        feats = reid_features(dets, embs, params["track_high_thresh"])
+        out = eng.update([dets], [feats], warps=warp[None])[0]
+        exp = rows[offs[f]:offs[f + 1]]
+        assert out.shape == exp.shape, (f, out.shape, exp.shape)
+        assert np.array_equal(out[:, 4:], exp[:, 4:]), f
+        np.testing.assert_allclose(out[:, :4], exp[:, :4], rtol=1e-9, atol=1e-9, err_msg=str(f))
+    st = eng.state(0)
+    assert np.array_equal(st["list"], g[f"{name}__st_list"])
+    assert np.array_equal(st["id"], g[f"{name}__st_id"])
+    np.testing.assert_allclose(st["mean"], g[f"{name}__st_mean"], rtol=1e-9, atol=1e-9)
+    np.testing.assert_allclose(st["cov"][::64], g[f"{name}__st_cov_sample"], rtol=1e-9,
+                               atol=1e-9)

@@ -8,6 +8,10 @@
 //   k_gather   N random 256-B records, the first 240 B of each (15 pieces) loaded straight into LDS
 //              with consecutive lanes on consecutive pieces (k_apply's global_load_lds gather)
 //   k_scatter  the same records written back from LDS (WRITE_SIZE)
+//   k_line0_32 k_finish's duplicate-removal read: one lane per random record, the record's first
+//              32 B (the Kalman mean's box half: two 16-B loads) - N distinct 128-B lines touched
+//   k_line0_80 k_finish's output-row read: one lane per random record, 32 B at offset 0 and the
+//              48-B meta at offset 64 (five 16-B loads) - N distinct 128-B lines touched
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -62,6 +66,24 @@ __global__ __launch_bounds__(T) void k_scatter(double2 *rec, const int *slot, in
     }
 }
 
+__global__ __launch_bounds__(256) void k_line0_32(const double2 *rec, const int *slot, int n,
+                                                   double *sink) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const double2 *r = rec + (long long)slot[i] * STRIDE;
+    const double2 a = r[0], b = r[1];
+    if (a.x + a.y + b.x + b.y == 12345.678) sink[0] = a.x;
+}
+
+__global__ __launch_bounds__(256) void k_line0_80(const double2 *rec, const int *slot, int n,
+                                                   double *sink) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const double2 *r = rec + (long long)slot[i] * STRIDE;
+    const double2 a = r[0], b = r[1], m0 = r[4], m1 = r[5], m2 = r[6];
+    if (a.x + a.y + b.x + b.y + m0.x + m1.y + m2.x == 12345.678) sink[0] = a.x;
+}
+
 int main() {
     const long long NS = (1LL << 30) / 16;   // 1 GiB of 16-B pieces
     const int CAP = 1 << 21, N = 1 << 20;    // 512 MiB of 256-B records, 1 Mi of them gathered
@@ -82,8 +104,17 @@ int main() {
     k_stream<<<4096, 256>>>(src, NS, sink);
     k_gather<<<N / T, T>>>(rec, dslot, N, sink);
     k_scatter<<<N / T, T>>>(rec, dslot, N);
+    // fresh records for the line-0 reads (the scatter's lines may still sit in the caches)
+    hipMemcpy(dslot, perm.data() + N, 4LL * N, hipMemcpyHostToDevice);
+    k_line0_32<<<N / 256, 256>>>(rec, dslot, N, sink);
+    std::shuffle(perm.begin(), perm.end(), std::mt19937(11));
+    hipMemcpy(dslot, perm.data(), 4LL * N, hipMemcpyHostToDevice);
+    k_stream<<<4096, 256>>>(src, NS, sink);   // flush the 256 MiB Infinity Cache between them
+    k_line0_80<<<N / 256, 256>>>(rec, dslot, N, sink);
     hipDeviceSynchronize();
     printf("k_stream reads %lld B; k_gather reads %lld B (%d records x %d B); k_scatter writes %lld B\n",
            16 * NS, 240LL * N, N, 240, 240LL * N);
+    printf("k_line0_32 reads %d records x 32 B (%d lines of 128 B); k_line0_80 reads %d x 80 B\n", N,
+           N, N);
     return 0;
 }
