@@ -88,6 +88,13 @@ int yta_grid_pairs(int device, const double *a, int na, const double *b, int nb,
 /* ---- ByteTrack Kalman filter, xyah state (parity / KAT entry points) -----------------------
  * mean: n x 8, cov: n x 8 x 8 (row-major, full matrices), meas / z: n x 4 [xc, yc, a, h]. */
 int yta_kf_xyah_initiate(int device, int n, const double *meas, double *mean, double *cov);
+/* Camera-motion correction KAT (SURVEY.md §8(b) affine_apply), in place on n states (mean 8,
+ * covariance 8 x 8 row-major, block-diagonal over {x, y, x', y'} / {w, h, w', h'} as every state
+ * of these trackers is), warps n row-major 2x3, with the engines' own device functions:
+ *   kind 0  BoT-SORT STrack.multi_gmc (bot_sort.py:95-111): kf_gmc (kf_xyah.hpp)
+ *   kind 1  DeepOCSORT apply_affine_correction, new-KF branch (deepocsort_kf.py:387-405;
+ *           deep_ocsort.py:250-267 calls it per tracker): kf8_affine (kf_deep.hpp) */
+int yta_affine_apply(int device, int kind, int n, const double *warps, double *mean, double *cov);
 /* in place; the caller applies the reference's `mean[7] = 0` for non-tracked tracks beforehand */
 int yta_kf_xyah_predict(int device, int n, double *mean, double *cov);
 int yta_kf_xyah_update(int device, int n, double *mean, double *cov, const double *z);

@@ -109,6 +109,7 @@ _SIGS = {
     "yta_lap_padded": ([_I, _I, _I, _P, _P, _P], _I),
     "yta_lap_rect": ([_I, _I, _I, _P, _P, _P], _I),
     "yta_lap_first_round": ([_I, _I, _I, _P, _P, _P, _P], _I),
+    "yta_affine_apply": ([_I, _I, _I, _P, _P, _P], _I),
     "yta_bytetrack_create": ([_I, _I, _I, _I, _P, _P], _I),
     "yta_bytetrack_destroy": ([_P], _I),
     "yta_bytetrack_reset": ([_P], _I),
@@ -418,6 +419,17 @@ def lap_rect(cost, device=0):
     y = np.empty(nc, dtype=np.int32)
     check(load_library().yta_lap_rect(device, nr, nc, ptr(c), ptr(x), ptr(y)))
     return x, y
+
+
+def affine_apply(kind, warps, mean, cov, device=0):
+    """Camera-motion correction of n Kalman states (yta_affine_apply): kind 0 BoT-SORT multi_gmc,
+    kind 1 DeepOCSORT apply_affine_correction.  Returns new (mean (n, 8), cov (n, 8, 8))."""
+    w = np.ascontiguousarray(warps, dtype=np.float64).reshape(-1, 6)
+    m = np.array(mean, dtype=np.float64).reshape(-1, 8)
+    c = np.array(cov, dtype=np.float64).reshape(-1, 8, 8)
+    assert len(w) == len(m) == len(c)
+    check(load_library().yta_affine_apply(device, int(kind), len(m), ptr(w), ptr(m), ptr(c)))
+    return m, c
 
 
 def lap_first_round(cost, device=0):

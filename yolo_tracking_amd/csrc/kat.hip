@@ -6,6 +6,7 @@
 #include "assoc.hpp"
 #include "aw.hpp"
 #include "grid.hpp"
+#include "kf_deep.hpp"
 #include "kf_xyah.hpp"
 #include "lap_dense.hpp"
 #include "lap_dense_block.hpp"
@@ -262,6 +263,56 @@ __global__ void k_aw_apply(const double *e, int nr, int nc, double w, const doub
     out[q] = ((w * rw[r]) * cw[c]) * e[q];
 }
 
+// Camera-motion correction of n Kalman states (mean 8, full 8 x 8 covariance, in place), with the
+// engines' own device functions: kind 0 = BoT-SORT STrack.multi_gmc (bot_sort.py:95-111, kf_gmc
+// on the compact record + cross terms), kind 1 = DeepOCSORT's KF correction
+// (deepocsort_kf.py:387-407, kf8_affine on the two 4x4 groups).  warps: n row-major 2x3.
+__global__ void k_affine(int kind, int n, const double *warps, double *mean, double *cov) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const double *H = warps + 6LL * i;
+    double *m = mean + 8LL * i, *P = cov + 64LL * i;
+    if (kind == 0) {
+        KfState s;
+        double x[16];
+        for (int k = 0; k < 8; ++k) s.m[k] = m[k];
+        for (int a = 0; a < 4; ++a) {   // compact 2x2 blocks {a, a+4}: pp, pv, vp, vv
+            s.c[4 * a + 0] = P[8 * a + a];
+            s.c[4 * a + 1] = P[8 * a + a + 4];
+            s.c[4 * a + 2] = P[8 * (a + 4) + a];
+            s.c[4 * a + 3] = P[8 * (a + 4) + a + 4];
+        }
+        for (int g = 0; g < 2; ++g)
+            for (int k = 0; k < 8; ++k) {
+                int r, c;
+                xcross(k, r, c);
+                x[8 * g + k] = P[8 * grp_global(g, r) + grp_global(g, c)];
+            }
+        kf_gmc(s, x, H);
+        for (int k = 0; k < 8; ++k) m[k] = s.m[k];
+        for (int k = 0; k < 64; ++k) P[k] = 0.0;
+        for (int g = 0; g < 2; ++g) {
+            double B[16];
+            grp_load(s, x, g, B);
+            for (int r = 0; r < 4; ++r)
+                for (int c = 0; c < 4; ++c) P[8 * grp_global(g, r) + grp_global(g, c)] = B[4 * r + c];
+        }
+    } else {
+        Kf8 s;
+        for (int k = 0; k < 8; ++k) s.x[k] = m[k];
+        for (int g = 0; g < 2; ++g)
+            for (int r = 0; r < 4; ++r)
+                for (int c = 0; c < 4; ++c) s.p[g][4 * r + c] = P[8 * dk_glob(g, r) + dk_glob(g, c)];
+        const double mm[4] = {H[0], H[1], H[3], H[4]}, t[2] = {H[2], H[5]};
+        kf8_affine(s, mm, t);
+        for (int k = 0; k < 8; ++k) m[k] = s.x[k];
+        for (int k = 0; k < 64; ++k) P[k] = 0.0;
+        for (int g = 0; g < 2; ++g)
+            for (int r = 0; r < 4; ++r)
+                for (int c = 0; c < 4; ++c) P[8 * dk_glob(g, r) + dk_glob(g, c)] = s.p[g][4 * r + c];
+    }
+}
+
 struct DevBuf {
     std::vector<void *> ptrs;
     ~DevBuf() {
@@ -356,6 +407,37 @@ static int kf_call(int device, int op, int n, const double *vec, double *mean, d
         YTA_HIP(hipMemcpy(dc, cov, sizeof(double) * 64 * n, hipMemcpyHostToDevice));
     }
     hipLaunchKernelGGL(k_kf, dim3((n + 127) / 128), dim3(128), 0, 0, op, n, dv, dm, dc);
+    YTA_HIP(hipGetLastError());
+    YTA_HIP(hipMemcpy(mean, dm, sizeof(double) * 8 * n, hipMemcpyDeviceToHost));
+    YTA_HIP(hipMemcpy(cov, dc, sizeof(double) * 64 * n, hipMemcpyDeviceToHost));
+    return YTA_OK;
+}
+
+int yta_affine_apply(int device, int kind, int n, const double *warps, double *mean,
+                     double *cov) {
+    YTA_CHECK(kind == 0 || kind == 1, YTA_ERR_INVALID, "kind %d: 0 (BoT-SORT multi_gmc) or 1 "
+              "(DeepOCSORT)", kind);
+    YTA_CHECK(n >= 0, YTA_ERR_INVALID, "negative n");
+    if (n == 0) return YTA_OK;
+    YTA_CHECK(warps && mean && cov, YTA_ERR_INVALID, "null buffer");
+    // the engines keep P block-diagonal over {x, y, x', y'} and {w, h, w', h'} (kf_xyah.hpp,
+    // kf_deep.hpp): a covariance coupling the two groups is not a state they can hold
+    for (long long q = 0; q < n; ++q)
+        for (int r = 0; r < 8; ++r)
+            for (int c = 0; c < 8; ++c)
+                YTA_CHECK(((r >> 1) & 1) == ((c >> 1) & 1) || cov[64 * q + 8 * r + c] == 0.0,
+                          YTA_ERR_INVALID, "track %lld: covariance couples (x, y) with (w, h)", q);
+    int rc = select_device(device);
+    if (rc) return rc;
+    DevBuf m;
+    double *dw, *dm, *dc;
+    YTA_HIP(m.get(&dw, 6 * (size_t)n));
+    YTA_HIP(m.get(&dm, 8 * (size_t)n));
+    YTA_HIP(m.get(&dc, 64 * (size_t)n));
+    YTA_HIP(hipMemcpy(dw, warps, sizeof(double) * 6 * n, hipMemcpyHostToDevice));
+    YTA_HIP(hipMemcpy(dm, mean, sizeof(double) * 8 * n, hipMemcpyHostToDevice));
+    YTA_HIP(hipMemcpy(dc, cov, sizeof(double) * 64 * n, hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(k_affine, dim3((n + 63) / 64), dim3(64), 0, 0, kind, n, dw, dm, dc);
     YTA_HIP(hipGetLastError());
     YTA_HIP(hipMemcpy(mean, dm, sizeof(double) * 8 * n, hipMemcpyDeviceToHost));
     YTA_HIP(hipMemcpy(cov, dc, sizeof(double) * 64 * n, hipMemcpyDeviceToHost));
