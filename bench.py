@@ -215,6 +215,12 @@ def launch_ranks(argv, n):
     return rc
 
 
+def peak_rss_mb():
+    """This process's peak resident set (MB), before the rank-0-only PCIe / CPU legs."""
+    import resource
+    return round(resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 1024.0, 1)
+
+
 def cpu_model():
     try:
         with open("/proc/cpuinfo") as f:
@@ -598,6 +604,12 @@ def main():
 
     elapsed = max_over_ranks(elapsed, dist, "cpu" if args.shared_gpu else "cuda")
     value = aggregate_rate(world, S, args.steps, elapsed)
+    # host memory of every rank after staging and the timed region (the frames live in HBM; the
+    # host holds one frame of every stream while staging): peak RSS per rank, in MB
+    rss = [peak_rss_mb()]
+    if dist:
+        rss = [None] * world
+        dist.all_gather_object(rss, peak_rss_mb())
     ms_per_step = 1000.0 * elapsed / args.steps
 
     st_launch = {k: v // Q for k, v in st.items()}   # one engine's launch (Q equal slices)
@@ -709,6 +721,7 @@ def main():
                                       "and a 576-B Kalman state that this build never forms",
             "dense_upper_bound_bytes_per_update": algorithmic_bytes(N, N),
             "stage_seconds": round(gen_s, 1),
+            "host_peak_rss_mb_by_rank": rss,
         }
         print(json.dumps(line))
     if dist:

@@ -169,3 +169,32 @@ def test_botsort_multistream_matches_oracle():
         for s in range(S):
             exp = ors[s].update(dets[s], feats[s]).reshape(-1, 8)
             assert np.array_equal(got[s], exp), (s, f)
+
+
+@pytest.mark.parametrize("crowd", [False, True])
+def test_split_stage1_equals_fused(monkeypatch, crowd):
+    """Stage 1 with ReID as three launches (k_bs_prep / k_bs_edges chip-wide / k_bs_lap, the
+    default for few streams) against the fused k_stage1 (YTA_BS_SPLIT=0): identical rows, states
+    and features every frame.  crowd: objects packed 8x denser than the generator's default, so
+    pool rows with more than E_SLOTS candidate edges send k_bs_lap down the fused association."""
+    from test_oracle_golden import reid_features
+    from yolo_tracking_amd.synth import make_frames
+    from yolo_tracking_amd.trackers.botsort import BoTSORTEngine
+    n, D = 400, 64
+    canvas = 64.0 * np.sqrt(n) / (8.0 if crowd else 1.0)
+    frames = make_frames(n, 12, seed=77 if crowd else 78, emb_dim=D, canvas=canvas)
+    P = dict(track_high_thresh=0.5, track_low_thresh=0.1, new_track_thresh=0.6,
+             track_buffer=30, match_thresh=0.8, proximity_thresh=0.5, appearance_thresh=0.25,
+             frame_rate=30)
+    engs = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("YTA_BS_SPLIT", mode)
+        engs[mode] = BoTSORTEngine(1, feat_dim=D, **P)
+    for f, (dets, embs) in enumerate(frames):
+        feats = reid_features(dets, embs, P["track_high_thresh"])
+        a = engs["1"].update([dets], [feats])[0]
+        b = engs["0"].update([dets], [feats])[0]
+        assert np.array_equal(a, b), f
+    sa, sb = engs["1"].state(0), engs["0"].state(0)
+    assert all(np.array_equal(sa[k], sb[k]) for k in sa)
+    assert np.array_equal(engs["1"].features(0)[0], engs["0"].features(0)[0])

@@ -112,8 +112,17 @@ struct StageShared {
     AssocShared as;
 };
 
+// The lists of stage 1 (everything before the association): detections split, pool and
+// unconfirmed lists with their boxes.
+struct S1Lists {
+    int nd, n_high, n_second, n_act, n_unc, n_pool;
+    Box *hbox;       // the high detections' boxes / scores staged in the arena (or nullptr)
+    double *hw;
+};
+
 template <int V>
-__device__ __forceinline__ bool stage1_body(const BtArgs &a, int s, Arena &ar, StageShared &sh) {
+__device__ __forceinline__ S1Lists stage1_lists(const BtArgs &a, int s, Arena &ar,
+                                                StageShared &sh) {
     int *wsum = sh.as.lap.wsum;
     const int t = threadIdx.x, nt = blockDim.x;
     BtCounters *c = a.cnt + s;
@@ -225,6 +234,18 @@ __device__ __forceinline__ bool stage1_body(const BtArgs &a, int s, Arena &ar, S
     const int n_pool = n_act + n_lost;
     block_sync();
     YTA_STAMP(4);
+    return S1Lists{nd, n_high, n_second, n_act, n_unc, n_pool, hbox, hw};
+}
+
+// Stage 1's association over the lists (bot_sort.py:307-322 / byte_tracker.py:181-186).
+template <int V>
+__device__ __forceinline__ bool stage1_assoc(const BtArgs &a, int s, const S1Lists &L, Arena &ar,
+                                             StageShared &sh) {
+    BtCounters *c = a.cnt + s;
+    const long long db = (long long)s * a.MAXD, tb = (long long)s * a.CAP;
+    const int n_pool = L.n_pool, n_high = L.n_high;
+    Box *hbox = L.hbox;
+    double *hw = L.hw;
     bool ok;
     if (V == VAR_BOTSORT && a.D > 0)   // min(iou, gated appearance) (bot_sort.py:307-322)
         ok = assoc_block_emb(
@@ -241,22 +262,33 @@ __device__ __forceinline__ bool stage1_body(const BtArgs &a, int s, Arena &ar, S
             [&](int j) { return a.high_box[db + j]; }, V == VAR_BYTETRACK || a.fuse_first != 0,
             [&](int j) { return a.high_score[db + j]; }, a.match_thresh, a.x1 + tb, a.y1 + db,
             &c->err, &c->n_edges[0], ar, slab_of(a, s), sh.as, hbox, hw);
-    if (!ok) return false;
-    if (t == 0) {
-        c->frame_id += 1;
-        c->n_dets = nd;
-        c->n_high = n_high;
-        c->n_second = n_second;
-        c->n_act = n_act;
-        c->n_unc = n_unc;
-        c->n_pool = n_pool;
-        c->n_left = 0;
-        c->n_rest = 0;
-        c->n_births = 0;
-        c->n_lazy = 0;
-        c->n_res1 = 0;
-        c->n_ref = 0;
-    }
+    return ok;
+}
+
+// The frame's stage-1 counters (frame_id advances with them unless `advance` is false: the split
+// BoT-SORT stage 1 advances it in k_bs_lap, after the solve)
+__device__ __forceinline__ void stage1_commit(BtCounters *c, const S1Lists &L, bool advance) {
+    if (threadIdx.x != 0) return;
+    if (advance) c->frame_id += 1;
+    c->n_dets = L.nd;
+    c->n_high = L.n_high;
+    c->n_second = L.n_second;
+    c->n_act = L.n_act;
+    c->n_unc = L.n_unc;
+    c->n_pool = L.n_pool;
+    c->n_left = 0;
+    c->n_rest = 0;
+    c->n_births = 0;
+    c->n_lazy = 0;
+    c->n_res1 = 0;
+    c->n_ref = 0;
+}
+
+template <int V>
+__device__ __forceinline__ bool stage1_body(const BtArgs &a, int s, Arena &ar, StageShared &sh) {
+    const S1Lists L = stage1_lists<V>(a, s, ar, sh);
+    if (!stage1_assoc<V>(a, s, L, ar, sh)) return false;
+    stage1_commit(a.cnt + s, L, true);
     return true;
 }
 
@@ -1120,6 +1152,143 @@ __global__ __launch_bounds__(BLKL, 4) void k_s1_lap(BtArgs a) {
     Arena ag(a.ws + s * a.ws_stride, a.ws_stride);
     if (!s1_lap_body(a, s, ag, lsh) && threadIdx.x == 0) atomicOr(&a.cnt[s].err, ERR_EDGE_OVERFLOW);
     YTA_BLK(2, 1);
+}
+
+// ------------------------------------------------------------ BoT-SORT stage 1, split (C3)
+// With ReID features, k_stage1's block per stream spends most of a few-stream frame on the
+// appearance costs of the candidate pairs (bot_sort.py:307-322: ~2.5 D-long dot products per pool
+// row, read through one CU).  For few streams the stage runs as three launches instead:
+//   k_bs_prep  block / stream: the lists and boxes of stage 1 (stage1_lists)
+//   k_bs_edges chip-wide, one wave per pool row: the row against every high detection (f64 box
+//              test), the IoU cost, and for pairs inside proximity_thresh the cosine distance of
+//              the features with the same 16-lane reduction k_stage1 uses (cosine_dist16), so
+//              every cost has the same bits; edges with cost < match_thresh into the row's
+//              E_SLOTS slots (e_cnt / e_col / e_cost, the layout k_s1_lap reads)
+//   k_bs_lap   block / stream: lap_block over the edges (s1_lap_body, which solves the problem on
+//              order-preserving renumberings: the same assignment as k_stage1's lap_block); a
+//              stream with a row of more than E_SLOTS edges runs k_stage1's association instead.
+// Same results as k_stage1 on every stream.
+constexpr int BSE_T = 256;   // k_bs_edges threads: 4 waves = 4 pool rows per block
+
+__global__ __launch_bounds__(PREP_T) void k_bs_prep(BtArgs a) {
+    __shared__ StageShared sh;
+    const int s = blockIdx.x;
+    if (stream_skipped(a, s)) return;
+    Arena none(nullptr, 0);   // no staged high boxes (the embedding association does not use them)
+    const S1Lists L = stage1_lists<VAR_BOTSORT>(a, s, none, sh);
+    stage1_commit(a.cnt + s, L, false);
+    if (threadIdx.x == 0) {
+        a.cnt[s].bs_spill = 0;
+        a.cnt[s].n_edges[0] = 0;
+    }
+}
+
+__global__ __launch_bounds__(BSE_T) void k_bs_edges(BtArgs a) {
+    const int s = blockIdx.y;
+    if (stream_skipped(a, s)) return;
+    BtCounters *c = a.cnt + s;
+    const int i = blockIdx.x * (BSE_T / WAVE) + threadIdx.x / WAVE;   // pool row (wave-uniform)
+    const int n_pool = c->n_pool, nh = c->n_high;
+    if (i >= n_pool) return;
+    const int lane = lane_id(), grp = lane >> 4;
+    const long long tb = (long long)s * a.CAP, db = (long long)s * a.MAXD;
+    const long long SC = (long long)a.S * a.CAP;
+    const double prox = a.prox_thresh, app = a.app_thresh, thresh = a.match_thresh;
+    const bool fused = a.fuse_first != 0;
+    const Box rb = a.pool_box[tb + i];
+    const float *rfeat = a.feat + (tb + a.pool[tb + i]) * a.D;
+    int n = 0;   // the row's edges (wave-uniform)
+    auto put = [&](bool e, int j, double cost) {   // edges of this pass in lane order
+        const unsigned long long m = __ballot(e);
+        if (e) {
+            const int k = n + __popcll(m & ((1ull << lane) - 1ull));
+            if (k < E_SLOTS) {
+                a.e_col[k * SC + tb + i] = j;
+                a.e_cost[k * SC + tb + i] = cost;
+            }
+        }
+        n += __popcll(m);
+    };
+    for (int j0 = 0; j0 < nh; j0 += WAVE) {
+        const int j = j0 + lane;
+        bool hit = false;
+        double d = 1.0, cc = 1.0;
+        if (j < nh) {
+            const Box cb = a.high_box[db + j];
+            if (intersects(rb, cb)) {
+                hit = true;
+                d = 1 - iou(rb, cb);                                        // matching.py:117
+                cc = fused ? 1 - (1 - d) * a.high_score[db + j] : d;       // matching.py:216-220
+            }
+        }
+        const bool masked = hit && d > prox;                               // emb masked (:319)
+        const double mc = np_min(cc, 1.0);
+        put(masked && mc < thresh, j, mc);
+        // pairs that need the appearance cost: four at a time, one 16-lane group each
+        unsigned long long pend = __ballot(hit && !masked);
+        while (pend) {
+            int src = -1;   // the pending lane this group takes
+            unsigned long long p = pend;
+            for (int g = 0; g < 4 && p; ++g) {
+                const int b = __ffsll((long long)p) - 1;
+                p &= p - 1;
+                if (g == grp) src = b;
+            }
+            pend = p;
+            const int jj = __shfl(j, src < 0 ? 0 : src);
+            const double ccj = __shfl(cc, src < 0 ? 0 : src);
+            const DetFeat f = det_feat(a, s, db, a.high[db + (src < 0 ? j0 : jj)]);
+            const double cd = cosine_dist16(rfeat, f, a.D);
+            double cost = 1.0;
+            if (src >= 0) {
+                double emb = np_max(0.0, cd) / 2.0;                           // matching.py:164-166
+                if (emb > app) emb = 1.0;                                       // bot_sort.py:318
+                cost = np_min(ccj, emb);                                        // bot_sort.py:320
+            }
+            put((lane & 15) == 0 && src >= 0 && cost < thresh, jj, cost);
+        }
+    }
+    if (lane == 0) {
+        a.e_cnt[tb + i] = n;
+        if (n > E_SLOTS) atomicOr(&c->bs_spill, 1);
+        if (n) atomicAdd(&c->n_edges[0], n);
+    }
+}
+
+__global__ __launch_bounds__(BLK1) void k_bs_lap(BtArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    __shared__ StageShared sh;
+    const int s = blockIdx.x, t = threadIdx.x, nt = blockDim.x;
+    if (stream_skipped(a, s)) return;
+    BtCounters *c = a.cnt + s;
+    const long long tb = (long long)s * a.CAP, db = (long long)s * a.MAXD;
+    const int n_pool = c->n_pool, n_high = c->n_high;
+    const bool spill = c->bs_spill != 0;
+    const S1Lists L{c->n_dets, n_high, c->n_second, c->n_act, c->n_unc, n_pool, nullptr, nullptr};
+    if (!spill) {   // s1_lap_body writes only the residual matches
+        for (int q = t; q < n_pool; q += nt) a.x1[tb + q] = -1;
+        for (int q = t; q < n_high; q += nt) a.y1[db + q] = -1;
+        block_sync();
+    }
+    bool ok;
+    {
+        Arena ar(smem, a.lds_bytes);
+        ok = spill ? stage1_assoc<VAR_BOTSORT>(a, s, L, ar, sh) : s1_lap_body(a, s, ar, sh.as.lap);
+    }
+    if (!ok) {   // the stream's global arena
+        block_sync();
+        if (t == 0) c->n_fallback[0] += 1;
+        if (!spill) {
+            for (int q = t; q < n_pool; q += nt) a.x1[tb + q] = -1;
+            for (int q = t; q < n_high; q += nt) a.y1[db + q] = -1;
+            block_sync();
+        }
+        Arena ag(a.ws + s * a.ws_stride, a.ws_stride);
+        ok = spill ? stage1_assoc<VAR_BOTSORT>(a, s, L, ag, sh) : s1_lap_body(a, s, ag, sh.as.lap);
+        if (!ok && t == 0) atomicOr(&c->err, ERR_EDGE_OVERFLOW);
+    }
+    block_sync();
+    if (t == 0) c->frame_id += 1;
 }
 
 // ------------------------------------------------------------------------------------ k_apply
@@ -2012,6 +2181,9 @@ struct yta_bytetrack {
     int *d_det_off = nullptr;
     float *d_det32 = nullptr, *h_det32 = nullptr;   // float32 detection rows (before widening)
     long long det32_cap = 0;
+    // BoT-SORT with ReID: stage 1 as k_bs_prep / k_bs_edges / k_bs_lap (few streams) instead of
+    // the fused k_stage1 (set at create; YTA_BS_SPLIT=0 / 1 overrides)
+    bool bs_split = false;
     // stream-subset updates: the [S] mask on the device and its pinned staging
     int *d_active = nullptr, *h_active = nullptr;
     // pipelined host-buffer updates (yta_bytetrack_submit / _collect): PIPE_DEPTH frame slots, a
@@ -2226,6 +2398,12 @@ int bt_alloc(yta_bytetrack *e) {
     a.lds_bytes_l = BT_LDSL_BYTES;
     a.lds_bytes_e = BT_LDSE_BYTES;
     a.ws_stride = assoc_arena_bytes(CAP, MAXD, CAP * MAXD);
+    if (e->variant == VAR_BOTSORT && e->D > 0) {   // split stage 1 (k_bs_edges / k_bs_lap)
+        a.ws_stride = std::max(a.ws_stride, s1_lap_arena_bytes(CAP, MAXD, CAP * MAXD));
+        DALLOC(a.e_cnt, S * CAP);
+        DALLOC(a.e_col, E_SLOTS * S * CAP);
+        DALLOC(a.e_cost, E_SLOTS * S * CAP);
+    }
     if (e->variant == VAR_BYTETRACK) {   // stage 1 as k_s1_prep / k_s1_edges / k_s1_lap
         a.ws_stride = std::max(a.ws_stride, s1_lap_arena_bytes(CAP, MAXD, CAP * MAXD));
         DALLOC(a.g_cell, S * (GRID_MAX_CELLS + 1));
@@ -2276,7 +2454,7 @@ int mark(yta_bytetrack *e) {
 int set_lds_limits(size_t bytes) {
     const int b = (int)bytes;
     for (const void *k : {(const void *)k_stage1<VAR_BYTETRACK>, (const void *)k_stage1<VAR_BOTSORT>,
-                          (const void *)k_stage23<VAR_BYTETRACK>,
+                          (const void *)k_bs_lap, (const void *)k_stage23<VAR_BYTETRACK>,
                           (const void *)k_stage23<VAR_BOTSORT>, (const void *)k_s1_lap})
         YTA_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, b));
     // k_s1_edges never launches with more than BT_LDSE_BYTES (its wave queues are static LDS)
@@ -2306,6 +2484,16 @@ int launch_frame(yta_bytetrack *e) {
         YTA_HIP(hipGetLastError());
         MARK();
         hipLaunchKernelGGL(k_s1_lap, dim3(a.S), dim3(BLKL), a.lds_bytes_l, e->stream, a);
+    } else if (V == VAR_BOTSORT && reid && e->bs_split && a.prox_thresh < 1.0 &&
+               a.match_thresh <= 1.0) {   // split stage 1 (k_bs_*): few streams
+        hipLaunchKernelGGL(k_bs_prep, dim3(a.S), dim3(PREP_T), 0, e->stream, a);
+        YTA_HIP(hipGetLastError());
+        MARK();
+        const dim3 ge((a.CAP + BSE_T / WAVE - 1) / (BSE_T / WAVE), a.S);
+        hipLaunchKernelGGL(k_bs_edges, ge, dim3(BSE_T), 0, e->stream, a);
+        YTA_HIP(hipGetLastError());
+        MARK();
+        hipLaunchKernelGGL(k_bs_lap, dim3(a.S), dim3(BLK1), a.lds_bytes, e->stream, a);
     } else {   // fused stage 1: the whole stage in the first phase, the next two empty
         hipLaunchKernelGGL(k_stage1<V>, dim3(a.S), dim3(BLK1), a.lds_bytes, e->stream, a);
         YTA_HIP(hipGetLastError());
@@ -3047,6 +3235,9 @@ int yta_botsort_create(int device, int n_streams, int track_capacity, int max_de
                              e->variant = VAR_BOTSORT;
                              e->bprm = prm;
                              e->D = D;
+                             // few streams: the appearance costs chip-wide (k_bs_edges)
+                             e->bs_split = D > 0 && n_streams <= 64;
+                             if (const char *v = getenv("YTA_BS_SPLIT")) e->bs_split = D > 0 && atoi(v);
                          });
 }
 

@@ -54,7 +54,9 @@ struct BtCounters {                  // one per stream, 128 B
     int n_ref;                       // re-found Lost tracks (refound list)
     int n_fallback_f;                // cumulative: k_finish's duplicate-removal grid over global
     int slot_cursor;                 // births take free slots from here on, cyclically
-    int pad[2];
+    int bs_spill;                    // BoT-SORT split stage 1: a pool row had more than E_SLOTS
+                                     // edges (k_bs_lap then runs the fused association)
+    int pad;
 };
 static_assert(sizeof(BtCounters) == 128, "BtCounters layout");
 
