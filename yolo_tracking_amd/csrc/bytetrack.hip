@@ -704,6 +704,18 @@ __device__ __forceinline__ void s1_edges_body(const BtArgs &a, int s, int nc, in
 // order-free).  Queues hold WQ_CAP entries; a larger candidate total is listed and scored in
 // windows.  Big items (larger than 4 x the mean box) are visited per lane, as grid_query does.
 constexpr int WQ_CAP = 384;
+#ifndef YTA_S1_SOA
+#define YTA_S1_SOA 1   // k_s1_edges' LDS grid keeps its boxes as four arrays (GridView::sx)
+#endif
+__device__ __forceinline__ Box s1_box(const GridView &gv, int k) {
+#if YTA_S1_SOA
+    const double *x = gv.sx;
+    const int n = gv.sn;
+    return Box{x[k], x[n + k], x[2 * n + k], x[3 * n + k]};
+#else
+    return gv.boxes[k];
+#endif
+}
 struct EdgeWaveQ {
     unsigned q[WQ_CAP];   // lane << 24 | grid position
     int cnt[WAVE];        // edges of the wave's row `lane`
@@ -767,7 +779,7 @@ __device__ __forceinline__ void s1_edges_rows_wave(const BtArgs &a, int s, int n
                 const int r = (int)(ent >> 24), pos = (int)(ent & 0xFFFFFFu);
                 const Box tb_{bperm_f64(rb.x1, r), bperm_f64(rb.y1, r), bperm_f64(rb.x2, r),
                               bperm_f64(rb.y2, r)};
-                const bool hit = k < n && intersects(tb_, gv.boxes[pos]);
+                const bool hit = k < n && intersects(tb_, s1_box(gv, pos));
                 const unsigned long long bal = __ballot(hit);
                 if (hit) wq.q[ns + __popcll(bal & ((1ull << lane) - 1ull))] = ent;
                 ns += __popcll(bal);
@@ -782,7 +794,7 @@ __device__ __forceinline__ void s1_edges_rows_wave(const BtArgs &a, int s, int n
                 const Box tb_{bperm_f64(rb.x1, r), bperm_f64(rb.y1, r), bperm_f64(rb.x2, r),
                               bperm_f64(rb.y2, r)};
                 if (k >= ns) continue;
-                const Box cb = gv.boxes[pos];
+                const Box cb = s1_box(gv, pos);
                 const double dist = 1 - iou(tb_, cb);                   // matching.py:117
                 const double cost = 1 - (1 - dist) * gv.w[pos];         // matching.py:216-220
                 if (!(cost < thresh)) continue;
@@ -917,7 +929,13 @@ __global__ __launch_bounds__(BLKE, 4) void k_s1_edges(BtArgs a) {
     gv.hdr = nullptr;
     gv.cell_start = ar.alloc<int>(grid_cells_for(nc) + 1);
     gv.ids = ar.alloc<int>(nc);
+#if YTA_S1_SOA
+    gv.boxes = nullptr;   // the boxes as four arrays (GridView::sx): conflict-free wave reads
+    gv.sx = ar.alloc<double>(4LL * nc);
+    gv.sn = nc;
+#else
     gv.boxes = ar.alloc<Box>(nc);
+#endif
     gv.w = ar.alloc<double>(nc);
     gv.big = ar.alloc<int>(nc);
     int *cdeg = ar.alloc<int>(nc);
@@ -938,7 +956,7 @@ __global__ __launch_bounds__(BLKE, 4) void k_s1_edges(BtArgs a) {
     for (int q = t; q <= ncell; q += nt) gg.cell_start[q] = gv.cell_start[q];
     for (int q = t; q < h.n_binned; q += nt) {
         gg.ids[q] = gv.ids[q];
-        gg.boxes[q] = gv.boxes[q];
+        gg.boxes[q] = s1_box(gv, q);
         gg.w[q] = gv.w[q];
     }
     for (int q = t; q < h.n_big; q += nt) gg.big[q] = gv.big[q];

@@ -41,10 +41,16 @@ struct GridView {
     double *w;         // optional per-item weight, same order (nullptr: none)
     int *big;          // items scanned by every query
     const Box *by_id = nullptr;   // with boxes == nullptr: every item's box, by item id
+    // structure-of-arrays boxes (x1[], y1[], x2[], y2[], cell order) instead of `boxes`: a wave
+    // reading the boxes of consecutive positions then reads consecutive 8-B words per component
+    // (no LDS bank conflicts), where 32-B records put two lanes on every bank pair it touches
+    double *sx = nullptr;         // 4 arrays of n doubles: sx, sx + n, sx + 2 n, sx + 3 n
+    int sn = 0;
 };
 
 // Box of the binned item at cell-order position k.
 __device__ __forceinline__ Box grid_box(const GridView &gv, int k) {
+    if (gv.sx) return Box{gv.sx[k], gv.sx[gv.sn + k], gv.sx[2 * gv.sn + k], gv.sx[3 * gv.sn + k]};
     return gv.boxes ? gv.boxes[k] : gv.by_id[gv.ids[k]];
 }
 
@@ -198,6 +204,12 @@ __device__ __forceinline__ void grid_build(int n, BoxOf box, WOf wof, GridView g
         const int pos = atomicAdd(&cs[cell_of(b) + 1], 1);
         gv.ids[pos] = i;
         if (gv.boxes) gv.boxes[pos] = b;
+        if (gv.sx) {
+            gv.sx[pos] = b.x1;
+            gv.sx[gv.sn + pos] = b.y1;
+            gv.sx[2 * gv.sn + pos] = b.x2;
+            gv.sx[3 * gv.sn + pos] = b.y2;
+        }
         if (gv.w) gv.w[pos] = wof(i);
     }
     block_sync();
