@@ -217,7 +217,8 @@ def main():
         fnst.argtypes = [ctypes.c_void_p]
         _lib.check(fnst(st.ctypes.data))
         print(f"k_hs_lap (block 0, {args.steps} frames): free rows {int(st[100])}, steps "
-              f"{int(st[101])}, scan {int(st[102]) / 100:.0f} us, reduce {int(st[103]) / 100:.0f} us",
+              f"{int(st[101])}, scan {int(st[102]) / 100:.0f} us, reduce {int(st[103]) / 100:.0f} us, "
+              f"bidding rounds {int(st[106])} ({int(st[107]) / 100:.0f} us)",
               file=sys.stderr)
     stats = eng.stats()
     if fam and len(engines) > 1:   # summed over the engines: the same totals as one engine of S

@@ -1021,7 +1021,7 @@ int doc_alloc(yta_deepocsort *e) {
     DOCALLOC(a.ema_row, S * (MAXD + CAP));
     DOCALLOC(a.out, S * CAP * 8);
     const long long n = std::max(CAP, MAXD);
-    a.lap_ws_stride = (n > OC_LDS_LAP_N ? ((dense_lap_ws_bytes(n) + 255) & ~255LL) : 256) + tight_ws_bytes();
+    a.lap_ws_stride = oc_lap_ws_stride(n);
     DOCALLOC(a.lap_ws, S * a.lap_ws_stride);
     e->lds = (size_t)oc_lds_bytes(CAP, MAXD);
     DOCALLOC(e->d_off, S + 1);

@@ -995,7 +995,7 @@ int hs_alloc(yta_hybridsort *e) {
     HSALLOC(a.ema_row, S * (MAXD + CAP));
     HSALLOC(a.out, S * CAP * 8);
     const long long n = std::max(CAP, MAXD);
-    a.lap_ws_stride = (n > OC_LDS_LAP_N ? ((dense_lap_ws_bytes(n) + 255) & ~255LL) : 256) + tight_ws_bytes();
+    a.lap_ws_stride = oc_lap_ws_stride(n);
     HSALLOC(a.lap_ws, S * a.lap_ws_stride);
     e->lds = (size_t)oc_lds_bytes(CAP, MAXD);
     HSALLOC(e->d_off, S + 1);

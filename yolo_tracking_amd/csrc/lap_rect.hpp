@@ -12,6 +12,9 @@
 //      first column, and s2_i = second minimum - minimum (a lower bound of row i's reduced costs
 //      off its own column);
 //   2. every row claims its argmin column; the lowest claiming row keeps it (tight, feasible);
+//      with the bidding arrays (RectWs::av, the OCSORT-family first round): rounds of bids instead
+//      (rect_arr below), the first from the pre-pass, which leave fewer free rows and shorter
+//      searches;
 //   3. every other row is augmented by Dijkstra over the columns, one block-wide step per row
 //      relaxation.  Pruning: the row of an assigned column j is only relaxed while
 //      spc_j + s2_row < B, B = the cheapest free column reached so far; any other row can only
@@ -46,32 +49,53 @@ struct RectMat {
 // the column duals on return (the transposed first round's uniqueness certificate); they cost 8 B
 // a column, which would push a 4096 x 4096 problem's arrays out of LDS.
 struct RectWs {
-    double *u, *s2;     // rows
+    double *u;          // rows
+    float *s2;          // rows: the bound, rounded down (still a lower bound)
     double *v;          // cols: the column duals on return (<= 0, 0 on free columns), or nullptr
     int *x, *fl;        // rows: assigned column, free-row list
     int *path, *yw;     // cols: predecessor row, owner row (authoritative copy)
+    // bidding rounds before the searches (rect_arr; nullptr: the claims only), global memory:
+    double *av = nullptr;               // cols: column duals during the rounds (LDS when it fits)
+    unsigned long long *abid = nullptr; // cols: the largest bid of the round
+    int *atgt = nullptr;                // rows: the column a free row bids for
+    double *adel = nullptr;             // rows: its bid (second minimum - minimum)
 };
+// The bidding rounds' arrays (rect_arr_ws), 16-B aligned pieces.
+__host__ __device__ inline long long arr_ws_bytes(long long rows, long long cols) {
+    return cols * 16 + rows * 12 + 64;
+}
+__host__ __device__ inline void rect_arr_ws(unsigned char *base, int rows, int cols, RectWs &w) {
+    w.av = reinterpret_cast<double *>(base);
+    w.abid = reinterpret_cast<unsigned long long *>(w.av + cols);
+    w.adel = reinterpret_cast<double *>(w.abid + cols);
+    w.atgt = reinterpret_cast<int *>(w.adel + rows);
+}
 __host__ __device__ inline long long rect_ws_bytes(long long rows, long long cols,
                                                    bool duals = false) {
-    return rows * 24 + cols * (duals ? 16 : 8) + 64;
+    return rows * 20 + cols * (duals ? 16 : 8) + 64;
 }
 __host__ __device__ inline RectWs rect_ws(unsigned char *base, int rows, int cols,
                                           bool duals = false) {
     RectWs w;
     w.u = reinterpret_cast<double *>(base);
-    w.s2 = w.u + rows;
-    w.x = reinterpret_cast<int *>(w.s2 + rows);
+    w.x = reinterpret_cast<int *>(w.u + rows);
     w.fl = w.x + rows;
-    w.path = w.fl + rows;
+    w.s2 = reinterpret_cast<float *>(w.fl + rows);
+    w.path = reinterpret_cast<int *>(w.s2 + rows);
     w.yw = w.path + cols;
-    // 8-aligned: 24 * rows + 8 * cols bytes precede it
-    w.v = duals ? reinterpret_cast<double *>(w.yw + cols) : nullptr;
+    // 8-aligned: 20 * rows + 8 * cols bytes precede it (+ 4 when rows is odd)
+    const size_t vo = ((size_t)20 * rows + (size_t)8 * cols + 7) & ~(size_t)7;
+    w.v = duals ? reinterpret_cast<double *>(base + vo) : nullptr;
     return w;
 }
 constexpr int RECT_CPT_MAX = 32;
 
-// One wave: minimum of row i (first column on ties), and second minimum - minimum.
-__device__ __forceinline__ void rect_row_pre(const RectMat M, int i, double *u, int *x, double *s2) {
+// One wave: minimum of row i (first column on ties), and second minimum - minimum (a float s2:
+// rounded down, so still a lower bound).
+__device__ __forceinline__ void store_s2(double *s2, int i, double d) { s2[i] = d; }
+__device__ __forceinline__ void store_s2(float *s2, int i, double d) { s2[i] = __double2float_rd(d); }
+template <typename S2T>
+__device__ __forceinline__ void rect_row_pre(const RectMat M, int i, double *u, int *x, S2T *s2) {
     const int lane = lane_id();
     double m1 = INFINITY, m2 = INFINITY;
     int k1 = INT_MAX;
@@ -94,7 +118,7 @@ __device__ __forceinline__ void rect_row_pre(const RectMat M, int i, double *u, 
     if (lane == 0) {
         u[i] = m1;
         x[i] = k1 == INT_MAX ? 0 : k1;
-        s2[i] = m2 - m1;
+        store_s2(s2, i, m2 - m1);
     }
 }
 
@@ -140,6 +164,144 @@ __device__ __forceinline__ void wave_rect_reduce(double &a, int &ka, double &b, 
     a = ra; ka = rka; b = rb; kb = rkb; m = rm;
 }
 
+// ---- bidding rounds (augmenting row reduction, all free rows at once)
+// A free row i bids for the column j1 of its smallest reduced cost c_ij - v_j with
+// delta = (second smallest) - (smallest); each column goes to its largest bid (lowest row on equal
+// bids), whose column dual drops by that delta: the winner is then tight on j1 and on its second
+// column (u_i = c_ij1 - v_j1, s2_i = 0), every dual stays feasible (v only decreases, so every
+// other row's reduced costs only grow), and a displaced owner becomes free with its old u_i, still
+// a lower bound of its reduced costs.  So after any number of rounds the state is what the searches
+// start from (duals feasible, every assigned edge tight, v = 0 on unassigned columns: a column
+// once taken stays taken), and the searches finish an optimum.  Round 1 takes the bids from the
+// row pre-pass (v = 0); later rounds rescan the free rows, one wave a row.  On the OCSORT-family
+// first rounds the rounds leave 2-10x fewer rows and row scans to the searches
+// (tools/sim_lap_parallel.py).  Rounds stop when a round frees no row (bids that only displace).
+constexpr int ARR_ROUNDS = 24;
+
+__device__ __forceinline__ unsigned long long arr_key(double d) {
+    return (unsigned long long)__double_as_longlong(d) + 1ull;   // d >= 0: bit order = order
+}
+__device__ __forceinline__ void top2_push(double c, int j, double &m1, int &k1, double &m2, int &k2) {
+    if (c < m1) { m2 = m1; k2 = k1; m1 = c; k1 = j; }
+    else if (c < m2) { m2 = c; k2 = j; }
+}
+// One wave: the smallest and second smallest reduced cost c_ij - v_j of row i and their columns
+// (lowest column on ties); wave-uniform results.
+__device__ __forceinline__ void rect_row_bid(const RectMat M, int i, const double *v, double &u1,
+                                             int &j1, double &u2, int &j2) {
+    const int lane = lane_id(), cols = M.cols;
+    constexpr int CH = 32;   // 64 loads of each lane in flight (c and v)
+    double m1 = INFINITY, m2 = INFINITY;
+    int k1 = INT_MAX, k2 = INT_MAX;
+    for (int j0 = 0; j0 < cols; j0 += CH * WAVE) {
+        double c[CH], vv[CH];
+#pragma unroll
+        for (int k = 0; k < CH; ++k) {
+            const int j = j0 + k * WAVE + lane;
+            c[k] = j < cols ? M.at(i, j) : INFINITY;
+            vv[k] = j < cols ? v[j] : 0.0;
+        }
+#pragma unroll
+        for (int k = 0; k < CH; ++k) top2_push(c[k] - vv[k], j0 + k * WAVE + lane, m1, k1, m2, k2);
+    }
+#pragma unroll
+    for (int s = 1; s < WAVE; s <<= 1) {
+        const double o1 = __shfl_xor(m1, s), o2 = __shfl_xor(m2, s);
+        const int q1 = __shfl_xor(k1, s), q2 = __shfl_xor(k2, s);
+        if (o1 < m1 || (o1 == m1 && q1 < k1)) {          // the other's first wins
+            if (m1 < o2 || (m1 == o2 && k1 < q2)) { m2 = m1; k2 = k1; }
+            else { m2 = o2; k2 = q2; }
+            m1 = o1; k1 = q1;
+        } else if (o1 < m2 || (o1 == m2 && q1 < k2)) {
+            m2 = o1; k2 = q1;
+        }
+    }
+    u1 = m1; j1 = k1; u2 = m2; j2 = k2;
+}
+
+// Block-wide; the rows' pre-pass in pu / px / ps2.  On return: w.x, w.u, w.s2, w.yw and w.av
+// describe a feasible partial assignment (w.path = INT_MAX on every column).
+__device__ __noinline__ void rect_arr(const RectMat M, const double *pu, const int *px,
+                                      const double *ps2, RectWs w, RectShared &sh) {
+    const int t = threadIdx.x, nt = blockDim.x, wid = t / WAVE, nw = nt / WAVE;
+    const int rows = M.rows, cols = M.cols;
+    for (int j = t; j < cols; j += nt) {
+        w.abid[j] = 0ull;
+        w.path[j] = INT_MAX;
+        w.yw[j] = -1;
+        w.av[j] = 0.0;
+    }
+    for (int i = t; i < rows; i += nt) {   // pu / px / ps2 may be w.u / w.x / w.s2: read first
+        const double d = ps2[i], ui = pu[i];
+        const int xi = px[i];
+        w.x[i] = -1;
+        w.u[i] = ui;
+        w.s2[i] = 0.0f;
+        w.atgt[i] = xi;
+        w.adel[i] = d < INFINITY ? d : 0.0;
+    }
+    block_sync();
+    int nbid = rows;
+    for (int round = 0; round < ARR_ROUNDS; ++round) {
+        YTA_COUNT(106);
+        if (round > 0) {   // the free rows bid under the current duals
+            for (int k = wid; k < nbid; k += nw) {
+                const int i = w.fl[k];
+                double u1, u2;
+                int j1, j2;
+                rect_row_bid(M, i, w.av, u1, j1, u2, j2);
+                double d = u2 - u1;
+                if (!(d < INFINITY) || j1 == INT_MAX) d = 0.0;
+                int tg = j1 == INT_MAX ? 0 : j1;
+                // a tie on an owned column: the other tight column when it is free
+                if (d == 0.0 && j2 != INT_MAX && w.yw[tg] >= 0 && w.yw[j2] < 0) tg = j2;
+                if (lane_id() == 0) {
+                    w.u[i] = u1;
+                    w.atgt[i] = tg;
+                    w.adel[i] = d;
+                }
+            }
+            block_sync();
+        }
+        for (int k = t; k < nbid; k += nt) {
+            const int i = round ? w.fl[k] : k;
+            atomicMax(&w.abid[w.atgt[i]], arr_key(w.adel[i]));
+        }
+        block_sync();
+        for (int k = t; k < nbid; k += nt) {
+            const int i = round ? w.fl[k] : k;
+            const int j = w.atgt[i];
+            if (w.abid[j] == arr_key(w.adel[i])) atomicMin(&w.path[j], i);
+        }
+        block_sync();
+        for (int k = t; k < nbid; k += nt) {   // one winner per column; bidders own nothing
+            const int i = round ? w.fl[k] : k;
+            const int j = w.atgt[i];
+            if (w.path[j] != i) continue;
+            const int old = w.yw[j];
+            if (old >= 0) w.x[old] = -1;
+            w.yw[j] = i;
+            w.x[i] = j;
+            const double vj = w.av[j] - w.adel[i];
+            w.av[j] = vj;
+            w.u[i] = M.at(i, j) - vj;
+            w.s2[i] = 0.0f;
+        }
+        block_sync();
+        for (int k = t; k < nbid; k += nt) {
+            const int j = w.atgt[round ? w.fl[k] : k];
+            w.abid[j] = 0ull;
+            w.path[j] = INT_MAX;
+        }
+        block_sync();
+        const int nf = block_compact(rows, sh.wsum, [&](int i) { return w.x[i] < 0; },
+                                     [&](int i, int pos) { w.fl[pos] = i; });
+        block_sync();
+        if (nf == 0 || (round > 0 && nf >= nbid)) break;
+        nbid = nf;
+    }
+}
+
 // Solve.  pre_u / pre_x / pre_s2: the row pre-pass (global, or nullptr: computed here).  Returns 0,
 // or -2 if a row cannot reach a free column (rows > cols, or NaN costs).  On return w.x[i] is the
 // column of row i.  All threads of the block must call it; blockDim.x * CPT >= M.cols.
@@ -152,21 +314,34 @@ __device__ __forceinline__ int lap_rect_body(const RectMat M, const double *pre_
     if (rows <= 0) return 0;
     if (rows > cols) return -2;
     // ---- 1. row pre-pass (when not supplied) and 2. claims
-    if (pre_u == nullptr) {
+    const bool own_pre = pre_u == nullptr;   // the bounds then already in w.s2 (as floats)
+    if (own_pre) {
         for (int i = wid; i < rows; i += nw) rect_row_pre(M, i, w.u, w.x, w.s2);
-        pre_u = w.u; pre_x = w.x; pre_s2 = w.s2;
+        pre_u = w.u; pre_x = w.x;
+        block_sync();
     }
-    for (int j = t; j < cols; j += nt) w.path[j] = INT_MAX;
-    block_sync();
-    for (int i = t; i < rows; i += nt) atomicMin(&w.path[pre_x[i]], i);
-    block_sync();
-    for (int i = t; i < rows; i += nt) {
-        const int xi = pre_x[i];
-        const double ui = pre_u[i], si = pre_s2[i];
-        const bool won = w.path[xi] == i;
-        w.u[i] = ui;
-        w.s2[i] = si;
-        w.x[i] = won ? xi : -1;
+    const bool arr = w.av != nullptr && !own_pre;
+    if (arr) {
+#ifdef YTA_STAMPS
+        const unsigned long long ta = wall_clock64();
+#endif
+        rect_arr(M, pre_u, pre_x, pre_s2, w, sh);
+#ifdef YTA_STAMPS
+        if (blockIdx.x == 0 && t == 0) g_stamps[107] += wall_clock64() - ta;
+#endif
+    } else {   // claims: every row its argmin column, the lowest row keeps it
+        for (int j = t; j < cols; j += nt) w.path[j] = INT_MAX;
+        block_sync();
+        for (int i = t; i < rows; i += nt) atomicMin(&w.path[pre_x[i]], i);
+        block_sync();
+        for (int i = t; i < rows; i += nt) {
+            const int xi = pre_x[i];
+            const double ui = pre_u[i];
+            const bool won = w.path[xi] == i;
+            w.u[i] = ui;
+            if (!own_pre) w.s2[i] = __double2float_rd(pre_s2[i]);
+            w.x[i] = won ? xi : -1;
+        }
     }
     block_sync();
     // s2c: the bound of each column's row, as a float rounded down (still a lower bound)
@@ -181,10 +356,15 @@ __device__ __forceinline__ int lap_rect_body(const RectMat M, const double *pre_
         y[q] = -1;
         s2c[q] = 0.0f;
         if (j < cols) {
-            const int r = w.path[j];
-            y[q] = r == INT_MAX ? -1 : r;
-            if (y[q] >= 0) s2c[q] = __double2float_rd(w.s2[y[q]]);
-            w.yw[j] = y[q];
+            if (arr) {
+                v[q] = w.av[j];
+                y[q] = w.yw[j];
+            } else {
+                const int r = w.path[j];
+                y[q] = r == INT_MAX ? -1 : r;
+                w.yw[j] = y[q];
+            }
+            if (y[q] >= 0) s2c[q] = w.s2[y[q]];
         }
     }
     YTA_STAMP_ABS(104);

@@ -712,7 +712,7 @@ int oc_alloc(yta_ocsort *e) {
     OCALLOC(a.upd, S * CAP);
     OCALLOC(a.out, S * CAP * 8);
     const long long n = std::max(CAP, MAXD);
-    a.lap_ws_stride = (n > OC_LDS_LAP_N ? ((dense_lap_ws_bytes(n) + 255) & ~255LL) : 256) + tight_ws_bytes();
+    a.lap_ws_stride = oc_lap_ws_stride(n);
     OCALLOC(a.lap_ws, S * a.lap_ws_stride);
     e->lds = (size_t)oc_lds_bytes(CAP, MAXD);
     OCALLOC(e->d_off, S + 1);
@@ -1280,7 +1280,8 @@ __global__ __launch_bounds__(LAP_T) void k_kat_fr(const double *m, int na, int n
     if (threadIdx.x == 0) *n_tight = -1;
     __syncthreads();
     first_round_lap(m, na, nb, rx, rx, false, u, x, s2, rx, lds, lds_bytes, gws, st, st + 1, &ls,
-                    gws + dense_lap_ws_bytes(na > nb ? na : nb), n_tight);
+                    gws + dense_lap_ws_bytes(na > nb ? na : nb) + arr_ws_region(na > nb ? na : nb),
+                    n_tight);
 }
 struct KatBuf {
     std::vector<void *> ptrs;
@@ -1317,7 +1318,7 @@ extern "C" int yta_lap_first_round(int device, int na, int nb, const double *cos
     YTA_HIP(m.get(&drx, na));
     YTA_HIP(m.get(&st, 2));
     YTA_HIP(m.get(&dg, 1));
-    YTA_HIP(m.get(&gws, (size_t)(dense_lap_ws_bytes(n) + tight_ws_bytes())));
+    YTA_HIP(m.get(&gws, (size_t)(dense_lap_ws_bytes(n) + arr_ws_region(n) + tight_ws_bytes())));
     YTA_HIP(hipMemcpy(dc, cost, sizeof(double) * na * nb, hipMemcpyHostToDevice));
     YTA_HIP(hipMemset(drx, 0, sizeof(int) * na));   // rcnt = 0: no fast path
     YTA_HIP(hipMemset(st, 0, sizeof(int) * 2));

@@ -87,10 +87,21 @@ __device__ __forceinline__ void padded_lap(const LapMat &M, int *rx, unsigned ch
 constexpr int LAP_T = YTA_LAP_T;                // threads of the first-round solve kernels
 constexpr long long LAP_LDS_MAX = 152 * 1024;   // their dynamic LDS cap (160 KiB - static)
 
+// Per-stream solver workspace (engines' lap_ws): the lapjv replay's arrays when they exceed LDS,
+// the bidding rounds' arrays (lap_rect.hpp rect_arr), the uniqueness certificate's edges (tws at
+// the end).  n = max(CAP, MAXD).
+#ifndef YTA_LAP_ARR
+#define YTA_LAP_ARR 1
+#endif
+__host__ __device__ inline long long arr_ws_region(long long n) {
+    return (arr_ws_bytes(n, n) + 255) & ~255LL;
+}
+
 // The first-round solve's work arrays, either orientation (first_round_lap transposes the
 // problem when detections outnumber trackers).
 __host__ __device__ inline long long lap_kernel_lds(long long CAP, long long MAXD) {
-    const long long b1 = rect_ws_bytes(MAXD, CAP), b2 = rect_ws_bytes(CAP, MAXD, true);
+    const long long b1 = rect_ws_bytes(MAXD, CAP) + 8 * CAP + 16,   // + the rounds' duals
+                    b2 = rect_ws_bytes(CAP, MAXD, true);
     const long long b = b1 > b2 ? b1 : b2;
     return b < LAP_LDS_MAX ? b : LAP_LDS_MAX;
 }
@@ -226,6 +237,10 @@ __device__ __forceinline__ void iou_lap(const LapMat &M, int *rx, unsigned char 
 constexpr double UNIQ_TOL = 1e-9;
 constexpr int TIGHT_CAP = 16384;
 __host__ __device__ inline long long tight_ws_bytes() { return 8LL * TIGHT_CAP; }
+__host__ __device__ inline long long oc_lap_ws_stride(long long n) {
+    return (n > OC_LDS_LAP_N ? ((dense_lap_ws_bytes(n) + 255) & ~255LL) : 256) + arr_ws_region(n) +
+           tight_ws_bytes();
+}
 __device__ __forceinline__ int unique_optimum_tr(const double *mat, int na, int nb, const RectWs &w,
                                                  int2 *tws, int *n_tight) {
     __shared__ int ne, bad, changed[2];
@@ -336,7 +351,16 @@ __device__ __forceinline__ void first_round_lap(const double *mat, int na, int n
         return;
     }
     unsigned char *base = rect_ws_bytes(rows, cols, tr) <= lds_bytes ? lds : gws;
-    const RectWs w = rect_ws(base, rows, cols, tr);
+    RectWs w = rect_ws(base, rows, cols, tr);
+    // the bidding rounds' arrays: the region just below tws (oc_lap_ws_stride).  Not for the
+    // transposed solve: a bid leaves its row tight on two columns, and a tight edge into an
+    // unmatched column fails the uniqueness certificate
+    if (YTA_LAP_ARR && !tr) {
+        rect_arr_ws(tws - arr_ws_region(rows > cols ? rows : cols), rows, cols, w);
+        // the column duals of the rounds (read by every bid scan) in LDS after the work arrays
+        const long long wo = (rect_ws_bytes(rows, cols) + 15) & ~15LL;
+        if (base == lds && wo + 8LL * cols <= lds_bytes) w.av = reinterpret_cast<double *>(lds + wo);
+    }
     const RectMat R = tr ? RectMat{mat, rows, cols, 1, nb, false} : RectMat{mat, rows, cols, nb, 1, false};
     const int rc = lap_rect<LAP_T>(R, pu, px, ps2, w, rsh);
     if (rc && t == 0) atomicOr(err, ERR_SOLVER);
