@@ -220,6 +220,10 @@ def main():
               f"{int(st[101])}, scan {int(st[102]) / 100:.0f} us, reduce {int(st[103]) / 100:.0f} us, "
               f"bidding rounds {int(st[106])} ({int(st[107]) / 100:.0f} us)",
               file=sys.stderr)
+        names = ["first round", "lists", "updates", "OCR round", "misses", "births", "outputs"]
+        ph = [f"{nm} {(int(st[41 + k]) - int(st[40 + k])) / 100:.1f}" for k, nm in enumerate(names)
+              if st[41 + k] and st[40 + k] and st[41 + k] >= st[40 + k]]
+        print("k_hs_assoc (block 0, last frame, us): " + ", ".join(ph), file=sys.stderr)
     stats = eng.stats()
     if fam and len(engines) > 1:   # summed over the engines: the same totals as one engine of S
         for e_ in engines[1:]:

@@ -2,10 +2,12 @@
 //
 // Follows boxmot/trackers/deepocsort/deep_ocsort.py:357-520 (new-KF branch, the only live one)
 // with the embedding-aware association of boxmot/utils/association.py:79-201.  One frame =
-//   k_doc_pre    [block/stream]  CMC correction of every tracker (:250-267, last observation,
+//   k_doc_predict [grid]         CMC correction of every tracker (:250-267, last observation,
 //                                observations within delta_t ages, Kalman state and its frozen
-//                                copy), predict (:269-293), NaN cull, column inputs, confidence
-//                                split, embedding weights alpha = af + (1 - af)(1 - trust) (:395-398)
+//                                copy), predict (:269-293), column inputs; one thread per tracker
+//   k_doc_pre    [block/stream]  NaN cull (compacts the column inputs when a tracker goes),
+//                                confidence split, embedding weights
+//                                alpha = af + (1 - af)(1 - trust) (:395-398)
 //   k_doc_cost   [grid]          dense asso (dets x trackers) and iou + angle (association.py:
 //                                111-170), per-row / per-column counts for the fast path
 //   k_doc_emb    [grid]          stage-1 embedding cost dets_embs @ trk_embs^T (float64 MFMA tiles)
@@ -289,6 +291,20 @@ __global__ __launch_bounds__(DOC_TRK_T) void k_doc_predict(DocArgs a) {
     doc_x_to_bbox(r.kf.x, b);
     a.nan_flag[tb + i] = (b[0] != b[0]) || (b[1] != b[1]) || (b[2] != b[2]) || (b[3] != b[3]);
     a.cbox[tb + i] = Box{b[0], b[1], b[2], b[3]};
+    // the rest of the column inputs at the tracker's list position (k_doc_pre keeps them in place
+    // when no tracker is culled, the steady state, and recomputes the survivors' otherwise)
+    double ko[5];
+    doc_prev_obs(r, a.delta_t, ko);
+    for (int k = 0; k < 5; ++k) {
+        a.ckobs[(tb + i) * 5 + k] = ko[k];
+        a.clast[(tb + i) * 5 + k] = r.last_obs[k];
+    }
+    const bool hv = (r.flags & OF_VELOCITY) != 0;
+    a.cvel[(tb + i) * 2] = hv ? r.vel[0] : 0.0;
+    a.cvel[(tb + i) * 2 + 1] = hv ? r.vel[1] : 0.0;
+    a.cslot[tb + i] = a.list[tb + i];
+    a.cmatched[tb + i] = 0;
+    a.upd[tb + i] = -1;
 }
 
 __global__ __launch_bounds__(OC_T) void k_doc_pre(DocArgs a) {
@@ -307,11 +323,11 @@ __global__ __launch_bounds__(OC_T) void k_doc_pre(DocArgs a) {
     int n_trk = c->n_trk;
     const int dt = a.delta_t;
     int *list = a.list + tb;
-    // CMC + predict ran chip-wide in k_doc_predict
-    {
-        int n_free = c->n_free;
-        const int n_nan = block_compact(n_trk, sh.wsum, [&](int i) { return a.nan_flag[tb + i] != 0; },
-                                        [&](int i, int pos) { a.tmp[ub + pos] = list[i]; });
+    // CMC + predict and the column inputs ran chip-wide in k_doc_predict (by list position)
+    int n_free = c->n_free;
+    const int n_nan = block_compact(n_trk, sh.wsum, [&](int i) { return a.nan_flag[tb + i] != 0; },
+                                    [&](int i, int pos) { a.tmp[ub + pos] = list[i]; });
+    if (n_nan > 0) {   // cull: the survivors' inputs compacted
         block_sync();   // the compaction's tmp stores (other threads' runs) before their reads
         for (int k = t; k < n_nan; k += nt) a.free_list[tb + n_free + k] = a.tmp[ub + k];
         n_free += n_nan;
@@ -808,40 +824,62 @@ __global__ __launch_bounds__(OC_T) void k_doc_finish(DocArgs a) {
     n_trk += n_b;
     block_sync();
     YTA_STAMP(5);
-    // ---- outputs in reversed tracker order, then removal (:505-520); ids as stored (:513)
+    // ---- outputs in reversed tracker order, then removal (:505-520); ids as stored (:513).
+    // Every record read is batched (block_compact_ld / batched_for2): a per-item chain of list ->
+    // record loads would cost a round trip per tracker.  The pass leaves the removal flags in
+    // nan_flag for the two removal compactions.
     double *out = a.out + tb * 8;
-    const int n_out = block_compact(
-        n_trk, sh.wsum,
-        [&](int q) {
-            const DocTrack &r = a.rec[tb + list[n_trk - 1 - q]];
-            return r.tsu < 1 && (r.hit_streak >= a.min_hits || frame <= a.min_hits);
+    struct TrkState {
+        int slot, tsu, hit_streak;
+    };
+    int *oslot = a.tmp + ub;   // the output trackers' slots, in output order
+    const int n_out = block_compact_ld<8>(
+        n_trk, sh.wsum, [&](int q) { return list[n_trk - 1 - q]; },
+        [&](int, int slot) {
+            const DocTrack &r = a.rec[tb + slot];
+            return TrkState{slot, r.tsu, r.hit_streak};
         },
-        [&](int q, int pos) {
-            const DocTrack &r = a.rec[tb + list[n_trk - 1 - q]];
-            double b[4];
-            if (np_sum5(r.last_obs) < 0) doc_x_to_bbox(r.kf.x, b);
-            else for (int k = 0; k < 4; ++k) b[k] = r.last_obs[k];
-            double *o = out + (long long)pos * 8;
-            o[0] = b[0];
-            o[1] = b[1];
-            o[2] = b[2];
-            o[3] = b[3];
-            o[4] = (double)r.id;
-            o[5] = r.conf;
-            o[6] = r.cls;
-            o[7] = (double)r.det_ind;
+        [&](int q, const TrkState &v) {
+            a.nan_flag[tb + n_trk - 1 - q] = v.tsu > a.max_age;
+            return v.tsu < 1 && (v.hit_streak >= a.min_hits || frame <= a.min_hits);
+        },
+        [&](int, const TrkState &v, int pos) { oslot[pos] = v.slot; });
+    block_sync();   // the slots (other threads' runs) before their reads
+    struct OutRow {
+        double b[4], id, conf, cls, det_ind;
+    };
+    batched_for2<4>(
+        n_out, [&](int pos) { return oslot[pos]; },
+        [&](int, int slot) {
+            const DocTrack &r = a.rec[tb + slot];
+            OutRow o;
+            if (np_sum5(r.last_obs) < 0) doc_x_to_bbox(r.kf.x, o.b);
+            else for (int k = 0; k < 4; ++k) o.b[k] = r.last_obs[k];
+            o.id = (double)r.id;
+            o.conf = r.conf;
+            o.cls = r.cls;
+            o.det_ind = (double)r.det_ind;
+            return o;
+        },
+        [&](int pos, const OutRow &o) {
+            double *d = out + (long long)pos * 8;
+            for (int k = 0; k < 4; ++k) d[k] = o.b[k];
+            d[4] = o.id;
+            d[5] = o.conf;
+            d[6] = o.cls;
+            d[7] = o.det_ind;
         });
-    const int n_dead = block_compact(n_trk, sh.wsum,
-                                     [&](int j) { return a.rec[tb + list[j]].tsu > a.max_age; },
+    block_sync();   // oslot (tmp) is reused below
+    const int n_dead = block_compact(n_trk, sh.wsum, [&](int j) { return a.nan_flag[tb + j] != 0; },
                                      [&](int j, int pos) { a.tmp[ub + pos] = list[j]; });
     block_sync();   // the compaction's tmp stores (other threads' runs) before their reads
     for (int k = t; k < n_dead; k += nt) a.free_list[tb + n_free + k] = a.tmp[ub + k];
     block_sync();
-    const int n_live = block_compact(n_trk, sh.wsum,
-                                     [&](int j) { return a.rec[tb + list[j]].tsu <= a.max_age; },
+    const int n_live = block_compact(n_trk, sh.wsum, [&](int j) { return a.nan_flag[tb + j] == 0; },
                                      [&](int j, int pos) { a.tmp[ub + pos] = list[j]; });
     block_sync();
     for (int j = t; j < n_live; j += nt) list[j] = a.tmp[ub + j];
+    for (int j = t; j < n_trk; j += nt) a.nan_flag[tb + j] = 0;
     if (t == 0) {
         c->frame = frame;
         c->n_trk = n_live;

@@ -6,10 +6,12 @@
 // hybridsort.py:346-360): TCM weight 0, ReID weight 1.3 on the short-term embedding cost,
 // long-term ReID weight 0, long-term correction at 0.4, no BYTE round (hybridsort.yaml).  One
 // frame (one undecorated update call) =
-//   k_hs_pre     [block/stream]  predict every tracker (:296-320: velocity clamp, 9-d Kalman
-//                                predict, kalman / simple scores), NaN cull (:406-416), column
-//                                inputs (box, kalman score, 4 corner velocities, k-previous and
-//                                last observations), confidence split (:391-404)
+//   k_hs_predict [grid]          predict every tracker (:296-320: velocity clamp, 9-d Kalman
+//                                predict, kalman / simple scores) and its column inputs (box,
+//                                kalman score, 4 corner velocities, k-previous and last
+//                                observations), one thread per tracker
+//   k_hs_pre     [block/stream]  NaN cull (:406-416: compacts the column inputs when a tracker
+//                                goes), confidence split (:391-404)
 //   k_hs_emb     [grid]          stage-1 cost tiles: dets_feats x smooth_feats on f64 MFMA
 //                                (v_mfma_f64_16x16x4_f64) with the row norms, cosine distance
 //                                max(0, 1 - uv / sqrt(uu vv)) (association.py:667-684), and in the
@@ -96,6 +98,7 @@ struct HsArgs {
     HsCounters *cnt;
     // per frame
     int *hi_row;                    // [S*MAXD]
+    int *corr;                      // [S*MAXD] first-round pair undone by the long-term correction
     HsCol *col;                     // [S*CAP]
     double *clast;                  // [S*CAP][5] last observations
     int *nan_flag, *cslot;          // [S*CAP]
@@ -281,10 +284,24 @@ __global__ __launch_bounds__(64) void k_hs_predict(HsArgs a) {
                   fabs(b[3]) < INFINITY && fabs(sc) < INFINITY))
         atomicOr(&c->err, ERR_INF_ROW);
     a.nan_flag[tb + i] = nan;
-    HsCol &q = a.col[tb + i];
+    // the column record at the tracker's list position, complete (k_hs_pre keeps it in place
+    // when no tracker is culled, the steady state; otherwise it compacts the survivors' records)
+    HsCol q;
     for (int k = 0; k < 4; ++k) q.box[k] = b[k];
     q.kscore = ks;
     (void)ss;   // simple score: trks[:, 5], read only by the BYTE round (use_byte = False)
+    double ko[5];
+    hs_prev_obs(r, a.delta_t, ko);
+    for (int k = 0; k < 5; ++k) q.kobs[k] = ko[k];
+    const bool hv = (r.flags & OF_VELOCITY) != 0;
+    for (int k = 0; k < 8; ++k) q.vel[k] = hv ? r.vel[k] : 0.0;
+    q.valid = ko[4] < 0 ? 0.0 : 1.0;
+    q.pad = 0.0;
+    a.col[tb + i] = q;
+    for (int k = 0; k < 5; ++k) a.clast[(tb + i) * 5 + k] = r.last_obs[k];
+    a.cslot[tb + i] = a.list[tb + i];
+    a.cmatched[tb + i] = 0;
+    a.upd[tb + i] = -1;
 }
 
 __global__ __launch_bounds__(OC_T) void k_hs_pre(HsArgs a) {
@@ -301,14 +318,13 @@ __global__ __launch_bounds__(OC_T) void k_hs_pre(HsArgs a) {
     }
     const double *din = a.det_in + (long long)a.det_off[s] * 6;
     int n_trk = c->n_trk;
-    const int dt = a.delta_t;
     int *list = a.list + tb;
     HsCol *col = a.col + tb;
-    // predict ran chip-wide in k_hs_predict
-    {
-        int n_free = c->n_free;
-        const int n_nan = block_compact(n_trk, sh.wsum, [&](int i) { return a.nan_flag[tb + i] != 0; },
-                                        [&](int i, int pos) { a.tmp[ub + pos] = list[i]; });
+    // predict and the column records ran chip-wide in k_hs_predict (by list position)
+    int n_free = c->n_free;
+    const int n_nan = block_compact(n_trk, sh.wsum, [&](int i) { return a.nan_flag[tb + i] != 0; },
+                                    [&](int i, int pos) { a.tmp[ub + pos] = list[i]; });
+    if (n_nan > 0) {   // cull: the survivors' records compacted
         block_sync();   // the compaction's tmp stores (other threads' runs) before their reads
         for (int k = t; k < n_nan; k += nt) a.free_list[tb + n_free + k] = a.tmp[ub + k];
         n_free += n_nan;
@@ -323,15 +339,7 @@ __global__ __launch_bounds__(OC_T) void k_hs_pre(HsArgs a) {
         HsCol *scratch = reinterpret_cast<HsCol *>(a.cost + hs_mb(a, s));
         for (int j = t; j < n_keep; j += nt) {
             const HsTrack &r = a.rec[tb + a.tmp[ub + j]];
-            HsCol q = col[a.upd[tb + j]];
-            double ko[5];
-            hs_prev_obs(r, dt, ko);
-            for (int k = 0; k < 5; ++k) q.kobs[k] = ko[k];
-            const bool hv = (r.flags & OF_VELOCITY) != 0;
-            for (int k = 0; k < 8; ++k) q.vel[k] = hv ? r.vel[k] : 0.0;
-            q.valid = ko[4] < 0 ? 0.0 : 1.0;
-            q.pad = 0.0;
-            scratch[j] = q;
+            scratch[j] = col[a.upd[tb + j]];
             for (int k = 0; k < 5; ++k) a.clast[(tb + j) * 5 + k] = r.last_obs[k];
         }
         block_sync();
@@ -609,7 +617,9 @@ __global__ __launch_bounds__(HS_UPD_T) void k_hs_upd(HsArgs a) {
     if (!c->lap_done || i >= n_hi || n_trk == 0) return;
     const long long tb = (long long)s * a.CAP, db = (long long)s * a.MAXD;
     const int k = a.rmatch[db + i];
-    if (k < 0 || hs_corrected(a, s, i, k, n_trk)) return;
+    const bool corr = k >= 0 && hs_corrected(a, s, i, k, n_trk);
+    a.corr[db + i] = corr;   // for k_hs_assoc's lists
+    if (k < 0 || corr) return;
     const double *din = a.det_in + (long long)a.det_off[s] * 6;
     // cls / det_ind from dets0 row i of the input (filtered position, :464)
     hs_update(a.rec[tb + a.list[tb + k]], din + (long long)a.hi_row[db + i] * 6,
@@ -673,10 +683,15 @@ __global__ __launch_bounds__(OC_T) void k_hs_assoc(HsArgs a) {
         n_ut = block_compact(n_trk, sh.wsum, [&](int j) { return a.cmatched[tb + j] == 0; },
                              [&](int j, int pos) { utrk[pos] = j; });
         // long-term correction (:557-567): emb > 0.4 and iou - |kalman score - score| < thr
-        auto corrected = [&](int i) {
-            const int k = a.rmatch[db + i];
-            return k >= 0 && hs_corrected(a, s, i, k, n_trk);
-        };
+        // (decided by k_hs_upd when k_hs_lap solved the round)
+        if (!c->lap_done) {
+            for (int i = t; i < n_hi; i += nt) {
+                const int k = a.rmatch[db + i];
+                a.corr[db + i] = k >= 0 && hs_corrected(a, s, i, k, n_trk);
+            }
+            block_sync();
+        }
+        auto corrected = [&](int i) { return a.corr[db + i] != 0; };
         n_corr = block_compact(n_hi, sh.wsum, corrected, [&](int i, int pos) {
             udet[n_ud + pos] = i;
             utrk[n_ut + pos] = a.rmatch[db + i];
@@ -778,40 +793,62 @@ __global__ __launch_bounds__(OC_T) void k_hs_assoc(HsArgs a) {
     n_trk += n_b;
     block_sync();
     YTA_STAMP(6);
-    // ---- outputs in reversed tracker order, then removal (:551-570); ids + 1 (:563)
+    // ---- outputs in reversed tracker order, then removal (:551-570); ids + 1 (:563).  Every
+    // record read is batched (block_compact_ld / batched_for2): a per-item chain of list ->
+    // record loads would cost a round trip per tracker.  The removal flags of the pass
+    // (nan_flag: 0 on entry) feed the two removal compactions.
     double *out = a.out + tb * 8;
-    const int n_out = block_compact(
-        n_trk, sh.wsum,
-        [&](int q) {
-            const HsTrack &r = a.rec[tb + list[n_trk - 1 - q]];
-            return r.tsu < 1 && (r.hit_streak >= a.min_hits || frame <= a.min_hits);
+    struct TrkState {
+        int slot, tsu, hit_streak;
+    };
+    int *oslot = a.tmp + ub;   // the output trackers' slots, in output order
+    const int n_out = block_compact_ld<8>(
+        n_trk, sh.wsum, [&](int q) { return list[n_trk - 1 - q]; },
+        [&](int, int slot) {
+            const HsTrack &r = a.rec[tb + slot];
+            return TrkState{slot, r.tsu, r.hit_streak};
         },
-        [&](int q, int pos) {
-            const HsTrack &r = a.rec[tb + list[n_trk - 1 - q]];
-            double b[4];
-            if (np_sum5(r.last_obs) < 0) hs_x_to_bbox(r.kf.x, b);
-            else for (int k = 0; k < 4; ++k) b[k] = r.last_obs[k];
-            double *o = out + (long long)pos * 8;
-            o[0] = b[0];
-            o[1] = b[1];
-            o[2] = b[2];
-            o[3] = b[3];
-            o[4] = (double)(r.id + 1);
-            o[5] = r.conf;
-            o[6] = r.cls;
-            o[7] = r.det_ind;
+        [&](int q, const TrkState &v) {
+            a.nan_flag[tb + n_trk - 1 - q] = v.tsu > a.max_age;
+            return v.tsu < 1 && (v.hit_streak >= a.min_hits || frame <= a.min_hits);
+        },
+        [&](int, const TrkState &v, int pos) { oslot[pos] = v.slot; });
+    block_sync();   // the slots (other threads' runs) before their reads
+    struct OutRow {
+        double b[4], id, conf, cls, det_ind;
+    };
+    batched_for2<4>(
+        n_out, [&](int pos) { return oslot[pos]; },
+        [&](int, int slot) {
+            const HsTrack &r = a.rec[tb + slot];
+            OutRow o;
+            if (np_sum5(r.last_obs) < 0) hs_x_to_bbox(r.kf.x, o.b);
+            else for (int k = 0; k < 4; ++k) o.b[k] = r.last_obs[k];
+            o.id = (double)(r.id + 1);
+            o.conf = r.conf;
+            o.cls = r.cls;
+            o.det_ind = r.det_ind;
+            return o;
+        },
+        [&](int pos, const OutRow &o) {
+            double *d = out + (long long)pos * 8;
+            for (int k = 0; k < 4; ++k) d[k] = o.b[k];
+            d[4] = o.id;
+            d[5] = o.conf;
+            d[6] = o.cls;
+            d[7] = o.det_ind;
         });
-    const int n_dead = block_compact(n_trk, sh.wsum,
-                                     [&](int j) { return a.rec[tb + list[j]].tsu > a.max_age; },
+    block_sync();   // oslot (tmp) is reused below
+    const int n_dead = block_compact(n_trk, sh.wsum, [&](int j) { return a.nan_flag[tb + j] != 0; },
                                      [&](int j, int pos) { a.tmp[ub + pos] = list[j]; });
     block_sync();   // the compaction's tmp stores (other threads' runs) before their reads
     for (int k = t; k < n_dead; k += nt) a.free_list[tb + n_free + k] = a.tmp[ub + k];
     block_sync();
-    const int n_live = block_compact(n_trk, sh.wsum,
-                                     [&](int j) { return a.rec[tb + list[j]].tsu <= a.max_age; },
+    const int n_live = block_compact(n_trk, sh.wsum, [&](int j) { return a.nan_flag[tb + j] == 0; },
                                      [&](int j, int pos) { a.tmp[ub + pos] = list[j]; });
     block_sync();
     for (int j = t; j < n_live; j += nt) list[j] = a.tmp[ub + j];
+    for (int j = t; j < n_trk; j += nt) a.nan_flag[tb + j] = 0;
     if (t == 0) {
         c->frame = frame;
         c->n_trk = n_live;
@@ -974,6 +1011,7 @@ int hs_alloc(yta_hybridsort *e) {
     HSALLOC(a.free_list, S * CAP);
     HSALLOC(a.cnt, S);
     HSALLOC(a.hi_row, S * MAXD);
+    HSALLOC(a.corr, S * MAXD);
     HSALLOC(a.col, S * CAP);
     HSALLOC(a.clast, S * CAP * 5);
     HSALLOC(a.nan_flag, S * CAP);

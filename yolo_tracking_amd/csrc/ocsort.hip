@@ -568,39 +568,60 @@ __global__ __launch_bounds__(OC_T) void k_oc_assoc(OcArgs a) {
     block_sync();
     // ---- J: outputs in reversed tracker order, then drop trackers unseen > max_age (:350-379)
     YTA_STAMP(9);
+    // every record read batched (block_compact_ld / batched_for2); the removal flags of the
+    // pass go to nan_flag for the two removal compactions
     double *out = a.out + tb * 8;
-    const int n_out = block_compact(
-        n_trk, sh.wsum,
-        [&](int q) {
-            const OcTrack &r = a.rec[tb + list[n_trk - 1 - q]];
-            return r.tsu < 1 && (r.hit_streak >= a.min_hits || frame <= a.min_hits);
+    struct TrkState {
+        int slot, tsu, hit_streak;
+    };
+    int *oslot = a.tmp + ub;   // the output trackers' slots, in output order
+    const int n_out = block_compact_ld<8>(
+        n_trk, sh.wsum, [&](int q) { return list[n_trk - 1 - q]; },
+        [&](int, int slot) {
+            const OcTrack &r = a.rec[tb + slot];
+            return TrkState{slot, r.tsu, r.hit_streak};
         },
-        [&](int q, int pos) {
-            const OcTrack &r = a.rec[tb + list[n_trk - 1 - q]];
-            double b[4];
-            if (np_sum5(r.last_obs) < 0) oc_x_to_bbox(r.kf.x, b);
-            else for (int k = 0; k < 4; ++k) b[k] = r.last_obs[k];
-            double *o = out + (long long)pos * 8;
-            o[0] = b[0];
-            o[1] = b[1];
-            o[2] = b[2];
-            o[3] = b[3];
-            o[4] = (double)(r.id + 1);
-            o[5] = r.conf;
-            o[6] = r.cls;
-            o[7] = (double)r.det_ind;
+        [&](int q, const TrkState &v) {
+            a.nan_flag[tb + n_trk - 1 - q] = v.tsu > a.max_age;
+            return v.tsu < 1 && (v.hit_streak >= a.min_hits || frame <= a.min_hits);
+        },
+        [&](int, const TrkState &v, int pos) { oslot[pos] = v.slot; });
+    block_sync();   // the slots (other threads' runs) before their reads
+    struct OutRow {
+        double b[4], id, conf, cls, det_ind;
+    };
+    batched_for2<4>(
+        n_out, [&](int pos) { return oslot[pos]; },
+        [&](int, int slot) {
+            const OcTrack &r = a.rec[tb + slot];
+            OutRow o;
+            if (np_sum5(r.last_obs) < 0) oc_x_to_bbox(r.kf.x, o.b);
+            else for (int k = 0; k < 4; ++k) o.b[k] = r.last_obs[k];
+            o.id = (double)(r.id + 1);
+            o.conf = r.conf;
+            o.cls = r.cls;
+            o.det_ind = (double)r.det_ind;
+            return o;
+        },
+        [&](int pos, const OutRow &o) {
+            double *d = out + (long long)pos * 8;
+            for (int k = 0; k < 4; ++k) d[k] = o.b[k];
+            d[4] = o.id;
+            d[5] = o.conf;
+            d[6] = o.cls;
+            d[7] = o.det_ind;
         });
-    const int n_dead = block_compact(n_trk, sh.wsum,
-                                     [&](int j) { return a.rec[tb + list[j]].tsu > a.max_age; },
+    block_sync();   // oslot (tmp) is reused below
+    const int n_dead = block_compact(n_trk, sh.wsum, [&](int j) { return a.nan_flag[tb + j] != 0; },
                                      [&](int j, int pos) { a.tmp[ub + pos] = list[j]; });
     block_sync();   // the compaction's tmp stores (other threads' runs) before their reads
     for (int k = t; k < n_dead; k += nt) a.free_list[tb + n_free + k] = a.tmp[ub + k];
     block_sync();
-    const int n_live = block_compact(n_trk, sh.wsum,
-                                     [&](int j) { return a.rec[tb + list[j]].tsu <= a.max_age; },
+    const int n_live = block_compact(n_trk, sh.wsum, [&](int j) { return a.nan_flag[tb + j] == 0; },
                                      [&](int j, int pos) { a.tmp[ub + pos] = list[j]; });
     block_sync();
     for (int j = t; j < n_live; j += nt) list[j] = a.tmp[ub + j];
+    for (int j = t; j < n_trk; j += nt) a.nan_flag[tb + j] = 0;
     YTA_STAMP(10);
     if (t == 0) {
         c->frame = frame;
