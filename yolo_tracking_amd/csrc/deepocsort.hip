@@ -725,7 +725,8 @@ __global__ __launch_bounds__(OC_T) void k_doc_assoc(DocArgs a) {
         block_sync();
         mx = block_max(mx, sh);
         if (mx > a.thr) {
-            iou_lap(LapMat{mat, n_ud, n_ut, true}, a.rmatch + db, lds, lds_bytes, gws, &c->err, &c->ls);
+            iou_lap(LapMat{mat, n_ud, n_ut, true}, a.rmatch + db, lds, lds_bytes, gws, &c->err, &c->ls,
+                    a.lap_ws + (s + 1) * a.lap_ws_stride - tight_ws_bytes());
             for (int i = t; i < n_hi; i += nt) a.tmp[ub + i] = 0;
             for (int j = t; j < n_trk; j += nt) a.nan_flag[tb + j] = 0;
             block_sync();

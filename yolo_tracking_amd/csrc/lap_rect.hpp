@@ -59,6 +59,7 @@ struct RectWs {
     unsigned long long *abid = nullptr; // cols: the largest bid of the round
     int *atgt = nullptr;                // rows: the column a free row bids for
     double *adel = nullptr;             // rows: its bid (second minimum - minimum)
+    int av_lds = 0;                     // av is in LDS
 };
 // The bidding rounds' arrays (rect_arr_ws), 16-B aligned pieces.
 __host__ __device__ inline long long arr_ws_bytes(long long rows, long long cols) {
@@ -187,22 +188,30 @@ __device__ __forceinline__ void top2_push(double c, int j, double &m1, int &k1, 
 }
 // One wave: the smallest and second smallest reduced cost c_ij - v_j of row i and their columns
 // (lowest column on ties); wave-uniform results.
+// Loads are unconditional (index clamped, value masked): a load under `j < cols` becomes a branch
+// per element with its own wait, one round trip per element.  AS: address space of v (3 = LDS).
+template <int AS>
 __device__ __forceinline__ void rect_row_bid(const RectMat M, int i, const double *v, double &u1,
                                              int &j1, double &u2, int &j2) {
+    typedef const __attribute__((address_space(AS))) double *VP;
+    const VP vp = (VP)v;
     const int lane = lane_id(), cols = M.cols;
-    constexpr int CH = 32;   // 64 loads of each lane in flight (c and v)
+    constexpr int CH = 16;
     double m1 = INFINITY, m2 = INFINITY;
     int k1 = INT_MAX, k2 = INT_MAX;
     for (int j0 = 0; j0 < cols; j0 += CH * WAVE) {
         double c[CH], vv[CH];
 #pragma unroll
         for (int k = 0; k < CH; ++k) {
-            const int j = j0 + k * WAVE + lane;
-            c[k] = j < cols ? M.at(i, j) : INFINITY;
-            vv[k] = j < cols ? v[j] : 0.0;
+            const int j = j0 + k * WAVE + lane, jc = j < cols ? j : cols - 1;
+            c[k] = M.at(i, jc);
+            vv[k] = vp[jc];
         }
 #pragma unroll
-        for (int k = 0; k < CH; ++k) top2_push(c[k] - vv[k], j0 + k * WAVE + lane, m1, k1, m2, k2);
+        for (int k = 0; k < CH; ++k) {
+            const int j = j0 + k * WAVE + lane;
+            top2_push(j < cols ? c[k] - vv[k] : INFINITY, j, m1, k1, m2, k2);
+        }
     }
 #pragma unroll
     for (int s = 1; s < WAVE; s <<= 1) {
@@ -221,8 +230,9 @@ __device__ __forceinline__ void rect_row_bid(const RectMat M, int i, const doubl
 
 // Block-wide; the rows' pre-pass in pu / px / ps2.  On return: w.x, w.u, w.s2, w.yw and w.av
 // describe a feasible partial assignment (w.path = INT_MAX on every column).
+template <typename S2T>
 __device__ __noinline__ void rect_arr(const RectMat M, const double *pu, const int *px,
-                                      const double *ps2, RectWs w, RectShared &sh) {
+                                      const S2T *ps2, RectWs w, RectShared &sh) {
     const int t = threadIdx.x, nt = blockDim.x, wid = t / WAVE, nw = nt / WAVE;
     const int rows = M.rows, cols = M.cols;
     for (int j = t; j < cols; j += nt) {
@@ -232,7 +242,7 @@ __device__ __noinline__ void rect_arr(const RectMat M, const double *pu, const i
         w.av[j] = 0.0;
     }
     for (int i = t; i < rows; i += nt) {   // pu / px / ps2 may be w.u / w.x / w.s2: read first
-        const double d = ps2[i], ui = pu[i];
+        const double d = (double)ps2[i], ui = pu[i];
         const int xi = px[i];
         w.x[i] = -1;
         w.u[i] = ui;
@@ -249,7 +259,8 @@ __device__ __noinline__ void rect_arr(const RectMat M, const double *pu, const i
                 const int i = w.fl[k];
                 double u1, u2;
                 int j1, j2;
-                rect_row_bid(M, i, w.av, u1, j1, u2, j2);
+                if (w.av_lds) rect_row_bid<3>(M, i, w.av, u1, j1, u2, j2);
+                else rect_row_bid<1>(M, i, w.av, u1, j1, u2, j2);
                 double d = u2 - u1;
                 if (!(d < INFINITY) || j1 == INT_MAX) d = 0.0;
                 int tg = j1 == INT_MAX ? 0 : j1;
@@ -320,12 +331,13 @@ __device__ __forceinline__ int lap_rect_body(const RectMat M, const double *pre_
         pre_u = w.u; pre_x = w.x;
         block_sync();
     }
-    const bool arr = w.av != nullptr && !own_pre;
+    const bool arr = w.av != nullptr;
     if (arr) {
 #ifdef YTA_STAMPS
         const unsigned long long ta = wall_clock64();
 #endif
-        rect_arr(M, pre_u, pre_x, pre_s2, w, sh);
+        if (own_pre) rect_arr(M, pre_u, pre_x, (const float *)w.s2, w, sh);
+        else rect_arr(M, pre_u, pre_x, pre_s2, w, sh);
 #ifdef YTA_STAMPS
         if (blockIdx.x == 0 && t == 0) g_stamps[107] += wall_clock64() - ta;
 #endif
@@ -395,9 +407,9 @@ __device__ __forceinline__ int lap_rect_body(const RectMat M, const double *pre_
             for (int q0 = 0; q0 < CPT; q0 += CH) {
                 double c[CH];
 #pragma unroll
-                for (int k = 0; k < CH; ++k) {
+                for (int k = 0; k < CH; ++k) {   // unconditional loads (see rect_row_bid)
                     const int j = t + (q0 + k) * nt;
-                    c[k] = j < cols ? M.at(i, j) : 0.0;
+                    c[k] = M.at(i, j < cols ? j : cols - 1);
                 }
 #pragma unroll
                 for (int k = 0; k < CH; ++k) {

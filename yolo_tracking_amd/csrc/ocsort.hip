@@ -460,7 +460,8 @@ __global__ __launch_bounds__(OC_T) void k_oc_assoc(OcArgs a) {
         block_sync();
         mx = block_max(mx, sh);
         if (mx > a.thr) {
-            iou_lap(LapMat{mat, n_lo, n_ut, true}, a.rmatch + db, lds, lds_bytes, gws, &c->err, &c->ls);
+            iou_lap(LapMat{mat, n_lo, n_ut, true}, a.rmatch + db, lds, lds_bytes, gws, &c->err, &c->ls,
+                    a.lap_ws + (s + 1) * a.lap_ws_stride - tight_ws_bytes());
             for (int k = t; k < n_ut; k += nt) a.tmp[ub + k] = 0;   // taken flags
             block_sync();
             for (int p = t; p < n_lo; p += nt) {
@@ -497,7 +498,8 @@ __global__ __launch_bounds__(OC_T) void k_oc_assoc(OcArgs a) {
         block_sync();
         mx = block_max(mx, sh);
         if (mx > a.thr) {
-            iou_lap(LapMat{mat, n_ud, n_ut, true}, a.rmatch + db, lds, lds_bytes, gws, &c->err, &c->ls);
+            iou_lap(LapMat{mat, n_ud, n_ut, true}, a.rmatch + db, lds, lds_bytes, gws, &c->err, &c->ls,
+                    a.lap_ws + (s + 1) * a.lap_ws_stride - tight_ws_bytes());
             // removed dets / trackers -> flags, then sorted set differences
             for (int i = t; i < n_hi; i += nt) a.tmp[ub + i] = 0;
             for (int j = t; j < n_trk; j += nt) a.nan_flag[tb + j] = 0;

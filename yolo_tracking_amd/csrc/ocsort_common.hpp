@@ -117,11 +117,20 @@ __host__ __device__ inline long long oc_lds_bytes(long long CAP, long long MAXD)
 __device__ __forceinline__ void rect_solve(const RectMat &R, const double *pu, const int *px,
                                            const double *ps2, bool tr, int na, int *rx,
                                            unsigned char *lds, long long lds_bytes,
-                                           unsigned char *gws, int *err) {
+                                           unsigned char *gws, int *err,
+                                           unsigned char *tws = nullptr) {
     __shared__ RectShared rsh;
     const int t = threadIdx.x, nt = blockDim.x;
     unsigned char *base = rect_ws_bytes(R.rows, R.cols) <= lds_bytes ? lds : gws;
-    const RectWs w = rect_ws(base, R.rows, R.cols);
+    RectWs w = rect_ws(base, R.rows, R.cols);
+    if (YTA_LAP_ARR && tws) {   // bidding rounds (lap_rect.hpp rect_arr): arrays just below tws
+        rect_arr_ws(tws - arr_ws_region(R.rows > R.cols ? R.rows : R.cols), R.rows, R.cols, w);
+        const long long wo = (rect_ws_bytes(R.rows, R.cols) + 15) & ~15LL;
+        if (base == lds && wo + 8LL * R.cols <= lds_bytes) {
+            w.av = reinterpret_cast<double *>(lds + wo);
+            w.av_lds = 1;
+        }
+    }
     const int rc = lap_rect(R, pu, px, ps2, w, rsh);
     if (rc && t == 0) atomicOr(err, ERR_SOLVER);
     if (!tr) {
@@ -206,7 +215,7 @@ __device__ __forceinline__ void main_lap_pre(const double *mat, int na, int nb, 
 // reference's result: the rectangular solver in whichever orientation has rows <= columns.
 __device__ __forceinline__ void iou_lap(const LapMat &M, int *rx, unsigned char *lds,
                                         long long lds_bytes, unsigned char *gws, int *err,
-                                        LapStats *ls) {
+                                        LapStats *ls, unsigned char *tws = nullptr) {
     const bool tr = M.na > M.nb;
     const int rows = tr ? M.nb : M.na, cols = tr ? M.na : M.nb;
     if (cols > RECT_CPT_MAX * (int)blockDim.x) {
@@ -215,7 +224,7 @@ __device__ __forceinline__ void iou_lap(const LapMat &M, int *rx, unsigned char 
     }
     const RectMat R = tr ? RectMat{M.m, rows, cols, 1, M.nb, M.neg}
                          : RectMat{M.m, rows, cols, M.nb, 1, M.neg};
-    rect_solve(R, nullptr, nullptr, nullptr, tr, M.na, rx, lds, lds_bytes, gws, err);
+    rect_solve(R, nullptr, nullptr, nullptr, tr, M.na, rx, lds, lds_bytes, gws, err, tws);
 }
 
 // Is x, the solution of the transposed first-round problem (rows = trackers, all matched;
@@ -359,7 +368,10 @@ __device__ __forceinline__ void first_round_lap(const double *mat, int na, int n
         rect_arr_ws(tws - arr_ws_region(rows > cols ? rows : cols), rows, cols, w);
         // the column duals of the rounds (read by every bid scan) in LDS after the work arrays
         const long long wo = (rect_ws_bytes(rows, cols) + 15) & ~15LL;
-        if (base == lds && wo + 8LL * cols <= lds_bytes) w.av = reinterpret_cast<double *>(lds + wo);
+        if (base == lds && wo + 8LL * cols <= lds_bytes) {
+            w.av = reinterpret_cast<double *>(lds + wo);
+            w.av_lds = 1;
+        }
     }
     const RectMat R = tr ? RectMat{mat, rows, cols, 1, nb, false} : RectMat{mat, rows, cols, nb, 1, false};
     const int rc = lap_rect<LAP_T>(R, pu, px, ps2, w, rsh);
