@@ -162,6 +162,33 @@ def test_first_round_normal_orientation_unchanged():
     assert np.array_equal(rx, xo)
 
 
+def _contested(rng, na, nb):
+    """Random costs whose row minima crowd onto a tenth of the columns: many rows claim the same
+    column, so the first-round solve's bidding rounds (lap_rect.hpp rect_arr) do real work."""
+    c = rng.random((na, nb))
+    hot = rng.integers(0, max(1, nb // 10), na)
+    c[np.arange(na), hot] -= rng.random(na)
+    return c
+
+
+@pytest.mark.parametrize("na,nb,kind", [(1, 1, "uniform"), (5, 9, "contested"),
+                                        (64, 64, "contested"), (300, 500, "contested"),
+                                        (1000, 1000, "contested"), (2048, 2100, "contested"),
+                                        (4096, 4264, "contested"), (4096, 4264, "uniform")])
+def test_first_round_bidding_matches_lapjv(na, nb, kind):
+    """Normal orientation (trackers >= detections), tie-free costs: the bidding rounds + searches
+    return lapjv's assignment row for row (the optimum is unique), at the C4 / C5 sizes too (the
+    rounds' duals in LDS up to the C5 shape)."""
+    from oracle.lap import lapjv
+    from yolo_tracking_amd import _lib
+    rng = np.random.default_rng(na * 7 + nb)
+    c = _contested(rng, na, nb) if kind == "contested" else rng.random((na, nb)) - 0.5
+    _, xo, _ = lapjv(c, extend_cost=True)
+    rx, done, n_tight = _lib.lap_first_round(c)
+    assert done and n_tight == -1
+    assert np.array_equal(rx, xo), np.nonzero(rx != xo)[0][:10]
+
+
 @pytest.mark.parametrize("gap", [1e-10, 1e-9, 3e-9, 1e-8])
 @pytest.mark.parametrize("scale", [1.0, 50.0])
 def test_first_round_near_ties_uncertified_or_lapjv(gap, scale):
