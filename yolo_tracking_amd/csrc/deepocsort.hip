@@ -97,6 +97,7 @@ struct DocArgs {
     int *pre_x;
     double *out;
     int *out_counts;
+    int arr_chip;                  // first rounds solved with the chip-wide bidding rounds
     const int *active;             // [S] nonzero = update the stream this frame; null = all
 };
 
@@ -623,7 +624,35 @@ __global__ __launch_bounds__(LAP_T) void k_doc_lap(DocArgs a) {
     first_round_lap(a.mat2 + doc_mb(a, s), c->n_high, c->n_trk, a.rmatch + db, a.cmatched + tb, true,
                     a.pre_u + db, a.pre_x + db, a.pre_s2 + db, a.rmatch + db, lds,
                     lap_kernel_lds(a.CAP, a.MAXD), a.lap_ws + s * a.lap_ws_stride, &c->err,
-                    &c->lap_done, &c->ls, a.lap_ws + (s + 1) * a.lap_ws_stride - tight_ws_bytes());
+                    &c->lap_done, &c->ls, a.lap_ws + (s + 1) * a.lap_ws_stride - tight_ws_bytes(),
+                    nullptr, a.arr_chip != 0);
+}
+
+// The chip-wide bidding rounds of the first round (ocsort_common.hpp fr_arr_*), when a.arr_chip.
+__global__ __launch_bounds__(OC_T) void k_doc_arr0(DocArgs a) {
+    __shared__ int wsum[32];
+    const int s = blockIdx.x;
+    if (a.active && !a.active[s]) return;   // stream not updated this frame
+    const DocCounters *c = a.cnt + s;
+    const long long tb = (long long)s * a.CAP, db = (long long)s * a.MAXD;
+    fr_arr_round0(a.mat2 + doc_mb(a, s), c->n_high, c->n_trk, a.rmatch + db, a.cmatched + tb, true,
+                  a.pre_u + db, a.pre_x + db, a.pre_s2 + db,
+                  a.lap_ws + (s + 1) * a.lap_ws_stride - tight_ws_bytes(), wsum);
+}
+__global__ __launch_bounds__(ARR_SCAN_WPB * WAVE) void k_doc_arrscan(DocArgs a) {
+    const int s = blockIdx.y;
+    if (a.active && !a.active[s]) return;
+    const DocCounters *c = a.cnt + s;
+    fr_arr_scan(a.mat2 + doc_mb(a, s), c->n_high, c->n_trk, a.lap_ws + (s + 1) * a.lap_ws_stride - tight_ws_bytes(),
+                blockIdx.x * ARR_SCAN_WPB + threadIdx.x / WAVE, gridDim.x * ARR_SCAN_WPB);
+}
+__global__ __launch_bounds__(OC_T) void k_doc_arrapply(DocArgs a) {
+    __shared__ int wsum[32];
+    const int s = blockIdx.x;
+    if (a.active && !a.active[s]) return;
+    const DocCounters *c = a.cnt + s;
+    fr_arr_apply(a.mat2 + doc_mb(a, s), c->n_high, c->n_trk, a.lap_ws + (s + 1) * a.lap_ws_stride - tight_ws_bytes(),
+                 wsum);
 }
 
 __global__ __launch_bounds__(OC_T) void k_doc_assoc(DocArgs a) {
@@ -712,18 +741,10 @@ __global__ __launch_bounds__(OC_T) void k_doc_assoc(DocArgs a) {
     YTA_STAMP(2);
     // ---- OCR round (:470-493): asso_func(left dets, last observations), no embedding term
     if (n_ud > 0 && n_ut > 0) {
-        const long long nm = (long long)n_ud * n_ut;
-        double mx = -INFINITY;
-        for (long long q = t; q < nm; q += nt) {
-            const int p = (int)(q / n_ut), k = (int)(q % n_ut);
-            const Box lb = box5(a.clast + (tb + utrk[k]) * 5);
-            const double v = asso_of(a.asso, hbox(udet[p]), lb, 0.0, 0.0);
-            if (a.asso == 1 && v != v) atomicOr(&c->err, ERR_GIOU);
-            mat[q] = v;
-            mx = np_max(mx, v);
-        }
-        block_sync();
-        mx = block_max(mx, sh);
+        const double mx = asso_matrix(
+            a.asso, n_ud, n_ut, [&](int p) { return hbox(udet[p]); },
+            [&](int k) { return box5(a.clast + (tb + utrk[k]) * 5); }, 0.0, 0.0, mat, lds, lds_bytes,
+            &c->err, sh);
         if (mx > a.thr) {
             iou_lap(LapMat{mat, n_ud, n_ut, true}, a.rmatch + db, lds, lds_bytes, gws, &c->err, &c->ls,
                     a.lap_ws + (s + 1) * a.lap_ws_stride - tight_ws_bytes());
@@ -1061,6 +1082,8 @@ int doc_alloc(yta_deepocsort *e) {
     DOCALLOC(a.out, S * CAP * 8);
     const long long n = std::max(CAP, MAXD);
     a.lap_ws_stride = oc_lap_ws_stride(n);
+    a.arr_chip = MAXD >= ARR_CHIP_MIN_DETS;
+    if (const char *v = getenv("YTA_ARR_CHIP")) a.arr_chip = atoi(v);
     DOCALLOC(a.lap_ws, S * a.lap_ws_stride);
     e->lds = (size_t)oc_lds_bytes(CAP, MAXD);
     DOCALLOC(e->d_off, S + 1);
@@ -1134,6 +1157,15 @@ int doc_launch(yta_deepocsort *e, const double *d_dets, const int *d_off, const 
         const long long rcap = std::max<long long>(4, 4096 / a.S);
         hipLaunchKernelGGL(k_doc_rowpre, dim3((unsigned)std::max<long long>(1, std::min(rows, rcap)), a.S),
                            dim3(OC_T), 0, e->stream, a);
+        YTA_HIP(hipGetLastError());
+    }
+    if (a.arr_chip) {   // the first round's bidding rounds over the chip
+        hipLaunchKernelGGL(k_doc_arr0, dim3(a.S), dim3(OC_T), 0, e->stream, a);
+        for (int r = 0; r < ARR_CHIP_ROUNDS; ++r) {
+            hipLaunchKernelGGL(k_doc_arrscan, dim3(ARR_SCAN_BLOCKS, a.S), dim3(ARR_SCAN_WPB * WAVE), 0,
+                               e->stream, a);
+            hipLaunchKernelGGL(k_doc_arrapply, dim3(a.S), dim3(OC_T), 0, e->stream, a);
+        }
         YTA_HIP(hipGetLastError());
     }
     hipLaunchKernelGGL(k_doc_lap, dim3(a.S), dim3(LAP_T), (size_t)lap_kernel_lds(a.CAP, a.MAXD),

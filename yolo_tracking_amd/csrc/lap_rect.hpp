@@ -60,6 +60,10 @@ struct RectWs {
     int *atgt = nullptr;                // rows: the column a free row bids for
     double *adel = nullptr;             // rows: its bid (second minimum - minimum)
     int av_lds = 0;                     // av is in LDS
+    // the state left by the chip-wide bidding rounds (ArrState) to start the searches from
+    const int *sx = nullptr, *syw = nullptr;
+    const double *su = nullptr, *sv = nullptr;
+    const float *ss2 = nullptr;
 };
 // The bidding rounds' arrays (rect_arr_ws), 16-B aligned pieces.
 __host__ __device__ inline long long arr_ws_bytes(long long rows, long long cols) {
@@ -313,6 +317,130 @@ __device__ __noinline__ void rect_arr(const RectMat M, const double *pu, const i
     }
 }
 
+// ---- the same rounds chip-wide (large first rounds: C4 / C5).  In one block, 8 waves rescan the
+// free rows (~100 per C5 frame) one after another; here every free row's wave runs at once on its
+// own CU.  One round = arr_scan (grid: each free row's bid, atomicMax into its column) + arr_apply
+// (block per stream: winners, displaced owners, the new free list); arr_round0 (block) takes the
+// first round's bids from the row pre-pass.  The state lives in global memory (ArrState) and
+// lap_rect_body starts its searches from it (RectWs::sx ...).  A bid is one 64-bit key: the bid
+// rounded down to float in the high half (any winner rule keeps the duals feasible, as the winner
+// pays its own exact bid), the complement of the row in the low half (lowest row on equal keys).
+struct ArrState {
+    int *hdr;                   // [0] rounds on, [1] free rows, [2] state valid, [3] rounds run
+    double *av, *au, *adel;     // cols: duals; rows: u, bid
+    unsigned long long *abid;   // cols: the round's largest key
+    int *ayw, *ax, *afl, *atgt; // cols: owner; rows: column, free list, bid column
+    float *as2;                 // rows: bound
+};
+__host__ __device__ inline long long arr_state_bytes(long long rows, long long cols) {
+    return 64 + cols * 20 + rows * 32 + 64;
+}
+__device__ __forceinline__ ArrState arr_state(unsigned char *base, int rows, int cols) {
+    ArrState st;
+    st.hdr = reinterpret_cast<int *>(base);
+    st.av = reinterpret_cast<double *>(base + 64);
+    st.abid = reinterpret_cast<unsigned long long *>(st.av + cols);
+    st.au = reinterpret_cast<double *>(st.abid + cols);
+    st.adel = st.au + rows;
+    st.ayw = reinterpret_cast<int *>(st.adel + rows);
+    st.ax = st.ayw + cols;
+    st.afl = st.ax + rows;
+    st.atgt = st.afl + rows;
+    st.as2 = reinterpret_cast<float *>(st.atgt + rows);
+    return st;
+}
+__device__ __forceinline__ unsigned long long arr_bid_key(double d, int i) {
+    return ((unsigned long long)__float_as_uint(__double2float_rd(d)) << 32) | (unsigned)(~i);
+}
+constexpr int ARR_CHIP_ROUNDS = 8;   // rounds launched after round 0 (idle ones return at once)
+
+// Winners of the bids of rows list[0..n) (list == nullptr: rows 0..n), then the new free list.
+// Block-wide.  Returns the number of free rows.
+__device__ __forceinline__ int arr_settle(const RectMat M, const ArrState &st, const int *list, int n,
+                                         int *wsum) {
+    const int t = threadIdx.x, nt = blockDim.x;
+    for (int k = t; k < n; k += nt) {   // one winner per column; bidders own nothing
+        const int i = list ? list[k] : k;
+        const int j = st.atgt[i];
+        if (st.abid[j] != arr_bid_key(st.adel[i], i)) continue;
+        const int old = st.ayw[j];
+        if (old >= 0) st.ax[old] = -1;
+        st.ayw[j] = i;
+        st.ax[i] = j;
+        const double vj = st.av[j] - st.adel[i];
+        st.av[j] = vj;
+        st.au[i] = M.at(i, j) - vj;
+        st.as2[i] = 0.0f;
+    }
+    block_sync();
+    for (int k = t; k < n; k += nt) st.abid[st.atgt[list ? list[k] : k]] = 0ull;
+    block_sync();
+    // the list is read above; the compaction may overwrite it (it is st.afl)
+    const int nf = block_compact(M.rows, wsum, [&](int i) { return st.ax[i] < 0; },
+                                 [&](int i, int pos) { st.afl[pos] = i; });
+    block_sync();
+    return nf;
+}
+
+// Round 0, block per stream: state from the row pre-pass, every row bids for its argmin column.
+__device__ __forceinline__ void arr_round0(const RectMat M, const double *pu, const int *px,
+                                           const double *ps2, const ArrState &st, int *wsum) {
+    const int t = threadIdx.x, nt = blockDim.x;
+    for (int j = t; j < M.cols; j += nt) {
+        st.av[j] = 0.0;
+        st.abid[j] = 0ull;
+        st.ayw[j] = -1;
+    }
+    for (int i = t; i < M.rows; i += nt) {
+        const double d = ps2[i];
+        st.ax[i] = -1;
+        st.au[i] = pu[i];
+        st.as2[i] = 0.0f;
+        st.atgt[i] = px[i];
+        st.adel[i] = d >= 0.0 && d < INFINITY ? d : 0.0;
+    }
+    block_sync();
+    for (int i = t; i < M.rows; i += nt) atomicMax(&st.abid[st.atgt[i]], arr_bid_key(st.adel[i], i));
+    block_sync();
+    const int nf = arr_settle(M, st, nullptr, M.rows, wsum);
+    if (t == 0) {
+        st.hdr[0] = nf > 0;
+        st.hdr[1] = nf;
+        st.hdr[2] = 1;
+        st.hdr[3] = 1;
+    }
+}
+
+// One wave: the bid of free-list entry k.
+__device__ __forceinline__ void arr_scan_row(const RectMat M, const ArrState &st, int k) {
+    const int i = st.afl[k];
+    double u1, u2;
+    int j1, j2;
+    rect_row_bid<1>(M, i, st.av, u1, j1, u2, j2);
+    double d = u2 - u1;
+    if (!(d >= 0.0 && d < INFINITY) || j1 == INT_MAX) d = 0.0;
+    int tg = j1 == INT_MAX ? 0 : j1;
+    if (d == 0.0 && j2 != INT_MAX && st.ayw[tg] >= 0 && st.ayw[j2] < 0) tg = j2;
+    if (lane_id() == 0) {
+        st.au[i] = u1;
+        st.atgt[i] = tg;
+        st.adel[i] = d;
+        atomicMax(&st.abid[tg], arr_bid_key(d, i));
+    }
+}
+
+// Block per stream after arr_scan: settle the round; stop when it freed no row.
+__device__ __forceinline__ void arr_apply(const RectMat M, const ArrState &st, int *wsum) {
+    const int n = st.hdr[1];
+    block_sync();   // every thread read the header
+    const int nf = arr_settle(M, st, st.afl, n, wsum);
+    if (threadIdx.x == 0) {
+        st.hdr[0] = nf > 0 && nf < n;
+        st.hdr[1] = nf;
+        st.hdr[3] += 1;
+    }
+}
+
 // Solve.  pre_u / pre_x / pre_s2: the row pre-pass (global, or nullptr: computed here).  Returns 0,
 // or -2 if a row cannot reach a free column (rows > cols, or NaN costs).  On return w.x[i] is the
 // column of row i.  All threads of the block must call it; blockDim.x * CPT >= M.cols.
@@ -325,14 +453,22 @@ __device__ __forceinline__ int lap_rect_body(const RectMat M, const double *pre_
     if (rows <= 0) return 0;
     if (rows > cols) return -2;
     // ---- 1. row pre-pass (when not supplied) and 2. claims
-    const bool own_pre = pre_u == nullptr;   // the bounds then already in w.s2 (as floats)
+    const bool chip = w.sx != nullptr;   // start from the chip-wide rounds' state (ArrState)
+    const bool own_pre = !chip && pre_u == nullptr;   // the bounds then already in w.s2 (floats)
     if (own_pre) {
         for (int i = wid; i < rows; i += nw) rect_row_pre(M, i, w.u, w.x, w.s2);
         pre_u = w.u; pre_x = w.x;
         block_sync();
     }
-    const bool arr = w.av != nullptr;
-    if (arr) {
+    const bool arr = !chip && w.av != nullptr;
+    if (chip) {
+        for (int i = t; i < rows; i += nt) {
+            w.x[i] = w.sx[i];
+            w.u[i] = w.su[i];
+            w.s2[i] = w.ss2[i];
+        }
+        for (int j = t; j < cols; j += nt) w.yw[j] = w.syw[j];
+    } else if (arr) {
 #ifdef YTA_STAMPS
         const unsigned long long ta = wall_clock64();
 #endif
@@ -368,7 +504,10 @@ __device__ __forceinline__ int lap_rect_body(const RectMat M, const double *pre_
         y[q] = -1;
         s2c[q] = 0.0f;
         if (j < cols) {
-            if (arr) {
+            if (chip) {
+                v[q] = w.sv[j];
+                y[q] = w.syw[j];
+            } else if (arr) {
                 v[q] = w.av[j];
                 y[q] = w.yw[j];
             } else {

@@ -447,18 +447,10 @@ __global__ __launch_bounds__(OC_T) void k_oc_assoc(OcArgs a) {
     // ---- F: BYTE round (:289-313)
     YTA_STAMP(5);
     if (a.use_byte && n_lo > 0 && n_ut > 0) {
-        const long long nm = (long long)n_lo * n_ut;
-        double mx = -INFINITY;
-        for (long long q = t; q < nm; q += nt) {
-            const int p = (int)(q / n_ut), k = (int)(q % n_ut);
-            const double v = asso_of(a.asso, box5(din + (long long)a.lo_row[db + p] * 6),
-                                     a.cbox[tb + utrk[k]], img_w, img_h);
-            if (a.asso == 1 && v != v) atomicOr(&c->err, ERR_GIOU);
-            mat[q] = v;
-            mx = np_max(mx, v);
-        }
-        block_sync();
-        mx = block_max(mx, sh);
+        const double mx = asso_matrix(
+            a.asso, n_lo, n_ut, [&](int p) { return box5(din + (long long)a.lo_row[db + p] * 6); },
+            [&](int k) { return a.cbox[tb + utrk[k]]; }, img_w, img_h, mat, lds, lds_bytes, &c->err,
+            sh);
         if (mx > a.thr) {
             iou_lap(LapMat{mat, n_lo, n_ut, true}, a.rmatch + db, lds, lds_bytes, gws, &c->err, &c->ls,
                     a.lap_ws + (s + 1) * a.lap_ws_stride - tight_ws_bytes());
@@ -485,18 +477,10 @@ __global__ __launch_bounds__(OC_T) void k_oc_assoc(OcArgs a) {
     // ---- G: OCR round (:315-342)
     YTA_STAMP(6);
     if (n_ud > 0 && n_ut > 0) {
-        const long long nm = (long long)n_ud * n_ut;
-        double mx = -INFINITY;
-        for (long long q = t; q < nm; q += nt) {
-            const int p = (int)(q / n_ut), k = (int)(q % n_ut);
-            const Box lb = box5(a.clast + (tb + utrk[k]) * 5);
-            const double v = asso_of(a.asso, hbox(udet[p]), lb, img_w, img_h);
-            if (a.asso == 1 && v != v) atomicOr(&c->err, ERR_GIOU);
-            mat[q] = v;
-            mx = np_max(mx, v);
-        }
-        block_sync();
-        mx = block_max(mx, sh);
+        const double mx = asso_matrix(
+            a.asso, n_ud, n_ut, [&](int p) { return hbox(udet[p]); },
+            [&](int k) { return box5(a.clast + (tb + utrk[k]) * 5); }, img_w, img_h, mat, lds,
+            lds_bytes, &c->err, sh);
         if (mx > a.thr) {
             iou_lap(LapMat{mat, n_ud, n_ut, true}, a.rmatch + db, lds, lds_bytes, gws, &c->err, &c->ls,
                     a.lap_ws + (s + 1) * a.lap_ws_stride - tight_ws_bytes());
@@ -1297,14 +1281,31 @@ __global__ __launch_bounds__(OC_T) void k_kat_fr_pre(const double *m, int na, in
 __global__ __launch_bounds__(LAP_T) void k_kat_fr(const double *m, int na, int nb, const double *u,
                                                   const int *x, const double *s2, int *rx,
                                                   long long lds_bytes, unsigned char *gws, int *st,
-                                                  int *n_tight) {
+                                                  int *n_tight, int chip) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     LapStats ls{0, 0, 0};
     if (threadIdx.x == 0) *n_tight = -1;
     __syncthreads();
     first_round_lap(m, na, nb, rx, rx, false, u, x, s2, rx, lds, lds_bytes, gws, st, st + 1, &ls,
                     gws + dense_lap_ws_bytes(na > nb ? na : nb) + arr_ws_region(na > nb ? na : nb),
-                    n_tight);
+                    n_tight, chip != 0);
+}
+// the engines' chip-wide bidding rounds (fr_arr_*) on the KAT's one problem
+__global__ __launch_bounds__(OC_T) void k_kat_arr0(const double *m, int na, int nb, const int *rcnt,
+                                                   const double *u, const int *x, const double *s2,
+                                                   unsigned char *tws) {
+    __shared__ int wsum[32];
+    fr_arr_round0(m, na, nb, rcnt, rcnt, false, u, x, s2, tws, wsum);
+}
+__global__ __launch_bounds__(ARR_SCAN_WPB * WAVE) void k_kat_arrscan(const double *m, int na, int nb,
+                                                                     unsigned char *tws) {
+    fr_arr_scan(m, na, nb, tws, blockIdx.x * ARR_SCAN_WPB + threadIdx.x / WAVE,
+                gridDim.x * ARR_SCAN_WPB);
+}
+__global__ __launch_bounds__(OC_T) void k_kat_arrapply(const double *m, int na, int nb,
+                                                       unsigned char *tws) {
+    __shared__ int wsum[32];
+    fr_arr_apply(m, na, nb, tws, wsum);
 }
 struct KatBuf {
     std::vector<void *> ptrs;
@@ -1354,8 +1355,20 @@ extern "C" int yta_lap_first_round(int device, int na, int nb, const double *cos
     const long long lds = lap_kernel_lds(nb, na);
     hipLaunchKernelGGL(k_kat_fr_pre, dim3(256), dim3(OC_T), 0, 0, dc, na, nb, u, x, s2);
     YTA_HIP(hipGetLastError());
+    // as the engines: the chip-wide bidding rounds for first rounds of ARR_CHIP_MIN_DETS or more
+    const int chip = n >= ARR_CHIP_MIN_DETS;
+    if (chip) {
+        unsigned char *tws = gws + dense_lap_ws_bytes(n) + arr_ws_region(n);
+        hipLaunchKernelGGL(k_kat_arr0, dim3(1), dim3(OC_T), 0, 0, dc, na, nb, drx, u, x, s2, tws);
+        for (int r = 0; r < ARR_CHIP_ROUNDS; ++r) {
+            hipLaunchKernelGGL(k_kat_arrscan, dim3(ARR_SCAN_BLOCKS), dim3(ARR_SCAN_WPB * WAVE), 0, 0,
+                               dc, na, nb, tws);
+            hipLaunchKernelGGL(k_kat_arrapply, dim3(1), dim3(OC_T), 0, 0, dc, na, nb, tws);
+        }
+        YTA_HIP(hipGetLastError());
+    }
     hipLaunchKernelGGL(k_kat_fr, dim3(1), dim3(LAP_T), (size_t)lds, 0, dc, na, nb, u, x, s2, drx,
-                       lds, gws, st, dg);
+                       lds, gws, st, dg, chip);
     YTA_HIP(hipGetLastError());
     int hst[2];
     YTA_HIP(hipMemcpy(hst, st, sizeof(hst), hipMemcpyDeviceToHost));

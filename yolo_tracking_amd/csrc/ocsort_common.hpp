@@ -93,8 +93,9 @@ constexpr long long LAP_LDS_MAX = 152 * 1024;   // their dynamic LDS cap (160 Ki
 #ifndef YTA_LAP_ARR
 #define YTA_LAP_ARR 1
 #endif
-__host__ __device__ inline long long arr_ws_region(long long n) {
-    return (arr_ws_bytes(n, n) + 255) & ~255LL;
+__host__ __device__ inline long long arr_ws_region(long long n) {   // in-block or chip-wide rounds
+    const long long a = arr_ws_bytes(n, n), b = arr_state_bytes(n, n);
+    return ((a > b ? a : b) + 255) & ~255LL;
 }
 
 // The first-round solve's work arrays, either orientation (first_round_lap transposes the
@@ -210,6 +211,45 @@ __device__ __forceinline__ void main_lap_pre(const double *mat, int na, int nb, 
     }
 }
 
+// A -IoU round's matrix (BYTE / OCR: asso(left dets, left trackers), association.py:20-28 input):
+// mat[p * nb + k] = asso(dbox(p), tbox(k)), and its maximum.  The na + nb boxes are gathered once
+// into LDS (every gather of a thread's batch in flight at once) when they fit `lds_bytes`, so
+// the na x nb evaluations read LDS; a gather chain per evaluation (index -> record, ~1 us) made
+// the C5 OCR round ~360 us.  Otherwise every evaluation gathers its two boxes.
+template <typename DB, typename TB>
+__device__ __forceinline__ double asso_matrix(int kind, int na, int nb, DB dbox, TB tbox, double w,
+                                              double h, double *mat, unsigned char *lds,
+                                              long long lds_bytes, int *err, OcShared &sh) {
+    const int t = threadIdx.x, nt = blockDim.x;
+    const long long nm = (long long)na * nb;
+    double mx = -INFINITY;
+    bool bad = false;
+    if ((long long)(na + nb) * (long long)sizeof(Box) <= lds_bytes) {
+        Box *bd = reinterpret_cast<Box *>(lds), *bt = bd + na;
+        batched_for<4>(na, [&](int p) { return dbox(p); }, [&](int p, const Box &b) { bd[p] = b; });
+        batched_for<4>(nb, [&](int k) { return tbox(k); }, [&](int k, const Box &b) { bt[k] = b; });
+        block_sync();
+        for (long long q = t; q < nm; q += nt) {
+            const int p = (int)(q / nb), k = (int)(q % nb);
+            const double v = asso_of(kind, bd[p], bt[k], w, h);
+            bad |= kind == 1 && v != v;
+            mat[q] = v;
+            mx = np_max(mx, v);
+        }
+    } else {
+        for (long long q = t; q < nm; q += nt) {
+            const int p = (int)(q / nb), k = (int)(q % nb);
+            const double v = asso_of(kind, dbox(p), tbox(k), w, h);
+            bad |= kind == 1 && v != v;
+            mat[q] = v;
+            mx = np_max(mx, v);
+        }
+    }
+    if (bad) atomicOr(err, ERR_GIOU);
+    block_sync();
+    return block_max(mx, sh);
+}
+
 // The -IoU rounds (BYTE / OCR: association.py:20-28 on -iou): only pairs with IoU >= threshold
 // survive and the leftover lists are re-sorted (np.setdiff1d), so any optimal solution gives the
 // reference's result: the rectangular solver in whichever orientation has rows <= columns.
@@ -224,7 +264,10 @@ __device__ __forceinline__ void iou_lap(const LapMat &M, int *rx, unsigned char 
     }
     const RectMat R = tr ? RectMat{M.m, rows, cols, 1, M.nb, M.neg}
                          : RectMat{M.m, rows, cols, M.nb, 1, M.neg};
-    rect_solve(R, nullptr, nullptr, nullptr, tr, M.na, rx, lds, lds_bytes, gws, err, tws);
+    // (no bidding rounds here: on the OCR matrices of the C5 run they cost more than they saved,
+    // k_hs_assoc 465 -> 567 us, profiles/r04k_*)
+    (void)tws;
+    rect_solve(R, nullptr, nullptr, nullptr, tr, M.na, rx, lds, lds_bytes, gws, err);
 }
 
 // Is x, the solution of the transposed first-round problem (rows = trackers, all matched;
@@ -313,6 +356,73 @@ __device__ __forceinline__ int unique_optimum_tr(const double *mat, int na, int 
     return bad == 0;
 }
 
+constexpr int ARR_SCAN_WPB = 4;       // fr_arr_scan: waves per block
+constexpr int ARR_SCAN_BLOCKS = 64;   // blocks per stream (a wave per free row, looping beyond)
+// Engines solve first rounds this large with the chip-wide rounds (smaller ones in the block)
+constexpr int ARR_CHIP_MIN_DETS = 1024;
+
+// Does the first round solve here (first_round_lap), and not take the fast path or leave it to the
+// association kernel?  Block-wide (all threads get the answer).
+__device__ __forceinline__ bool fr_solves(int na, int nb, const int *rcnt, const int *ccnt,
+                                          bool fast_rule) {
+    __shared__ int flags[2];
+    const int t = threadIdx.x, nt = blockDim.x;
+    const int rows = na > nb ? nb : na, cols = na > nb ? na : nb;
+    bool solve = rows > 0 && cols <= RECT_CPT_MAX * LAP_T;
+    if (solve && fast_rule) {
+        if (t < 2) flags[t] = 0;
+        __syncthreads();
+        int over = 0, bad = 0;
+        for (int i = t; i < na; i += nt) {
+            const int k = rcnt[i];
+            over |= k;
+            bad |= k > 1;
+        }
+        for (int j = t; j < nb; j += nt) bad |= ccnt[j] > 1;
+        if (over) atomicOr(&flags[0], 1);
+        if (bad) atomicOr(&flags[1], 1);
+        __syncthreads();
+        if (flags[1] == 0 && flags[0]) solve = false;   // the fast path
+        __syncthreads();
+    }
+    return solve;
+}
+
+// The chip-wide bidding rounds of a first round solved in the normal orientation (lap_rect.hpp
+// ArrState), between the row pre-pass and first_round_lap: fr_arr_round0 (block per stream),
+// then ARR_CHIP_ROUNDS x (fr_arr_scan: a wave per free row over the grid, fr_arr_apply: block per
+// stream).  The state sits in the bidding region below tws; hdr[2] tells first_round_lap to start
+// from it.  Same arguments as first_round_lap.
+__device__ __forceinline__ void fr_arr_round0(const double *mat, int na, int nb, const int *rcnt,
+                                              const int *ccnt, bool fast_rule, const double *pu,
+                                              const int *px, const double *ps2, unsigned char *tws,
+                                              int *wsum) {
+    const bool ok = YTA_LAP_ARR && na <= nb && fr_solves(na, nb, rcnt, ccnt, fast_rule);
+    const ArrState st = arr_state(tws - arr_ws_region(nb), na, nb);
+    if (!ok) {
+        if (threadIdx.x == 0 && nb > 0) st.hdr[0] = st.hdr[2] = 0;
+        return;
+    }
+    arr_round0(RectMat{mat, na, nb, nb, 1, false}, pu, px, ps2, st, wsum);
+}
+// wave w of the grid's waves for this stream (nwaves in all)
+__device__ __forceinline__ void fr_arr_scan(const double *mat, int na, int nb, unsigned char *tws,
+                                            int w, int nwaves) {
+    if (na > nb || na <= 0) return;
+    const ArrState st = arr_state(tws - arr_ws_region(nb), na, nb);
+    if (!st.hdr[0]) return;
+    const int n = st.hdr[1];
+    const RectMat M{mat, na, nb, nb, 1, false};
+    for (int k = w; k < n; k += nwaves) arr_scan_row(M, st, k);
+}
+__device__ __forceinline__ void fr_arr_apply(const double *mat, int na, int nb, unsigned char *tws,
+                                             int *wsum) {
+    if (na > nb || na <= 0) return;
+    const ArrState st = arr_state(tws - arr_ws_region(nb), na, nb);
+    if (!st.hdr[0]) return;
+    arr_apply(RectMat{mat, na, nb, nb, 1, false}, st, wsum);
+}
+
 // First-round solve in its own launch, one LAP_T-thread block per stream (up to 32 columns per
 // thread: 16384 columns, every cost load of a step in flight at once), when the fast path
 // (association.py:156-159, `fast_rule`) does not apply; rx and *done = 1 on success, else the
@@ -333,39 +443,31 @@ __device__ __forceinline__ void first_round_lap(const double *mat, int na, int n
                                                 unsigned char *lds, long long lds_bytes,
                                                 unsigned char *gws, int *err, int *done,
                                                 LapStats *ls, unsigned char *tws,
-                                                int *n_tight = nullptr) {
+                                                int *n_tight = nullptr, bool chip = false) {
     __shared__ RectShared rsh;
-    __shared__ int flags[2];
     const int t = threadIdx.x, nt = blockDim.x;
     const bool tr = na > nb;
     const int rows = tr ? nb : na, cols = tr ? na : nb;
-    bool solve = rows > 0 && cols <= RECT_CPT_MAX * nt;
-    if (solve && fast_rule) {
-        if (t < 2) flags[t] = 0;
-        __syncthreads();
-        int over = 0, bad = 0;
-        for (int i = t; i < na; i += nt) {
-            const int k = rcnt[i];
-            over |= k;
-            bad |= k > 1;
-        }
-        for (int j = t; j < nb; j += nt) bad |= ccnt[j] > 1;
-        if (over) atomicOr(&flags[0], 1);
-        if (bad) atomicOr(&flags[1], 1);
-        __syncthreads();
-        if (flags[1] == 0 && flags[0]) solve = false;   // the fast path
-    }
+    const bool solve = fr_solves(na, nb, rcnt, ccnt, fast_rule);
     if (!solve) {
         if (t == 0) *done = 0;
         return;
     }
     unsigned char *base = rect_ws_bytes(rows, cols, tr) <= lds_bytes ? lds : gws;
     RectWs w = rect_ws(base, rows, cols, tr);
-    // the bidding rounds' arrays: the region just below tws (oc_lap_ws_stride).  Not for the
-    // transposed solve: a bid leaves its row tight on two columns, and a tight edge into an
-    // unmatched column fails the uniqueness certificate
-    if (YTA_LAP_ARR && !tr) {
-        rect_arr_ws(tws - arr_ws_region(rows > cols ? rows : cols), rows, cols, w);
+    unsigned char *aws = tws - arr_ws_region(rows > cols ? rows : cols);
+    const ArrState st = arr_state(aws, rows, cols);
+    if (YTA_LAP_ARR && chip && !tr && st.hdr[2]) {   // the chip-wide rounds ran: their state
+        w.sx = st.ax;
+        w.su = st.au;
+        w.ss2 = st.as2;
+        w.syw = st.ayw;
+        w.sv = st.av;
+    } else if (YTA_LAP_ARR && !tr) {
+        // the bidding rounds in this block: the region just below tws (oc_lap_ws_stride).  Not for
+        // the transposed solve: a bid leaves its row tight on two columns, and a tight edge into
+        // an unmatched column fails the uniqueness certificate
+        rect_arr_ws(aws, rows, cols, w);
         // the column duals of the rounds (read by every bid scan) in LDS after the work arrays
         const long long wo = (rect_ws_bytes(rows, cols) + 15) & ~15LL;
         if (base == lds && wo + 8LL * cols <= lds_bytes) {
