@@ -306,12 +306,13 @@ __device__ __forceinline__ int block_compact_ld(int n, int *wsum, First first, S
         const int hi = lo + per < base + m ? lo + per : base + m;
         K kk[PER];
         V v[PER];
+        if (lo < hi) {   // loads unconditional within the run (items past it load the run's last
+                         // item, unused): a guarded load compiles to a branch and a wait per item
 #pragma unroll
-        for (int k = 0; k < PER; ++k)
-            if (lo + k < hi) kk[k] = first(lo + k);
+            for (int k = 0; k < PER; ++k) kk[k] = first(lo + k < hi ? lo + k : hi - 1);
 #pragma unroll
-        for (int k = 0; k < PER; ++k)
-            if (lo + k < hi) v[k] = second(lo + k, kk[k]);
+            for (int k = 0; k < PER; ++k) v[k] = second(lo + k < hi ? lo + k : hi - 1, kk[k]);
+        }
         unsigned bits = 0;
 #pragma unroll
         for (int k = 0; k < PER; ++k)
@@ -336,12 +337,11 @@ __device__ __forceinline__ void batched_for2(int n, First first, Second second, 
     for (int base = t; base < n; base += B * nt) {
         K kk[B];
         V v[B];
+        // unconditional loads (items past n load item `base`, unused): see block_compact_ld
 #pragma unroll
-        for (int b = 0; b < B; ++b)
-            if (base + b * nt < n) kk[b] = first(base + b * nt);
+        for (int b = 0; b < B; ++b) kk[b] = first(base + b * nt < n ? base + b * nt : base);
 #pragma unroll
-        for (int b = 0; b < B; ++b)
-            if (base + b * nt < n) v[b] = second(base + b * nt, kk[b]);
+        for (int b = 0; b < B; ++b) v[b] = second(base + b * nt < n ? base + b * nt : base, kk[b]);
 #pragma unroll
         for (int b = 0; b < B; ++b)
             if (base + b * nt < n) use(base + b * nt, v[b]);
@@ -357,9 +357,9 @@ __device__ __forceinline__ void batched_for(int n, Load load, Use use) {
     for (int base = t; base < n; base += B * nt) {
         V v[B];
 #pragma unroll
-        for (int b = 0; b < B; ++b) {
+        for (int b = 0; b < B; ++b) {   // unconditional loads: see block_compact_ld
             const int i = base + b * nt;
-            if (i < n) v[b] = load(i);
+            v[b] = load(i < n ? i : base);
         }
 #pragma unroll
         for (int b = 0; b < B; ++b) {

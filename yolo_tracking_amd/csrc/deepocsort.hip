@@ -644,7 +644,7 @@ __global__ __launch_bounds__(ARR_SCAN_WPB * WAVE) void k_doc_arrscan(DocArgs a) 
     if (a.active && !a.active[s]) return;
     const DocCounters *c = a.cnt + s;
     fr_arr_scan(a.mat2 + doc_mb(a, s), c->n_high, c->n_trk, a.lap_ws + (s + 1) * a.lap_ws_stride - tight_ws_bytes(),
-                blockIdx.x * ARR_SCAN_WPB + threadIdx.x / WAVE, gridDim.x * ARR_SCAN_WPB);
+                blockIdx.x, gridDim.x);
 }
 __global__ __launch_bounds__(OC_T) void k_doc_arrapply(DocArgs a) {
     __shared__ int wsum[32];

@@ -606,7 +606,7 @@ __global__ __launch_bounds__(ARR_SCAN_WPB * WAVE) void k_hs_arrscan(HsArgs a) {
     if (a.active && !a.active[s]) return;
     const HsCounters *c = a.cnt + s;
     fr_arr_scan(a.cost + hs_mb(a, s), c->n_high, c->n_trk, a.lap_ws + (s + 1) * a.lap_ws_stride - tight_ws_bytes(),
-                blockIdx.x * ARR_SCAN_WPB + threadIdx.x / WAVE, gridDim.x * ARR_SCAN_WPB);
+                blockIdx.x, gridDim.x);
 }
 __global__ __launch_bounds__(OC_T) void k_hs_arrapply(HsArgs a) {
     __shared__ int wsum[32];

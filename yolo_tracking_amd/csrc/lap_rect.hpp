@@ -194,42 +194,53 @@ __device__ __forceinline__ void top2_push(double c, int j, double &m1, int &k1, 
 // (lowest column on ties); wave-uniform results.
 // Loads are unconditional (index clamped, value masked): a load under `j < cols` becomes a branch
 // per element with its own wait, one round trip per element.  AS: address space of v (3 = LDS).
+// Merge of two (smallest, second smallest) pairs with their columns, lexicographic (value, column).
+__device__ __forceinline__ void top2_merge(double &m1, int &k1, double &m2, int &k2, double o1, int q1,
+                                           double o2, int q2) {
+    if (o1 < m1 || (o1 == m1 && q1 < k1)) {          // the other's first wins
+        if (m1 < o2 || (m1 == o2 && k1 < q2)) { m2 = m1; k2 = k1; }
+        else { m2 = o2; k2 = q2; }
+        m1 = o1; k1 = q1;
+    } else if (o1 < m2 || (o1 == m2 && q1 < k2)) {
+        m2 = o1; k2 = q1;
+    }
+}
+// Columns [jb, je) of row i, lanes strided; wave-uniform results.
 template <int AS>
-__device__ __forceinline__ void rect_row_bid(const RectMat M, int i, const double *v, double &u1,
-                                             int &j1, double &u2, int &j2) {
+__device__ __forceinline__ void rect_row_bid_range(const RectMat M, int i, const double *v, int jb,
+                                                   int je, double &u1, int &j1, double &u2, int &j2) {
     typedef const __attribute__((address_space(AS))) double *VP;
     const VP vp = (VP)v;
-    const int lane = lane_id(), cols = M.cols;
+    const int lane = lane_id();
     constexpr int CH = 16;
     double m1 = INFINITY, m2 = INFINITY;
     int k1 = INT_MAX, k2 = INT_MAX;
-    for (int j0 = 0; j0 < cols; j0 += CH * WAVE) {
+    for (int j0 = jb; j0 < je; j0 += CH * WAVE) {
         double c[CH], vv[CH];
 #pragma unroll
         for (int k = 0; k < CH; ++k) {
-            const int j = j0 + k * WAVE + lane, jc = j < cols ? j : cols - 1;
+            const int j = j0 + k * WAVE + lane, jc = j < je ? j : je - 1;
             c[k] = M.at(i, jc);
             vv[k] = vp[jc];
         }
 #pragma unroll
         for (int k = 0; k < CH; ++k) {
             const int j = j0 + k * WAVE + lane;
-            top2_push(j < cols ? c[k] - vv[k] : INFINITY, j, m1, k1, m2, k2);
+            top2_push(j < je ? c[k] - vv[k] : INFINITY, j, m1, k1, m2, k2);
         }
     }
 #pragma unroll
     for (int s = 1; s < WAVE; s <<= 1) {
         const double o1 = __shfl_xor(m1, s), o2 = __shfl_xor(m2, s);
         const int q1 = __shfl_xor(k1, s), q2 = __shfl_xor(k2, s);
-        if (o1 < m1 || (o1 == m1 && q1 < k1)) {          // the other's first wins
-            if (m1 < o2 || (m1 == o2 && k1 < q2)) { m2 = m1; k2 = k1; }
-            else { m2 = o2; k2 = q2; }
-            m1 = o1; k1 = q1;
-        } else if (o1 < m2 || (o1 == m2 && q1 < k2)) {
-            m2 = o1; k2 = q1;
-        }
+        top2_merge(m1, k1, m2, k2, o1, q1, o2, q2);
     }
     u1 = m1; j1 = k1; u2 = m2; j2 = k2;
+}
+template <int AS>
+__device__ __forceinline__ void rect_row_bid(const RectMat M, int i, const double *v, double &u1,
+                                             int &j1, double &u2, int &j2) {
+    rect_row_bid_range<AS>(M, i, v, 0, M.cols, u1, j1, u2, j2);
 }
 
 // Block-wide; the rows' pre-pass in pu / px / ps2.  On return: w.x, w.u, w.s2, w.yw and w.av
@@ -411,22 +422,38 @@ __device__ __forceinline__ void arr_round0(const RectMat M, const double *pu, co
     }
 }
 
-// One wave: the bid of free-list entry k.
-__device__ __forceinline__ void arr_scan_row(const RectMat M, const ArrState &st, int k) {
+// One block: the bid of free-list entry k, each wave over its share of the columns (one or two
+// chunks of loads in flight per lane instead of five for a whole C5 row on one wave).
+struct ArrTop2 {
+    double m1, m2;
+    int k1, k2;
+};
+__device__ __forceinline__ void arr_scan_row(const RectMat M, const ArrState &st, int k,
+                                             ArrTop2 *slot) {
+    const int nw = blockDim.x / WAVE, wid = threadIdx.x / WAVE;
     const int i = st.afl[k];
+    const int per = (M.cols + nw - 1) / nw;
+    const int jb = wid * per < M.cols ? wid * per : M.cols;
+    const int je = jb + per < M.cols ? jb + per : M.cols;
     double u1, u2;
     int j1, j2;
-    rect_row_bid<1>(M, i, st.av, u1, j1, u2, j2);
-    double d = u2 - u1;
-    if (!(d >= 0.0 && d < INFINITY) || j1 == INT_MAX) d = 0.0;
-    int tg = j1 == INT_MAX ? 0 : j1;
-    if (d == 0.0 && j2 != INT_MAX && st.ayw[tg] >= 0 && st.ayw[j2] < 0) tg = j2;
-    if (lane_id() == 0) {
-        st.au[i] = u1;
+    rect_row_bid_range<1>(M, i, st.av, jb, je, u1, j1, u2, j2);
+    if (lane_id() == 0) slot[wid] = ArrTop2{u1, u2, j1, j2};
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double m1 = INFINITY, m2 = INFINITY;
+        int k1 = INT_MAX, k2 = INT_MAX;
+        for (int w = 0; w < nw; ++w) top2_merge(m1, k1, m2, k2, slot[w].m1, slot[w].k1, slot[w].m2, slot[w].k2);
+        double d = m2 - m1;
+        if (!(d >= 0.0 && d < INFINITY) || k1 == INT_MAX) d = 0.0;
+        int tg = k1 == INT_MAX ? 0 : k1;
+        if (d == 0.0 && k2 != INT_MAX && st.ayw[tg] >= 0 && st.ayw[k2] < 0) tg = k2;
+        st.au[i] = m1;
         st.atgt[i] = tg;
         st.adel[i] = d;
         atomicMax(&st.abid[tg], arr_bid_key(d, i));
     }
+    __syncthreads();   // the slots are reused by the block's next row
 }
 
 // Block per stream after arr_scan: settle the round; stop when it freed no row.

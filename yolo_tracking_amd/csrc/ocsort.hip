@@ -1299,8 +1299,7 @@ __global__ __launch_bounds__(OC_T) void k_kat_arr0(const double *m, int na, int 
 }
 __global__ __launch_bounds__(ARR_SCAN_WPB * WAVE) void k_kat_arrscan(const double *m, int na, int nb,
                                                                      unsigned char *tws) {
-    fr_arr_scan(m, na, nb, tws, blockIdx.x * ARR_SCAN_WPB + threadIdx.x / WAVE,
-                gridDim.x * ARR_SCAN_WPB);
+    fr_arr_scan(m, na, nb, tws, blockIdx.x, gridDim.x);
 }
 __global__ __launch_bounds__(OC_T) void k_kat_arrapply(const double *m, int na, int nb,
                                                        unsigned char *tws) {

@@ -357,7 +357,7 @@ __device__ __forceinline__ int unique_optimum_tr(const double *mat, int na, int 
 }
 
 constexpr int ARR_SCAN_WPB = 4;       // fr_arr_scan: waves per block
-constexpr int ARR_SCAN_BLOCKS = 64;   // blocks per stream (a wave per free row, looping beyond)
+constexpr int ARR_SCAN_BLOCKS = 256;  // blocks per stream (a block per free row, looping beyond)
 // Engines solve first rounds this large with the chip-wide rounds (smaller ones in the block)
 constexpr int ARR_CHIP_MIN_DETS = 1024;
 
@@ -405,15 +405,16 @@ __device__ __forceinline__ void fr_arr_round0(const double *mat, int na, int nb,
     }
     arr_round0(RectMat{mat, na, nb, nb, 1, false}, pu, px, ps2, st, wsum);
 }
-// wave w of the grid's waves for this stream (nwaves in all)
+// block blk of the grid's nblk blocks for this stream: a free row at a time
 __device__ __forceinline__ void fr_arr_scan(const double *mat, int na, int nb, unsigned char *tws,
-                                            int w, int nwaves) {
+                                            int blk, int nblk) {
+    __shared__ ArrTop2 slot[ARR_SCAN_WPB];
     if (na > nb || na <= 0) return;
     const ArrState st = arr_state(tws - arr_ws_region(nb), na, nb);
     if (!st.hdr[0]) return;
     const int n = st.hdr[1];
     const RectMat M{mat, na, nb, nb, 1, false};
-    for (int k = w; k < n; k += nwaves) arr_scan_row(M, st, k);
+    for (int k = blk; k < n; k += nblk) arr_scan_row(M, st, k, slot);
 }
 __device__ __forceinline__ void fr_arr_apply(const double *mat, int na, int nb, unsigned char *tws,
                                              int *wsum) {
