@@ -120,27 +120,66 @@ __device__ int lapb_relax_scan(int n, const LapMat &M, int &lo, int &hi, DP d, D
         const double hh = M.at(r, k) - v[k] - dk;
         const int base = h, cnt = n - h;
         for (int q = t; q < (cnt + 31) / 32; q += nt) sh.bits[q] = 0u;
-        // the first free column reached at the minimum (in position order)
+        // the first free column reached at the minimum (in position order).  Up to RP positions
+        // per thread: the row's entries of all of them loaded at once (unconditional loads,
+        // clamped index) and kept for the update pass, instead of one load round trip per
+        // position and the row read twice
+        constexpr int RP = 8;
+        const bool regs = cnt <= RP * nt;
         int my_fin = INT_MAX;
-        for (int p = base + t; p < n; p += nt) {
-            const int kk = cols[p];
-            const double nd = M.at(r, kk) - v[kk] - hh;
-            if (nd < d[kk] && nd == dk && y[kk] < 0) {
-                my_fin = p;
-                break;
+        int kkr[RP];
+        double ndr[RP];
+        if (regs) {
+#pragma unroll
+            for (int q = 0; q < RP; ++q) {
+                const int p = base + t + q * nt;
+                kkr[q] = cols[p < n ? p : n - 1];
+            }
+            double cr[RP];
+#pragma unroll
+            for (int q = 0; q < RP; ++q) cr[q] = M.at(r, kkr[q]);
+#pragma unroll
+            for (int q = 0; q < RP; ++q) {
+                const int p = base + t + q * nt, kk = kkr[q];
+                ndr[q] = cr[q] - v[kk] - hh;
+                if (my_fin == INT_MAX && p < n && ndr[q] < d[kk] && ndr[q] == dk && y[kk] < 0)
+                    my_fin = p;
+            }
+        } else {
+            for (int p = base + t; p < n; p += nt) {
+                const int kk = cols[p];
+                const double nd = M.at(r, kk) - v[kk] - hh;
+                if (nd < d[kk] && nd == dk && y[kk] < 0) {
+                    my_fin = p;
+                    break;
+                }
             }
         }
         const double ff = lapb_reduce(true, my_fin == INT_MAX ? 1e300 : (double)my_fin, sh, par);
         const int ffin = ff >= 1e300 ? INT_MAX : (int)ff;
         // every position up to it is visited: distance updates, hits into the bitmap
-        for (int p = base + t; p < n && p <= ffin; p += nt) {
-            const int kk = cols[p];
-            const double nd = M.at(r, kk) - v[kk] - hh;
-            if (nd < d[kk]) {
-                d[kk] = nd;
-                pred[kk] = r;
-                if (nd == dk && p < ffin)
-                    atomicOr(&sh.bits[(p - base) >> 5], 1u << ((p - base) & 31));
+        if (regs) {
+#pragma unroll
+            for (int q = 0; q < RP; ++q) {
+                const int p = base + t + q * nt, kk = kkr[q];
+                const double nd = ndr[q];
+                if (p < n && p <= ffin && nd < d[kk]) {
+                    d[kk] = nd;
+                    pred[kk] = r;
+                    if (nd == dk && p < ffin)
+                        atomicOr(&sh.bits[(p - base) >> 5], 1u << ((p - base) & 31));
+                }
+            }
+        } else {
+            for (int p = base + t; p < n && p <= ffin; p += nt) {
+                const int kk = cols[p];
+                const double nd = M.at(r, kk) - v[kk] - hh;
+                if (nd < d[kk]) {
+                    d[kk] = nd;
+                    pred[kk] = r;
+                    if (nd == dk && p < ffin)
+                        atomicOr(&sh.bits[(p - base) >> 5], 1u << ((p - base) & 31));
+                }
             }
         }
         block_sync();
