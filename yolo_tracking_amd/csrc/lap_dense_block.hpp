@@ -103,6 +103,47 @@ __device__ __forceinline__ double lapb_reduce(bool is_min, double v, LapBShared 
     return r;
 }
 
+// One relax_scan sweep of row r over positions [base, n) with RP >= (n - base) / blockDim
+// positions per thread: the cols / cost loads of all of them issued at once (unconditional,
+// clamped index: a guarded load becomes a branch and a wait per position), the first free column
+// reached at the minimum found, then the updates from the kept values.  Returns that position.
+template <int RP, typename DP, typename IP>
+__device__ __forceinline__ int lapb_relax_regs(int n, const LapMat &M, int base, int r, double dk,
+                                               double hh, DP d, DP v, IP cols, IP pred, IP y,
+                                               LapBShared &sh, int &par) {
+    const int t = threadIdx.x, nt = blockDim.x;
+    int kkr[RP];
+    double ndr[RP];
+#pragma unroll
+    for (int q = 0; q < RP; ++q) {
+        const int p = base + t + q * nt;
+        kkr[q] = cols[p < n ? p : n - 1];
+    }
+    double cr[RP];
+#pragma unroll
+    for (int q = 0; q < RP; ++q) cr[q] = M.at(r, kkr[q]);
+    int my_fin = INT_MAX;
+#pragma unroll
+    for (int q = 0; q < RP; ++q) {
+        const int p = base + t + q * nt, kk = kkr[q];
+        ndr[q] = cr[q] - v[kk] - hh;
+        if (my_fin == INT_MAX && p < n && ndr[q] < d[kk] && ndr[q] == dk && y[kk] < 0) my_fin = p;
+    }
+    const double ff = lapb_reduce(true, my_fin == INT_MAX ? 1e300 : (double)my_fin, sh, par);
+    const int ffin = ff >= 1e300 ? INT_MAX : (int)ff;
+#pragma unroll
+    for (int q = 0; q < RP; ++q) {
+        const int p = base + t + q * nt, kk = kkr[q];
+        const double nd = ndr[q];
+        if (p < n && p <= ffin && nd < d[kk]) {
+            d[kk] = nd;
+            pred[kk] = r;
+            if (nd == dk && p < ffin) atomicOr(&sh.bits[(p - base) >> 5], 1u << ((p - base) & 31));
+        }
+    }
+    return ffin;
+}
+
 // relax_scan (lapjv.c) by the block.  Returns a free column reached at the minimum distance
 // (lo / hi left as they were, as the C code's early return leaves *plo / *phi), or -1 with
 // lo / hi advanced.
@@ -120,32 +161,17 @@ __device__ int lapb_relax_scan(int n, const LapMat &M, int &lo, int &hi, DP d, D
         const double hh = M.at(r, k) - v[k] - dk;
         const int base = h, cnt = n - h;
         for (int q = t; q < (cnt + 31) / 32; q += nt) sh.bits[q] = 0u;
-        // the first free column reached at the minimum (in position order).  Up to RP positions
-        // per thread: the row's entries of all of them loaded at once (unconditional loads,
-        // clamped index) and kept for the update pass, instead of one load round trip per
-        // position and the row read twice
-        constexpr int RP = 8;
-        const bool regs = cnt <= RP * nt;
-        int my_fin = INT_MAX;
-        int kkr[RP];
-        double ndr[RP];
-        if (regs) {
-#pragma unroll
-            for (int q = 0; q < RP; ++q) {
-                const int p = base + t + q * nt;
-                kkr[q] = cols[p < n ? p : n - 1];
-            }
-            double cr[RP];
-#pragma unroll
-            for (int q = 0; q < RP; ++q) cr[q] = M.at(r, kkr[q]);
-#pragma unroll
-            for (int q = 0; q < RP; ++q) {
-                const int p = base + t + q * nt, kk = kkr[q];
-                ndr[q] = cr[q] - v[kk] - hh;
-                if (my_fin == INT_MAX && p < n && ndr[q] < d[kk] && ndr[q] == dk && y[kk] < 0)
-                    my_fin = p;
-            }
-        } else {
+        // the first free column reached at the minimum (in position order), then every position
+        // up to it: distance updates, hits into the bitmap.  Up to 8 positions per thread go
+        // through lapb_relax_regs (the row's entries of all of them loaded at once, kept for the
+        // update pass); larger problems loop
+        int ffin;
+        const int m = (cnt + nt - 1) / nt;   // positions per thread, block-uniform
+        if (m <= 2) ffin = lapb_relax_regs<2>(n, M, base, r, dk, hh, d, v, cols, pred, y, sh, par);
+        else if (m <= 4) ffin = lapb_relax_regs<4>(n, M, base, r, dk, hh, d, v, cols, pred, y, sh, par);
+        else if (m <= 8) ffin = lapb_relax_regs<8>(n, M, base, r, dk, hh, d, v, cols, pred, y, sh, par);
+        else {
+            int my_fin = INT_MAX;
             for (int p = base + t; p < n; p += nt) {
                 const int kk = cols[p];
                 const double nd = M.at(r, kk) - v[kk] - hh;
@@ -154,23 +180,8 @@ __device__ int lapb_relax_scan(int n, const LapMat &M, int &lo, int &hi, DP d, D
                     break;
                 }
             }
-        }
-        const double ff = lapb_reduce(true, my_fin == INT_MAX ? 1e300 : (double)my_fin, sh, par);
-        const int ffin = ff >= 1e300 ? INT_MAX : (int)ff;
-        // every position up to it is visited: distance updates, hits into the bitmap
-        if (regs) {
-#pragma unroll
-            for (int q = 0; q < RP; ++q) {
-                const int p = base + t + q * nt, kk = kkr[q];
-                const double nd = ndr[q];
-                if (p < n && p <= ffin && nd < d[kk]) {
-                    d[kk] = nd;
-                    pred[kk] = r;
-                    if (nd == dk && p < ffin)
-                        atomicOr(&sh.bits[(p - base) >> 5], 1u << ((p - base) & 31));
-                }
-            }
-        } else {
+            const double ff = lapb_reduce(true, my_fin == INT_MAX ? 1e300 : (double)my_fin, sh, par);
+            ffin = ff >= 1e300 ? INT_MAX : (int)ff;
             for (int p = base + t; p < n && p <= ffin; p += nt) {
                 const int kk = cols[p];
                 const double nd = M.at(r, kk) - v[kk] - hh;
