@@ -224,6 +224,10 @@ def main():
         ph = [f"{nm} {(int(st[41 + k]) - int(st[40 + k])) / 100:.1f}" for k, nm in enumerate(names)
               if st[41 + k] and st[40 + k] and st[41 + k] >= st[40 + k]]
         print("k_hs_assoc (block 0, last frame, us): " + ", ".join(ph), file=sys.stderr)
+        if st[48] and st[43] and st[44] >= st[48] >= st[43]:
+            print(f"  OCR round: matrix {(int(st[48]) - int(st[43])) / 100:.1f} us, solve "
+                  f"{(int(st[44]) - int(st[48])) / 100:.1f} us ({int(st[49])} x {int(st[50])}: {int(st[51])} free "
+                  f"rows, {int(st[52])} search steps)", file=sys.stderr)
     stats = eng.stats()
     if fam and len(engines) > 1:   # summed over the engines: the same totals as one engine of S
         for e_ in engines[1:]:

@@ -71,7 +71,10 @@ struct HsCounters {
     int err;
     int lap_done;                  // first round solved by k_hs_lap this frame
     LapStats ls;                   // cumulative solver counters
-    int pad[14];
+    int n_ud, n_ut, n_upd;         // k_hs_assoc -> k_hs_ocr -> k_hs_assoc_b: the OCR round's sizes
+    int ocr_nan;                   // the OCR matrix holds a NaN (its max is then NaN)
+    unsigned long long ocr_max;    // its maximum, order-preserving bits (hs_ord)
+    int pad[8];
 };
 static_assert(sizeof(HsCounters) == 128, "HsCounters layout");
 
@@ -672,12 +675,11 @@ __global__ __launch_bounds__(OC_T) void k_hs_assoc(HsArgs a) {
     unsigned char *gws = a.lap_ws + s * a.lap_ws_stride;
     const long long lds_bytes = oc_lds_bytes(a.CAP, a.MAXD);
     const double *din = a.det_in + (long long)a.det_off[s] * 6;
-    const int frame = c->frame + 1;
     int n_trk = c->n_trk;
     const int n_hi = c->n_high;
     const int dt = a.delta_t;
     int *list = a.list + tb;
-    double *cost = a.cost + mb, *emat = a.emat + mb;
+    double *cost = a.cost + mb;
     int *udet = a.udet + ub, *utrk = a.utrk + ub;
     int n_ud = 0, n_ut = 0;
     int n_corr = 0;
@@ -753,16 +755,113 @@ __global__ __launch_bounds__(OC_T) void k_hs_assoc(HsArgs a) {
     }
     block_sync();
     YTA_STAMP(3);
+    // the OCR round's matrix is filled chip-wide (k_hs_ocr); k_hs_assoc_b solves and finishes
+    if (t == 0) {
+        c->n_ud = n_ud;
+        c->n_ut = n_ut;
+        c->n_upd = n_upd;
+        c->corrections = n_corr;
+        c->ocr_nan = 0;
+        c->ocr_max = 0ull;
+    }
+}
+
+// Order-preserving bits of a double (larger value, larger bits), for the OCR matrix's maximum.
+__device__ __forceinline__ unsigned long long hs_ord(double v) {
+    const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+    return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+}
+__device__ __forceinline__ double hs_unord(unsigned long long o) {
+    const unsigned long long b = (o >> 63) ? (o & 0x7FFFFFFFFFFFFFFFull) : ~o;
+    return __longlong_as_double((long long)b);
+}
+
+// OCR round matrix (:512-542): asso_func(left dets, last observations) over the chip, one entry per
+// thread, with its maximum (np.max: NaN-propagating, ocr_nan) for k_hs_assoc_b.
+__global__ __launch_bounds__(256) void k_hs_ocr(HsArgs a) {
+    __shared__ OcShared sh;
+    const int s = blockIdx.y;
+    if (a.active && !a.active[s]) return;
+    HsCounters *c = a.cnt + s;
+    const int n_ud = c->n_ud, n_ut = c->n_ut;
+    if (n_ud <= 0 || n_ut <= 0) return;
+    const long long tb = (long long)s * a.CAP, db = (long long)s * a.MAXD, mb = hs_mb(a, s);
+    const long long ub = (long long)s * (a.MAXD + a.CAP);
+    const double *din = a.det_in + (long long)a.det_off[s] * 6;
+    const int *udet = a.udet + ub, *utrk = a.utrk + ub;
+    double *mat = a.emat + mb;   // the embedding costs are no longer needed
+    const long long nm = (long long)n_ud * n_ut;
+    double mx = -INFINITY;
+    bool bad = false, nan = false;
+    for (long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x; q < nm;
+         q += (long long)gridDim.x * blockDim.x) {
+        const int p = (int)(q / n_ut), k = (int)(q % n_ut);
+        const Box db_ = box5(din + (long long)a.hi_row[db + udet[p]] * 6);
+        const Box tb_ = box5(a.clast + (tb + utrk[k]) * 5);
+        const double v = asso_of(a.asso, db_, tb_, 0.0, 0.0);
+        bad |= a.asso == 1 && v != v;
+        nan |= v != v;
+        mat[q] = v;
+        if (v == v) mx = v > mx ? v : mx;
+    }
+    if (bad) atomicOr(&c->err, ERR_GIOU);
+    if (nan) atomicOr(&c->ocr_nan, 1);
+    mx = block_max(mx, sh);
+    if (threadIdx.x == 0 && mx > -INFINITY) atomicMax(&c->ocr_max, hs_ord(mx));
+}
+
+// The rest of the association after k_hs_ocr: the OCR round's solve (:512-542), misses, births,
+// outputs, removal (:544-570).
+__global__ __launch_bounds__(OC_T) void k_hs_assoc_b(HsArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    __shared__ OcShared sh;
+    const int s = blockIdx.x, t = threadIdx.x, nt = blockDim.x;
+    if (a.active && !a.active[s]) return;   // (k_hs_assoc reported no rows)
+    HsCounters *c = a.cnt + s;
+    const long long tb = (long long)s * a.CAP, db = (long long)s * a.MAXD, mb = hs_mb(a, s);
+    const long long ub = (long long)s * (a.MAXD + a.CAP);
+    unsigned char *gws = a.lap_ws + s * a.lap_ws_stride;
+    const long long lds_bytes = oc_lds_bytes(a.CAP, a.MAXD);
+    const double *din = a.det_in + (long long)a.det_off[s] * 6;
+    const int frame = c->frame + 1;
+    int n_trk = c->n_trk;
+    const int n_hi = c->n_high;
+    const int dt = a.delta_t;
+    int *list = a.list + tb;
+    double *emat = a.emat + mb;
+    int *udet = a.udet + ub, *utrk = a.utrk + ub;
+    int n_ud = 0, n_ut = 0;
+    int n_corr = 0;
+    // dets[p] (x1, y1, x2, y2, score) of kept detection p: input row hi_row[p]
+    auto hrow = [&](int p) { return din + (long long)a.hi_row[db + p] * 6; };
+    YTA_STAMP_BASE(40);
+    YTA_STAMP_BASE(40);
+    n_ud = c->n_ud;
+    n_ut = c->n_ut;
+    n_corr = c->corrections;
+    const int n_upd = c->n_upd;
+    const long long eb = (long long)s * (a.CAP + a.MAXD);
     // ---- OCR round (:512-542): asso_func(left dets, last observations), no feature update
     if (n_ud > 0 && n_ut > 0) {
-        double *mat = emat;   // the embedding costs are no longer needed
-        const double mx = asso_matrix(
-            a.asso, n_ud, n_ut, [&](int p) { return box5(hrow(udet[p])); },
-            [&](int k) { return box5(a.clast + (tb + utrk[k]) * 5); }, 0.0, 0.0, mat, lds, lds_bytes,
-            &c->err, sh);
+        double *mat = emat;   // filled by k_hs_ocr
+        const double mx = c->ocr_nan ? NAN : hs_unord(c->ocr_max);
+        YTA_STAMP(8);
+#ifdef YTA_STAMPS
+        const unsigned long long fr0 = g_stamps[100], st0 = g_stamps[101];
+        if (blockIdx.x == 0 && t == 0) {
+            g_stamps[49] = n_ud;
+            g_stamps[50] = n_ut;
+        }
+#endif
         if (mx > a.thr) {
             iou_lap(LapMat{mat, n_ud, n_ut, true}, a.rmatch + db, lds, lds_bytes, gws, &c->err, &c->ls,
                     a.lap_ws + (s + 1) * a.lap_ws_stride - tight_ws_bytes());
+#ifdef YTA_STAMPS
+            if (blockIdx.x == 0 && t == 0) {   // this solve's free rows and search steps
+                g_stamps[51] = g_stamps[100] - fr0;
+                g_stamps[52] = g_stamps[101] - st0;
+            }
+#endif
             for (int i = t; i < n_hi; i += nt) a.tmp[ub + i] = 0;
             for (int j = t; j < n_trk; j += nt) a.nan_flag[tb + j] = 0;
             block_sync();
@@ -1068,6 +1167,9 @@ int hs_alloc(yta_hybridsort *e) {
     YTA_HIP(hipFuncSetAttribute((const void *)k_hs_assoc,
                                 hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)dense_lap_ws_bytes(OC_LDS_LAP_N)));
+    YTA_HIP(hipFuncSetAttribute((const void *)k_hs_assoc_b,
+                                hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)dense_lap_ws_bytes(OC_LDS_LAP_N)));
     return YTA_OK;
 }
 
@@ -1128,6 +1230,11 @@ int hs_launch(yta_hybridsort *e, const double *d_dets, const int *d_off, const f
                        e->stream, a);
     YTA_HIP(hipGetLastError());
     hipLaunchKernelGGL(k_hs_assoc, dim3(a.S), dim3(OC_T), e->lds, e->stream, a);
+    YTA_HIP(hipGetLastError());
+    hipLaunchKernelGGL(k_hs_ocr, dim3((unsigned)std::max(4, 2048 / a.S), a.S), dim3(256), 0, e->stream,
+                       a);
+    YTA_HIP(hipGetLastError());
+    hipLaunchKernelGGL(k_hs_assoc_b, dim3(a.S), dim3(OC_T), e->lds, e->stream, a);
     YTA_HIP(hipGetLastError());
     const dim3 gj((a.CAP + a.MAXD + 3) / 4, a.S);
     hipLaunchKernelGGL(k_hs_ema, gj, dim3(256), 0, e->stream, a);

@@ -229,12 +229,15 @@ __device__ __forceinline__ double asso_matrix(int kind, int na, int nb, DB dbox,
         batched_for<4>(na, [&](int p) { return dbox(p); }, [&](int p, const Box &b) { bd[p] = b; });
         batched_for<4>(nb, [&](int k) { return tbox(k); }, [&](int k, const Box &b) { bt[k] = b; });
         block_sync();
-        for (long long q = t; q < nm; q += nt) {
-            const int p = (int)(q / nb), k = (int)(q % nb);
-            const double v = asso_of(kind, bd[p], bt[k], w, h);
-            bad |= kind == 1 && v != v;
-            mat[q] = v;
-            mx = np_max(mx, v);
+        for (int p = 0; p < na; ++p) {   // a row at a time: no index division per entry
+            const Box dp = bd[p];
+            double *row = mat + (long long)p * nb;
+            for (int k = t; k < nb; k += nt) {
+                const double v = asso_of(kind, dp, bt[k], w, h);
+                bad |= kind == 1 && v != v;
+                row[k] = v;
+                mx = np_max(mx, v);
+            }
         }
     } else {
         for (long long q = t; q < nm; q += nt) {
