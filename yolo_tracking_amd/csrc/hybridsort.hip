@@ -854,7 +854,7 @@ __global__ __launch_bounds__(OC_T) void k_hs_assoc_b(HsArgs a) {
         }
 #endif
         if (mx > a.thr) {
-            iou_lap(LapMat{mat, n_ud, n_ut, true}, a.rmatch + db, lds, lds_bytes, gws, &c->err, &c->ls,
+            iou_lap<1024>(LapMat{mat, n_ud, n_ut, true}, a.rmatch + db, lds, lds_bytes, gws, &c->err, &c->ls,
                     a.lap_ws + (s + 1) * a.lap_ws_stride - tight_ws_bytes());
 #ifdef YTA_STAMPS
             if (blockIdx.x == 0 && t == 0) {   // this solve's free rows and search steps

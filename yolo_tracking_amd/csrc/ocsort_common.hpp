@@ -115,6 +115,7 @@ __host__ __device__ inline long long oc_lds_bytes(long long CAP, long long MAXD)
 
 // Rectangular solve (lap_rect.hpp) of R; `tr`: R is the transposed view of an na-row problem, so
 // the solver's rows are the caller's columns.  rx[caller row] = caller column or -1.
+template <int MAXT = 256>
 __device__ __forceinline__ void rect_solve(const RectMat &R, const double *pu, const int *px,
                                            const double *ps2, bool tr, int na, int *rx,
                                            unsigned char *lds, long long lds_bytes,
@@ -132,7 +133,7 @@ __device__ __forceinline__ void rect_solve(const RectMat &R, const double *pu, c
             w.av_lds = 1;
         }
     }
-    const int rc = lap_rect(R, pu, px, ps2, w, rsh);
+    const int rc = lap_rect<MAXT>(R, pu, px, ps2, w, rsh);
     if (rc && t == 0) atomicOr(err, ERR_SOLVER);
     if (!tr) {
         for (int i = t; i < R.rows; i += nt) rx[i] = rc ? -1 : w.x[i];
@@ -256,6 +257,8 @@ __device__ __forceinline__ double asso_matrix(int kind, int na, int nb, DB dbox,
 // The -IoU rounds (BYTE / OCR: association.py:20-28 on -iou): only pairs with IoU >= threshold
 // survive and the leftover lists are re-sorted (np.setdiff1d), so any optimal solution gives the
 // reference's result: the rectangular solver in whichever orientation has rows <= columns.
+// MAXT > 256: the solver bodies inlined (a kernel that has the registers for them)
+template <int MAXT = 256>
 __device__ __forceinline__ void iou_lap(const LapMat &M, int *rx, unsigned char *lds,
                                         long long lds_bytes, unsigned char *gws, int *err,
                                         LapStats *ls, unsigned char *tws = nullptr) {
@@ -270,7 +273,7 @@ __device__ __forceinline__ void iou_lap(const LapMat &M, int *rx, unsigned char 
     // (no bidding rounds here: on the OCR matrices of the C5 run they cost more than they saved,
     // k_hs_assoc 465 -> 567 us, profiles/r04k_*)
     (void)tws;
-    rect_solve(R, nullptr, nullptr, nullptr, tr, M.na, rx, lds, lds_bytes, gws, err);
+    rect_solve<MAXT>(R, nullptr, nullptr, nullptr, tr, M.na, rx, lds, lds_bytes, gws, err);
 }
 
 // Is x, the solution of the transposed first-round problem (rows = trackers, all matched;
