@@ -228,6 +228,9 @@ def main():
             print(f"  OCR round: matrix {(int(st[48]) - int(st[43])) / 100:.1f} us, solve "
                   f"{(int(st[44]) - int(st[48])) / 100:.1f} us ({int(st[49])} x {int(st[50])}: {int(st[51])} free "
                   f"rows, {int(st[52])} search steps)", file=sys.stderr)
+            if st[104] >= st[48] and st[105] >= st[104]:   # lap_rect_body's stamps, last call
+                print(f"  OCR solve: pre-pass + claims {(int(st[104]) - int(st[48])) / 100:.1f} us, "
+                      f"searches {(int(st[105]) - int(st[104])) / 100:.1f} us", file=sys.stderr)
     stats = eng.stats()
     if fam and len(engines) > 1:   # summed over the engines: the same totals as one engine of S
         for e_ in engines[1:]:
