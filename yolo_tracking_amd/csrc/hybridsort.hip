@@ -810,6 +810,19 @@ __global__ __launch_bounds__(256) void k_hs_ocr(HsArgs a) {
     if (threadIdx.x == 0 && mx > -INFINITY) atomicMax(&c->ocr_max, hs_ord(mx));
 }
 
+// The OCR solve's row pre-pass over the grid (main_lap_pre, as k_hs_rowpre for the first round),
+// when the solve runs (max > thr).  The first round's pre-pass arrays are free by now.
+__global__ __launch_bounds__(OC_T) void k_hs_ocr_pre(HsArgs a) {
+    const int s = blockIdx.y;
+    if (a.active && !a.active[s]) return;
+    const HsCounters *c = a.cnt + s;
+    const int n_ud = c->n_ud, n_ut = c->n_ut;
+    if (n_ud <= 0 || n_ut <= 0 || c->ocr_nan || !(hs_unord(c->ocr_max) > a.thr)) return;
+    const long long db = (long long)s * a.MAXD;
+    main_lap_pre(a.emat + hs_mb(a, s), n_ud, n_ut, a.pre_u + db, a.pre_x + db, a.pre_s2 + db,
+                 true);   // the -IoU round solves -mat
+}
+
 // The rest of the association after k_hs_ocr: the OCR round's solve (:512-542), misses, births,
 // outputs, removal (:544-570).
 __global__ __launch_bounds__(OC_T) void k_hs_assoc_b(HsArgs a) {
@@ -855,7 +868,8 @@ __global__ __launch_bounds__(OC_T) void k_hs_assoc_b(HsArgs a) {
 #endif
         if (mx > a.thr) {
             iou_lap<1024>(LapMat{mat, n_ud, n_ut, true}, a.rmatch + db, lds, lds_bytes, gws, &c->err, &c->ls,
-                    a.lap_ws + (s + 1) * a.lap_ws_stride - tight_ws_bytes());
+                          a.lap_ws + (s + 1) * a.lap_ws_stride - tight_ws_bytes(), a.pre_u + db,
+                          a.pre_x + db, a.pre_s2 + db);   // row pre-pass: k_hs_ocr_pre
 #ifdef YTA_STAMPS
             if (blockIdx.x == 0 && t == 0) {   // this solve's free rows and search steps
                 g_stamps[51] = g_stamps[100] - fr0;
@@ -1234,6 +1248,13 @@ int hs_launch(yta_hybridsort *e, const double *d_dets, const int *d_off, const f
     hipLaunchKernelGGL(k_hs_ocr, dim3((unsigned)std::max(4, 2048 / a.S), a.S), dim3(256), 0, e->stream,
                        a);
     YTA_HIP(hipGetLastError());
+    {
+        const long long rows = (a.MAXD + OC_T / WAVE - 1) / (OC_T / WAVE);
+        const long long rcap = std::max<long long>(4, 4096 / a.S);
+        hipLaunchKernelGGL(k_hs_ocr_pre, dim3((unsigned)std::max<long long>(1, std::min(rows, rcap)), a.S),
+                           dim3(OC_T), 0, e->stream, a);
+        YTA_HIP(hipGetLastError());
+    }
     hipLaunchKernelGGL(k_hs_assoc_b, dim3(a.S), dim3(OC_T), e->lds, e->stream, a);
     YTA_HIP(hipGetLastError());
     const dim3 gj((a.CAP + a.MAXD + 3) / 4, a.S);

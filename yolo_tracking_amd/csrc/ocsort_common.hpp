@@ -165,12 +165,12 @@ __device__ __forceinline__ void main_lap(const LapMat &M, const double *pu, cons
 // problem (first_round_lap), i.e. the columns of mat: a block takes 64 tracker columns, lane =
 // column (coalesced across the wave), its waves split the detection rows, partials merged in LDS.
 __device__ __forceinline__ void main_lap_pre(const double *mat, int na, int nb, double *u, int *x,
-                                             double *s2) {
+                                             double *s2, bool neg = false) {   // neg: costs -mat
     if (na <= 0 || nb <= 0) return;
     const int nw = blockDim.x / WAVE;
     if (na <= nb) {
         if (nb > RECT_CPT_MAX * LAP_T) return;
-        const RectMat M{mat, na, nb, nb, 1, false};
+        const RectMat M{mat, na, nb, nb, 1, neg};
         for (int i = blockIdx.x * nw + threadIdx.x / WAVE; i < na; i += gridDim.x * nw)
             rect_row_pre(M, i, u, x, s2);
         return;
@@ -185,7 +185,7 @@ __device__ __forceinline__ void main_lap_pre(const double *mat, int na, int nb, 
         int k1 = INT_MAX;
         if (j < nb)
             for (int i = wid; i < na; i += nw) {   // ascending rows: strict < keeps the first
-                const double c = mat[(long long)i * nb + j];
+                const double c = neg ? -mat[(long long)i * nb + j] : mat[(long long)i * nb + j];
                 if (c < m1) { m2 = m1; m1 = c; k1 = i; }
                 else if (c < m2) m2 = c;
             }
@@ -258,10 +258,14 @@ __device__ __forceinline__ double asso_matrix(int kind, int na, int nb, DB dbox,
 // survive and the leftover lists are re-sorted (np.setdiff1d), so any optimal solution gives the
 // reference's result: the rectangular solver in whichever orientation has rows <= columns.
 // MAXT > 256: the solver bodies inlined (a kernel that has the registers for them)
+// pu / px / ps2: the solved orientation's row pre-pass (main_lap_pre) when a grid kernel ran it,
+// else nullptr (the block runs it).
 template <int MAXT = 256>
 __device__ __forceinline__ void iou_lap(const LapMat &M, int *rx, unsigned char *lds,
                                         long long lds_bytes, unsigned char *gws, int *err,
-                                        LapStats *ls, unsigned char *tws = nullptr) {
+                                        LapStats *ls, unsigned char *tws = nullptr,
+                                        const double *pu = nullptr, const int *px = nullptr,
+                                        const double *ps2 = nullptr) {
     const bool tr = M.na > M.nb;
     const int rows = tr ? M.nb : M.na, cols = tr ? M.na : M.nb;
     if (cols > RECT_CPT_MAX * (int)blockDim.x) {
@@ -273,7 +277,7 @@ __device__ __forceinline__ void iou_lap(const LapMat &M, int *rx, unsigned char 
     // (no bidding rounds here: on the OCR matrices of the C5 run they cost more than they saved,
     // k_hs_assoc 465 -> 567 us, profiles/r04k_*)
     (void)tws;
-    rect_solve<MAXT>(R, nullptr, nullptr, nullptr, tr, M.na, rx, lds, lds_bytes, gws, err);
+    rect_solve<MAXT>(R, pu, px, ps2, tr, M.na, rx, lds, lds_bytes, gws, err);
 }
 
 // Is x, the solution of the transposed first-round problem (rows = trackers, all matched;
