@@ -43,6 +43,12 @@ PHASES = ["s1_prep", "s1_edges", "s1_lap", "stage23", "apply", "finish"]
 STATS = ["dets", "high", "second", "pool", "act", "unc", "left", "rest", "births", "t2", "l2",
          "tracked", "lost", "out", "edges1", "edges23", "fallback1", "fallback23", "lazy", "res1",
          "fallback_f"]
+# yta_bytetrack_pipe_stats slots (bench reports them per frame, "frames" as the total)
+PIPE_STATS = ["frames", "in_direct_bytes", "in_staged_bytes", "out_direct_bytes", "out_staged_bytes",
+              "host_stage_in_ms", "host_submit_ms", "host_wait_ms", "host_copy_out_ms",
+              "gpu_in_ms", "gpu_kernels_ms", "gpu_out_ms", "gpu_span_ms", "host_h2d_call_ms",
+              "host_launch_ms", "host_d2h_call_ms", "host_small_h2d_ms", "host_small_d2h_ms",
+              "host_pinned_check_ms"]
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # Canonical algorithmic bytes per update: ByteTrack 1024 x 1024
 BYTES_PER_UPDATE_1024 = 19_259_392
@@ -165,6 +171,8 @@ def parse(argv=None):
                    help="engines (host threads) of the host-buffer leg")
     p.add_argument("--no-pcie-pinned", action="store_true",
                    help="skip the host-buffer leg's page-locked variant")
+    p.add_argument("--no-dropin", action="store_true", help="skip the one-stream drop-in leg")
+    p.add_argument("--no-configs", action="store_true", help="skip the configs C2-C5 legs")
     p.add_argument("--no-isolated", action="store_true",
                    help="skip the engine-0-alone frames after the timed region (profiling runs)")
     p.add_argument("--cpu-frames", type=int, default=40)
@@ -323,6 +331,14 @@ def cpu_baseline(n, frames, seed):
     return line
 
 
+def pinned_empty(shape, dtype):
+    """A page-locked host array (torch's pinned allocator), as a detector writing its boxes into
+    pinned memory would hand it over.  tools/pipe_probe.py swaps in other allocators."""
+    import torch
+    return torch.empty(shape, dtype=torch.float32 if dtype == np.float32 else torch.float64,
+                       pin_memory=True).numpy()
+
+
 def pcie_inclusive(frame_of, S, N, device, first, frames=8, engines=1, pinned=False):
     """The same workload through the host-buffer ABI (yta_bytetrack_update: packed host dets in,
     output rows back to the host every call, synchronous) on fresh engines, frames 0..first-1
@@ -347,7 +363,7 @@ def pcie_inclusive(frame_of, S, N, device, first, frames=8, engines=1, pinned=Fa
     def buf(shape):
         if not pinned:
             return np.empty(shape)
-        return torch.empty(shape, dtype=torch.float64, pin_memory=True).numpy()
+        return pinned_empty(shape, np.float64)
     for q in range(E):
         a, b = bounds[q], bounds[q + 1]
         # capacity 3N: the host path reserves ahead of need (tracked + lost + this frame's dets,
@@ -417,8 +433,7 @@ def pcie_pipelined(frame_of, S, N, device, first, frames=8, pinned=False, f32=Fa
     def buf(shape, dt=np.float64):
         if not pinned:
             return np.empty(shape, dtype=dt)
-        return torch.empty(shape, dtype=torch.float32 if dt == np.float32 else torch.float64,
-                           pin_memory=True).numpy()
+        return pinned_empty(shape, dt)
     offs = np.ascontiguousarray(np.arange(S + 1, dtype=np.int32) * N)
     in_dt = np.float32 if f32 else np.float64
     submit_fn = lib.yta_bytetrack_submit_f32 if f32 else lib.yta_bytetrack_submit
@@ -442,6 +457,7 @@ def pcie_pipelined(frame_of, S, N, device, first, frames=8, pinned=False, f32=Fa
         b = buf((S * N, 6), in_dt)
         b[:] = frame_of(f)
         timed.append(b)
+    _lib.check(lib.yta_bytetrack_pipe_stats(h, None, 0, 1))   # accounting from here
     t0 = time.perf_counter()
     for k, src in enumerate(timed):
         submit(src, first + k)
@@ -450,12 +466,82 @@ def pcie_pipelined(frame_of, S, N, device, first, frames=8, pinned=False, f32=Fa
     for _ in range(min(DEPTH - 1, len(timed))):
         collect()
     dt = (time.perf_counter() - t0) / frames
+    ps = (ctypes.c_double * len(PIPE_STATS))()
+    _lib.check(lib.yta_bytetrack_pipe_stats(h, ps, len(PIPE_STATS), 1))
+    nfr = max(ps[0], 1.0)
+    acct = {k: (ps[i] / nfr if i else ps[i]) for i, k in enumerate(PIPE_STATS)}
     eng.close()
     return {"value": S / dt, "unit": "calls/s", "steps": frames, "ms_per_step": 1000 * dt,
+            "per_frame": {k: round(v, 4) for k, v in acct.items()},
             "note": "pipelined host-buffer ABI (submit/collect, up to three frames in flight), "
                     f"{'page-locked' if pinned else 'pageable numpy'} caller buffers"
                     f"{', float32 detection rows' if f32 else ''}; "
                     "wall time of the timed loop / frames"}
+
+
+def dropin_leg(n, frames, seed, device):
+    """North star's per-stream claim: one camera stream through the reference's plugin surface,
+    exactly as examples/track.py:43-57 drives it - create_tracker('bytetrack', ...) then
+    tracker.update(dets, img) with NumPy in and out every call (float32 boxes, as ultralytics hands
+    them over; host -> device, kernels, device -> host inside every call).  Median over frames
+    2..frames.  Beside it in the line: the 1-core oracle on the same workload
+    (cpu_baseline)."""
+    from yolo_tracking_amd import create_tracker, get_tracker_config
+    from yolo_tracking_amd.synth import make_frames
+    fr = [d.astype(np.float32) for d, _ in make_frames(n, frames, seed)]
+    img = np.zeros((8, 8, 3), np.uint8)     # ignored by ByteTrack (byte_tracker.py:132)
+    t = create_tracker("bytetrack", get_tracker_config("bytetrack"), None, device, False, False)
+    dts, rows = [], 0
+    for d in fr:
+        t0 = time.perf_counter()
+        out = t.update(d, img)
+        dts.append(time.perf_counter() - t0)
+        rows = len(out)
+    med = float(np.median(dts[1:]))
+    return {"value": 1.0 / med, "unit": "calls/s", "median_ms": 1e3 * med,
+            "p90_ms": 1e3 * float(np.percentile(dts[1:], 90)), "frames": f"2..{frames}",
+            "rows_last_frame": rows,
+            "workload": f"bytetrack {n}x{n}, one stream, create_tracker + update(dets, img), "
+                        "float32 NumPy dets in, (K, 8) float64 NumPy rows out per call"}
+
+
+# configs 2-5 (BASELINE.json configs[1..4]) at their stated sizes, single GPU: tools/bench_tracker.py
+CONFIGS = [
+    ("C2", ["--tracker", "ocsort", "--n", "256", "--streams", "1", "--steps", "50"]),
+    ("C3", ["--tracker", "botsort", "--n", "1024", "--dim", "512", "--streams", "1",
+            "--steps", "30"]),
+    ("C4", ["--tracker", "deepocsort", "--n", "2048", "--dim", "512", "--streams", "1",
+            "--steps", "20"]),
+    ("C5", ["--tracker", "hybridsort", "--n", "4096", "--dim", "512", "--streams", "8",
+            "--steps", "8", "--warmup", "3"]),
+]
+
+
+def configs_leg():
+    """Configs C2-C5 on this GPU (tools/bench_tracker.py: inputs staged in HBM, the engines'
+    device-buffer entry points, timed frames between device syncs), each with its 1-core oracle
+    (started together beside the GPU legs, collected after).  C5 runs its per-GPU share of the
+    64-stream config: 8 streams in two engines."""
+    sys.path.insert(0, os.path.join(REPO, "tools"))
+    import bench_tracker as bt
+    todo = [(name, bt.parse(argv)) for name, argv in CONFIGS]
+    cpus = {name: bt.start_cpu_leg(a) for name, a in todo}
+    res = {}
+    for name, a in todo:
+        t0 = time.time()
+        try:
+            line = bt.run(a, cpu=cpus[name])
+        except Exception as exc:   # report, never fail the bench on a config leg
+            res[name] = {"value": None, "error": repr(exc)[:300]}
+            continue
+        cpu = line.get("cpu_baseline") or {}
+        res[name] = {"metric": line["metric"], "value": line["value"], "unit": "calls/s",
+                     "ms_per_step": line["ms_per_step"], "steps": line["steps"],
+                     "workload": line["config"]["workload"], "cpu_1core": cpu.get("value"),
+                     "cpu_sample": cpu.get("sample"),
+                     "vs_cpu_1core": (line["value"] / cpu["value"] if cpu.get("value") else None),
+                     "wall_s": round(time.time() - t0, 1)}
+    return res
 
 
 def run_dry(args, world, rank):
@@ -644,7 +730,6 @@ def main():
         # per-kernel figures above, summed, over the streams); SURVEY §8(d)'s canonical figure
         # charges a dense N x M cost matrix and a 576-B Kalman state, neither of which exists here
         impl_bytes = sum(kernel_bytes(p, st) for p in PHASES) / S
-        cpu = None if args.no_cpu_baseline else cpu_baseline(N, args.cpu_frames, args.seed)
         pcie = (None if args.no_pcie else
                 pcie_inclusive(frame_of, S, N, local_rank, first=min(PRE, FT - 8),
                                engines=args.pcie_engines))
@@ -661,6 +746,11 @@ def main():
                                                              first=min(PRE, FT - 8), pinned=True)
                 pcie["pipelined"]["pinned_f32"] = pcie_pipelined(
                     frame_of, S, N, local_rank, first=min(PRE, FT - 8), pinned=True, f32=True)
+        dropin = None if args.no_dropin else dropin_leg(N, 60, args.seed, f"cuda:{local_rank}")
+        configs = None if args.no_configs else configs_leg()
+        cpu = None if args.no_cpu_baseline else cpu_baseline(N, args.cpu_frames, args.seed)
+        if dropin is not None and cpu and cpu.get("value"):
+            dropin["vs_cpu_1core"] = dropin["value"] / cpu["value"]
         dk = traffic.get(PHASE_KERNEL[dom], {})
         line = {
             "metric": "tracker.update() calls/sec @ 1024 tracks×1024 dets; 1/2/4/8 MI355X",
@@ -710,6 +800,8 @@ def main():
                                      "kernels, so its event duration includes their share"})},
             "pcie_inclusive": pcie,
             "cpu_baseline": cpu,
+            "dropin": dropin,
+            "configs": configs,
             "per_kernel": per_kernel,
             "per_kernel_overlapped": overlapped,
             "frame_counts": st,

@@ -175,6 +175,10 @@ int yta_bytetrack_update(yta_bytetrack *engine, const double *dets, const int *d
 int yta_bytetrack_update_device(yta_bytetrack *engine, const double *d_dets,
                                 const int *d_det_offsets, double *d_out, int *d_out_counts);
 int yta_bytetrack_sync(yta_bytetrack *engine);      /* waits; reports device-side errors */
+/* The S per-stream ID counters on the device (waits): the last ID each stream issued, i.e. the
+ * reference's BaseTrack._count after that stream's frames (basetrack.py:37-40), for the
+ * device-buffer path where no host copy follows the frames. */
+int yta_bytetrack_next_ids(yta_bytetrack *engine, long long *next_id);
 
 /* Pipelined host-buffer update (ByteTrack engines): submit enqueues one frame of every stream and
  * returns at once; collect waits for the OLDEST submitted frame and reports it.  Up to three
@@ -194,6 +198,16 @@ int yta_bytetrack_sync(yta_bytetrack *engine);      /* waits; reports device-sid
 int yta_bytetrack_submit(yta_bytetrack *engine, const double *dets, const int *det_offsets,
                          const long long *next_id, double *out, int out_capacity);
 int yta_bytetrack_collect(yta_bytetrack *engine, long long *next_id, int *out_offsets);
+/* Accounting of the pipelined path since the last reset (n doubles, up to 19): frames collected;
+ * detection bytes DMA'd straight from the caller's page-locked buffer / staged through the
+ * engine's pinned buffers; output-row bytes DMA'd straight into the caller's buffer / staged;
+ * host milliseconds spent staging detections, inside submit, waiting in collect, copying staged
+ * rows out; GPU milliseconds (per frame, from its events, summed) of the copy-in, the kernels +
+ * row snapshot, the copy-out, and the frame's whole span (copy-in start to copy-out end); host
+ * milliseconds inside the direct copy-in call, the kernel launches and the copy-out call, the
+ * small offset copy in, the small counter / offset copies out, and the page-locked checks.
+ * reset != 0 zeroes the accounting after the read. */
+int yta_bytetrack_pipe_stats(yta_bytetrack *engine, double *stats, int n, int reset);
 /* float32 detections (ultralytics hands BoxMOT float32 boxes; the reference promotes them to
  * float64 exactly, byte_tracker.py:143): packed rows of 6 float32 cross PCIe at half the bytes and
  * are widened on the device, so every result equals the float64 call on the promoted rows.  Same

@@ -55,7 +55,7 @@ def cpu_leg(code, timeout=900):
         return {"error": str(exc)}
 
 
-def main():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--tracker", choices=["ocsort", "botsort", "deepocsort", "hybridsort"],
                    required=True)
@@ -71,7 +71,102 @@ def main():
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--cpu-frames", type=int, default=None)
     p.add_argument("--seed", type=int, default=2000)
-    args = p.parse_args()
+    return p.parse_args(argv)
+
+
+def cpu_code(args, N, D, cf):
+    """The oracle leg's script (one stream, one thread, frames 2..cf+1), or None."""
+    oc = args.tracker == "ocsort"
+    if cf == 0:
+        return None
+    if args.tracker == "deepocsort":
+        return ("import sys,time,json; sys.path.insert(0,%r)\n"
+                "import numpy as np\n"
+                "from oracle.deepocsort import DeepOCSortOracle\n"
+                "from yolo_tracking_amd.synth import make_frames, SyntheticStream\n"
+                "fr=make_frames(%d,%d,%d,emb_dim=%d,low_conf_frac=0.0)\n"
+                "sh=SyntheticStream(%d,%d,emb_dim=%d,low_conf_frac=0.0).img_shape\n"
+                "w=np.array(%r)\n"
+                "t=DeepOCSortOracle(**%r); t.update(fr[0][0],sh,fr[0][1]/np.linalg.norm(fr[0][1]),w)\n"
+                "t0=time.perf_counter()\n"
+                "for d,e in fr[1:]: t.update(d,sh,e/np.linalg.norm(e),w)\n"
+                "print(json.dumps({'frames':len(fr)-1,'seconds':time.perf_counter()-t0}))\n"
+                % (REPO, N, cf + 1, args.seed, D, N, args.seed, D, CMC_AFFINE, DEEPOCSORT_YAML))
+    if args.tracker == "hybridsort":
+        return ("import sys,time,json; sys.path.insert(0,%r)\n"
+                "import numpy as np\n"
+                "from oracle.hybridsort import HybridSortOracle\n"
+                "from yolo_tracking_amd.synth import make_frames\n"
+                "fr=make_frames(%d,%d,%d,emb_dim=%d,low_conf_frac=0.0)\n"
+                "t=HybridSortOracle(**%r); t.update(fr[0][0],fr[0][1]/np.linalg.norm(fr[0][1]))\n"
+                "t0=time.perf_counter()\n"
+                "for d,e in fr[1:]: t.update(d,e/np.linalg.norm(e))\n"
+                "print(json.dumps({'frames':len(fr)-1,'seconds':time.perf_counter()-t0}))\n"
+                % (REPO, N, cf + 1, args.seed, D, HYBRIDSORT_YAML))
+    if oc:
+        return ("import sys,time,json; sys.path.insert(0,%r)\n"
+                "from oracle.ocsort import OCSortOracle\n"
+                "from yolo_tracking_amd.synth import make_frames, SyntheticStream\n"
+                "fr=[d for d,_ in make_frames(%d,%d,%d,low_conf_frac=0.0)]\n"
+                "sh=SyntheticStream(%d,%d,low_conf_frac=0.0).img_shape\n"
+                "t=OCSortOracle(**%r); t.update(fr[0],sh)\n"
+                "t0=time.perf_counter()\n"
+                "for d in fr[1:]: t.update(d,sh)\n"
+                "print(json.dumps({'frames':len(fr)-1,'seconds':time.perf_counter()-t0}))\n"
+                % (REPO, N, cf + 1, args.seed, N, args.seed, OCSORT_YAML))
+    return ("import sys,time,json; sys.path.insert(0,%r)\n"
+            "import numpy as np\n"
+            "from oracle.botsort import BoTSORTOracle\n"
+            "from yolo_tracking_amd.synth import make_frames\n"
+            "fr=make_frames(%d,%d,%d,emb_dim=%d)\n"
+            "kw=%r\n"
+            "def rows(d,e):\n"
+            "    f=e[d[:,4]>kw['track_high_thresh']]; return f/np.linalg.norm(f)\n"
+            "t=BoTSORTOracle(**kw); t.update(fr[0][0],rows(*fr[0]))\n"
+            "t0=time.perf_counter()\n"
+            "for d,e in fr[1:]: t.update(d,rows(d,e))\n"
+            "print(json.dumps({'frames':len(fr)-1,'seconds':time.perf_counter()-t0}))\n"
+            % (REPO, N, cf + 1, args.seed, D, BOTSORT_YAML))
+
+
+def default_cpu_frames(args):
+    oc = args.tracker == "ocsort"
+    fam = args.tracker in ("deepocsort", "hybridsort")
+    return args.cpu_frames if args.cpu_frames is not None else (30 if oc else (2 if fam else 6))
+
+
+def start_cpu_leg(args):
+    """The oracle leg as a background process (bench.py runs it beside the GPU legs)."""
+    N = args.n or DEFAULT_N[args.tracker]
+    D = 0 if args.tracker == "ocsort" else args.dim
+    cf = default_cpu_frames(args)
+    code = cpu_code(args, N, D, cf)
+    if code is None:
+        return None, cf
+    env = dict(os.environ, OMP_NUM_THREADS="1", OPENBLAS_NUM_THREADS="1", MKL_NUM_THREADS="1")
+    return subprocess.Popen([sys.executable, "-c", code], env=env, stdout=subprocess.PIPE,
+                            stderr=subprocess.PIPE, text=True), cf
+
+
+def finish_cpu_leg(args, proc, cf, timeout=900):
+    N = args.n or DEFAULT_N[args.tracker]
+    if proc is None:
+        res = {"error": "skipped (--cpu-frames 0)"}
+    else:
+        try:
+            out, _ = proc.communicate(timeout=timeout)
+            res = json.loads(out.strip().splitlines()[-1])
+        except Exception as exc:
+            res = {"error": str(exc)}
+    return ({"value": res["frames"] / res["seconds"], "unit": "calls/s", "cores": 1, "kind": "port",
+             "sample": f"oracle {args.tracker} 1 stream {N}x{N}, frames 2..{cf + 1} of seed "
+                       f"{args.seed}, {res['seconds']:.1f} s, 1 thread"}
+            if "frames" in res else {"value": None, "sample": res.get("error")})
+
+
+def run(args, cpu=None):
+    """One config on the GPU -> its JSON line.  cpu: a (process, frames) pair from start_cpu_leg
+    to collect for the line's cpu_baseline (None: run the CPU leg here, after the GPU legs)."""
     import torch
     from yolo_tracking_amd import _lib
     from yolo_tracking_amd.synth import SyntheticStream, make_frames
@@ -238,63 +333,9 @@ def main():
                 if isinstance(v, (int, float)) and isinstance(stats.get(k), (int, float)):
                     stats[k] += v
     # CPU leg: the oracle on stream 0, 1 thread, bounded sample
-    cf = args.cpu_frames if args.cpu_frames is not None else (30 if oc else (2 if fam else 6))
-    if cf == 0:
-        code = None
-    elif args.tracker == "deepocsort":
-        code = ("import sys,time,json; sys.path.insert(0,%r)\n"
-                "import numpy as np\n"
-                "from oracle.deepocsort import DeepOCSortOracle\n"
-                "from yolo_tracking_amd.synth import make_frames, SyntheticStream\n"
-                "fr=make_frames(%d,%d,%d,emb_dim=%d,low_conf_frac=0.0)\n"
-                "sh=SyntheticStream(%d,%d,emb_dim=%d,low_conf_frac=0.0).img_shape\n"
-                "w=np.array(%r)\n"
-                "t=DeepOCSortOracle(**%r); t.update(fr[0][0],sh,fr[0][1]/np.linalg.norm(fr[0][1]),w)\n"
-                "t0=time.perf_counter()\n"
-                "for d,e in fr[1:]: t.update(d,sh,e/np.linalg.norm(e),w)\n"
-                "print(json.dumps({'frames':len(fr)-1,'seconds':time.perf_counter()-t0}))\n"
-                % (REPO, N, cf + 1, args.seed, D, N, args.seed, D, CMC_AFFINE, DEEPOCSORT_YAML))
-    elif args.tracker == "hybridsort":
-        code = ("import sys,time,json; sys.path.insert(0,%r)\n"
-                "import numpy as np\n"
-                "from oracle.hybridsort import HybridSortOracle\n"
-                "from yolo_tracking_amd.synth import make_frames\n"
-                "fr=make_frames(%d,%d,%d,emb_dim=%d,low_conf_frac=0.0)\n"
-                "t=HybridSortOracle(**%r); t.update(fr[0][0],fr[0][1]/np.linalg.norm(fr[0][1]))\n"
-                "t0=time.perf_counter()\n"
-                "for d,e in fr[1:]: t.update(d,e/np.linalg.norm(e))\n"
-                "print(json.dumps({'frames':len(fr)-1,'seconds':time.perf_counter()-t0}))\n"
-                % (REPO, N, cf + 1, args.seed, D, HYBRIDSORT_YAML))
-    elif oc:
-        code = ("import sys,time,json; sys.path.insert(0,%r)\n"
-                "from oracle.ocsort import OCSortOracle\n"
-                "from yolo_tracking_amd.synth import make_frames, SyntheticStream\n"
-                "fr=[d for d,_ in make_frames(%d,%d,%d,low_conf_frac=0.0)]\n"
-                "sh=SyntheticStream(%d,%d,low_conf_frac=0.0).img_shape\n"
-                "t=OCSortOracle(**%r); t.update(fr[0],sh)\n"
-                "t0=time.perf_counter()\n"
-                "for d in fr[1:]: t.update(d,sh)\n"
-                "print(json.dumps({'frames':len(fr)-1,'seconds':time.perf_counter()-t0}))\n"
-                % (REPO, N, cf + 1, args.seed, N, args.seed, OCSORT_YAML))
-    else:
-        code = ("import sys,time,json; sys.path.insert(0,%r)\n"
-                "import numpy as np\n"
-                "from oracle.botsort import BoTSORTOracle\n"
-                "from yolo_tracking_amd.synth import make_frames\n"
-                "fr=make_frames(%d,%d,%d,emb_dim=%d)\n"
-                "kw=%r\n"
-                "def rows(d,e):\n"
-                "    f=e[d[:,4]>kw['track_high_thresh']]; return f/np.linalg.norm(f)\n"
-                "t=BoTSORTOracle(**kw); t.update(fr[0][0],rows(*fr[0]))\n"
-                "t0=time.perf_counter()\n"
-                "for d,e in fr[1:]: t.update(d,rows(d,e))\n"
-                "print(json.dumps({'frames':len(fr)-1,'seconds':time.perf_counter()-t0}))\n"
-                % (REPO, N, cf + 1, args.seed, D, BOTSORT_YAML))
-    res = cpu_leg(code) if code else {"error": "skipped (--cpu-frames 0)"}
-    cpu = ({"value": res["frames"] / res["seconds"], "unit": "calls/s", "cores": 1, "kind": "port",
-            "sample": f"oracle {args.tracker} 1 stream {N}x{N}, frames 2..{cf + 1} of seed "
-                      f"{args.seed}, {res['seconds']:.1f} s, 1 thread"}
-           if "frames" in res else {"value": None, "sample": res.get("error")})
+    if cpu is None:
+        cpu = start_cpu_leg(args)
+    cpu = finish_cpu_leg(args, *cpu)
     line = {"metric": f"{args.tracker} tracker.update() calls/sec @ {N} tracks x {N} dets",
             "value": value, "unit": "calls/s", "n_gpus": 1, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": 1000 * el / args.steps,
@@ -303,7 +344,11 @@ def main():
                                    + f", {S} streams, inputs resident in HBM",
                        "streams": S, "queues": max(1, args.queues) if fam else 1},
             "cpu_baseline": cpu, "frame_counts": stats}
-    print(json.dumps(line))
+    return line
+
+
+def main():
+    print(json.dumps(run(parse())))
 
 
 if __name__ == "__main__":

@@ -123,6 +123,8 @@ _SIGS = {
     "yta_bytetrack_reset_stream": ([_P, _I], _I),
     "yta_bytetrack_submit": ([_P, _P, _P, _P, _P, _I], _I),
     "yta_bytetrack_collect": ([_P, _P, _P], _I),
+    "yta_bytetrack_pipe_stats": ([_P, _P, _I, _I], _I),
+    "yta_bytetrack_next_ids": ([_P, _P], _I),
     "yta_bytetrack_submit_f32": ([_P, _P, _P, _P, _P, _I], _I),
     "yta_bytetrack_update_f32": ([_P, _P, _P, _P, _P, _I, _P], _I),
     "yta_bytetrack_get_state": ([_P, _I, _P, _P, _P, _P], _I),

@@ -21,6 +21,7 @@
 //                             incl. the removed_stracks quirk (:257-265), duplicate removal
 //                             (:312-325) through a grid over the lost list, output rows (:270-281),
 //                             free-slot list
+#include <chrono>
 #include <algorithm>
 #include <cmath>
 #include <cstring>
@@ -2062,11 +2063,13 @@ __global__ __launch_bounds__(BLKF, 4) void k_finish(BtArgs a) {
 
 // Rebuild the free-slot list of every stream from its tracked + lost lists (after a reserve).
 // Host-buffer update: every stream's output rows (a.out + s * CAP * 8) packed back to back at the
-// prefix offsets, so one copy returns them.  Block per stream, 16-B pieces.
+// prefix offsets, so one copy returns them.  Block per stream, 16-B pieces.  Rows at or past
+// `limit` (the destination's capacity) are not written: the host compares the offsets with it.
 __global__ __launch_bounds__(256) void k_pack_out(const double *src, long long cap_rows,
-                                                   const int *off, double *dst) {
+                                                   const int *off, double *dst, long long limit) {
     const int s = blockIdx.x;
-    const long long n2 = (long long)(off[s + 1] - off[s]) * 4;   // double2 pieces
+    const long long end = min((long long)off[s + 1], limit);
+    const long long n2 = max(end - (long long)off[s], 0LL) * 4;   // double2 pieces
     const double2 *a = reinterpret_cast<const double2 *>(src + s * cap_rows * 8);
     double2 *b = reinterpret_cast<double2 *>(dst + (long long)off[s] * 8);
     for (long long k = threadIdx.x; k < n2; k += blockDim.x) b[k] = a[k];
@@ -2173,6 +2176,36 @@ __global__ void k_reset(BtArgs a, int s0) {
 using namespace yta;
 
 constexpr int PIPE_DEPTH = 3;   // frames in flight of the pipelined host-buffer update
+// yta_bytetrack_pipe_stats slots (include/yolo_tracking_amd.h): frames collected; detection
+// bytes DMA'd straight from the caller / staged through pinned buffers; row bytes DMA'd straight
+// into the caller / staged; host ms staging detections, in submit, waiting in collect, copying
+// rows out; GPU ms of the copy-in, the kernels (+ row snapshot), the copy-out (per frame, from
+// its events) and of a frame's whole span (copy-in start to copy-out end)
+enum {
+    PS_FRAMES, PS_IN_DIRECT, PS_IN_STAGED, PS_OUT_DIRECT, PS_OUT_STAGED, PS_STAGE_IN_MS,
+    PS_SUBMIT_MS, PS_WAIT_MS, PS_COPY_OUT_MS, PS_GPU_IN_MS, PS_GPU_KERN_MS, PS_GPU_OUT_MS,
+    PS_GPU_SPAN_MS, PS_H2D_CALL_MS, PS_LAUNCH_MS, PS_D2H_CALL_MS, PS_SMALL_H2D_MS, PS_SMALL_D2H_MS,
+    PS_PINNED_CHECK_MS, PS_N
+};
+static_assert(PS_N <= 24, "pstat holds 24 slots");
+// Direct copies of the pipelined path in pieces of YTA_PIPE_CHUNK_MB (0: one copy each way)
+static size_t pipe_chunk_bytes() {
+    static const size_t c = [] {
+        const char *v = getenv("YTA_PIPE_CHUNK_MB");
+        return v ? (size_t)atoi(v) << 20 : (size_t)0;
+    }();
+    return c;
+}
+static hipError_t copy_pieces(void *dst, const void *src, size_t bytes, hipMemcpyKind kind,
+                              hipStream_t st) {
+    const size_t ch = pipe_chunk_bytes() ? pipe_chunk_bytes() : bytes;
+    for (size_t o = 0; o < bytes; o += ch) {
+        const hipError_t e = hipMemcpyAsync((char *)dst + o, (const char *)src + o,
+                                            std::min(ch, bytes - o), kind, st);
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
 
 struct yta_bytetrack {
     int device = 0, S = 0, CAP = 0, MAXD = 0;
@@ -2204,6 +2237,9 @@ struct yta_bytetrack {
     bool bs_split = false;
     // stream-subset updates: the [S] mask on the device and its pinned staging
     int *d_active = nullptr, *h_active = nullptr;
+    // the engine's own [S * CAP][8] output rows (the host-buffer paths); a.out is whatever buffer
+    // the last launch wrote (the caller's on the device-buffer path)
+    double *out_own = nullptr;
     // pipelined host-buffer updates (yta_bytetrack_submit / _collect): PIPE_DEPTH frame slots, a
     // copy-in and a copy-out stream beside the compute stream
     struct PipeSlot {
@@ -2218,13 +2254,21 @@ struct yta_bytetrack {
         BtCounters *d_cnt = nullptr, *h_cnt = nullptr;      // counters after this frame
         long long *h_nid = nullptr;                  // next_id staging
         hipEvent_t in_done = nullptr, kern_done = nullptr, out_done = nullptr;
+        // timing events: the start of the slot's copy-in, kernels and copy-out (the *_done
+        // events above mark their ends), for yta_bytetrack_pipe_stats
+        hipEvent_t in_start = nullptr, kern_start = nullptr, out_start = nullptr;
         double *user_out = nullptr;                  // the caller's buffer
         long long rows_bound = 0;                    // det_offsets[S] of the frame
         bool direct_out = false;                     // DMA straight into user_out
+        long long in_bytes = 0;                      // detection bytes over the link
+        bool direct_in = false;                      // DMA straight from the caller's buffer
+        bool dirty = false;                          // an enqueue failed part way: wait first
     };
     PipeSlot pipe[PIPE_DEPTH];
     int pipe_head = 0, pipe_count = 0;
     hipStream_t s_in = nullptr, s_out = nullptr;
+    // pipelined-path accounting (yta_bytetrack_pipe_stats): PIPE_STATS doubles
+    double pstat[24] = {};
     // optional per-kernel timing with HIP events on the engine stream
     bool prof = false;
     std::vector<hipEvent_t> ev;
@@ -2400,6 +2444,7 @@ int bt_alloc(yta_bytetrack *e) {
     DALLOC(a.y2, S * MAXD);
     DALLOC(a.y3, S * MAXD);
     DALLOC(a.out, S * CAP * 8);
+    e->out_own = a.out;
     if (e->variant == VAR_BOTSORT) {
         DALLOC(a.cls_hist, S * CAP * CLS_K);
         if (e->D > 0) {
@@ -2636,6 +2681,7 @@ int reserve(yta_bytetrack *e, int cap, int maxd) {
     n->a.lds_bytes_l = e->a.lds_bytes_l;
     n->a.lds_bytes_e = e->a.lds_bytes_e;
     e->a = n->a;
+    e->out_own = n->out_own;
     e->d_warp = n->d_warp;
     e->d_warp_id = n->d_warp_id;
     e->h_off = n->h_off;
@@ -2889,7 +2935,7 @@ int update_host(yta_bytetrack *e, const double *dets, const int *det_offsets, co
                                e->stream));
         e->a.active = e->d_active;
     }
-    int rc = launch_pipeline(e, e->d_det_in, e->d_det_off, e->a.out, nullptr, e->d_feat_in);
+    int rc = launch_pipeline(e, e->d_det_in, e->d_det_off, e->out_own, nullptr, e->d_feat_in);
     e->a.active = nullptr;
     if (rc) return rc;
     // Small engines (every stream's worst-case rows <= 1 MiB, e.g. one camera stream): rows packed
@@ -2900,8 +2946,8 @@ int update_host(yta_bytetrack *e, const double *dets, const int *det_offsets, co
         if (rc) return rc;
         hipLaunchKernelGGL(k_out_offsets, dim3(1), dim3(64), 0, e->stream, e->a.cnt, S,
                            e->CAP, e->d_pack_off);
-        hipLaunchKernelGGL(k_pack_out, dim3(S), dim3(256), 0, e->stream, e->a.out,
-                           (long long)e->CAP, e->d_pack_off, e->d_pack);
+        hipLaunchKernelGGL(k_pack_out, dim3(S), dim3(256), 0, e->stream, e->out_own,
+                           (long long)e->CAP, e->d_pack_off, e->d_pack, e->pack_cap);
         YTA_HIP(hipGetLastError());
         YTA_HIP(hipMemcpyAsync(e->h_cnt, e->a.cnt, sizeof(BtCounters) * S, hipMemcpyDeviceToHost,
                                e->stream));
@@ -2945,8 +2991,8 @@ int update_host(yta_bytetrack *e, const double *dets, const int *det_offsets, co
         memcpy(e->h_pack_off, out_offsets, sizeof(int) * (S + 1));
         YTA_HIP(hipMemcpyAsync(e->d_pack_off, e->h_pack_off, sizeof(int) * (S + 1),
                                hipMemcpyHostToDevice, e->stream));
-        hipLaunchKernelGGL(k_pack_out, dim3(S), dim3(256), 0, e->stream, e->a.out,
-                           (long long)e->CAP, e->d_pack_off, e->d_pack);
+        hipLaunchKernelGGL(k_pack_out, dim3(S), dim3(256), 0, e->stream, e->out_own,
+                           (long long)e->CAP, e->d_pack_off, e->d_pack, e->pack_cap);
         YTA_HIP(hipGetLastError());
         const size_t bytes = sizeof(double) * 8 * rows, ch = stage_chunk(bytes);
         if (host_pinned(out, bytes)) {   // straight into the caller's buffer
@@ -3048,7 +3094,8 @@ void pipe_free(yta_bytetrack *e) {
         for (void *h : {(void *)p.h_in, (void *)p.h_off, (void *)p.h_pack, (void *)p.h_pack_off,
                         (void *)p.h_cnt, (void *)p.h_nid, (void *)p.h_in32})
             if (h) (void)hipHostFree(h);
-        for (hipEvent_t ev : {p.in_done, p.kern_done, p.out_done})
+        for (hipEvent_t ev : {p.in_done, p.kern_done, p.out_done, p.in_start, p.kern_start,
+                              p.out_start})
             if (ev) (void)hipEventDestroy(ev);
         p = yta_bytetrack::PipeSlot{};
     }
@@ -3066,8 +3113,9 @@ int pipe_slot_ready(yta_bytetrack *e, yta_bytetrack::PipeSlot &p, long long dets
         YTA_HIP(hipStreamCreateWithFlags(&e->s_out, hipStreamNonBlocking));
     }
     if (!p.in_done) {
-        for (hipEvent_t *ev : {&p.in_done, &p.kern_done, &p.out_done})
-            YTA_HIP(hipEventCreateWithFlags(ev, hipEventDisableTiming));
+        for (hipEvent_t *ev : {&p.in_done, &p.kern_done, &p.out_done, &p.in_start, &p.kern_start,
+                               &p.out_start})
+            YTA_HIP(hipEventCreateWithFlags(ev, hipEventDefault));
         YTA_HIP(hipMalloc((void **)&p.d_off, sizeof(int) * (S + 1)));
         YTA_HIP(hipHostMalloc((void **)&p.h_off, sizeof(int) * (S + 1), hipHostMallocDefault));
         YTA_HIP(hipMalloc((void **)&p.d_pack_off, sizeof(int) * (S + 1)));
@@ -3092,6 +3140,117 @@ int pipe_slot_ready(yta_bytetrack *e, yta_bytetrack::PipeSlot &p, long long dets
                               hipHostMallocDefault));
         p.in_cap = p.pack_cap = cap;
     }
+    return YTA_OK;
+}
+
+// The frame's copy-in (s_in), kernels + row snapshot (compute stream) and copy-out (s_out).
+int pipe_enqueue(yta_bytetrack *e, yta_bytetrack::PipeSlot &p, const double *dets,
+                 const int *det_offsets, const long long *next_id, double *out, long long total,
+                 const float *dets32) {
+    const int S = e->S;
+    int rc = YTA_OK;
+    // this slot's last frame was collected (its events completed): its buffers are free
+    YTA_HIP(hipEventRecord(p.in_start, e->s_in));
+    memcpy(p.h_off, det_offsets, sizeof(int) * (S + 1));
+    auto ts = std::chrono::steady_clock::now();
+    YTA_HIP(hipMemcpyAsync(p.d_off, p.h_off, sizeof(int) * (S + 1), hipMemcpyHostToDevice,
+                           e->s_in));
+    e->pstat[PS_SMALL_H2D_MS] += std::chrono::duration<double, std::milli>(
+                                     std::chrono::steady_clock::now() - ts)
+                                     .count();
+    p.direct_in = false;
+    p.in_bytes = 0;
+    if (total && dets32) {   // float32 rows: half the bytes over the link, widened on the device
+        p.in_bytes = (long long)sizeof(float) * 6 * total;
+        p.direct_in = host_pinned(dets32, (size_t)p.in_bytes);
+        rc = stage_f32(e, dets32, 6 * total, &p.d_in32, &p.h_in32, &p.in32_cap, e->s_in);
+        if (rc) return rc;
+    } else if (total) {
+        const size_t bytes = sizeof(double) * 6 * total;
+        p.in_bytes = (long long)bytes;
+        ts = std::chrono::steady_clock::now();
+        const bool pinned_in = host_pinned(dets, bytes);
+        e->pstat[PS_PINNED_CHECK_MS] += std::chrono::duration<double, std::milli>(
+                                            std::chrono::steady_clock::now() - ts)
+                                            .count();
+        if (pinned_in) {   // straight from the caller (kept until collected)
+            p.direct_in = true;
+            const auto t0 = std::chrono::steady_clock::now();
+            YTA_HIP(copy_pieces(p.d_in, dets, bytes, hipMemcpyHostToDevice, e->s_in));
+            e->pstat[PS_H2D_CALL_MS] += std::chrono::duration<double, std::milli>(
+                                            std::chrono::steady_clock::now() - t0)
+                                            .count();
+        } else {   // staged: chunk k's DMA overlaps chunk k+1's host copy
+            const auto t0 = std::chrono::steady_clock::now();
+            const size_t ch = stage_chunk(bytes);
+            for (size_t o = 0; o < bytes; o += ch) {
+                const size_t n = std::min(ch, bytes - o);
+                par_copy(e, (char *)p.h_in + o, (const char *)dets + o, n);
+                YTA_HIP(hipMemcpyAsync((char *)p.d_in + o, (char *)p.h_in + o, n,
+                                       hipMemcpyHostToDevice, e->s_in));
+            }
+            e->pstat[PS_STAGE_IN_MS] += std::chrono::duration<double, std::milli>(
+                                            std::chrono::steady_clock::now() - t0)
+                                            .count();
+        }
+    }
+    e->pstat[p.direct_in ? PS_IN_DIRECT : PS_IN_STAGED] += (double)p.in_bytes;
+    YTA_HIP(hipEventRecord(p.in_done, e->s_in));
+    // compute stream: the frame, then its rows and counters snapshotted into the slot
+    YTA_HIP(hipStreamWaitEvent(e->stream, p.in_done, 0));
+    YTA_HIP(hipEventRecord(p.kern_start, e->stream));
+    if (next_id) {
+        memcpy(p.h_nid, next_id, sizeof(long long) * S);
+        YTA_HIP(hipMemcpy2DAsync(&e->a.cnt[0].next_id, sizeof(BtCounters), p.h_nid,
+                                 sizeof(long long), sizeof(long long), S, hipMemcpyHostToDevice,
+                                 e->stream));
+    }
+    if (total && dets32) {
+        rc = widen_f32(p.d_in32, p.d_in, 6 * total, e->stream);
+        if (rc) return rc;
+    }
+    const auto tl = std::chrono::steady_clock::now();
+    rc = launch_pipeline(e, p.d_in, p.d_off, e->out_own, nullptr);
+    if (rc) return rc;
+    e->pstat[PS_LAUNCH_MS] += std::chrono::duration<double, std::milli>(
+                                  std::chrono::steady_clock::now() - tl)
+                                  .count();
+    hipLaunchKernelGGL(k_out_offsets_scan, dim3(1), dim3(OFFS_T), 0, e->stream, e->a.cnt, S,
+                       e->CAP, p.d_pack_off);
+    hipLaunchKernelGGL(k_pack_out, dim3(S), dim3(256), 0, e->stream, e->out_own, (long long)e->CAP,
+                       p.d_pack_off, p.d_pack, p.pack_cap);
+    YTA_HIP(hipGetLastError());
+    YTA_HIP(hipMemcpyAsync(p.d_cnt, e->a.cnt, sizeof(BtCounters) * S, hipMemcpyDeviceToDevice,
+                           e->stream));
+    YTA_HIP(hipEventRecord(p.kern_done, e->stream));
+    // copy-out stream: counters, offsets and at most det_offsets[S] rows (every output row is a
+    // track matched to or born from one of the frame's detections)
+    YTA_HIP(hipStreamWaitEvent(e->s_out, p.kern_done, 0));
+    YTA_HIP(hipEventRecord(p.out_start, e->s_out));
+    ts = std::chrono::steady_clock::now();
+    YTA_HIP(hipMemcpyAsync(p.h_cnt, p.d_cnt, sizeof(BtCounters) * S, hipMemcpyDeviceToHost,
+                           e->s_out));
+    YTA_HIP(hipMemcpyAsync(p.h_pack_off, p.d_pack_off, sizeof(int) * (S + 1),
+                           hipMemcpyDeviceToHost, e->s_out));
+    e->pstat[PS_SMALL_D2H_MS] += std::chrono::duration<double, std::milli>(
+                                     std::chrono::steady_clock::now() - ts)
+                                     .count();
+    p.user_out = out;
+    p.rows_bound = total;
+    ts = std::chrono::steady_clock::now();
+    p.direct_out = total > 0 && host_pinned(out, sizeof(double) * 8 * total);
+    e->pstat[PS_PINNED_CHECK_MS] += std::chrono::duration<double, std::milli>(
+                                        std::chrono::steady_clock::now() - ts)
+                                        .count();
+    if (total) {
+        const auto t0 = std::chrono::steady_clock::now();
+        YTA_HIP(copy_pieces(p.direct_out ? out : p.h_pack, p.d_pack, sizeof(double) * 8 * total,
+                            hipMemcpyDeviceToHost, e->s_out));
+        e->pstat[PS_D2H_CALL_MS] += std::chrono::duration<double, std::milli>(
+                                        std::chrono::steady_clock::now() - t0)
+                                        .count();
+    }
+    YTA_HIP(hipEventRecord(p.out_done, e->s_out));
     return YTA_OK;
 }
 
@@ -3138,66 +3297,22 @@ int pipe_submit(yta_bytetrack *e, const double *dets, const int *det_offsets,
         }
     }
     auto &p = e->pipe[(e->pipe_head + e->pipe_count) % PIPE_DEPTH];
+    if (p.dirty) {   // a failed submit may have left copies from this slot's buffers queued
+        YTA_HIP(hipStreamSynchronize(e->s_in));
+        YTA_HIP(hipStreamSynchronize(e->stream));
+        YTA_HIP(hipStreamSynchronize(e->s_out));
+        p.dirty = false;
+    }
     int rc = pipe_slot_ready(e, p, total);
     if (rc) return rc;
-    // this slot's last frame was collected (its events completed): its buffers are free
-    memcpy(p.h_off, det_offsets, sizeof(int) * (S + 1));
-    YTA_HIP(hipMemcpyAsync(p.d_off, p.h_off, sizeof(int) * (S + 1), hipMemcpyHostToDevice,
-                           e->s_in));
-    if (total && dets32) {   // float32 rows: half the bytes over the link, widened on the device
-        rc = stage_f32(e, dets32, 6 * total, &p.d_in32, &p.h_in32, &p.in32_cap, e->s_in);
-        if (rc) return rc;
-    } else if (total) {
-        const size_t bytes = sizeof(double) * 6 * total;
-        if (host_pinned(dets, bytes)) {   // straight from the caller (kept until collected)
-            YTA_HIP(hipMemcpyAsync(p.d_in, dets, bytes, hipMemcpyHostToDevice, e->s_in));
-        } else {   // staged: chunk k's DMA overlaps chunk k+1's host copy
-            const size_t ch = stage_chunk(bytes);
-            for (size_t o = 0; o < bytes; o += ch) {
-                const size_t n = std::min(ch, bytes - o);
-                par_copy(e, (char *)p.h_in + o, (const char *)dets + o, n);
-                YTA_HIP(hipMemcpyAsync((char *)p.d_in + o, (char *)p.h_in + o, n,
-                                       hipMemcpyHostToDevice, e->s_in));
-            }
-        }
+    const auto t0 = std::chrono::steady_clock::now();
+    rc = pipe_enqueue(e, p, dets, det_offsets, next_id, out, total, dets32);
+    if (rc) {   // copies from the slot's pinned staging may be in flight: the next use waits
+        p.dirty = true;
+        return rc;
     }
-    YTA_HIP(hipEventRecord(p.in_done, e->s_in));
-    // compute stream: the frame, then its rows and counters snapshotted into the slot
-    YTA_HIP(hipStreamWaitEvent(e->stream, p.in_done, 0));
-    if (next_id) {
-        memcpy(p.h_nid, next_id, sizeof(long long) * S);
-        YTA_HIP(hipMemcpy2DAsync(&e->a.cnt[0].next_id, sizeof(BtCounters), p.h_nid,
-                                 sizeof(long long), sizeof(long long), S, hipMemcpyHostToDevice,
-                                 e->stream));
-    }
-    if (total && dets32) {
-        rc = widen_f32(p.d_in32, p.d_in, 6 * total, e->stream);
-        if (rc) return rc;
-    }
-    rc = launch_pipeline(e, p.d_in, p.d_off, e->a.out, nullptr);
-    if (rc) return rc;
-    hipLaunchKernelGGL(k_out_offsets_scan, dim3(1), dim3(OFFS_T), 0, e->stream, e->a.cnt, S,
-                       e->CAP, p.d_pack_off);
-    hipLaunchKernelGGL(k_pack_out, dim3(S), dim3(256), 0, e->stream, e->a.out, (long long)e->CAP,
-                       p.d_pack_off, p.d_pack);
-    YTA_HIP(hipGetLastError());
-    YTA_HIP(hipMemcpyAsync(p.d_cnt, e->a.cnt, sizeof(BtCounters) * S, hipMemcpyDeviceToDevice,
-                           e->stream));
-    YTA_HIP(hipEventRecord(p.kern_done, e->stream));
-    // copy-out stream: counters, offsets and at most det_offsets[S] rows (every output row is a
-    // track matched to or born from one of the frame's detections)
-    YTA_HIP(hipStreamWaitEvent(e->s_out, p.kern_done, 0));
-    YTA_HIP(hipMemcpyAsync(p.h_cnt, p.d_cnt, sizeof(BtCounters) * S, hipMemcpyDeviceToHost,
-                           e->s_out));
-    YTA_HIP(hipMemcpyAsync(p.h_pack_off, p.d_pack_off, sizeof(int) * (S + 1),
-                           hipMemcpyDeviceToHost, e->s_out));
-    p.user_out = out;
-    p.rows_bound = total;
-    p.direct_out = total > 0 && host_pinned(out, sizeof(double) * 8 * total);
-    if (total)
-        YTA_HIP(hipMemcpyAsync(p.direct_out ? out : p.h_pack, p.d_pack, sizeof(double) * 8 * total,
-                               hipMemcpyDeviceToHost, e->s_out));
-    YTA_HIP(hipEventRecord(p.out_done, e->s_out));
+    e->pstat[PS_SUBMIT_MS] +=
+        std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     ++e->pipe_count;
     return YTA_OK;
 }
@@ -3209,7 +3324,23 @@ int pipe_collect(yta_bytetrack *e, long long *next_id, int *out_offsets) {
     auto &p = e->pipe[e->pipe_head];
     e->pipe_head = (e->pipe_head + 1) % PIPE_DEPTH;
     --e->pipe_count;
+    const auto t0 = std::chrono::steady_clock::now();
     YTA_HIP(hipEventSynchronize(p.out_done));
+    const auto t1 = std::chrono::steady_clock::now();
+    e->pstat[PS_WAIT_MS] += std::chrono::duration<double, std::milli>(t1 - t0).count();
+    {   // the frame's GPU-side phases from its events (all complete)
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, p.in_start, p.in_done) == hipSuccess)
+            e->pstat[PS_GPU_IN_MS] += ms;
+        if (hipEventElapsedTime(&ms, p.kern_start, p.kern_done) == hipSuccess)
+            e->pstat[PS_GPU_KERN_MS] += ms;
+        if (hipEventElapsedTime(&ms, p.out_start, p.out_done) == hipSuccess)
+            e->pstat[PS_GPU_OUT_MS] += ms;
+        if (hipEventElapsedTime(&ms, p.in_start, p.out_done) == hipSuccess)
+            e->pstat[PS_GPU_SPAN_MS] += ms;
+        (void)hipGetLastError();
+    }
+    e->pstat[PS_FRAMES] += 1;
     const int S = e->S;
     memcpy(e->h_cnt, p.h_cnt, sizeof(BtCounters) * S);   // the latest known counters
     if (next_id)
@@ -3220,8 +3351,13 @@ int pipe_collect(yta_bytetrack *e, long long *next_id, int *out_offsets) {
     const long long rows = out_offsets[S];
     YTA_CHECK(rows <= p.rows_bound, YTA_ERR_HIP, "%lld output rows > %lld detections", rows,
               p.rows_bound);
-    if (rows > 0 && !p.direct_out)
+    e->pstat[p.direct_out ? PS_OUT_DIRECT : PS_OUT_STAGED] += 64.0 * (double)rows;
+    if (rows > 0 && !p.direct_out) {
         par_copy(e, p.user_out, p.h_pack, sizeof(double) * 8 * rows);
+        e->pstat[PS_COPY_OUT_MS] += std::chrono::duration<double, std::milli>(
+                                        std::chrono::steady_clock::now() - t1)
+                                        .count();
+    }
     return YTA_OK;
 }
 
@@ -3335,6 +3471,7 @@ int yta_bytetrack_update(yta_bytetrack *e, const double *dets, const int *det_of
 int yta_bytetrack_update_device(yta_bytetrack *e, const double *d_dets, const int *d_det_offsets,
                                 double *d_out, int *d_out_counts) {
     YTA_CHECK(e && d_det_offsets && d_out, YTA_ERR_INVALID, "null argument");
+    YTA_CHECK(e->pipe_count == 0, YTA_ERR_INVALID, "pipelined frames in flight: collect them first");
     return launch_pipeline(e, d_dets, d_det_offsets, d_out, d_out_counts);
 }
 
@@ -3349,6 +3486,7 @@ int yta_bytetrack_update_device_masked(yta_bytetrack *e, const int *d_active,
                                        const double *d_dets, const int *d_det_offsets,
                                        double *d_out, int *d_out_counts) {
     YTA_CHECK(e && d_det_offsets && d_out, YTA_ERR_INVALID, "null argument");
+    YTA_CHECK(e->pipe_count == 0, YTA_ERR_INVALID, "pipelined frames in flight: collect them first");
     e->a.active = d_active;
     const int rc = launch_pipeline(e, d_dets, d_det_offsets, d_out, d_out_counts);
     e->a.active = nullptr;
@@ -3376,8 +3514,27 @@ int yta_bytetrack_collect(yta_bytetrack *e, long long *next_id, int *out_offsets
     return pipe_collect(e, next_id, out_offsets);
 }
 
+int yta_bytetrack_pipe_stats(yta_bytetrack *e, double *stats, int n, int reset) {
+    YTA_CHECK(e && (stats || n == 0), YTA_ERR_INVALID, "null argument");
+    for (int k = 0; k < n; ++k) stats[k] = k < PS_N ? e->pstat[k] : 0.0;
+    if (reset)
+        for (double &v : e->pstat) v = 0.0;
+    return YTA_OK;
+}
+
+int yta_bytetrack_next_ids(yta_bytetrack *e, long long *next_id) {
+    YTA_CHECK(e && next_id, YTA_ERR_INVALID, "null argument");
+    YTA_CHECK(e->pipe_count == 0, YTA_ERR_INVALID, "pipelined frames in flight: collect them first");
+    YTA_HIP(hipSetDevice(e->device));
+    const int rc = read_counters(e);
+    if (rc) return rc;
+    for (int s = 0; s < e->S; ++s) next_id[s] = e->h_cnt[s].next_id;
+    return YTA_OK;
+}
+
 int yta_bytetrack_sync(yta_bytetrack *e) {
     YTA_CHECK(e, YTA_ERR_INVALID, "null engine");
+    YTA_CHECK(e->pipe_count == 0, YTA_ERR_INVALID, "pipelined frames in flight: collect them first");
     const int rc = read_counters(e);
     if (rc) return rc;
     return check_errors(e);
@@ -3387,6 +3544,7 @@ int yta_bytetrack_get_state(yta_bytetrack *e, int stream, int *n_tracks, long lo
                             double *mean, double *cov) {
     YTA_CHECK(e && n_tracks && ints && mean && cov, YTA_ERR_INVALID, "null argument");
     YTA_CHECK(stream >= 0 && stream < e->S, YTA_ERR_INVALID, "bad stream %d", stream);
+    YTA_CHECK(e->pipe_count == 0, YTA_ERR_INVALID, "pipelined frames in flight: collect them first");
     YTA_HIP(hipSetDevice(e->device));
     const int rc = read_counters(e);
     if (rc) return rc;
