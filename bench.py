@@ -48,7 +48,7 @@ PIPE_STATS = ["frames", "in_direct_bytes", "in_staged_bytes", "out_direct_bytes"
               "host_stage_in_ms", "host_submit_ms", "host_wait_ms", "host_copy_out_ms",
               "gpu_in_ms", "gpu_kernels_ms", "gpu_out_ms", "gpu_span_ms", "host_h2d_call_ms",
               "host_launch_ms", "host_d2h_call_ms", "host_small_h2d_ms", "host_small_d2h_ms",
-              "host_pinned_check_ms"]
+              "host_pinned_check_ms", "capacity_waits", "capacity_drains"]
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # Canonical algorithmic bytes per update: ByteTrack 1024 x 1024
 BYTES_PER_UPDATE_1024 = 19_259_392
@@ -437,7 +437,9 @@ def pcie_pipelined(frame_of, S, N, device, first, frames=8, pinned=False, f32=Fa
     offs = np.ascontiguousarray(np.arange(S + 1, dtype=np.int32) * N)
     in_dt = np.float32 if f32 else np.float64
     submit_fn = lib.yta_bytetrack_submit_f32 if f32 else lib.yta_bytetrack_submit
-    DEPTH = 3   # frames in flight (csrc/bytetrack.hip PIPE_DEPTH)
+    # frames in flight (csrc/bytetrack.hip PIPE_DEPTH; YTA_PIPE_DEPTH names a -DYTA_PIPE_DEPTH
+    # variant library's depth for A/B runs)
+    DEPTH = int(os.environ.get("YTA_PIPE_DEPTH", "3"))
     outs = [buf((S * N, 8)) for _ in range(DEPTH)]
     out_off = np.zeros(S + 1, np.int32)
     stage = buf((S * N, 6), in_dt)

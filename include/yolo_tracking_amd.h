@@ -198,14 +198,16 @@ int yta_bytetrack_next_ids(yta_bytetrack *engine, long long *next_id);
 int yta_bytetrack_submit(yta_bytetrack *engine, const double *dets, const int *det_offsets,
                          const long long *next_id, double *out, int out_capacity);
 int yta_bytetrack_collect(yta_bytetrack *engine, long long *next_id, int *out_offsets);
-/* Accounting of the pipelined path since the last reset (n doubles, up to 19): frames collected;
+/* Accounting of the pipelined path since the last reset (n doubles, up to 21): frames collected;
  * detection bytes DMA'd straight from the caller's page-locked buffer / staged through the
  * engine's pinned buffers; output-row bytes DMA'd straight into the caller's buffer / staged;
  * host milliseconds spent staging detections, inside submit, waiting in collect, copying staged
  * rows out; GPU milliseconds (per frame, from its events, summed) of the copy-in, the kernels +
  * row snapshot, the copy-out, and the frame's whole span (copy-in start to copy-out end); host
  * milliseconds inside the direct copy-in call, the kernel launches and the copy-out call, the
- * small offset copy in, the small counter / offset copies out, and the page-locked checks.
+ * small offset copy in, the small counter / offset copies out (0: the kernels store them), and
+ * the page-locked checks; the submits that waited for the newest frame's kernels to bound the
+ * track capacity, and the submits that drained the pipeline to check or grow it.
  * reset != 0 zeroes the accounting after the read. */
 int yta_bytetrack_pipe_stats(yta_bytetrack *engine, double *stats, int n, int reset);
 /* float32 detections (ultralytics hands BoxMOT float32 boxes; the reference promotes them to

@@ -175,7 +175,7 @@ def test_botsort_multistream_matches_oracle():
 def test_split_stage1_equals_fused(monkeypatch, crowd):
     """Stage 1 with ReID as three launches (k_bs_prep / k_bs_edges chip-wide / k_bs_lap, the
     default for few streams) against the fused k_stage1 (YTA_BS_SPLIT=0): identical rows, states
-    and features every frame.  crowd: objects packed 8x denser than the generator's default, so
+    features and frame counters every frame.  crowd: objects packed 8x denser than the generator's default, so
     pool rows with more than E_SLOTS candidate edges send k_bs_lap down the fused association."""
     from test_oracle_golden import reid_features
     from yolo_tracking_amd.synth import make_frames
@@ -195,6 +195,11 @@ def test_split_stage1_equals_fused(monkeypatch, crowd):
         a = engs["1"].update([dets], [feats])[0]
         b = engs["0"].update([dets], [feats])[0]
         assert np.array_equal(a, b), f
+        # the frame's counters mean the same in both paths (the LDS-fallback counts aside: the
+        # two association bodies size their arenas differently)
+        sta, stb = engs["1"].stats(), engs["0"].stats()
+        sta.pop("fallback1"), stb.pop("fallback1")
+        assert sta == stb, (f, sta, stb)
     sa, sb = engs["1"].state(0), engs["0"].state(0)
     assert all(np.array_equal(sa[k], sb[k]) for k in sa)
     assert np.array_equal(engs["1"].features(0)[0], engs["0"].features(0)[0])

@@ -28,7 +28,20 @@ def test_subset_result_back_in_caller_order():
     e._out = np.arange(5 * 8, dtype=np.float64).reshape(5, 8)
     o = np.array([0, 2, 5], np.int32)           # stream 1: rows 0-1, stream 4: rows 2-4
     nid_user = np.zeros(2, np.int64)
-    res = e._subset_result(o, order, np.array([11, 44], np.int64), nid_user)
+    e._subset_check(0, order, np.array([11, 44], np.int64), nid_user)
+    res = e._subset_result(o, order)
     assert res[0].shape == (3, 8) and res[1].shape == (2, 8)   # caller's [4, 1]
     assert np.array_equal(res[1], e._out[0:2]) and np.array_equal(res[0], e._out[2:5])
     assert list(nid_user) == [44, 11]
+
+
+def test_subset_counters_written_back_before_an_error():
+    """The C layer advances the listed streams' counters even when it then reports an error:
+    they reach the caller's next_id (a list too) before the exception."""
+    from yolo_tracking_amd import _lib
+    e = _Eng()
+    _, order = e._subset([4, 1], 2)
+    nid_user = [0, 0]
+    with pytest.raises(_lib.YTAError):
+        e._subset_check(_lib.YTA_ERR_INVALID, order, np.array([11, 44], np.int64), nid_user)
+    assert nid_user == [44, 11]

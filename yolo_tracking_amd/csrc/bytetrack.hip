@@ -1307,7 +1307,10 @@ __global__ __launch_bounds__(BLK1) void k_bs_lap(BtArgs a) {
         if (!ok && t == 0) atomicOr(&c->err, ERR_EDGE_OVERFLOW);
     }
     block_sync();
-    if (t == 0) c->frame_id += 1;
+    if (t == 0) {
+        c->frame_id += 1;
+        c->n_res1 = 0;   // a ByteTrack statistic (s1_lap_body sets it): 0, as the fused k_stage1
+    }
 }
 
 // ------------------------------------------------------------------------------------ k_apply
@@ -2106,7 +2109,7 @@ __global__ __launch_bounds__(256) void k_widen_f32(const float *src, double *dst
 // thread summing a run of streams, then a block scan.
 constexpr int OFFS_T = 1024;
 __global__ __launch_bounds__(OFFS_T) void k_out_offsets_scan(const BtCounters *cnt, int S, int cap,
-                                                              int *off) {
+                                                              int *off, int *off_host) {
     __shared__ int part[OFFS_T];
     const int t = threadIdx.x;
     const int per = (S + OFFS_T - 1) / OFFS_T, s0 = min(S, t * per), s1 = min(S, s0 + per);
@@ -2121,11 +2124,48 @@ __global__ __launch_bounds__(OFFS_T) void k_out_offsets_scan(const BtCounters *c
         __syncthreads();
     }
     int r = part[t] - sum;   // exclusive prefix of this thread's run
-    if (t == 0) off[0] = 0;
+    if (t == 0) {
+        off[0] = 0;
+        if (off_host) off_host[0] = 0;
+    }
     for (int s = s0; s < s1; ++s) {
         r += min(max(cnt[s].n_out, 0), cap);
         off[s + 1] = r;
+        if (off_host) off_host[s + 1] = r;   // mapped host memory: no copy on the copy-out stream
     }
+}
+
+// Pipelined path: a frame's packed rows (off[S] of them, 64 B each) stored by the copy-out
+// stream's kernel straight into mapped page-locked host memory (the caller's buffer or the slot's
+// staging), 16-B pieces a lane, so a wave writes 1 KiB runs over PCIe.  Replaces the copy engine's
+// device -> host copy, whose enqueue held the host until that stream drained (r05e:
+// yta_bytetrack_pipe_stats host_d2h_call_ms ~1.7-1.8 ms a frame).  tools/pcie_bench.hip: 55 GB/s
+// from 64 blocks, as the copy engines, and 88 GB/s beside a copy-engine host -> device copy.
+constexpr int ROWS_H_BLOCKS = 128;
+__global__ __launch_bounds__(1024) void k_copy_ints(const int *src, int *dst, int n) {
+    for (int i = threadIdx.x; i < n; i += blockDim.x) dst[i] = src[i];
+}
+__global__ __launch_bounds__(256) void k_rows_to_host(const double *src, const int *off, int S,
+                                                      long long limit, int4 *dst) {
+    // int4 pieces of the packed rows, never past the destination's `limit` rows (the collect
+    // compares off[S] with it and reports the frame)
+    const long long n = min((long long)off[S], limit) * 4;
+    const int4 *s4 = reinterpret_cast<const int4 *>(src);
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (long long)gridDim.x * blockDim.x)
+        dst[i] = s4[i];
+}
+
+// Pipelined path: the frame's counters stored straight into mapped, coherent host memory (16-B
+// pieces over PCIe) by the compute stream, so the copy-out stream carries only the rows: a small
+// hipMemcpyAsync device -> host there held the host until that stream drained (r05d:
+// yta_bytetrack_pipe_stats host_small_d2h_ms ~1-2 ms a frame, which serialised the pipeline).
+__global__ __launch_bounds__(256) void k_cnt_to_host(const BtCounters *cnt, int S, int4 *dst) {
+    const int4 *src = reinterpret_cast<const int4 *>(cnt);
+    const long long n = (long long)S * (long long)(sizeof(BtCounters) / sizeof(int4));
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (long long)gridDim.x * blockDim.x)
+        dst[i] = src[i];
 }
 
 __global__ __launch_bounds__(BLKF) void k_rebuild_free(BtArgs a) {
@@ -2175,7 +2215,10 @@ __global__ void k_reset(BtArgs a, int s0) {
 // ================================================================================== host engine
 using namespace yta;
 
-constexpr int PIPE_DEPTH = 3;   // frames in flight of the pipelined host-buffer update
+#ifndef YTA_PIPE_DEPTH
+#define YTA_PIPE_DEPTH 3
+#endif
+constexpr int PIPE_DEPTH = YTA_PIPE_DEPTH;   // frames in flight of the pipelined host-buffer update
 // yta_bytetrack_pipe_stats slots (include/yolo_tracking_amd.h): frames collected; detection
 // bytes DMA'd straight from the caller / staged through pinned buffers; row bytes DMA'd straight
 // into the caller / staged; host ms staging detections, in submit, waiting in collect, copying
@@ -2185,7 +2228,7 @@ enum {
     PS_FRAMES, PS_IN_DIRECT, PS_IN_STAGED, PS_OUT_DIRECT, PS_OUT_STAGED, PS_STAGE_IN_MS,
     PS_SUBMIT_MS, PS_WAIT_MS, PS_COPY_OUT_MS, PS_GPU_IN_MS, PS_GPU_KERN_MS, PS_GPU_OUT_MS,
     PS_GPU_SPAN_MS, PS_H2D_CALL_MS, PS_LAUNCH_MS, PS_D2H_CALL_MS, PS_SMALL_H2D_MS, PS_SMALL_D2H_MS,
-    PS_PINNED_CHECK_MS, PS_N
+    PS_PINNED_CHECK_MS, PS_CAP_WAITS, PS_CAP_DRAINS, PS_N
 };
 static_assert(PS_N <= 24, "pstat holds 24 slots");
 // Direct copies of the pipelined path in pieces of YTA_PIPE_CHUNK_MB (0: one copy each way)
@@ -2195,6 +2238,29 @@ static size_t pipe_chunk_bytes() {
         return v ? (size_t)atoi(v) << 20 : (size_t)0;
     }();
     return c;
+}
+static bool env_flag(const char *name, bool dflt) {
+    const char *v = getenv(name);
+    return v ? atoi(v) != 0 : dflt;
+}
+// Per-frame GPU timing events of the pipelined path (yta_bytetrack_pipe_stats' GPU columns)
+static bool pipe_timing() {
+    static const bool k = env_flag("YTA_PIPE_TIMING", false);
+    return k;
+}
+// A frame's detection offsets read by the compute stream from the slot's mapped host copy
+// (k_copy_ints) instead of a small copy on the copy-in stream
+static bool pipe_off_kernel() {
+    static const bool k = env_flag("YTA_PIPE_OFF_KERNEL", false);
+    return k;
+}
+// Rows device -> host by k_rows_to_host (1, default) or by the copy engines (YTA_PIPE_KERNEL_D2H=0)
+static bool pipe_kernel_d2h() {
+    static const bool k = [] {
+        const char *v = getenv("YTA_PIPE_KERNEL_D2H");
+        return !v || atoi(v) != 0;
+    }();
+    return k;
 }
 static hipError_t copy_pieces(void *dst, const void *src, size_t bytes, hipMemcpyKind kind,
                               hipStream_t st) {
@@ -2251,12 +2317,16 @@ struct yta_bytetrack {
         double *d_pack = nullptr, *h_pack = nullptr; // packed output rows
         long long pack_cap = 0;
         int *d_pack_off = nullptr, *h_pack_off = nullptr;   // S + 1 row offsets
-        BtCounters *d_cnt = nullptr, *h_cnt = nullptr;      // counters after this frame
+        BtCounters *d_cnt = nullptr, *h_cnt = nullptr;      // counters after this frame (d_cnt unused)
+        BtCounters *m_cnt = nullptr;                 // h_cnt as the device sees it (mapped)
+        int *m_pack_off = nullptr;                   // h_pack_off as the device sees it
+        double *m_pack = nullptr;                    // h_pack as the device sees it
         long long *h_nid = nullptr;                  // next_id staging
-        hipEvent_t in_done = nullptr, kern_done = nullptr, out_done = nullptr;
-        // timing events: the start of the slot's copy-in, kernels and copy-out (the *_done
-        // events above mark their ends), for yta_bytetrack_pipe_stats
-        hipEvent_t in_start = nullptr, kern_start = nullptr, out_start = nullptr;
+        hipEvent_t in_done = nullptr, kern_done = nullptr, out_done = nullptr;   // dependencies
+        // timing events (YTA_PIPE_TIMING=1 only): start / end of the slot's copy-in, kernels and
+        // copy-out, for yta_bytetrack_pipe_stats
+        hipEvent_t t_ev[6] = {};
+        int *m_off = nullptr;                        // h_off as the device sees it (mapped)
         double *user_out = nullptr;                  // the caller's buffer
         long long rows_bound = 0;                    // det_offsets[S] of the frame
         bool direct_out = false;                     // DMA straight into user_out
@@ -2329,7 +2399,9 @@ constexpr int STAGE_CHUNKS = YTA_STAGE_CHUNKS;
 // Is [p, p + bytes) one page-locked host allocation?  Both ends page-locked is not enough (a
 // view spanning two pinned allocations with pageable pages between them): the whole range must
 // lie inside the allocation that holds p.  Anything the runtime cannot vouch for is staged.
-bool host_pinned(const void *p, size_t bytes) {
+// dev (optional): the address the GPU's kernels use for p (mapped page-locked memory), or null.
+bool host_pinned(const void *p, size_t bytes, void **dev = nullptr) {
+    if (dev) *dev = nullptr;
     if (!p || !bytes) return false;
     hipPointerAttribute_t at;
     if (hipPointerGetAttributes(&at, p) != hipSuccess) {
@@ -2347,7 +2419,9 @@ bool host_pinned(const void *p, size_t bytes) {
         return false;
     }
     const char *b = (const char *)base, *q = (const char *)p;
-    return b && q >= b && bytes <= size && (size_t)(q - b) <= size - bytes;
+    const bool inside = b && q >= b && bytes <= size && (size_t)(q - b) <= size - bytes;
+    if (inside && dev) *dev = at.devicePointer;
+    return inside;
 }
 inline size_t stage_chunk(size_t bytes) {
     const int n = bytes >= (16u << 20) ? STAGE_CHUNKS : 1;
@@ -3094,8 +3168,8 @@ void pipe_free(yta_bytetrack *e) {
         for (void *h : {(void *)p.h_in, (void *)p.h_off, (void *)p.h_pack, (void *)p.h_pack_off,
                         (void *)p.h_cnt, (void *)p.h_nid, (void *)p.h_in32})
             if (h) (void)hipHostFree(h);
-        for (hipEvent_t ev : {p.in_done, p.kern_done, p.out_done, p.in_start, p.kern_start,
-                              p.out_start})
+        for (hipEvent_t ev : {p.in_done, p.kern_done, p.out_done, p.t_ev[0], p.t_ev[1], p.t_ev[2],
+                              p.t_ev[3], p.t_ev[4], p.t_ev[5]})
             if (ev) (void)hipEventDestroy(ev);
         p = yta_bytetrack::PipeSlot{};
     }
@@ -3113,16 +3187,22 @@ int pipe_slot_ready(yta_bytetrack *e, yta_bytetrack::PipeSlot &p, long long dets
         YTA_HIP(hipStreamCreateWithFlags(&e->s_out, hipStreamNonBlocking));
     }
     if (!p.in_done) {
-        for (hipEvent_t *ev : {&p.in_done, &p.kern_done, &p.out_done, &p.in_start, &p.kern_start,
-                               &p.out_start})
-            YTA_HIP(hipEventCreateWithFlags(ev, hipEventDefault));
+        for (hipEvent_t *ev : {&p.in_done, &p.kern_done, &p.out_done})
+            YTA_HIP(hipEventCreateWithFlags(ev, hipEventDisableTiming));
+        if (pipe_timing())
+            for (hipEvent_t &ev : p.t_ev) YTA_HIP(hipEventCreateWithFlags(&ev, hipEventDefault));
         YTA_HIP(hipMalloc((void **)&p.d_off, sizeof(int) * (S + 1)));
-        YTA_HIP(hipHostMalloc((void **)&p.h_off, sizeof(int) * (S + 1), hipHostMallocDefault));
+        YTA_HIP(hipHostMalloc((void **)&p.h_off, sizeof(int) * (S + 1),
+                              hipHostMallocMapped | hipHostMallocCoherent));
+        YTA_HIP(hipHostGetDevicePointer((void **)&p.m_off, p.h_off, 0));
         YTA_HIP(hipMalloc((void **)&p.d_pack_off, sizeof(int) * (S + 1)));
-        YTA_HIP(hipHostMalloc((void **)&p.h_pack_off, sizeof(int) * (S + 1),
-                              hipHostMallocDefault));
-        YTA_HIP(hipMalloc((void **)&p.d_cnt, sizeof(BtCounters) * S));
-        YTA_HIP(hipHostMalloc((void **)&p.h_cnt, sizeof(BtCounters) * S, hipHostMallocDefault));
+        // counters and row offsets: written by the compute stream's kernels straight into mapped,
+        // coherent host memory (k_out_offsets_scan, k_cnt_to_host)
+        const unsigned mf = hipHostMallocMapped | hipHostMallocCoherent;
+        YTA_HIP(hipHostMalloc((void **)&p.h_pack_off, sizeof(int) * (S + 1), mf));
+        YTA_HIP(hipHostMalloc((void **)&p.h_cnt, sizeof(BtCounters) * S, mf));
+        YTA_HIP(hipHostGetDevicePointer((void **)&p.m_pack_off, p.h_pack_off, 0));
+        YTA_HIP(hipHostGetDevicePointer((void **)&p.m_cnt, p.h_cnt, 0));
         YTA_HIP(hipHostMalloc((void **)&p.h_nid, sizeof(long long) * S, hipHostMallocDefault));
     }
     if (dets > p.in_cap) {   // detections and packed rows: both bounded by the frame's dets
@@ -3137,24 +3217,25 @@ int pipe_slot_ready(yta_bytetrack *e, yta_bytetrack::PipeSlot &p, long long dets
         YTA_HIP(hipHostMalloc((void **)&p.h_in, sizeof(double) * 6 * cap, hipHostMallocDefault));
         YTA_HIP(hipMalloc((void **)&p.d_pack, sizeof(double) * 8 * cap));
         YTA_HIP(hipHostMalloc((void **)&p.h_pack, sizeof(double) * 8 * cap,
-                              hipHostMallocDefault));
+                              hipHostMallocMapped | hipHostMallocCoherent));
+        YTA_HIP(hipHostGetDevicePointer((void **)&p.m_pack, p.h_pack, 0));
         p.in_cap = p.pack_cap = cap;
     }
     return YTA_OK;
 }
 
-// The frame's copy-in (s_in), kernels + row snapshot (compute stream) and copy-out (s_out).
-int pipe_enqueue(yta_bytetrack *e, yta_bytetrack::PipeSlot &p, const double *dets,
-                 const int *det_offsets, const long long *next_id, double *out, long long total,
-                 const float *dets32) {
+// The frame's copy-in (s_in): offsets and detections into the slot.
+int pipe_enqueue_in(yta_bytetrack *e, yta_bytetrack::PipeSlot &p, const double *dets,
+                    const int *det_offsets, long long total, const float *dets32) {
     const int S = e->S;
     int rc = YTA_OK;
     // this slot's last frame was collected (its events completed): its buffers are free
-    YTA_HIP(hipEventRecord(p.in_start, e->s_in));
+    if (p.t_ev[0]) YTA_HIP(hipEventRecord(p.t_ev[0], e->s_in));
     memcpy(p.h_off, det_offsets, sizeof(int) * (S + 1));
     auto ts = std::chrono::steady_clock::now();
-    YTA_HIP(hipMemcpyAsync(p.d_off, p.h_off, sizeof(int) * (S + 1), hipMemcpyHostToDevice,
-                           e->s_in));
+    if (!pipe_off_kernel())   // else the compute stream reads them from the mapped h_off
+        YTA_HIP(hipMemcpyAsync(p.d_off, p.h_off, sizeof(int) * (S + 1), hipMemcpyHostToDevice,
+                               e->s_in));
     e->pstat[PS_SMALL_H2D_MS] += std::chrono::duration<double, std::milli>(
                                      std::chrono::steady_clock::now() - ts)
                                      .count();
@@ -3195,10 +3276,23 @@ int pipe_enqueue(yta_bytetrack *e, yta_bytetrack::PipeSlot &p, const double *det
         }
     }
     e->pstat[p.direct_in ? PS_IN_DIRECT : PS_IN_STAGED] += (double)p.in_bytes;
+    if (p.t_ev[1]) YTA_HIP(hipEventRecord(p.t_ev[1], e->s_in));
     YTA_HIP(hipEventRecord(p.in_done, e->s_in));
+    return YTA_OK;
+}
+
+// The frame's kernels + row / counter snapshot (compute stream) and copy-out (s_out).
+int pipe_enqueue_run(yta_bytetrack *e, yta_bytetrack::PipeSlot &p, const long long *next_id,
+                     double *out, long long total, const float *dets32) {
+    const int S = e->S;
+    int rc = YTA_OK;
     // compute stream: the frame, then its rows and counters snapshotted into the slot
     YTA_HIP(hipStreamWaitEvent(e->stream, p.in_done, 0));
-    YTA_HIP(hipEventRecord(p.kern_start, e->stream));
+    if (p.t_ev[2]) YTA_HIP(hipEventRecord(p.t_ev[2], e->stream));
+    if (pipe_off_kernel()) {
+        hipLaunchKernelGGL(k_copy_ints, dim3(1), dim3(1024), 0, e->stream, p.m_off, p.d_off, S + 1);
+        YTA_HIP(hipGetLastError());
+    }
     if (next_id) {
         memcpy(p.h_nid, next_id, sizeof(long long) * S);
         YTA_HIP(hipMemcpy2DAsync(&e->a.cnt[0].next_id, sizeof(BtCounters), p.h_nid,
@@ -3216,41 +3310,108 @@ int pipe_enqueue(yta_bytetrack *e, yta_bytetrack::PipeSlot &p, const double *det
                                   std::chrono::steady_clock::now() - tl)
                                   .count();
     hipLaunchKernelGGL(k_out_offsets_scan, dim3(1), dim3(OFFS_T), 0, e->stream, e->a.cnt, S,
-                       e->CAP, p.d_pack_off);
+                       e->CAP, p.d_pack_off, p.m_pack_off);
     hipLaunchKernelGGL(k_pack_out, dim3(S), dim3(256), 0, e->stream, e->out_own, (long long)e->CAP,
                        p.d_pack_off, p.d_pack, p.pack_cap);
+    hipLaunchKernelGGL(k_cnt_to_host, dim3((S * 8 + 255) / 256), dim3(256), 0, e->stream,
+                       e->a.cnt, S, (int4 *)p.m_cnt);
     YTA_HIP(hipGetLastError());
-    YTA_HIP(hipMemcpyAsync(p.d_cnt, e->a.cnt, sizeof(BtCounters) * S, hipMemcpyDeviceToDevice,
-                           e->stream));
+    if (p.t_ev[3]) YTA_HIP(hipEventRecord(p.t_ev[3], e->stream));
     YTA_HIP(hipEventRecord(p.kern_done, e->stream));
     // copy-out stream: counters, offsets and at most det_offsets[S] rows (every output row is a
     // track matched to or born from one of the frame's detections)
     YTA_HIP(hipStreamWaitEvent(e->s_out, p.kern_done, 0));
-    YTA_HIP(hipEventRecord(p.out_start, e->s_out));
-    ts = std::chrono::steady_clock::now();
-    YTA_HIP(hipMemcpyAsync(p.h_cnt, p.d_cnt, sizeof(BtCounters) * S, hipMemcpyDeviceToHost,
-                           e->s_out));
-    YTA_HIP(hipMemcpyAsync(p.h_pack_off, p.d_pack_off, sizeof(int) * (S + 1),
-                           hipMemcpyDeviceToHost, e->s_out));
-    e->pstat[PS_SMALL_D2H_MS] += std::chrono::duration<double, std::milli>(
-                                     std::chrono::steady_clock::now() - ts)
-                                     .count();
+    if (p.t_ev[4]) YTA_HIP(hipEventRecord(p.t_ev[4], e->s_out));
     p.user_out = out;
     p.rows_bound = total;
-    ts = std::chrono::steady_clock::now();
-    p.direct_out = total > 0 && host_pinned(out, sizeof(double) * 8 * total);
+    auto ts = std::chrono::steady_clock::now();
+    void *out_dev = nullptr;
+    p.direct_out = total > 0 && host_pinned(out, sizeof(double) * 8 * total, &out_dev);
     e->pstat[PS_PINNED_CHECK_MS] += std::chrono::duration<double, std::milli>(
                                         std::chrono::steady_clock::now() - ts)
                                         .count();
     if (total) {
         const auto t0 = std::chrono::steady_clock::now();
-        YTA_HIP(copy_pieces(p.direct_out ? out : p.h_pack, p.d_pack, sizeof(double) * 8 * total,
-                            hipMemcpyDeviceToHost, e->s_out));
+        void *dst_dev = p.direct_out ? out_dev : (void *)p.m_pack;
+        if (pipe_kernel_d2h() && dst_dev) {   // the rows stored by a kernel (k_rows_to_host)
+            hipLaunchKernelGGL(k_rows_to_host, dim3(ROWS_H_BLOCKS), dim3(256), 0, e->s_out,
+                               p.d_pack, p.d_pack_off, S, total, (int4 *)dst_dev);
+            YTA_HIP(hipGetLastError());
+        } else {
+            YTA_HIP(copy_pieces(p.direct_out ? out : p.h_pack, p.d_pack,
+                                sizeof(double) * 8 * total, hipMemcpyDeviceToHost, e->s_out));
+        }
         e->pstat[PS_D2H_CALL_MS] += std::chrono::duration<double, std::milli>(
                                         std::chrono::steady_clock::now() - t0)
                                         .count();
     }
+    if (p.t_ev[5]) YTA_HIP(hipEventRecord(p.t_ev[5], e->s_out));
     YTA_HIP(hipEventRecord(p.out_done, e->s_out));
+    return YTA_OK;
+}
+
+// Track capacity for the next frame of the pipeline.  Each stream's tracked + lost lists after it
+// are at most the live tracks after some earlier frame plus every detection from that frame on
+// (every tracked track is matched to or born from one of its frame's detections; lost tracks were
+// tracked before).  The counters used: the newest frame in flight whose kernels have run (the
+// compute stream stored them into its slot's mapped h_cnt, k_cnt_to_host), else the last
+// collected ones; if that bound does not fit, wait for the newest frame's kernels (not its
+// copies) and use its exact counters; only a frame that still does not fit drains the pipeline
+// and grows the engine.  (Round 4 bounded from the last COLLECTED frame only: at the bench's
+// 3N capacity that never fit with two frames in flight, so every submit drained the compute
+// stream and read the counters synchronously - the pipeline ran one frame at a time.)
+int pipe_capacity(yta_bytetrack *e, const int *det_offsets) {
+    const int S = e->S;
+    int need_d = e->MAXD;
+    for (int s = 0; s < S; ++s) {
+        const int m = det_offsets[s + 1] - det_offsets[s];
+        YTA_CHECK(m >= 0, YTA_ERR_INVALID, "det_offsets must be non-decreasing");
+        need_d = std::max(need_d, m);
+    }
+    auto slot = [&](int k) -> yta_bytetrack::PipeSlot & {
+        return e->pipe[(e->pipe_head + k) % PIPE_DEPTH];
+    };
+    // k0: the in-flight frame (in flight order) whose counters are used, -1 for e->h_cnt
+    auto fits = [&](int k0) {
+        const BtCounters *c = k0 < 0 ? e->h_cnt : slot(k0).h_cnt;
+        for (int s = 0; s < S; ++s) {
+            long long bound = (long long)c[s].n_tracked + c[s].n_lost +
+                              (det_offsets[s + 1] - det_offsets[s]);
+            for (int k = k0 + 1; k < e->pipe_count; ++k)
+                bound += slot(k).h_off[s + 1] - slot(k).h_off[s];
+            if (bound > e->CAP) return false;
+        }
+        return true;
+    };
+    if (need_d <= e->MAXD) {
+        int k0 = -1;
+        for (int k = e->pipe_count - 1; k >= 0; --k) {
+            const hipError_t q = hipEventQuery(slot(k).kern_done);
+            if (q == hipSuccess) {
+                k0 = k;
+                break;
+            }
+            (void)hipGetLastError();   // hipErrorNotReady
+        }
+        if (fits(k0)) return YTA_OK;
+        if (k0 != e->pipe_count - 1) {
+            YTA_HIP(hipEventSynchronize(slot(e->pipe_count - 1).kern_done));
+            ++e->pstat[PS_CAP_WAITS];
+            if (fits(e->pipe_count - 1)) return YTA_OK;
+        }
+    }
+    // drain the kernels in flight, then the exact need
+    ++e->pstat[PS_CAP_DRAINS];
+    YTA_HIP(host_wait(e->stream));   // every frame in flight has run: a.cnt is current
+    std::vector<BtCounters> c(S);
+    YTA_HIP(hipMemcpy(c.data(), e->a.cnt, sizeof(BtCounters) * S, hipMemcpyDeviceToHost));
+    int need_c = e->CAP;
+    for (int s = 0; s < S; ++s)
+        need_c = std::max(need_c, c[s].n_tracked + c[s].n_lost +
+                                      (det_offsets[s + 1] - det_offsets[s]));
+    if (need_d > e->MAXD || need_c > e->CAP)
+        return reserve(e, need_c > e->CAP ? std::max(need_c, 2 * e->CAP) : e->CAP,
+                       need_d > e->MAXD ? std::max(need_d, 2 * e->MAXD) : e->MAXD);
     return YTA_OK;
 }
 
@@ -3268,34 +3429,9 @@ int pipe_submit(yta_bytetrack *e, const double *dets, const int *det_offsets,
     YTA_CHECK(total == 0 || dets || dets32, YTA_ERR_INVALID, "null dets");
     YTA_CHECK(out_capacity >= total && (total == 0 || out), YTA_ERR_CAPACITY,
               "out holds %lld rows, the frame needs det_offsets[S] = %lld", out_capacity, total);
-    // capacity: the live tracks of the last collected frame plus every detection of the frames in
-    // flight and of this one bound each stream's tracked + lost lists
-    int need_d = e->MAXD, need_c = e->CAP;
-    bool grow = false;
-    for (int s = 0; s < S; ++s) {
-        const int m = det_offsets[s + 1] - det_offsets[s];
-        YTA_CHECK(m >= 0, YTA_ERR_INVALID, "det_offsets must be non-decreasing");
-        need_d = std::max(need_d, m);
-        long long bound = (long long)e->h_cnt[s].n_tracked + e->h_cnt[s].n_lost + m;
-        for (int k = 0; k < e->pipe_count; ++k) {
-            const auto &q = e->pipe[(e->pipe_head + k) % PIPE_DEPTH];
-            bound += q.h_off[s + 1] - q.h_off[s];
-        }
-        if (bound > e->CAP) grow = true;
-    }
-    if (grow || need_d > e->MAXD) {   // drain the kernels in flight, then the exact need
-        YTA_HIP(host_wait(e->stream));   // every frame in flight has run: a.cnt is current
-        std::vector<BtCounters> c(S);
-        YTA_HIP(hipMemcpy(c.data(), e->a.cnt, sizeof(BtCounters) * S, hipMemcpyDeviceToHost));
-        for (int s = 0; s < S; ++s)
-            need_c = std::max(need_c, c[s].n_tracked + c[s].n_lost +
-                                          (det_offsets[s + 1] - det_offsets[s]));
-        if (need_d > e->MAXD || need_c > e->CAP) {
-            const int rc = reserve(e, need_c > e->CAP ? std::max(need_c, 2 * e->CAP) : e->CAP,
-                                   need_d > e->MAXD ? std::max(need_d, 2 * e->MAXD) : e->MAXD);
-            if (rc) return rc;
-        }
-    }
+    for (int s = 0; s < S; ++s)
+        YTA_CHECK(det_offsets[s + 1] >= det_offsets[s], YTA_ERR_INVALID,
+                  "det_offsets must be non-decreasing");
     auto &p = e->pipe[(e->pipe_head + e->pipe_count) % PIPE_DEPTH];
     if (p.dirty) {   // a failed submit may have left copies from this slot's buffers queued
         YTA_HIP(hipStreamSynchronize(e->s_in));
@@ -3306,7 +3442,10 @@ int pipe_submit(yta_bytetrack *e, const double *dets, const int *det_offsets,
     int rc = pipe_slot_ready(e, p, total);
     if (rc) return rc;
     const auto t0 = std::chrono::steady_clock::now();
-    rc = pipe_enqueue(e, p, dets, det_offsets, next_id, out, total, dets32);
+    // the copy-in first (it needs only the slot), so it overlaps any wait for capacity below
+    rc = pipe_enqueue_in(e, p, dets, det_offsets, total, dets32);
+    if (!rc) rc = pipe_capacity(e, det_offsets);
+    if (!rc) rc = pipe_enqueue_run(e, p, next_id, out, total, dets32);
     if (rc) {   // copies from the slot's pinned staging may be in flight: the next use waits
         p.dirty = true;
         return rc;
@@ -3328,15 +3467,15 @@ int pipe_collect(yta_bytetrack *e, long long *next_id, int *out_offsets) {
     YTA_HIP(hipEventSynchronize(p.out_done));
     const auto t1 = std::chrono::steady_clock::now();
     e->pstat[PS_WAIT_MS] += std::chrono::duration<double, std::milli>(t1 - t0).count();
-    {   // the frame's GPU-side phases from its events (all complete)
+    if (p.t_ev[0]) {   // the frame's GPU-side phases from its timing events (all complete)
         float ms = 0.f;
-        if (hipEventElapsedTime(&ms, p.in_start, p.in_done) == hipSuccess)
+        if (hipEventElapsedTime(&ms, p.t_ev[0], p.t_ev[1]) == hipSuccess)
             e->pstat[PS_GPU_IN_MS] += ms;
-        if (hipEventElapsedTime(&ms, p.kern_start, p.kern_done) == hipSuccess)
+        if (hipEventElapsedTime(&ms, p.t_ev[2], p.t_ev[3]) == hipSuccess)
             e->pstat[PS_GPU_KERN_MS] += ms;
-        if (hipEventElapsedTime(&ms, p.out_start, p.out_done) == hipSuccess)
+        if (hipEventElapsedTime(&ms, p.t_ev[4], p.t_ev[5]) == hipSuccess)
             e->pstat[PS_GPU_OUT_MS] += ms;
-        if (hipEventElapsedTime(&ms, p.in_start, p.out_done) == hipSuccess)
+        if (hipEventElapsedTime(&ms, p.t_ev[0], p.t_ev[5]) == hipSuccess)
             e->pstat[PS_GPU_SPAN_MS] += ms;
         (void)hipGetLastError();
     }

@@ -3,6 +3,8 @@ stream_ids, ...)): a subset call lists the streams to update; every other stream
 left exactly as it was (the C ABI's *_update_streams)."""
 import numpy as np
 
+from .. import _lib
+
 
 class StreamSubset:
     def _subset(self, streams, n_items):
@@ -21,10 +23,18 @@ class StreamSubset:
     def _reorder(v, order):
         return None if v is None else [v[k] for k in order]
 
-    def _subset_result(self, o, order, nid, nid_user):
+    @staticmethod
+    def _subset_check(rc, order, nid, nid_user):
+        """Hand the listed streams' ID counters back to the caller's next_id (any sequence, in the
+        caller's order) BEFORE raising on rc: the C layer advances them even when it reports an
+        error after the launch (include/yolo_tracking_amd.h, host-buffer update rules)."""
+        if nid_user is not None and nid is not None:
+            for k, pos in enumerate(order):
+                nid_user[pos] = int(nid[k])
+        _lib.check(rc)
+
+    def _subset_result(self, o, order):
         res = [None] * len(order)
         for k, pos in enumerate(order):
             res[pos] = self._out[o[k]:o[k + 1]].copy()
-        if nid_user is not None:
-            nid_user[order] = nid
         return res

@@ -133,10 +133,11 @@ class BoTSORTEngine(ByteTrackEngine):
             o = self._out_off
             return [self._out[o[s]:o[s + 1]].copy() for s in range(self.n_streams)]
         o = np.zeros(n + 1, dtype=np.int32)
-        _lib.check(self.lib.yta_botsort_update_streams(
+        rc = self.lib.yta_botsort_update_streams(
             self._h, n, _lib.ptr(ids), _lib.ptr(packed), _lib.ptr(off), _lib.ptr(feats),
-            _lib.ptr(w), _lib.ptr(nid), _lib.ptr(self._out), len(self._out), _lib.ptr(o)))
-        return self._subset_result(o, order, nid, nid_user)
+            _lib.ptr(w), _lib.ptr(nid), _lib.ptr(self._out), len(self._out), _lib.ptr(o))
+        self._subset_check(rc, order, nid, nid_user)
+        return self._subset_result(o, order)
 
     def features(self, stream=0):
         """Smoothed features, class histograms (n, 8, 2) and their entry counts of the live

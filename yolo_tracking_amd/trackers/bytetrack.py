@@ -120,10 +120,11 @@ class ByteTrackEngine(StreamSubset):
             o = self._out_off
             return [self._out[o[s]:o[s + 1]].copy() for s in range(self.n_streams)]
         o = np.zeros(n + 1, dtype=np.int32)
-        _lib.check(self.lib.yta_bytetrack_update_streams(
+        rc = self.lib.yta_bytetrack_update_streams(
             self._h, n, _lib.ptr(ids), _lib.ptr(packed), _lib.ptr(off), _lib.ptr(nid),
-            _lib.ptr(self._out), len(self._out), _lib.ptr(o)))
-        return self._subset_result(o, order, nid, nid_user)
+            _lib.ptr(self._out), len(self._out), _lib.ptr(o))
+        self._subset_check(rc, order, nid, nid_user)
+        return self._subset_result(o, order)
 
     def submit(self, dets_per_stream, out=None):
         """Pipelined update, first half (yta_bytetrack_submit): enqueue one frame of every stream

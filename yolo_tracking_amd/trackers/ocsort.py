@@ -121,10 +121,11 @@ class OCSortEngine(StreamSubset):
             nid = np.ascontiguousarray(next_id, dtype=np.int64)
         if ids is not None:
             o = np.zeros(n + 1, dtype=np.int32)
-            _lib.check(self.lib.yta_ocsort_update_streams(
+            rc = self.lib.yta_ocsort_update_streams(
                 self._h, n, _lib.ptr(ids), _lib.ptr(packed), _lib.ptr(off), _lib.ptr(wh),
-                _lib.ptr(nid), _lib.ptr(self._out), len(self._out), _lib.ptr(o)))
-            return self._subset_result(o, order, nid, nid_user)
+                _lib.ptr(nid), _lib.ptr(self._out), len(self._out), _lib.ptr(o))
+            self._subset_check(rc, order, nid, nid_user)
+            return self._subset_result(o, order)
         _lib.check(self.lib.yta_ocsort_update(self._h, _lib.ptr(packed), _lib.ptr(off),
                                               _lib.ptr(wh), _lib.ptr(nid), _lib.ptr(self._out),
                                               len(self._out), _lib.ptr(self._out_off)))
