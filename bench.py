@@ -415,7 +415,7 @@ def pcie_inclusive(frame_of, S, N, device, first, frames=8, engines=1, pinned=Fa
                     f"{E} engine(s) on as many host threads); median step"}
 
 
-def pcie_pipelined(frame_of, S, N, device, first, frames=8, pinned=False, f32=False):
+def pcie_pipelined(frame_of, S, N, device, first, frames=8, pinned=False, f32=False, cap_mult=3):
     """The host-buffer path pipelined (yta_bytetrack_submit / _collect, one engine): frame f's
     detections go host -> device while frame f-1's kernels run and frame f-2's rows come back (up
     to three frames in flight), so both PCIe directions and the kernels overlap.  Every timed frame's packed dets sit in their
@@ -427,7 +427,7 @@ def pcie_pipelined(frame_of, S, N, device, first, frames=8, pinned=False, f32=Fa
 
     from yolo_tracking_amd import ByteTrackEngine, _lib
     eng = ByteTrackEngine(S, track_thresh=0.5, match_thresh=0.8, track_buffer=30, frame_rate=30,
-                          device=device, track_capacity=3 * N, max_dets=N)
+                          device=device, track_capacity=cap_mult * N, max_dets=N)
     lib, h = eng.lib, eng.handle
 
     def buf(shape, dt=np.float64):

@@ -375,10 +375,11 @@ int yta_ocsort_get_state(yta_ocsort *engine, int stream, int *n_tracks, long lon
 /* Last frame's counts summed over streams: dets, first-round dets, BYTE dets, live trackers,
  * output rows, births, LAP calls, fast-path frames (8 int64). */
 int yta_ocsort_stats(yta_ocsort *engine, long long *stats);
-/* Solver counters since create / reset, summed over streams (3 int64): first-round solves of the
+/* Solver counters since create / reset, summed over streams (4 int64): first-round solves of the
  * transposed problem (more detections than trackers, association.py:20-28 with dummy columns),
- * those of them whose optimum was not certified unique (exact ties: lapjv replayed instead), and
- * lapjv replays in any round (the single-wavefront restatement of lapx's tie-breaking). */
+ * those of them whose optimum was not certified unique (exact ties: lapjv replayed instead),
+ * lapjv replays in any round (the single-wavefront restatement of lapx's tie-breaking), and -IoU
+ * rounds (BYTE / OCR) solved on the rows and columns that have a positive entry. */
 int yta_ocsort_lap_stats(yta_ocsort *engine, long long *stats);
 int yta_ocsort_hip_stream(yta_ocsort *engine, void **stream);
 /* OCSORT Kalman KAT: n tracks initialised from z0 (n x 4, [u, v, s, r]) run `steps` steps of
@@ -451,11 +452,12 @@ int yta_deepocsort_get_state(yta_deepocsort *engine, int stream, int *n_tracks, 
 /* Last frame's counts summed over streams: dets, kept dets, 0, live trackers, output rows,
  * births, LAP calls, fast-path frames (8 int64). */
 int yta_deepocsort_stats(yta_deepocsort *engine, long long *stats);
-/* Solver counters since create / reset, summed over streams (3 int64): first-round solves of the
+/* Solver counters since create / reset, summed over streams (4 int64): first-round solves of the
  * transposed problem (more detections than trackers, association.py:20-28 with dummy columns),
- * those of them whose optimum was not certified unique (exact ties: lapjv replayed instead), and
- * lapjv replays in any round (the single-wavefront restatement of lapx's tie-breaking). */
-int yta_deepocsort_lap_stats(yta_deepocsort *engine, long long *stats);
+ * those of them whose optimum was not certified unique (exact ties: lapjv replayed instead),
+ * lapjv replays in any round (the single-wavefront restatement of lapx's tie-breaking), and -IoU
+ * rounds (BYTE / OCR) solved on the rows and columns that have a positive entry. */
+int yta_deepocsort_lap_stats(yta_deepocsort *engine, long long *stats);   /* 4 int64 */
 int yta_deepocsort_hip_stream(yta_deepocsort *engine, void **stream);
 /* DeepOCSORT Kalman KAT (deep_ocsort.py:103-136, 198-293 new-KF branch): n tracks initialised
  * from boxes b0 (n x 4, x1 y1 x2 y2) run `steps` steps of [affine (warps: steps x n x 6, NULL =
@@ -523,11 +525,12 @@ int yta_hybridsort_classes(yta_hybridsort *engine, int stream, double *cls, int 
 /* Last frame's counts summed over streams: dets, kept dets, live trackers, output rows, births,
  * LAP calls, long-term corrections, feature jobs (8 int64). */
 int yta_hybridsort_stats(yta_hybridsort *engine, long long *stats);
-/* Solver counters since create / reset, summed over streams (3 int64): first-round solves of the
+/* Solver counters since create / reset, summed over streams (4 int64): first-round solves of the
  * transposed problem (more detections than trackers, association.py:20-28 with dummy columns),
- * those of them whose optimum was not certified unique (exact ties: lapjv replayed instead), and
- * lapjv replays in any round (the single-wavefront restatement of lapx's tie-breaking). */
-int yta_hybridsort_lap_stats(yta_hybridsort *engine, long long *stats);
+ * those of them whose optimum was not certified unique (exact ties: lapjv replayed instead),
+ * lapjv replays in any round (the single-wavefront restatement of lapx's tie-breaking), and -IoU
+ * rounds (BYTE / OCR) solved on the rows and columns that have a positive entry. */
+int yta_hybridsort_lap_stats(yta_hybridsort *engine, long long *stats);   /* 4 int64 */
 int yta_hybridsort_hip_stream(yta_hybridsort *engine, void **stream);
 /* HybridSORT Kalman KAT (hybridsort.py:112-320): n tracks initialised from rows b0 (n x 5:
  * x1 y1 x2 y2 score) run `steps` steps of predict (velocity clamp) + update(b[step] (n x 5); a

@@ -99,6 +99,7 @@ def test_deepocsort_2048_d512_cmc_four_streams(g):
         np.testing.assert_allclose(st["P"][::64], g[f"{name}__st_P_sample"], rtol=1e-9, atol=1e-9)
         np.testing.assert_allclose(st["emb"][::64], g[f"{name}__st_emb_sample"], rtol=0,
                                    atol=1e-12)
+    assert eng.lap_stats()["reduced"] > 0, eng.lap_stats()
 
 
 def test_deepocsort_2048_detection_surge(g):
@@ -150,6 +151,8 @@ def test_hybridsort_4096_d512_two_streams(g):
         np.testing.assert_allclose(st["feat"][::64], g[f"{name}__st_feat_sample"], rtol=0,
                                    atol=2e-7)
         assert nid[s] == int(g[f"{name}__count"])
+    # the OCR rounds ran on their positive part (ocsort_common.hpp iou_lap_reduced)
+    assert eng.lap_stats()["reduced"] > 0, eng.lap_stats()
 
 
 def test_hybridsort_4096_python_surface(g):

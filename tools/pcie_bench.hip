@@ -105,6 +105,32 @@ int main(int argc, char **argv) {
         put(k, timed([&] { kh2d(blocks); }), H2D);
     }
     put("duplex_sdma_in_kern_out_1024", timed([&] { h2d(); kd2h(1024); }), H2D + D2H);
+    put("duplex_kern_out_then_sdma_in_128", timed([&] { kd2h(128); h2d(); }), H2D + D2H);
+    put("duplex_sdma_in_then_kern_out_128", timed([&] { h2d(); kd2h(128); }), H2D + D2H);
+    {   // when does a copy-engine H2D start if a kernel D2H is already streaming?
+        hipEvent_t e0, e1, e2, e3;
+        for (hipEvent_t *ev : {&e0, &e1, &e2, &e3}) CK(hipEventCreate(ev));
+        float a = 0, b = 0, c = 0;
+        double sa = 0, sb = 0, sc = 0;
+        for (int r = 0; r < REP; ++r) {
+            CK(hipDeviceSynchronize());
+            CK(hipEventRecord(e0, s2));
+            kd2h(128);
+            CK(hipEventRecord(e1, s2));
+            CK(hipEventRecord(e2, s1));
+            h2d();
+            CK(hipEventRecord(e3, s1));
+            CK(hipDeviceSynchronize());
+            CK(hipEventElapsedTime(&a, e0, e1));   // kernel D2H
+            CK(hipEventElapsedTime(&b, e0, e2));   // H2D start after the kernel's start
+            CK(hipEventElapsedTime(&c, e2, e3));   // H2D duration
+            sa += a; sb += b; sc += c;
+        }
+        char buf[200];
+        snprintf(buf, sizeof buf, ", \"overlap_probe\": {\"kern_d2h_ms\": %.3f, \"h2d_start_after_ms\": %.3f, \"h2d_ms\": %.3f}",
+                 sa / REP, sb / REP, sc / REP);
+        js += buf;
+    }
     put("duplex_kern_in_sdma_out_1024", timed([&] { kh2d(1024); d2h(); }), H2D + D2H);
     put("duplex_kern_both_1024", timed([&] { kh2d(1024); kd2h(1024); }), H2D + D2H);
     int node = -1;

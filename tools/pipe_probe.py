@@ -58,6 +58,7 @@ def main():
     p.add_argument("--first", type=int, default=10)
     p.add_argument("--frames", type=int, default=8)
     p.add_argument("--extra-streams", type=int, default=0)
+    p.add_argument("--cap-mult", type=int, default=3, help="pipelined engine capacity, x N")
     p.add_argument("--legs", default="sync,sync_pinned,pipe,pipe_pinned,pipe_pinned_f32")
     p.add_argument("--alloc", default="torch", choices=["torch", "hiphostmalloc", "register"],
                    help="page-locked caller buffers: torch's pinned allocator, hipHostMalloc, or "
@@ -95,13 +96,14 @@ def main():
         elif leg == "sync_pinned":
             r = bench.pcie_inclusive(frame_of, S, N, 0, first=a.first, frames=a.frames, pinned=True)
         elif leg == "pipe":
-            r = bench.pcie_pipelined(frame_of, S, N, 0, first=a.first, frames=a.frames)
+            r = bench.pcie_pipelined(frame_of, S, N, 0, first=a.first, frames=a.frames,
+                                     cap_mult=a.cap_mult)
         elif leg == "pipe_pinned":
             r = bench.pcie_pipelined(frame_of, S, N, 0, first=a.first, frames=a.frames,
-                                     pinned=True)
+                                     pinned=True, cap_mult=a.cap_mult)
         elif leg == "pipe_pinned_f32":
             r = bench.pcie_pipelined(frame_of, S, N, 0, first=a.first, frames=a.frames,
-                                     pinned=True, f32=True)
+                                     pinned=True, f32=True, cap_mult=a.cap_mult)
         else:
             raise SystemExit(f"unknown leg {leg}")
         r.pop("note", None)

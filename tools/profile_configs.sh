@@ -11,8 +11,11 @@ run() {   # name, bench_tracker args
   timeout -k 10 300 python3 $R/tools/bench_tracker.py "$@" > $O/${n}_bench.json 2> $O/${n}_bench.err || return $?
   echo bench $n
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/$n -o run -- python3 $R/tools/bench_tracker.py "$@" --cpu-frames 0 > $O/$n.json 2> $O/$n.err || return $?
+  # measured HBM bytes: FETCH_SIZE and WRITE_SIZE, each in its own pass
+  timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/${n}_fetch -o run -- python3 $R/tools/bench_tracker.py "$@" --cpu-frames 0 > $O/${n}_fetch.log 2>&1 || return $?
+  timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/${n}_write -o run -- python3 $R/tools/bench_tracker.py "$@" --cpu-frames 0 > $O/${n}_write.log 2>&1 || return $?
   local ks=$(find $O/$n -name '*kernel_stats.csv' | head -1)
-  python3 $R/tools/config_roofline.py $O/${n}_bench.json $ks > $O/${n}_roofline.json || return $?
+  python3 $R/tools/config_roofline.py $O/${n}_bench.json $ks $O/${n}_fetch $O/${n}_write > $O/${n}_roofline.json || return $?
   echo prof $n
 }
 run ocsort --tracker ocsort --steps 30 --warmup 3 || exit $?

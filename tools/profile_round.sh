@@ -11,7 +11,7 @@ R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/prof_$TAG
 mkdir -p $O
 cd /tmp && export TMPDIR=/tmp
-ARGS="--streams $S --queues $Q --steps 20 --warmup 5 --no-cpu-baseline --no-pcie"
+ARGS="--streams $S --queues $Q --steps 20 --warmup 5 --no-cpu-baseline --no-pcie --no-dropin --no-configs"
 ISO=3; [ "$Q" = "1" ] && ISO=0
 timeout -k 10 400 python3 $R/bench.py $ARGS > $O/bench.json 2> $O/bench.err
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt -o run -- python3 $R/bench.py $ARGS > $O/kt.log 2>&1

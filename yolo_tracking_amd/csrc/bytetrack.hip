@@ -2248,6 +2248,11 @@ static bool pipe_timing() {
     static const bool k = env_flag("YTA_PIPE_TIMING", false);
     return k;
 }
+// Each frame slot copies in on its own stream (else one copy-in stream for all)
+static bool pipe_slot_streams() {
+    static const bool k = env_flag("YTA_PIPE_SLOT_STREAMS", false);
+    return k;
+}
 // A frame's detection offsets read by the compute stream from the slot's mapped host copy
 // (k_copy_ints) instead of a small copy on the copy-in stream
 static bool pipe_off_kernel() {
@@ -2327,6 +2332,8 @@ struct yta_bytetrack {
         // copy-out, for yta_bytetrack_pipe_stats
         hipEvent_t t_ev[6] = {};
         int *m_off = nullptr;                        // h_off as the device sees it (mapped)
+        hipStream_t s_in = nullptr;                  // this slot's copy-in stream
+        bool own_s_in = false;                       // (its own, YTA_PIPE_SLOT_STREAMS=1)
         double *user_out = nullptr;                  // the caller's buffer
         long long rows_bound = 0;                    // det_offsets[S] of the frame
         bool direct_out = false;                     // DMA straight into user_out
@@ -3171,8 +3178,10 @@ void pipe_free(yta_bytetrack *e) {
         for (hipEvent_t ev : {p.in_done, p.kern_done, p.out_done, p.t_ev[0], p.t_ev[1], p.t_ev[2],
                               p.t_ev[3], p.t_ev[4], p.t_ev[5]})
             if (ev) (void)hipEventDestroy(ev);
+        if (p.own_s_in && p.s_in) (void)hipStreamDestroy(p.s_in);
         p = yta_bytetrack::PipeSlot{};
     }
+    for (auto &p : e->pipe) p = yta_bytetrack::PipeSlot{};
     for (hipStream_t st : {e->s_in, e->s_out})
         if (st) (void)hipStreamDestroy(st);
     e->s_in = e->s_out = nullptr;
@@ -3182,10 +3191,15 @@ void pipe_free(yta_bytetrack *e) {
 
 int pipe_slot_ready(yta_bytetrack *e, yta_bytetrack::PipeSlot &p, long long dets) {
     const int S = e->S;
+    if (!p.s_in && pipe_slot_streams()) {
+        YTA_HIP(hipStreamCreateWithFlags(&p.s_in, hipStreamNonBlocking));
+        p.own_s_in = true;
+    }
     if (!e->s_in) {
         YTA_HIP(hipStreamCreateWithFlags(&e->s_in, hipStreamNonBlocking));
         YTA_HIP(hipStreamCreateWithFlags(&e->s_out, hipStreamNonBlocking));
     }
+    if (!p.s_in) p.s_in = e->s_in;
     if (!p.in_done) {
         for (hipEvent_t *ev : {&p.in_done, &p.kern_done, &p.out_done})
             YTA_HIP(hipEventCreateWithFlags(ev, hipEventDisableTiming));
@@ -3230,12 +3244,12 @@ int pipe_enqueue_in(yta_bytetrack *e, yta_bytetrack::PipeSlot &p, const double *
     const int S = e->S;
     int rc = YTA_OK;
     // this slot's last frame was collected (its events completed): its buffers are free
-    if (p.t_ev[0]) YTA_HIP(hipEventRecord(p.t_ev[0], e->s_in));
+    if (p.t_ev[0]) YTA_HIP(hipEventRecord(p.t_ev[0], p.s_in));
     memcpy(p.h_off, det_offsets, sizeof(int) * (S + 1));
     auto ts = std::chrono::steady_clock::now();
     if (!pipe_off_kernel())   // else the compute stream reads them from the mapped h_off
         YTA_HIP(hipMemcpyAsync(p.d_off, p.h_off, sizeof(int) * (S + 1), hipMemcpyHostToDevice,
-                               e->s_in));
+                               p.s_in));
     e->pstat[PS_SMALL_H2D_MS] += std::chrono::duration<double, std::milli>(
                                      std::chrono::steady_clock::now() - ts)
                                      .count();
@@ -3244,7 +3258,7 @@ int pipe_enqueue_in(yta_bytetrack *e, yta_bytetrack::PipeSlot &p, const double *
     if (total && dets32) {   // float32 rows: half the bytes over the link, widened on the device
         p.in_bytes = (long long)sizeof(float) * 6 * total;
         p.direct_in = host_pinned(dets32, (size_t)p.in_bytes);
-        rc = stage_f32(e, dets32, 6 * total, &p.d_in32, &p.h_in32, &p.in32_cap, e->s_in);
+        rc = stage_f32(e, dets32, 6 * total, &p.d_in32, &p.h_in32, &p.in32_cap, p.s_in);
         if (rc) return rc;
     } else if (total) {
         const size_t bytes = sizeof(double) * 6 * total;
@@ -3257,7 +3271,7 @@ int pipe_enqueue_in(yta_bytetrack *e, yta_bytetrack::PipeSlot &p, const double *
         if (pinned_in) {   // straight from the caller (kept until collected)
             p.direct_in = true;
             const auto t0 = std::chrono::steady_clock::now();
-            YTA_HIP(copy_pieces(p.d_in, dets, bytes, hipMemcpyHostToDevice, e->s_in));
+            YTA_HIP(copy_pieces(p.d_in, dets, bytes, hipMemcpyHostToDevice, p.s_in));
             e->pstat[PS_H2D_CALL_MS] += std::chrono::duration<double, std::milli>(
                                             std::chrono::steady_clock::now() - t0)
                                             .count();
@@ -3268,7 +3282,7 @@ int pipe_enqueue_in(yta_bytetrack *e, yta_bytetrack::PipeSlot &p, const double *
                 const size_t n = std::min(ch, bytes - o);
                 par_copy(e, (char *)p.h_in + o, (const char *)dets + o, n);
                 YTA_HIP(hipMemcpyAsync((char *)p.d_in + o, (char *)p.h_in + o, n,
-                                       hipMemcpyHostToDevice, e->s_in));
+                                       hipMemcpyHostToDevice, p.s_in));
             }
             e->pstat[PS_STAGE_IN_MS] += std::chrono::duration<double, std::milli>(
                                             std::chrono::steady_clock::now() - t0)
@@ -3276,8 +3290,8 @@ int pipe_enqueue_in(yta_bytetrack *e, yta_bytetrack::PipeSlot &p, const double *
         }
     }
     e->pstat[p.direct_in ? PS_IN_DIRECT : PS_IN_STAGED] += (double)p.in_bytes;
-    if (p.t_ev[1]) YTA_HIP(hipEventRecord(p.t_ev[1], e->s_in));
-    YTA_HIP(hipEventRecord(p.in_done, e->s_in));
+    if (p.t_ev[1]) YTA_HIP(hipEventRecord(p.t_ev[1], p.s_in));
+    YTA_HIP(hipEventRecord(p.in_done, p.s_in));
     return YTA_OK;
 }
 
@@ -3434,7 +3448,7 @@ int pipe_submit(yta_bytetrack *e, const double *dets, const int *det_offsets,
                   "det_offsets must be non-decreasing");
     auto &p = e->pipe[(e->pipe_head + e->pipe_count) % PIPE_DEPTH];
     if (p.dirty) {   // a failed submit may have left copies from this slot's buffers queued
-        YTA_HIP(hipStreamSynchronize(e->s_in));
+        YTA_HIP(hipStreamSynchronize(p.s_in ? p.s_in : e->s_in));
         YTA_HIP(hipStreamSynchronize(e->stream));
         YTA_HIP(hipStreamSynchronize(e->s_out));
         p.dirty = false;

@@ -61,7 +61,7 @@ struct DocCounters {
     int lap_done;                  // first round solved by k_doc_lap this frame
     int n_ud, n_upd;               // k_doc_assoc -> k_doc_finish: unmatched detections, updates
     LapStats ls;                   // cumulative solver counters
-    int pad[12];
+    int pad[11];
 };
 static_assert(sizeof(DocCounters) == 128, "DocCounters layout");
 
@@ -747,7 +747,8 @@ __global__ __launch_bounds__(OC_T) void k_doc_assoc(DocArgs a) {
             &c->err, sh);
         if (mx > a.thr) {
             iou_lap(LapMat{mat, n_ud, n_ut, true}, a.rmatch + db, lds, lds_bytes, gws, &c->err, &c->ls,
-                    a.lap_ws + (s + 1) * a.lap_ws_stride - tight_ws_bytes());
+                    a.lap_ws + (s + 1) * a.lap_ws_stride - tight_ws_bytes(), nullptr, nullptr,
+                    nullptr, a.thr);
             for (int i = t; i < n_hi; i += nt) a.tmp[ub + i] = 0;
             for (int j = t; j < n_trk; j += nt) a.nan_flag[tb + j] = 0;
             block_sync();
@@ -1590,12 +1591,13 @@ int yta_deepocsort_lap_stats(yta_deepocsort *e, long long *stats) {
     YTA_CHECK(e && stats, YTA_ERR_INVALID, "null argument");
     const int rc = doc_read_counters(e);
     if (rc) return rc;
-    for (int k = 0; k < 3; ++k) stats[k] = 0;
+    for (int k = 0; k < 4; ++k) stats[k] = 0;
     for (int s = 0; s < e->S; ++s) {
         const LapStats &l = e->h_cnt[s].ls;
         stats[0] += l.transposed;
         stats[1] += l.uncertified;
         stats[2] += l.replays;
+        stats[3] += l.reduced;
     }
     return YTA_OK;
 }

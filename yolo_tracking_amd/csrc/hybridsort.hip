@@ -74,7 +74,7 @@ struct HsCounters {
     int n_ud, n_ut, n_upd;         // k_hs_assoc -> k_hs_ocr -> k_hs_assoc_b: the OCR round's sizes
     int ocr_nan;                   // the OCR matrix holds a NaN (its max is then NaN)
     unsigned long long ocr_max;    // its maximum, order-preserving bits (hs_ord)
-    int pad[8];
+    int pad[7];
 };
 static_assert(sizeof(HsCounters) == 128, "HsCounters layout");
 
@@ -869,7 +869,7 @@ __global__ __launch_bounds__(OC_T) void k_hs_assoc_b(HsArgs a) {
         if (mx > a.thr) {
             iou_lap<1024>(LapMat{mat, n_ud, n_ut, true}, a.rmatch + db, lds, lds_bytes, gws, &c->err, &c->ls,
                           a.lap_ws + (s + 1) * a.lap_ws_stride - tight_ws_bytes(), a.pre_u + db,
-                          a.pre_x + db, a.pre_s2 + db);   // row pre-pass: k_hs_ocr_pre
+                          a.pre_x + db, a.pre_s2 + db, a.thr);   // row pre-pass: k_hs_ocr_pre
 #ifdef YTA_STAMPS
             if (blockIdx.x == 0 && t == 0) {   // this solve's free rows and search steps
                 g_stamps[51] = g_stamps[100] - fr0;
@@ -1652,12 +1652,13 @@ int yta_hybridsort_lap_stats(yta_hybridsort *e, long long *stats) {
     YTA_CHECK(e && stats, YTA_ERR_INVALID, "null argument");
     const int rc = hs_read_counters(e);
     if (rc) return rc;
-    for (int k = 0; k < 3; ++k) stats[k] = 0;
+    for (int k = 0; k < 4; ++k) stats[k] = 0;
     for (int s = 0; s < e->S; ++s) {
         const LapStats &l = e->h_cnt[s].ls;
         stats[0] += l.transposed;
         stats[1] += l.uncertified;
         stats[2] += l.replays;
+        stats[3] += l.reduced;
     }
     return YTA_OK;
 }

@@ -57,7 +57,7 @@ struct OcCounters {                // one per stream
     int err;
     int lap_done;                  // first round solved by k_oc_lap this frame
     LapStats ls;                   // cumulative solver counters
-    int pad[14];
+    int pad[13];
 };
 static_assert(sizeof(OcCounters) == 128, "OcCounters layout");
 
@@ -453,7 +453,8 @@ __global__ __launch_bounds__(OC_T) void k_oc_assoc(OcArgs a) {
             sh);
         if (mx > a.thr) {
             iou_lap(LapMat{mat, n_lo, n_ut, true}, a.rmatch + db, lds, lds_bytes, gws, &c->err, &c->ls,
-                    a.lap_ws + (s + 1) * a.lap_ws_stride - tight_ws_bytes());
+                    a.lap_ws + (s + 1) * a.lap_ws_stride - tight_ws_bytes(), nullptr, nullptr,
+                    nullptr, a.thr);
             for (int k = t; k < n_ut; k += nt) a.tmp[ub + k] = 0;   // taken flags
             block_sync();
             for (int p = t; p < n_lo; p += nt) {
@@ -483,7 +484,8 @@ __global__ __launch_bounds__(OC_T) void k_oc_assoc(OcArgs a) {
             lds_bytes, &c->err, sh);
         if (mx > a.thr) {
             iou_lap(LapMat{mat, n_ud, n_ut, true}, a.rmatch + db, lds, lds_bytes, gws, &c->err, &c->ls,
-                    a.lap_ws + (s + 1) * a.lap_ws_stride - tight_ws_bytes());
+                    a.lap_ws + (s + 1) * a.lap_ws_stride - tight_ws_bytes(), nullptr, nullptr,
+                    nullptr, a.thr);
             // removed dets / trackers -> flags, then sorted set differences
             for (int i = t; i < n_hi; i += nt) a.tmp[ub + i] = 0;
             for (int j = t; j < n_trk; j += nt) a.nan_flag[tb + j] = 0;
@@ -1109,12 +1111,13 @@ int yta_ocsort_lap_stats(yta_ocsort *e, long long *stats) {
     YTA_CHECK(e && stats, YTA_ERR_INVALID, "null argument");
     const int rc = oc_read_counters(e);
     if (rc) return rc;
-    for (int k = 0; k < 3; ++k) stats[k] = 0;
+    for (int k = 0; k < 4; ++k) stats[k] = 0;
     for (int s = 0; s < e->S; ++s) {
         const LapStats &l = e->h_cnt[s].ls;
         stats[0] += l.transposed;
         stats[1] += l.uncertified;
         stats[2] += l.replays;
+        stats[3] += l.reduced;
     }
     return YTA_OK;
 }
@@ -1283,7 +1286,7 @@ __global__ __launch_bounds__(LAP_T) void k_kat_fr(const double *m, int na, int n
                                                   long long lds_bytes, unsigned char *gws, int *st,
                                                   int *n_tight, int chip) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-    LapStats ls{0, 0, 0};
+    LapStats ls{0, 0, 0, 0};
     if (threadIdx.x == 0) *n_tight = -1;
     __syncthreads();
     first_round_lap(m, na, nb, rx, rx, false, u, x, s2, rx, lds, lds_bytes, gws, st, st + 1, &ls,

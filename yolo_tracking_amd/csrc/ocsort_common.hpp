@@ -53,6 +53,7 @@ __device__ __forceinline__ double block_max(double v, OcShared &sh) {
 // unique, and lapjv replays (padded_lap, any round).
 struct LapStats {
     int transposed, uncertified, replays;
+    int reduced;   // -IoU rounds solved on their positive part (iou_lap_reduced)
 };
 
 // association.py:20-28 on the padded problem M: wave 0 solves, x[r] = column or -1 -> rx.
@@ -254,18 +255,108 @@ __device__ __forceinline__ double asso_matrix(int kind, int na, int nb, DB dbox,
     return block_max(mx, sh);
 }
 
+// The -IoU round's problem reduced to its positive part.  The padded lapjv the reference runs
+// (association.py:20-28, extend_cost: every row may stay unassigned at cost 0) maximises the summed
+// IoU, so the positive pairs of any optimum form a maximum-weight matching of the graph of
+// positive entries, and conversely; rows and columns with no positive entry only ever hold
+// zero-IoU pairs, which the caller drops (IoU < threshold, threshold > 0).  Solving the rows x
+// columns that have a positive entry (their zero entries kept) therefore keeps exactly the pairs
+// of the full solve whenever the positive part's optimum is unique - the same condition the
+// full rectangular solve relies on.  The matrix must hold only values >= 0 (IoU / GIoU as the
+// reference computes them are exactly 0 for disjoint boxes: iou.py:6-25, :52-60); anything else,
+// a reduction of less than half the entries, or a reduced matrix larger than the `tws` region
+// returns false (the caller solves the full matrix).  The OCR rounds of the steady state keep
+// ~20 of ~70 rows and a few dozen of ~1200 columns (C5): the searches of the rows that overlap
+// nothing - each a block-wide Dijkstra step over every column - disappear.
+__host__ __device__ inline long long tight_ws_bytes();   // below: the certificate's edge region
+template <int MAXT>
+__device__ __noinline__ bool iou_lap_reduced(const LapMat &M, int *rx, unsigned char *lds,
+                                             long long lds_bytes, unsigned char *gws, int *err,
+                                             unsigned char *tws) {
+    __shared__ int wsum[32];
+    __shared__ int s_bad;
+    const int t = threadIdx.x, nt = blockDim.x;
+    const int na = M.na, nb = M.nb;
+    if (na <= 0 || nb <= 0 || (long long)na + nb > lds_bytes) return false;
+    unsigned char *rf = lds, *cf = lds + na;   // positive-entry flags of rows / columns
+    for (int i = t; i < na + nb; i += nt) lds[i] = 0;
+    if (t == 0) s_bad = 0;
+    block_sync();
+    bool bad = false;
+    for (int p = 0; p < na; ++p) {   // a row at a time: no index division per entry
+        const double *row = M.m + (long long)p * nb;
+        bool any = false;
+        for (int k = t; k < nb; k += nt) {
+            const double v = row[k];
+            if (v > 0.0) {
+                any = true;
+                cf[k] = 1;
+            } else if (!(v == 0.0)) {
+                bad = true;   // negative or NaN
+            }
+        }
+        if (any) rf[p] = 1;
+    }
+    if (bad) s_bad = 1;
+    block_sync();
+    if (s_bad) return false;
+    int *ra = reinterpret_cast<int *>(tws), *ca = ra + na;
+    const int nr = block_compact(na, wsum, [&](int i) { return rf[i] != 0; },
+                                 [&](int i, int pos) { ra[pos] = i; });
+    const int nc = block_compact(nb, wsum, [&](int j) { return cf[j] != 0; },
+                                 [&](int j, int pos) { ca[pos] = j; });
+    int *rxr = ca + nb;
+    const long long mo = ((4LL * (na + nb + nr) + 15) & ~15LL);
+    if (2LL * nr * nc > (long long)na * nb || mo + 8LL * nr * nc > tight_ws_bytes() ||
+        (nr > nc ? nr : nc) > RECT_CPT_MAX * nt)
+        return false;
+    block_sync();   // ra / ca (other threads' runs) before their reads
+    if (nr == 0) {
+        for (int p = t; p < na; p += nt) rx[p] = -1;
+        block_sync();
+        return true;
+    }
+    double *R = reinterpret_cast<double *>(tws + mo);
+    for (int i = 0; i < nr; ++i) {
+        const double *row = M.m + (long long)ra[i] * nb;
+        for (int j = t; j < nc; j += nt) R[(long long)i * nc + j] = row[ca[j]];
+    }
+    block_sync();   // R in global memory: every store before the solver's loads
+    const bool tr = nr > nc;
+    const RectMat Rm = tr ? RectMat{R, nc, nr, 1, nc, true} : RectMat{R, nr, nc, nc, 1, true};
+    rect_solve<MAXT>(Rm, nullptr, nullptr, nullptr, tr, nr, rxr, lds, lds_bytes, gws, err);
+    for (int p = t; p < na; p += nt) rx[p] = -1;
+    block_sync();
+    for (int i = t; i < nr; i += nt) {
+        const int k = rxr[i];
+        rx[ra[i]] = k >= 0 ? ca[k] : -1;
+    }
+    block_sync();
+    return true;
+}
+
 // The -IoU rounds (BYTE / OCR: association.py:20-28 on -iou): only pairs with IoU >= threshold
 // survive and the leftover lists are re-sorted (np.setdiff1d), so any optimal solution gives the
-// reference's result: the rectangular solver in whichever orientation has rows <= columns.
+// reference's result: the rectangular solver in whichever orientation has rows <= columns, on the
+// positive part of the matrix when that is much smaller (iou_lap_reduced; needs `tws` and the
+// caller's keep threshold thr > 0).
 // MAXT > 256: the solver bodies inlined (a kernel that has the registers for them)
 // pu / px / ps2: the solved orientation's row pre-pass (main_lap_pre) when a grid kernel ran it,
 // else nullptr (the block runs it).
+#ifndef YTA_IOU_REDUCE
+#define YTA_IOU_REDUCE 1
+#endif
 template <int MAXT = 256>
 __device__ __forceinline__ void iou_lap(const LapMat &M, int *rx, unsigned char *lds,
                                         long long lds_bytes, unsigned char *gws, int *err,
                                         LapStats *ls, unsigned char *tws = nullptr,
                                         const double *pu = nullptr, const int *px = nullptr,
-                                        const double *ps2 = nullptr) {
+                                        const double *ps2 = nullptr, double thr = 0.0) {
+    if (YTA_IOU_REDUCE && tws && thr > 0.0 && M.neg &&
+        iou_lap_reduced<MAXT>(M, rx, lds, lds_bytes, gws, err, tws)) {
+        if (threadIdx.x == 0) ls->reduced += 1;
+        return;
+    }
     const bool tr = M.na > M.nb;
     const int rows = tr ? M.nb : M.na, cols = tr ? M.na : M.nb;
     if (cols > RECT_CPT_MAX * (int)blockDim.x) {

@@ -86,8 +86,8 @@ class DeepOCSortEngine(StreamSubset):
     def lap_stats(self):
         """Solver counters since create / reset (yta_deepocsort_lap_stats): first-round solves of the
         transposed problem (more detections than trackers), those not certified unique, and
-        lapjv replays."""
-        names = ["transposed", "uncertified", "replays"]
+        lapjv replays, -IoU rounds solved on their positive part."""
+        names = ["transposed", "uncertified", "replays", "reduced"]
         buf = (ctypes.c_longlong * len(names))()
         _lib.check(self.lib.yta_deepocsort_lap_stats(self._h, buf))
         return {k: int(buf[i]) for i, k in enumerate(names)}

@@ -85,8 +85,8 @@ class HybridSortEngine(StreamSubset):
     def lap_stats(self):
         """Solver counters since create / reset (yta_hybridsort_lap_stats): first-round solves of the
         transposed problem (more detections than trackers), those not certified unique, and
-        lapjv replays."""
-        names = ["transposed", "uncertified", "replays"]
+        lapjv replays, -IoU rounds solved on their positive part."""
+        names = ["transposed", "uncertified", "replays", "reduced"]
         buf = (ctypes.c_longlong * len(names))()
         _lib.check(self.lib.yta_hybridsort_lap_stats(self._h, buf))
         return {k: int(buf[i]) for i, k in enumerate(names)}

@@ -72,8 +72,8 @@ class OCSortEngine(StreamSubset):
     def lap_stats(self):
         """Solver counters since create / reset (yta_ocsort_lap_stats): first-round solves of the
         transposed problem (more detections than trackers), those not certified unique, and
-        lapjv replays."""
-        names = ["transposed", "uncertified", "replays"]
+        lapjv replays, -IoU rounds solved on their positive part."""
+        names = ["transposed", "uncertified", "replays", "reduced"]
         buf = (ctypes.c_longlong * len(names))()
         _lib.check(self.lib.yta_ocsort_lap_stats(self._h, buf))
         return {k: int(buf[i]) for i, k in enumerate(names)}
