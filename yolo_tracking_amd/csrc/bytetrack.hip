@@ -488,6 +488,76 @@ __device__ __forceinline__ TrkRec bt_trk_rec(const BtArgs &a, long long tb, int 
     return r;
 }
 
+// The stage-1 pool of the NEXT frame from the current tracked / lost lists (:169-178): tracked ->
+// activated (pool head, multi_predict's predicted box :35-48) / unconfirmed (current box), pool
+// tail = the lost tracks, lazily predicted (kf_xyah.hpp).  k_finish builds it at the end of every
+// frame from the rows it already has in registers (finish_next_pool); this block-per-stream form
+// (k_pool_build) rebuilds it after a reserve, which moves the records.
+__device__ __forceinline__ void s1_pool_build(const BtArgs &a, int s, PrepShared &sh) {
+    const int t = threadIdx.x;
+    BtCounters *c = a.cnt + s;
+    const long long tb = (long long)s * a.CAP;
+    // tracked -> activated (pool head, predicted box) / unconfirmed (current box) (:169-178)
+    const int n_tracked = c->n_tracked, n_lost = c->n_lost;
+    int n_act = 0, n_unc = 0;
+    for (int c0 = 0; c0 < n_tracked; c0 += PREP_CH) {
+        const int m = n_tracked - c0 < PREP_CH ? n_tracked - c0 : PREP_CH;
+        batched_for2<3>(
+            m, [&](int i) { return a.tracked[tb + c0 + i]; },
+            [&](int, int slot) { return bt_trk_rec(a, tb, slot); },
+            [&](int i, const TrkRec &r) {
+                const bool act = (r.flags & FL_ACTIVATED) != 0;
+                sh.u.t.cat[i] = act ? 1 : 2;
+                sh.u.t.slot[i] = r.slot;
+                sh.u.t.box[i] = act ? bt_pred_box(r) : xyah_mean_to_box(r.m[0], r.m[1], r.m[2], r.m[3]);
+            });
+        lds_sync();
+        const int2 au = block_compact2<false>(
+            m, sh.wsum, [&](int i) { return (int)sh.u.t.cat[i]; },
+            [&](int i, int cat, int pos) {
+                if (cat == 1) {
+                    const long long p = tb + n_act + pos;
+                    a.pool[p] = sh.u.t.slot[i];
+                    a.pool_box[p] = sh.u.t.box[i];
+                } else {
+                    const long long p = tb + n_unc + pos;
+                    a.unc[p] = sh.u.t.slot[i];
+                    a.unc_box[p] = sh.u.t.box[i];
+                }
+            });
+        n_act += au.x;
+        n_unc += au.y;
+        lds_sync();
+    }
+    // pool tail: the lost tracks, predicted (their predicts since they were lost replayed first)
+    const int fid_prev = c->frame_id;
+    batched_for2<3>(
+        n_lost, [&](int i) { return a.lost[tb + i]; },
+        [&](int, int slot) {
+            TrkRec r = bt_trk_rec(a, tb, slot);
+            r.flags = fid_prev - a.kf_frame[tb + slot];   // pending predicts (state is Lost)
+            return r;
+        },
+        [&](int i, TrkRec r) {
+            kf_predict_lost_mean(r.m, r.flags);
+            r.flags = ST_LOST;
+            a.pool[tb + n_act + i] = r.slot;
+            a.pool_box[tb + n_act + i] = bt_pred_box(r);
+        });
+    if (t == 0) {
+        c->n_act = n_act;
+        c->n_unc = n_unc;
+        c->n_pool = n_act + n_lost;
+    }
+}
+
+__global__ __launch_bounds__(PREP_T) void k_pool_build(BtArgs a) {
+    __shared__ PrepShared sh;
+    const int s = blockIdx.x;
+    if (stream_skipped(a, s)) return;
+    s1_pool_build(a, s, sh);
+}
+
 __global__ __launch_bounds__(PREP_T) void k_s1_prep(BtArgs a) {
     __shared__ PrepShared sh;
     const int s = blockIdx.x, t = threadIdx.x;
@@ -496,7 +566,7 @@ __global__ __launch_bounds__(PREP_T) void k_s1_prep(BtArgs a) {
     YTA_STAMP(0);
     YTA_BLK(0, 0);
     BtCounters *c = a.cnt + s;
-    const long long db = (long long)s * a.MAXD, tb = (long long)s * a.CAP;
+    const long long db = (long long)s * a.MAXD;
     int nd = a.det_off[s + 1] - a.det_off[s];
     if (nd > a.MAXD || nd < 0) {
         if (t == 0) atomicOr(&c->err, ERR_DET_CAPACITY);
@@ -553,62 +623,11 @@ __global__ __launch_bounds__(PREP_T) void k_s1_prep(BtArgs a) {
         lds_sync();   // the staging area is reused
     }
     YTA_STAMP(1);
-    // tracked -> activated (pool head, predicted box) / unconfirmed (current box) (:169-178)
-    const int n_tracked = c->n_tracked, n_lost = c->n_lost;
-    int n_act = 0, n_unc = 0;
-    for (int c0 = 0; c0 < n_tracked; c0 += PREP_CH) {
-        const int m = n_tracked - c0 < PREP_CH ? n_tracked - c0 : PREP_CH;
-        batched_for2<3>(
-            m, [&](int i) { return a.tracked[tb + c0 + i]; },
-            [&](int, int slot) { return bt_trk_rec(a, tb, slot); },
-            [&](int i, const TrkRec &r) {
-                const bool act = (r.flags & FL_ACTIVATED) != 0;
-                sh.u.t.cat[i] = act ? 1 : 2;
-                sh.u.t.slot[i] = r.slot;
-                sh.u.t.box[i] = act ? bt_pred_box(r) : xyah_mean_to_box(r.m[0], r.m[1], r.m[2], r.m[3]);
-            });
-        lds_sync();
-        const int2 au = block_compact2<false>(
-            m, sh.wsum, [&](int i) { return (int)sh.u.t.cat[i]; },
-            [&](int i, int cat, int pos) {
-                if (cat == 1) {
-                    const long long p = tb + n_act + pos;
-                    a.pool[p] = sh.u.t.slot[i];
-                    a.pool_box[p] = sh.u.t.box[i];
-                } else {
-                    const long long p = tb + n_unc + pos;
-                    a.unc[p] = sh.u.t.slot[i];
-                    a.unc_box[p] = sh.u.t.box[i];
-                }
-            });
-        n_act += au.x;
-        n_unc += au.y;
-        lds_sync();
-    }
-    YTA_STAMP(2);
-    // pool tail: the lost tracks, predicted (their predicts since they were lost replayed first)
-    const int fid_prev = c->frame_id;
-    batched_for2<3>(
-        n_lost, [&](int i) { return a.lost[tb + i]; },
-        [&](int, int slot) {
-            TrkRec r = bt_trk_rec(a, tb, slot);
-            r.flags = fid_prev - a.kf_frame[tb + slot];   // pending predicts (state is Lost)
-            return r;
-        },
-        [&](int i, TrkRec r) {
-            kf_predict_lost_mean(r.m, r.flags);
-            r.flags = ST_LOST;
-            a.pool[tb + n_act + i] = r.slot;
-            a.pool_box[tb + n_act + i] = bt_pred_box(r);
-        });
-    if (t == 0) {
+    if (t == 0) {   // the pool (n_act / n_unc / n_pool) was built by the last k_finish
         c->frame_id += 1;
         c->n_dets = nd;
         c->n_high = n_high;
         c->n_second = n_second;
-        c->n_act = n_act;
-        c->n_unc = n_unc;
-        c->n_pool = n_act + n_lost;
         c->n_left = 0;
         c->n_rest = 0;
         c->n_births = 0;
@@ -1875,11 +1894,12 @@ __device__ __forceinline__ void finish_body(const BtArgs &a, int s, unsigned *bi
             if (V == VAR_BYTETRACK) kf_predict_lost_mean(v.m, v.lag);
             return V == VAR_BOTSORT ? xywh_to_box(v.m) : xyah_mean_to_box(v.m[0], v.m[1], v.m[2], v.m[3]);
         };
-        auto exact_lbox = [&](int q) {
-            if (V == VAR_BYTETRACK) return a.pool_box[tb + a.l2pos[tb + q]];
-            return lbox_of(lmean_of(a.l2[tb + q]));
-        };
-        if (V == VAR_BYTETRACK)   // the predicted box stage 1 used (k_s1_prep): same mean
+        // a lost' track's box is the one stage 1 used, pool_box at its pool position: ByteTrack's
+        // lazily predicted mean (k_s1_prep / the last k_finish), BoT-SORT's predicted and warped
+        // mean (stage1_lists: the same x + v and kron(I4, R) x + t operations as k_apply's
+        // kf_predict / kf_predict_x and kf_gmc on the record, so the same bits, and no record read)
+        auto exact_lbox = [&](int q) { return a.pool_box[tb + a.l2pos[tb + q]]; };
+        if (V == VAR_BYTETRACK || V == VAR_BOTSORT)
             batched_for<4>(
                 n_l2, [&](int q) { return a.pool_box[tb + a.l2pos[tb + q]]; },
                 [&](int q, const Box &b) { lcache[q] = box_outer_f32(b); });
@@ -1926,7 +1946,13 @@ __device__ __forceinline__ void finish_body(const BtArgs &a, int s, unsigned *bi
     lds_sync();
     YTA_STAMP(6);
     // final lists (tracked, lost) and the output slots (activated tracked, in order) in one pass
-    // over tracked' (one scan of packed counts), output rows, free slots
+    // over tracked' (one scan of packed counts), output rows, free slots.  ByteTrack (split stage
+    // 1): the next frame's stage-1 pool too (NP): its head = the output slots with their predicted
+    // boxes (the output pass holds their means), the unconfirmed = the kept non-activated entries
+    // (births), the tail = the final lost list, lazily predicted - what k_s1_prep gathered from the
+    // records at the start of the next frame (s1_pool_build), from rows this kernel already reads.
+    constexpr bool NPV = V == VAR_BYTETRACK;
+    const bool NP = NPV && a.match_thresh <= 1.0;
     ar.lo = 0;   // the dedup grid is dead: its arena holds the output slot list
     int *outslot = reinterpret_cast<int *>(ar.base);
     const bool os_arena = ar.hi >= (size_t)4 * (n_t2 > 0 ? n_t2 : 1);
@@ -1960,12 +1986,15 @@ __device__ __forceinline__ void finish_body(const BtArgs &a, int s, unsigned *bi
         for (int k = 0; k < 8; ++k) {
             if (!((keep >> k) & 1u)) continue;
             const int slot = v[k].slot;
-            a.tracked[tb + pk++] = slot;
+            const int kidx = pk++;
+            a.tracked[tb + kidx] = slot;
             atomicOr(&live[slot >> 5], 1u << (slot & 31));
             if ((outb >> k) & 1u) {
                 if (os_arena) outslot[po] = slot;
                 else a.t2[tb + po] = slot;   // t2 entries < po were all read above
                 ++po;
+            } else if (NP) {
+                a.unc[tb + (kidx - po)] = slot;   // the next pool's unconfirmed, in tracked order
             }
         }
         n_tr += tot & 0xFFFF;
@@ -1985,22 +2014,72 @@ __device__ __forceinline__ void finish_body(const BtArgs &a, int s, unsigned *bi
         Box b;
         TrackMeta m;
     };
-    batched_for<4>(
-        n_out,
-        [&](int pos) {
-            const long long slot = tb + (os_arena ? outslot[pos] : a.t2[tb + pos]);
-            Row r;
-            r.b = kf_box<V>(a.kf, slot);
-            r.m = bt_meta(a, slot);
-            return r;
-        },
-        [&](int pos, const Row &r) {
-            double2 *o = reinterpret_cast<double2 *>(out + (long long)pos * 8);
-            o[0] = make_double2(r.b.x1, r.b.y1);
-            o[1] = make_double2(r.b.x2, r.b.y2);
-            o[2] = make_double2((double)r.m.id, r.m.score);
-            o[3] = make_double2(r.m.cls, (double)r.m.det_ind);
-        });
+    auto put_row = [&](int pos, const Box &b, const TrackMeta &m) {
+        double2 *o = reinterpret_cast<double2 *>(out + (long long)pos * 8);
+        o[0] = make_double2(b.x1, b.y1);
+        o[1] = make_double2(b.x2, b.y2);
+        o[2] = make_double2((double)m.id, m.score);
+        o[3] = make_double2(m.cls, (double)m.det_ind);
+    };
+    if (NPV && NP) {
+        // output rows + the next pool's head: mean (8 f64) and meta of line 0 per row
+        struct MRow {
+            double m[8];
+            TrackMeta meta;
+            int slot;
+        };
+        batched_for<2>(
+            n_out,
+            [&](int pos) {
+                MRow r;
+                r.slot = os_arena ? outslot[pos] : a.t2[tb + pos];
+                const double2 *src = reinterpret_cast<const double2 *>(a.kf + (tb + r.slot) * TRK_STRIDE);
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const double2 q = src[k];
+                    r.m[2 * k] = q.x;
+                    r.m[2 * k + 1] = q.y;
+                }
+                r.meta = bt_meta(a, tb + r.slot);
+                return r;
+            },
+            [&](int pos, const MRow &r) {
+                put_row(pos, xyah_mean_to_box(r.m[0], r.m[1], r.m[2], r.m[3]), r.meta);
+                a.pool[tb + pos] = r.slot;   // activated Tracked: multi_predict keeps vh (:35-48)
+                a.pool_box[tb + pos] = xyah_mean_to_box(r.m[0] + r.m[4], r.m[1] + r.m[5],
+                                                        r.m[2] + r.m[6], r.m[3] + r.m[7]);
+            });
+        // the next pool's unconfirmed (current box) and its tail: the final lost list, predicted
+        // through the frames since each was lost (fid - kf_frame, as s1_pool_build next frame)
+        batched_for2<4>(
+            n_tr - n_out, [&](int q) { return a.unc[tb + q]; },
+            [&](int, int sl) { return kf_box<V>(a.kf, tb + sl); },
+            [&](int q, const Box &b) { a.unc_box[tb + q] = b; });
+        batched_for2<3>(
+            n_lo, [&](int q) { return a.lost[tb + q]; },
+            [&](int, int slot) {
+                TrkRec r = bt_trk_rec(a, tb, slot);
+                r.flags = fid - a.kf_frame[tb + slot];   // pending predicts (state is Lost)
+                return r;
+            },
+            [&](int q, TrkRec r) {
+                kf_predict_lost_mean(r.m, r.flags);
+                r.flags = ST_LOST;
+                a.pool[tb + n_out + q] = r.slot;
+                a.pool_box[tb + n_out + q] = bt_pred_box(r);
+            });
+    } else {
+        batched_for<4>(
+            n_out,
+            [&](int pos) {
+                const long long slot = tb + (os_arena ? outslot[pos] : a.t2[tb + pos]);
+                Row r;
+                r.b = kf_box<V>(a.kf, slot);
+                r.m = bt_meta(a, slot);
+                return r;
+            },
+            [&](int pos, const Row &r) { put_row(pos, r.b, r.m); });
+    }
     YTA_STAMP(8);
     // free slots in cyclic order from the slot after this frame's last birth: births then take
     // ascending slots across frames, so the tracked list (survivors in order, births appended)
@@ -2028,6 +2107,11 @@ __device__ __forceinline__ void finish_body(const BtArgs &a, int s, unsigned *bi
         c->slot_cursor = cur;
         c->n_out = n_out;
         if (a.out_counts) a.out_counts[s] = n_out;
+        if (NP) {   // the next frame's stage-1 pool (built above)
+            c->n_act = n_out;
+            c->n_unc = n_tr - n_out;
+            c->n_pool = n_out + n_lo;
+        }
     }
 }
 
@@ -2773,6 +2857,11 @@ int reserve(yta_bytetrack *e, int cap, int maxd) {
     n->h_cnt = nullptr;
     n->stream = nullptr;
     delete n;
+    if (e->variant == VAR_BYTETRACK && e->a.match_thresh <= 1.0) {
+        // the next frame's stage-1 pool (k_finish builds it each frame) from the moved records
+        hipLaunchKernelGGL(k_pool_build, dim3(e->S), dim3(PREP_T), 0, e->stream, e->a);
+        YTA_HIP(hipGetLastError());
+    }
     return YTA_OK;
 }
 
