@@ -791,8 +791,16 @@ def main():
                          # every kernel of every engine: measured HBM bytes per step / step time
                          "chip_gbs": (step_traffic / (ms_per_step * 1e-3) / 1e9
                                       if step_traffic else None),
-                         "beside": {p: per_kernel[p] for p in ("s1_edges", "finish")
-                                    if p != dom},
+                         "beside": {p: dict(per_kernel[p], timed_ms=phase_ms[p],
+                                            timed_share=(phase_ms[p] / ms_per_step
+                                                         if ms_per_step > 0 else None))
+                                    for p in ("s1_edges", "finish") if p != dom},
+                         "timed_share": {p: (phase_ms[p] / ms_per_step if ms_per_step > 0
+                                             else None) for p in PHASES},
+                         "timed_share_note": "each kernel's average launch in the timed region "
+                                             "(engine 0's HIP events; the engines' launches "
+                                             "overlap, so the shares sum to more than 1) / "
+                                             "ms_per_step",
                          "overlapped": (None if Q == 1 else {
                              "avg_launch_ms": phase_ms[dom],
                              "frac": (kernel_bytes(dom, st_launch) / (phase_ms[dom] * 1e-3) / 1e9

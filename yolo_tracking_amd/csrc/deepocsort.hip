@@ -52,7 +52,7 @@ struct DocTrack {
 
 struct DocCounters {
     long long next_id;
-    int frame;
+    unsigned long long ocr_max;    // k_doc_ocr -> k_doc_assoc_b: the OCR matrix's maximum (hs_ord)
     int n_trk, n_free;
     int n_dets, n_high, n_out, n_births;
     int lap_calls, fast_path;
@@ -61,7 +61,10 @@ struct DocCounters {
     int lap_done;                  // first round solved by k_doc_lap this frame
     int n_ud, n_upd;               // k_doc_assoc -> k_doc_finish: unmatched detections, updates
     LapStats ls;                   // cumulative solver counters
-    int pad[11];
+    int frame;
+    int n_ut;                      // k_doc_assoc -> k_doc_ocr -> k_doc_assoc_b: OCR round columns
+    int ocr_nan;                   // the OCR matrix holds a NaN (its max is then NaN)
+    int pad[8];
 };
 static_assert(sizeof(DocCounters) == 128, "DocCounters layout");
 
@@ -739,12 +742,80 @@ __global__ __launch_bounds__(OC_T) void k_doc_assoc(DocArgs a) {
         block_sync();
     }
     YTA_STAMP(2);
-    // ---- OCR round (:470-493): asso_func(left dets, last observations), no embedding term
+    // the OCR round's matrix is filled chip-wide (k_doc_ocr); k_doc_assoc_b solves the round
+    if (t == 0) {
+        c->n_ud = n_ud;
+        c->n_ut = n_ut;
+        c->ocr_nan = 0;
+        c->ocr_max = 0ull;
+    }
+}
+
+// Order-preserving bits of a double (larger value, larger bits), for the OCR matrix's maximum.
+__device__ __forceinline__ unsigned long long doc_ord(double v) {
+    const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+    return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+}
+__device__ __forceinline__ double doc_unord(unsigned long long o) {
+    const unsigned long long b = (o >> 63) ? (o & 0x7FFFFFFFFFFFFFFFull) : ~o;
+    return __longlong_as_double((long long)b);
+}
+
+// OCR round matrix (:470-493): asso_func(left dets, last observations) over the chip, one entry
+// per thread, with its maximum (np.max: NaN-propagating) for k_doc_assoc_b.  In the block it was
+// one thread per ~60 entries of f64 GIoU (C4: ~40 x 400 entries, ~90 us for the round).
+__global__ __launch_bounds__(256) void k_doc_ocr(DocArgs a) {
+    __shared__ OcShared sh;
+    const int s = blockIdx.y;
+    if (a.active && !a.active[s]) return;
+    DocCounters *c = a.cnt + s;
+    const int n_ud = c->n_ud, n_ut = c->n_ut;
+    if (n_ud <= 0 || n_ut <= 0) return;
+    const long long tb = (long long)s * a.CAP, db = (long long)s * a.MAXD, mb = doc_mb(a, s);
+    const long long ub = (long long)s * (a.MAXD + a.CAP);
+    const double *din = a.det_in + (long long)a.det_off[s] * 6;
+    const int *udet = a.udet + ub, *utrk = a.utrk + ub;
+    double *mat = a.mat + mb;
+    const long long nm = (long long)n_ud * n_ut;
+    double mx = -INFINITY;
+    bool bad = false, nan = false;
+    for (long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x; q < nm;
+         q += (long long)gridDim.x * blockDim.x) {
+        const int p = (int)(q / n_ut), k = (int)(q % n_ut);
+        const Box db_ = box5(din + (long long)a.hi_row[db + udet[p]] * 6);
+        const Box tb_ = box5(a.clast + (tb + utrk[k]) * 5);
+        const double v = asso_of(a.asso, db_, tb_, 0.0, 0.0);
+        bad |= a.asso == 1 && v != v;
+        nan |= v != v;
+        mat[q] = v;
+        if (v == v) mx = v > mx ? v : mx;
+    }
+    if (bad) atomicOr(&c->err, ERR_GIOU);
+    if (nan) atomicOr(&c->ocr_nan, 1);
+    mx = block_max(mx, sh);
+    if (threadIdx.x == 0 && mx > -INFINITY) atomicMax(&c->ocr_max, doc_ord(mx));
+}
+
+// The OCR round's solve (:470-493) after k_doc_ocr, then the update jobs.
+__global__ __launch_bounds__(OC_T) void k_doc_assoc_b(DocArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    __shared__ OcShared sh;
+    const int s = blockIdx.x, t = threadIdx.x, nt = blockDim.x;
+    if (a.active && !a.active[s]) return;   // stream not updated this frame
+    DocCounters *c = a.cnt + s;
+    const long long tb = (long long)s * a.CAP, db = (long long)s * a.MAXD, mb = doc_mb(a, s);
+    const long long ub = (long long)s * (a.MAXD + a.CAP);
+    unsigned char *gws = a.lap_ws + s * a.lap_ws_stride;
+    const long long lds_bytes = oc_lds_bytes(a.CAP, a.MAXD);
+    const int n_trk = c->n_trk;
+    const int n_hi = c->n_high;
+    int *list = a.list + tb;
+    double *mat = a.mat + mb;
+    int *udet = a.udet + ub, *utrk = a.utrk + ub;
+    int n_ud = c->n_ud, n_ut = c->n_ut;
+    YTA_STAMP_BASE(40);
     if (n_ud > 0 && n_ut > 0) {
-        const double mx = asso_matrix(
-            a.asso, n_ud, n_ut, [&](int p) { return hbox(udet[p]); },
-            [&](int k) { return box5(a.clast + (tb + utrk[k]) * 5); }, 0.0, 0.0, mat, lds, lds_bytes,
-            &c->err, sh);
+        const double mx = c->ocr_nan ? NAN : doc_unord(c->ocr_max);
         if (mx > a.thr) {
             iou_lap(LapMat{mat, n_ud, n_ut, true}, a.rmatch + db, lds, lds_bytes, gws, &c->err, &c->ls,
                     a.lap_ws + (s + 1) * a.lap_ws_stride - tight_ws_bytes(), nullptr, nullptr,
@@ -805,6 +876,8 @@ __global__ __launch_bounds__(DOC_TRK_T) void k_doc_upd(DocArgs a) {
                a.delta_t);
 }
 
+constexpr int DOC_BIRTH_CH = 16;   // births staged in LDS at a time (k_doc_finish)
+
 // Births, outputs, removal (deep_ocsort.py:495-520), after k_doc_upd.
 __global__ __launch_bounds__(OC_T) void k_doc_finish(DocArgs a) {
     __shared__ OcShared sh;
@@ -835,13 +908,32 @@ __global__ __launch_bounds__(OC_T) void k_doc_finish(DocArgs a) {
         n_b = n_free;
     }
     const long long next_id = c->next_id;
-    for (int b = t; b < n_b; b += nt) {
-        const int slot = a.free_list[tb + n_free - 1 - b];
-        const double *dr = din + (long long)a.hi_row[db + udet[b]] * 6;
-        doc_birth(a.rec[tb + slot], dr, next_id + b, a.hi_row[db + udet[b]]);
-        list[n_trk + b] = slot;
-        a.ema_slot[eb + n_upd + b] = slot;
-        a.ema_row[eb + n_upd + b] = ~udet[b];   // birth: copy the detection's embedding
+    // a birth's 1216-B record is built in LDS by its thread and stored by the whole block in
+    // 16-B pieces, consecutive lanes on consecutive pieces: one thread storing its record word by
+    // word beside the others' made every store instruction touch a line per birth (C4: ~33 us for
+    // 33 births)
+    static_assert(sizeof(DocTrack) % 16 == 0, "DocTrack is stored in 16-B pieces");
+    constexpr int REC_Q = (int)(sizeof(DocTrack) / 16);
+    __shared__ DocTrack bstage[DOC_BIRTH_CH];
+    for (int b0 = 0; b0 < n_b; b0 += DOC_BIRTH_CH) {
+        const int m = n_b - b0 < DOC_BIRTH_CH ? n_b - b0 : DOC_BIRTH_CH;
+        for (int r = t; r < m; r += nt) {
+            const int b = b0 + r;
+            const int slot = a.free_list[tb + n_free - 1 - b];
+            const double *dr = din + (long long)a.hi_row[db + udet[b]] * 6;
+            doc_birth(bstage[r], dr, next_id + b, a.hi_row[db + udet[b]]);
+            list[n_trk + b] = slot;
+            a.ema_slot[eb + n_upd + b] = slot;
+            a.ema_row[eb + n_upd + b] = ~udet[b];   // birth: copy the detection's embedding
+        }
+        lds_sync();
+        for (int q = t; q < m * REC_Q; q += nt) {
+            const int r = q / REC_Q, k = q - r * REC_Q;
+            const int slot = a.free_list[tb + n_free - 1 - (b0 + r)];
+            reinterpret_cast<double2 *>(&a.rec[tb + slot])[k] =
+                reinterpret_cast<const double2 *>(&bstage[r])[k];
+        }
+        lds_sync();
     }
     n_free -= n_b;
     n_trk += n_b;
@@ -1099,6 +1191,9 @@ int doc_alloc(yta_deepocsort *e) {
     YTA_HIP(hipFuncSetAttribute((const void *)k_doc_assoc,
                                 hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)dense_lap_ws_bytes(OC_LDS_LAP_N)));
+    YTA_HIP(hipFuncSetAttribute((const void *)k_doc_assoc_b,
+                                hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)dense_lap_ws_bytes(OC_LDS_LAP_N)));
     return YTA_OK;
 }
 
@@ -1173,6 +1268,11 @@ int doc_launch(yta_deepocsort *e, const double *d_dets, const int *d_off, const 
                        e->stream, a);
     YTA_HIP(hipGetLastError());
     hipLaunchKernelGGL(k_doc_assoc, dim3(a.S), dim3(OC_T), e->lds, e->stream, a);
+    YTA_HIP(hipGetLastError());
+    hipLaunchKernelGGL(k_doc_ocr, dim3((unsigned)std::max(4, 2048 / a.S), a.S), dim3(256), 0,
+                       e->stream, a);
+    YTA_HIP(hipGetLastError());
+    hipLaunchKernelGGL(k_doc_assoc_b, dim3(a.S), dim3(OC_T), e->lds, e->stream, a);
     YTA_HIP(hipGetLastError());
     hipLaunchKernelGGL(k_doc_upd, dim3((a.CAP + DOC_TRK_T - 1) / DOC_TRK_T, a.S), dim3(DOC_TRK_T), 0,
                        e->stream, a);

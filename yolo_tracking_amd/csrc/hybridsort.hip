@@ -915,14 +915,35 @@ __global__ __launch_bounds__(OC_T) void k_hs_assoc_b(HsArgs a) {
         n_b = n_free;
     }
     const long long next_id = c->next_id;
-    for (int b = t; b < n_b; b += nt) {
-        const int slot = a.free_list[tb + n_free - 1 - b];
-        const int p = udet[b];
-        hs_birth(a.rec[tb + slot], hrow(p), din[(long long)p * 6 + 5], din[(long long)p * 6 + 4],
-                 next_id + b);
-        list[n_trk + b] = slot;
-        a.ema_slot[eb + n_upd + b] = slot;
-        a.ema_row[eb + n_upd + b] = ~p;
+    // a birth's record is built in LDS (the solver's arena is free by now) by its thread and
+    // stored by the whole block in 16-B pieces, consecutive lanes on consecutive pieces (one
+    // thread storing its record word by word beside the others' touched a line per birth and
+    // store instruction); 8-B pieces (the record is a multiple of 8 B)
+    static_assert(sizeof(HsTrack) % 8 == 0, "HsTrack is stored in 8-B pieces");
+    constexpr int REC_Q = (int)(sizeof(HsTrack) / 8);
+    HsTrack *bstage = reinterpret_cast<HsTrack *>(lds);
+    int bch = (int)(lds_bytes / (long long)sizeof(HsTrack));
+    bch = bch < 1 ? 1 : (bch > nt ? nt : bch);
+    for (int b0 = 0; b0 < n_b; b0 += bch) {
+        const int m = n_b - b0 < bch ? n_b - b0 : bch;
+        for (int r = t; r < m; r += nt) {
+            const int b = b0 + r;
+            const int slot = a.free_list[tb + n_free - 1 - b];
+            const int p = udet[b];
+            hs_birth(bstage[r], hrow(p), din[(long long)p * 6 + 5], din[(long long)p * 6 + 4],
+                     next_id + b);
+            list[n_trk + b] = slot;
+            a.ema_slot[eb + n_upd + b] = slot;
+            a.ema_row[eb + n_upd + b] = ~p;
+        }
+        lds_sync();
+        for (int q = t; q < m * REC_Q; q += nt) {
+            const int r = q / REC_Q, k = q - r * REC_Q;
+            const int slot = a.free_list[tb + n_free - 1 - (b0 + r)];
+            reinterpret_cast<double *>(&a.rec[tb + slot])[k] =
+                reinterpret_cast<const double *>(&bstage[r])[k];
+        }
+        lds_sync();
     }
     n_free -= n_b;
     n_trk += n_b;

@@ -528,7 +528,18 @@ __global__ __launch_bounds__(OC_T) void k_oc_assoc(OcArgs a) {
         n_b = n_free;
     }
     const long long next_id = c->next_id;
-    for (int b = t; b < n_b; b += nt) {
+    // a birth's record is built in LDS (the solver's arena is free by now) by its thread and
+    // stored by the whole block in 8-B pieces, consecutive lanes on consecutive pieces (one thread
+    // storing its record word by word beside the others' touched a line per birth and store)
+    static_assert(sizeof(OcTrack) % 8 == 0, "OcTrack is stored in 8-B pieces");
+    constexpr int REC_Q = (int)(sizeof(OcTrack) / 8);
+    OcTrack *bstage = reinterpret_cast<OcTrack *>(lds);
+    int bch = (int)(lds_bytes / (long long)sizeof(OcTrack));
+    bch = bch < 1 ? 1 : (bch > nt ? nt : bch);
+    for (int b0 = 0; b0 < n_b; b0 += bch) {
+      const int mb_ = n_b - b0 < bch ? n_b - b0 : bch;
+      for (int rr = t; rr < mb_; rr += nt) {
+        const int b = b0 + rr;
         const int slot = a.free_list[tb + n_free - 1 - b];
         const double *dr = din + (long long)a.hi_row[db + udet[b]] * 6;
         OcTrack r;
@@ -548,8 +559,17 @@ __global__ __launch_bounds__(OC_T) void k_oc_assoc(OcArgs a) {
         r.age = r.hits = r.hit_streak = r.tsu = 0;
         r.flags = 0;
         r.hist_since = 0;
-        a.rec[tb + slot] = r;
+        bstage[rr] = r;
         list[n_trk + b] = slot;
+      }
+      lds_sync();
+      for (int q = t; q < mb_ * REC_Q; q += nt) {
+        const int r = q / REC_Q, k = q - r * REC_Q;
+        const int slot = a.free_list[tb + n_free - 1 - (b0 + r)];
+        reinterpret_cast<double *>(&a.rec[tb + slot])[k] =
+            reinterpret_cast<const double *>(&bstage[r])[k];
+      }
+      lds_sync();
     }
     n_free -= n_b;
     n_trk += n_b;
