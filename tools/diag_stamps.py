@@ -60,6 +60,8 @@ def main():
     ap.add_argument("--frames", type=int, default=6)
     ap.add_argument("--lib", default=OUT, help="diagnostic library to build / load")
     ap.add_argument("--flags", default="", help="extra compile flags (build)")
+    ap.add_argument("--tracker", choices=["bytetrack", "botsort"], default="bytetrack",
+                    help="botsort: C3's engine (ReID D=512, botsort.yaml, one stream per frame)")
     args = ap.parse_args()
     if args.build:
         build(args.lib, args.flags.split())
@@ -72,10 +74,21 @@ def main():
     _lib._lib = lib
     from yolo_tracking_amd import ByteTrackEngine
     S = args.streams
-    base = [d for d, _ in make_frames(1024, args.frames, seed=5)]
-    eng = ByteTrackEngine(S, 0.5, 0.8, 30, 30, track_capacity=2048, max_dets=1024)
-    for f in range(args.frames):
-        eng.update([base[f]] * S)
+    if args.tracker == "botsort":
+        sys.path.insert(0, os.path.join(REPO, "tools"))
+        from bench_tracker import BOTSORT_YAML, reid_rows
+        from yolo_tracking_amd.trackers.botsort import BoTSORTEngine
+        fr = make_frames(1024, args.frames, seed=5, emb_dim=512)
+        eng = BoTSORTEngine(S, feat_dim=512, **BOTSORT_YAML, track_capacity=2048, max_dets=1024)
+        thr = BOTSORT_YAML["track_high_thresh"]
+        for f in range(args.frames):
+            d, e = fr[f]
+            eng.update([d] * S, [reid_rows(d, e, thr)] * S)
+    else:
+        base = [d for d, _ in make_frames(1024, args.frames, seed=5)]
+        eng = ByteTrackEngine(S, 0.5, 0.8, 30, 30, track_capacity=2048, max_dets=1024)
+        for f in range(args.frames):
+            eng.update([base[f]] * S)
     st = np.zeros(128, dtype=np.uint64)
     _lib.check(lib.yta_debug_stamps(st.ctypes.data))
     st = st.astype(np.int64)
