@@ -106,7 +106,8 @@ def main():
         print("  stage-1 LAP: n16 %d n64 %d nbig %d edges %d complex nodes %d" % tuple(st[15:20]))
     show(st, 20, {4: "left/rest lists", **{k: v for k, v in STAGE1.items() if k >= 5}},
          "k_stage23 stage 2")
-    show(st, 40, {k: v for k, v in STAGE1.items() if k >= 5}, "k_stage23 stage 3")
+    show(st, 40, {1: "grid build", 2: "pass A (boxes)", 3: "pass B (features)",
+                  **{k: v for k, v in STAGE1.items() if k >= 8}, 15: "end"}, "k_stage23 stage 3")
     show(st, 80, {1: "zero bits", 2: "births", 3: "expiry", 4: "t2/l2 lists", 5: "dedup grid",
                   6: "dedup queries", 7: "final lists", 8: "output rows", 9: "free list"},
          "k_finish")

@@ -250,7 +250,23 @@ template <typename ColElem>
 __device__ __forceinline__ double cosine_dist16(const float *u, ColElem v, int D) {
     const int l16 = lane_id() & 15;
     double d = 0.0, nu = 0.0, nv = 0.0;
-    for (int k = l16; k < D; k += 16) {
+    constexpr int CB = 16;   // elements per lane loaded before any is used (one round trip)
+    int k = l16;
+    for (; k + 16 * (CB - 1) < D; k += 16 * CB) {
+        float ua[CB], va[CB];
+#pragma unroll
+        for (int j = 0; j < CB; ++j) ua[j] = u[k + 16 * j];
+#pragma unroll
+        for (int j = 0; j < CB; ++j) va[j] = v(k + 16 * j);
+#pragma unroll
+        for (int j = 0; j < CB; ++j) {   // the same order of operations as the scalar loop
+            const double a = (double)ua[j], b = (double)va[j];
+            d += a * b;
+            nu += a * a;
+            nv += b * b;
+        }
+    }
+    for (; k < D; k += 16) {
         const double a = (double)u[k], b = (double)v(k);
         d += a * b;
         nu += a * a;
@@ -327,6 +343,7 @@ __device__ __forceinline__ bool assoc_block_emb(int nr, RowBox rowbox, int nc, C
             nc, colbox, [&](int j) { return fused ? colscore(j) : 1.0; }, gv, sh.gs, sh.lap.wsum);
     }
     block_sync();
+    YTA_STAMP(1);
     const GridHdr gh = sh.gs.hdr;
     auto push_edge = [&](int i, int j, double c) {
         const int p = atomicAdd(&sh.lap.cnt[1], 1);
@@ -370,15 +387,37 @@ __device__ __forceinline__ bool assoc_block_emb(int nr, RowBox rowbox, int nc, C
         }
     }
     block_sync();
+    YTA_STAMP(2);
     if (sh.lap.cnt[2]) return false;
     const int n_pend = sh.lap.cnt[0];
-    // pass B: appearance cost of the pending pairs, one 16-lane group each
+    // pass B: appearance cost of the pending pairs, one 16-lane group each.  The feature rows'
+    // addresses (index chains through the stream's lists) are resolved for every pair first, a
+    // thread per pair, where the pending list's reserved span has room
     {
+        using CF = decltype(colfeat(0));
+        struct RC {
+            const float *r;
+            CF c;
+        };
+        // after the pending list's used entries, inside its reserved span
+        RC *rcs = reinterpret_cast<RC *>(((uintptr_t)(pend + n_pend) + 15) & ~(uintptr_t)15);
+        const bool pre = (uintptr_t)(rcs + n_pend) <= (uintptr_t)(pend + pcap);
+        if (pre) {
+            batched_for<4>(
+                n_pend,
+                [&](int p) {
+                    const int2 ij = pend[p];
+                    return RC{rowfeat(ij.x), colfeat(ij.y)};
+                },
+                [&](int p, const RC &v) { rcs[p] = v; });
+            block_sync();
+        }
         const int groups = nt / 16, g = t / 16;
         for (int p = g; p < n_pend; p += groups) {
             const int2 ij = pend[p];
-            const auto cf = colfeat(ij.y);
-            const double cd = cosine_dist16(rowfeat(ij.x), cf, D);
+            const RC rc = pre ? rcs[p] : RC{rowfeat(ij.x), colfeat(ij.y)};
+            const auto &cf = rc.c;
+            const double cd = cosine_dist16(rc.r, cf, D);
             if ((lane_id() & 15) == 0) {
                 double emb = np_max(0.0, cd) / 2.0;                 // matching.py:164-166
                 if (emb > app) emb = 1.0;                           // bot_sort.py:318
@@ -391,6 +430,7 @@ __device__ __forceinline__ bool assoc_block_emb(int nr, RowBox rowbox, int nc, C
         }
     }
     block_sync();
+    YTA_STAMP(3);
     if (sh.lap.cnt[2]) return false;
     const int E = sh.lap.cnt[1];
     if (t == 0) *n_edges = E;

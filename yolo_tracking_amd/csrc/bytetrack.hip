@@ -338,6 +338,7 @@ __device__ __forceinline__ bool stage23_body(const BtArgs &a, int s, Arena &ar, 
     if (!ok) return false;
     ar.reset();
     YTA_STAMP_BASE(40);
+    YTA_STAMP(0);
     if (V == VAR_BOTSORT && a.D > 0)   // bot_sort.py:355-370
         ok = assoc_block_emb(
             n_unc, [&](int j) { return a.unc_box[tb + j]; }, n_rest,
@@ -354,6 +355,7 @@ __device__ __forceinline__ bool stage23_body(const BtArgs &a, int s, Arena &ar, 
             [&](int r) { return a.rest_score[db + r]; }, 0.7, a.x3 + tb, a.y3 + db, &c->err,
             &c->n_edges[2], ar, slab, sh.as);
     if (!ok) return false;
+    YTA_STAMP(15);
     if (t == 0) {
         c->n_left = n_left;
         c->n_rest = n_rest;
@@ -1192,6 +1194,89 @@ __global__ __launch_bounds__(BLKL, 4) void k_s1_lap(BtArgs a) {
     YTA_BLK(2, 1);
 }
 
+// ------------------------------------------------------------------------------ k_feat / k_ema
+// BoT-SORT features, one wave per row.  Norms follow np.linalg.norm on a float32 row (the sum of
+// squares rounded to float32, then sqrt in float32); the sum is accumulated in float64 here,
+// where OpenBLAS sdot accumulates in float32 lanes, so a norm may differ from the reference's in
+// its last bit (the parity tests compare features with a tolerance).
+__device__ __forceinline__ float f32_norm(double sumsq) { return sqrtf((float)sumsq); }
+
+// k_feat: per high detection (conf > track_high_thresh, the stage-1 predicate) the norms of the
+// in-place normalisations the reference applies to its row: n1 = |e|, n2 = |e/n1| (STrack
+// construction, :40-48) and n3 = |(e/n1)/n2| (when a track takes it, :40-41).
+constexpr int FEAT_T = 256;
+__host__ __device__ __forceinline__ int feat_blocks(int maxd) {
+    return (maxd + FEAT_T / WAVE - 1) / (FEAT_T / WAVE);
+}
+__device__ __forceinline__ void feat_body(const BtArgs &a, int s, int bx) {
+    const int lane = lane_id();
+    if (stream_skipped(a, s)) return;
+    const int d = bx * (FEAT_T / WAVE) + threadIdx.x / WAVE;
+    const int nd = min(a.det_off[s + 1] - a.det_off[s], a.MAXD);
+    if (d >= nd) return;
+    const long long row = (long long)a.det_off[s] + d;
+    if (!(a.det_in[row * 6 + 4] > a.track_thresh)) return;
+    const float *e = a.det_feat + row * a.D;
+    double q = 0.0;
+    for (int k = lane; k < a.D; k += WAVE) q += (double)e[k] * (double)e[k];
+    const float n1 = f32_norm(wave_reduce(RED_SUM, q));
+    q = 0.0;
+    for (int k = lane; k < a.D; k += WAVE) {
+        const float f = e[k] / n1;
+        q += (double)f * (double)f;
+    }
+    const float n2 = f32_norm(wave_reduce(RED_SUM, q));
+    q = 0.0;
+    for (int k = lane; k < a.D; k += WAVE) {
+        const float f = (e[k] / n1) / n2;
+        q += (double)f * (double)f;
+    }
+    const float n3 = f32_norm(wave_reduce(RED_SUM, q));
+    if (lane == 0) {
+        float *fn = a.det_fn + ((long long)s * a.MAXD + d) * 4;
+        fn[0] = n1;
+        fn[1] = n2;
+        fn[2] = n3;
+        fn[3] = 0.f;
+    }
+}
+__global__ __launch_bounds__(FEAT_T) void k_feat(BtArgs a) { feat_body(a, blockIdx.y, blockIdx.x); }
+
+// k_ema: update_features of every track that took a high detection this frame (bot_sort.py:40-48):
+// f = curr / |curr| with curr = (e/n1)/n2, smooth = 0.9 * smooth + 0.1 * f (float32), then
+// smooth /= |smooth|.
+constexpr int EMA_T = 256;
+__host__ __device__ __forceinline__ int ema_blocks(int cap) {
+    return (cap + EMA_T / WAVE - 1) / (EMA_T / WAVE);
+}
+__device__ __forceinline__ void ema_body(const BtArgs &a, int s, int bx) {
+    const int lane = lane_id();
+    if (stream_skipped(a, s)) return;
+    const BtCounters *c = a.cnt + s;
+    const int n_pool = c->n_pool, n_items = n_pool + c->n_unc;
+    const int item = bx * (EMA_T / WAVE) + threadIdx.x / WAVE;
+    if (item >= n_items) return;
+    const long long tb = (long long)s * a.CAP, db = (long long)s * a.MAXD;
+    const int h = a.ema_job[tb + item];
+    if (h < 0) return;
+    const int slot = item < n_pool ? a.pool[tb + item] : a.unc[tb + item - n_pool];
+    const int d = a.high[db + h];
+    const float *fn = a.det_fn + (db + d) * 4;
+    const float n1 = fn[0], n2 = fn[1], n3 = fn[2];
+    const float *e = a.det_feat + ((long long)a.det_off[s] + d) * a.D;
+    float *sm = a.feat + (tb + slot) * a.D;
+    double q = 0.0;
+    for (int k = lane; k < a.D; k += WAVE) {
+        const float f = ((e[k] / n1) / n2) / n3;
+        const float v = 0.9f * sm[k] + 0.1f * f;
+        sm[k] = v;
+        q += (double)v * (double)v;
+    }
+    const float nrm = f32_norm(wave_reduce(RED_SUM, q));
+    for (int k = lane; k < a.D; k += WAVE) sm[k] = sm[k] / nrm;
+}
+__global__ __launch_bounds__(EMA_T) void k_ema(BtArgs a) { ema_body(a, blockIdx.y, blockIdx.x); }
+
 // ------------------------------------------------------------ BoT-SORT stage 1, split (C3)
 // With ReID features, k_stage1's block per stream spends most of a few-stream frame on the
 // appearance costs of the candidate pairs (bot_sort.py:307-322: ~2.5 D-long dot products per pool
@@ -1210,6 +1295,11 @@ constexpr int BSE_T = 256;   // k_bs_edges threads: 4 waves = 4 pool rows per bl
 
 __global__ __launch_bounds__(PREP_T) void k_bs_prep(BtArgs a) {
     __shared__ StageShared sh;
+    if ((int)blockIdx.x >= a.S) {   // k_feat's blocks, launched with this grid (independent work)
+        const int b = blockIdx.x - a.S, fb = feat_blocks(a.MAXD);
+        feat_body(a, b / fb, b % fb);
+        return;
+    }
     const int s = blockIdx.x;
     if (stream_skipped(a, s)) return;
     Arena none(nullptr, 0);   // no staged high boxes (the embedding association does not use them)
@@ -1221,7 +1311,17 @@ __global__ __launch_bounds__(PREP_T) void k_bs_prep(BtArgs a) {
     }
 }
 
+// A pool row's pairs that need the appearance cost (inside proximity_thresh) are queued per wave
+// while the row's column passes run, then costed four at a time (one 16-lane group each) with their
+// feature rows' loads in flight together, instead of one dependent chain per column pass.
+constexpr int BS_PQ = 64;   // queued pairs per wave (a full queue is costed before more are added)
+struct BsPend {
+    int j, dj;   // high position, detection index
+    double cc;   // the (fused) IoU cost
+};
+
 __global__ __launch_bounds__(BSE_T) void k_bs_edges(BtArgs a) {
+    __shared__ BsPend pq[BSE_T / WAVE][BS_PQ];
     const int s = blockIdx.y;
     if (stream_skipped(a, s)) return;
     BtCounters *c = a.cnt + s;
@@ -1231,11 +1331,14 @@ __global__ __launch_bounds__(BSE_T) void k_bs_edges(BtArgs a) {
     const int lane = lane_id(), grp = lane >> 4;
     const long long tb = (long long)s * a.CAP, db = (long long)s * a.MAXD;
     const long long SC = (long long)a.S * a.CAP;
+    const long long doff = a.det_off[s];
     const double prox = a.prox_thresh, app = a.app_thresh, thresh = a.match_thresh;
     const bool fused = a.fuse_first != 0;
     const Box rb = a.pool_box[tb + i];
     const float *rfeat = a.feat + (tb + a.pool[tb + i]) * a.D;
-    int n = 0;   // the row's edges (wave-uniform)
+    BsPend *q = pq[threadIdx.x / WAVE];
+    int n = 0;    // the row's edges (wave-uniform)
+    int nq = 0;   // queued pairs (wave-uniform)
     auto put = [&](bool e, int j, double cost) {   // edges of this pass in lane order
         const unsigned long long m = __ballot(e);
         if (e) {
@@ -1247,12 +1350,52 @@ __global__ __launch_bounds__(BSE_T) void k_bs_edges(BtArgs a) {
         }
         n += __popcll(m);
     };
+    auto flush = [&]() {   // the queued pairs' appearance costs, four at a time
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+        for (int p0 = 0; p0 < nq; p0 += 4) {
+            const int p = p0 + grp;
+            const bool v = p < nq;
+            const BsPend e = q[v ? p : p0];
+            const float *fn = a.det_fn + (db + e.dj) * 4;
+            const DetFeat f{a.det_feat + (doff + e.dj) * a.D, fn[0], fn[1]};
+            const double cd = cosine_dist16(rfeat, f, a.D);
+            double cost = 1.0;
+            if (v) {
+                double emb = np_max(0.0, cd) / 2.0;                           // matching.py:164-166
+                if (emb > app) emb = 1.0;                                       // bot_sort.py:318
+                cost = np_min(e.cc, emb);                                       // bot_sort.py:320
+            }
+            put((lane & 15) == 0 && v && cost < thresh, e.j, cost);
+        }
+        __builtin_amdgcn_wave_barrier();   // the queue is rewritten next
+        nq = 0;
+    };
+    constexpr int BOX_BATCH = 4;   // column boxes of 4 passes loaded at once (one round trip)
+    Box cbs[BOX_BATCH];
+    int hds[BOX_BATCH];   // the columns' detection indices (their feature rows), loaded alongside
     for (int j0 = 0; j0 < nh; j0 += WAVE) {
         const int j = j0 + lane;
+        const int kb = (j0 / WAVE) % BOX_BATCH;
+        if (kb == 0) {
+#pragma unroll
+            for (int k = 0; k < BOX_BATCH; ++k) {
+                const int jk = j + k * WAVE < nh ? j + k * WAVE : 0;
+                cbs[k] = a.high_box[db + jk];
+                hds[k] = a.high[db + jk];
+            }
+        }
+        Box cb = cbs[0];
+        int hd = hds[0];
+#pragma unroll
+        for (int k = 1; k < BOX_BATCH; ++k)
+            if (kb == k) {
+                cb = cbs[k];
+                hd = hds[k];
+            }
         bool hit = false;
         double d = 1.0, cc = 1.0;
         if (j < nh) {
-            const Box cb = a.high_box[db + j];
             if (intersects(rb, cb)) {
                 hit = true;
                 d = 1 - iou(rb, cb);                                        // matching.py:117
@@ -1262,30 +1405,15 @@ __global__ __launch_bounds__(BSE_T) void k_bs_edges(BtArgs a) {
         const bool masked = hit && d > prox;                               // emb masked (:319)
         const double mc = np_min(cc, 1.0);
         put(masked && mc < thresh, j, mc);
-        // pairs that need the appearance cost: four at a time, one 16-lane group each
-        unsigned long long pend = __ballot(hit && !masked);
-        while (pend) {
-            int src = -1;   // the pending lane this group takes
-            unsigned long long p = pend;
-            for (int g = 0; g < 4 && p; ++g) {
-                const int b = __ffsll((long long)p) - 1;
-                p &= p - 1;
-                if (g == grp) src = b;
-            }
-            pend = p;
-            const int jj = __shfl(j, src < 0 ? 0 : src);
-            const double ccj = __shfl(cc, src < 0 ? 0 : src);
-            const DetFeat f = det_feat(a, s, db, a.high[db + (src < 0 ? j0 : jj)]);
-            const double cd = cosine_dist16(rfeat, f, a.D);
-            double cost = 1.0;
-            if (src >= 0) {
-                double emb = np_max(0.0, cd) / 2.0;                           // matching.py:164-166
-                if (emb > app) emb = 1.0;                                       // bot_sort.py:318
-                cost = np_min(ccj, emb);                                        // bot_sort.py:320
-            }
-            put((lane & 15) == 0 && src >= 0 && cost < thresh, jj, cost);
+        const bool pend = hit && !masked;
+        const unsigned long long pm = __ballot(pend);
+        if (pm) {
+            if (nq + __popcll(pm) > BS_PQ) flush();
+            if (pend) q[nq + __popcll(pm & ((1ull << lane) - 1ull))] = BsPend{j, hd, cc};
+            nq += __popcll(pm);
         }
     }
+    if (nq) flush();
     if (lane == 0) {
         a.e_cnt[tb + i] = n;
         if (n > E_SLOTS) atomicOr(&c->bs_spill, 1);
@@ -1616,81 +1744,6 @@ __global__ __launch_bounds__(APPLY_T) void k_apply(BtArgs a) {
     YTA_APL(4);
 }
 
-// ------------------------------------------------------------------------------ k_feat / k_ema
-// BoT-SORT features, one wave per row.  Norms follow np.linalg.norm on a float32 row (the sum of
-// squares rounded to float32, then sqrt in float32); the sum is accumulated in float64 here,
-// where OpenBLAS sdot accumulates in float32 lanes, so a norm may differ from the reference's in
-// its last bit (the parity tests compare features with a tolerance).
-__device__ __forceinline__ float f32_norm(double sumsq) { return sqrtf((float)sumsq); }
-
-// k_feat: per high detection (conf > track_high_thresh, the stage-1 predicate) the norms of the
-// in-place normalisations the reference applies to its row: n1 = |e|, n2 = |e/n1| (STrack
-// construction, :40-48) and n3 = |(e/n1)/n2| (when a track takes it, :40-41).
-constexpr int FEAT_T = 256;
-__global__ __launch_bounds__(FEAT_T) void k_feat(BtArgs a) {
-    const int s = blockIdx.y, lane = lane_id();
-    if (stream_skipped(a, s)) return;
-    const int d = blockIdx.x * (FEAT_T / WAVE) + threadIdx.x / WAVE;
-    const int nd = min(a.det_off[s + 1] - a.det_off[s], a.MAXD);
-    if (d >= nd) return;
-    const long long row = (long long)a.det_off[s] + d;
-    if (!(a.det_in[row * 6 + 4] > a.track_thresh)) return;
-    const float *e = a.det_feat + row * a.D;
-    double q = 0.0;
-    for (int k = lane; k < a.D; k += WAVE) q += (double)e[k] * (double)e[k];
-    const float n1 = f32_norm(wave_reduce(RED_SUM, q));
-    q = 0.0;
-    for (int k = lane; k < a.D; k += WAVE) {
-        const float f = e[k] / n1;
-        q += (double)f * (double)f;
-    }
-    const float n2 = f32_norm(wave_reduce(RED_SUM, q));
-    q = 0.0;
-    for (int k = lane; k < a.D; k += WAVE) {
-        const float f = (e[k] / n1) / n2;
-        q += (double)f * (double)f;
-    }
-    const float n3 = f32_norm(wave_reduce(RED_SUM, q));
-    if (lane == 0) {
-        float *fn = a.det_fn + ((long long)s * a.MAXD + d) * 4;
-        fn[0] = n1;
-        fn[1] = n2;
-        fn[2] = n3;
-        fn[3] = 0.f;
-    }
-}
-
-// k_ema: update_features of every track that took a high detection this frame (bot_sort.py:40-48):
-// f = curr / |curr| with curr = (e/n1)/n2, smooth = 0.9 * smooth + 0.1 * f (float32), then
-// smooth /= |smooth|.
-constexpr int EMA_T = 256;
-__global__ __launch_bounds__(EMA_T) void k_ema(BtArgs a) {
-    const int s = blockIdx.y, lane = lane_id();
-    if (stream_skipped(a, s)) return;
-    const BtCounters *c = a.cnt + s;
-    const int n_pool = c->n_pool, n_items = n_pool + c->n_unc;
-    const int item = blockIdx.x * (EMA_T / WAVE) + threadIdx.x / WAVE;
-    if (item >= n_items) return;
-    const long long tb = (long long)s * a.CAP, db = (long long)s * a.MAXD;
-    const int h = a.ema_job[tb + item];
-    if (h < 0) return;
-    const int slot = item < n_pool ? a.pool[tb + item] : a.unc[tb + item - n_pool];
-    const int d = a.high[db + h];
-    const float *fn = a.det_fn + (db + d) * 4;
-    const float n1 = fn[0], n2 = fn[1], n3 = fn[2];
-    const float *e = a.det_feat + ((long long)a.det_off[s] + d) * a.D;
-    float *sm = a.feat + (tb + slot) * a.D;
-    double q = 0.0;
-    for (int k = lane; k < a.D; k += WAVE) {
-        const float f = ((e[k] / n1) / n2) / n3;
-        const float v = 0.9f * sm[k] + 0.1f * f;
-        sm[k] = v;
-        q += (double)v * (double)v;
-    }
-    const float nrm = f32_norm(wave_reduce(RED_SUM, q));
-    for (int k = lane; k < a.D; k += WAVE) sm[k] = sm[k] / nrm;
-}
-
 // ------------------------------------------------------------------------------------ k_finish
 // Per stream: births (:242-248), lost expiry (:250-253), joint/sub list algebra incl. the
 // removed_stracks quirk (:257-265), duplicate removal (:312-325) through a grid over lost' (in an
@@ -1739,6 +1792,12 @@ __device__ __forceinline__ void finish_body(const BtArgs &a, int s, unsigned *bi
         int y3, det;
         double score;
     };
+    // BoT-SORT births' feature rows are copied by the whole block below from (slot, detection)
+    // pairs staged in the (not yet used) dedup arena: one pass of independent loads instead of a
+    // chain of index loads per birth on one wave
+    int2 *bstage = V == VAR_BOTSORT && a.D > 0 && ar.cap >= (size_t)8 * (n_rest > 0 ? n_rest : 1)
+                       ? reinterpret_cast<int2 *>(ar.base)
+                       : nullptr;
     const int n_births_all = block_compact_ld<4>(
         n_rest, wsum,
         [&](int j) {
@@ -1758,6 +1817,7 @@ __device__ __forceinline__ void finish_body(const BtArgs &a, int s, unsigned *bi
             if (b >= n_free) return;   // capacity (flagged below)
             const int slot = a.free_list[tb + b];
             const int d = r.det;
+            if (bstage) bstage[b] = make_int2(slot, d);
             const DetMeas dm = det_meas<V>(a, s, d);
             KfState st;
             kf_initiate<kf_model<V>()>(dm.z, st);
@@ -1784,7 +1844,39 @@ __device__ __forceinline__ void finish_body(const BtArgs &a, int s, unsigned *bi
         if (t == 0) atomicOr(&c->err, ERR_TRACK_CAPACITY);
         n_births = n_free;
     }
-    if (V == VAR_BOTSORT && a.D > 0) {   // smooth_feat of a birth = its detection's curr_feat
+    if (V == VAR_BOTSORT && a.D > 0 && bstage) {   // smooth_feat of a birth = its curr_feat
+        block_sync();
+        if ((a.D & 3) == 0) {   // 16-B pieces: rows of D floats stay 16-B aligned
+            const int D4 = a.D >> 2;
+            struct Piece {
+                float4 e;
+                float n1, n2;
+                int slot;
+            };
+            batched_for<4>(
+                n_births * D4,
+                [&](int q) {
+                    const int2 sd = bstage[q / D4];
+                    const DetFeat f = det_feat(a, s, db, sd.y);
+                    return Piece{reinterpret_cast<const float4 *>(f.e)[q % D4], f.n1, f.n2, sd.x};
+                },
+                [&](int q, const Piece &p) {
+                    const float4 e = p.e;
+                    reinterpret_cast<float4 *>(a.feat + (tb + p.slot) * a.D)[q % D4] =
+                        make_float4((e.x / p.n1) / p.n2, (e.y / p.n1) / p.n2, (e.z / p.n1) / p.n2,
+                                    (e.w / p.n1) / p.n2);
+                });
+        } else {
+            batched_for<8>(
+                n_births * a.D,
+                [&](int q) {
+                    const int2 sd = bstage[q / a.D];
+                    return det_feat(a, s, db, sd.y)(q % a.D);
+                },
+                [&](int q, float v) { a.feat[(tb + bstage[q / a.D].x) * a.D + q % a.D] = v; });
+        }
+        block_sync();   // the arena is the dedup grid's next
+    } else if (V == VAR_BOTSORT && a.D > 0) {
         block_sync();
         const int lane = lane_id(), nw = nt / WAVE;
         for (int b = t / WAVE; b < n_births; b += nw) {
@@ -2120,6 +2212,14 @@ template <int V>
 __global__ __launch_bounds__(BLKF, 4) void k_finish(BtArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char fsmem[];
     __shared__ FinishShared sh;
+    if (V == VAR_BOTSORT && (int)blockIdx.x >= a.S) {
+        // split BoT-SORT: k_ema's blocks in this grid.  Independent of the finish work: the EMA
+        // rewrites the smoothed features of tracks that took a detection this frame, the finish
+        // writes only births' (free slots') features and reads none
+        const int b = blockIdx.x - a.S, eb = ema_blocks(a.CAP);
+        ema_body(a, b / eb, b % eb);
+        return;
+    }
     const int s = blockIdx.x;
     if (stream_skipped(a, s)) {   // not updated this frame: no output rows
         if (threadIdx.x == 0) {
@@ -2698,8 +2798,12 @@ template <int V>
 int launch_frame(yta_bytetrack *e) {
     BtArgs &a = e->a;
     const bool reid = V == VAR_BOTSORT && a.D > 0;
+    // split BoT-SORT stage 1 (few streams): k_feat's blocks ride in k_bs_prep's grid and k_ema's
+    // in k_finish's (two launches fewer on a latency-bound chain)
+    const bool bs = V == VAR_BOTSORT && reid && e->bs_split && a.prox_thresh < 1.0 &&
+                    a.match_thresh <= 1.0;
     MARK();
-    if (reid) {
+    if (reid && !bs) {
         const dim3 gf((a.MAXD + FEAT_T / WAVE - 1) / (FEAT_T / WAVE), a.S);
         hipLaunchKernelGGL(k_feat, gf, dim3(FEAT_T), 0, e->stream, a);
         YTA_HIP(hipGetLastError());
@@ -2712,9 +2816,10 @@ int launch_frame(yta_bytetrack *e) {
         YTA_HIP(hipGetLastError());
         MARK();
         hipLaunchKernelGGL(k_s1_lap, dim3(a.S), dim3(BLKL), a.lds_bytes_l, e->stream, a);
-    } else if (V == VAR_BOTSORT && reid && e->bs_split && a.prox_thresh < 1.0 &&
-               a.match_thresh <= 1.0) {   // split stage 1 (k_bs_*): few streams
-        hipLaunchKernelGGL(k_bs_prep, dim3(a.S), dim3(PREP_T), 0, e->stream, a);
+    } else if (bs) {   // split stage 1 (k_bs_*): few streams
+        static_assert(FEAT_T == PREP_T, "k_feat's blocks run in k_bs_prep's grid");
+        hipLaunchKernelGGL(k_bs_prep, dim3(a.S + a.S * feat_blocks(a.MAXD)), dim3(PREP_T), 0,
+                           e->stream, a);
         YTA_HIP(hipGetLastError());
         MARK();
         const dim3 ge((a.CAP + BSE_T / WAVE - 1) / (BSE_T / WAVE), a.S);
@@ -2736,15 +2841,16 @@ int launch_frame(yta_bytetrack *e) {
     const dim3 gt((a.CAP + APPLY_T - 1) / APPLY_T, a.S);
     hipLaunchKernelGGL(k_apply<V>, gt, dim3(APPLY_T), 0, e->stream, a);
     YTA_HIP(hipGetLastError());
-    if (reid) {
-        const dim3 ge((a.CAP + EMA_T / WAVE - 1) / (EMA_T / WAVE), a.S);
+    if (reid && !bs) {
+        const dim3 ge(ema_blocks(a.CAP), a.S);
         hipLaunchKernelGGL(k_ema, ge, dim3(EMA_T), 0, e->stream, a);
         YTA_HIP(hipGetLastError());
     }
     MARK();
     const size_t bits_bytes = ((size_t)12 * ((a.CAP + 31) / 32) + 15) & ~(size_t)15;
-    hipLaunchKernelGGL(k_finish<V>, dim3(a.S), dim3(BLKF), bits_bytes + a.lds_bytes_f, e->stream,
-                       a);
+    static_assert(EMA_T == BLKF, "k_ema's blocks run in k_finish's grid");
+    hipLaunchKernelGGL(k_finish<V>, dim3(a.S + (bs ? a.S * ema_blocks(a.CAP) : 0)), dim3(BLKF),
+                       bits_bytes + a.lds_bytes_f, e->stream, a);
     YTA_HIP(hipGetLastError());
     MARK();
     return YTA_OK;
