@@ -64,9 +64,14 @@ struct DocCounters {
     int frame;
     int n_ut;                      // k_doc_assoc -> k_doc_ocr -> k_doc_assoc_b: OCR round columns
     int ocr_nan;                   // the OCR matrix holds a NaN (its max is then NaN)
-    int pad[8];
+    int n_pos;                     // k_doc_cost -> k_doc_emb*: some row has more than POS_K pairs
+                                   // whose asso value is not <= 0 (the dense tiles run)
+    int col_ovf;                   // k_doc_emb_pairs -> k_doc_aw*: a column listed more than POS_K
+    int pad[6];
 };
 static_assert(sizeof(DocCounters) == 128, "DocCounters layout");
+
+constexpr int POS_K = 16;   // listed embedding pairs per detection row (k_doc_cost)
 
 struct DocArgs {
     int S, CAP, MAXD, D;
@@ -102,6 +107,10 @@ struct DocArgs {
     int *out_counts;
     int arr_chip;                  // first rounds solved with the chip-wide bidding rounds
     const int *active;             // [S] nonzero = update the stream this frame; null = all
+    int *pos_q;                    // [S*MAXD*POS_K] per kept detection: trackers whose pair's
+    int *pos_cnt;                  // embedding term is used; [S*MAXD] their count
+    double *col_e;                 // [S*CAP*POS_K] per tracker: its listed pairs' embedding terms
+    int *col_cnt;                  // [S*CAP] their count
 };
 
 __device__ __forceinline__ long long doc_mb(const DocArgs &a, int s) {
@@ -377,11 +386,17 @@ __global__ __launch_bounds__(OC_T) void k_doc_pre(DocArgs a) {
                                                             (1 - a.det_thresh);
                                        a.alpha[db + pos] = a.af + (1 - a.af) * (1 - trust);
                                    });
-    for (int i = t; i < n_hi; i += nt) a.rmatch[db + i] = 0;
+    for (int i = t; i < n_hi; i += nt) {
+        a.rmatch[db + i] = 0;
+        a.pos_cnt[db + i] = 0;
+    }
+    for (int j = t; j < n_trk; j += nt) a.col_cnt[tb + j] = 0;
     if (t == 0) {
         c->n_trk = n_trk;
         c->n_high = n_hi;
         c->n_dets = nd;
+        c->n_pos = 0;
+        c->col_ovf = 0;
     }
 }
 
@@ -416,6 +431,13 @@ __global__ __launch_bounds__(OC_T) void k_doc_cost(DocArgs a) {
         const double angle = ((valid * ang) * a.inertia) * dr[4];
         mat[q] = v;
         mat2[q] = v + angle;            // iou + angle; the embedding term joins in k_doc_final
+        // emb_cost[iou_matrix <= 0] = 0 (association.py:165): only these pairs' dot products
+        // are read (k_doc_aw, k_doc_final); listed per detection row
+        if (!(v <= 0)) {
+            const int k = atomicAdd(&a.pos_cnt[db + i], 1);
+            if (k < POS_K) a.pos_q[(db + i) * POS_K + k] = j;
+            else c->n_pos = 1;   // a row with more: the dense tiles
+        }
         if (v > a.thr) {
             atomicAdd(&a.rmatch[db + i], 1);
             atomicAdd(&a.cmatched[tb + j], 1);
@@ -437,6 +459,7 @@ __global__ __launch_bounds__(256) void k_doc_emb(DocArgs a) {
     const int s = blockIdx.z;
     if (a.active && !a.active[s]) return;   // stream not updated this frame
     const DocCounters *c = a.cnt + s;
+    if (c->n_pos == 0) return;               // the listed pairs only (k_doc_emb_pairs)
     const int n_trk = c->n_trk, n_hi = c->n_high, D = a.D;
     int bx, by;
     xcd_tile(bx, by);                                         // row bands per XCD (common.hpp)
@@ -501,6 +524,69 @@ __global__ __launch_bounds__(256) void k_doc_emb(DocArgs a) {
             }
 }
 
+// The embedding term is read only where the asso value is not <= 0 (association.py:165): a few
+// pairs per detection, listed per row by k_doc_cost.  One wave per detection row, its pairs four at
+// a time (a 16-lane group each: float64 accumulation, cosine_dist16's reduction), written at their
+// positions of emat; with AW on, the row's top two of emb (zero elsewhere) give its weight here,
+// and every column's listed values for k_doc_aw_cols (k_doc_aw's dense scans then do not run).
+// The dense tiles (k_doc_emb) and scans run instead when a row or column listed more than POS_K.
+constexpr int EMBP_T = 256;
+__global__ __launch_bounds__(EMBP_T) void k_doc_emb_pairs(DocArgs a) {
+    const int s = blockIdx.y;
+    if (a.active && !a.active[s]) return;   // stream not updated this frame
+    const DocCounters *c = a.cnt + s;
+    if (c->n_pos != 0) return;               // dense path
+    const int n_trk = c->n_trk, n_hi = c->n_high, D = a.D;
+    const int i = blockIdx.x * (EMBP_T / WAVE) + threadIdx.x / WAVE;
+    if (i >= n_hi) return;
+    const long long tb = (long long)s * a.CAP, db = (long long)s * a.MAXD, mb = doc_mb(a, s);
+    const int lane = lane_id(), grp = lane >> 4, l16 = lane & 15;
+    const int cnt = a.pos_cnt[db + i];   // <= POS_K (n_pos == 0)
+    const float *ar = a.det_feat + ((long long)a.det_off[s] + a.hi_row[db + i]) * D;
+    double m1 = -INFINITY, m2 = -INFINITY;
+    for (int p0 = 0; p0 < cnt; p0 += 4) {
+        const int p = p0 + grp;
+        const bool v = p < cnt;
+        const int j = a.pos_q[(db + i) * POS_K + (v ? p : p0)];
+        const double *br = a.emb + (tb + a.cslot[tb + j]) * D;
+        double acc = 0.0;
+        constexpr int CB = 16;
+        int k = l16;
+        for (; k + 16 * (CB - 1) < D; k += 16 * CB) {
+            float av[CB];
+            double bv[CB];
+#pragma unroll
+            for (int u = 0; u < CB; ++u) {
+                av[u] = ar[k + 16 * u];
+                bv[u] = br[k + 16 * u];
+            }
+#pragma unroll
+            for (int u = 0; u < CB; ++u) acc += (double)av[u] * bv[u];
+        }
+        for (; k < D; k += 16) acc += (double)ar[k] * br[k];
+        acc = row_allreduce(RED_SUM, acc);
+        if (v && l16 == 0) {
+            a.emat[mb + (long long)i * n_trk + j] = acc;
+            top2_push(acc, m1, m2);
+            if (!a.aw_off) {   // the column's share for k_doc_aw_cols
+                const int kc = atomicAdd(&a.col_cnt[tb + j], 1);
+                if (kc < POS_K) a.col_e[(tb + j) * POS_K + kc] = acc;
+                else atomicOr(const_cast<int *>(&c->col_ovf), 1);
+            }
+        }
+    }
+    if (a.aw_off) return;
+    for (int o = 32; o >= 1; o >>= 1) {   // merge the lanes' top-2
+        const double o1 = __shfl_xor(m1, o), o2 = __shfl_xor(m2, o);
+        top2_push(o1, m1, m2);
+        top2_push(o2, m1, m2);
+    }
+    // the row's other entries are 0 (emb zeroed where the asso value is <= 0)
+    if (n_trk - cnt >= 1) top2_push(0.0, m1, m2);
+    if (n_trk - cnt >= 2) top2_push(0.0, m1, m2);
+    if (lane == 0) a.rw[db + i] = aw_weight(m1, m2, a.aw_param, n_trk);
+}
+
 // compute_aw_max_metric (association.py:79-108) on emb[iou <= 0] = 0: the top two values of each
 // row (blockIdx.x < row blocks) or column; one wave per row / per 64 columns.
 // compute_aw_max_metric (association.py:79-108) on emb (zeroed where iou <= 0).  Rows: one wave
@@ -522,10 +608,21 @@ __global__ __launch_bounds__(256) void k_doc_aw(DocArgs a) {
         return I[q] <= 0 ? 0.0 : E[q];
     };
     if ((int)blockIdx.x < row_blocks) {
+        if (c->n_pos == 0) return;   // the row weights came with the listed pairs (k_doc_emb_pairs)
         const int r = blockIdx.x * 4 + wv;
         if (r >= n_hi) return;
         double m1 = -INFINITY, m2 = -INFINITY;
-        for (int cc = lane; cc < n_trk; cc += WAVE) top2_push(val(r, cc), m1, m2);
+        constexpr int RB = 8;   // a lane's next 8 entries loaded before any is used
+        int cc = lane;
+        for (; cc + WAVE * (RB - 1) < n_trk; cc += WAVE * RB) {
+            double iv[RB];
+#pragma unroll
+            for (int u = 0; u < RB; ++u) iv[u] = I[(long long)r * n_trk + cc + WAVE * u];
+#pragma unroll
+            for (int u = 0; u < RB; ++u)   // the embedding term only where it is kept
+                top2_push(iv[u] <= 0 ? 0.0 : E[(long long)r * n_trk + cc + WAVE * u], m1, m2);
+        }
+        for (; cc < n_trk; cc += WAVE) top2_push(val(r, cc), m1, m2);
         for (int o = 32; o >= 1; o >>= 1) {   // merge the lanes' top-2
             const double o1 = __shfl_xor(m1, o), o2 = __shfl_xor(m2, o);
             top2_push(o1, m1, m2);
@@ -534,6 +631,7 @@ __global__ __launch_bounds__(256) void k_doc_aw(DocArgs a) {
         if (lane == 0) a.rw[db + r] = aw_weight(m1, m2, a.aw_param, n_trk);
     } else {
         __shared__ double part[4][WAVE][2];
+        if (c->n_pos == 0 && c->col_ovf == 0) return;   // listed columns (k_doc_aw_cols)
         const int q = (int)blockIdx.x - row_blocks;
         const int tile = q / AW_CHUNKS, chunk = q % AW_CHUNKS;
         const int cc = tile * WAVE + lane;
@@ -574,6 +672,15 @@ __global__ __launch_bounds__(256) void k_doc_aw_cols(DocArgs a) {
     const int cc = blockIdx.x * blockDim.x + threadIdx.x;
     if (cc >= n_trk) return;
     double m1 = -INFINITY, m2 = -INFINITY;
+    if (c->n_pos == 0 && c->col_ovf == 0) {   // the column's listed values, zeros elsewhere
+        const long long tb = (long long)s * a.CAP;
+        const int cnt = a.col_cnt[tb + cc];
+        for (int k = 0; k < cnt; ++k) top2_push(a.col_e[(tb + cc) * POS_K + k], m1, m2);
+        if (n_hi - cnt >= 1) top2_push(0.0, m1, m2);
+        if (n_hi - cnt >= 2) top2_push(0.0, m1, m2);
+        a.cw[tb + cc] = aw_weight(m1, m2, a.aw_param, n_hi);
+        return;
+    }
     for (int k = 0; k < AW_CHUNKS; ++k) {
         const double *o = a.cw_part + ((long long)s * AW_CHUNKS + k) * a.CAP * 2 + 2LL * cc;
         top2_push(o[0], m1, m2);
@@ -1158,6 +1265,10 @@ int doc_alloc(yta_deepocsort *e) {
     DOCALLOC(a.mat, S * mat);
     DOCALLOC(a.mat2, S * mat);
     DOCALLOC(a.emat, S * mat);
+    DOCALLOC(a.pos_q, S * MAXD * POS_K);
+    DOCALLOC(a.pos_cnt, S * MAXD);
+    DOCALLOC(a.col_e, S * CAP * POS_K);
+    DOCALLOC(a.col_cnt, S * CAP);
     DOCALLOC(a.rw, S * MAXD);
     DOCALLOC(a.cw, S * CAP);
     DOCALLOC(a.cw_part, S * AW_CHUNKS * CAP * 2);
@@ -1234,6 +1345,9 @@ int doc_launch(yta_deepocsort *e, const double *d_dets, const int *d_off, const 
     hipLaunchKernelGGL(k_doc_cost, gm, dim3(OC_T), 0, e->stream, a);
     YTA_HIP(hipGetLastError());
     if (!a.embedding_off) {
+        const dim3 gp((a.MAXD + EMBP_T / WAVE - 1) / (EMBP_T / WAVE), a.S);
+        hipLaunchKernelGGL(k_doc_emb_pairs, gp, dim3(EMBP_T), 0, e->stream, a);
+        YTA_HIP(hipGetLastError());
         const dim3 ge((a.CAP + EMB_TILE - 1) / EMB_TILE, (a.MAXD + EMB_TILE - 1) / EMB_TILE, a.S);
         hipLaunchKernelGGL(k_doc_emb, ge, dim3(256), 0, e->stream, a);
         YTA_HIP(hipGetLastError());
