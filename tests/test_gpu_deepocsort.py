@@ -176,3 +176,43 @@ def test_deepocsort_multistream_matches_oracle():
             d, e = streams[s][f]
             exp = np.asarray(ors[s].update(d, shape, e), dtype=np.float64).reshape(-1, 8)
             assert np.array_equal(got[s], exp), (s, f)
+
+
+def _crowd(frames, grow):
+    """Boxes scaled about their centres: with grow 4 a detection overlaps dozens of trackers."""
+    out = []
+    for d, e in frames:
+        d = d.copy()
+        c = (d[:, :2] + d[:, 2:4]) / 2
+        h = (d[:, 2:4] - d[:, :2]) / 2 * grow
+        d[:, :2], d[:, 2:4] = c - h, c + h
+        out.append((d, e))
+    return out
+
+
+def test_deepocsort_dense_embedding_fallback_matches_oracle():
+    """A stream whose detections overlap more than 16 trackers each takes the dense embedding
+    tiles and AW scans (k_doc_emb, k_doc_aw); the other stream of the same engine the listed
+    pairs (k_doc_emb_pairs).  Both against the oracle frame by frame."""
+    S, n, nf, D = 2, 96, 12, 32
+    kw = dict(det_thresh=0.0, max_age=30, min_hits=1, iou_threshold=0.3, delta_t=3,
+              asso_func="giou", inertia=0.2)
+    raw = [make_frames(n, nf, 700 + s, emb_dim=D, low_conf_frac=0.0, drop_frac=0.1)
+           for s in range(S)]
+    streams = [[(d, (e / np.linalg.norm(e, axis=1, keepdims=True)).astype(np.float32))
+                for d, e in r] for r in raw]
+    streams[0] = _crowd(streams[0], 4.0)
+    d0 = streams[0][1][0]
+    ov = ((d0[:, None, 0] < d0[None, :, 2]) & (d0[None, :, 0] < d0[:, None, 2]) &
+          (d0[:, None, 1] < d0[None, :, 3]) & (d0[None, :, 1] < d0[:, None, 3])).sum(1)
+    assert ov.max() > 16   # the crowded stream does list more than POS_K pairs in some row
+    eng = DeepOCSortEngine(S, feat_dim=D, **kw, track_capacity=256, max_dets=128)
+    ors = [DeepOCSortOracle(**kw) for _ in range(S)]
+    shape = (640, 640, 3)
+    for f in range(nf):
+        got = eng.update([streams[s][f][0] for s in range(S)],
+                         [streams[s][f][1] for s in range(S)], img_shapes=[shape] * S)
+        for s in range(S):
+            d, e = streams[s][f]
+            exp = np.asarray(ors[s].update(d, shape, e), dtype=np.float64).reshape(-1, 8)
+            assert np.array_equal(got[s], exp), (s, f)
