@@ -51,6 +51,7 @@ namespace {
 constexpr int BLK1 = YTA_BLK1, BLK23 = YTA_BLK23, BLKF = YTA_BLKF;
 constexpr int BLK_MAX = 1024;
 constexpr int SLAB_WAVES = BLK_MAX / WAVE;   // solver slabs per stream (any block size)
+static_assert(2 * YTA_BLK23 / WAVE <= SLAB_WAVES, "k_stage23's two blocks take disjoint slabs");
 
 __device__ __forceinline__ void store_kf(double *kf, long long slot, const KfState &s) {
     double2 *dst = reinterpret_cast<double2 *>(kf + slot * TRK_STRIDE);
@@ -297,46 +298,68 @@ __device__ __forceinline__ bool stage1_body(const BtArgs &a, int s, Arena &ar, S
 // Per stream: leftovers = unmatched Tracked pool rows (:205-209) x low detections, IoU, cost_limit
 // 0.5 (:210-211); rest = unmatched high detections (:229); unconfirmed x rest, fused IoU,
 // cost_limit 0.7 (:230-233).
+// role -1: both stages in this block; 0: stage 2 only (leftovers, re-found); 1: stage 3 only (the
+// rest of the high detections), its solver slabs after stage 2's (split23: one block each).
 template <int V>
-__device__ __forceinline__ bool stage23_body(const BtArgs &a, int s, Arena &ar, StageShared &sh) {
+__device__ __forceinline__ bool stage23_body(const BtArgs &a, int s, Arena &ar, StageShared &sh,
+                                             int role = -1) {
     int *wsum = sh.as.lap.wsum;
     const int t = threadIdx.x, nt = blockDim.x;
     BtCounters *c = a.cnt + s;
     const long long tb = (long long)s * a.CAP, db = (long long)s * a.MAXD;
     const int n_pool = c->n_pool, n_high = c->n_high, n_second = c->n_second, n_unc = c->n_unc;
     const int n_act = c->n_act;
-    for (int i = t; i < n_pool; i += nt) a.left_of_pool[tb + i] = -1;
-    block_sync();
-    // leftovers: the pool's Tracked rows (its head, the activated tracks: pool = act ++ lost)
-    // left unmatched in stage 1 (:205-209)
-    const int n_left = block_compact_ld<8>(
-        n_act, wsum, [&](int i) { return a.x1[tb + i]; }, [&](int, int h) { return h; },
-        [&](int, int h) { return h < 0; },
-        [&](int i, int, int pos) {
-            a.left[tb + pos] = i;
-            a.left_of_pool[tb + i] = pos;
-        });
-    // re-found: the pool's Lost rows matched in stage 1 (refind_stracks, :193-196), pool order,
-    // with their slot and detection (k_apply visits these and no other Lost row)
-    const int n_ref = block_compact_ld<8>(
-        n_pool - n_act, wsum,
-        [&](int k) { return make_int2(a.pool[tb + n_act + k], a.x1[tb + n_act + k]); },
-        [&](int, int2 v) { return v; }, [&](int, const int2 &v) { return v.y >= 0; },
-        [&](int, const int2 &v, int pos) { a.refound[tb + pos] = v; });
-    const int n_rest = block_compact(n_high, wsum, [&](int h) { return a.y1[db + h] < 0; },
-                                     [&](int h, int pos) {
-                                         a.rest[db + pos] = h;
-                                         a.rest_score[db + pos] = a.high_score[db + h];
-                                     });
+    LapSlab slab = slab_of(a, s);
+    if (role == 1) {
+        slab.i += (long long)(BLK23 / WAVE) * slab.i_stride;
+        slab.d += (long long)(BLK23 / WAVE) * slab.d_stride;
+    }
+    int n_left = 0, n_ref = 0, n_rest = 0;
+    bool ok = true;
+    if (role <= 0) {
+        for (int i = t; i < n_pool; i += nt) a.left_of_pool[tb + i] = -1;
+        block_sync();
+        // leftovers: the pool's Tracked rows (its head, the activated tracks: pool = act ++ lost)
+        // left unmatched in stage 1 (:205-209)
+        n_left = block_compact_ld<8>(
+            n_act, wsum, [&](int i) { return a.x1[tb + i]; }, [&](int, int h) { return h; },
+            [&](int, int h) { return h < 0; },
+            [&](int i, int, int pos) {
+                a.left[tb + pos] = i;
+                a.left_of_pool[tb + i] = pos;
+            });
+        // re-found: the pool's Lost rows matched in stage 1 (refind_stracks, :193-196), pool order,
+        // with their slot and detection (k_apply visits these and no other Lost row)
+        n_ref = block_compact_ld<8>(
+            n_pool - n_act, wsum,
+            [&](int k) { return make_int2(a.pool[tb + n_act + k], a.x1[tb + n_act + k]); },
+            [&](int, int2 v) { return v; }, [&](int, const int2 &v) { return v.y >= 0; },
+            [&](int, const int2 &v, int pos) { a.refound[tb + pos] = v; });
+    }
+    if (role != 0)
+        n_rest = block_compact(n_high, wsum, [&](int h) { return a.y1[db + h] < 0; },
+                               [&](int h, int pos) {
+                                   a.rest[db + pos] = h;
+                                   a.rest_score[db + pos] = a.high_score[db + h];
+                               });
     block_sync();
     YTA_STAMP(4);
-    const LapSlab slab = slab_of(a, s);
-    bool ok = assoc_block(
-        n_left, [&](int k) { return a.pool_box[tb + a.left[tb + k]]; }, n_second,
-        [&](int q) { return a.second_box[db + q]; }, false, [&](int) { return 1.0; }, 0.5,
-        a.x2 + tb, a.y2 + db, &c->err, &c->n_edges[1], ar, slab, sh.as);
-    if (!ok) return false;
-    ar.reset();
+    if (role <= 0) {
+        ok = assoc_block(
+            n_left, [&](int k) { return a.pool_box[tb + a.left[tb + k]]; }, n_second,
+            [&](int q) { return a.second_box[db + q]; }, false, [&](int) { return 1.0; }, 0.5,
+            a.x2 + tb, a.y2 + db, &c->err, &c->n_edges[1], ar, slab, sh.as);
+        if (!ok) return false;
+        ar.reset();
+    }
+    if (role == 0) {
+        if (t == 0) {
+            c->n_left = n_left;
+            c->n_ref = n_ref;
+            c->n_lazy = V == VAR_BYTETRACK ? n_pool - n_act - n_ref : 0;
+        }
+        return true;
+    }
     YTA_STAMP_BASE(40);
     YTA_STAMP(0);
     if (V == VAR_BOTSORT && a.D > 0)   // bot_sort.py:355-370
@@ -357,11 +380,13 @@ __device__ __forceinline__ bool stage23_body(const BtArgs &a, int s, Arena &ar, 
     if (!ok) return false;
     YTA_STAMP(15);
     if (t == 0) {
-        c->n_left = n_left;
         c->n_rest = n_rest;
-        c->n_ref = n_ref;
-        // ByteTrack: the Lost rows k_apply leaves untouched (lazy prediction)
-        c->n_lazy = V == VAR_BYTETRACK ? n_pool - n_act - n_ref : 0;
+        if (role < 0) {
+            c->n_left = n_left;
+            c->n_ref = n_ref;
+            // ByteTrack: the Lost rows k_apply leaves untouched (lazy prediction)
+            c->n_lazy = V == VAR_BYTETRACK ? n_pool - n_act - n_ref : 0;
+        }
     }
     return true;
 }
@@ -391,22 +416,24 @@ template <int V>
 __global__ __launch_bounds__(BLK23) void k_stage23(BtArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     __shared__ StageShared sh;
-    const int s = blockIdx.x;
+    const int s = a.split23 ? blockIdx.x >> 1 : blockIdx.x;
+    const int role = a.split23 ? (int)(blockIdx.x & 1) : -1;
     if (stream_skipped(a, s)) return;
     YTA_STAMP_BASE(20);
     YTA_STAMP(0);
     YTA_BLK(3, 0);
     {
         Arena ar(smem, a.lds_bytes23);
-        if (stage23_body<V>(a, s, ar, sh)) {
+        if (stage23_body<V>(a, s, ar, sh, role)) {
             YTA_BLK(3, 1);
             return;
         }
     }
     block_sync();
-    if (threadIdx.x == 0) a.cnt[s].n_fallback[1] += 1;
-    Arena ag(a.ws + s * a.ws_stride, a.ws_stride);
-    if (!stage23_body<V>(a, s, ag, sh) && threadIdx.x == 0) atomicOr(&a.cnt[s].err, ERR_EDGE_OVERFLOW);
+    if (threadIdx.x == 0) atomicAdd(&a.cnt[s].n_fallback[1], 1);
+    Arena ag((role == 1 ? a.ws3 : a.ws) + s * a.ws_stride, a.ws_stride);
+    if (!stage23_body<V>(a, s, ag, sh, role) && threadIdx.x == 0)
+        atomicOr(&a.cnt[s].err, ERR_EDGE_OVERFLOW);
 }
 
 // ------------------------------------------------------------------ ByteTrack stage 1, split
@@ -2490,6 +2517,9 @@ struct yta_bytetrack {
     // BoT-SORT with ReID: stage 1 as k_bs_prep / k_bs_edges / k_bs_lap (few streams) instead of
     // the fused k_stage1 (set at create; YTA_BS_SPLIT=0 / 1 overrides)
     bool bs_split = false;
+    // few streams: k_stage23's two stages in two blocks per stream (set at create; YTA_SPLIT23=0 / 1
+    // overrides)
+    bool split23 = false;
     // stream-subset updates: the [S] mask on the device and its pinned staging
     int *d_active = nullptr, *h_active = nullptr;
     // the engine's own [S * CAP][8] output rows (the host-buffer paths); a.out is whatever buffer
@@ -2749,6 +2779,9 @@ int bt_alloc(yta_bytetrack *e) {
         a.ws_stride = std::max(a.ws_stride, assoc_emb_arena_bytes(CAP, MAXD));
     a.ws_stride = (a.ws_stride + 255) & ~255LL;
     DALLOC(a.ws, S * a.ws_stride);
+    a.split23 = e->split23;
+    a.ws3 = nullptr;
+    if (a.split23) DALLOC(a.ws3, S * a.ws_stride);
     a.slab.R = (int)CAP;
     a.slab.C = (int)MAXD;
     a.slab.i_stride = lap_slab_ints((int)CAP, (int)MAXD);
@@ -2835,7 +2868,8 @@ int launch_frame(yta_bytetrack *e) {
     }
     YTA_HIP(hipGetLastError());
     MARK();
-    hipLaunchKernelGGL(k_stage23<V>, dim3(a.S), dim3(BLK23), a.lds_bytes23, e->stream, a);
+    hipLaunchKernelGGL(k_stage23<V>, dim3(a.split23 ? 2 * a.S : a.S), dim3(BLK23), a.lds_bytes23,
+                       e->stream, a);
     YTA_HIP(hipGetLastError());
     MARK();
     const dim3 gt((a.CAP + APPLY_T - 1) / APPLY_T, a.S);
@@ -3011,6 +3045,8 @@ int create_engine(int device, int n_streams, int track_capacity, int max_dets,
     e->S = n_streams;
     e->CAP = track_capacity;
     e->MAXD = max_dets;
+    e->split23 = n_streams <= 64;
+    if (const char *v = getenv("YTA_SPLIT23")) e->split23 = atoi(v) != 0;
     init(e);
     hipError_t he = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
     if (he != hipSuccess) {

@@ -111,6 +111,10 @@ struct BtArgs {
     size_t lds_bytes, lds_bytes23, lds_bytes_f;   // arenas of k_stage1 / k_stage23 / k_finish
     unsigned char *ws;
     long long ws_stride;
+    // few streams: k_stage23 runs stage 2 and stage 3 (independent given stage 1) in two blocks
+    // per stream; stage 3's block has its own fallback arena [S * ws_stride] and solver slabs
+    int split23;
+    unsigned char *ws3;
     LapSlab slab;             // per stream: (threads / 64) slabs
     // ByteTrack stage 1 as three launches (k_s1_prep / k_s1_edges / k_s1_lap): the per-stream
     // grid over the high detections and every pool row's first candidate edges, in HBM
