@@ -2017,11 +2017,26 @@ __device__ __forceinline__ void finish_body(const BtArgs &a, int s, unsigned *bi
         // lazily predicted mean (k_s1_prep / the last k_finish), BoT-SORT's predicted and warped
         // mean (stage1_lists: the same x + v and kron(I4, R) x + t operations as k_apply's
         // kf_predict / kf_predict_x and kf_gmc on the record, so the same bits, and no record read)
-        auto exact_lbox = [&](int q) { return a.pool_box[tb + a.l2pos[tb + q]]; };
+        // each entry's pool position kept beside its float box (one global round trip, not two,
+        // for a candidate's exact box) when the arena has room
+        int *lpos = ar.try_alloc<int>(n_l2);
+        auto exact_lbox = [&](int q) {
+            return a.pool_box[tb + (lpos ? lpos[q] : a.l2pos[tb + q])];
+        };
         if (V == VAR_BYTETRACK || V == VAR_BOTSORT)
-            batched_for<4>(
-                n_l2, [&](int q) { return a.pool_box[tb + a.l2pos[tb + q]]; },
-                [&](int q, const Box &b) { lcache[q] = box_outer_f32(b); });
+            batched_for2<4>(
+                n_l2, [&](int q) { return a.l2pos[tb + q]; },
+                [&](int, int pos) {
+                    struct PB {
+                        Box b;
+                        int pos;
+                    };
+                    return PB{a.pool_box[tb + pos], pos};
+                },
+                [&](int q, const auto &v) {
+                    lcache[q] = box_outer_f32(v.b);
+                    if (lpos) lpos[q] = v.pos;
+                });
         else
             batched_for2<3>(
                 n_l2, [&](int q) { return a.l2[tb + q]; },
