@@ -100,6 +100,8 @@ struct DocArgs {
     int *upd;                       // [S*CAP] update source per tracker (input row) or -1
     int *ema_slot, *ema_row;        // [S*(CAP+MAXD)] embedding jobs: slot, input row (birth: ~row)
     unsigned char *lap_ws;
+    unsigned char *lap_csr;         // per stream: the replay's row entries (nullptr: n < LAPB_MIN_N)
+    long long lap_csr_stride;
     long long lap_ws_stride;
     double *pre_u, *pre_s2;        // [S*MAXD] first-round row pre-pass (lap_rect.hpp)
     int *pre_x;
@@ -817,7 +819,8 @@ __global__ __launch_bounds__(OC_T) void k_doc_assoc(DocArgs a) {
         } else if (n_hi > 0 && !solved) {
             block_sync();
             main_lap(LapMat{mat2, n_hi, n_trk, false}, a.pre_u + db, a.pre_x + db, a.pre_s2 + db,
-                     a.rmatch + db, lds, lds_bytes, gws, &c->err, &c->ls);
+                     a.rmatch + db, lds, lds_bytes, gws, &c->err, &c->ls,
+                     a.lap_csr ? a.lap_csr + s * a.lap_csr_stride : nullptr);
         }
         YTA_STAMP(1);
         if (t == 0) { c->fast_path = fast; c->lap_calls = (fast || n_hi == 0) ? 0 : 1; }
@@ -1289,6 +1292,9 @@ int doc_alloc(yta_deepocsort *e) {
     a.arr_chip = MAXD >= ARR_CHIP_MIN_DETS;
     if (const char *v = getenv("YTA_ARR_CHIP")) a.arr_chip = atoi(v);
     DOCALLOC(a.lap_ws, S * a.lap_ws_stride);
+    a.lap_csr = nullptr;
+    a.lap_csr_stride = n >= LAPB_MIN_N && lap_sparse_on() ? (lap_csr_bytes(n) + 255) & ~255LL : 0;
+    if (a.lap_csr_stride) DOCALLOC(a.lap_csr, S * a.lap_csr_stride);
     e->lds = (size_t)oc_lds_bytes(CAP, MAXD);
     DOCALLOC(e->d_off, S + 1);
     DOCALLOC(e->d_wh, 2 * S);

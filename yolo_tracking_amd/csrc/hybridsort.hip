@@ -111,6 +111,8 @@ struct HsArgs {
     int *upd;                       // [S*CAP] kept-detection index updating each tracker or -1
     int *ema_slot, *ema_row;        // [S*(CAP+MAXD)] feature jobs: slot, kept index (birth: ~p)
     unsigned char *lap_ws;
+    unsigned char *lap_csr;         // per stream: the replay's row entries (nullptr: n < LAPB_MIN_N)
+    long long lap_csr_stride;
     long long lap_ws_stride;
     double *pre_u, *pre_s2;        // [S*MAXD] first-round row pre-pass (lap_rect.hpp)
     int *pre_x;
@@ -699,7 +701,8 @@ __global__ __launch_bounds__(OC_T) void k_hs_assoc(HsArgs a) {
         block_sync();
         if (!c->lap_done)   // else solved by k_hs_lap
             main_lap(LapMat{cost, n_hi, n_trk, false}, a.pre_u + db, a.pre_x + db, a.pre_s2 + db,
-                 a.rmatch + db, lds, lds_bytes, gws, &c->err, &c->ls);
+                 a.rmatch + db, lds, lds_bytes, gws, &c->err, &c->ls,
+                     a.lap_csr ? a.lap_csr + s * a.lap_csr_stride : nullptr);
         YTA_STAMP(1);
         if (t == 0) c->lap_calls = 1;
         for (int j = t; j < n_trk; j += nt) a.cmatched[tb + j] = 0;
@@ -1193,6 +1196,9 @@ int hs_alloc(yta_hybridsort *e) {
     a.arr_chip = MAXD >= ARR_CHIP_MIN_DETS;
     if (const char *v = getenv("YTA_ARR_CHIP")) a.arr_chip = atoi(v);
     HSALLOC(a.lap_ws, S * a.lap_ws_stride);
+    a.lap_csr = nullptr;
+    a.lap_csr_stride = n >= LAPB_MIN_N && lap_sparse_on() ? (lap_csr_bytes(n) + 255) & ~255LL : 0;
+    if (a.lap_csr_stride) HSALLOC(a.lap_csr, S * a.lap_csr_stride);
     e->lds = (size_t)oc_lds_bytes(CAP, MAXD);
     HSALLOC(e->d_off, S + 1);
     YTA_HIP(hipHostMalloc((void **)&e->h_off, sizeof(int) * (S + 1), hipHostMallocDefault));

@@ -125,12 +125,13 @@ constexpr int LAP_PADDED_T = 512;
 __global__ __launch_bounds__(LAP_PADDED_T) void k_lap_padded(const double *cost, int nr, int nc,
                                                              int *X, int *Y, int *err,
                                                              unsigned char *gws,
-                                                             long long lds_bytes) {
+                                                             long long lds_bytes,
+                                                             unsigned char *csr) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int n = nr > nc ? nr : nc;
     const LapMat M{cost, nr, nc, false};
     DenseLapWs w;
-    const int rc = lap_dense_block(n, M, smem, lds_bytes, gws, w);
+    const int rc = lap_dense_block(n, M, smem, lds_bytes, gws, w, csr);
     if (rc && threadIdx.x == 0) atomicOr(err, ERR_SOLVER);
     for (int r = threadIdx.x; r < nr; r += blockDim.x) X[r] = w.x[r] < nc ? w.x[r] : -1;
     for (int k = threadIdx.x; k < nc; k += blockDim.x) Y[k] = w.y[k] < nr ? w.y[k] : -1;
@@ -570,6 +571,8 @@ int yta_lap_padded(int device, int nr, int nc, const double *cost, int *x, int *
     YTA_HIP(m.get(&dy, nc > 0 ? nc : 1));
     YTA_HIP(m.get(&derr, 1));
     YTA_HIP(m.get(&gws, ws));
+    unsigned char *csr = nullptr;   // the sparse sweeps' row entries (lap_dense_block.hpp)
+    if (n >= LAPB_MIN_N && lap_sparse_on()) YTA_HIP(m.get(&csr, (size_t)lap_csr_bytes(n)));
     YTA_HIP(hipMemset(derr, 0, sizeof(int)));
     if (dcost)
         YTA_HIP(hipMemcpy(dcost, cost, sizeof(double) * nr * nc, hipMemcpyHostToDevice));
@@ -579,7 +582,7 @@ int yta_lap_padded(int device, int nr, int nc, const double *cost, int *x, int *
     YTA_HIP(hipFuncSetAttribute((const void *)k_lap_padded,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)LAP_PADDED_LDS));
     hipLaunchKernelGGL(k_lap_padded, dim3(1), dim3(LAP_PADDED_T), (size_t)lds, 0, dcost, nr, nc, dx,
-                       dy, derr, gws, lds);
+                       dy, derr, gws, lds, csr);
     YTA_HIP(hipGetLastError());
     int herr = 0;
     if (nr) YTA_HIP(hipMemcpy(x, dx, sizeof(int) * nr, hipMemcpyDeviceToHost));

@@ -12,10 +12,41 @@
 // hits' swaps from a position bitmap in order.  gather_min: a position qualifies when its
 // distance is <= the running minimum of the earlier ones; a block prefix-minimum over contiguous
 // position ranges marks them, and thread 0 replays their swaps (with the resets) in order.
+//
+// Sparse sweeps (tools/lapjv_sparse_proto.c): a sweep from scanned column k (row
+// r, h = c[r][k] - v[k] - d[k]) relaxes a zero entry kk only if -h < d[kk] + v[kk], and d[kk] +
+// v[kk] <= c[src][kk] <= cmax (the search's source row maximum) for the whole search.  When
+// -h >= cmax only the row's nonzero entries can change anything, and the columns not yet visited
+// keep their positions during a sweep, so wave 0 visits just those entries, in position order
+// (pos: the inverse of cols), and runs such sweeps back to back without block barriers; a sweep
+// that needs the dense form (or a row with more than LAPS_K nonzero entries) goes to the block.
+// The rows' nonzero entries are collected once per replay into `csr_ws` (lap_csr_bytes).
 #pragma once
+#include <cstdlib>
+
 #include "lap_dense.hpp"
 
 namespace yta {
+
+constexpr int LAPS_K = 16;   // nonzero entries per row kept for the sparse sweeps
+__host__ __device__ inline long long lap_csr_bytes(long long n) { return 16 * n * LAPS_K; }
+// the sparse sweeps are on unless YTA_LAP_SPARSE=0 (host: engines' workspace, the KAT)
+inline bool lap_sparse_on() {
+    const char *v = getenv("YTA_LAP_SPARSE");
+    return !v || atoi(v) != 0;
+}
+// Row r's entries at ent[r * LAPS_K + i], ascending columns: (value, bits(count << 32 | column)),
+// every entry of the row carrying the row's count of nonzero entries (-1: more than LAPS_K;
+// entry 0 holds it also when the row has none), so one 16-B load per lane brings a sweep its row.
+struct LapCsr {
+    double2 *ent;
+};
+__device__ __forceinline__ LapCsr lap_csr(unsigned char *base, int) {
+    return LapCsr{reinterpret_cast<double2 *>(base)};
+}
+__device__ __forceinline__ double2 lap_csr_entry(double val, int col, int cnt) {
+    return make_double2(val, __longlong_as_double(((long long)cnt << 32) | (unsigned)col));
+}
 
 constexpr int LAPB_MAX_N = 8192;    // positions covered by the sweep bitmap (1 KiB of LDS)
 constexpr int LAPB_MIN_N = 768;     // below this the one-wave replay is as fast
@@ -50,7 +81,8 @@ struct LapBShared {
 // bits: the marks over positions [h0, h0 + 32 nwords) (nwords <= blockDim.x).  hitpos (n ints)
 // and tmp (2 n ints) are scratch.  Returns m.
 template <typename IP, typename HP, typename TP>
-__device__ int lapb_swap_front(int h0, int nwords, IP cols, HP hitpos, TP tmp, LapBShared &sh) {
+__device__ int lapb_swap_front(int h0, int nwords, IP cols, HP hitpos, TP tmp, LapBShared &sh,
+                               IP pos = nullptr) {
     const int t = threadIdx.x, nt = blockDim.x;
     LAPB_T0();
     const unsigned wbits = t < nwords ? sh.bits[t] : 0u;
@@ -80,8 +112,16 @@ __device__ int lapb_swap_front(int h0, int nwords, IP cols, HP hitpos, TP tmp, L
         if (!marked) tmp[m + (o - rank_before(q))] = cols[q];
     }
     block_sync();
-    for (int i = t; i < m; i += nt) cols[h0 + i] = tmp[i];
-    for (int r = t; r < m - k; r += nt) cols[hitpos[k + r]] = tmp[m + r];
+    for (int i = t; i < m; i += nt) {
+        const int c = tmp[i];
+        cols[h0 + i] = c;
+        if (pos) pos[c] = h0 + i;
+    }
+    for (int r = t; r < m - k; r += nt) {
+        const int q = hitpos[k + r], c = tmp[m + r];
+        cols[q] = c;
+        if (pos) pos[c] = q;
+    }
     block_sync();
     LAPB_DT(66);
     LAPB_ADD(67, m);
@@ -144,15 +184,103 @@ __device__ __forceinline__ int lapb_relax_regs(int n, const LapMat &M, int base,
     return ffin;
 }
 
+// Sparse sweeps by wave 0 (the header's argument): from position l while l != h, as long as the
+// scanned row has <= LAPS_K nonzero entries and -h >= cmax.  Returns a free column reached at the
+// minimum (l / h then as the caller passed them, as lapjv.c's early return), else -1 with l / h
+// advanced over the sweeps done.  Stores of one lane are read by others after lap_sync<false>.
+template <typename DP, typename IP>
+__device__ int lapb_sparse_sweeps(int &l, int &h, DP d, DP v, IP cols, IP pred, IP y, IP pos,
+                                  const LapCsr &cs, double cmax) {
+    const int lane = lane_id();
+    int ll = l, hh = h;
+    while (ll != hh) {
+        const int k = cols[ll];
+        const int r = y[k];
+        const double dk = d[k], vk = v[k];
+        double2 en = make_double2(0.0, 0.0);
+        if (lane < LAPS_K) en = cs.ent[(long long)r * LAPS_K + lane];
+        const long long bits = __double_as_longlong(en.y);
+        const int cnt = __shfl((int)(bits >> 32), 0);
+        if (cnt < 0) break;   // a row with more entries: the block's sweep
+        const bool in = lane < cnt;
+        const int kk = in ? (int)(unsigned)bits : -1;
+        const double cv = in ? en.x : 0.0;
+        const unsigned long long mk = __ballot(in && kk == k);
+        const double crk = mk ? __shfl(cv, __ffsll((long long)mk) - 1) : 0.0;
+        const double hr = crk - vk - dk;
+        if (!(-hr >= cmax)) break;   // a zero entry may relax: the block's sweep
+        ++ll;
+        const int p = in ? pos[kk] : -1;
+        double nd = 0.0;
+        bool upd = false;
+        if (in && p >= hh) {
+            nd = cv - v[kk] - hr;
+            upd = nd < d[kk];
+        }
+        const bool eq = upd && nd == dk;
+        const bool fr = eq && y[kk] < 0;
+        const double pfd = wave_reduce(RED_MIN, fr ? (double)p : 1e300);
+        const int pf = pfd >= 1e300 ? INT_MAX : (int)pfd;
+        if (upd && p <= pf) {   // the updates up to the first free hit (inclusive)
+            d[kk] = nd;
+            pred[kk] = r;
+        }
+        if (pf != INT_MAX) {
+            lap_sync<false>();
+            const unsigned long long mf = __ballot(fr && p == pf);
+            return __shfl(kk, __ffsll((long long)mf) - 1);
+        }
+        // the hits to the front, in position order
+        bool pend = eq;
+        while (__ballot(pend)) {
+            const double pm = wave_reduce(RED_MIN, pend ? (double)p : 1e300);
+            lap_sync<false>();
+            if (pend && (double)p == pm) {
+                const int c = cols[hh];
+                cols[p] = c;
+                pos[c] = p;
+                cols[hh] = kk;
+                pos[kk] = hh;
+                pend = false;
+            }
+            ++hh;
+        }
+        lap_sync<false>();
+    }
+    l = ll;
+    h = hh;
+    return -1;
+}
+
 // relax_scan (lapjv.c) by the block.  Returns a free column reached at the minimum distance
 // (lo / hi left as they were, as the C code's early return leaves *plo / *phi), or -1 with
-// lo / hi advanced.
+// lo / hi advanced.  cs: the rows' nonzero entries (sparse sweeps by wave 0 where they apply, pos
+// maintained), or nullptr.
 template <typename DP, typename IP, typename HP, typename TP>
 __device__ int lapb_relax_scan(int n, const LapMat &M, int &lo, int &hi, DP d, DP v, IP cols,
-                               IP pred, IP y, HP hitpos, TP tmp, LapBShared &sh, int &par) {
+                               IP pred, IP y, HP hitpos, TP tmp, LapBShared &sh, int &par,
+                               IP pos = nullptr, const LapCsr *cs = nullptr, double cmax = 0.0) {
     const int t = threadIdx.x, nt = blockDim.x;
     int l = lo, h = hi;
     while (l != h) {
+        if (cs) {
+            if (t < WAVE) {
+                int ls = l, hs = h;
+                const int e = lapb_sparse_sweeps(ls, hs, d, v, cols, pred, y, pos, *cs, cmax);
+                if (t == 0) {
+                    sh.lo = ls;
+                    sh.hi = hs;
+                    sh.end = e;
+                }
+            }
+            block_sync();
+            const int e = sh.end;
+            l = sh.lo;
+            h = sh.hi;
+            block_sync();
+            if (e >= 0) return e;
+            if (l == h) break;
+        }
         LAPB_ADD(63, 1);
         LAPB_T0();
         const int k = cols[l++];
@@ -195,7 +323,7 @@ __device__ int lapb_relax_scan(int n, const LapMat &M, int &lo, int &hi, DP d, D
         }
         block_sync();
         const int last = ffin < n ? ffin - base : cnt;
-        h += lapb_swap_front(base, (last + 31) / 32, cols, hitpos, tmp, sh);
+        h += lapb_swap_front(base, (last + 31) / 32, cols, hitpos, tmp, sh, pos);
         const int end = ffin < n ? cols[ffin] : -1;   // ffin is beyond every moved position
         LAPB_DT(64);
         if (end >= 0) return end;
@@ -213,7 +341,7 @@ __device__ int lapb_relax_scan(int n, const LapMat &M, int &lo, int &hi, DP d, D
 // by thread 0 (with their resets), then q* and the later ties to m* are one swap-to-front from lo.
 template <typename DP, typename IP, typename HP, typename TP>
 __device__ int lapb_gather_min(int n, int lo, DP d, IP cols, HP hitpos, TP tmp, LapBShared &sh,
-                               int &par) {
+                               int &par, IP pos = nullptr) {
     const int t = threadIdx.x, nt = blockDim.x, lane = lane_id(), wv = t / WAVE;
     LAPB_ADD(65, 1);
     const double m0 = d[cols[lo]];
@@ -230,7 +358,7 @@ __device__ int lapb_gather_min(int n, int lo, DP d, IP cols, HP hitpos, TP tmp, 
         for (int q = first + t; q < n; q += nt)
             if (d[cols[q]] == m0) atomicOr(&sh.bits[(q - first) >> 5], 1u << ((q - first) & 31));
         block_sync();
-        return first + lapb_swap_front(first, (cnt + 31) / 32, cols, hitpos, tmp, sh);
+        return first + lapb_swap_front(first, (cnt + 31) / 32, cols, hitpos, tmp, sh, pos);
     }
     // q*: the first position holding the minimum
     double fq = 1e300;
@@ -279,8 +407,13 @@ __device__ int lapb_gather_min(int n, int lo, DP d, IP cols, HP hitpos, TP tmp, 
                     hi = lo;
                     m = e;
                 }
-                cols[p] = cols[hi];
+                const int c = cols[hi];
+                cols[p] = c;
                 cols[hi] = k;
+                if (pos) {
+                    pos[c] = p;
+                    pos[k] = hi;
+                }
                 ++hi;
             }
         }
@@ -293,35 +426,84 @@ __device__ int lapb_gather_min(int n, int lo, DP d, IP cols, HP hitpos, TP tmp, 
     for (int q = qs + t; q < n; q += nt)
         if (d[cols[q]] == gmin) atomicOr(&sh.bits[(q - lo) >> 5], 1u << ((q - lo) & 31));
     block_sync();
-    return lo + lapb_swap_front(lo, (cnt2 + 31) / 32, cols, hitpos, tmp, sh);
+    return lo + lapb_swap_front(lo, (cnt2 + 31) / 32, cols, hitpos, tmp, sh, pos);
 }
 
 // Phase 3 for the free rows w.free_rows[0 .. nfree) left by phases 1-2 (all threads of the block).
 // Returns 0, or -2 when an augmenting path does not close.
-template <bool LDS_WS>
-__device__ int lap_dense_block_p3(int n, const LapMat M, const DenseLapWs w, int nfree) {
-    __shared__ LapBShared sh;
+// The rows' nonzero entries (M.at != 0, ascending columns, up to LAPS_K; more: cnt -1), one wave
+// per row, columns over the lanes.
+__device__ __forceinline__ void lap_csr_build(int n, const LapMat &M, const LapCsr &cs) {
+    const int lane = lane_id(), nw = blockDim.x / WAVE;
+    for (int r = threadIdx.x / WAVE; r < n; r += nw) {
+        int c = 0;   // the row's nonzero entries (counted first: each kept entry carries it)
+        if (r < M.na)
+            for (int k0 = 0; k0 < M.nb && c <= LAPS_K; k0 += WAVE) {
+                const int k = k0 + lane;
+                c += __popcll(__ballot(k < M.nb && M.real(r, k) != 0.0));
+            }
+        const int cnt = c <= LAPS_K ? c : -1;
+        if (cnt <= 0) {
+            if (lane == 0) cs.ent[(long long)r * LAPS_K] = lap_csr_entry(0.0, 0, cnt);
+            continue;
+        }
+        int w = 0;
+        for (int k0 = 0; k0 < M.nb && w < cnt; k0 += WAVE) {
+            const int k = k0 + lane;
+            const double e = k < M.nb ? M.real(r, k) : 0.0;
+            const bool nz = k < M.nb && e != 0.0;
+            const unsigned long long b = __ballot(nz);
+            if (nz) cs.ent[(long long)r * LAPS_K + w + __popcll(b & ((1ull << lane) - 1ull))] =
+                lap_csr_entry(e, k, cnt);
+            w += __popcll(b);
+        }
+    }
+}
+
+// sh: the caller's (one static LDS instance for every instantiation).
+template <bool LDS_WS, bool SPARSE>
+__device__ int lap_dense_block_p3(int n, const LapMat M, const DenseLapWs w, int nfree,
+                                  unsigned char *csr_ws, LapBShared &sh) {
     const int t = threadIdx.x, nt = blockDim.x;
     auto x = ws_ptr<LDS_WS>(w.x), y = ws_ptr<LDS_WS>(w.y), fr = ws_ptr<LDS_WS>(w.free_rows);
     auto cols = ws_ptr<LDS_WS>(w.cols), pred = ws_ptr<LDS_WS>(w.pred);
     auto v = ws_ptr<LDS_WS>(w.v), d = ws_ptr<LDS_WS>(w.d);
-    // scratch of the swap-to-front: aux (n ints) and the unused row buffers (2 n doubles)
-    auto hitpos = ws_ptr<LDS_WS>(w.aux);
+    // scratch of the swap-to-front: aux (n ints) and the unused row buffers (2 n doubles); with
+    // the sparse sweeps aux holds the inverse permutation of cols and the hit positions go to the
+    // row buffers' second half
     int *tmp = reinterpret_cast<int *>(w.row);
+    constexpr bool sparse = SPARSE;
+    auto hitpos = [&] {
+        if constexpr (SPARSE) return tmp + 2 * n;
+        else return ws_ptr<LDS_WS>(w.aux);
+    }();
+    decltype(ws_ptr<LDS_WS>(w.aux)) pos = SPARSE ? ws_ptr<LDS_WS>(w.aux) : nullptr;
+    LapCsr cs{};
+    if (sparse) {
+        cs = lap_csr(csr_ws, n);
+        lap_csr_build(n, M, cs);
+        block_sync();
+    }
     int par = 0;
     for (int f = 0; f < nfree; ++f) {
         const int src = fr[f];
+        double lmax = -LAP_BIG;
         for (int k = t; k < n; k += nt) {
+            const double c = M.at(src, k);
             cols[k] = k;
+            if (sparse) pos[k] = k;
             pred[k] = src;
-            d[k] = M.at(src, k) - v[k];
+            d[k] = c - v[k];
+            lmax = c > lmax ? c : lmax;
         }
+        // the source row's maximum (bounds d + v of every column during this search)
+        const double cmax = sparse ? lapb_reduce(false, lmax, sh, par) : 0.0;
         block_sync();
         int lo = 0, hi = 0, ready = 0, end = -1;
         while (end < 0) {
             if (lo == hi) {
                 ready = lo;
-                hi = lapb_gather_min(n, lo, d, cols, hitpos, tmp, sh, par);
+                hi = lapb_gather_min(n, lo, d, cols, hitpos, tmp, sh, par, pos);
                 // the last free column of the gathered set
                 double e = -1.0;
                 for (int q = lo + t; q < hi; q += nt)
@@ -329,7 +511,9 @@ __device__ int lap_dense_block_p3(int n, const LapMat M, const DenseLapWs w, int
                 e = lapb_reduce(false, e, sh, par);
                 if (e >= 0.0) end = cols[(int)e];
             }
-            if (end < 0) end = lapb_relax_scan(n, M, lo, hi, d, v, cols, pred, y, hitpos, tmp, sh, par);
+            if (end < 0)
+                end = lapb_relax_scan(n, M, lo, hi, d, v, cols, pred, y, hitpos, tmp, sh, par, pos,
+                                      sparse ? &cs : nullptr, cmax);
         }
         const double m = d[cols[lo]];
         for (int q = t; q < ready; q += nt) {
@@ -365,7 +549,7 @@ __device__ int lap_dense_block_p3(int n, const LapMat M, const DenseLapWs w, int
 // solver's rc (0 on success).
 __device__ __forceinline__ int lap_dense_block(int n, const LapMat M, unsigned char *lds,
                                                long long lds_bytes, unsigned char *gws,
-                                               DenseLapWs &w) {
+                                               DenseLapWs &w, unsigned char *csr_ws = nullptr) {
     __shared__ int s_rc;
     if (n < LAPB_MIN_N || n > LAPB_MAX_N || blockDim.x < 256) {
         if (threadIdx.x < WAVE) {
@@ -392,8 +576,12 @@ __device__ __forceinline__ int lap_dense_block(int n, const LapMat M, unsigned c
     block_sync();
     YTA_STAMP_ABS(61);
     if (nfree < 0) return nfree;
-    const int rc = in_lds ? lap_dense_block_p3<true>(n, M, w, nfree)
-                          : lap_dense_block_p3<false>(n, M, w, nfree);
+    __shared__ LapBShared sh;
+    int rc;
+    if (csr_ws) rc = in_lds ? lap_dense_block_p3<true, true>(n, M, w, nfree, csr_ws, sh)
+                            : lap_dense_block_p3<false, true>(n, M, w, nfree, csr_ws, sh);
+    else rc = in_lds ? lap_dense_block_p3<true, false>(n, M, w, nfree, nullptr, sh)
+                     : lap_dense_block_p3<false, false>(n, M, w, nfree, nullptr, sh);
     YTA_STAMP_ABS(62);
     return rc;
 }

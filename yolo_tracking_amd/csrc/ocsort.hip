@@ -82,6 +82,8 @@ struct OcArgs {
     int *udet, *utrk, *tmp;        // [S*(MAXD+CAP)]
     int *upd;                      // [S*CAP] update source per tracker: input row, -1 none
     unsigned char *lap_ws;         // per stream (n > OC_LDS_LAP_N)
+    unsigned char *lap_csr;         // per stream: the replay's row entries (nullptr: n < LAPB_MIN_N)
+    long long lap_csr_stride;
     long long lap_ws_stride;
     double *pre_u, *pre_s2;        // [S*MAXD] first-round row pre-pass (lap_rect.hpp)
     int *pre_x;
@@ -411,7 +413,8 @@ __global__ __launch_bounds__(OC_T) void k_oc_assoc(OcArgs a) {
         } else if (n_hi > 0 && !solved) {
             block_sync();
             main_lap(LapMat{mat2, n_hi, n_trk, false}, a.pre_u + db, a.pre_x + db, a.pre_s2 + db,
-                     a.rmatch + db, lds, lds_bytes, gws, &c->err, &c->ls);
+                     a.rmatch + db, lds, lds_bytes, gws, &c->err, &c->ls,
+                     a.lap_csr ? a.lap_csr + s * a.lap_csr_stride : nullptr);
         }
         YTA_STAMP(4);
         if (t == 0) { c->fast_path = fast; c->lap_calls = (fast || n_hi == 0) ? 0 : 1; }
@@ -743,6 +746,9 @@ int oc_alloc(yta_ocsort *e) {
     const long long n = std::max(CAP, MAXD);
     a.lap_ws_stride = oc_lap_ws_stride(n);
     OCALLOC(a.lap_ws, S * a.lap_ws_stride);
+    a.lap_csr = nullptr;
+    a.lap_csr_stride = n >= LAPB_MIN_N && lap_sparse_on() ? (lap_csr_bytes(n) + 255) & ~255LL : 0;
+    if (a.lap_csr_stride) OCALLOC(a.lap_csr, S * a.lap_csr_stride);
     e->lds = (size_t)oc_lds_bytes(CAP, MAXD);
     OCALLOC(e->d_off, S + 1);
     OCALLOC(e->d_wh, 2 * S);

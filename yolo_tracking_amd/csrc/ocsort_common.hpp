@@ -63,7 +63,7 @@ struct LapStats {
 // in `gws` when those fit (n <= ~3900 in the 156 KiB of the first-round kernels); else all in gws.
 __device__ __forceinline__ void padded_lap(const LapMat &M, int *rx, unsigned char *lds,
                                            long long lds_bytes, unsigned char *gws, int *err,
-                                           LapStats *ls) {
+                                           LapStats *ls, unsigned char *csr = nullptr) {
     const int n = M.na > M.nb ? M.na : M.nb;
     if (threadIdx.x == 0 && n > 0) ls->replays += 1;
     {
@@ -75,7 +75,7 @@ __device__ __forceinline__ void padded_lap(const LapMat &M, int *rx, unsigned ch
     }
     if (n > 0) {   // the whole block (phase 3 block-wide for large n, lap_dense_block.hpp)
         DenseLapWs w;
-        const int rc = lap_dense_block(n, M, lds, lds_bytes, gws, w);
+        const int rc = lap_dense_block(n, M, lds, lds_bytes, gws, w, csr);
         if (rc && threadIdx.x == 0) atomicOr(err, ERR_SOLVER);
         for (int r = threadIdx.x; r < M.na; r += blockDim.x) rx[r] = w.x[r] < M.nb ? w.x[r] : -1;
     }
@@ -150,15 +150,16 @@ __device__ __forceinline__ void rect_solve(const RectMat &R, const double *pu, c
 // First-round solve of association.py:20-28 on the padded problem M (rows = detections, columns =
 // trackers) when k_*_lap left it (more than 16384 trackers): the rectangular solver with
 // trackers >= detections, otherwise the lapjv replay.
+// csr: the engine's lap_csr region of the stream (lap_dense_block.hpp sparse sweeps) or nullptr.
 __device__ __forceinline__ void main_lap(const LapMat &M, const double *pu, const int *px,
                                          const double *ps2, int *rx, unsigned char *lds,
                                          long long lds_bytes, unsigned char *gws, int *err,
-                                         LapStats *ls) {
+                                         LapStats *ls, unsigned char *csr = nullptr) {
     if (M.na <= M.nb && M.nb <= RECT_CPT_MAX * (int)blockDim.x)
         rect_solve(RectMat{M.m, M.na, M.nb, M.nb, 1, M.neg}, pu, px, ps2, false, M.na, rx, lds,
                    lds_bytes, gws, err);
     else
-        padded_lap(M, rx, lds, lds_bytes, gws, err, ls);
+        padded_lap(M, rx, lds, lds_bytes, gws, err, ls, csr);
 }
 
 // Row pre-pass of the first-round solve for one stream, spread over the blocks of a chip-wide
