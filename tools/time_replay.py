@@ -44,7 +44,8 @@ if os.environ.get("YTA_STAMPS_READ"):   # diagnostic library: phase split of the
     print(f"phases 1-2 {(int(st[61]) - int(st[60])) / 100:.0f} us, phase 3 "
           f"{(int(st[62]) - int(st[61])) / 100:.0f} us (100 MHz stamps); sweeps {int(st[63])} "
           f"({int(st[64]) / 100:.0f} us incl. swaps), gathers {int(st[65])}, swap-to-front "
-          f"{int(st[66]) / 100:.0f} us moving {int(st[67])} marked columns", flush=True)
+          f"{int(st[66]) / 100:.0f} us moving {int(st[67])} marked columns); sparse sweeps "
+          f"{int(st[68])} ({int(st[69]) / 100:.0f} us, wave 0)", flush=True)
 same = np.array_equal(np.where(np.asarray(x) < args.nb, x, -1), np.where(x_ref < args.nb, x_ref, -1))
 print(f"replay {t_gpu * 1e3:.1f} ms on the device, oracle/lapjv.c {t_cpu * 1e3:.1f} ms on one core, "
       f"assignments equal: {same}", flush=True)

@@ -265,6 +265,7 @@ __device__ int lapb_relax_scan(int n, const LapMat &M, int &lo, int &hi, DP d, D
     while (l != h) {
         if (cs) {
             if (t < WAVE) {
+                LAPB_T0();
                 int ls = l, hs = h;
                 const int e = lapb_sparse_sweeps(ls, hs, d, v, cols, pred, y, pos, *cs, cmax);
                 if (t == 0) {
@@ -272,6 +273,8 @@ __device__ int lapb_relax_scan(int n, const LapMat &M, int &lo, int &hi, DP d, D
                     sh.hi = hs;
                     sh.end = e;
                 }
+                LAPB_DT(69);
+                LAPB_ADD(68, ls - l + (e >= 0));
             }
             block_sync();
             const int e = sh.end;
