@@ -46,6 +46,10 @@ if os.environ.get("YTA_STAMPS_READ"):   # diagnostic library: phase split of the
           f"({int(st[64]) / 100:.0f} us incl. swaps), gathers {int(st[65])}, swap-to-front "
           f"{int(st[66]) / 100:.0f} us moving {int(st[67])} marked columns); sparse sweeps "
           f"{int(st[68])} ({int(st[69]) / 100:.0f} us, wave 0)", flush=True)
+    if st[20] and st[21] and st[22]:
+        print(f"  phase 1 column reduction {(int(st[20]) - int(st[60])) / 100:.0f} us, reduction "
+              f"transfer {(int(st[21]) - int(st[20])) / 100:.0f} us, phase 2 "
+              f"{(int(st[22]) - int(st[21])) / 100:.0f} us", flush=True)
 same = np.array_equal(np.where(np.asarray(x) < args.nb, x, -1), np.where(x_ref < args.nb, x_ref, -1))
 print(f"replay {t_gpu * 1e3:.1f} ms on the device, oracle/lapjv.c {t_cpu * 1e3:.1f} ms on one core, "
       f"assignments equal: {same}", flush=True)

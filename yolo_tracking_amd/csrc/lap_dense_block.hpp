@@ -210,17 +210,24 @@ __device__ int lapb_sparse_sweeps(int &l, int &h, DP d, DP v, IP cols, IP pred, 
         const double hr = crk - vk - dk;
         if (!(-hr >= cmax)) break;   // a zero entry may relax: the block's sweep
         ++ll;
-        const int p = in ? pos[kk] : -1;
+        // the entry columns' position, price, distance and row in one round trip
+        const int ks = in ? kk : k;
+        const int p0 = pos[ks], yk = y[ks];
+        const double vkk = v[ks], dkk = d[ks];
+        const int p = in ? p0 : -1;
         double nd = 0.0;
         bool upd = false;
         if (in && p >= hh) {
-            nd = cv - v[kk] - hr;
-            upd = nd < d[kk];
+            nd = cv - vkk - hr;
+            upd = nd < dkk;
         }
         const bool eq = upd && nd == dk;
-        const bool fr = eq && y[kk] < 0;
-        const double pfd = wave_reduce(RED_MIN, fr ? (double)p : 1e300);
-        const int pf = pfd >= 1e300 ? INT_MAX : (int)pfd;
+        const bool fr = eq && yk < 0;
+        int pf = INT_MAX;   // the first free hit's position (a reduction only when there is one)
+        if (__ballot(fr)) {
+            const double pfd = wave_reduce(RED_MIN, fr ? (double)p : 1e300);
+            pf = (int)pfd;
+        }
         if (upd && p <= pf) {   // the updates up to the first free hit (inclusive)
             d[kk] = nd;
             pred[kk] = r;
