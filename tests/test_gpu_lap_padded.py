@@ -57,17 +57,30 @@ def _surge(rng, na, nb, per_col):
     return c
 
 
+def _mixed(rng, na, nb):
+    """Rows of 0-20 nonzero entries of either sign among exact zeros: rows on both sides of the
+    sparse sweeps' 16-entry limit, positive entries (a source row maximum above 0)."""
+    c = np.zeros((na, nb))
+    for i in range(na):
+        k = int(rng.integers(0, 21))
+        c[i, rng.choice(nb, size=k, replace=False)] = rng.uniform(-0.9, 0.3, k)
+    return c
+
+
 @pytest.mark.parametrize("case", ["ints_900x700", "zeros_1200", "ties_800x1500", "surge_2000x800",
-                                  "surge_4000x500"])
+                                  "surge_4000x500", "mixed_1500x900", "mixed_900x1400"])
 def test_lap_padded_block_replay_tie_heavy(case):
     """n >= 768: phase 3 runs block-wide (lap_dense_block.hpp); tie-heavy matrices exercise its
-    swap-to-front and gather resets; 4000 x 500 also puts the work arrays in global memory."""
+    swap-to-front and gather resets, the zero-heavy ones its sparse sweeps; 4000 x 500 also puts
+    the work arrays in global memory."""
     rng = np.random.default_rng(sum(map(ord, case)))
     c = {"ints_900x700": lambda: rng.integers(0, 4, size=(900, 700)).astype(np.float64),
          "zeros_1200": lambda: np.zeros((1200, 1200)),
          "ties_800x1500": lambda: -rng.integers(0, 3, size=(800, 1500)).astype(np.float64),
          "surge_2000x800": lambda: _surge(rng, 2000, 800, 3),
-         "surge_4000x500": lambda: _surge(rng, 4000, 500, 2)}[case]()
+         "surge_4000x500": lambda: _surge(rng, 4000, 500, 2),
+         "mixed_1500x900": lambda: _mixed(rng, 1500, 900),
+         "mixed_900x1400": lambda: _mixed(rng, 900, 1400)}[case]()
     _, xo, yo = lapjv(c, extend_cost=True)
     x, y = _lib.lap_padded(c)
     assert np.array_equal(x, xo), (case, np.nonzero(x != xo)[0][:10])
