@@ -93,7 +93,13 @@ def main():
     _lib.check(lib.yta_debug_stamps(st.ctypes.data))
     st = st.astype(np.int64)
     print("stats", eng.stats())
-    if st[60]:   # ByteTrack: stage 1 as k_s1_prep / k_s1_edges / k_s1_lap
+    if args.tracker == "botsort":   # split stage 1: k_bs_prep (stage1_lists), k_bs_lap (s1_lap_body)
+        show(st, 0, {2: "dets pass", 4: "tracked/lost pass"}, "k_bs_prep")
+        show(st, 90, [(1, "row offsets"), (2, "CSR fill"), (8, "lap init"), (9, "lap P1 union"),
+                      (10, "lap P2 roots"), (11, "lap P3 lists"), (12, "lap P4 gather"),
+                      (13, "lap classify"), (14, "lap solve"), (3, "lap return"),
+                      (4, "results out")], "k_bs_lap")
+    elif st[60]:   # ByteTrack: stage 1 as k_s1_prep / k_s1_edges / k_s1_lap
         show(st, 60, {1: "dets pass", 2: "tracked pass", 3: "lost pass"}, "k_s1_prep")
         show(st, 66, {1: "grid build", 2: "edges"}, "k_s1_edges")
         show(st, 90, [(1, "row offsets"), (2, "CSR fill"), (8, "lap init"), (9, "lap P1 union"),

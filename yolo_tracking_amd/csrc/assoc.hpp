@@ -246,11 +246,10 @@ namespace yta {
 // Cosine distance of two float32 feature rows in float64 (scipy cdist 'cosine':
 // 1 - u.v / (|u| |v|)), by one 16-lane row group: every lane accumulates a strided share, the
 // row group reduces with DPP.  Returns the value on every lane of the group.
-template <typename ColElem>
+template <int CB = 16, typename ColElem>   // CB: elements per lane loaded before any is used
 __device__ __forceinline__ double cosine_dist16(const float *u, ColElem v, int D) {
     const int l16 = lane_id() & 15;
     double d = 0.0, nu = 0.0, nv = 0.0;
-    constexpr int CB = 16;   // elements per lane loaded before any is used (one round trip)
     int k = l16;
     for (; k + 16 * (CB - 1) < D; k += 16 * CB) {
         float ua[CB], va[CB];
@@ -302,6 +301,8 @@ __host__ __device__ inline long long assoc_emb_arena_bytes(long long R, long lon
            512;
 }
 
+constexpr int EMB_PAIRS_SMALL = 4096;   // assoc_block_emb: every pair tested up to this many
+
 template <typename RowBox, typename ColBox, typename ColScore, typename RowFeat, typename ColFeat>
 __device__ __forceinline__ bool assoc_block_emb(int nr, RowBox rowbox, int nc, ColBox colbox,
                                                 bool fused, ColScore colscore, RowFeat rowfeat,
@@ -310,8 +311,24 @@ __device__ __forceinline__ bool assoc_block_emb(int nr, RowBox rowbox, int nc, C
                                                 int *n_edges, Arena &ar, const LapSlab &slab,
                                                 AssocShared &sh) {
     const int t = threadIdx.x, nt = blockDim.x;
-    const bool use_grid = prox < 1.0 && thresh <= 1.0 && nr > 0 && nc > 0;
+    bool use_grid = prox < 1.0 && thresh <= 1.0 && nr > 0 && nc > 0;
     const size_t lo0 = ar.lo;
+    // few pairs (prox < 1, thresh <= 1): every pair tested, pairs over the threads, from row and
+    // column boxes staged in the arena - one round of loads instead of a grid's five passes
+    Box *rst = nullptr, *cst = nullptr;
+    double *wst = nullptr;
+    if (use_grid && (long long)nr * nc <= EMB_PAIRS_SMALL) {
+        rst = ar.try_alloc<Box>(nr);
+        cst = ar.try_alloc<Box>(nc);
+        wst = ar.try_alloc<double>(nc);
+        if (!rst || !cst || !wst) {
+            ar.lo = lo0;
+            rst = cst = nullptr;
+            wst = nullptr;
+        } else {
+            use_grid = false;
+        }
+    }
     GridView gv{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
     if (use_grid) {
         gv.cell_start = ar.alloc<int>(grid_cells_for(nc) + 1);
@@ -334,8 +351,17 @@ __device__ __forceinline__ bool assoc_block_emb(int nr, RowBox rowbox, int nc, C
     int2 *edge = ar.alloc_top<int2>(ecap);
     double *edge_c = ar.alloc_top<double>(ecap);
     if (ar.fail) return false;
-    for (int i = t; i <= nr; i += nt) row_off[i] = 0;
-    for (int j = t; j < nc; j += nt) col_deg[j] = 0;
+    for (int i = t; i <= nr; i += nt) {
+        row_off[i] = 0;
+        if (rst && i < nr) rst[i] = rowbox(i);
+    }
+    for (int j = t; j < nc; j += nt) {
+        col_deg[j] = 0;
+        if (cst) {
+            cst[j] = colbox(j);
+            wst[j] = fused ? colscore(j) : 1.0;
+        }
+    }
     if (t == 0) { sh.lap.cnt[0] = 0; sh.lap.cnt[1] = 0; sh.lap.cnt[2] = 0; }
     if (use_grid) {
         block_sync();
@@ -373,7 +399,14 @@ __device__ __forceinline__ bool assoc_block_emb(int nr, RowBox rowbox, int nc, C
         }
     };
     // pass A
-    for (int i = t; i < nr; i += nt) {
+    if (rst) {   // a disjoint pair is masked at cost 1 (prox < 1, thresh <= 1): no candidate
+        for (int q = t; q < nr * nc; q += nt) {
+            const int i = q / nc, j = q - (q / nc) * nc;
+            const Box rb = rst[i], cb = cst[j];
+            if (intersects(rb, cb)) pair(i, rb, j, cb, wst[j]);
+        }
+    }
+    for (int i = t; i < nr && !rst; i += nt) {
         const Box rb = rowbox(i);
         if (use_grid) {
             grid_query(
@@ -417,7 +450,7 @@ __device__ __forceinline__ bool assoc_block_emb(int nr, RowBox rowbox, int nc, C
             const int2 ij = pend[p];
             const RC rc = pre ? rcs[p] : RC{rowfeat(ij.x), colfeat(ij.y)};
             const auto &cf = rc.c;
-            const double cd = cosine_dist16(rc.r, cf, D);
+            const double cd = cosine_dist16<32>(rc.r, cf, D);   // D = 512: one round trip
             if ((lane_id() & 15) == 0) {
                 double emb = np_max(0.0, cd) / 2.0;                 // matching.py:164-166
                 if (emb > app) emb = 1.0;                           // bot_sort.py:318

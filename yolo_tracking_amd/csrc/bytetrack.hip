@@ -1329,6 +1329,8 @@ __global__ __launch_bounds__(PREP_T) void k_bs_prep(BtArgs a) {
     }
     const int s = blockIdx.x;
     if (stream_skipped(a, s)) return;
+    YTA_STAMP_BASE(0);
+    YTA_STAMP(0);
     Arena none(nullptr, 0);   // no staged high boxes (the embedding association does not use them)
     const S1Lists L = stage1_lists<VAR_BOTSORT>(a, s, none, sh);
     stage1_commit(a.cnt + s, L, false);
