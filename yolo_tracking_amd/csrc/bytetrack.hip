@@ -2579,6 +2579,15 @@ struct yta_bytetrack {
     double pstat[24] = {};
     // optional per-kernel timing with HIP events on the engine stream
     bool prof = false;
+    // small host-buffer updates: the frame's launches, the packing and the copies back replayed
+    // as one HIP graph, captured with the arguments below and re-captured when they change
+    // (YTA_GRAPHS=0 disables)
+    bool graphs = true;
+    hipGraph_t g_graph = nullptr;
+    hipGraphExec_t g_exec = nullptr;
+    BtArgs g_args{};
+    const void *g_ptrs[5] = {};
+    long long g_cap = -1;
     std::vector<hipEvent_t> ev;
     size_t ev_used = 0;
     // host-buffer staging copies: persistent worker threads (created on the first large copy)
@@ -3064,6 +3073,7 @@ int create_engine(int device, int n_streams, int track_capacity, int max_dets,
     e->MAXD = max_dets;
     e->split23 = n_streams <= 64;
     if (const char *v = getenv("YTA_SPLIT23")) e->split23 = atoi(v) != 0;
+    if (const char *v = getenv("YTA_GRAPHS")) e->graphs = atoi(v) != 0;
     init(e);
     hipError_t he = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
     if (he != hipSuccess) {
@@ -3152,6 +3162,52 @@ int widen_f32(const float *src, double *dst, long long n, hipStream_t st) {
     const unsigned blocks = (unsigned)std::min<long long>(4096, (pairs + 255) / 256);
     hipLaunchKernelGGL(k_widen_f32, dim3(std::max(1u, blocks)), dim3(256), 0, st, src, dst, n);
     YTA_HIP(hipGetLastError());
+    return YTA_OK;
+}
+
+// Run `work` (the stream-ordered device work of one small host-buffer frame) through the engine's
+// cached graph: replayed when the launch arguments and buffers are the ones it was captured with,
+// else captured anew.  Kernel arguments are fixed at capture, so the comparison covers every
+// pointer and scalar the launches read on the host side (BtArgs, the packing buffers, S / CAP).
+// A capture failure turns graphs off for the engine and runs `work` directly.
+template <typename Work>
+int graph_run(yta_bytetrack *e, long long worst, Work work) {
+    BtArgs cur = e->a;   // the arguments launch_pipeline will set
+    cur.det_in = e->d_det_in;
+    cur.det_off = e->d_det_off;
+    cur.out = e->out_own;
+    cur.out_counts = nullptr;
+    cur.det_feat = e->d_feat_in;
+    const void *ptrs[5] = {e->d_pack, e->h_pack, e->d_pack_off, e->h_cnt, e->out_own};
+    const bool same = e->g_exec && e->g_cap == worst && memcmp(&cur, &e->g_args, sizeof cur) == 0 &&
+                      memcmp(ptrs, e->g_ptrs, sizeof ptrs) == 0;
+    if (!same) {
+        if (e->g_exec) (void)hipGraphExecDestroy(e->g_exec);
+        if (e->g_graph) (void)hipGraphDestroy(e->g_graph);
+        e->g_exec = nullptr;
+        e->g_graph = nullptr;
+        if (hipStreamBeginCapture(e->stream, hipStreamCaptureModeThreadLocal) != hipSuccess) {
+            (void)hipGetLastError();
+            e->graphs = false;
+            return work();
+        }
+        const int r = work();
+        hipGraph_t g = nullptr;
+        const hipError_t he = hipStreamEndCapture(e->stream, &g);
+        if (r || he != hipSuccess || !g ||
+            hipGraphInstantiate(&e->g_exec, g, nullptr, nullptr, 0) != hipSuccess) {
+            if (g) (void)hipGraphDestroy(g);
+            e->g_exec = nullptr;
+            (void)hipGetLastError();
+            e->graphs = false;
+            return r ? r : work();   // not captured: run it as plain launches
+        }
+        e->g_graph = g;
+        e->g_args = e->a;
+        memcpy(e->g_ptrs, ptrs, sizeof ptrs);
+        e->g_cap = worst;
+    }
+    YTA_HIP(hipGraphLaunch(e->g_exec, e->stream));
     return YTA_OK;
 }
 
@@ -3264,15 +3320,18 @@ int update_host(yta_bytetrack *e, const double *dets, const int *det_offsets, co
                                e->stream));
         e->a.active = e->d_active;
     }
-    int rc = launch_pipeline(e, e->d_det_in, e->d_det_off, e->out_own, nullptr, e->d_feat_in);
-    e->a.active = nullptr;
-    if (rc) return rc;
     // Small engines (every stream's worst-case rows <= 1 MiB, e.g. one camera stream): rows packed
     // at device-computed offsets and copied back with the counters, one round trip per frame
     const long long worst = (long long)S * e->CAP;
-    if (worst * 64 <= SMALL_PACK_BYTES) {
+    const bool small = worst * 64 <= SMALL_PACK_BYTES;
+    int rc = YTA_OK;
+    if (small) {
         rc = ensure_pack(e, worst);
         if (rc) return rc;
+    }
+    auto device_work = [&]() -> int {   // the frame's launches (+ packing and copies back)
+        int r = launch_pipeline(e, e->d_det_in, e->d_det_off, e->out_own, nullptr, e->d_feat_in);
+        if (r || !small) return r;
         hipLaunchKernelGGL(k_out_offsets, dim3(1), dim3(64), 0, e->stream, e->a.cnt, S,
                            e->CAP, e->d_pack_off);
         hipLaunchKernelGGL(k_pack_out, dim3(S), dim3(256), 0, e->stream, e->out_own,
@@ -3282,6 +3341,16 @@ int update_host(yta_bytetrack *e, const double *dets, const int *det_offsets, co
                                e->stream));
         YTA_HIP(hipMemcpyAsync(e->h_pack, e->d_pack, sizeof(double) * 8 * worst,
                                hipMemcpyDeviceToHost, e->stream));
+        return YTA_OK;
+    };
+    if (small && e->graphs && !e->prof && !active) {
+        rc = graph_run(e, worst, device_work);
+    } else {
+        rc = device_work();
+    }
+    e->a.active = nullptr;
+    if (rc) return rc;
+    if (small) {
         YTA_HIP(host_wait(e->stream));
         if (next_id)   // the device counters have advanced: hand them back even on an error below
             for (int q = 0; q < S; ++q) next_id[q] = e->h_cnt[q].next_id;
@@ -3800,6 +3869,8 @@ int yta_bytetrack_destroy(yta_bytetrack *e) {
     if (!e) return YTA_OK;
     (void)hipSetDevice(e->device);
     if (e->stream) (void)host_wait(e->stream);
+    if (e->g_exec) (void)hipGraphExecDestroy(e->g_exec);
+    if (e->g_graph) (void)hipGraphDestroy(e->g_graph);
     release_buffers(e);
     if (e->h_dets) (void)hipHostFree(e->h_dets);
     if (e->d_det_in) (void)hipFree(e->d_det_in);
