@@ -412,12 +412,14 @@ __global__ __launch_bounds__(BLK1) void k_stage1(BtArgs a) {
     if (!stage1_body<V>(a, s, ag, sh) && threadIdx.x == 0) atomicOr(&a.cnt[s].err, ERR_EDGE_OVERFLOW);
 }
 
-template <int V>
+// SPLIT (a.split23): two blocks per stream, block 2s + r running role r; else one block per
+// stream with both stages (role -1 a constant: the one-block kernel keeps its registers).
+template <int V, bool SPLIT>
 __global__ __launch_bounds__(BLK23) void k_stage23(BtArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     __shared__ StageShared sh;
-    const int s = a.split23 ? blockIdx.x >> 1 : blockIdx.x;
-    const int role = a.split23 ? (int)(blockIdx.x & 1) : -1;
+    const int s = SPLIT ? blockIdx.x >> 1 : blockIdx.x;
+    const int role = SPLIT ? (int)(blockIdx.x & 1) : -1;
     if (stream_skipped(a, s)) return;
     YTA_STAMP_BASE(20);
     YTA_STAMP(0);
@@ -2841,8 +2843,10 @@ int mark(yta_bytetrack *e) {
 int set_lds_limits(size_t bytes) {
     const int b = (int)bytes;
     for (const void *k : {(const void *)k_stage1<VAR_BYTETRACK>, (const void *)k_stage1<VAR_BOTSORT>,
-                          (const void *)k_bs_lap, (const void *)k_stage23<VAR_BYTETRACK>,
-                          (const void *)k_stage23<VAR_BOTSORT>, (const void *)k_s1_lap})
+                          (const void *)k_bs_lap, (const void *)k_stage23<VAR_BYTETRACK, false>,
+                          (const void *)k_stage23<VAR_BOTSORT, false>,
+                          (const void *)k_stage23<VAR_BYTETRACK, true>,
+                          (const void *)k_stage23<VAR_BOTSORT, true>, (const void *)k_s1_lap})
         YTA_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, b));
     // k_s1_edges never launches with more than BT_LDSE_BYTES (its wave queues are static LDS)
     YTA_HIP(hipFuncSetAttribute((const void *)k_s1_edges, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -2894,8 +2898,12 @@ int launch_frame(yta_bytetrack *e) {
     }
     YTA_HIP(hipGetLastError());
     MARK();
-    hipLaunchKernelGGL(k_stage23<V>, dim3(a.split23 ? 2 * a.S : a.S), dim3(BLK23), a.lds_bytes23,
-                       e->stream, a);
+    if (a.split23)
+        hipLaunchKernelGGL((k_stage23<V, true>), dim3(2 * a.S), dim3(BLK23), a.lds_bytes23,
+                           e->stream, a);
+    else
+        hipLaunchKernelGGL((k_stage23<V, false>), dim3(a.S), dim3(BLK23), a.lds_bytes23,
+                           e->stream, a);
     YTA_HIP(hipGetLastError());
     MARK();
     const dim3 gt((a.CAP + APPLY_T - 1) / APPLY_T, a.S);
