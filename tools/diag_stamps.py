@@ -117,6 +117,11 @@ def main():
     show(st, 80, {1: "zero bits", 2: "births", 3: "expiry", 4: "t2/l2 lists", 5: "dedup grid",
                   6: "dedup queries", 7: "final lists", 8: "output rows", 9: "free list"},
          "k_finish")
+    if st[126] and st[85] and st[86] and st[85] <= st[126] <= st[86]:
+        print(f"  (dedup queries: tracked' boxes in {(st[126] - st[85]) / 100.0:.2f} us, the "
+              f"grid queries {(st[86] - st[126]) / 100.0:.2f} us; grid {st[127] // 1000000} "
+              f"cells, {st[127] % 1000000} big items; thread 0 visited {st[125]} candidates "
+              f"over all frames)")
     show(st, 110, {1: "reduce", 2: "zero cells", 3: "count", 5: "cell scan", 6: "scatter"},
          "grid_build (last call)")
     # per-block timeline of the last frame's block/stream kernels

@@ -1275,15 +1275,15 @@ __global__ __launch_bounds__(FEAT_T) void k_feat(BtArgs a) { feat_body(a, blockI
 // f = curr / |curr| with curr = (e/n1)/n2, smooth = 0.9 * smooth + 0.1 * f (float32), then
 // smooth /= |smooth|.
 constexpr int EMA_T = 256;
-__host__ __device__ __forceinline__ int ema_blocks(int cap) {
-    return (cap + EMA_T / WAVE - 1) / (EMA_T / WAVE);
+__host__ __device__ __forceinline__ int ema_blocks(int cap, int threads = EMA_T) {
+    return (cap + threads / WAVE - 1) / (threads / WAVE);
 }
 __device__ __forceinline__ void ema_body(const BtArgs &a, int s, int bx) {
     const int lane = lane_id();
     if (stream_skipped(a, s)) return;
     const BtCounters *c = a.cnt + s;
     const int n_pool = c->n_pool, n_items = n_pool + c->n_unc;
-    const int item = bx * (EMA_T / WAVE) + threadIdx.x / WAVE;
+    const int item = bx * (int)(blockDim.x / WAVE) + threadIdx.x / WAVE;
     if (item >= n_items) return;
     const long long tb = (long long)s * a.CAP, db = (long long)s * a.MAXD;
     const int h = a.ema_job[tb + item];
@@ -2064,8 +2064,15 @@ __device__ __forceinline__ void finish_body(const BtArgs &a, int s, unsigned *bi
                 return v;
             },
             [&](int p, const TBox &v) {
+                if (p == 0) YTA_STAMP_ABS(126);   // diagnostic: thread 0's boxes have arrived
+#ifdef YTA_STAMPS
+                if (p == 0) g_stamps[127] = gh.n_big + 1000000ull * gh.gx * gh.gy;
+#endif
                 const Box &tbx = v.b;
                 auto pair = [&](int q, const float4 &lf) {
+#ifdef YTA_STAMPS
+                    if (blockIdx.x == 0 && threadIdx.x == 0) g_stamps[125] += 1;
+#endif
                     if (!iou_may_exceed(tbx, lf, 0.85)) return;
                     const Box lb = exact_lbox(q);
                     if (!intersects(tbx, lb)) return;
@@ -2253,16 +2260,18 @@ __device__ __forceinline__ void finish_body(const BtArgs &a, int s, unsigned *bi
     }
 }
 
-template <int V>
 // four 256-thread blocks per CU: <= 128 VGPRs (the diagnostic build's stamps would add some)
-__global__ __launch_bounds__(BLKF, 4) void k_finish(BtArgs a) {
+// NT: threads per block - BLKF (four blocks per CU: many streams) or 1024 (few streams: the
+// single block of a stream then takes every pass's items one or two per thread)
+template <int V, int NT>
+__global__ __launch_bounds__(NT, NT == BLKF ? 4 : 1) void k_finish(BtArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char fsmem[];
     __shared__ FinishShared sh;
     if (V == VAR_BOTSORT && (int)blockIdx.x >= a.S) {
         // split BoT-SORT: k_ema's blocks in this grid.  Independent of the finish work: the EMA
         // rewrites the smoothed features of tracks that took a detection this frame, the finish
         // writes only births' (free slots') features and reads none
-        const int b = blockIdx.x - a.S, eb = ema_blocks(a.CAP);
+        const int b = blockIdx.x - a.S, eb = ema_blocks(a.CAP, NT);
         ema_body(a, b / eb, b % eb);
         return;
     }
@@ -2916,9 +2925,15 @@ int launch_frame(yta_bytetrack *e) {
     }
     MARK();
     const size_t bits_bytes = ((size_t)12 * ((a.CAP + 31) / 32) + 15) & ~(size_t)15;
-    static_assert(EMA_T == BLKF, "k_ema's blocks run in k_finish's grid");
-    hipLaunchKernelGGL(k_finish<V>, dim3(a.S + (bs ? a.S * ema_blocks(a.CAP) : 0)), dim3(BLKF),
-                       bits_bytes + a.lds_bytes_f, e->stream, a);
+    // few streams: 1024-thread finish blocks (k_ema's blocks in its grid take 16 tracks each)
+    if (e->split23) {
+        constexpr int FT = 1024;
+        hipLaunchKernelGGL((k_finish<V, FT>), dim3(a.S + (bs ? a.S * ema_blocks(a.CAP, FT) : 0)),
+                           dim3(FT), bits_bytes + a.lds_bytes_f, e->stream, a);
+    } else {
+        hipLaunchKernelGGL((k_finish<V, BLKF>), dim3(a.S + (bs ? a.S * ema_blocks(a.CAP, BLKF) : 0)),
+                           dim3(BLKF), bits_bytes + a.lds_bytes_f, e->stream, a);
+    }
     YTA_HIP(hipGetLastError());
     MARK();
     return YTA_OK;
