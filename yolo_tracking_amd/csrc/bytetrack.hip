@@ -1234,13 +1234,13 @@ __device__ __forceinline__ float f32_norm(double sumsq) { return sqrtf((float)su
 // in-place normalisations the reference applies to its row: n1 = |e|, n2 = |e/n1| (STrack
 // construction, :40-48) and n3 = |(e/n1)/n2| (when a track takes it, :40-41).
 constexpr int FEAT_T = 256;
-__host__ __device__ __forceinline__ int feat_blocks(int maxd) {
-    return (maxd + FEAT_T / WAVE - 1) / (FEAT_T / WAVE);
+__host__ __device__ __forceinline__ int feat_blocks(int maxd, int threads = FEAT_T) {
+    return (maxd + threads / WAVE - 1) / (threads / WAVE);
 }
 __device__ __forceinline__ void feat_body(const BtArgs &a, int s, int bx) {
     const int lane = lane_id();
     if (stream_skipped(a, s)) return;
-    const int d = bx * (FEAT_T / WAVE) + threadIdx.x / WAVE;
+    const int d = bx * (int)(blockDim.x / WAVE) + threadIdx.x / WAVE;
     const int nd = min(a.det_off[s + 1] - a.det_off[s], a.MAXD);
     if (d >= nd) return;
     const long long row = (long long)a.det_off[s] + d;
@@ -1322,10 +1322,11 @@ __global__ __launch_bounds__(EMA_T) void k_ema(BtArgs a) { ema_body(a, blockIdx.
 // Same results as k_stage1 on every stream.
 constexpr int BSE_T = 256;   // k_bs_edges threads: 4 waves = 4 pool rows per block
 
-__global__ __launch_bounds__(PREP_T) void k_bs_prep(BtArgs a) {
+constexpr int BS_PREP_T = 1024;   // k_bs_prep (few streams: one block per stream takes the lists)
+__global__ __launch_bounds__(BS_PREP_T) void k_bs_prep(BtArgs a) {
     __shared__ StageShared sh;
     if ((int)blockIdx.x >= a.S) {   // k_feat's blocks, launched with this grid (independent work)
-        const int b = blockIdx.x - a.S, fb = feat_blocks(a.MAXD);
+        const int b = blockIdx.x - a.S, fb = feat_blocks(a.MAXD, BS_PREP_T);
         feat_body(a, b / fb, b % fb);
         return;
     }
@@ -2889,9 +2890,8 @@ int launch_frame(yta_bytetrack *e) {
         MARK();
         hipLaunchKernelGGL(k_s1_lap, dim3(a.S), dim3(BLKL), a.lds_bytes_l, e->stream, a);
     } else if (bs) {   // split stage 1 (k_bs_*): few streams
-        static_assert(FEAT_T == PREP_T, "k_feat's blocks run in k_bs_prep's grid");
-        hipLaunchKernelGGL(k_bs_prep, dim3(a.S + a.S * feat_blocks(a.MAXD)), dim3(PREP_T), 0,
-                           e->stream, a);
+        hipLaunchKernelGGL(k_bs_prep, dim3(a.S + a.S * feat_blocks(a.MAXD, BS_PREP_T)),
+                           dim3(BS_PREP_T), 0, e->stream, a);
         YTA_HIP(hipGetLastError());
         MARK();
         const dim3 ge((a.CAP + BSE_T / WAVE - 1) / (BSE_T / WAVE), a.S);
