@@ -311,8 +311,8 @@ __device__ __forceinline__ bool stage23_body(const BtArgs &a, int s, Arena &ar, 
     const int n_act = c->n_act;
     LapSlab slab = slab_of(a, s);
     if (role == 1) {
-        slab.i += (long long)(BLK23 / WAVE) * slab.i_stride;
-        slab.d += (long long)(BLK23 / WAVE) * slab.d_stride;
+        slab.i += (long long)(nt / WAVE) * slab.i_stride;
+        slab.d += (long long)(nt / WAVE) * slab.d_stride;
     }
     int n_left = 0, n_ref = 0, n_rest = 0;
     bool ok = true;
@@ -414,8 +414,11 @@ __global__ __launch_bounds__(BLK1) void k_stage1(BtArgs a) {
 
 // SPLIT (a.split23): two blocks per stream, block 2s + r running role r; else one block per
 // stream with both stages (role -1 a constant: the one-block kernel keeps its registers).
+// The split blocks take BLK23S threads (few streams: the chip is idle but for them).
+constexpr int BLK23S = 512;
+static_assert(2 * BLK23S / WAVE <= SLAB_WAVES, "k_stage23's two blocks take disjoint slabs");
 template <int V, bool SPLIT>
-__global__ __launch_bounds__(BLK23) void k_stage23(BtArgs a) {
+__global__ __launch_bounds__(SPLIT ? BLK23S : BLK23) void k_stage23(BtArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     __shared__ StageShared sh;
     const int s = SPLIT ? blockIdx.x >> 1 : blockIdx.x;
@@ -2908,7 +2911,7 @@ int launch_frame(yta_bytetrack *e) {
     YTA_HIP(hipGetLastError());
     MARK();
     if (a.split23)
-        hipLaunchKernelGGL((k_stage23<V, true>), dim3(2 * a.S), dim3(BLK23), a.lds_bytes23,
+        hipLaunchKernelGGL((k_stage23<V, true>), dim3(2 * a.S), dim3(BLK23S), a.lds_bytes23,
                            e->stream, a);
     else
         hipLaunchKernelGGL((k_stage23<V, false>), dim3(a.S), dim3(BLK23), a.lds_bytes23,
