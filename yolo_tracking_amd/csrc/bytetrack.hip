@@ -592,7 +592,9 @@ __global__ __launch_bounds__(PREP_T) void k_pool_build(BtArgs a) {
     s1_pool_build(a, s, sh);
 }
 
-__global__ __launch_bounds__(PREP_T) void k_s1_prep(BtArgs a) {
+// NT: PREP_T, or 1024 with few streams (split23: one block per stream takes the lists)
+template <int NT>
+__global__ __launch_bounds__(NT) void k_s1_prep(BtArgs a) {
     __shared__ PrepShared sh;
     const int s = blockIdx.x, t = threadIdx.x;
     if (stream_skipped(a, s)) return;
@@ -2885,7 +2887,10 @@ int launch_frame(yta_bytetrack *e) {
         YTA_HIP(hipGetLastError());
     }
     if (V == VAR_BYTETRACK && a.match_thresh <= 1.0) {   // grid-exact candidates (assoc.hpp)
-        hipLaunchKernelGGL(k_s1_prep, dim3(a.S), dim3(PREP_T), 0, e->stream, a);
+        if (e->split23)
+            hipLaunchKernelGGL(k_s1_prep<1024>, dim3(a.S), dim3(1024), 0, e->stream, a);
+        else
+            hipLaunchKernelGGL(k_s1_prep<PREP_T>, dim3(a.S), dim3(PREP_T), 0, e->stream, a);
         YTA_HIP(hipGetLastError());
         MARK();
         hipLaunchKernelGGL(k_s1_edges, dim3(a.S), dim3(BLKE), a.lds_bytes_e, e->stream, a);
