@@ -933,13 +933,15 @@ __device__ __forceinline__ void s1_single_edges(const BtArgs &a, int s, int nc, 
     }
 }
 
-// two 512-thread blocks per CU: <= 128 VGPRs (the diagnostic build's stamps would add some)
-__global__ __launch_bounds__(BLKE, 4) void k_s1_edges(BtArgs a) {
+// two 512-thread blocks per CU: <= 128 VGPRs (the diagnostic build's stamps would add some);
+// NT 1024 with few streams (split23)
+template <int NT>
+__global__ __launch_bounds__(NT, NT == BLKE ? 4 : 1) void k_s1_edges(BtArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     __shared__ GridScratch gs;
     __shared__ int wsum[32];
     __shared__ int spill, n_edges;
-    __shared__ EdgeWaveQ ewq[BLKE / WAVE];
+    __shared__ EdgeWaveQ ewq[NT / WAVE];
     const int s = blockIdx.x, t = threadIdx.x, nt = blockDim.x;
     if (stream_skipped(a, s)) return;
     YTA_STAMP_BASE(66);
@@ -1207,8 +1209,10 @@ __device__ __forceinline__ bool s1_lap_body(const BtArgs &a, int s, Arena &ar, L
     return true;
 }
 
-// four 256-thread blocks per CU: <= 128 VGPRs (4 waves per SIMD) and a <= 36 KiB arena
-__global__ __launch_bounds__(BLKL, 4) void k_s1_lap(BtArgs a) {
+// four 256-thread blocks per CU: <= 128 VGPRs (4 waves per SIMD) and a <= 36 KiB arena; NT 1024
+// with few streams (split23)
+template <int NT>
+__global__ __launch_bounds__(NT, NT == BLKL ? 4 : 1) void k_s1_lap(BtArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     __shared__ LapShared lsh;
     const int s = blockIdx.x;
@@ -2861,11 +2865,13 @@ int set_lds_limits(size_t bytes) {
                           (const void *)k_bs_lap, (const void *)k_stage23<VAR_BYTETRACK, false>,
                           (const void *)k_stage23<VAR_BOTSORT, false>,
                           (const void *)k_stage23<VAR_BYTETRACK, true>,
-                          (const void *)k_stage23<VAR_BOTSORT, true>, (const void *)k_s1_lap})
+                          (const void *)k_stage23<VAR_BOTSORT, true>, (const void *)k_s1_lap<BLKL>,
+                          (const void *)k_s1_lap<1024>})
         YTA_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, b));
     // k_s1_edges never launches with more than BT_LDSE_BYTES (its wave queues are static LDS)
-    YTA_HIP(hipFuncSetAttribute((const void *)k_s1_edges, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)std::min(bytes, BT_LDSE_BYTES)));
+    for (const void *k : {(const void *)k_s1_edges<BLKE>, (const void *)k_s1_edges<1024>})
+        YTA_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)std::min(bytes, BT_LDSE_BYTES)));
     return YTA_OK;
 }
 
@@ -2893,10 +2899,16 @@ int launch_frame(yta_bytetrack *e) {
             hipLaunchKernelGGL(k_s1_prep<PREP_T>, dim3(a.S), dim3(PREP_T), 0, e->stream, a);
         YTA_HIP(hipGetLastError());
         MARK();
-        hipLaunchKernelGGL(k_s1_edges, dim3(a.S), dim3(BLKE), a.lds_bytes_e, e->stream, a);
+        if (e->split23)
+            hipLaunchKernelGGL(k_s1_edges<1024>, dim3(a.S), dim3(1024), a.lds_bytes_e, e->stream, a);
+        else
+            hipLaunchKernelGGL(k_s1_edges<BLKE>, dim3(a.S), dim3(BLKE), a.lds_bytes_e, e->stream, a);
         YTA_HIP(hipGetLastError());
         MARK();
-        hipLaunchKernelGGL(k_s1_lap, dim3(a.S), dim3(BLKL), a.lds_bytes_l, e->stream, a);
+        if (e->split23)
+            hipLaunchKernelGGL(k_s1_lap<1024>, dim3(a.S), dim3(1024), a.lds_bytes_l, e->stream, a);
+        else
+            hipLaunchKernelGGL(k_s1_lap<BLKL>, dim3(a.S), dim3(BLKL), a.lds_bytes_l, e->stream, a);
     } else if (bs) {   // split stage 1 (k_bs_*): few streams
         hipLaunchKernelGGL(k_bs_prep, dim3(a.S + a.S * feat_blocks(a.MAXD, BS_PREP_T)),
                            dim3(BS_PREP_T), 0, e->stream, a);
