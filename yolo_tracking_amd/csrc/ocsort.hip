@@ -171,7 +171,10 @@ __device__ void tracker_update(OcTrack &r, const double *det, int det_local, int
     kf7_correct(r.kf, z);
 }
 
-__global__ __launch_bounds__(OC_T) void k_oc_pre(OcArgs a) {
+// NT: OC_T, or 1024 with few streams (one block per stream takes the lists; only sh.wsum is
+// shared state sized per wave)
+template <int NT>
+__global__ __launch_bounds__(NT) void k_oc_pre(OcArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     __shared__ OcShared sh;
     const int s = blockIdx.x, t = threadIdx.x, nt = blockDim.x;
@@ -784,7 +787,10 @@ int oc_launch(yta_ocsort *e, const double *d_dets, const int *d_off, const int *
         const int mrc = e->mask.stage(a.S, e->stream, &a.active);
         if (mrc) return mrc;
     }
-    hipLaunchKernelGGL(k_oc_pre, dim3(a.S), dim3(OC_T), 0, e->stream, a);
+    if (a.S <= 64)
+        hipLaunchKernelGGL(k_oc_pre<1024>, dim3(a.S), dim3(1024), 0, e->stream, a);
+    else
+        hipLaunchKernelGGL(k_oc_pre<OC_T>, dim3(a.S), dim3(OC_T), 0, e->stream, a);
     YTA_HIP(hipGetLastError());
     const long long per = ((long long)a.MAXD * a.CAP + OC_T - 1) / OC_T;
     const long long cap = std::max<long long>(4, 4096 / a.S);
