@@ -59,43 +59,65 @@ def algorithmic_bytes(n, m):
     return 4 * 576 * n + 56 * m + 16 * n * m + 64 * n
 
 
-def kernel_bytes(phase, st):
-    """Algorithmic HBM bytes one launch of `phase` must move, from the last frame's counts summed
-    over streams.  Kalman record = 24 f64 (192 B), track meta = 48 B, box = 32 B,
-    detection row = 48 B, candidate edge = 12 B (int column + f64 cost)."""
+def kernel_bytes(phase, st, slots=0):
+    """Algorithmic HBM bytes one launch of `phase` must move: every array element the kernel has
+    to read or write once, from the last frame's counts summed over the launch's streams
+    (csrc/bytetrack.hip).  Kalman state = 24 f64 (192 B), track meta = 48 B,
+    box = 32 B, detection row = 48 B (6 f64), list entry / index = 4 B, candidate edge = 12 B (int
+    column + f64 cost).  slots: S * track capacity of the launch (k_finish rewrites the free list).
+    Line granularity (a 32-B box read moves a 128-B line) and whole-line record writes are not
+    algorithmic: they show as counter bytes above these (`pmc_over_alg` > 1)."""
     pool, unc, high, dets = st["pool"], st["unc"], st["high"], st["dets"]
-    act, lazy = st["act"], st["lazy"]
-    lost_list = pool - act
-    matched = st["tracked"]            # tracks updated this frame (upper bound: tracked list)
+    act, lazy, second, left, rest = st["act"], st["lazy"], st["second"], st["left"], st["rest"]
+    births, t2, l2, out = st["births"], st["t2"], st["l2"], st["out"]
+    tracked, lost = st["tracked"], st["lost"]
+    lost_pool = pool - act              # the pool's tail: the previous frame's lost list
+    refound = max(lost_pool - lazy, 0)  # lost tracks matched in stage 1
+    updated = max(t2 - births, 0)       # tracks that took a detection (tracked' minus births)
     if phase == "s1_prep":
-        # dets read, measurement / conf / cls written; high and low lists with boxes (+ score);
-        # tracked list, flags and Kalman mean of every pool / unconfirmed track (+ the lazy frame
-        # of lost ones), pool / unconfirmed lists with boxes written
-        return (dets * (48 + 48) + high * (4 + 32 + 8) + st["second"] * (4 + 32)
-                + (act + unc) * (4 + 4 + 64 + 4 + 32) + lost_list * (4 + 4 + 4 + 64 + 4 + 32))
+        # detection rows read; high list (index, box, score) and low list (index, box) written
+        # (the pool itself is built by the previous frame's k_finish, DESIGN.md §12.7)
+        return dets * 48 + high * (4 + 32 + 8) + second * (4 + 32)
     if phase == "s1_edges":
-        # high boxes + scores read once (grid built in LDS), every pool box read, edge count and
-        # edges written, single-edge matches: x1 of every pool row, y1 of every high detection
+        # high boxes + scores read once (grid built in LDS), y1 written per high detection; every
+        # pool box read, edge count and single-edge result x1 written per row; edge slots written
         return high * (32 + 8 + 4) + pool * (32 + 4 + 4) + st["edges1"] * 12
     if phase == "s1_lap":
-        # edge counts and the edges left after the single-edge components read, the solver's
-        # matches written
+        # every pool row's edge count; the residual rows' edges (after the single-edge
+        # components) read; their matches written (x1 / y1, at most one per residual edge)
         return pool * 4 + st["res1"] * (12 + 8)
-    if phase == "apply":
-        # every pool / unconfirmed track but the lazily predicted lost ones: Kalman record + meta
-        # read, record written; matched tracks: meta written, the detection's row read; every
-        # pool item: index + stage results read, stage-1 kind written
-        touched = pool - lazy + unc
-        return touched * (192 + 48 + 192) + matched * (48 + 48) + pool * (4 + 4 + 4 + 4) + unc * 8
     if phase == "stage23":
-        return (pool * (4 + 48 + 4) + high * (4 + 8 + 8) + st["left"] * (8 + 32 + 4)
-                + st["second"] * (32 + 4) + unc * (32 + 4) + st["rest"] * (4 + 32 + 8 + 4))
+        # left_of_pool reset, stage-1 results of the pool head (leftovers) and tail (re-found:
+        # slot + result read, pair written), y1 of the high detections (rest), rest entries with
+        # scores; stage 2: leftover boxes x low boxes, x2 / y2; stage 3: unconfirmed boxes x rest
+        # boxes + scores, x3 / y3
+        return (pool * 4 + act * 4 + lost_pool * 8 + refound * 8 + high * 4
+                + left * (4 + 32 + 4) + second * (32 + 4)
+                + rest * (4 + 8 + 8) + unc * (32 + 4) + rest * (4 + 32 + 8 + 4))
+    if phase == "apply":
+        # every pool / unconfirmed item: slot + stage results; every track but the lazily
+        # predicted lost ones: flags, Kalman state + meta read, Kalman state written; tracks that
+        # took a detection: meta written, the detection's row + its list index read
+        touched = pool - lazy + unc
+        return (pool * 12 + unc * 8 + touched * (4 + 192 + 48 + 192) + updated * (48 + 48 + 4))
     if phase == "finish":
-        # lost list expiry (slot, flags, lost frame); tracked' boxes (mean), lost' means (lazily
-        # predicted) for duplicate removal, list entries; output rows: mean + meta read, row
-        # written; births: record + meta written
-        return (lost_list * 12 + st["t2"] * (32 + 12) + st["l2"] * (64 + 4 + 12)
-                + st["out"] * (32 + 48 + 64) + st["births"] * (192 + 48))
+        # births: rest entries (result, score, index, high index); per birth: free slot, detection
+        # row, Kalman state + meta + flags written.  tracked' = previous tracked list (slot, flags)
+        # ++ births ++ re-found; lost' = previous lost list (slot, flags, lost frame) ++ leftovers
+        # (result, position, slot, flags); duplicate removal: lost' pool boxes, tracked' boxes;
+        # final lists (tracked' flags, tracked / lost / unconfirmed written); output rows: mean +
+        # meta read, row written, and the next frame's pool: head boxes, unconfirmed boxes, the
+        # lost tail (mean, flags, lost frame) predicted; the free list rewritten
+        free = max(slots - tracked - lost, 0)
+        return (rest * (4 + 8 + 4 + 4) + births * (4 + 4 + 48 + 192 + 48 + 4)
+                + (act + st["unc"]) * 8 + t2 * 4 + births * 4 + refound * 8
+                + lost_pool * 12 + left * 16 + l2 * 8
+                + l2 * (4 + 32) + t2 * (4 + 32)
+                + t2 * (4 + 4) + tracked * 4 + l2 * 4 + lost * 4
+                + out * (4 + 64 + 48) + out * (64 + 4 + 32)
+                + (tracked - out) * (4 + 32 + 4 + 32)
+                + lost * (4 + 64 + 4 + 4) + lost * (4 + 32)
+                + free * 4)
     return 0
 
 
@@ -163,8 +185,18 @@ def parse(argv=None):
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--preroll", type=int, default=35,
                    help="untimed frames before the warmup (steady state: > max_time_lost = 30)")
-    p.add_argument("--streams", type=int, default=2048, help="streams per GPU")
-    p.add_argument("--n", type=int, default=1024, help="tracks = detections per frame")
+    p.add_argument("--streams", type=int, default=None,
+                   help="streams per GPU (default: bytetrack 2048; the other trackers their "
+                        "config's per-GPU share, CONFIG_SHARE)")
+    p.add_argument("--n", type=int, default=None,
+                   help="tracks = detections per frame (default: bytetrack 1024; the other "
+                        "trackers their config's size)")
+    p.add_argument("--tracker", default="bytetrack",
+                   choices=["bytetrack", "ocsort", "botsort", "deepocsort", "hybridsort"],
+                   help="bytetrack: the headline (BASELINE.json metric); the others run their "
+                        "BASELINE config (C2-C5) as the measured workload, streams sharded s mod "
+                        "G over the ranks (tools/bench_tracker.py engines)")
+    p.add_argument("--dim", type=int, default=512, help="embedding width (ReID trackers)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-pcie", action="store_true", help="skip the host-buffer (PCIe) leg")
     p.add_argument("--pcie-engines", type=int, default=1,
@@ -185,7 +217,28 @@ def parse(argv=None):
                         "measurement: the ranks share the card)")
     p.add_argument("--dry-cpu", action="store_true",
                    help="harness rehearsal: CPU ranks over gloo, NumPy stand-in step, no GPU")
-    return p.parse_args(argv)
+    a = p.parse_args(argv)
+    if a.tracker == "bytetrack":
+        a.streams = 2048 if a.streams is None else a.streams
+        a.n = 1024 if a.n is None else a.n
+    else:
+        a.streams = CONFIG_SHARE[a.tracker][1] if a.streams is None else a.streams
+        a.n = CONFIG_SHARE[a.tracker][0] if a.n is None else a.n
+    return a
+
+
+# BASELINE.json configs of the other trackers: (tracks = dets, streams per GPU).  C4 = 8 DeepOCSORT
+# streams over 8 GPUs (1 per GPU), C5 = 64 HybridSORT streams over 8 GPUs (8 per GPU); C2 / C3
+# are single-GPU configs (1 stream).  With --gpus G every GPU runs this share (weak scaling), so
+# G = 8 is the config as BASELINE states it.
+CONFIG_SHARE = {"ocsort": (256, 1), "botsort": (1024, 1), "deepocsort": (2048, 1),
+                "hybridsort": (4096, 8)}
+
+
+def config_seeds(seed, rank, world, streams):
+    """Stream s of the job -> rank s mod G (examples/val.py:147-226 hands sequences to devices in
+    turn); rank r's k-th stream is global stream r + k G, seeded seed + r + k G."""
+    return [seed + rank + world * k for k in range(streams)]
 
 
 # ---------------------------------------------------------------- rank launcher (--gpus N)
@@ -415,14 +468,20 @@ def pcie_inclusive(frame_of, S, N, device, first, frames=8, engines=1, pinned=Fa
                     f"{E} engine(s) on as many host threads); median step"}
 
 
-def pcie_pipelined(frame_of, S, N, device, first, frames=8, pinned=False, f32=False, cap_mult=3):
+def pcie_pipelined(frame_of, S, N, device, first, frames=8, pinned=False, f32=False, cap_mult=3,
+                   check=None, offsets_of=None):
     """The host-buffer path pipelined (yta_bytetrack_submit / _collect, one engine): frame f's
     detections go host -> device while frame f-1's kernels run and frame f-2's rows come back (up
     to three frames in flight), so both PCIe directions and the kernels overlap.  Every timed frame's packed dets sit in their
     own caller buffer before the timed region (page-locked: written there by the detector, DMA'd
     directly; pageable: staged by the library during submit); output rows land in three
     rotating caller buffers (page-locked: DMA'd directly).  value = frames / wall time of the
-    timed submit/collect loop.  Never `value` of the bench line."""
+    timed submit/collect loop.  Never `value` of the bench line.
+
+    Parity hooks (tests/test_gpu_pipelined_bench_shape.py runs this very function):
+    offsets_of(f) -> the S + 1 detection offsets of frame f (default: N rows per stream);
+    check(f, rows, out_off) is called after each collect with frame f's packed output rows (a view
+    of the caller buffer) and offsets, and check(None, next_ids, pipe_stats) once at the end."""
     import torch
 
     from yolo_tracking_amd import ByteTrackEngine, _lib
@@ -434,29 +493,40 @@ def pcie_pipelined(frame_of, S, N, device, first, frames=8, pinned=False, f32=Fa
         if not pinned:
             return np.empty(shape, dtype=dt)
         return pinned_empty(shape, dt)
-    offs = np.ascontiguousarray(np.arange(S + 1, dtype=np.int32) * N)
+    uniform = np.ascontiguousarray(np.arange(S + 1, dtype=np.int32) * N)
+    offs_all = [uniform if offsets_of is None else
+                np.ascontiguousarray(offsets_of(f), dtype=np.int32) for f in range(first + frames)]
+    rows_max = max(int(o[-1]) for o in offs_all)
     in_dt = np.float32 if f32 else np.float64
     submit_fn = lib.yta_bytetrack_submit_f32 if f32 else lib.yta_bytetrack_submit
     # frames in flight (csrc/bytetrack.hip PIPE_DEPTH; YTA_PIPE_DEPTH names a -DYTA_PIPE_DEPTH
     # variant library's depth for A/B runs)
     DEPTH = int(os.environ.get("YTA_PIPE_DEPTH", "3"))
-    outs = [buf((S * N, 8)) for _ in range(DEPTH)]
+    outs = [buf((rows_max, 8)) for _ in range(DEPTH)]
     out_off = np.zeros(S + 1, np.int32)
-    stage = buf((S * N, 6), in_dt)
+    stage = buf((rows_max, 6), in_dt)
+    inflight = []
 
     def submit(src, f):
-        _lib.check(submit_fn(h, src.ctypes.data, offs.ctypes.data, None,
-                             outs[f % DEPTH].ctypes.data, S * N))
+        o = offs_all[f]
+        _lib.check(submit_fn(h, src.ctypes.data, o.ctypes.data, None,
+                             outs[f % DEPTH].ctypes.data, rows_max))
+        inflight.append(f)
 
     def collect():
         _lib.check(lib.yta_bytetrack_collect(h, None, out_off.ctypes.data))
+        f = inflight.pop(0)
+        if check is not None:
+            check(f, outs[f % DEPTH][:out_off[-1]], out_off.copy())
     for f in range(first):   # untimed: steady state
-        stage[:] = frame_of(f)
+        n = int(offs_all[f][-1])
+        stage[:n] = frame_of(f)
         submit(stage, f)
         collect()
     timed = []
     for f in range(first, first + frames):
-        b = buf((S * N, 6), in_dt)
+        n = int(offs_all[f][-1])
+        b = buf((n, 6), in_dt)
         b[:] = frame_of(f)
         timed.append(b)
     _lib.check(lib.yta_bytetrack_pipe_stats(h, None, 0, 1))   # accounting from here
@@ -472,6 +542,10 @@ def pcie_pipelined(frame_of, S, N, device, first, frames=8, pinned=False, f32=Fa
     _lib.check(lib.yta_bytetrack_pipe_stats(h, ps, len(PIPE_STATS), 1))
     nfr = max(ps[0], 1.0)
     acct = {k: (ps[i] / nfr if i else ps[i]) for i, k in enumerate(PIPE_STATS)}
+    if check is not None:
+        nid = np.zeros(S, np.int64)
+        _lib.check(lib.yta_bytetrack_next_ids(h, nid.ctypes.data))
+        check(None, nid, {k: ps[i] for i, k in enumerate(PIPE_STATS)})
     eng.close()
     return {"value": S / dt, "unit": "calls/s", "steps": frames, "ms_per_step": 1000 * dt,
             "per_frame": {k: round(v, 4) for k, v in acct.items()},
@@ -519,14 +593,15 @@ CONFIGS = [
 ]
 
 
-def configs_leg():
+def configs_leg(names=None):
     """Configs C2-C5 on this GPU (tools/bench_tracker.py: inputs staged in HBM, the engines'
     device-buffer entry points, timed frames between device syncs), each with its 1-core oracle
     (started together beside the GPU legs, collected after).  C5 runs its per-GPU share of the
-    64-stream config: 8 streams in two engines."""
+    64-stream config: 8 streams in two engines.  names: a subset (N > 1 ranks: C2 / C3, the
+    single-GPU configs; C4 / C5 then run on every rank, MULTI_CONFIGS)."""
     sys.path.insert(0, os.path.join(REPO, "tools"))
     import bench_tracker as bt
-    todo = [(name, bt.parse(argv)) for name, argv in CONFIGS]
+    todo = [(name, bt.parse(argv)) for name, argv in CONFIGS if names is None or name in names]
     cpus = {name: bt.start_cpu_leg(a) for name, a in todo}
     res = {}
     for name, a in todo:
@@ -549,26 +624,33 @@ def configs_leg():
 def run_dry(args, world, rank):
     """--dry-cpu: the multi-rank harness end to end on CPU ranks (gloo): stream sharding, frame
     staging, barrier-bracketed timed region, max over ranks, rank-0 JSON line.  The step is a
-    NumPy stand-in over the staged frames (no GPU, no tracker)."""
+    NumPy stand-in over the staged frames (no GPU, no tracker).  With --tracker other than
+    bytetrack: that config's streams (embeddings for the ReID trackers), sharded s mod G."""
     dist = None
     if world > 1:
         import torch.distributed as dist
         dist.init_process_group("gloo")
     S, N = args.streams, args.n
-    seeds = stream_seeds(args.seed, rank, S)
-    F = args.preroll + args.warmup + args.steps
-    frames = [gen_stream_frames(N, F, sd) for sd in seeds]
+    cfg = args.tracker != "bytetrack"
+    seeds = config_seeds(args.seed, rank, world, S) if cfg else stream_seeds(args.seed, rank, S)
+    F = (0 if cfg else args.preroll) + args.warmup + args.steps
+    if cfg and args.tracker != "ocsort":
+        from yolo_tracking_amd.synth import make_frames
+        frames = [make_frames(N, F, sd, emb_dim=args.dim) for sd in seeds]
+    else:
+        frames = [[(d, None) for d in gen_stream_frames(N, F, sd)] for sd in seeds]
     acc = np.zeros(S)
 
     def step(f):
         for s in range(S):
-            acc[s] += frames[s][f][:, 4].sum()
+            d, e = frames[s][f]
+            acc[s] += d[:, 4].sum() + (float(e[:, 0].sum()) if e is not None else 0.0)
 
-    for f in range(args.preroll + args.warmup):
+    for f in range(F - args.steps):
         step(f)
 
     def run_steps():
-        for f in range(args.preroll + args.warmup, F):
+        for f in range(F - args.steps, F):
             step(f)
 
     elapsed = timed_region(run_steps, lambda: None, dist)
@@ -581,10 +663,70 @@ def run_dry(args, world, rank):
         print(json.dumps({"metric": "dry-run harness", "value": aggregate_rate(world, S, args.steps,
                                                                               elapsed),
                           "unit": "calls/s", "n_gpus": world, "steps": args.steps,
-                          "warmup": args.warmup, "dry_run": True, "stream_seeds_by_rank": every,
+                          "warmup": args.warmup, "dry_run": True, "tracker": args.tracker,
+                          "tracks": N, "streams_per_gpu": S, "stream_seeds_by_rank": every,
                           "checksum": float(acc.sum())}))
     if dist:
         dist.destroy_process_group()
+
+
+def config_shard_leg(tracker, n, dim, streams, steps, warmup, seed, world, rank, dist, device,
+                     cpu=False):
+    """One BASELINE config on every rank at once (tools/bench_tracker.py's engines, inputs staged in
+    HBM): rank r runs `streams` streams, global streams r, r + G, ... (s mod G); the timed region
+    is bracketed by the ranks' barrier, the job's time is the slowest rank's, value = all ranks'
+    update calls / that time.  cpu: the 1-core oracle beside it (rank 0, N = 1 only)."""
+    sys.path.insert(0, os.path.join(REPO, "tools"))
+    import bench_tracker as bt
+    argv = ["--tracker", tracker, "--n", str(n), "--streams", str(streams), "--steps", str(steps),
+            "--warmup", str(warmup), "--seed", str(seed)]
+    if tracker != "ocsort":
+        argv += ["--dim", str(dim)]
+    a = bt.parse(argv)
+    seeds = config_seeds(seed, rank, world, streams)
+    cpu_proc = bt.start_cpu_leg(a) if cpu and rank == 0 else (None, 0)
+    line = bt.run(a, cpu=cpu_proc, seeds=seeds, barrier=(dist.barrier if dist else None))
+    el = max_over_ranks(line["elapsed_s"], dist, device)
+    every = [seeds]
+    if dist:
+        every = [None] * world
+        dist.all_gather_object(every, seeds)
+    return {"metric": f"{tracker} tracker.update() calls/sec @ {n} tracks x {n} dets",
+            "value": aggregate_rate(world, streams, steps, el), "unit": "calls/s",
+            "n_gpus": world, "streams_per_gpu": streams, "streams_total": world * streams,
+            "steps": steps, "warmup": warmup, "ms_per_step": 1000.0 * el / steps,
+            "scaling": "weak", "sharding": "stream s -> rank s mod G",
+            "stream_seeds_by_rank": every, "workload": line["config"]["workload"],
+            "queues_per_gpu": line["config"].get("queues"),
+            "cpu_baseline": line.get("cpu_baseline") if cpu else None,
+            "frame_counts_rank0": line.get("frame_counts")}
+
+
+def run_config(args, world, rank, local_rank):
+    """--tracker other than bytetrack: that BASELINE config is the measured workload (C4: one
+    DeepOCSORT stream of 2048 x 2048 + CMC per GPU, C5: eight HybridSORT streams of 4096 x 4096 per
+    GPU; 8 GPUs = the config as stated), one JSON line on rank 0."""
+    import torch
+    torch.cuda.set_device(local_rank)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    line = config_shard_leg(args.tracker, args.n, args.dim, args.streams, args.steps, args.warmup,
+                            args.seed, world, rank, dist, "cuda",
+                            cpu=world == 1 and not args.no_cpu_baseline)
+    if rank == 0:
+        line.update(higher_is_better=True, vs_baseline=None, dtype="f64", data="synthetic",
+                    config={"workload": line.pop("workload"), "tracker": args.tracker,
+                            "tracks": args.n, "dets": args.n, "streams_per_gpu": args.streams,
+                            "parallelism": f"stream-sharded x{world}"})
+        print(json.dumps(line))
+    if dist:
+        dist.destroy_process_group()
+
+
+# C4 / C5 in the default (headline) run with N > 1 ranks: every rank runs its share at once
+MULTI_CONFIGS = [("C4", "deepocsort", 2048, 1, 20, 5), ("C5", "hybridsort", 4096, 8, 8, 3)]
 
 
 def main():
@@ -599,6 +741,8 @@ def main():
               file=sys.stderr)
     if args.dry_cpu:
         return run_dry(args, world, rank)
+    if args.tracker != "bytetrack":
+        return run_config(args, world, rank, local_rank)
     import torch
     if args.shared_gpu:
         local_rank = local_rank % max(1, torch.cuda.device_count())
@@ -699,39 +843,59 @@ def main():
         rss = [None] * world
         dist.all_gather_object(rss, peak_rss_mb())
     ms_per_step = 1000.0 * elapsed / args.steps
+    # N > 1: C4 / C5 with every rank running its share at once (weak scaling: 8 ranks = the
+    # configs as BASELINE.json states them); one failing rank would leave the others at a barrier,
+    # so a failure is reported, not raised, and the legs run only while every rank is healthy
+    multi_cfg = None
+    if world > 1 and not args.no_configs:
+        multi_cfg = {}
+        for name, tr, n, sp, stp, wu in MULTI_CONFIGS:
+            try:
+                multi_cfg[name] = config_shard_leg(tr, n, 512, sp, stp, wu, 2000, world, rank, dist,
+                                                   "cpu" if args.shared_gpu else "cuda")
+            except Exception as exc:   # report, never fail the bench on a config leg
+                multi_cfg[name] = {"value": None, "error": repr(exc)[:300]}
 
     st_launch = {k: v // Q for k, v in st.items()}   # one engine's launch (Q equal slices)
     if rank == 0:
         traffic, step_traffic, traffic_tag = pmc_traffic(S, N, Q)
-        # Roofline kernel: the longest launch of a frame with the chip to itself (the isolated
-        # leg: engine 0 alone, HIP events on its stream; with Q = 1 the timed region is that
-        # already).  The overlapped launches of the timed region (two engines interleaving on the
-        # chip) are reported beside it: their events include the other engine's share.
+        # Roofline kernel: the launch with the largest share of the timed step (engine 0's HIP
+        # events in the timed region).  Its achieved rate comes from the isolated leg (engine 0
+        # alone after the timed region, HIP events on its stream; with Q = 1 the timed region is
+        # that already): in the timed region the two engines' launches interleave on the chip and
+        # an event duration includes the other engine's share.  k_apply, the HBM-heaviest launch,
+        # is reported beside it.
         ref_ms, ref_st = (iso_ms, st_iso) if iso_ms else (phase_ms, st_launch)
-        dom = max(ref_ms, key=lambda p: ref_ms[p])
+        slots_launch = (S // Q) * cap
+        dom = max(phase_ms, key=lambda p: phase_ms[p])
         dom_ms = ref_ms[dom]
-        b = kernel_bytes(dom, ref_st)
+        b = kernel_bytes(dom, ref_st, slots_launch)
         achieved = b / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
 
         def kline(p, t_ms, stc):
-            alg = kernel_bytes(p, stc)
+            alg = kernel_bytes(p, stc, slots_launch)
             k = traffic.get(PHASE_KERNEL[p], {})
             hbm = k.get("hbm_bytes_per_launch")
-            return {"ms": t_ms, "alg_bytes": alg,
-                    "gbs": alg / (t_ms * 1e-3) / 1e9 if t_ms > 0 else 0.0,
-                    "frac": alg / (t_ms * 1e-3) / 1e9 / HBM_PEAK_GBS if t_ms > 0 else 0.0,
+            gbs = alg / (t_ms * 1e-3) / 1e9 if t_ms > 0 else 0.0
+            line = {"ms": t_ms, "alg_bytes": alg, "gbs": gbs,
+                    "frac": gbs / HBM_PEAK_GBS,
                     "pmc_bytes": hbm,
                     "pmc_over_alg": (hbm / alg) if hbm and alg else None,
                     "rocprof_avg_us": k.get("avg_us_isolated" if ref_ms is iso_ms
                                             else "avg_us_timed")}
+            if line["frac"] > 1.0:   # never a fraction above the peak: operands from on-die cache
+                line.update(frac=None, bound="cache",
+                            note="algorithmic bytes over the launch exceed the HBM peak: reads "
+                                 "served from L2 / MALL")
+            return line
         per_kernel = {p: kline(p, ref_ms[p], ref_st) for p in PHASES}
         overlapped = {p: {"ms": phase_ms[p],
-                          "gbs": (kernel_bytes(p, st_launch) / (phase_ms[p] * 1e-3) / 1e9
-                                  if phase_ms[p] > 0 else 0.0)} for p in PHASES}
+                          "gbs": (kernel_bytes(p, st_launch, slots_launch) / (phase_ms[p] * 1e-3)
+                                  / 1e9 if phase_ms[p] > 0 else 0.0)} for p in PHASES}
         # implemented minimum: what this build's six launches must move per update (the
         # per-kernel figures above, summed, over the streams); SURVEY §8(d)'s canonical figure
         # charges a dense N x M cost matrix and a 576-B Kalman state, neither of which exists here
-        impl_bytes = sum(kernel_bytes(p, st) for p in PHASES) / S
+        impl_bytes = sum(kernel_bytes(p, st, S * cap) for p in PHASES) / S
         pcie = (None if args.no_pcie else
                 pcie_inclusive(frame_of, S, N, local_rank, first=min(PRE, FT - 8),
                                engines=args.pcie_engines))
@@ -749,7 +913,9 @@ def main():
                 pcie["pipelined"]["pinned_f32"] = pcie_pipelined(
                     frame_of, S, N, local_rank, first=min(PRE, FT - 8), pinned=True, f32=True)
         dropin = None if args.no_dropin else dropin_leg(N, 60, args.seed, f"cuda:{local_rank}")
-        configs = None if args.no_configs else configs_leg()
+        configs = None if args.no_configs else configs_leg(None if world == 1 else ["C2", "C3"])
+        if multi_cfg:
+            configs = dict(configs or {}, **multi_cfg)
         cpu = None if args.no_cpu_baseline else cpu_baseline(N, args.cpu_frames, args.seed)
         if dropin is not None and cpu and cpu.get("value"):
             dropin["vs_cpu_1core"] = dropin["value"] / cpu["value"]
@@ -794,7 +960,10 @@ def main():
                          "beside": {p: dict(per_kernel[p], timed_ms=phase_ms[p],
                                             timed_share=(phase_ms[p] / ms_per_step
                                                          if ms_per_step > 0 else None))
-                                    for p in ("s1_edges", "finish") if p != dom},
+                                    for p in ("apply", "s1_edges", "finish") if p != dom},
+                         "selection": "the launch with the largest timed share (engine 0's HIP "
+                                      "events in the timed window); its achieved rate from the "
+                                      "isolated leg",
                          "timed_share": {p: (phase_ms[p] / ms_per_step if ms_per_step > 0
                                              else None) for p in PHASES},
                          "timed_share_note": "each kernel's average launch in the timed region "
@@ -803,7 +972,8 @@ def main():
                                              "ms_per_step",
                          "overlapped": (None if Q == 1 else {
                              "avg_launch_ms": phase_ms[dom],
-                             "frac": (kernel_bytes(dom, st_launch) / (phase_ms[dom] * 1e-3) / 1e9
+                             "frac": (kernel_bytes(dom, st_launch, slots_launch)
+                                      / (phase_ms[dom] * 1e-3) / 1e9
                                       / HBM_PEAK_GBS if phase_ms[dom] > 0 else None),
                              "note": f"{Q} engines of {S // Q} streams on {Q} HIP streams in the "
                                      "timed region: each launch overlaps the other engines' "
@@ -816,6 +986,11 @@ def main():
             "per_kernel_overlapped": overlapped,
             "frame_counts": st,
             "busiest_kernel": dom,
+            "kernel_bytes_note": "per_kernel.alg_bytes: bench.kernel_bytes (every array element a "
+                                 "launch must read or write once, from the frame's counts); "
+                                 "pmc_bytes: rocprofv3 counters of the same kernel "
+                                 "(profiles/roofline_traffic.json); the ratio above 1 is line "
+                                 "granularity and whole-line writes",
             "algorithmic_bytes_per_update": impl_bytes,
             "algorithmic_bytes_note": "implemented minimum (sum of the six launches' algorithmic "
                                       "bytes / streams); SURVEY §8(d)'s canonical figure "

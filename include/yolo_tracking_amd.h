@@ -261,6 +261,13 @@ int yta_bytetrack_profile_collect(yta_bytetrack *engine, double *ms, int *frames
  * cumulative number of stream-frames whose duplicate-removal grid (k_finish) did not fit in LDS
  * (21 int64). */
 int yta_bytetrack_stats(yta_bytetrack *engine, long long *stats);
+/* Introspection of the engine's launch modes (writes min(n, YTA_BT_MODES) int64): the few-stream
+ * mode chosen at create (YTA_SPLIT23), the mode the kernel arguments carry (stage 2 / 3 in two
+ * blocks per stream), its second arena allocated, cached HIP graphs enabled (YTA_GRAPHS), BoT-SORT
+ * split stage 1 (YTA_BS_SPLIT), graph captures and graph replays so far, track capacity, max
+ * detections.  The first three agree for the engine's whole life, reserve() included. */
+#define YTA_BT_MODES 9
+int yta_bytetrack_modes(yta_bytetrack *engine, long long *out, int n);
 /* Tuning / testing: bytes of LDS the association kernels may use per stream (default 150 KiB,
  * at most 150 KiB); a stream-frame that does not fit runs over global memory.  0 forces the
  * global-memory path for every stream. */
@@ -380,7 +387,10 @@ int yta_ocsort_stats(yta_ocsort *engine, long long *stats);
  * those of them whose optimum was not certified unique (exact ties: lapjv replayed instead),
  * lapjv replays in any round (the single-wavefront restatement of lapx's tie-breaking), and -IoU
  * rounds (BYTE / OCR) solved on the rows and columns that have a positive entry. */
-int yta_ocsort_lap_stats(yta_ocsort *engine, long long *stats);
+#define YTA_LAP_STATS 4
+/* n: the length of stats; min(n, YTA_LAP_STATS) values are written (round 6: the n argument is
+ * new - round 5 wrote 4 values with no length, round 4 three). */
+int yta_ocsort_lap_stats(yta_ocsort *engine, long long *stats, int n);
 int yta_ocsort_hip_stream(yta_ocsort *engine, void **stream);
 /* OCSORT Kalman KAT: n tracks initialised from z0 (n x 4, [u, v, s, r]) run `steps` steps of
  * predict + update(z[step] (n x 4 per step); a NaN first value = update(None)), freeze /
@@ -457,7 +467,7 @@ int yta_deepocsort_stats(yta_deepocsort *engine, long long *stats);
  * those of them whose optimum was not certified unique (exact ties: lapjv replayed instead),
  * lapjv replays in any round (the single-wavefront restatement of lapx's tie-breaking), and -IoU
  * rounds (BYTE / OCR) solved on the rows and columns that have a positive entry. */
-int yta_deepocsort_lap_stats(yta_deepocsort *engine, long long *stats);   /* 4 int64 */
+int yta_deepocsort_lap_stats(yta_deepocsort *engine, long long *stats, int n);
 int yta_deepocsort_hip_stream(yta_deepocsort *engine, void **stream);
 /* DeepOCSORT Kalman KAT (deep_ocsort.py:103-136, 198-293 new-KF branch): n tracks initialised
  * from boxes b0 (n x 4, x1 y1 x2 y2) run `steps` steps of [affine (warps: steps x n x 6, NULL =
@@ -530,7 +540,7 @@ int yta_hybridsort_stats(yta_hybridsort *engine, long long *stats);
  * those of them whose optimum was not certified unique (exact ties: lapjv replayed instead),
  * lapjv replays in any round (the single-wavefront restatement of lapx's tie-breaking), and -IoU
  * rounds (BYTE / OCR) solved on the rows and columns that have a positive entry. */
-int yta_hybridsort_lap_stats(yta_hybridsort *engine, long long *stats);   /* 4 int64 */
+int yta_hybridsort_lap_stats(yta_hybridsort *engine, long long *stats, int n);
 int yta_hybridsort_hip_stream(yta_hybridsort *engine, void **stream);
 /* HybridSORT Kalman KAT (hybridsort.py:112-320): n tracks initialised from rows b0 (n x 5:
  * x1 y1 x2 y2 score) run `steps` steps of predict (velocity clamp) + update(b[step] (n x 5); a

@@ -77,3 +77,45 @@ def test_bench_launches_n_ranks_dry_cpu():
     seeds = d["stream_seeds_by_rank"]
     assert seeds == [[1000, 1001, 1002], [1003, 1004, 1005]]
     assert d["value"] > 0
+
+
+@pytest.mark.parametrize("tracker,streams", [("deepocsort", 1), ("hybridsort", 3)])
+def test_bench_config_dry_cpu_two_ranks(tracker, streams):
+    """`bench.py --gpus 2 --dry-cpu --tracker deepocsort|hybridsort`: the C4 / C5 harness (their
+    streams with embeddings, sharded s mod G: rank r takes global streams r, r + G, ...), two
+    rank processes over gloo, rank 0's single JSON line with the aggregate."""
+    import json
+    import subprocess
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--dry-cpu",
+                        "--tracker", tracker, "--streams", str(streams), "--n", "24", "--dim", "16",
+                        "--steps", "3", "--warmup", "1", "--seed", "2000"], env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["tracker"] == tracker and d["streams_per_gpu"] == streams
+    seeds = d["stream_seeds_by_rank"]
+    assert seeds == [[2000 + 2 * k for k in range(streams)], [2001 + 2 * k for k in range(streams)]]
+    assert d["value"] > 0
+
+
+def test_config_seeds_shard_mod_g():
+    """C5's 64 streams over 8 ranks: rank r holds global streams r, r + 8, ... (8 each), every
+    stream exactly once."""
+    G, per = 8, 8
+    every = [bench.config_seeds(0, r, G, per) for r in range(G)]
+    flat = sorted(x for r in every for x in r)
+    assert flat == list(range(G * per))
+    assert all(all(x % G == r for x in every[r]) for r in range(G))
+
+
+def test_bench_defaults_per_tracker():
+    a = bench.parse([])
+    assert (a.tracker, a.n, a.streams) == ("bytetrack", 1024, 2048)
+    a = bench.parse(["--tracker", "deepocsort"])
+    assert (a.n, a.streams) == (2048, 1)     # C4: 8 streams over 8 GPUs
+    a = bench.parse(["--tracker", "hybridsort"])
+    assert (a.n, a.streams) == (4096, 8)     # C5: 64 streams over 8 GPUs

@@ -216,3 +216,45 @@ def test_deepocsort_dense_embedding_fallback_matches_oracle():
             d, e = streams[s][f]
             exp = np.asarray(ors[s].update(d, shape, e), dtype=np.float64).reshape(-1, 8)
             assert np.array_equal(got[s], exp), (s, f)
+
+
+def test_deepocsort_dense_and_listed_paths_agree(monkeypatch):
+    """The same frames through an engine forced onto the dense embedding tiles and AW scans for
+    every frame (YTA_DOC_DENSE=1: k_doc_emb's f64 MFMA tiles, k_doc_aw) and through the default
+    engine, where only the crowded stream takes them (the other lists its pairs: k_doc_emb_pairs,
+    k_doc_aw_cols).  The two sum each dot product in a different order (MFMA tiles vs 16-lane
+    groups), so an embedding cost may differ in its last bits (<= 1e-15 relative); that can only
+    matter on an exact tie or a threshold hit exactly.  Bar: rows, ID counters and every tracker's
+    state (ids, counters, x, P, embedding) bit-identical between the two engines on these streams,
+    and the oracle agrees with both."""
+    S, n, nf, D = 2, 96, 12, 32
+    kw = dict(det_thresh=0.0, max_age=30, min_hits=1, iou_threshold=0.3, delta_t=3,
+              asso_func="giou", inertia=0.2)
+    raw = [make_frames(n, nf, 740 + s, emb_dim=D, low_conf_frac=0.0, drop_frac=0.1)
+           for s in range(S)]
+    streams = [[(d, (e / np.linalg.norm(e, axis=1, keepdims=True)).astype(np.float32))
+                for d, e in r] for r in raw]
+    streams[0] = _crowd(streams[0], 4.0)
+    monkeypatch.setenv("YTA_DOC_DENSE", "1")
+    dense = DeepOCSortEngine(S, feat_dim=D, **kw, track_capacity=256, max_dets=128)
+    monkeypatch.delenv("YTA_DOC_DENSE")
+    listed = DeepOCSortEngine(S, feat_dim=D, **kw, track_capacity=256, max_dets=128)
+    ors = [DeepOCSortOracle(**kw) for _ in range(S)]
+    shape = (640, 640, 3)
+    nd = np.zeros(S, np.int64)
+    nl = np.zeros(S, np.int64)
+    for f in range(nf):
+        args = ([streams[s][f][0] for s in range(S)], [streams[s][f][1] for s in range(S)])
+        gd = dense.update(*args, img_shapes=[shape] * S, next_id=nd)
+        gl = listed.update(*args, img_shapes=[shape] * S, next_id=nl)
+        assert np.array_equal(nd, nl), f
+        for s in range(S):
+            assert np.array_equal(gd[s].view(np.int64), gl[s].view(np.int64)), (s, f)
+            d, e = streams[s][f]
+            exp = np.asarray(ors[s].update(d, shape, e), dtype=np.float64).reshape(-1, 8)
+            assert np.array_equal(gl[s], exp), (s, f)
+    for s in range(S):
+        a, b = dense.state(s), listed.state(s)
+        for k in a:
+            if a[k] is not None:
+                assert np.array_equal(np.asarray(a[k]), np.asarray(b[k])), (s, k)

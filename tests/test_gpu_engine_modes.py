@@ -1,0 +1,134 @@
+"""GPU: the ByteTrack engine's launch modes and teardown.
+
+* Capacity growth mid-run (reserve(): every buffer reallocated, the state copied over, the next
+  stage-1 pool rebuilt) on engines created under every combination of YTA_GRAPHS (cached HIP graph
+  of a small host-buffer frame, re-captured when an argument changes) and YTA_SPLIT23 (stage 2 and
+  stage 3 in two blocks per stream, the 1024-thread stage-1 / finish blocks): rows and ID counters
+  bit-identical across the four engines and equal to the oracle (byte_tracker.py:132-281), and
+  the mode the kernel arguments carry (with its second arena) still the one chosen at create after
+  the growth (yta_bytetrack_modes).  Round 5's reserve() dropped the split mode on growth.
+* Destroying an engine with pipelined frames submitted and not collected: the copy streams are
+  drained before their buffers are freed; a new engine of the same sizes then runs exactly as a
+  fresh one.
+"""
+import ctypes
+import itertools
+
+import numpy as np
+import pytest
+
+from oracle.bytetrack import ByteTrackOracle
+from yolo_tracking_amd import ByteTrackEngine, _lib
+from yolo_tracking_amd.synth import make_frames
+
+pytestmark = pytest.mark.gpu
+
+KW = dict(track_thresh=0.5, match_thresh=0.8, track_buffer=30, frame_rate=30)
+MODES = ["split23", "args_split23", "ws3", "graphs", "bs_split", "captures", "replays", "cap",
+         "maxd"]
+
+
+def modes(eng):
+    buf = (ctypes.c_longlong * len(MODES))()
+    _lib.check(eng.lib.yta_bytetrack_modes(eng.handle, buf, len(MODES)))
+    return {k: int(buf[i]) for i, k in enumerate(MODES)}
+
+
+def _growing_streams(S, F, grow_at):
+    """S streams of 120 objects; before frame grow_at only the first 10 objects are detected, so
+    the engine (capacity 32, 32 detections) has to grow mid-run."""
+    out = []
+    for s in range(S):
+        fr = [d for d, _ in make_frames(120, F, seed=910 + s)]
+        out.append([d[:10] if f < grow_at else d for f, d in enumerate(fr)])
+    return out
+
+
+def test_growth_under_every_launch_mode(monkeypatch):
+    S, F, G = 3, 36, 12
+    frames = _growing_streams(S, F, G)
+    ors = [ByteTrackOracle(**KW) for _ in range(S)]
+    exp = [[ors[s].update(frames[s][f]).reshape(-1, 8) for f in range(F)] for s in range(S)]
+    results = {}
+    for graphs, split in itertools.product([0, 1], [0, 1]):
+        monkeypatch.setenv("YTA_GRAPHS", str(graphs))
+        monkeypatch.setenv("YTA_SPLIT23", str(split))
+        eng = ByteTrackEngine(S, track_capacity=32, max_dets=32, **KW)
+        m0 = modes(eng)
+        assert (m0["split23"], m0["args_split23"], m0["ws3"]) == (split,) * 3, m0
+        assert m0["graphs"] == graphs and (m0["cap"], m0["maxd"]) == (32, 32), m0
+        nid = np.zeros(S, np.int64)
+        got, caps = [], []
+        for f in range(F):
+            got.append(eng.update([frames[s][f] for s in range(S)], next_id=nid))
+            caps.append(modes(eng)["cap"])
+        assert caps[0] == 32 and caps[G - 1] < caps[-1], caps   # grew mid-run
+        m1 = modes(eng)
+        assert m1["cap"] > 32 and m1["maxd"] >= 120, m1
+        # the kernel arguments still carry the mode chosen at create, with its second arena
+        assert (m1["split23"], m1["args_split23"], m1["ws3"]) == (split,) * 3, m1
+        if graphs:   # captured at least before and after the growth, then replayed
+            assert m1["captures"] >= 2 and m1["replays"] >= F, m1
+        else:
+            assert m1["captures"] == 0 and m1["replays"] == 0, m1
+        results[(graphs, split)] = (got, nid.copy())
+        eng.close()
+    base_rows, base_nid = results[(1, 1)]
+    for key, (rows, nid) in results.items():
+        assert np.array_equal(nid, base_nid), key
+        for f in range(F):
+            for s in range(S):
+                assert np.array_equal(rows[f][s].view(np.int64),
+                                      base_rows[f][s].view(np.int64)), (key, f, s)
+    for f in range(F):
+        for s in range(S):
+            g, e = base_rows[f][s], exp[s][f]
+            assert g.shape == e.shape, (f, s)
+            assert np.array_equal(g[:, 4:], e[:, 4:]), (f, s)
+            np.testing.assert_allclose(g[:, :4], e[:, :4], rtol=1e-9, atol=1e-9)
+
+
+def test_reserve_keeps_modes(monkeypatch):
+    """yta_bytetrack_reserve (the explicit growth entry point) keeps the create-time modes too."""
+    for split in (0, 1):
+        monkeypatch.setenv("YTA_SPLIT23", str(split))
+        eng = ByteTrackEngine(2, track_capacity=16, max_dets=16, **KW)
+        eng.reserve(64, 48)
+        m = modes(eng)
+        assert (m["split23"], m["args_split23"], m["ws3"]) == (split,) * 3, m
+        assert (m["cap"], m["maxd"]) == (64, 48), m
+        eng.close()
+
+
+@pytest.mark.parametrize("pinned", [False, True])
+def test_destroy_with_frames_in_flight(pinned):
+    import torch
+    S, N, F = 4, 200, 6
+    frames = [[d for d, _ in make_frames(N, F, seed=1300 + s)] for s in range(S)]
+
+    def pbuf(shape):
+        if not pinned:
+            return np.empty(shape)
+        return torch.empty(shape, dtype=torch.float64, pin_memory=True).numpy()
+    for rounds in range(3):
+        eng = ByteTrackEngine(S, track_capacity=512, max_dets=N, **KW)
+        ins = [pbuf((S * N, 6)) for _ in range(2)]
+        outs = [pbuf((S * N, 8)) for _ in range(2)]
+        for f in range(2):
+            ins[f][:] = np.concatenate([frames[s][f] for s in range(S)])
+            off = np.arange(S + 1, dtype=np.int32) * N
+            _lib.check(eng.lib.yta_bytetrack_submit(eng.handle, ins[f].ctypes.data,
+                                                    off.ctypes.data, None, outs[f].ctypes.data,
+                                                    S * N))
+        eng.close()    # two frames submitted, none collected
+        del ins, outs
+        # an engine of the same sizes right after: same results as a fresh reference engine
+        new = ByteTrackEngine(S, track_capacity=512, max_dets=N, **KW)
+        ref = ByteTrackEngine(S, track_capacity=512, max_dets=N, **KW)
+        for f in range(F):
+            a = new.update([frames[s][f] for s in range(S)])
+            b = ref.update([frames[s][f] for s in range(S)])
+            for s in range(S):
+                assert np.array_equal(a[s].view(np.int64), b[s].view(np.int64)), (rounds, f, s)
+        new.close()
+        ref.close()

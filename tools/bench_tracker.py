@@ -164,9 +164,13 @@ def finish_cpu_leg(args, proc, cf, timeout=900):
             if "frames" in res else {"value": None, "sample": res.get("error")})
 
 
-def run(args, cpu=None):
+def run(args, cpu=None, seeds=None, barrier=None):
     """One config on the GPU -> its JSON line.  cpu: a (process, frames) pair from start_cpu_leg
-    to collect for the line's cpu_baseline (None: run the CPU leg here, after the GPU legs)."""
+    to collect for the line's cpu_baseline (None: run the CPU leg here, after the GPU legs;
+    (None, 0): no CPU leg).  seeds: the streams' generator seeds (default seed + s; bench.py's
+    multi-GPU legs pass stream s's global seed, streams sharded s mod G over the ranks).
+    barrier: called on both sides of the timed region after the device syncs (bench.py: the
+    ranks' barrier, so the slowest rank's elapsed time is the job's)."""
     import torch
     from yolo_tracking_amd import _lib
     from yolo_tracking_amd.synth import SyntheticStream, make_frames
@@ -181,7 +185,10 @@ def run(args, cpu=None):
     kw_stream = dict(low_conf_frac=0.0) if oc else dict(emb_dim=D)
     if fam:
         kw_stream["low_conf_frac"] = 0.0
-    streams = [make_frames(N, F, args.seed + s, **kw_stream) for s in range(S)]
+    if seeds is None:
+        seeds = [args.seed + s for s in range(S)]
+    assert len(seeds) == S
+    streams = [make_frames(N, F, seeds[s], **kw_stream) for s in range(S)]
     dets = np.stack([np.concatenate([streams[s][f][0] for s in range(S)]) for f in range(F)])
     off = np.array([[sum(len(streams[q][f][0]) for q in range(s)) for s in range(S + 1)]
                     for f in range(F)], dtype=np.int32)
@@ -299,11 +306,16 @@ def run(args, cpu=None):
     stamps = os.environ.get("YTA_HS_STAMPS") and args.tracker == "hybridsort"
     if stamps:   # diagnostic library: k_hs_lap's solver phases over the timed frames
         eng.lib.yta_hs_debug_stamps_reset()
+    if barrier is not None:
+        barrier()
+        torch.cuda.synchronize()
     t0 = time.perf_counter()
     for f in range(args.warmup, F):
         step(f)
     _lib.check(sync(eng.handle))
     torch.cuda.synchronize()
+    if barrier is not None:
+        barrier()
     el = time.perf_counter() - t0
     value = S * args.steps / el
     if stamps:
@@ -343,7 +355,8 @@ def run(args, cpu=None):
             "config": {"workload": f"{args.tracker} {N}x{N}" + (f" D={D}" if D else "")
                                    + f", {S} streams, inputs resident in HBM",
                        "streams": S, "queues": max(1, args.queues) if fam else 1},
-            "cpu_baseline": cpu, "frame_counts": stats}
+            "cpu_baseline": cpu, "frame_counts": stats, "elapsed_s": el,
+            "stream_seeds": list(seeds)}
     return line
 
 

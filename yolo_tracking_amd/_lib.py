@@ -131,6 +131,7 @@ _SIGS = {
     "yta_bytetrack_profile": ([_P, _I], _I),
     "yta_bytetrack_profile_collect": ([_P, _P, _P], _I),
     "yta_bytetrack_stats": ([_P, _P], _I),
+    "yta_bytetrack_modes": ([_P, _P, _I], _I),
     "yta_bytetrack_hip_stream": ([_P, _P], _I),
     "yta_bytetrack_set_lds": ([_P, _I], _I),
     "yta_selftest": ([_I], _I),
@@ -151,7 +152,7 @@ _SIGS = {
     "yta_ocsort_sync": ([_P], _I),
     "yta_ocsort_get_state": ([_P, _I, _P, _P, _P, _P], _I),
     "yta_ocsort_stats": ([_P, _P], _I),
-    "yta_ocsort_lap_stats": ([_P, _P], _I),
+    "yta_ocsort_lap_stats": ([_P, _P, _I], _I),
     "yta_ocsort_hip_stream": ([_P, _P], _I),
     "yta_kf7_run": ([_I, _I, _I, _P, _P, _P, _P], _I),
     "yta_deepocsort_create": ([_I, _I, _I, _I, _I, _P, _P], _I),
@@ -166,7 +167,7 @@ _SIGS = {
     "yta_deepocsort_sync": ([_P], _I),
     "yta_deepocsort_get_state": ([_P, _I, _P, _P, _P, _P, _P], _I),
     "yta_deepocsort_stats": ([_P, _P], _I),
-    "yta_deepocsort_lap_stats": ([_P, _P], _I),
+    "yta_deepocsort_lap_stats": ([_P, _P, _I], _I),
     "yta_deepocsort_hip_stream": ([_P, _P], _I),
     "yta_kf8_run": ([_I, _I, _I, _P, _P, _P, _P, _P], _I),
     "yta_hybridsort_create": ([_I, _I, _I, _I, _I, _P, _P], _I),
@@ -182,7 +183,7 @@ _SIGS = {
     "yta_hybridsort_get_state": ([_P, _I, _P, _P, _P, _P, _P, _P], _I),
     "yta_hybridsort_classes": ([_P, _I, _P, _I, _P], _I),
     "yta_hybridsort_stats": ([_P, _P], _I),
-    "yta_hybridsort_lap_stats": ([_P, _P], _I),
+    "yta_hybridsort_lap_stats": ([_P, _P, _I], _I),
     "yta_hybridsort_hip_stream": ([_P, _P], _I),
     "yta_kf9_run": ([_I, _I, _I, _P, _P, _P, _P], _I),
     "yta_gsi_interpolate": ([_I, _P, _I, _I, _I, _I, _P, ctypes.c_longlong, _P], _I),

@@ -2609,6 +2609,7 @@ struct yta_bytetrack {
     BtArgs g_args{};
     const void *g_ptrs[5] = {};
     long long g_cap = -1;
+    long long g_captures = 0, g_replays = 0;   // yta_bytetrack_modes
     std::vector<hipEvent_t> ev;
     size_t ev_used = 0;
     // host-buffer staging copies: persistent worker threads (created on the first large copy)
@@ -2997,6 +2998,10 @@ int reserve(yta_bytetrack *e, int cap, int maxd) {
     n->D = e->D;
     n->bprm = e->bprm;
     n->stream = e->stream;
+    // every create-time mode bt_alloc reads (the split stage 2 / 3 blocks and their ws3 arena)
+    n->split23 = e->split23;
+    n->bs_split = e->bs_split;
+    n->graphs = e->graphs;
     int rc = bt_alloc(n);
     const size_t S = e->S, oc = e->CAP, nc = cap;
     auto copy2d = [&](void *dst, size_t dpitch, const void *src, size_t spitch, size_t width,
@@ -3249,7 +3254,9 @@ int graph_run(yta_bytetrack *e, long long worst, Work work) {
         e->g_args = e->a;
         memcpy(e->g_ptrs, ptrs, sizeof ptrs);
         e->g_cap = worst;
+        ++e->g_captures;
     }
+    ++e->g_replays;
     YTA_HIP(hipGraphLaunch(e->g_exec, e->stream));
     return YTA_OK;
 }
@@ -3912,6 +3919,13 @@ int yta_bytetrack_destroy(yta_bytetrack *e) {
     if (!e) return YTA_OK;
     (void)hipSetDevice(e->device);
     if (e->stream) (void)host_wait(e->stream);
+    // pipelined frames submitted and not collected: their copy-in (slot / shared s_in) and
+    // copy-out (s_out, k_rows_to_host into the caller's or the slot's mapped memory) may still be
+    // running; drain every copy stream before any buffer they touch is freed
+    for (auto &p : e->pipe)
+        if (p.s_in) (void)hipStreamSynchronize(p.s_in);
+    for (hipStream_t st : {e->s_in, e->s_out})
+        if (st) (void)hipStreamSynchronize(st);
     if (e->g_exec) (void)hipGraphExecDestroy(e->g_exec);
     if (e->g_graph) (void)hipGraphDestroy(e->g_graph);
     release_buffers(e);
@@ -4162,6 +4176,15 @@ int yta_bytetrack_stats(yta_bytetrack *e, long long *stats) {
                                  c.n_fallback[1], c.n_lazy, c.n_res1, c.n_fallback_f};
         for (int k = 0; k < NS; ++k) stats[k] += v[k];
     }
+    return YTA_OK;
+}
+
+int yta_bytetrack_modes(yta_bytetrack *e, long long *out, int n) {
+    YTA_CHECK(e && (out || n <= 0), YTA_ERR_INVALID, "null argument");
+    const long long v[YTA_BT_MODES] = {e->split23,          e->a.split23,   e->a.ws3 != nullptr,
+                                       e->graphs,           e->bs_split,    e->g_captures,
+                                       e->g_replays,        e->CAP,         e->MAXD};
+    for (int k = 0; k < n && k < YTA_BT_MODES; ++k) out[k] = v[k];
     return YTA_OK;
 }
 

@@ -113,6 +113,8 @@ struct DocArgs {
     int *pos_cnt;                  // embedding term is used; [S*MAXD] their count
     double *col_e;                 // [S*CAP*POS_K] per tracker: its listed pairs' embedding terms
     int *col_cnt;                  // [S*CAP] their count
+    int force_dense;               // YTA_DOC_DENSE=1: every frame on the dense tiles / AW scans
+                                   // (tests/test_gpu_deepocsort.py compares both paths)
 };
 
 __device__ __forceinline__ long long doc_mb(const DocArgs &a, int s) {
@@ -397,7 +399,7 @@ __global__ __launch_bounds__(OC_T) void k_doc_pre(DocArgs a) {
         c->n_trk = n_trk;
         c->n_high = n_hi;
         c->n_dets = nd;
-        c->n_pos = 0;
+        c->n_pos = a.force_dense ? 1 : 0;
         c->col_ovf = 0;
     }
 }
@@ -1291,6 +1293,7 @@ int doc_alloc(yta_deepocsort *e) {
     a.lap_ws_stride = oc_lap_ws_stride(n);
     a.arr_chip = MAXD >= ARR_CHIP_MIN_DETS;
     if (const char *v = getenv("YTA_ARR_CHIP")) a.arr_chip = atoi(v);
+    if (const char *v = getenv("YTA_DOC_DENSE")) a.force_dense = atoi(v) != 0;
     DOCALLOC(a.lap_ws, S * a.lap_ws_stride);
     a.lap_csr = nullptr;
     a.lap_csr_stride = n >= LAPB_MIN_N && lap_sparse_on() ? (lap_csr_bytes(n) + 255) & ~255LL : 0;
@@ -1807,18 +1810,19 @@ int yta_kf8_run(int device, int n, int steps, const double *b0, const double *b,
     return YTA_OK;
 }
 
-int yta_deepocsort_lap_stats(yta_deepocsort *e, long long *stats) {
-    YTA_CHECK(e && stats, YTA_ERR_INVALID, "null argument");
+int yta_deepocsort_lap_stats(yta_deepocsort *e, long long *stats, int n) {
+    YTA_CHECK(e && (stats || n <= 0), YTA_ERR_INVALID, "null argument");
     const int rc = doc_read_counters(e);
     if (rc) return rc;
-    for (int k = 0; k < 4; ++k) stats[k] = 0;
+    long long v[YTA_LAP_STATS] = {};
     for (int s = 0; s < e->S; ++s) {
         const LapStats &l = e->h_cnt[s].ls;
-        stats[0] += l.transposed;
-        stats[1] += l.uncertified;
-        stats[2] += l.replays;
-        stats[3] += l.reduced;
+        v[0] += l.transposed;
+        v[1] += l.uncertified;
+        v[2] += l.replays;
+        v[3] += l.reduced;
     }
+    for (int k = 0; k < n && k < YTA_LAP_STATS; ++k) stats[k] = v[k];
     return YTA_OK;
 }
 

@@ -1675,18 +1675,19 @@ int yta_kf9_run(int device, int n, int steps, const double *b0, const double *b,
     return YTA_OK;
 }
 
-int yta_hybridsort_lap_stats(yta_hybridsort *e, long long *stats) {
-    YTA_CHECK(e && stats, YTA_ERR_INVALID, "null argument");
+int yta_hybridsort_lap_stats(yta_hybridsort *e, long long *stats, int n) {
+    YTA_CHECK(e && (stats || n <= 0), YTA_ERR_INVALID, "null argument");
     const int rc = hs_read_counters(e);
     if (rc) return rc;
-    for (int k = 0; k < 4; ++k) stats[k] = 0;
+    long long v[YTA_LAP_STATS] = {};
     for (int s = 0; s < e->S; ++s) {
         const LapStats &l = e->h_cnt[s].ls;
-        stats[0] += l.transposed;
-        stats[1] += l.uncertified;
-        stats[2] += l.replays;
-        stats[3] += l.reduced;
+        v[0] += l.transposed;
+        v[1] += l.uncertified;
+        v[2] += l.replays;
+        v[3] += l.reduced;
     }
+    for (int k = 0; k < n && k < YTA_LAP_STATS; ++k) stats[k] = v[k];
     return YTA_OK;
 }
 

@@ -89,7 +89,7 @@ class DeepOCSortEngine(StreamSubset):
         lapjv replays, -IoU rounds solved on their positive part."""
         names = ["transposed", "uncertified", "replays", "reduced"]
         buf = (ctypes.c_longlong * len(names))()
-        _lib.check(self.lib.yta_deepocsort_lap_stats(self._h, buf))
+        _lib.check(self.lib.yta_deepocsort_lap_stats(self._h, buf, len(names)))
         return {k: int(buf[i]) for i, k in enumerate(names)}
 
     def stats(self):

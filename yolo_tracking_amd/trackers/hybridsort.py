@@ -88,7 +88,7 @@ class HybridSortEngine(StreamSubset):
         lapjv replays, -IoU rounds solved on their positive part."""
         names = ["transposed", "uncertified", "replays", "reduced"]
         buf = (ctypes.c_longlong * len(names))()
-        _lib.check(self.lib.yta_hybridsort_lap_stats(self._h, buf))
+        _lib.check(self.lib.yta_hybridsort_lap_stats(self._h, buf, len(names)))
         return {k: int(buf[i]) for i, k in enumerate(names)}
 
     def stats(self):
