@@ -263,9 +263,11 @@ int yta_bytetrack_profile_collect(yta_bytetrack *engine, double *ms, int *frames
 int yta_bytetrack_stats(yta_bytetrack *engine, long long *stats);
 /* Introspection of the engine's launch modes (writes min(n, YTA_BT_MODES) int64): the few-stream
  * mode chosen at create (YTA_SPLIT23), the mode the kernel arguments carry (stage 2 / 3 in two
- * blocks per stream), its second arena allocated, cached HIP graphs enabled (YTA_GRAPHS), BoT-SORT
+ * blocks per stream), the fallback arenas pooled, cached HIP graphs enabled (YTA_GRAPHS), BoT-SORT
  * split stage 1 (YTA_BS_SPLIT), graph captures and graph replays so far, track capacity, max
- * detections.  The first three agree for the engine's whole life, reserve() included. */
+ * detections.  The third is the number of pooled global fallback arenas (a stream-frame whose
+ * association does not fit in LDS claims one): two per stream in the split mode up to a bound of 32
+ * (YTA_WS_POOL).  The first two agree for the engine's whole life, reserve() included. */
 #define YTA_BT_MODES 9
 int yta_bytetrack_modes(yta_bytetrack *engine, long long *out, int n);
 /* Tuning / testing: bytes of LDS the association kernels may use per stream (default 150 KiB,

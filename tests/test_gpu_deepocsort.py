@@ -241,13 +241,10 @@ def test_deepocsort_dense_and_listed_paths_agree(monkeypatch):
     listed = DeepOCSortEngine(S, feat_dim=D, **kw, track_capacity=256, max_dets=128)
     ors = [DeepOCSortOracle(**kw) for _ in range(S)]
     shape = (640, 640, 3)
-    nd = np.zeros(S, np.int64)
-    nl = np.zeros(S, np.int64)
     for f in range(nf):
         args = ([streams[s][f][0] for s in range(S)], [streams[s][f][1] for s in range(S)])
-        gd = dense.update(*args, img_shapes=[shape] * S, next_id=nd)
-        gl = listed.update(*args, img_shapes=[shape] * S, next_id=nl)
-        assert np.array_equal(nd, nl), f
+        gd = dense.update(*args, img_shapes=[shape] * S)   # the engines' own ID counters (from 1)
+        gl = listed.update(*args, img_shapes=[shape] * S)
         for s in range(S):
             assert np.array_equal(gd[s].view(np.int64), gl[s].view(np.int64)), (s, f)
             d, e = streams[s][f]

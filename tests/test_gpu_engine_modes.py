@@ -5,8 +5,8 @@
   of a small host-buffer frame, re-captured when an argument changes) and YTA_SPLIT23 (stage 2 and
   stage 3 in two blocks per stream, the 1024-thread stage-1 / finish blocks): rows and ID counters
   bit-identical across the four engines and equal to the oracle (byte_tracker.py:132-281), and
-  the mode the kernel arguments carry (with its second arena) still the one chosen at create after
-  the growth (yta_bytetrack_modes).  Round 5's reserve() dropped the split mode on growth.
+  the mode the kernel arguments carry (with its pooled fallback arenas) still the one chosen at
+  create after the growth (yta_bytetrack_modes).  Round 5's reserve() dropped the split mode on growth.
 * Destroying an engine with pipelined frames submitted and not collected: the copy streams are
   drained before their buffers are freed; a new engine of the same sizes then runs exactly as a
   fresh one.
@@ -24,7 +24,7 @@ from yolo_tracking_amd.synth import make_frames
 pytestmark = pytest.mark.gpu
 
 KW = dict(track_thresh=0.5, match_thresh=0.8, track_buffer=30, frame_rate=30)
-MODES = ["split23", "args_split23", "ws3", "graphs", "bs_split", "captures", "replays", "cap",
+MODES = ["split23", "args_split23", "ws_slots", "graphs", "bs_split", "captures", "replays", "cap",
          "maxd"]
 
 
@@ -55,7 +55,8 @@ def test_growth_under_every_launch_mode(monkeypatch):
         monkeypatch.setenv("YTA_SPLIT23", str(split))
         eng = ByteTrackEngine(S, track_capacity=32, max_dets=32, **KW)
         m0 = modes(eng)
-        assert (m0["split23"], m0["args_split23"], m0["ws3"]) == (split,) * 3, m0
+        assert (m0["split23"], m0["args_split23"]) == (split,) * 2, m0
+        assert m0["ws_slots"] == (2 * S if split else S), m0   # every block can fall back at once
         assert m0["graphs"] == graphs and (m0["cap"], m0["maxd"]) == (32, 32), m0
         nid = np.zeros(S, np.int64)
         got, caps = [], []
@@ -66,7 +67,8 @@ def test_growth_under_every_launch_mode(monkeypatch):
         m1 = modes(eng)
         assert m1["cap"] > 32 and m1["maxd"] >= 120, m1
         # the kernel arguments still carry the mode chosen at create, with its second arena
-        assert (m1["split23"], m1["args_split23"], m1["ws3"]) == (split,) * 3, m1
+        assert (m1["split23"], m1["args_split23"]) == (split,) * 2, m1
+        assert m1["ws_slots"] == (2 * S if split else S), m1
         if graphs:   # captured at least before and after the growth, then replayed
             assert m1["captures"] >= 2 and m1["replays"] >= F, m1
         else:
@@ -95,7 +97,8 @@ def test_reserve_keeps_modes(monkeypatch):
         eng = ByteTrackEngine(2, track_capacity=16, max_dets=16, **KW)
         eng.reserve(64, 48)
         m = modes(eng)
-        assert (m["split23"], m["args_split23"], m["ws3"]) == (split,) * 3, m
+        assert (m["split23"], m["args_split23"]) == (split,) * 2, m
+        assert m["ws_slots"] == (4 if split else 2), m
         assert (m["cap"], m["maxd"]) == (64, 48), m
         eng.close()
 
@@ -132,3 +135,25 @@ def test_destroy_with_frames_in_flight(pinned):
                 assert np.array_equal(a[s].view(np.int64), b[s].view(np.int64)), (rounds, f, s)
         new.close()
         ref.close()
+
+
+def test_fallback_pool_under_contention(monkeypatch):
+    """Every stream-frame on the global fallback arenas (LDS budget 0) with a pool of two arenas
+    for eight streams (YTA_WS_POOL=2): the blocks of a launch queue for the arenas (ws_claim /
+    ws_release, arenas written by blocks on other XCDs in between), and every row equals the
+    LDS-arena engine's."""
+    S, F = 8, 14
+    frames = [[d for d, _ in make_frames(300, F, seed=1500 + s)] for s in range(S)]
+    ref = ByteTrackEngine(S, track_capacity=512, max_dets=300, **KW)
+    monkeypatch.setenv("YTA_WS_POOL", "2")
+    monkeypatch.setenv("YTA_SPLIT23", "0")
+    eng = ByteTrackEngine(S, track_capacity=512, max_dets=300, **KW)
+    assert modes(eng)["ws_slots"] == 2
+    eng.set_lds(0)
+    for f in range(F):
+        a = eng.update([frames[s][f] for s in range(S)])
+        b = ref.update([frames[s][f] for s in range(S)])
+        for s in range(S):
+            assert np.array_equal(a[s].view(np.int64), b[s].view(np.int64)), (f, s)
+    st = eng.stats()
+    assert st["fallback1"] >= S * (F - 1) and st["fallback23"] >= S * F, st

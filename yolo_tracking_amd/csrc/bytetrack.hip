@@ -391,6 +391,49 @@ __device__ __forceinline__ bool stage23_body(const BtArgs &a, int s, Arena &ar, 
     return true;
 }
 
+// ---- pooled global fallback arenas ---------------------------------------------------------
+// A stream-frame whose association does not fit its LDS arena is redone over a global arena.
+// Sized for the worst case (every pair a candidate edge), one such arena per stream costs
+// S x O(CAP x MAXD) bytes (154 GB for 2048 streams at CAP 3072 x MAXD 2048); fallbacks are rare
+// (none in the headline's steady state), so the engine keeps a pool of ws_slots arenas and a
+// falling-back block claims one (thread 0: first clear bit of ws_bits by atomicOr, from a
+// block-dependent start), runs on it and releases it.  A holder never waits for another block, so
+// a waiting claimer always gets an arena; the wait is bounded anyway (every wave reaches the end:
+// an exhausted bound flags ERR_EDGE_OVERFLOW).  The arena may have been written by a block on
+// another XCD (another L2): the claim and the release fence at agent scope.
+constexpr long long WS_SPIN_MAX = 1LL << 22;
+__device__ int ws_claim(const BtArgs &a, int *sh_slot) {
+    if (threadIdx.x == 0) {
+        int got = -1;
+        const int P = a.ws_slots, first = (int)(blockIdx.x % (unsigned)P);
+        for (long long spin = 0; got < 0 && spin < WS_SPIN_MAX; ++spin) {
+            for (int q = 0; q < P; ++q) {
+                const int b = first + q < P ? first + q : first + q - P;
+                const unsigned long long bit = 1ull << (b & 63);
+                if (!(atomicOr(&a.ws_bits[b >> 6], bit) & bit)) {
+                    got = b;
+                    break;
+                }
+            }
+            if (got < 0) __builtin_amdgcn_s_sleep(8);
+        }
+        __threadfence();
+        *sh_slot = got;
+    }
+    __syncthreads();
+    return *sh_slot;
+}
+__device__ void ws_release(const BtArgs &a, int slot) {
+    block_sync();   // every thread's arena accesses have completed
+    if (threadIdx.x == 0 && slot >= 0) {
+        __threadfence();
+        atomicAnd(&a.ws_bits[slot >> 6], ~(1ull << (slot & 63)));
+    }
+}
+__device__ __forceinline__ unsigned char *ws_base(const BtArgs &a, int slot) {
+    return a.ws + (long long)slot * a.ws_stride;
+}
+
 // LDS first; a frame whose association does not fit is redone over the stream's global arena
 // (both bodies only write values that the redo rewrites identically, and bump the frame counter
 // only on success).
@@ -408,8 +451,15 @@ __global__ __launch_bounds__(BLK1) void k_stage1(BtArgs a) {
     }
     block_sync();
     if (threadIdx.x == 0) a.cnt[s].n_fallback[0] += 1;
-    Arena ag(a.ws + s * a.ws_stride, a.ws_stride);
-    if (!stage1_body<V>(a, s, ag, sh) && threadIdx.x == 0) atomicOr(&a.cnt[s].err, ERR_EDGE_OVERFLOW);
+    __shared__ int ws_slot;
+    const int slot = ws_claim(a, &ws_slot);
+    bool ok = false;
+    if (slot >= 0) {
+        Arena ag(ws_base(a, slot), a.ws_stride);
+        ok = stage1_body<V>(a, s, ag, sh);
+    }
+    ws_release(a, slot);
+    if (!ok && threadIdx.x == 0) atomicOr(&a.cnt[s].err, ERR_EDGE_OVERFLOW);
 }
 
 // SPLIT (a.split23): two blocks per stream, block 2s + r running role r; else one block per
@@ -435,10 +485,20 @@ __global__ __launch_bounds__(SPLIT ? BLK23S : BLK23) void k_stage23(BtArgs a) {
         }
     }
     block_sync();
-    if (threadIdx.x == 0) atomicAdd(&a.cnt[s].n_fallback[1], 1);
-    Arena ag((role == 1 ? a.ws3 : a.ws) + s * a.ws_stride, a.ws_stride);
-    if (!stage23_body<V>(a, s, ag, sh, role) && threadIdx.x == 0)
-        atomicOr(&a.cnt[s].err, ERR_EDGE_OVERFLOW);
+    // a stream-frame is counted once: the split blocks mark it, k_finish counts the mark
+    if (threadIdx.x == 0) {
+        if (SPLIT) atomicOr(&a.cnt[s].fb23_mark, 1);
+        else atomicAdd(&a.cnt[s].n_fallback[1], 1);
+    }
+    __shared__ int ws_slot;
+    const int slot = ws_claim(a, &ws_slot);
+    bool ok = false;
+    if (slot >= 0) {
+        Arena ag(ws_base(a, slot), a.ws_stride);
+        ok = stage23_body<V>(a, s, ag, sh, role);
+    }
+    ws_release(a, slot);
+    if (!ok && threadIdx.x == 0) atomicOr(&a.cnt[s].err, ERR_EDGE_OVERFLOW);
 }
 
 // ------------------------------------------------------------------ ByteTrack stage 1, split
@@ -760,6 +820,9 @@ __device__ __forceinline__ void s1_edges_body(const BtArgs &a, int s, int nc, in
 // order-free).  Queues hold WQ_CAP entries; a larger candidate total is listed and scored in
 // windows.  Big items (larger than 4 x the mean box) are visited per lane, as grid_query does.
 constexpr int WQ_CAP = 384;
+#ifndef YTA_S1_P1
+#define YTA_S1_P1 1   // k_s1_edges' queue passes: two chunks per trip, branch-free tests (round 6)
+#endif
 #ifndef YTA_S1_SOA
 #define YTA_S1_SOA 1   // k_s1_edges' LDS grid keeps its boxes as four arrays (GridView::sx)
 #endif
@@ -829,6 +892,34 @@ __device__ __forceinline__ void s1_edges_rows_wave(const BtArgs &a, int s, int n
             // pass 1: keep the intersecting candidates (compacted in place: a survivor's new index
             // is at most its old one, and a chunk is read before any of it is overwritten)
             int ns = 0;
+#if YTA_S1_P1
+            // Two chunks of 64 per trip, every load of both issued before any test, and the test
+            // branch-free: a queued row box has x2 > x1 and y2 > y1 (grid_scan_window lists
+            // nothing otherwise, NaN included) and a binned box is usable, so intersects()
+            // reduces to its four cross comparisons - the same predicate on every queued pair.
+            // (The short-circuit form compiled to a chain of exec-masked LDS round trips.)
+            const unsigned long long lt = (1ull << lane) - 1ull;
+            for (int k0 = 0; k0 < n; k0 += 2 * WAVE) {   // wave-uniform trip count
+                const int ka = k0 + lane, kb = ka + WAVE;
+                const unsigned ea = wq.q[ka < n ? ka : 0], eb = wq.q[kb < n ? kb : 0];
+                const int ra = (int)(ea >> 24), pa = (int)(ea & 0xFFFFFFu);
+                const int rb_ = (int)(eb >> 24), pb = (int)(eb & 0xFFFFFFu);
+                const Box A{bperm_f64(rb.x1, ra), bperm_f64(rb.y1, ra), bperm_f64(rb.x2, ra),
+                            bperm_f64(rb.y2, ra)};
+                const Box B{bperm_f64(rb.x1, rb_), bperm_f64(rb.y1, rb_), bperm_f64(rb.x2, rb_),
+                            bperm_f64(rb.y2, rb_)};
+                const Box ca = s1_box(gv, pa), cb = s1_box(gv, pb);
+                const bool ha = (ka < n) & (A.x2 > ca.x1) & (ca.x2 > A.x1) & (A.y2 > ca.y1) &
+                                (ca.y2 > A.y1);
+                const bool hb = (kb < n) & (B.x2 > cb.x1) & (cb.x2 > B.x1) & (B.y2 > cb.y1) &
+                                (cb.y2 > B.y1);
+                const unsigned long long ba = __ballot(ha), bb = __ballot(hb);
+                const int na = __popcll(ba);
+                if (ha) wq.q[ns + __popcll(ba & lt)] = ea;
+                if (hb) wq.q[ns + na + __popcll(bb & lt)] = eb;
+                ns += na + __popcll(bb);
+            }
+#else
             for (int k0 = 0; k0 < n; k0 += WAVE) {   // wave-uniform trip count
                 const int k = k0 + lane;
                 const unsigned ent = k < n ? wq.q[k] : 0u;
@@ -840,11 +931,25 @@ __device__ __forceinline__ void s1_edges_rows_wave(const BtArgs &a, int s, int n
                 if (hit) wq.q[ns + __popcll(bal & ((1ull << lane) - 1ull))] = ent;
                 ns += __popcll(bal);
             }
+#endif
             __builtin_amdgcn_wave_barrier();
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             // pass 2: score the survivors (full lanes for the float64 IoU)
             for (int k0 = 0; k0 < ns; k0 += WAVE) {
                 const int k = k0 + lane;
+#if YTA_S1_P1   // every operand's load issued before the row box arrives and before any branch
+                const unsigned ent = wq.q[k < ns ? k : 0];
+                const int r = (int)(ent >> 24), pos = (int)(ent & 0xFFFFFFu);
+                const Box cb = s1_box(gv, pos);
+                const double wj = gv.w[pos];
+                const int j = gv.ids[pos];
+                const Box tb_{bperm_f64(rb.x1, r), bperm_f64(rb.y1, r), bperm_f64(rb.x2, r),
+                              bperm_f64(rb.y2, r)};
+                if (k >= ns) continue;
+                const double dist = 1 - iou(tb_, cb);                   // matching.py:117
+                const double cost = 1 - (1 - dist) * wj;                // matching.py:216-220
+                if (!(cost < thresh)) continue;
+#else
                 const unsigned ent = k < ns ? wq.q[k] : 0u;
                 const int r = (int)(ent >> 24), pos = (int)(ent & 0xFFFFFFu);
                 const Box tb_{bperm_f64(rb.x1, r), bperm_f64(rb.y1, r), bperm_f64(rb.x2, r),
@@ -855,6 +960,7 @@ __device__ __forceinline__ void s1_edges_rows_wave(const BtArgs &a, int s, int n
                 const double cost = 1 - (1 - dist) * gv.w[pos];         // matching.py:216-220
                 if (!(cost < thresh)) continue;
                 const int j = gv.ids[pos];
+#endif
                 const int c = atomicAdd(&wq.cnt[r], 1);
                 if (c < E_SLOTS) {
                     a.e_col[c * SC + tb + base + r] = j;
@@ -1227,8 +1333,15 @@ __global__ __launch_bounds__(NT, NT == BLKL ? 4 : 1) void k_s1_lap(BtArgs a) {
     }
     block_sync();
     if (threadIdx.x == 0) a.cnt[s].n_fallback[0] += 1;
-    Arena ag(a.ws + s * a.ws_stride, a.ws_stride);
-    if (!s1_lap_body(a, s, ag, lsh) && threadIdx.x == 0) atomicOr(&a.cnt[s].err, ERR_EDGE_OVERFLOW);
+    __shared__ int ws_slot;
+    const int slot = ws_claim(a, &ws_slot);
+    bool ok = false;
+    if (slot >= 0) {
+        Arena ag(ws_base(a, slot), a.ws_stride);
+        ok = s1_lap_body(a, s, ag, lsh);
+    }
+    ws_release(a, slot);
+    if (!ok && threadIdx.x == 0) atomicOr(&a.cnt[s].err, ERR_EDGE_OVERFLOW);
     YTA_BLK(2, 1);
 }
 
@@ -1490,8 +1603,15 @@ __global__ __launch_bounds__(BLK1) void k_bs_lap(BtArgs a) {
             for (int q = t; q < n_high; q += nt) a.y1[db + q] = -1;
             block_sync();
         }
-        Arena ag(a.ws + s * a.ws_stride, a.ws_stride);
-        ok = spill ? stage1_assoc<VAR_BOTSORT>(a, s, L, ag, sh) : s1_lap_body(a, s, ag, sh.as.lap);
+        __shared__ int ws_slot;
+        const int slot = ws_claim(a, &ws_slot);
+        ok = false;
+        if (slot >= 0) {
+            Arena ag(ws_base(a, slot), a.ws_stride);
+            ok = spill ? stage1_assoc<VAR_BOTSORT>(a, s, L, ag, sh)
+                       : s1_lap_body(a, s, ag, sh.as.lap);
+        }
+        ws_release(a, slot);
         if (!ok && t == 0) atomicOr(&c->err, ERR_EDGE_OVERFLOW);
     }
     block_sync();
@@ -2261,6 +2381,10 @@ __device__ __forceinline__ void finish_body(const BtArgs &a, int s, unsigned *bi
         c->n_free = n_fr;
         c->slot_cursor = cur;
         c->n_out = n_out;
+        if (c->fb23_mark) {   // split k_stage23 redone over global memory (either block)
+            c->n_fallback[1] += 1;
+            c->fb23_mark = 0;
+        }
         if (a.out_counts) a.out_counts[s] = n_out;
         if (NP) {   // the next frame's stage-1 pool (built above)
             c->n_act = n_out;
@@ -2307,8 +2431,15 @@ __global__ __launch_bounds__(NT, NT == BLKF ? 4 : 1) void k_finish(BtArgs a) {
         finish_body<V>(a, s, bits, ar, sh);
     } else {
         if (threadIdx.x == 0) a.cnt[s].n_fallback_f += 1;
-        Arena ag(a.ws + s * a.ws_stride, a.ws_stride);
-        finish_body<V>(a, s, bits, ag, sh);
+        __shared__ int ws_slot;
+        const int slot = ws_claim(a, &ws_slot);
+        if (slot >= 0) {
+            Arena ag(ws_base(a, slot), a.ws_stride);
+            finish_body<V>(a, s, bits, ag, sh);
+        } else {   // no arena within the bound: the frame's lists are not rebuilt (flagged)
+            if (threadIdx.x == 0) atomicOr(&a.cnt[s].err, ERR_EDGE_OVERFLOW);
+        }
+        ws_release(a, slot);
     }
     YTA_BLK(5, 1);
 }
@@ -2391,6 +2522,7 @@ __global__ __launch_bounds__(OFFS_T) void k_out_offsets_scan(const BtCounters *c
 // yta_bytetrack_pipe_stats host_d2h_call_ms ~1.7-1.8 ms a frame).  tools/pcie_bench.hip: 55 GB/s
 // from 64 blocks, as the copy engines, and 88 GB/s beside a copy-engine host -> device copy.
 constexpr int ROWS_H_BLOCKS = 128;
+__global__ void k_nop() {}
 __global__ __launch_bounds__(1024) void k_copy_ints(const int *src, int *dst, int n) {
     for (int i = threadIdx.x; i < n; i += blockDim.x) dst[i] = src[i];
 }
@@ -2507,6 +2639,51 @@ static bool pipe_slot_streams() {
 static bool pipe_off_kernel() {
     static const bool k = env_flag("YTA_PIPE_OFF_KERNEL", false);
     return k;
+}
+// The copy-in stream ends each frame with an empty kernel (k_nop) that the frame's completion
+// event follows (1, default), instead of the event directly after the copy engine's transfer
+// (YTA_PIPE_IN_FENCE=0)
+static bool pipe_in_kernel_fence() {
+    static const bool k = env_flag("YTA_PIPE_IN_FENCE", true);
+    return k;
+}
+// The pipelined path's host waits poll the event with hipEventQuery (1, default) instead of
+// blocking in hipEventSynchronize (YTA_PIPE_SPIN=0): traced (tools/pipe_timeline.py), a frame's
+// kernels - enqueued behind a wait on its copy-in's event - started only when the host made its
+// next HIP call (the next frame's copy-in enqueue), ~1.3 ms after the copy-in had ended; a host
+// thread blocked in a synchronize makes no such call
+static bool pipe_spin() {
+    static const bool k = env_flag("YTA_PIPE_SPIN", true);
+    return k;
+}
+// The copy-in's completion event with a device-scope release (1, default; YTA_PIPE_IN_DEVREL=0:
+// the default system scope, an L2 writeback + invalidate that waits behind k_rows_to_host's
+// stream of host stores - an empty kernel then took ~1 ms to complete, gpurun_out/r6g_pipe)
+static bool pipe_in_device_release() {
+    static const bool k = env_flag("YTA_PIPE_IN_DEVREL", true);
+    return k;
+}
+// An empty kernel enqueued right after each of the pipelined path's events (1, default;
+// YTA_PIPE_FLUSH=0 off): traced (gpurun_out/r6h_pipe), a frame's kernels waiting on its copy-in
+// event started only when the NEXT command on the copy-in stream ran, ~1.3 ms after the copy (and
+// the empty kernel before the event) had completed - as if the event's packet reached the copy-in
+// queue's hardware only with the next submission.  A dispatch behind it makes the queue advance.
+static bool pipe_flush_on() {
+    static const bool k = env_flag("YTA_PIPE_FLUSH", true);
+    return k;
+}
+static hipError_t pipe_flush(hipStream_t st) {
+    if (!pipe_flush_on()) return hipSuccess;
+    hipLaunchKernelGGL(k_nop, dim3(1), dim3(64), 0, st);
+    return hipGetLastError();
+}
+static hipError_t pipe_event_wait(hipEvent_t ev) {
+    if (!pipe_spin()) return hipEventSynchronize(ev);
+    for (;;) {
+        const hipError_t q = hipEventQuery(ev);
+        if (q != hipErrorNotReady) return q;
+        std::this_thread::yield();
+    }
 }
 // Rows device -> host by k_rows_to_host (1, default) or by the copy engines (YTA_PIPE_KERNEL_D2H=0)
 static bool pipe_kernel_d2h() {
@@ -2826,10 +3003,17 @@ int bt_alloc(yta_bytetrack *e) {
     if (e->variant == VAR_BOTSORT && e->D > 0)
         a.ws_stride = std::max(a.ws_stride, assoc_emb_arena_bytes(CAP, MAXD));
     a.ws_stride = (a.ws_stride + 255) & ~255LL;
-    DALLOC(a.ws, S * a.ws_stride);
     a.split23 = e->split23;
     a.ws3 = nullptr;
-    if (a.split23) DALLOC(a.ws3, S * a.ws_stride);
+    {   // pooled fallback arenas (ws_claim): enough for every block of a few-stream engine, a
+        // bounded pool for many streams (YTA_WS_POOL overrides the bound, 2..256)
+        int pool = 32;
+        if (const char *v = getenv("YTA_WS_POOL")) pool = std::max(2, std::min(256, atoi(v)));
+        a.ws_slots = (int)std::min<long long>(S * (a.split23 ? 2 : 1), pool);
+    }
+    DALLOC(a.ws, (long long)a.ws_slots * a.ws_stride);
+    DALLOC(a.ws_bits, 4);
+    YTA_HIP(hipMemset(a.ws_bits, 0, 4 * sizeof(unsigned long long)));
     a.slab.R = (int)CAP;
     a.slab.C = (int)MAXD;
     a.slab.i_stride = lap_slab_ints((int)CAP, (int)MAXD);
@@ -2998,7 +3182,7 @@ int reserve(yta_bytetrack *e, int cap, int maxd) {
     n->D = e->D;
     n->bprm = e->bprm;
     n->stream = e->stream;
-    // every create-time mode bt_alloc reads (the split stage 2 / 3 blocks and their ws3 arena)
+    // every create-time mode bt_alloc reads (the split stage 2 / 3 blocks, the fallback pool size)
     n->split23 = e->split23;
     n->bs_split = e->bs_split;
     n->graphs = e->graphs;
@@ -3568,7 +3752,14 @@ int pipe_slot_ready(yta_bytetrack *e, yta_bytetrack::PipeSlot &p, long long dets
     }
     if (!p.s_in) p.s_in = e->s_in;
     if (!p.in_done) {
-        for (hipEvent_t *ev : {&p.in_done, &p.kern_done, &p.out_done})
+        // in_done is waited on by the compute stream only (device work reading device memory): a
+        // device-scope release; kern_done / out_done are also waited on by the host, which then
+        // reads what the kernels stored into mapped host memory: the default system scope
+        YTA_HIP(hipEventCreateWithFlags(&p.in_done, hipEventDisableTiming |
+                                                        (pipe_in_device_release()
+                                                             ? hipEventReleaseToDevice
+                                                             : 0u)));
+        for (hipEvent_t *ev : {&p.kern_done, &p.out_done})
             YTA_HIP(hipEventCreateWithFlags(ev, hipEventDisableTiming));
         if (pipe_timing())
             for (hipEvent_t &ev : p.t_ev) YTA_HIP(hipEventCreateWithFlags(&ev, hipEventDefault));
@@ -3657,8 +3848,18 @@ int pipe_enqueue_in(yta_bytetrack *e, yta_bytetrack::PipeSlot &p, const double *
         }
     }
     e->pstat[p.direct_in ? PS_IN_DIRECT : PS_IN_STAGED] += (double)p.in_bytes;
+    if (pipe_in_kernel_fence()) {
+        // the copy-in stream ends with an empty kernel, so in_done completes when the copy does:
+        // traced (tools/pipe_timeline.py, gpurun_out/r6d_pipe, r6f_pipe) an event recorded right
+        // after the copy engine's transfer completed only when the NEXT command on the copy-in
+        // stream ran (the next frame's offsets copy, a blit kernel) - ~1.3 ms later, the frame's
+        // kernels waiting on it that long
+        hipLaunchKernelGGL(k_nop, dim3(1), dim3(64), 0, p.s_in);
+        YTA_HIP(hipGetLastError());
+    }
     if (p.t_ev[1]) YTA_HIP(hipEventRecord(p.t_ev[1], p.s_in));
     YTA_HIP(hipEventRecord(p.in_done, p.s_in));
+    YTA_HIP(pipe_flush(p.s_in));
     return YTA_OK;
 }
 
@@ -3699,6 +3900,7 @@ int pipe_enqueue_run(yta_bytetrack *e, yta_bytetrack::PipeSlot &p, const long lo
     YTA_HIP(hipGetLastError());
     if (p.t_ev[3]) YTA_HIP(hipEventRecord(p.t_ev[3], e->stream));
     YTA_HIP(hipEventRecord(p.kern_done, e->stream));
+    YTA_HIP(pipe_flush(e->stream));
     // copy-out stream: counters, offsets and at most det_offsets[S] rows (every output row is a
     // track matched to or born from one of the frame's detections)
     YTA_HIP(hipStreamWaitEvent(e->s_out, p.kern_done, 0));
@@ -3728,6 +3930,7 @@ int pipe_enqueue_run(yta_bytetrack *e, yta_bytetrack::PipeSlot &p, const long lo
     }
     if (p.t_ev[5]) YTA_HIP(hipEventRecord(p.t_ev[5], e->s_out));
     YTA_HIP(hipEventRecord(p.out_done, e->s_out));
+    YTA_HIP(pipe_flush(e->s_out));
     return YTA_OK;
 }
 
@@ -3776,7 +3979,7 @@ int pipe_capacity(yta_bytetrack *e, const int *det_offsets) {
         }
         if (fits(k0)) return YTA_OK;
         if (k0 != e->pipe_count - 1) {
-            YTA_HIP(hipEventSynchronize(slot(e->pipe_count - 1).kern_done));
+            YTA_HIP(pipe_event_wait(slot(e->pipe_count - 1).kern_done));
             ++e->pstat[PS_CAP_WAITS];
             if (fits(e->pipe_count - 1)) return YTA_OK;
         }
@@ -3845,7 +4048,7 @@ int pipe_collect(yta_bytetrack *e, long long *next_id, int *out_offsets) {
     e->pipe_head = (e->pipe_head + 1) % PIPE_DEPTH;
     --e->pipe_count;
     const auto t0 = std::chrono::steady_clock::now();
-    YTA_HIP(hipEventSynchronize(p.out_done));
+    YTA_HIP(pipe_event_wait(p.out_done));
     const auto t1 = std::chrono::steady_clock::now();
     e->pstat[PS_WAIT_MS] += std::chrono::duration<double, std::milli>(t1 - t0).count();
     if (p.t_ev[0]) {   // the frame's GPU-side phases from its timing events (all complete)
@@ -4181,7 +4384,7 @@ int yta_bytetrack_stats(yta_bytetrack *e, long long *stats) {
 
 int yta_bytetrack_modes(yta_bytetrack *e, long long *out, int n) {
     YTA_CHECK(e && (out || n <= 0), YTA_ERR_INVALID, "null argument");
-    const long long v[YTA_BT_MODES] = {e->split23,          e->a.split23,   e->a.ws3 != nullptr,
+    const long long v[YTA_BT_MODES] = {e->split23,          e->a.split23,   e->a.ws_slots,
                                        e->graphs,           e->bs_split,    e->g_captures,
                                        e->g_replays,        e->CAP,         e->MAXD};
     for (int k = 0; k < n && k < YTA_BT_MODES; ++k) out[k] = v[k];

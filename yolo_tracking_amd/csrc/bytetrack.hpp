@@ -56,7 +56,8 @@ struct BtCounters {                  // one per stream, 128 B
     int slot_cursor;                 // births take free slots from here on, cyclically
     int bs_spill;                    // BoT-SORT split stage 1: a pool row had more than E_SLOTS
                                      // edges (k_bs_lap then runs the fused association)
-    int pad;
+    int fb23_mark;                   // split k_stage23: a block of this frame fell back (k_finish
+                                     // counts the stream-frame once in n_fallback[1])
 };
 static_assert(sizeof(BtCounters) == 128, "BtCounters layout");
 
@@ -114,7 +115,12 @@ struct BtArgs {
     // few streams: k_stage23 runs stage 2 and stage 3 (independent given stage 1) in two blocks
     // per stream; stage 3's block has its own fallback arena [S * ws_stride] and solver slabs
     int split23;
-    unsigned char *ws3;
+    unsigned char *ws3;       // unused (round 6: the stage-3 block claims from the pool below)
+    // the global fallback arenas are a pool of ws_slots arenas of ws_stride bytes shared by the
+    // engine's streams (a block claims one when its LDS arena is too small, bytetrack.hip
+    // ws_claim): worst-case arenas for every stream cost O(S * CAP * MAXD) bytes of HBM
+    int ws_slots;
+    unsigned long long *ws_bits;   // [4] claimed-arena bitmap
     LapSlab slab;             // per stream: (threads / 64) slabs
     // ByteTrack stage 1 as three launches (k_s1_prep / k_s1_edges / k_s1_lap): the per-stream
     // grid over the high detections and every pool row's first candidate edges, in HBM
