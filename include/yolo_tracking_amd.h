@@ -266,8 +266,8 @@ int yta_bytetrack_stats(yta_bytetrack *engine, long long *stats);
  * blocks per stream), the fallback arenas pooled, cached HIP graphs enabled (YTA_GRAPHS), BoT-SORT
  * split stage 1 (YTA_BS_SPLIT), graph captures and graph replays so far, track capacity, max
  * detections.  The third is the number of pooled global fallback arenas (a stream-frame whose
- * association does not fit in LDS claims one): two per stream in the split mode up to a bound of 32
- * (YTA_WS_POOL).  The first two agree for the engine's whole life, reserve() included. */
+ * association does not fit in LDS is redone over one of them by the launch's redo kernel, which
+ * runs that many blocks): two per stream in the split mode up to a bound of 32 (YTA_WS_POOL).  The first two agree for the engine's whole life, reserve() included. */
 #define YTA_BT_MODES 9
 int yta_bytetrack_modes(yta_bytetrack *engine, long long *out, int n);
 /* Tuning / testing: bytes of LDS the association kernels may use per stream (default 150 KiB,

@@ -139,9 +139,10 @@ def test_destroy_with_frames_in_flight(pinned):
 
 def test_fallback_pool_under_contention(monkeypatch):
     """Every stream-frame on the global fallback arenas (LDS budget 0) with a pool of two arenas
-    for eight streams (YTA_WS_POOL=2): the blocks of a launch queue for the arenas (ws_claim /
-    ws_release, arenas written by blocks on other XCDs in between), and every row equals the
-    LDS-arena engine's."""
+    for eight streams (YTA_WS_POOL=2): every block of a launch queues its stream and the launch's
+    two-block redo kernel takes four streams per arena in turn (bytetrack.hip redo_drain; the
+    queue cleared by its last block for the next launch), and every row equals the LDS-arena
+    engine's."""
     S, F = 8, 14
     frames = [[d for d, _ in make_frames(300, F, seed=1500 + s)] for s in range(S)]
     ref = ByteTrackEngine(S, track_capacity=512, max_dets=300, **KW)

@@ -395,48 +395,47 @@ __device__ __forceinline__ bool stage23_body(const BtArgs &a, int s, Arena &ar, 
 // A stream-frame whose association does not fit its LDS arena is redone over a global arena.
 // Sized for the worst case (every pair a candidate edge), one such arena per stream costs
 // S x O(CAP x MAXD) bytes (154 GB for 2048 streams at CAP 3072 x MAXD 2048); fallbacks are rare
-// (none in the headline's steady state), so the engine keeps a pool of ws_slots arenas and a
-// falling-back block claims one (thread 0: first clear bit of ws_bits by atomicOr, from a
-// block-dependent start), runs on it and releases it.  A holder never waits for another block, so
-// a waiting claimer always gets an arena; the wait is bounded anyway (every wave reaches the end:
-// an exhausted bound flags ERR_EDGE_OVERFLOW).  The arena may have been written by a block on
-// another XCD (another L2): the claim and the release fence at agent scope.
-constexpr long long WS_SPIN_MAX = 1LL << 22;
-__device__ int ws_claim(const BtArgs &a, int *sh_slot) {
+// (none in the headline's steady state), so the engine keeps a pool of ws_slots arenas.  A
+// launch with no more blocks than arenas (few streams) redoes in place over arena blockIdx; in a
+// larger launch the block that falls back queues its block id (redo_queue) and returns, and the
+// launch's redo kernel (k_redo_*, ws_slots blocks, right behind it on the same stream) takes
+// queued block q, q + ws_slots, ... on arena blockIdx.x (redo_drain).  The last redo block out
+// clears the queue for the next launch.  (An in-kernel claim of a pooled arena - a bitmap,
+// released after the redo - put code behind the second inlined body: k_stage23 went from 120
+// VGPRs to 167 with 696 B of scratch, k_s1_lap and k_finish spilled, and the headline fell from
+// 2.0 M to 1.5 M calls/s, gpurun_out/r6t.)
+// A launch of at most ws_slots association blocks (few streams) has an arena per block: its blocks
+// redo in place over arena `block` and no redo kernel is launched (redo_launch).
+__device__ __forceinline__ bool redo_in_place(const BtArgs &a, int blocks) { return blocks <= a.ws_slots; }
+__device__ __forceinline__ unsigned char *redo_arena(const BtArgs &a, int block) {
+    return a.ws + (long long)block * a.ws_stride;
+}
+__device__ __forceinline__ void redo_queue(const BtArgs &a, int block) {
+    const int q = atomicAdd(&a.redo_q[0], 1);
+    a.redo_q[2 + q] = block;
+}
+// redo(block id, arena) -> false: the arena was too small as well (ERR_EDGE_OVERFLOW)
+template <class Redo>
+__device__ __forceinline__ void redo_drain(const BtArgs &a, Redo &&redo) {
+    const int n = __builtin_amdgcn_readfirstlane(a.redo_q[0]);
+    for (int q = blockIdx.x; q < n; q += gridDim.x) {
+        Arena ag(redo_arena(a, blockIdx.x), a.ws_stride);
+        redo(__builtin_amdgcn_readfirstlane(a.redo_q[2 + q]), ag);
+        block_sync();
+    }
+    __syncthreads();   // every thread has read the count
     if (threadIdx.x == 0) {
-        int got = -1;
-        const int P = a.ws_slots, first = (int)(blockIdx.x % (unsigned)P);
-        for (long long spin = 0; got < 0 && spin < WS_SPIN_MAX; ++spin) {
-            for (int q = 0; q < P; ++q) {
-                const int b = first + q < P ? first + q : first + q - P;
-                const unsigned long long bit = 1ull << (b & 63);
-                if (!(atomicOr(&a.ws_bits[b >> 6], bit) & bit)) {
-                    got = b;
-                    break;
-                }
-            }
-            if (got < 0) __builtin_amdgcn_s_sleep(8);
+        __threadfence();
+        if (atomicAdd(&a.redo_q[1], 1) == (int)gridDim.x - 1) {
+            atomicExch(&a.redo_q[0], 0);
+            atomicExch(&a.redo_q[1], 0);
         }
-        __threadfence();
-        *sh_slot = got;
     }
-    __syncthreads();
-    return *sh_slot;
-}
-__device__ void ws_release(const BtArgs &a, int slot) {
-    block_sync();   // every thread's arena accesses have completed
-    if (threadIdx.x == 0 && slot >= 0) {
-        __threadfence();
-        atomicAnd(&a.ws_bits[slot >> 6], ~(1ull << (slot & 63)));
-    }
-}
-__device__ __forceinline__ unsigned char *ws_base(const BtArgs &a, int slot) {
-    return a.ws + (long long)slot * a.ws_stride;
 }
 
-// LDS first; a frame whose association does not fit is redone over the stream's global arena
-// (both bodies only write values that the redo rewrites identically, and bump the frame counter
-// only on success).
+// LDS first; a frame whose association does not fit is redone by k_redo_stage1 over a global
+// arena (the body only writes values that the redo rewrites identically, and bumps the frame
+// counter only on success).
 template <int V>
 __global__ __launch_bounds__(BLK1) void k_stage1(BtArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -445,21 +444,25 @@ __global__ __launch_bounds__(BLK1) void k_stage1(BtArgs a) {
     if (stream_skipped(a, s)) return;
     YTA_STAMP_BASE(0);
     YTA_STAMP(0);
-    {
-        Arena ar(smem, a.lds_bytes);
-        if (stage1_body<V>(a, s, ar, sh)) return;
-    }
+    Arena ar(smem, a.lds_bytes);
+    if (stage1_body<V>(a, s, ar, sh)) return;
     block_sync();
     if (threadIdx.x == 0) a.cnt[s].n_fallback[0] += 1;
-    __shared__ int ws_slot;
-    const int slot = ws_claim(a, &ws_slot);
-    bool ok = false;
-    if (slot >= 0) {
-        Arena ag(ws_base(a, slot), a.ws_stride);
-        ok = stage1_body<V>(a, s, ag, sh);
+    if (redo_in_place(a, a.S)) {
+        Arena ag(redo_arena(a, s), a.ws_stride);
+        if (!stage1_body<V>(a, s, ag, sh) && threadIdx.x == 0)
+            atomicOr(&a.cnt[s].err, ERR_EDGE_OVERFLOW);
+    } else if (threadIdx.x == 0) {
+        redo_queue(a, s);
     }
-    ws_release(a, slot);
-    if (!ok && threadIdx.x == 0) atomicOr(&a.cnt[s].err, ERR_EDGE_OVERFLOW);
+}
+template <int V>
+__global__ __launch_bounds__(BLK1) void k_redo_stage1(BtArgs a) {
+    __shared__ StageShared sh;
+    redo_drain(a, [&](int s, Arena &ag) {
+        if (!stage1_body<V>(a, s, ag, sh) && threadIdx.x == 0)
+            atomicOr(&a.cnt[s].err, ERR_EDGE_OVERFLOW);
+    });
 }
 
 // SPLIT (a.split23): two blocks per stream, block 2s + r running role r; else one block per
@@ -477,12 +480,10 @@ __global__ __launch_bounds__(SPLIT ? BLK23S : BLK23) void k_stage23(BtArgs a) {
     YTA_STAMP_BASE(20);
     YTA_STAMP(0);
     YTA_BLK(3, 0);
-    {
-        Arena ar(smem, a.lds_bytes23);
-        if (stage23_body<V>(a, s, ar, sh, role)) {
-            YTA_BLK(3, 1);
-            return;
-        }
+    Arena ar(smem, a.lds_bytes23);
+    if (stage23_body<V>(a, s, ar, sh, role)) {
+        YTA_BLK(3, 1);
+        return;
     }
     block_sync();
     // a stream-frame is counted once: the split blocks mark it, k_finish counts the mark
@@ -490,15 +491,22 @@ __global__ __launch_bounds__(SPLIT ? BLK23S : BLK23) void k_stage23(BtArgs a) {
         if (SPLIT) atomicOr(&a.cnt[s].fb23_mark, 1);
         else atomicAdd(&a.cnt[s].n_fallback[1], 1);
     }
-    __shared__ int ws_slot;
-    const int slot = ws_claim(a, &ws_slot);
-    bool ok = false;
-    if (slot >= 0) {
-        Arena ag(ws_base(a, slot), a.ws_stride);
-        ok = stage23_body<V>(a, s, ag, sh, role);
+    if (redo_in_place(a, SPLIT ? 2 * a.S : a.S)) {
+        Arena ag(redo_arena(a, blockIdx.x), a.ws_stride);
+        if (!stage23_body<V>(a, s, ag, sh, role) && threadIdx.x == 0)
+            atomicOr(&a.cnt[s].err, ERR_EDGE_OVERFLOW);
+    } else if (threadIdx.x == 0) {
+        redo_queue(a, blockIdx.x);
     }
-    ws_release(a, slot);
-    if (!ok && threadIdx.x == 0) atomicOr(&a.cnt[s].err, ERR_EDGE_OVERFLOW);
+}
+template <int V, bool SPLIT>
+__global__ __launch_bounds__(SPLIT ? BLK23S : BLK23) void k_redo_stage23(BtArgs a) {
+    __shared__ StageShared sh;
+    redo_drain(a, [&](int b, Arena &ag) {
+        const int s = SPLIT ? b >> 1 : b;
+        if (!stage23_body<V>(a, s, ag, sh, SPLIT ? (b & 1) : -1) && threadIdx.x == 0)
+            atomicOr(&a.cnt[s].err, ERR_EDGE_OVERFLOW);
+    });
 }
 
 // ------------------------------------------------------------------ ByteTrack stage 1, split
@@ -1324,25 +1332,28 @@ __global__ __launch_bounds__(NT, NT == BLKL ? 4 : 1) void k_s1_lap(BtArgs a) {
     const int s = blockIdx.x;
     if (stream_skipped(a, s)) return;
     YTA_BLK(2, 0);
-    {
-        Arena ar(smem, a.lds_bytes_l);
-        if (s1_lap_body(a, s, ar, lsh)) {
-            YTA_BLK(2, 1);
-            return;
+    Arena ar(smem, a.lds_bytes_l);
+    if (!s1_lap_body(a, s, ar, lsh)) {
+        block_sync();
+        if (threadIdx.x == 0) a.cnt[s].n_fallback[0] += 1;
+        // the many-stream kernel always queues: a redo in place costs it 48 B more scratch
+        if (NT == 1024 && redo_in_place(a, a.S)) {
+            Arena ag(redo_arena(a, s), a.ws_stride);
+            if (!s1_lap_body(a, s, ag, lsh) && threadIdx.x == 0)
+                atomicOr(&a.cnt[s].err, ERR_EDGE_OVERFLOW);
+        } else if (threadIdx.x == 0) {
+            redo_queue(a, s);
         }
     }
-    block_sync();
-    if (threadIdx.x == 0) a.cnt[s].n_fallback[0] += 1;
-    __shared__ int ws_slot;
-    const int slot = ws_claim(a, &ws_slot);
-    bool ok = false;
-    if (slot >= 0) {
-        Arena ag(ws_base(a, slot), a.ws_stride);
-        ok = s1_lap_body(a, s, ag, lsh);
-    }
-    ws_release(a, slot);
-    if (!ok && threadIdx.x == 0) atomicOr(&a.cnt[s].err, ERR_EDGE_OVERFLOW);
     YTA_BLK(2, 1);
+}
+template <int NT>
+__global__ __launch_bounds__(NT) void k_redo_s1_lap(BtArgs a) {
+    __shared__ LapShared lsh;
+    redo_drain(a, [&](int s, Arena &ag) {
+        if (!s1_lap_body(a, s, ag, lsh) && threadIdx.x == 0)
+            atomicOr(&a.cnt[s].err, ERR_EDGE_OVERFLOW);
+    });
 }
 
 // ------------------------------------------------------------------------------ k_feat / k_ema
@@ -1590,28 +1601,22 @@ __global__ __launch_bounds__(BLK1) void k_bs_lap(BtArgs a) {
         for (int q = t; q < n_high; q += nt) a.y1[db + q] = -1;
         block_sync();
     }
-    bool ok;
-    {
-        Arena ar(smem, a.lds_bytes);
-        ok = spill ? stage1_assoc<VAR_BOTSORT>(a, s, L, ar, sh) : s1_lap_body(a, s, ar, sh.as.lap);
-    }
-    if (!ok) {   // the stream's global arena
+    Arena ar(smem, a.lds_bytes);
+    bool ok = spill ? stage1_assoc<VAR_BOTSORT>(a, s, L, ar, sh) : s1_lap_body(a, s, ar, sh.as.lap);
+    if (!ok) {   // a global arena: here, or by k_redo_bs_lap (which then advances the frame)
         block_sync();
         if (t == 0) c->n_fallback[0] += 1;
+        if (!redo_in_place(a, a.S)) {
+            if (t == 0) redo_queue(a, s);
+            return;
+        }
         if (!spill) {
             for (int q = t; q < n_pool; q += nt) a.x1[tb + q] = -1;
             for (int q = t; q < n_high; q += nt) a.y1[db + q] = -1;
             block_sync();
         }
-        __shared__ int ws_slot;
-        const int slot = ws_claim(a, &ws_slot);
-        ok = false;
-        if (slot >= 0) {
-            Arena ag(ws_base(a, slot), a.ws_stride);
-            ok = spill ? stage1_assoc<VAR_BOTSORT>(a, s, L, ag, sh)
-                       : s1_lap_body(a, s, ag, sh.as.lap);
-        }
-        ws_release(a, slot);
+        Arena ag(redo_arena(a, s), a.ws_stride);
+        ok = spill ? stage1_assoc<VAR_BOTSORT>(a, s, L, ag, sh) : s1_lap_body(a, s, ag, sh.as.lap);
         if (!ok && t == 0) atomicOr(&c->err, ERR_EDGE_OVERFLOW);
     }
     block_sync();
@@ -1619,6 +1624,30 @@ __global__ __launch_bounds__(BLK1) void k_bs_lap(BtArgs a) {
         c->frame_id += 1;
         c->n_res1 = 0;   // a ByteTrack statistic (s1_lap_body sets it): 0, as the fused k_stage1
     }
+}
+__global__ __launch_bounds__(BLK1) void k_redo_bs_lap(BtArgs a) {
+    __shared__ StageShared sh;
+    const int t = threadIdx.x, nt = blockDim.x;
+    redo_drain(a, [&](int s, Arena &ag) {
+        BtCounters *c = a.cnt + s;
+        const long long tb = (long long)s * a.CAP, db = (long long)s * a.MAXD;
+        const int n_pool = c->n_pool, n_high = c->n_high;
+        const bool spill = c->bs_spill != 0;
+        const S1Lists L{c->n_dets, n_high, c->n_second, c->n_act, c->n_unc, n_pool, nullptr, nullptr};
+        if (!spill) {
+            for (int q = t; q < n_pool; q += nt) a.x1[tb + q] = -1;
+            for (int q = t; q < n_high; q += nt) a.y1[db + q] = -1;
+            block_sync();
+        }
+        const bool ok = spill ? stage1_assoc<VAR_BOTSORT>(a, s, L, ag, sh)
+                              : s1_lap_body(a, s, ag, sh.as.lap);
+        block_sync();
+        if (t == 0) {
+            if (!ok) atomicOr(&c->err, ERR_EDGE_OVERFLOW);
+            c->frame_id += 1;
+            c->n_res1 = 0;
+        }
+    });
 }
 
 // ------------------------------------------------------------------------------------ k_apply
@@ -2429,19 +2458,23 @@ __global__ __launch_bounds__(NT, NT == BLKF ? 4 : 1) void k_finish(BtArgs a) {
     if (need <= (long long)a.lds_bytes_f) {
         Arena ar(fsmem + bits_bytes, a.lds_bytes_f);
         finish_body<V>(a, s, bits, ar, sh);
-    } else {
+    } else {   // a global arena: here, or by k_redo_finish
         if (threadIdx.x == 0) a.cnt[s].n_fallback_f += 1;
-        __shared__ int ws_slot;
-        const int slot = ws_claim(a, &ws_slot);
-        if (slot >= 0) {
-            Arena ag(ws_base(a, slot), a.ws_stride);
+        if (redo_in_place(a, a.S)) {
+            Arena ag(redo_arena(a, s), a.ws_stride);
             finish_body<V>(a, s, bits, ag, sh);
-        } else {   // no arena within the bound: the frame's lists are not rebuilt (flagged)
-            if (threadIdx.x == 0) atomicOr(&a.cnt[s].err, ERR_EDGE_OVERFLOW);
+        } else if (threadIdx.x == 0) {
+            redo_queue(a, s);
         }
-        ws_release(a, slot);
     }
     YTA_BLK(5, 1);
+}
+template <int V, int NT>
+__global__ __launch_bounds__(NT) void k_redo_finish(BtArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char fsmem[];
+    __shared__ FinishShared sh;
+    unsigned *bits = reinterpret_cast<unsigned *>(fsmem);
+    redo_drain(a, [&](int s, Arena &ag) { finish_body<V>(a, s, bits, ag, sh); });
 }
 
 // Rebuild the free-slot list of every stream from its tracked + lost lists (after a reserve).
@@ -2521,8 +2554,19 @@ __global__ __launch_bounds__(OFFS_T) void k_out_offsets_scan(const BtCounters *c
 // device -> host copy, whose enqueue held the host until that stream drained (r05e:
 // yta_bytetrack_pipe_stats host_d2h_call_ms ~1.7-1.8 ms a frame).  tools/pcie_bench.hip: 55 GB/s
 // from 64 blocks, as the copy engines, and 88 GB/s beside a copy-engine host -> device copy.
-constexpr int ROWS_H_BLOCKS = 128;
-__global__ void k_nop() {}
+// Round 6 (traces: tools/pipe_timeline.py, tools/trace_dump.py, gpurun_out/r6d-r6s): with 128
+// blocks of plain stores, every other command completing while the rows streamed out took ~1 ms
+// longer (an empty kernel on the copy-in stream ran 1.1 ms; the event the compute stream waited on
+// behind it followed), so each frame's kernels started ~1.3 ms after their copy-in had ended;
+// with system-coherent write-through stores (sc0 sc1: no dirty host lines left in L2 for another
+// command's release to flush) the completions were prompt but the frame's first kernel ran
+// 1.7 ms beside them.  Fewer blocks keep fewer host stores in flight: 2048 streams, 3 frames in
+// flight, page-locked buffers, same box: 128 blocks 574 k calls/s, 64 620 k, 48 700 k, 32 750 k,
+// 24 743 k, 16 717 k, 8 605 k; 32 blocks with plain stores 563 k.
+constexpr int ROWS_H_BLOCKS = 32;
+#ifndef YTA_D2H_STORE
+#define YTA_D2H_STORE 2   // k_rows_to_host's stores: 0 plain, 1 nontemporal, 2 sc0 sc1, 3 sc0 sc1 nt
+#endif
 __global__ __launch_bounds__(1024) void k_copy_ints(const int *src, int *dst, int n) {
     for (int i = threadIdx.x; i < n; i += blockDim.x) dst[i] = src[i];
 }
@@ -2533,8 +2577,22 @@ __global__ __launch_bounds__(256) void k_rows_to_host(const double *src, const i
     const long long n = min((long long)off[S], limit) * 4;
     const int4 *s4 = reinterpret_cast<const int4 *>(src);
     for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
-         i += (long long)gridDim.x * blockDim.x)
+         i += (long long)gridDim.x * blockDim.x) {
+#if YTA_D2H_STORE >= 1
+        typedef int v4i __attribute__((ext_vector_type(4)));
+        const v4i v = reinterpret_cast<const v4i *>(s4)[i];
+        v4i *d = reinterpret_cast<v4i *>(dst) + i;
+#if YTA_D2H_STORE == 1
+        __builtin_nontemporal_store(v, d);
+#elif YTA_D2H_STORE == 2
+        asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(d), "v"(v) : "memory");
+#else
+        asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1 nt" ::"v"(d), "v"(v) : "memory");
+#endif
+#else
         dst[i] = s4[i];
+#endif
+    }
 }
 
 // Pipelined path: the frame's counters stored straight into mapped, coherent host memory (16-B
@@ -2640,50 +2698,14 @@ static bool pipe_off_kernel() {
     static const bool k = env_flag("YTA_PIPE_OFF_KERNEL", false);
     return k;
 }
-// The copy-in stream ends each frame with an empty kernel (k_nop) that the frame's completion
-// event follows (1, default), instead of the event directly after the copy engine's transfer
-// (YTA_PIPE_IN_FENCE=0)
-static bool pipe_in_kernel_fence() {
-    static const bool k = env_flag("YTA_PIPE_IN_FENCE", true);
+// k_rows_to_host's grid (YTA_PIPE_D2H_BLOCKS overrides ROWS_H_BLOCKS, for A/B runs)
+static int pipe_d2h_blocks() {
+    static const int k = [] {
+        const char *v = getenv("YTA_PIPE_D2H_BLOCKS");
+        const int b = v ? atoi(v) : ROWS_H_BLOCKS;
+        return b < 1 ? 1 : (b > 4096 ? 4096 : b);
+    }();
     return k;
-}
-// The pipelined path's host waits poll the event with hipEventQuery (1, default) instead of
-// blocking in hipEventSynchronize (YTA_PIPE_SPIN=0): traced (tools/pipe_timeline.py), a frame's
-// kernels - enqueued behind a wait on its copy-in's event - started only when the host made its
-// next HIP call (the next frame's copy-in enqueue), ~1.3 ms after the copy-in had ended; a host
-// thread blocked in a synchronize makes no such call
-static bool pipe_spin() {
-    static const bool k = env_flag("YTA_PIPE_SPIN", true);
-    return k;
-}
-// The copy-in's completion event with a device-scope release (1, default; YTA_PIPE_IN_DEVREL=0:
-// the default system scope, an L2 writeback + invalidate that waits behind k_rows_to_host's
-// stream of host stores - an empty kernel then took ~1 ms to complete, gpurun_out/r6g_pipe)
-static bool pipe_in_device_release() {
-    static const bool k = env_flag("YTA_PIPE_IN_DEVREL", true);
-    return k;
-}
-// An empty kernel enqueued right after each of the pipelined path's events (1, default;
-// YTA_PIPE_FLUSH=0 off): traced (gpurun_out/r6h_pipe), a frame's kernels waiting on its copy-in
-// event started only when the NEXT command on the copy-in stream ran, ~1.3 ms after the copy (and
-// the empty kernel before the event) had completed - as if the event's packet reached the copy-in
-// queue's hardware only with the next submission.  A dispatch behind it makes the queue advance.
-static bool pipe_flush_on() {
-    static const bool k = env_flag("YTA_PIPE_FLUSH", true);
-    return k;
-}
-static hipError_t pipe_flush(hipStream_t st) {
-    if (!pipe_flush_on()) return hipSuccess;
-    hipLaunchKernelGGL(k_nop, dim3(1), dim3(64), 0, st);
-    return hipGetLastError();
-}
-static hipError_t pipe_event_wait(hipEvent_t ev) {
-    if (!pipe_spin()) return hipEventSynchronize(ev);
-    for (;;) {
-        const hipError_t q = hipEventQuery(ev);
-        if (q != hipErrorNotReady) return q;
-        std::this_thread::yield();
-    }
 }
 // Rows device -> host by k_rows_to_host (1, default) or by the copy engines (YTA_PIPE_KERNEL_D2H=0)
 static bool pipe_kernel_d2h() {
@@ -3005,15 +3027,15 @@ int bt_alloc(yta_bytetrack *e) {
     a.ws_stride = (a.ws_stride + 255) & ~255LL;
     a.split23 = e->split23;
     a.ws3 = nullptr;
-    {   // pooled fallback arenas (ws_claim): enough for every block of a few-stream engine, a
+    {   // pooled fallback arenas (redo_drain): enough for every block of a few-stream engine, a
         // bounded pool for many streams (YTA_WS_POOL overrides the bound, 2..256)
         int pool = 32;
         if (const char *v = getenv("YTA_WS_POOL")) pool = std::max(2, std::min(256, atoi(v)));
         a.ws_slots = (int)std::min<long long>(S * (a.split23 ? 2 : 1), pool);
     }
     DALLOC(a.ws, (long long)a.ws_slots * a.ws_stride);
-    DALLOC(a.ws_bits, 4);
-    YTA_HIP(hipMemset(a.ws_bits, 0, 4 * sizeof(unsigned long long)));
+    DALLOC(a.redo_q, 2 + 2 * S);
+    YTA_HIP(hipMemset(a.redo_q, 0, 2 * sizeof(int)));
     a.slab.R = (int)CAP;
     a.slab.C = (int)MAXD;
     a.slab.i_stride = lap_slab_ints((int)CAP, (int)MAXD);
@@ -3061,8 +3083,13 @@ int set_lds_limits(size_t bytes) {
 }
 
 // One frame of every stream: 6 launches (ByteTrack), 4 + k_feat and k_ema (BoT-SORT, fused stage
-// 1).  Profiling marks bracket the phases s1_prep / s1_edges / s1_lap (BoT-SORT: k_feat + k_stage1,
+// 1); with more streams than pooled fallback arenas each association kernel is followed by its
+// redo kernel (ws_slots blocks that return at once unless a stream fell back).  Profiling marks bracket the phases s1_prep / s1_edges / s1_lap (BoT-SORT: k_feat + k_stage1,
 // empty, empty), stage23, apply (k_apply + k_ema), finish.
+// a launch of more association blocks than pooled arenas queues its fallbacks for a redo kernel
+// (redo_in_place on the device)
+static bool redo_launch(const BtArgs &a, int blocks) { return blocks > a.ws_slots; }
+
 template <int V>
 int launch_frame(yta_bytetrack *e) {
     BtArgs &a = e->a;
@@ -3090,10 +3117,14 @@ int launch_frame(yta_bytetrack *e) {
             hipLaunchKernelGGL(k_s1_edges<BLKE>, dim3(a.S), dim3(BLKE), a.lds_bytes_e, e->stream, a);
         YTA_HIP(hipGetLastError());
         MARK();
-        if (e->split23)
+        if (e->split23) {
             hipLaunchKernelGGL(k_s1_lap<1024>, dim3(a.S), dim3(1024), a.lds_bytes_l, e->stream, a);
-        else
+            if (redo_launch(a, a.S))
+                hipLaunchKernelGGL(k_redo_s1_lap<1024>, dim3(a.ws_slots), dim3(1024), 0, e->stream, a);
+        } else {
             hipLaunchKernelGGL(k_s1_lap<BLKL>, dim3(a.S), dim3(BLKL), a.lds_bytes_l, e->stream, a);
+            hipLaunchKernelGGL(k_redo_s1_lap<BLKL>, dim3(a.ws_slots), dim3(BLKL), 0, e->stream, a);
+        }
     } else if (bs) {   // split stage 1 (k_bs_*): few streams
         hipLaunchKernelGGL(k_bs_prep, dim3(a.S + a.S * feat_blocks(a.MAXD, BS_PREP_T)),
                            dim3(BS_PREP_T), 0, e->stream, a);
@@ -3104,20 +3135,31 @@ int launch_frame(yta_bytetrack *e) {
         YTA_HIP(hipGetLastError());
         MARK();
         hipLaunchKernelGGL(k_bs_lap, dim3(a.S), dim3(BLK1), a.lds_bytes, e->stream, a);
+        if (redo_launch(a, a.S))
+            hipLaunchKernelGGL(k_redo_bs_lap, dim3(a.ws_slots), dim3(BLK1), 0, e->stream, a);
     } else {   // fused stage 1: the whole stage in the first phase, the next two empty
         hipLaunchKernelGGL(k_stage1<V>, dim3(a.S), dim3(BLK1), a.lds_bytes, e->stream, a);
+        if (redo_launch(a, a.S))
+            hipLaunchKernelGGL(k_redo_stage1<V>, dim3(a.ws_slots), dim3(BLK1), 0, e->stream, a);
         YTA_HIP(hipGetLastError());
         MARK();
         MARK();
     }
     YTA_HIP(hipGetLastError());
     MARK();
-    if (a.split23)
+    if (a.split23) {
         hipLaunchKernelGGL((k_stage23<V, true>), dim3(2 * a.S), dim3(BLK23S), a.lds_bytes23,
                            e->stream, a);
-    else
+        if (redo_launch(a, 2 * a.S))
+            hipLaunchKernelGGL((k_redo_stage23<V, true>), dim3(a.ws_slots), dim3(BLK23S), 0,
+                               e->stream, a);
+    } else {
         hipLaunchKernelGGL((k_stage23<V, false>), dim3(a.S), dim3(BLK23), a.lds_bytes23,
                            e->stream, a);
+        if (redo_launch(a, a.S))
+            hipLaunchKernelGGL((k_redo_stage23<V, false>), dim3(a.ws_slots), dim3(BLK23), 0,
+                               e->stream, a);
+    }
     YTA_HIP(hipGetLastError());
     MARK();
     const dim3 gt((a.CAP + APPLY_T - 1) / APPLY_T, a.S);
@@ -3135,9 +3177,15 @@ int launch_frame(yta_bytetrack *e) {
         constexpr int FT = 1024;
         hipLaunchKernelGGL((k_finish<V, FT>), dim3(a.S + (bs ? a.S * ema_blocks(a.CAP, FT) : 0)),
                            dim3(FT), bits_bytes + a.lds_bytes_f, e->stream, a);
+        if (redo_launch(a, a.S))
+            hipLaunchKernelGGL((k_redo_finish<V, FT>), dim3(a.ws_slots), dim3(FT), bits_bytes,
+                               e->stream, a);
     } else {
         hipLaunchKernelGGL((k_finish<V, BLKF>), dim3(a.S + (bs ? a.S * ema_blocks(a.CAP, BLKF) : 0)),
                            dim3(BLKF), bits_bytes + a.lds_bytes_f, e->stream, a);
+        if (redo_launch(a, a.S))
+            hipLaunchKernelGGL((k_redo_finish<V, BLKF>), dim3(a.ws_slots), dim3(BLKF), bits_bytes,
+                               e->stream, a);
     }
     YTA_HIP(hipGetLastError());
     MARK();
@@ -3752,14 +3800,7 @@ int pipe_slot_ready(yta_bytetrack *e, yta_bytetrack::PipeSlot &p, long long dets
     }
     if (!p.s_in) p.s_in = e->s_in;
     if (!p.in_done) {
-        // in_done is waited on by the compute stream only (device work reading device memory): a
-        // device-scope release; kern_done / out_done are also waited on by the host, which then
-        // reads what the kernels stored into mapped host memory: the default system scope
-        YTA_HIP(hipEventCreateWithFlags(&p.in_done, hipEventDisableTiming |
-                                                        (pipe_in_device_release()
-                                                             ? hipEventReleaseToDevice
-                                                             : 0u)));
-        for (hipEvent_t *ev : {&p.kern_done, &p.out_done})
+        for (hipEvent_t *ev : {&p.in_done, &p.kern_done, &p.out_done})
             YTA_HIP(hipEventCreateWithFlags(ev, hipEventDisableTiming));
         if (pipe_timing())
             for (hipEvent_t &ev : p.t_ev) YTA_HIP(hipEventCreateWithFlags(&ev, hipEventDefault));
@@ -3848,18 +3889,8 @@ int pipe_enqueue_in(yta_bytetrack *e, yta_bytetrack::PipeSlot &p, const double *
         }
     }
     e->pstat[p.direct_in ? PS_IN_DIRECT : PS_IN_STAGED] += (double)p.in_bytes;
-    if (pipe_in_kernel_fence()) {
-        // the copy-in stream ends with an empty kernel, so in_done completes when the copy does:
-        // traced (tools/pipe_timeline.py, gpurun_out/r6d_pipe, r6f_pipe) an event recorded right
-        // after the copy engine's transfer completed only when the NEXT command on the copy-in
-        // stream ran (the next frame's offsets copy, a blit kernel) - ~1.3 ms later, the frame's
-        // kernels waiting on it that long
-        hipLaunchKernelGGL(k_nop, dim3(1), dim3(64), 0, p.s_in);
-        YTA_HIP(hipGetLastError());
-    }
     if (p.t_ev[1]) YTA_HIP(hipEventRecord(p.t_ev[1], p.s_in));
     YTA_HIP(hipEventRecord(p.in_done, p.s_in));
-    YTA_HIP(pipe_flush(p.s_in));
     return YTA_OK;
 }
 
@@ -3900,7 +3931,6 @@ int pipe_enqueue_run(yta_bytetrack *e, yta_bytetrack::PipeSlot &p, const long lo
     YTA_HIP(hipGetLastError());
     if (p.t_ev[3]) YTA_HIP(hipEventRecord(p.t_ev[3], e->stream));
     YTA_HIP(hipEventRecord(p.kern_done, e->stream));
-    YTA_HIP(pipe_flush(e->stream));
     // copy-out stream: counters, offsets and at most det_offsets[S] rows (every output row is a
     // track matched to or born from one of the frame's detections)
     YTA_HIP(hipStreamWaitEvent(e->s_out, p.kern_done, 0));
@@ -3917,7 +3947,7 @@ int pipe_enqueue_run(yta_bytetrack *e, yta_bytetrack::PipeSlot &p, const long lo
         const auto t0 = std::chrono::steady_clock::now();
         void *dst_dev = p.direct_out ? out_dev : (void *)p.m_pack;
         if (pipe_kernel_d2h() && dst_dev) {   // the rows stored by a kernel (k_rows_to_host)
-            hipLaunchKernelGGL(k_rows_to_host, dim3(ROWS_H_BLOCKS), dim3(256), 0, e->s_out,
+            hipLaunchKernelGGL(k_rows_to_host, dim3(pipe_d2h_blocks()), dim3(256), 0, e->s_out,
                                p.d_pack, p.d_pack_off, S, total, (int4 *)dst_dev);
             YTA_HIP(hipGetLastError());
         } else {
@@ -3930,7 +3960,6 @@ int pipe_enqueue_run(yta_bytetrack *e, yta_bytetrack::PipeSlot &p, const long lo
     }
     if (p.t_ev[5]) YTA_HIP(hipEventRecord(p.t_ev[5], e->s_out));
     YTA_HIP(hipEventRecord(p.out_done, e->s_out));
-    YTA_HIP(pipe_flush(e->s_out));
     return YTA_OK;
 }
 
@@ -3979,7 +4008,7 @@ int pipe_capacity(yta_bytetrack *e, const int *det_offsets) {
         }
         if (fits(k0)) return YTA_OK;
         if (k0 != e->pipe_count - 1) {
-            YTA_HIP(pipe_event_wait(slot(e->pipe_count - 1).kern_done));
+            YTA_HIP(hipEventSynchronize(slot(e->pipe_count - 1).kern_done));
             ++e->pstat[PS_CAP_WAITS];
             if (fits(e->pipe_count - 1)) return YTA_OK;
         }
@@ -4048,7 +4077,7 @@ int pipe_collect(yta_bytetrack *e, long long *next_id, int *out_offsets) {
     e->pipe_head = (e->pipe_head + 1) % PIPE_DEPTH;
     --e->pipe_count;
     const auto t0 = std::chrono::steady_clock::now();
-    YTA_HIP(pipe_event_wait(p.out_done));
+    YTA_HIP(hipEventSynchronize(p.out_done));
     const auto t1 = std::chrono::steady_clock::now();
     e->pstat[PS_WAIT_MS] += std::chrono::duration<double, std::milli>(t1 - t0).count();
     if (p.t_ev[0]) {   // the frame's GPU-side phases from its timing events (all complete)

@@ -117,10 +117,11 @@ struct BtArgs {
     int split23;
     unsigned char *ws3;       // unused (round 6: the stage-3 block claims from the pool below)
     // the global fallback arenas are a pool of ws_slots arenas of ws_stride bytes shared by the
-    // engine's streams (a block claims one when its LDS arena is too small, bytetrack.hip
-    // ws_claim): worst-case arenas for every stream cost O(S * CAP * MAXD) bytes of HBM
+    // engine's streams: a block whose LDS arena is too small queues its stream in redo_q and the
+    // launch's redo kernel (bytetrack.hip k_redo_*, ws_slots blocks) redoes it over arena
+    // blockIdx.x; worst-case arenas for every stream cost O(S * CAP * MAXD) bytes of HBM
     int ws_slots;
-    unsigned long long *ws_bits;   // [4] claimed-arena bitmap
+    int *redo_q;              // [2 + 2S]: queued count, redo blocks done, queued block ids
     LapSlab slab;             // per stream: (threads / 64) slabs
     // ByteTrack stage 1 as three launches (k_s1_prep / k_s1_edges / k_s1_lap): the per-stream
     // grid over the high detections and every pool row's first candidate edges, in HBM
