@@ -905,13 +905,17 @@ def main():
             pcie["pinned"] = {k: pp[k] for k in ("value", "ms_per_step", "ms_per_step_all")}
             pcie["pinned"]["note"] = pp["note"]
         if pcie is not None:
-            pcie["pipelined"] = pcie_pipelined(frame_of, S, N, local_rank,
-                                               first=min(PRE, FT - 8))
+            # 16 timed frames: the loop's fill and drain (two frames' latency not overlapped) are
+            # charged to fewer frames at 8 (tools/pipe_frames_ab.sh, gpurun_out/r6w: 711 k at 8,
+            # 756 k at 16, page-locked)
+            PF = min(16, FT)
+            pf0 = min(PRE, FT - PF)
+            pcie["pipelined"] = pcie_pipelined(frame_of, S, N, local_rank, first=pf0, frames=PF)
             if not args.no_pcie_pinned:
                 pcie["pipelined"]["pinned"] = pcie_pipelined(frame_of, S, N, local_rank,
-                                                             first=min(PRE, FT - 8), pinned=True)
+                                                             first=pf0, frames=PF, pinned=True)
                 pcie["pipelined"]["pinned_f32"] = pcie_pipelined(
-                    frame_of, S, N, local_rank, first=min(PRE, FT - 8), pinned=True, f32=True)
+                    frame_of, S, N, local_rank, first=pf0, frames=PF, pinned=True, f32=True)
         dropin = None if args.no_dropin else dropin_leg(N, 60, args.seed, f"cuda:{local_rank}")
         configs = None if args.no_configs else configs_leg(None if world == 1 else ["C2", "C3"])
         if multi_cfg:

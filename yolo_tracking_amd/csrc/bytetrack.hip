@@ -2682,6 +2682,10 @@ static bool env_flag(const char *name, bool dflt) {
     const char *v = getenv(name);
     return v ? atoi(v) != 0 : dflt;
 }
+static int env_int(const char *name, int dflt) {
+    const char *v = getenv(name);
+    return v ? atoi(v) : dflt;
+}
 // Per-frame GPU timing events of the pipelined path (yta_bytetrack_pipe_stats' GPU columns)
 static bool pipe_timing() {
     static const bool k = env_flag("YTA_PIPE_TIMING", false);
@@ -2691,6 +2695,23 @@ static bool pipe_timing() {
 static bool pipe_slot_streams() {
     static const bool k = env_flag("YTA_PIPE_SLOT_STREAMS", false);
     return k;
+}
+// The copy-in / copy-out streams at the device's greatest stream priority (YTA_PIPE_PRIO: bit 0
+// copy-in, bit 1 copy-out; default 3 = both).  The HIP runtime maps a process's streams onto at
+// most GPU_MAX_HW_QUEUES hardware queues per priority (4 on the pool) and, past that, shares the
+// least-used one.  In bench.py's process (two headline engines alive) the pipelined engine's
+// streams shared queues: a frame's copy-in waited behind the previous frame's kernels and
+// k_rows_to_host's ~2.4 ms of host stores ran beside nothing - 535 k calls/s page-locked against
+// 711 k with GPU_MAX_HW_QUEUES=8.  The greater priority draws from its own pool of queues, which
+// no compute stream uses (gpurun_out/r6z2: both 710 k, copy-out alone 534 k, a dedicated queue
+// per stream through an every-CU mask 708 k).
+static hipError_t pipe_stream_create(hipStream_t *st, int which) {
+    static const int prio = env_int("YTA_PIPE_PRIO", 3);
+    if (!(prio & (1 << which))) return hipStreamCreateWithFlags(st, hipStreamNonBlocking);
+    int lo = 0, hi = 0;
+    const hipError_t r = hipDeviceGetStreamPriorityRange(&lo, &hi);
+    if (r != hipSuccess) return r;
+    return hipStreamCreateWithPriority(st, hipStreamNonBlocking, hi);
 }
 // A frame's detection offsets read by the compute stream from the slot's mapped host copy
 // (k_copy_ints) instead of a small copy on the copy-in stream
@@ -3791,12 +3812,12 @@ void pipe_free(yta_bytetrack *e) {
 int pipe_slot_ready(yta_bytetrack *e, yta_bytetrack::PipeSlot &p, long long dets) {
     const int S = e->S;
     if (!p.s_in && pipe_slot_streams()) {
-        YTA_HIP(hipStreamCreateWithFlags(&p.s_in, hipStreamNonBlocking));
+        YTA_HIP(pipe_stream_create(&p.s_in, 0));
         p.own_s_in = true;
     }
     if (!e->s_in) {
-        YTA_HIP(hipStreamCreateWithFlags(&e->s_in, hipStreamNonBlocking));
-        YTA_HIP(hipStreamCreateWithFlags(&e->s_out, hipStreamNonBlocking));
+        YTA_HIP(pipe_stream_create(&e->s_in, 0));
+        YTA_HIP(pipe_stream_create(&e->s_out, 1));
     }
     if (!p.s_in) p.s_in = e->s_in;
     if (!p.in_done) {
