@@ -3109,7 +3109,10 @@ int set_lds_limits(size_t bytes) {
 // empty, empty), stage23, apply (k_apply + k_ema), finish.
 // a launch of more association blocks than pooled arenas queues its fallbacks for a redo kernel
 // (redo_in_place on the device)
-static bool redo_launch(const BtArgs &a, int blocks) { return blocks > a.ws_slots; }
+#ifndef YTA_REDO_LAUNCH
+#define YTA_REDO_LAUNCH 1   // 0: an A/B build without the redo launches (unsafe if a stream falls back)
+#endif
+static bool redo_launch(const BtArgs &a, int blocks) { return YTA_REDO_LAUNCH && blocks > a.ws_slots; }
 
 template <int V>
 int launch_frame(yta_bytetrack *e) {
@@ -3144,7 +3147,8 @@ int launch_frame(yta_bytetrack *e) {
                 hipLaunchKernelGGL(k_redo_s1_lap<1024>, dim3(a.ws_slots), dim3(1024), 0, e->stream, a);
         } else {
             hipLaunchKernelGGL(k_s1_lap<BLKL>, dim3(a.S), dim3(BLKL), a.lds_bytes_l, e->stream, a);
-            hipLaunchKernelGGL(k_redo_s1_lap<BLKL>, dim3(a.ws_slots), dim3(BLKL), 0, e->stream, a);
+            if (YTA_REDO_LAUNCH)
+                hipLaunchKernelGGL(k_redo_s1_lap<BLKL>, dim3(a.ws_slots), dim3(BLKL), 0, e->stream, a);
         }
     } else if (bs) {   // split stage 1 (k_bs_*): few streams
         hipLaunchKernelGGL(k_bs_prep, dim3(a.S + a.S * feat_blocks(a.MAXD, BS_PREP_T)),
