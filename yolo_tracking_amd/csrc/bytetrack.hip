@@ -1942,6 +1942,7 @@ __global__ __launch_bounds__(APPLY_T) void k_apply(BtArgs a) {
 struct FinishShared {
     GridScratch gs;
     int wsum[32];
+    int cur;   // the free list's cyclic start (read before the old list is overwritten)
 };
 
 // lost' float boxes (by position) + a grid of ids over them (cell starts, ids, big list)
@@ -1962,11 +1963,17 @@ struct SlotFlags {
 
 template <int V>
 __device__ __forceinline__ void finish_body(const BtArgs &a, int s, unsigned *bits, Arena &ar,
-                                            FinishShared &sh) {
+                                            FinishShared &sh, bool lds_ar) {
     int *wsum = sh.wsum;
     const int t = threadIdx.x, nt = blockDim.x;
     BtCounters *c = a.cnt + s;
     const long long tb = (long long)s * a.CAP, db = (long long)s * a.MAXD;
+    // Barriers: the compactions' scans hand off LDS only (GSYNC false); the global lists and
+    // records this kernel writes and reads back are handed over at two block_syncs, before the
+    // duplicate removal (births' records and flags, t2, l2, l2pos, expiry flags) and before the
+    // output rows (tracked, unc, lost, t2 when the slot list is not in the arena).  A block_sync
+    // waits for every outstanding store of the block - a memory round trip per barrier on a
+    // one-stream frame's chain.  lds_ar: the arena is LDS.
     const int fid = c->frame_id;
     const int n_tracked = c->n_tracked, n_lost = c->n_lost;
     const int n_rest = c->n_rest, n_left = c->n_left, n_free = c->n_free;
@@ -1988,7 +1995,7 @@ __device__ __forceinline__ void finish_body(const BtArgs &a, int s, unsigned *bi
     int2 *bstage = V == VAR_BOTSORT && a.D > 0 && ar.cap >= (size_t)8 * (n_rest > 0 ? n_rest : 1)
                        ? reinterpret_cast<int2 *>(ar.base)
                        : nullptr;
-    const int n_births_all = block_compact_ld<4>(
+    const int n_births_all = block_compact_ld<4, false>(
         n_rest, wsum,
         [&](int j) {
             RestItem r;
@@ -2035,7 +2042,8 @@ __device__ __forceinline__ void finish_body(const BtArgs &a, int s, unsigned *bi
         n_births = n_free;
     }
     if (V == VAR_BOTSORT && a.D > 0 && bstage) {   // smooth_feat of a birth = its curr_feat
-        block_sync();
+        if (lds_ar) lds_sync();
+        else block_sync();
         if ((a.D & 3) == 0) {   // 16-B pieces: rows of D floats stay 16-B aligned
             const int D4 = a.D >> 2;
             struct Piece {
@@ -2065,7 +2073,8 @@ __device__ __forceinline__ void finish_body(const BtArgs &a, int s, unsigned *bi
                 },
                 [&](int q, float v) { a.feat[(tb + bstage[q / a.D].x) * a.D + q % a.D] = v; });
         }
-        block_sync();   // the arena is the dedup grid's next
+        if (lds_ar) lds_sync();   // the arena is the dedup grid's next
+        else block_sync();
     } else if (V == VAR_BOTSORT && a.D > 0) {
         block_sync();
         const int lane = lane_id(), nw = nt / WAVE;
@@ -2079,7 +2088,7 @@ __device__ __forceinline__ void finish_body(const BtArgs &a, int s, unsigned *bi
     YTA_STAMP(2);
     // tracked' = [Tracked survivors of tracked_stracks] ++ births ++ re-found (:257-261)
     auto with_flags = [&](int, int slot) { return SlotFlags{slot, a.flags[tb + slot]}; };
-    int n_t2 = block_compact_ld<8>(
+    int n_t2 = block_compact_ld<8, false>(
         n_tracked, wsum, [&](int i) { return a.tracked[tb + i]; }, with_flags,
         [&](int, const SlotFlags &v) { return st_of(v.flags) == ST_TRACKED; },
         [&](int, const SlotFlags &v, int pos) { a.t2[tb + pos] = v.slot; });
@@ -2099,7 +2108,7 @@ __device__ __forceinline__ void finish_body(const BtArgs &a, int s, unsigned *bi
     struct LostItem {
         int slot, flags, frame;
     };
-    int n_l2 = block_compact_ld<8>(
+    int n_l2 = block_compact_ld<8, false>(
         n_lost, wsum, [&](int i) { return a.lost[tb + i]; },
         [&](int, int sl) {
             LostItem v;
@@ -2125,7 +2134,7 @@ __device__ __forceinline__ void finish_body(const BtArgs &a, int s, unsigned *bi
         int x2, pos;
         SlotFlags sf;
     };
-    n_l2 += block_compact_ld<4>(
+    n_l2 += block_compact_ld<4, false>(
         n_left, wsum,
         [&](int i) {
             LeftItem v;
@@ -2284,7 +2293,7 @@ __device__ __forceinline__ void finish_body(const BtArgs &a, int s, unsigned *bi
             }
         }
         int tot;   // counts <= 8 * 1024 each: 16 bits apiece
-        const int ex = block_exclusive_scan(__popc(keep) | (__popc(outb) << 16), wsum, &tot);
+        const int ex = block_exclusive_scan<false>(__popc(keep) | (__popc(outb) << 16), wsum, &tot);
         int pk = n_tr + (ex & 0xFFFF), po = n_out + (ex >> 16);
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
@@ -2304,13 +2313,19 @@ __device__ __forceinline__ void finish_body(const BtArgs &a, int s, unsigned *bi
         n_tr += tot & 0xFFFF;
         n_out += tot >> 16;
     }
-    const int n_lo = block_compact_ld<8>(
+    const int n_lo = block_compact_ld<8, false>(
         n_l2, wsum, [&](int q) { return a.l2[tb + q]; }, [&](int, int slot) { return slot; },
         [&](int q, int) { return !((dropB[q >> 5] >> (q & 31)) & 1u); },
         [&](int, int slot, int pos) {
             a.lost[tb + pos] = slot;
             atomicOr(&live[slot >> 5], 1u << (slot & 31));
         });
+    // free slots below start in cyclic order from the slot after this frame's last birth: births
+    // then take ascending slots across frames, so the tracked list (survivors in order, births
+    // appended) stays sorted by slot up to a rotation, and the record gathers of k_s1_prep /
+    // k_apply / k_finish walk memory in (gapped) ascending order instead of at random.  Read here,
+    // so that only LDS is handed over between the output rows and the free-list pass.
+    if (t == 0) sh.cur = n_births > 0 ? (a.free_list[tb + n_births - 1] + 1) % a.CAP : c->slot_cursor;
     block_sync();
     YTA_STAMP(7);
     double *out = a.out + tb * 8;
@@ -2385,13 +2400,10 @@ __device__ __forceinline__ void finish_body(const BtArgs &a, int s, unsigned *bi
             [&](int pos, const Row &r) { put_row(pos, r.b, r.m); });
     }
     YTA_STAMP(8);
-    // free slots in cyclic order from the slot after this frame's last birth: births then take
-    // ascending slots across frames, so the tracked list (survivors in order, births appended)
-    // stays sorted by slot up to a rotation, and the record gathers of k_s1_prep / k_apply /
-    // k_finish walk memory in (gapped) ascending order instead of at random
-    const int cur0 = c->slot_cursor;
-    const int cur = n_births > 0 ? (a.free_list[tb + n_births - 1] + 1) % a.CAP : cur0;
-    block_sync();   // every thread read the old free list above
+    // every read of the old free list was consumed before the block_sync above (births, t2,
+    // sh.cur); the live bits are LDS
+    lds_sync();
+    const int cur = sh.cur;
     const int n_fr = block_compact<false>(
         a.CAP, wsum,
         [&](int i) {
@@ -2457,12 +2469,12 @@ __global__ __launch_bounds__(NT, NT == BLKF ? 4 : 1) void k_finish(BtArgs a) {
     YTA_BLK(5, 0);
     if (need <= (long long)a.lds_bytes_f) {
         Arena ar(fsmem + bits_bytes, a.lds_bytes_f);
-        finish_body<V>(a, s, bits, ar, sh);
+        finish_body<V>(a, s, bits, ar, sh, true);
     } else {   // a global arena: here, or by k_redo_finish
         if (threadIdx.x == 0) a.cnt[s].n_fallback_f += 1;
         if (redo_in_place(a, a.S)) {
             Arena ag(redo_arena(a, s), a.ws_stride);
-            finish_body<V>(a, s, bits, ag, sh);
+            finish_body<V>(a, s, bits, ag, sh, false);
         } else if (threadIdx.x == 0) {
             redo_queue(a, s);
         }
@@ -2474,7 +2486,7 @@ __global__ __launch_bounds__(NT) void k_redo_finish(BtArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char fsmem[];
     __shared__ FinishShared sh;
     unsigned *bits = reinterpret_cast<unsigned *>(fsmem);
-    redo_drain(a, [&](int s, Arena &ag) { finish_body<V>(a, s, bits, ag, sh); });
+    redo_drain(a, [&](int s, Arena &ag) { finish_body<V>(a, s, bits, ag, sh, false); });
 }
 
 // Rebuild the free-slot list of every stream from its tracked + lost lists (after a reserve).
