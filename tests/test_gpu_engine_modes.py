@@ -158,3 +158,55 @@ def test_fallback_pool_under_contention(monkeypatch):
             assert np.array_equal(a[s].view(np.int64), b[s].view(np.int64)), (f, s)
     st = eng.stats()
     assert st["fallback1"] >= S * (F - 1) and st["fallback23"] >= S * F, st
+
+
+BS_P = dict(track_high_thresh=0.5, track_low_thresh=0.1, new_track_thresh=0.6, track_buffer=30,
+            match_thresh=0.8, proximity_thresh=0.5, appearance_thresh=0.25, frame_rate=30)
+
+
+@pytest.mark.parametrize("case", ["bytetrack_split", "botsort_reid", "botsort_fused",
+                                  "botsort_split23_off"])
+def test_redo_kernels_every_variant(monkeypatch, case):
+    """The redo kernels of every association kernel variant (bytetrack.hip k_redo_s1_lap<1024>,
+    k_redo_stage23<V, true / false>, k_redo_finish<V, 1024 / 256>, k_redo_bs_lap,
+    k_redo_stage1<BoT-SORT>): ten streams, a pool of two arenas (YTA_WS_POOL=2, so every launch
+    has more blocks than arenas and queues), the LDS budget 0 (every stream-frame falls back):
+    rows bit-identical to the same engine kind on its LDS arenas, frame by frame.  bytetrack_split:
+    the few-stream mode's split stage 2 / 3 and 1024-thread stage-1 / finish blocks;
+    botsort_reid: split stage 1 (k_bs_lap) with 32-d embeddings; botsort_fused: the fused
+    k_stage1 (YTA_BS_SPLIT=0); botsort_split23_off: one block per stream for stages 2 / 3."""
+    from test_oracle_golden import reid_features
+    from yolo_tracking_amd.trackers.botsort import BoTSORTEngine
+    S, F, n, D = 10, 12, 300, 32
+    bot = case.startswith("botsort")
+    streams = [make_frames(n, F, 2600 + s, emb_dim=D if bot else 0) for s in range(S)]
+    env = {"bytetrack_split": {"YTA_SPLIT23": "1"},
+           "botsort_reid": {"YTA_SPLIT23": "1", "YTA_BS_SPLIT": "1"},
+           "botsort_fused": {"YTA_SPLIT23": "1", "YTA_BS_SPLIT": "0"},
+           "botsort_split23_off": {"YTA_SPLIT23": "0", "YTA_BS_SPLIT": "1"}}[case]
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+
+    def make():
+        if bot:
+            return BoTSORTEngine(S, feat_dim=D, track_capacity=512, max_dets=n, **BS_P)
+        return ByteTrackEngine(S, track_capacity=512, max_dets=n, **KW)
+    ref = make()
+    monkeypatch.setenv("YTA_WS_POOL", "2")
+    eng = make()
+    assert modes(eng)["ws_slots"] == 2
+    assert modes(eng)["split23"] == int(env["YTA_SPLIT23"])
+    eng.set_lds(0)
+    for f in range(F):
+        dets = [streams[s][f][0] for s in range(S)]
+        if bot:
+            feats = [reid_features(dets[s], streams[s][f][1], BS_P["track_high_thresh"])
+                     for s in range(S)]
+            a, b = eng.update(dets, feats), ref.update(dets, feats)
+        else:
+            a, b = eng.update(dets), ref.update(dets)
+        for s in range(S):
+            assert np.array_equal(a[s].view(np.int64), b[s].view(np.int64)), (case, f, s)
+    st = eng.stats()   # every association that needed an arena ran on a pooled one
+    assert st["fallback1"] > 0 and st["fallback23"] > 0, st
+    assert st["fallback_f"] >= S * (F - 1), st
