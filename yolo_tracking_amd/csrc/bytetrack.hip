@@ -1474,6 +1474,11 @@ __global__ __launch_bounds__(BS_PREP_T) void k_bs_prep(BtArgs a) {
         a.cnt[s].bs_spill = 0;
         a.cnt[s].n_edges[0] = 0;
     }
+    // stage 1's results start unmatched (s1_lap_body writes only the residual matches; the fused
+    // association, taken on a spill, writes every entry): cleared here, off k_bs_lap's chain
+    const long long tb = (long long)s * a.CAP, db = (long long)s * a.MAXD;
+    for (int q = threadIdx.x; q < L.n_pool; q += blockDim.x) a.x1[tb + q] = -1;
+    for (int q = threadIdx.x; q < L.n_high; q += blockDim.x) a.y1[db + q] = -1;
 }
 
 // A pool row's pairs that need the appearance cost (inside proximity_thresh) are queued per wave
@@ -1596,11 +1601,7 @@ __global__ __launch_bounds__(BLK1) void k_bs_lap(BtArgs a) {
     const int n_pool = c->n_pool, n_high = c->n_high;
     const bool spill = c->bs_spill != 0;
     const S1Lists L{c->n_dets, n_high, c->n_second, c->n_act, c->n_unc, n_pool, nullptr, nullptr};
-    if (!spill) {   // s1_lap_body writes only the residual matches
-        for (int q = t; q < n_pool; q += nt) a.x1[tb + q] = -1;
-        for (int q = t; q < n_high; q += nt) a.y1[db + q] = -1;
-        block_sync();
-    }
+    // x1 / y1 were cleared by k_bs_prep
     Arena ar(smem, a.lds_bytes);
     bool ok = spill ? stage1_assoc<VAR_BOTSORT>(a, s, L, ar, sh) : s1_lap_body(a, s, ar, sh.as.lap);
     if (!ok) {   // a global arena: here, or by k_redo_bs_lap (which then advances the frame)
