@@ -707,13 +707,18 @@ def run_config(args, world, rank, local_rank):
     DeepOCSORT stream of 2048 x 2048 + CMC per GPU, C5: eight HybridSORT streams of 4096 x 4096 per
     GPU; 8 GPUs = the config as stated), one JSON line on rank 0."""
     import torch
+    if args.shared_gpu:   # rehearsal: ranks share the box's card(s), gloo between them
+        local_rank = local_rank % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local_rank)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if args.shared_gpu:   # RCCL refuses two ranks on one device
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
     line = config_shard_leg(args.tracker, args.n, args.dim, args.streams, args.steps, args.warmup,
-                            args.seed, world, rank, dist, "cuda",
+                            args.seed, world, rank, dist, "cpu" if args.shared_gpu else "cuda",
                             cpu=world == 1 and not args.no_cpu_baseline)
     if rank == 0:
         line.update(higher_is_better=True, vs_baseline=None, dtype="f64", data="synthetic",
