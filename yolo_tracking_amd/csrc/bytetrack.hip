@@ -2433,6 +2433,7 @@ __device__ __forceinline__ void finish_body(const BtArgs &a, int s, unsigned *bi
             c->n_unc = n_tr - n_out;
             c->n_pool = n_out + n_lo;
         }
+        if (a.cnt_mirror) a.cnt_mirror[s] = *c;   // every field above is final
     }
 }
 
@@ -3019,7 +3020,7 @@ int bt_alloc(yta_bytetrack *e) {
     DALLOC(a.y1, S * MAXD);
     DALLOC(a.y2, S * MAXD);
     DALLOC(a.y3, S * MAXD);
-    DALLOC(a.out, S * CAP * 8);
+    DALLOC(a.out, S * CAP * 8 + 16 * S);   // + the counters' mirror (BtArgs::cnt_mirror)
     e->out_own = a.out;
     if (e->variant == VAR_BOTSORT) {
         DALLOC(a.cls_hist, S * CAP * CLS_K);
@@ -3649,17 +3650,35 @@ int update_host(yta_bytetrack *e, const double *dets, const int *det_offsets, co
         rc = ensure_pack(e, worst);
         if (rc) return rc;
     }
+    // one stream: its rows already start at row 0 of out_own, so the packing launches (two
+    // dependent kernels on a one-camera frame's chain, ~9 us) are skipped, and k_finish mirrors
+    // the counters right after the rows, so one copy returns both
+    const bool one = small && S == 1 && !active;
+    if (one) {
+        rc = ensure_pack(e, worst + 2);
+        if (rc) return rc;
+    }
+    e->a.cnt_mirror = one ? reinterpret_cast<BtCounters *>(e->out_own + worst * 8) : nullptr;
     auto device_work = [&]() -> int {   // the frame's launches (+ packing and copies back)
         int r = launch_pipeline(e, e->d_det_in, e->d_det_off, e->out_own, nullptr, e->d_feat_in);
         if (r || !small) return r;
-        hipLaunchKernelGGL(k_out_offsets, dim3(1), dim3(64), 0, e->stream, e->a.cnt, S,
-                           e->CAP, e->d_pack_off);
-        hipLaunchKernelGGL(k_pack_out, dim3(S), dim3(256), 0, e->stream, e->out_own,
-                           (long long)e->CAP, e->d_pack_off, e->d_pack, e->pack_cap);
-        YTA_HIP(hipGetLastError());
+        if (one) {
+            YTA_HIP(hipMemcpyAsync(e->h_pack, e->out_own, sizeof(double) * 8 * (worst + 2),
+                                   hipMemcpyDeviceToHost, e->stream));
+            return YTA_OK;
+        }
+        const double *src = e->out_own;
+        if (S > 1) {
+            hipLaunchKernelGGL(k_out_offsets, dim3(1), dim3(64), 0, e->stream, e->a.cnt, S,
+                               e->CAP, e->d_pack_off);
+            hipLaunchKernelGGL(k_pack_out, dim3(S), dim3(256), 0, e->stream, e->out_own,
+                               (long long)e->CAP, e->d_pack_off, e->d_pack, e->pack_cap);
+            YTA_HIP(hipGetLastError());
+            src = e->d_pack;
+        }
         YTA_HIP(hipMemcpyAsync(e->h_cnt, e->a.cnt, sizeof(BtCounters) * S, hipMemcpyDeviceToHost,
                                e->stream));
-        YTA_HIP(hipMemcpyAsync(e->h_pack, e->d_pack, sizeof(double) * 8 * worst,
+        YTA_HIP(hipMemcpyAsync(e->h_pack, src, sizeof(double) * 8 * worst,
                                hipMemcpyDeviceToHost, e->stream));
         return YTA_OK;
     };
@@ -3669,9 +3688,11 @@ int update_host(yta_bytetrack *e, const double *dets, const int *det_offsets, co
         rc = device_work();
     }
     e->a.active = nullptr;
+    e->a.cnt_mirror = nullptr;
     if (rc) return rc;
     if (small) {
         YTA_HIP(host_wait(e->stream));
+        if (one) memcpy(e->h_cnt, e->h_pack + worst * 8, sizeof(BtCounters));
         if (next_id)   // the device counters have advanced: hand them back even on an error below
             for (int q = 0; q < S; ++q) next_id[q] = e->h_cnt[q].next_id;
         rc = check_errors(e);

@@ -139,6 +139,9 @@ struct BtArgs {
     // outputs
     double *out;              // [S*CAP][8]
     int *out_counts;          // optional [S]
+    BtCounters *cnt_mirror;   // optional [S]: k_finish copies each stream's final counters here
+                              // (one-stream host update: right after the rows, so one copy
+                              // returns both)
     // stream subset: [S] nonzero = update this stream this frame; nullptr = every stream.  A
     // skipped stream's kernels return at once (its state, frame counter and ID counter are not
     // touched); k_finish reports 0 output rows for it.

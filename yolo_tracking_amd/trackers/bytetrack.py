@@ -98,7 +98,9 @@ class ByteTrackEngine(StreamSubset):
         # are widened on the device, exactly as the reference's promotion (yta_bytetrack_update_f32)
         f32 = ids is None and all(np.asarray(d).dtype == np.float32 for d in dets_per_stream)
         dt = np.float32 if f32 else np.float64
-        if off[-1]:
+        if off[-1] and n == 1:   # one stream (the drop-in): no concatenation copy
+            packed = np.ascontiguousarray(np.asarray(dets_per_stream[0], dtype=dt).reshape(-1, 6))
+        elif off[-1]:
             packed = np.ascontiguousarray(np.concatenate(
                 [np.asarray(d, dtype=dt).reshape(-1, 6) for d in dets_per_stream]))
         else:
