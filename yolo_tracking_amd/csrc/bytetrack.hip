@@ -3394,7 +3394,18 @@ int create_engine(int device, int n_streams, int track_capacity, int max_dets,
     if (const char *v = getenv("YTA_SPLIT23")) e->split23 = atoi(v) != 0;
     if (const char *v = getenv("YTA_GRAPHS")) e->graphs = atoi(v) != 0;
     init(e);
-    hipError_t he = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
+    hipError_t he;
+    {   // A/B (round 6): YTA_ENGINE_PRIO=1 gives every other engine created a high-priority
+        // compute stream (its dispatches go first when CU resources free up)
+        static int n_created = 0;
+        const char *v = getenv("YTA_ENGINE_PRIO");
+        int lo = 0, hi = 0;
+        if (v && atoi(v) && (n_created++ & 1) == 0 &&
+            hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess)
+            he = hipStreamCreateWithPriority(&e->stream, hipStreamNonBlocking, hi);
+        else
+            he = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
+    }
     if (he != hipSuccess) {
         set_error("hipStreamCreate: %s", hipGetErrorString(he));
         delete e;
