@@ -671,7 +671,7 @@ int yta_sof_kat_affine(int device, const float *src, const float *dst, int n, do
  * by `scale` (ecc.py:87-89); the identity on the first frame (ecc.py:66-68) and when OpenCV raises
  * (NaN correlation, or a step that would minimise it; ecc.py:82-84: prev_img kept).  warp_mode:
  * MOTION_TRANSLATION 0, MOTION_EUCLIDEAN 1 (the reference's default), MOTION_AFFINE 2
- * (MOTION_HOMOGRAPHY is refused).  S streams per engine, one 1024-thread block runs a stream's
+ * (MOTION_HOMOGRAPHY is refused; align=True's preview image: yta_ecc_aligned).  S streams per engine, one 1024-thread block runs a stream's
  * whole Gauss-Newton loop.  Restatement and parity: oracle/cmc_ecc.py (unpinned against cv2). */
 typedef struct yta_ecc yta_ecc;
 int yta_ecc_create(int device, int n_streams, int warp_mode, double eps, int max_iter,
@@ -692,6 +692,12 @@ int yta_ecc_outcome(yta_ecc *engine, int *outcome, int *iters, double *rho);
  * NULL). */
 int yta_ecc_get_state(yta_ecc *engine, int stream, int *initialized, int *h, int *w,
                       uint8_t *prev_img, int img_cap);
+/* align=True (ecc.py:91-98, replaces the cv2.warpAffine(prev_img, warp, (w, h), INTER_LINEAR)
+ * call there): stream s's previous gray frame - the template its last estimate registered against
+ * - warped by the returned matrix, h x w uint8 into out (cap bytes).  *h = *w = 0 and nothing
+ * written when the last apply was not an estimate (first frame, or OpenCV would have raised: the
+ * reference returns before ecc.py:91).  out = NULL: only *h / *w (size query). */
+int yta_ecc_aligned(yta_ecc *engine, int stream, uint8_t *out, long long cap, int *h, int *w);
 int yta_ecc_hip_stream(yta_ecc *engine, void **stream);
 
 /* ---- OSNet omni-scale block kernels (boxmot/appearance/backbones/osnet.py LightConv3x3 /

@@ -372,8 +372,59 @@ def find_transform_ecc(template, image, warp, mode, max_iter, eps, stats=None):
     return rho, warp
 
 
+def invert_affine(M):
+    """cv::warpAffine without WARP_INVERSE_MAP (imgwarp.cpp): the float32 2x3 matrix widened to
+    float64 and inverted in place - D = 1 / (M0 M4 - M1 M3) (0 when singular), M0 = M4 D,
+    M1 = -M1 D, M3 = -M3 D, M4 = M0 D, M2 = -M0' M2 - M1' M5, M5 = -M3' M2 - M4' M5."""
+    m = [float(v) for v in np.asarray(M, dtype=np.float32).astype(np.float64).ravel()]
+    D = m[0] * m[4] - m[1] * m[3]
+    D = 1.0 / D if D != 0 else 0.0
+    a11, a22 = m[4] * D, m[0] * D
+    m[0] = a11
+    m[1] *= -D
+    m[3] *= -D
+    m[4] = a22
+    b1 = -m[0] * m[2] - m[1] * m[5]
+    b2 = -m[3] * m[2] - m[4] * m[5]
+    m[2], m[5] = b1, b2
+    return np.array(m, dtype=np.float64)
+
+
+def warp_affine_u8(src, M, out_h, out_w):
+    """cv2.warpAffine(src, M, (out_w, out_h), flags=INTER_LINEAR) on a uint8 image (ecc.py:97,
+    align=True): the inverted map (invert_affine), WarpAffineInvoker's fixed-point coordinates
+    (warp_coords, fed the float64 inverse), remapBilinear's integer path - the 15-bit table
+    (initInterTab2D fixed point: (32 - fy)(32 - fx) 32 ..., summing to 2^15 exactly), taps outside
+    the image read 0 (BORDER_CONSTANT), (sum + 2^14) >> 15.  Integer sums: order-free."""
+    src = np.asarray(src, dtype=np.uint8)
+    h, w = src.shape
+    Minv = invert_affine(M)
+    x = np.arange(out_w, dtype=np.float64)
+    y = np.arange(out_h, dtype=np.float64)
+    adelta = cv_round(Minv[0] * x * AB_SCALE)
+    bdelta = cv_round(Minv[3] * x * AB_SCALE)
+    xr = cv_round((Minv[1] * y + Minv[2]) * AB_SCALE)
+    yr = cv_round((Minv[4] * y + Minv[5]) * AB_SCALE)
+    X = (xr[:, None] + 16 + adelta[None, :]) >> (AB_BITS - INTER_BITS)
+    Y = (yr[:, None] + 16 + bdelta[None, :]) >> (AB_BITS - INTER_BITS)
+    sx = np.clip(X >> INTER_BITS, -32768, 32767)
+    sy = np.clip(Y >> INTER_BITS, -32768, 32767)
+    fx, fy = X & 31, Y & 31
+    wts = [(32 - fx) * (32 - fy) * 32, fx * (32 - fy) * 32, (32 - fx) * fy * 32, fx * fy * 32]
+    img = src.astype(np.int64)
+
+    def tap(yy, xx):
+        ok = (xx >= 0) & (xx < w) & (yy >= 0) & (yy < h)
+        return np.where(ok, img[np.clip(yy, 0, h - 1), np.clip(xx, 0, w - 1)], 0)
+
+    acc = (tap(sy, sx) * wts[0] + tap(sy, sx + 1) * wts[1] + tap(sy + 1, sx) * wts[2] +
+           tap(sy + 1, sx + 1) * wts[3])
+    return np.clip((acc + (1 << 14)) >> 15, 0, 255).astype(np.uint8)
+
+
 class ECCOracle:
-    """ECC (ecc.py:13-104) over the restated OpenCV calls; align is not restated."""
+    """ECC (ecc.py:13-104) over the restated OpenCV calls, align=True's preview image included
+    (ecc.py:91-100, affine models: warp_affine_u8)."""
 
     def __init__(self, warp_mode=MOTION_EUCLIDEAN, eps=1e-5, max_iter=100, scale=0.1,
                  align=False, grayscale=True):
@@ -381,7 +432,9 @@ class ECCOracle:
         self.eps = eps
         self.max_iter = max_iter
         self.scale = scale
+        self.align = align
         self.prev_img = None
+        self.prev_img_aligned = None
         self.last = {}
 
     def apply(self, img, dets=None):
@@ -403,5 +456,10 @@ class ECCOracle:
         if self.scale < 1:
             warp[0, 2] /= self.scale
             warp[1, 2] /= self.scale
+        if self.align:   # ecc.py:91-98: the previous frame warped by the upscaled matrix
+            h, w = self.prev_img.shape
+            self.prev_img_aligned = warp_affine_u8(self.prev_img, warp, h, w)
+        else:
+            self.prev_img_aligned = None
         self.prev_img = curr
         return warp

@@ -174,3 +174,59 @@ def test_uncorrelated_frames_raise():
     for mode in (0, 1, 2):
         with pytest.raises(ce.ECCError):
             ce.find_transform_ecc(a, b, np.eye(2, 3, dtype=np.float32), mode, 100, 1e-5)
+
+
+def test_warp_affine_u8_identity_and_shift():
+    """align=True's warpAffine (INTER_LINEAR, forward matrix inverted first, BORDER_CONSTANT 0):
+    the identity returns the image bit for bit; an integer translation moves it with zeros
+    entering (dst(x, y) = src(x - tx, y - ty))."""
+    img = u8(smooth_scene(37, 53, 3))
+    assert np.array_equal(ce.warp_affine_u8(img, np.eye(2, 3, dtype=np.float32), 37, 53), img)
+    M = np.array([[1, 0, 5], [0, 1, -3]], np.float32)
+    out = ce.warp_affine_u8(img, M, 37, 53)
+    want = np.zeros_like(img)
+    want[:34, 5:] = img[3:, :48]
+    assert np.array_equal(out, want)
+
+
+def test_warp_affine_u8_rotation_close_to_float_bilinear():
+    """A rotation + subpixel shift: within one grey level of a float64 bilinear warp of the same
+    inverse map (the 1/32-pixel fixed-point grid and the 15-bit weights are the only differences),
+    away from the border; the direction of the map is the forward one (cv2's default)."""
+    img = u8(smooth_scene(90, 120, 8))
+    th = 0.05
+    M = np.array([[np.cos(th), -np.sin(th), 4.3], [np.sin(th), np.cos(th), -2.7]], np.float32)
+    out = ce.warp_affine_u8(img, M, 90, 120).astype(np.float64)
+    A = np.vstack([M.astype(np.float64), [0, 0, 1]])
+    Ai = np.linalg.inv(A)[:2]
+    ys, xs = np.mgrid[0:90, 0:120].astype(np.float64)
+    sx = Ai[0, 0] * xs + Ai[0, 1] * ys + Ai[0, 2]
+    sy = Ai[1, 0] * xs + Ai[1, 1] * ys + Ai[1, 2]
+    ref = ndimage.map_coordinates(img.astype(np.float64), [sy, sx], order=1, mode="constant")
+    inner = (sx > 1) & (sx < 118) & (sy > 1) & (sy < 88)
+    assert np.abs(out - ref)[inner].max() <= 2.0
+    assert np.abs(out - ref)[inner].mean() < 0.6
+
+
+def test_ecc_oracle_align_preview():
+    """ECC(align=True) (ecc.py:91-98): after an estimate prev_img_aligned is the previous gray
+    frame (its shape) warped by the returned matrix; align=False leaves None; the identity-on-error
+    path returns before it and keeps the last preview."""
+    big = smooth_scene(1080, 1920, 1)
+    frame = np.repeat(u8(big)[..., None], 3, axis=2)
+    shifted = np.repeat(u8(np.roll(big, (-20, 30), axis=(0, 1)))[..., None], 3, axis=2)
+    o = ce.ECCOracle(align=True)
+    o.apply(frame)
+    assert o.prev_img_aligned is None
+    prev = o.prev_img.copy()
+    W = o.apply(shifted)
+    assert o.last["outcome"] == 1
+    assert o.prev_img_aligned.shape == prev.shape == (108, 192)
+    assert np.array_equal(o.prev_img_aligned, ce.warp_affine_u8(prev, W, 108, 192))
+    kept = o.prev_img_aligned.copy()
+    assert np.array_equal(o.apply(np.full_like(frame, 90)), np.eye(2, 3))
+    assert o.last["outcome"] == 2 and np.array_equal(o.prev_img_aligned, kept)
+    n = ce.ECCOracle(align=False)
+    n.apply(frame)
+    n.apply(shifted)
+    assert n.prev_img_aligned is None

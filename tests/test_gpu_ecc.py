@@ -136,3 +136,45 @@ def test_capacity_error_leaves_engine_intact():
     st = eng.state(0, with_image=True)
     assert np.array_equal(st["prev_img"], o.prev_img)
     eng.close()
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2])
+def test_align_preview_bit_exact(mode):
+    """ECC(align=True) (ecc.py:91-98): prev_img_aligned - the previous gray frame warped by the
+    returned matrix on the device (k_ecc_align, yta_ecc_aligned) - equals the restatement's
+    warpAffine (oracle/cmc_ecc.py warp_affine_u8) bit for bit after every estimate, and the
+    identity-on-error path keeps the last preview."""
+    fr = moving_frames(540, 960, 4, 11, step=(0.003, 6.0, -3.0))
+    ecc = ECC(warp_mode=mode, scale=0.2, align=True)
+    o = ce.ECCOracle(warp_mode=mode, scale=0.2, align=True)
+    seen = 0
+    for f in fr + [np.full_like(fr[0], 90), fr[0]]:
+        assert np.array_equal(ecc.apply(f, None), o.apply(f))
+        if o.prev_img_aligned is None:
+            assert ecc.prev_img_aligned is None
+        else:
+            assert np.array_equal(ecc.prev_img_aligned, o.prev_img_aligned)
+            seen += 1
+    assert seen >= 3
+
+
+def test_align_preview_streams():
+    """EccEngine.aligned(s) per stream of a 3-stream engine against one oracle per stream; None
+    where the stream's last apply was not an estimate (first frame, identity on error)."""
+    a = moving_frames(270, 480, 3, 12)
+    b = moving_frames(270, 480, 3, 13, step=(-0.002, -4.0, 2.0))
+    eng = EccEngine(3, 2, 1e-5, 100, 0.25, 0, 270, 480)
+    oracles = [ce.ECCOracle(warp_mode=2, scale=0.25, align=True) for _ in range(3)]
+    for k in range(3):
+        frames = [a[k], b[k], b[0] if k < 2 else a[0]]
+        got = eng.apply(frames)
+        for s in range(3):   # stream 2: the same frame twice, then another scene
+            want = oracles[s].apply(frames[s])
+            assert np.array_equal(got[s], want), (k, s)
+            out, _, _ = eng.outcome()
+            al = eng.aligned(s)
+            if out[s] == 1:
+                assert np.array_equal(al, oracles[s].prev_img_aligned), (k, s)
+            else:
+                assert al is None, (k, s)
+    eng.close()

@@ -216,6 +216,7 @@ _SIGS = {
     "yta_ecc_sync": ([_P], _I),
     "yta_ecc_outcome": ([_P, _P, _P, _P], _I),
     "yta_ecc_get_state": ([_P, _I, _P, _P, _P, _P, _I], _I),
+    "yta_ecc_aligned": ([_P, _I, _P, ctypes.c_longlong, _P, _P], _I),
     "yta_ecc_hip_stream": ([_P, _P], _I),
     "yta_osnet_dw3x3": ([_P, ctypes.c_longlong, ctypes.c_longlong, _P, _P, _I, _I, _I, _I, _I, _P,
                          ctypes.c_longlong, _I, _P, ctypes.c_longlong, _P, ctypes.c_longlong, _P],

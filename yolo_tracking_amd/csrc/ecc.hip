@@ -22,6 +22,8 @@
 //                                      error projection), each closed by a block reduction, and
 //                                      the small solves done redundantly by every thread so that
 //                                      the loop's exit is block-uniform.
+// align=True's preview image (ecc.py:91-98) is a third, on-demand launch: k_ecc_align
+// [grid, pixel/thread] warps the retired template with the returned matrix (yta_ecc_aligned).
 //
 // HBM layout per stream: two u8 slots (previous accepted frame / current frame) of
 // round(max_h * scale) x round(max_w * scale) bytes, EccState, the 2x3 float32 warp.
@@ -686,6 +688,54 @@ __global__ __launch_bounds__(ecc_threads(MODE)) void k_ecc(EccArgs a) {
     }
 }
 
+// --------------------------------------------------------------------------------- k_ecc_align
+// align=True (ecc.py:91-98): cv2.warpAffine(prev_img, warp, (w, h), INTER_LINEAR) of the template
+// the last estimate registered against - the slot that estimate retired (1 - prev), intact until
+// the next frame's k_ecc_small - with the returned warp (translation already divided by the
+// scale).  Without WARP_INVERSE_MAP warpAffine inverts the float64-widened matrix first
+// (imgwarp.cpp), then the same WarpAffineInvoker fixed-point map as warp_px, and remapBilinear's
+// u8 path: the 15-bit integer table ((32 - fy)(32 - fx) 32, ...), taps outside the image 0
+// (BORDER_CONSTANT), (sum + 2^14) >> 15.  One pixel per thread; streams whose last outcome was
+// not an estimate are skipped (the reference returns before ecc.py:91 there).
+__global__ __launch_bounds__(256) void k_ecc_align(EccArgs a, int s, uint8_t *out) {
+    const EccState &st = a.state[s];
+    if (!st.init || st.outcome != ECC_OUT_EST) return;
+    const int slot = 1 - st.prev;
+    const int h = st.h[slot], w = st.w[slot];
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= h * w) return;
+    const int y = i / w, x = i - y * w;
+    double M[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) M[k] = (double)a.warps[6 * s + k];
+    double D = M[0] * M[4] - M[1] * M[3];
+    D = D != 0.0 ? 1.0 / D : 0.0;
+    const double A11 = M[4] * D, A22 = M[0] * D;
+    M[0] = A11;
+    M[1] *= -D;
+    M[3] *= -D;
+    M[4] = A22;
+    const double b1 = -M[0] * M[2] - M[1] * M[5];
+    const double b2 = -M[3] * M[2] - M[4] * M[5];
+    M[2] = b1;
+    M[5] = b2;
+    const int xr = cv_round((M[1] * y + M[2]) * 1024.0), yr = cv_round((M[4] * y + M[5]) * 1024.0);
+    const int ad = cv_round(M[0] * x * 1024.0), bd = cv_round(M[3] * x * 1024.0);
+    const int X = (xr + 16 + ad) >> 5, Y = (yr + 16 + bd) >> 5;
+    const int sx = sat16(X >> 5), sy = sat16(Y >> 5);
+    const int fx = X & 31, fy = Y & 31;
+    const int wn[4] = {(32 - fx) * (32 - fy) * 32, fx * (32 - fy) * 32, (32 - fx) * fy * 32,
+                       fx * fy * 32};
+    const uint8_t *p = a.img + ((long long)s * 2 + slot) * a.slot_px;
+    int acc = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int xx = sx + (k & 1), yy = sy + (k >> 1);
+        if ((unsigned)xx < (unsigned)w && (unsigned)yy < (unsigned)h) acc += (int)p[yy * w + xx] * wn[k];
+    }
+    out[i] = (uint8_t)min(max((acc + (1 << 14)) >> 15, 0), 255);
+}
+
 }  // namespace
 }  // namespace yta
 
@@ -706,6 +756,8 @@ struct yta_ecc {
     long long *d_frame_off = nullptr;
     int *d_frame_hw = nullptr;
     EccState *h_state = nullptr;
+    uint8_t *d_aligned = nullptr;   // align=True preview image (yta_ecc_aligned), slot_px bytes
+    long long aligned_cap = 0;
 };
 
 namespace {
@@ -838,7 +890,7 @@ int yta_ecc_destroy(yta_ecc *e) {
     if (e->stream) (void)host_wait(e->stream);
     ecc_free_slots(e);
     for (void *p : {(void *)e->state, (void *)e->d_warps, (void *)e->d_frames,
-                    (void *)e->d_frame_off, (void *)e->d_frame_hw})
+                    (void *)e->d_frame_off, (void *)e->d_frame_hw, (void *)e->d_aligned})
         if (p) (void)hipFree(p);
     if (e->h_state) (void)hipHostFree(e->h_state);
     if (e->stream) (void)hipStreamDestroy(e->stream);
@@ -959,6 +1011,42 @@ int yta_ecc_get_state(yta_ecc *e, int stream, int *initialized, int *h, int *w,
         YTA_HIP(hipMemcpy(prev_img, e->img + ((long long)stream * 2 + st.prev) * e->a.slot_px,
                           (size_t)n, hipMemcpyDeviceToHost));
     }
+    return YTA_OK;
+}
+
+int yta_ecc_aligned(yta_ecc *e, int stream, uint8_t *out, long long cap, int *h, int *w) {
+    YTA_CHECK(e && h && w, YTA_ERR_INVALID, "null argument");
+    YTA_CHECK(stream >= 0 && stream < e->S, YTA_ERR_INVALID, "stream out of range");
+    YTA_HIP(hipSetDevice(e->device));
+    YTA_HIP(host_wait(e->stream));
+    EccState st;
+    YTA_HIP(hipMemcpy(&st, e->state + stream, sizeof(st), hipMemcpyDeviceToHost));
+    *h = 0;
+    *w = 0;
+    if (!st.init || st.outcome != ECC_OUT_EST || !e->a.warps) return YTA_OK;
+    const int slot = 1 - st.prev;
+    const long long n = (long long)st.h[slot] * st.w[slot];
+    YTA_CHECK(n > 0 && n <= e->a.slot_px, YTA_ERR_INVALID, "stream %d: bad template size", stream);
+    if (!out) {   // size query
+        *h = st.h[slot];
+        *w = st.w[slot];
+        return YTA_OK;
+    }
+    YTA_CHECK(cap >= n, YTA_ERR_CAPACITY, "out holds %lld bytes, %lld needed", cap, n);
+    if (e->aligned_cap < e->a.slot_px) {
+        if (e->d_aligned) (void)hipFree(e->d_aligned);
+        e->d_aligned = nullptr;
+        e->aligned_cap = 0;
+        YTA_HIP(hipMalloc((void **)&e->d_aligned, (size_t)e->a.slot_px));
+        e->aligned_cap = e->a.slot_px;
+    }
+    hipLaunchKernelGGL(k_ecc_align, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, e->stream, e->a,
+                       stream, e->d_aligned);
+    YTA_HIP(hipGetLastError());
+    YTA_HIP(hipMemcpyAsync(out, e->d_aligned, (size_t)n, hipMemcpyDeviceToHost, e->stream));
+    YTA_HIP(host_wait(e->stream));
+    *h = st.h[slot];
+    *w = st.w[slot];
     return YTA_OK;
 }
 

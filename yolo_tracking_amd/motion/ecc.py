@@ -80,6 +80,20 @@ class EccEngine:
                                             _lib.ptr(rho)))
         return out, iters, rho
 
+    def aligned(self, stream=0):
+        """align=True's preview (ecc.py:91-98): the stream's previous gray frame warped by the
+        last returned matrix (cv2.warpAffine INTER_LINEAR), or None when the last apply was not
+        an estimate (first frame / identity because OpenCV would have raised)."""
+        hh, ww = ctypes.c_int(), ctypes.c_int()
+        _lib.check(self.lib.yta_ecc_aligned(self._h, int(stream), None, 0, ctypes.byref(hh),
+                                            ctypes.byref(ww)))
+        if hh.value == 0:
+            return None
+        img = np.zeros((hh.value, ww.value), np.uint8)
+        _lib.check(self.lib.yta_ecc_aligned(self._h, int(stream), _lib.ptr(img), img.size,
+                                            ctypes.byref(hh), ctypes.byref(ww)))
+        return img
+
     def state(self, stream=0, with_image=False):
         init, hh, ww = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
         _lib.check(self.lib.yta_ecc_get_state(self._h, int(stream), ctypes.byref(init),
@@ -96,8 +110,10 @@ class EccEngine:
 
 class ECC:
     """Drop-in for boxmot.motion.cmc.ecc.ECC (ecc.py:13-57): same constructor arguments,
-    `apply(img, dets) -> 2x3 float32` (dets unused, as in the reference).  MOTION_HOMOGRAPHY,
-    grayscale=False and align=True (the aligned preview image of ecc.py:91-100) are refused."""
+    `apply(img, dets) -> 2x3 float32` (dets unused, as in the reference).  align=True keeps the
+    previous gray frame warped by each estimate in `prev_img_aligned` (ecc.py:91-98, warped on the
+    device: yta_ecc_aligned), None with align=False; MOTION_HOMOGRAPHY and grayscale=False are
+    refused."""
 
     def __init__(self, warp_mode=MOTION_EUCLIDEAN, eps=1e-5, max_iter=100, scale=0.1, align=False,
                  grayscale=True, device=0):
@@ -106,8 +122,6 @@ class ECC:
                                       "euclidean and affine models are on the MI355X path")
         if not grayscale:
             raise NotImplementedError("ECC(grayscale=False): findTransformECC needs one channel")
-        if align:
-            raise NotImplementedError("ECC(align=True): the aligned preview image is not built")
         if scale is None or not 0 < scale <= 1:
             raise ValueError("ECC(scale): a resize factor in (0, 1] (ecc.py:87 compares it to 1)")
         self.warp_mode = warp_mode
@@ -125,4 +139,9 @@ class ECC:
             _, max_iter, eps = self.termination_criteria
             self._engine = EccEngine(1, self.warp_mode, eps, max_iter, self.scale, self._device,
                                      img.shape[0], img.shape[1])
-        return self._engine.apply([img])[0]
+        warp = self._engine.apply([img])[0]
+        if self.align:   # after an estimate only: the other paths return before ecc.py:91
+            aligned = self._engine.aligned(0)
+            if aligned is not None:
+                self.prev_img_aligned = aligned
+        return warp
