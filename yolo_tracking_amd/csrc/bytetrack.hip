@@ -1962,7 +1962,10 @@ struct SlotFlags {
     int slot, flags;
 };
 
-template <int V>
+// PRE (the few-stream 1024-thread variant): when tracked' and lost' each fit one item per
+// thread, the duplicate removal's tracked' boxes are loaded beside the lost' boxes (two dependent
+// round trips for both instead of two each, before and after the grid build).
+template <int V, bool PRE = false>
 __device__ __forceinline__ void finish_body(const BtArgs &a, int s, unsigned *bits, Arena &ar,
                                             FinishShared &sh, bool lds_ar) {
     int *wsum = sh.wsum;
@@ -2196,7 +2199,20 @@ __device__ __forceinline__ void finish_body(const BtArgs &a, int s, unsigned *bi
         auto exact_lbox = [&](int q) {
             return a.pool_box[tb + (lpos ? lpos[q] : a.l2pos[tb + q])];
         };
-        if (V == VAR_BYTETRACK || V == VAR_BOTSORT)
+        const bool pre = PRE && n_t2 <= nt && n_l2 <= nt;   // block-uniform
+        long long pslot = 0;
+        Box pbox{0.0, 0.0, 0.0, 0.0};
+        if (pre) {
+            const int sl = t < n_t2 ? a.t2[tb + t] : 0;
+            const int lp = t < n_l2 ? a.l2pos[tb + t] : 0;
+            const Box lb = a.pool_box[tb + lp];
+            pslot = tb + sl;
+            pbox = kf_box<V>(a.kf, pslot);
+            if (t < n_l2) {
+                lcache[t] = box_outer_f32(lb);
+                if (lpos) lpos[t] = lp;
+            }
+        } else if (V == VAR_BYTETRACK || V == VAR_BOTSORT)
             batched_for2<4>(
                 n_l2, [&](int q) { return a.l2pos[tb + q]; },
                 [&](int, int pos) {
@@ -2224,15 +2240,7 @@ __device__ __forceinline__ void finish_body(const BtArgs &a, int s, unsigned *bi
             long long slot;
             Box b;
         };
-        batched_for2<5>(
-            n_t2, [&](int p) { return a.t2[tb + p]; },
-            [&](int, int sl) {
-                TBox v;
-                v.slot = tb + sl;
-                v.b = kf_box<V>(a.kf, v.slot);
-                return v;
-            },
-            [&](int p, const TBox &v) {
+        auto query = [&](int p, const TBox &v) {
                 if (p == 0) YTA_STAMP_ABS(126);   // diagnostic: thread 0's boxes have arrived
 #ifdef YTA_STAMPS
                 if (p == 0) g_stamps[127] = gh.n_big + 1000000ull * gh.gx * gh.gy;
@@ -2255,7 +2263,20 @@ __device__ __forceinline__ void finish_body(const BtArgs &a, int s, unsigned *bi
                 // 1 - IoU < 0.15  <=>  IoU > 0.85: only corners within 0.18 w of tbx's
                 grid_query_iou_above_f4(gv, gh, lcache, tbx, 0.85, pair,
                                         [&](int q) { pair(q, lcache[q]); });
-            });
+            };
+        if (pre) {
+            if (t < n_t2) query(t, TBox{pslot, pbox});
+        } else {
+            batched_for2<5>(
+                n_t2, [&](int p) { return a.t2[tb + p]; },
+                [&](int, int sl) {
+                    TBox v;
+                    v.slot = tb + sl;
+                    v.b = kf_box<V>(a.kf, v.slot);
+                    return v;
+                },
+                query);
+        }
     }
     lds_sync();
     YTA_STAMP(6);
@@ -2471,7 +2492,7 @@ __global__ __launch_bounds__(NT, NT == BLKF ? 4 : 1) void k_finish(BtArgs a) {
     YTA_BLK(5, 0);
     if (need <= (long long)a.lds_bytes_f) {
         Arena ar(fsmem + bits_bytes, a.lds_bytes_f);
-        finish_body<V>(a, s, bits, ar, sh, true);
+        finish_body<V, NT == 1024>(a, s, bits, ar, sh, true);
     } else {   // a global arena: here, or by k_redo_finish
         if (threadIdx.x == 0) a.cnt[s].n_fallback_f += 1;
         if (redo_in_place(a, a.S)) {
